@@ -1,0 +1,30 @@
+# Builds the product library (HIP, gfx950) and the CPU oracle (test infrastructure).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
+LIB := fury_amd/lib/libfory_rowfmt.so
+ORACLE := oracle/_build/liboracle.so
+SRCS := fury_amd/csrc/kernels.hip fury_amd/csrc/capi.cpp fury_amd/csrc/plan.cpp
+HDRS := fury_amd/csrc/kernels.h fury_amd/csrc/plan.h include/fory_rowfmt.h
+
+all: $(LIB) $(ORACLE)
+
+fury_amd/lib/%.o: fury_amd/csrc/%.hip $(HDRS)
+	@mkdir -p fury_amd/lib
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+fury_amd/lib/%.o: fury_amd/csrc/%.cpp $(HDRS)
+	@mkdir -p fury_amd/lib
+	$(HIPCC) $(HIPFLAGS) -x hip -c -o $@ $<
+
+$(LIB): fury_amd/lib/kernels.o fury_amd/lib/capi.o fury_amd/lib/plan.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+$(ORACLE): oracle/rowfmt_oracle.c include/fory_rowfmt.h
+	@mkdir -p oracle/_build
+	gcc -O2 -std=c11 -Wall -Wextra -fPIC -shared -o $@ $<
+
+clean:
+	rm -rf fury_amd/lib oracle/_build
+
+.PHONY: all clean

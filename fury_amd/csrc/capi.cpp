@@ -1,0 +1,367 @@
+// capi.cpp — the extern "C" boundary (include/fory_rowfmt.h).
+//
+// Host-side glue only: validate arguments the way the reference validates
+// them (Preconditions / bounds checks / schema-hash check), bind the
+// caller's columns into a device table in the caller's workspace, and
+// enqueue the kernels of kernels.hip on the caller's stream.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/fory_rowfmt.h"
+#include "kernels.h"
+#include "plan.h"
+
+using fory_amd::ColumnDev;
+using fory_amd::FixedFieldDev;
+using fory_amd::Plan;
+
+struct fory_plan {
+  Plan p;
+};
+
+namespace fory_amd {
+bool fixed_tiled_supported(int stride);
+}
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(FORY_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+constexpr int64_t kAlign = 256;
+int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+int64_t table_bytes(const Plan& p) {
+  if (p.fixed_width) return align_up((int64_t)p.top.size() * (int64_t)sizeof(FixedFieldDev));
+  return align_up((int64_t)p.nodes.size() * (int64_t)sizeof(ColumnDev)) +
+         align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::Op));
+}
+
+bool use_tiled(const Plan& p, int frame) {
+  return p.fixed_width && fory_amd::fixed_tiled_supported(p.fixed_size + (frame ? 12 : 0));
+}
+
+int check_common(const fory_plan* plan, const fory_column* cols, int64_t n, int frame,
+                 void* ws, int64_t ws_bytes) {
+  if (!plan) return fail(FORY_ERR_INVALID_ARGUMENT, "plan is null");
+  if (n < 0) return fail(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
+  if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM)
+    return fail(FORY_ERR_INVALID_ARGUMENT, "frame_mode must be 0 (raw) or 1 (stream)");
+  if (n > 0 && !cols) return fail(FORY_ERR_INVALID_ARGUMENT, "cols is null");
+  const int64_t need = fory_rowfmt_workspace_bytes(plan, n);
+  if (n > 0 && (!ws || ws_bytes < need))
+    return fail(FORY_ERR_INVALID_ARGUMENT,
+                "workspace too small: need " + std::to_string(need) + " bytes");
+  return FORY_OK;
+}
+
+// Binds the top-level columns of a fixed-width plan (encode: inputs; decode: outputs).
+int bind_fixed(const Plan& p, const fory_column* cols, int64_t n, bool decode,
+               std::vector<FixedFieldDev>* out) {
+  out->resize(p.top.size());
+  for (size_t k = 0; k < p.top.size(); ++k) {
+    const int32_t idx = p.top[k];
+    const fory_amd::Node& nd = p.nodes[idx];
+    const fory_column& c = cols[idx];
+    if (n > 0 && !c.values)
+      return fail(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(idx) + " has no values");
+    if (n > 0 && c.length < n)
+      return fail(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(idx) + " shorter than num_rows");
+    if (decode && n > 0 && c.capacity > 0 && c.capacity < n * nd.width)
+      return fail(FORY_ERR_CAPACITY, "column " + std::to_string(idx) + " capacity too small");
+    FixedFieldDev f{};
+    f.width = nd.width;
+    f.flags = (nd.nullable ? 1 : 0) | (nd.kind == fory_amd::KIND_BOOL ? 2 : 0);
+    if (decode) {
+      f.out_values = static_cast<uint8_t*>(c.values);
+      f.out_validity = nd.nullable ? c.validity : nullptr;
+    } else {
+      f.values = static_cast<const uint8_t*>(c.values);
+      f.validity = nd.nullable ? c.validity : nullptr;
+    }
+    (*out)[k] = f;
+  }
+  return FORY_OK;
+}
+
+int bind_var(const Plan& p, const fory_column* cols, int64_t n, std::vector<ColumnDev>* out) {
+  out->resize(p.nodes.size());
+  for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
+    const fory_amd::Node& nd = p.nodes[idx];
+    const fory_column& c = cols[idx];
+    ColumnDev d{};
+    d.values = static_cast<const uint8_t*>(c.values);
+    d.offsets = c.offsets;
+    d.validity = nd.nullable ? c.validity : nullptr;
+    d.out_values = static_cast<uint8_t*>(c.values);
+    d.out_offsets = c.offsets;
+    d.out_validity = nd.nullable ? c.validity : nullptr;
+    if (n > 0) {
+      if ((nd.kind == fory_amd::KIND_BYTES || nd.kind == fory_amd::KIND_LIST) && !c.offsets)
+        return fail(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(idx) + " needs offsets");
+    }
+    (*out)[idx] = d;
+  }
+  return FORY_OK;
+}
+
+int upload(void* ws, const void* host, int64_t bytes, hipStream_t s) {
+  if (bytes == 0) return FORY_OK;
+  hipError_t e = hipMemcpyAsync(ws, host, (size_t)bytes, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(plan table)");
+  return FORY_OK;
+}
+
+fory_amd::FixedLaunch fixed_launch(const Plan& p, const void* table, int64_t n, int frame) {
+  fory_amd::FixedLaunch L{};
+  L.fields = static_cast<const FixedFieldDev*>(table);
+  L.num_fields = (int32_t)p.top.size();
+  L.bitmap_bytes = p.bitmap_bytes;
+  L.fixed_size = p.fixed_size;
+  L.stride = p.fixed_size + (frame ? 12 : 0);
+  L.schema_hash = p.schema_hash;
+  L.num_rows = n;
+  L.any_nullable = p.any_nullable ? 1 : 0;
+  L.frame = frame;
+  return L;
+}
+
+// Var launch: columns table then program in the workspace.
+int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, void* ws,
+                hipStream_t s, fory_amd::VarLaunch* L) {
+  std::vector<ColumnDev> cd;
+  int rc = bind_var(p, cols, n, &cd);
+  if (rc) return rc;
+  const int64_t col_bytes = align_up((int64_t)cd.size() * (int64_t)sizeof(ColumnDev));
+  std::vector<uint8_t> host((size_t)table_bytes(p), 0);
+  std::memcpy(host.data(), cd.data(), cd.size() * sizeof(ColumnDev));
+  std::memcpy(host.data() + col_bytes, p.program.data(), p.program.size() * sizeof(fory_amd::Op));
+  rc = upload(ws, host.data(), (int64_t)host.size(), s);
+  if (rc) return rc;
+  L->cols = static_cast<const ColumnDev*>(ws);
+  L->prog = reinterpret_cast<const fory_amd::Op*>(static_cast<uint8_t*>(ws) + col_bytes);
+  L->num_ops = (int32_t)p.program.size();
+  L->num_top = (int32_t)p.top.size();
+  L->bitmap_bytes = p.bitmap_bytes;
+  L->fixed_size = p.fixed_size;
+  L->schema_hash = p.schema_hash;
+  L->num_rows = n;
+  L->frame = frame;
+  return FORY_OK;
+}
+
+int64_t* partials_ptr(const Plan& p, void* ws) {
+  return reinterpret_cast<int64_t*>(static_cast<uint8_t*>(ws) + table_bytes(p));
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t fory_rowfmt_abi_version(void) { return FORY_ROWFMT_ABI_VERSION; }
+
+const char* fory_rowfmt_last_error(void) { return g_err.c_str(); }
+
+int fory_rowfmt_plan_create(const fory_field_desc* fields, int32_t num_desc, fory_plan** out_plan) {
+  if (!out_plan) return fail(FORY_ERR_INVALID_ARGUMENT, "out_plan is null");
+  *out_plan = nullptr;
+  fory_plan* plan = new fory_plan();
+  std::string err;
+  int rc = fory_amd::build_plan(fields, num_desc, &plan->p, &err);
+  if (rc) {
+    delete plan;
+    return fail(rc, "Create encoder failed: " + err);
+  }
+  if (!plan->p.fixed_width && plan->p.max_depth > 8) {
+    delete plan;
+    return fail(FORY_ERR_UNSUPPORTED, "device path supports struct nesting depth <= 8");
+  }
+  *out_plan = plan;
+  return FORY_OK;
+}
+
+void fory_rowfmt_plan_destroy(fory_plan* plan) { delete plan; }
+
+int fory_rowfmt_plan_info(const fory_plan* plan, fory_plan_info* info) {
+  if (!plan || !info) return fail(FORY_ERR_INVALID_ARGUMENT, "plan or info is null");
+  const Plan& p = plan->p;
+  info->schema_hash = p.schema_hash;
+  info->num_fields = (int32_t)p.top.size();
+  info->num_columns = (int32_t)p.nodes.size();
+  info->bitmap_bytes = p.bitmap_bytes;
+  info->fixed_size = p.fixed_size;
+  info->fixed_width = p.fixed_width ? 1 : 0;
+  info->row_size = p.fixed_width ? p.fixed_size : -1;
+  return FORY_OK;
+}
+
+int64_t fory_rowfmt_workspace_bytes(const fory_plan* plan, int64_t num_rows) {
+  if (!plan) return -1;
+  const int64_t n = num_rows < 0 ? 0 : num_rows;
+  return table_bytes(plan->p) + align_up((fory_amd::scan_partials(n) + 2) * 8);
+}
+
+int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols, int64_t num_rows,
+                             int32_t frame_mode, int64_t* d_row_offsets, void* d_workspace,
+                             int64_t workspace_bytes, void* stream) {
+  int rc = check_common(plan, cols, num_rows, frame_mode, d_workspace, workspace_bytes);
+  if (rc) return rc;
+  if (!d_row_offsets) return fail(FORY_ERR_INVALID_ARGUMENT, "d_row_offsets is null");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const Plan& p = plan->p;
+  hipError_t e;
+  if (p.fixed_width) {
+    e = fory_amd::launch_fill_offsets(d_row_offsets, num_rows, p.fixed_size + (frame_mode ? 12 : 0), s);
+    return e == hipSuccess ? FORY_OK : hip_fail(e, "fill_offsets");
+  }
+  if (num_rows == 0) {
+    e = hipMemsetAsync(d_row_offsets, 0, sizeof(int64_t), s);
+    return e == hipSuccess ? FORY_OK : hip_fail(e, "hipMemsetAsync");
+  }
+  fory_amd::VarLaunch L{};
+  rc = prepare_var(p, cols, num_rows, frame_mode, d_workspace, s, &L);
+  if (rc) return rc;
+  e = fory_amd::launch_var_sizes(L, d_row_offsets, s);
+  if (e != hipSuccess) return hip_fail(e, "var_sizes");
+  e = fory_amd::launch_scan_i64(d_row_offsets, num_rows, partials_ptr(p, d_workspace), s);
+  return e == hipSuccess ? FORY_OK : hip_fail(e, "scan");
+}
+
+int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t num_rows,
+                       int32_t frame_mode, const int64_t* d_row_offsets, void* d_out,
+                       int64_t out_capacity, int32_t* d_status, void* d_workspace,
+                       int64_t workspace_bytes, void* stream) {
+  int rc = check_common(plan, cols, num_rows, frame_mode, d_workspace, workspace_bytes);
+  if (rc) return rc;
+  if (num_rows == 0) return FORY_OK;
+  if (!d_out) return fail(FORY_ERR_INVALID_ARGUMENT, "d_out is null");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const Plan& p = plan->p;
+  hipError_t e;
+  if (use_tiled(p, frame_mode)) {
+    const int64_t stride = p.fixed_size + (frame_mode ? 12 : 0);
+    if (num_rows * stride > out_capacity)
+      return fail(FORY_ERR_CAPACITY, "output capacity " + std::to_string(out_capacity) + " < " +
+                                         std::to_string(num_rows * stride) + " bytes");
+    if (reinterpret_cast<uintptr_t>(d_out) & 15)
+      return fail(FORY_ERR_INVALID_ARGUMENT, "d_out must be 16-byte aligned");
+    std::vector<FixedFieldDev> tab;
+    rc = bind_fixed(p, cols, num_rows, false, &tab);
+    if (rc) return rc;
+    rc = upload(d_workspace, tab.data(), (int64_t)(tab.size() * sizeof(FixedFieldDev)), s);
+    if (rc) return rc;
+    e = fory_amd::launch_encode_fixed(fixed_launch(p, d_workspace, num_rows, frame_mode),
+                                      static_cast<uint8_t*>(d_out), s);
+    return e == hipSuccess ? FORY_OK : hip_fail(e, "encode_fixed");
+  }
+  if (p.fixed_width)
+    return fail(FORY_ERR_UNSUPPORTED, "row too wide for the device path");
+  if (!d_row_offsets)
+    return fail(FORY_ERR_INVALID_ARGUMENT, "varlen schema: d_row_offsets (from encoded_size) required");
+  fory_amd::VarLaunch L{};
+  rc = prepare_var(p, cols, num_rows, frame_mode, d_workspace, s, &L);
+  if (rc) return rc;
+  e = fory_amd::launch_var_encode(L, d_row_offsets, static_cast<uint8_t*>(d_out), out_capacity, d_status, s);
+  return e == hipSuccess ? FORY_OK : hip_fail(e, "var_encode");
+}
+
+int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const int64_t* d_row_offsets,
+                             int64_t num_rows, int32_t frame_mode, const fory_column* out_cols,
+                             int32_t* d_status, void* d_workspace, int64_t workspace_bytes,
+                             void* stream) {
+  int rc = check_common(plan, out_cols, num_rows, frame_mode, d_workspace, workspace_bytes);
+  if (rc) return rc;
+  const Plan& p = plan->p;
+  if (p.fixed_width || num_rows == 0) {
+    if (!p.fixed_width) {
+      hipStream_t s0 = static_cast<hipStream_t>(stream);
+      for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
+        const int k = p.nodes[idx].kind;
+        if ((k == fory_amd::KIND_BYTES || k == fory_amd::KIND_LIST) && out_cols && out_cols[idx].offsets)
+          (void)hipMemsetAsync(out_cols[idx].offsets, 0, sizeof(int32_t), s0);
+      }
+    }
+    return FORY_OK;
+  }
+  if (!d_rows || !d_row_offsets)
+    return fail(FORY_ERR_INVALID_ARGUMENT, "varlen schema: d_rows and d_row_offsets required");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  fory_amd::VarLaunch L{};
+  rc = prepare_var(p, out_cols, num_rows, frame_mode, d_workspace, s, &L);
+  if (rc) return rc;
+  hipError_t e = fory_amd::launch_var_decode_lengths(L, static_cast<const uint8_t*>(d_rows), d_row_offsets,
+                                                     d_status, s);
+  if (e != hipSuccess) return hip_fail(e, "var_decode_lengths");
+  for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
+    const int k = p.nodes[idx].kind;
+    if (k != fory_amd::KIND_BYTES && k != fory_amd::KIND_LIST) continue;
+    e = fory_amd::launch_scan_offsets_i32(out_cols[idx].offsets, num_rows, partials_ptr(p, d_workspace),
+                                          d_status, s);
+    if (e != hipSuccess) return hip_fail(e, "scan offsets");
+  }
+  return FORY_OK;
+}
+
+int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows, const int64_t* d_row_offsets,
+                       int64_t num_rows, int32_t frame_mode, const fory_column* out_cols,
+                       int32_t* d_status, void* d_workspace, int64_t workspace_bytes, void* stream) {
+  int rc = check_common(plan, out_cols, num_rows, frame_mode, d_workspace, workspace_bytes);
+  if (rc) return rc;
+  if (num_rows == 0) return FORY_OK;
+  if (!d_rows) return fail(FORY_ERR_INVALID_ARGUMENT, "d_rows is null");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const Plan& p = plan->p;
+  hipError_t e;
+  if (use_tiled(p, frame_mode)) {
+    if (reinterpret_cast<uintptr_t>(d_rows) & 15)
+      return fail(FORY_ERR_INVALID_ARGUMENT, "d_rows must be 16-byte aligned");
+    std::vector<FixedFieldDev> tab;
+    rc = bind_fixed(p, out_cols, num_rows, true, &tab);
+    if (rc) return rc;
+    rc = upload(d_workspace, tab.data(), (int64_t)(tab.size() * sizeof(FixedFieldDev)), s);
+    if (rc) return rc;
+    e = fory_amd::launch_decode_fixed(fixed_launch(p, d_workspace, num_rows, frame_mode),
+                                      static_cast<const uint8_t*>(d_rows), d_status, s);
+    return e == hipSuccess ? FORY_OK : hip_fail(e, "decode_fixed");
+  }
+  if (p.fixed_width) return fail(FORY_ERR_UNSUPPORTED, "row too wide for the device path");
+  if (!d_row_offsets)
+    return fail(FORY_ERR_INVALID_ARGUMENT, "varlen schema: d_row_offsets required");
+  fory_amd::VarLaunch L{};
+  rc = prepare_var(p, out_cols, num_rows, frame_mode, d_workspace, s, &L);
+  if (rc) return rc;
+  e = fory_amd::launch_var_decode(L, static_cast<const uint8_t*>(d_rows), d_row_offsets, d_status, s);
+  return e == hipSuccess ? FORY_OK : hip_fail(e, "var_decode");
+}
+
+int fory_rowfmt_read_status(const int32_t* d_status, void* stream) {
+  if (!d_status) return FORY_OK;
+  int32_t h = 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e = hipMemcpyAsync(&h, d_status, sizeof(h), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "read_status");
+  switch (h) {
+    case FORY_OK: return FORY_OK;
+    case FORY_ERR_SCHEMA_MISMATCH:
+      return fail(h, "Schema is not consistent: peer schema hash differs from this encoder's schema hash. "
+                     "Please check writer schema.");
+    case FORY_ERR_CORRUPT: return fail(h, "Malformed row or frame (size field out of range)");
+    case FORY_ERR_CAPACITY: return fail(h, "Output buffer too small (IndexOutOfBounds)");
+    default: return fail(h, "device status " + std::to_string(h));
+  }
+}
+
+}  // extern "C"

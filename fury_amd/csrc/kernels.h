@@ -1,0 +1,61 @@
+// kernels.h — launchers for the gfx950 row-format kernels (kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "plan.h"
+
+namespace fory_amd {
+
+struct FixedLaunch {
+  const FixedFieldDev* fields;  // device table
+  int32_t num_fields;
+  int32_t bitmap_bytes;
+  int32_t fixed_size;
+  int32_t stride;               // fixed_size (+12 in frame mode)
+  int64_t schema_hash;
+  int64_t num_rows;
+  int32_t any_nullable;
+  int32_t frame;
+};
+
+hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s);
+hipError_t launch_decode_fixed(const FixedLaunch& L, const uint8_t* rows, int32_t* status,
+                               hipStream_t s);
+hipError_t launch_fill_offsets(int64_t* offs, int64_t n, int64_t stride, hipStream_t s);
+
+struct VarLaunch {
+  const Op* prog;               // device
+  int32_t num_ops;
+  const ColumnDev* cols;        // device
+  int32_t num_top;
+  int32_t bitmap_bytes;
+  int32_t fixed_size;
+  int64_t schema_hash;
+  int64_t num_rows;
+  int32_t frame;
+};
+
+// sizes -> d_row_offsets[0..n-1] (row/frame byte sizes), then exclusive scan.
+hipError_t launch_var_sizes(const VarLaunch& L, int64_t* d_row_offsets, hipStream_t s);
+hipError_t launch_var_encode(const VarLaunch& L, const int64_t* d_row_offsets, uint8_t* out,
+                             int64_t capacity, int32_t* status, hipStream_t s);
+// decode: per-row lengths of every varlen column into out_offsets[i+1]
+hipError_t launch_var_decode_lengths(const VarLaunch& L, const uint8_t* rows,
+                                     const int64_t* d_row_offsets, int32_t* status,
+                                     hipStream_t s);
+hipError_t launch_var_decode(const VarLaunch& L, const uint8_t* rows,
+                             const int64_t* d_row_offsets, int32_t* status, hipStream_t s);
+
+// Exclusive scan of n int64 values in place; data[n] receives the total.
+// partials: >= scan_partials(n) int64 of workspace.
+int64_t scan_partials(int64_t n);
+hipError_t launch_scan_i64(int64_t* data, int64_t n, int64_t* partials, hipStream_t s);
+// Arrow offsets: offs[1..n] hold lengths; writes offs[0]=0 and inclusive
+// prefix into offs[1..n] (int32). Overflow past INT32_MAX sets *status.
+hipError_t launch_scan_offsets_i32(int32_t* offs, int64_t n, int64_t* partials,
+                                   int32_t* status, hipStream_t s);
+
+}  // namespace fory_amd

@@ -1,0 +1,191 @@
+// plan.cpp — schema → layout plan (see plan.h for the reference mapping).
+#include "plan.h"
+
+#include <cstdio>
+
+namespace fory_amd {
+
+int32_t type_width(int32_t t) {
+  // DataTypes.getTypeWidth (DataTypes.java:68-133): bool 1, intN N/8,
+  // float 4, double 8, date 4, timestamp 8; struct/list/map/utf8/binary/decimal -1.
+  switch (t) {
+    case FORY_TYPE_BOOL:
+    case FORY_TYPE_INT8:
+      return 1;
+    case FORY_TYPE_INT16:
+      return 2;
+    case FORY_TYPE_INT32:
+    case FORY_TYPE_FLOAT:
+    case FORY_TYPE_DATE32:
+      return 4;
+    case FORY_TYPE_INT64:
+    case FORY_TYPE_DOUBLE:
+    case FORY_TYPE_TIMESTAMP:
+      return 8;
+    default:
+      return -1;
+  }
+}
+
+static bool supported_type(int32_t t) {
+  switch (t) {
+    case FORY_TYPE_BOOL: case FORY_TYPE_INT8: case FORY_TYPE_INT16: case FORY_TYPE_INT32:
+    case FORY_TYPE_INT64: case FORY_TYPE_FLOAT: case FORY_TYPE_DOUBLE: case FORY_TYPE_STRING:
+    case FORY_TYPE_BINARY: case FORY_TYPE_DATE32: case FORY_TYPE_TIMESTAMP: case FORY_TYPE_LIST:
+    case FORY_TYPE_STRUCT:
+      return true;
+    default:
+      return false;
+  }
+}
+
+static int parse_node(const fory_field_desc* d, int32_t n, int32_t at, Plan* p, int depth,
+                      int32_t* next, std::string* err) {
+  if (at >= n) {
+    *err = "schema descriptor truncated";
+    return FORY_ERR_ENCODER;
+  }
+  if (depth > 16) {
+    *err = "schema nesting deeper than 16";
+    return FORY_ERR_UNSUPPORTED;
+  }
+  const fory_field_desc& f = d[at];
+  if (f.reserved != 0 || f.num_children < 0) {
+    *err = "invalid field descriptor at index " + std::to_string(at);
+    return FORY_ERR_INVALID_ARGUMENT;
+  }
+  if (!supported_type(f.type_id)) {
+    // DataTypes.unsupported(type) -> UnsupportedOperationException
+    *err = "Unsupported type id " + std::to_string(f.type_id) + " at field descriptor " +
+           std::to_string(at);
+    return FORY_ERR_UNSUPPORTED;
+  }
+  Node& nd = p->nodes[at];
+  nd.type_id = f.type_id;
+  nd.nullable = f.nullable ? 1 : 0;
+  nd.width = type_width(f.type_id);
+  if (nd.nullable) p->any_nullable = true;
+  if (f.type_id == FORY_TYPE_LIST && f.num_children != 1) {
+    *err = "list field must have exactly one child (DataTypes.arrayField)";
+    return FORY_ERR_ENCODER;
+  }
+  if (f.type_id != FORY_TYPE_LIST && f.type_id != FORY_TYPE_STRUCT && f.num_children != 0) {
+    // DataTypes.java:533-538 "field type should not be nested"
+    *err = "field type should not be nested, but got type id " + std::to_string(f.type_id);
+    return FORY_ERR_ENCODER;
+  }
+  switch (f.type_id) {
+    case FORY_TYPE_BOOL: nd.kind = KIND_BOOL; break;
+    case FORY_TYPE_STRING: case FORY_TYPE_BINARY: nd.kind = KIND_BYTES; break;
+    case FORY_TYPE_STRUCT: nd.kind = KIND_STRUCT; break;
+    case FORY_TYPE_LIST: nd.kind = KIND_LIST; break;
+    default: nd.kind = KIND_FIXED; break;
+  }
+  int32_t cur = at + 1;
+  for (int32_t c = 0; c < f.num_children; ++c) {
+    nd.children.push_back(cur);
+    int32_t nx = 0;
+    int rc = parse_node(d, n, cur, p, depth + 1, &nx, err);
+    if (rc) return rc;
+    cur = nx;
+  }
+  if (depth + 1 > p->max_depth) p->max_depth = depth + 1;
+  *next = cur;
+  return FORY_OK;
+}
+
+// DataTypes.computeHash (DataTypes.java:507-544).
+static int64_t hash_node(int64_t h, const Plan& p, int32_t idx) {
+  const Node& nd = p.nodes[idx];
+  for (;;) {
+    int64_t m, s;
+    if (!__builtin_mul_overflow(h, (int64_t)31, &m) &&
+        !__builtin_add_overflow(m, (int64_t)nd.type_id, &s)) {
+      h = s;
+      break;
+    }
+    h >>= 2;  // catch (ArithmeticException e) { hash = hash >> 2; }
+  }
+  for (int32_t c : nd.children) h = hash_node(h, p, c);
+  return h;
+}
+
+static int32_t bitmap_bytes(int64_t n) { return (int32_t)(((n + 63) / 64) * 8); }
+
+static int compile_field(const Plan& p, int32_t idx, int32_t ordinal, std::vector<Op>* prog,
+                         std::string* err) {
+  const Node& nd = p.nodes[idx];
+  int32_t flags = (nd.nullable ? 1 : 0) | (nd.kind == KIND_BOOL ? 2 : 0);
+  switch (nd.kind) {
+    case KIND_FIXED:
+    case KIND_BOOL:
+      prog->push_back({OP_FIXED, ordinal, idx, nd.width, flags, 0});
+      return FORY_OK;
+    case KIND_BYTES:
+      prog->push_back({OP_BYTES, ordinal, idx, 0, flags, 0});
+      return FORY_OK;
+    case KIND_STRUCT: {
+      size_t begin = prog->size();
+      prog->push_back({OP_STRUCT_BEGIN, ordinal, idx, (int32_t)nd.children.size(), flags, 0});
+      for (size_t k = 0; k < nd.children.size(); ++k) {
+        int rc = compile_field(p, nd.children[k], (int32_t)k, prog, err);
+        if (rc) return rc;
+      }
+      (*prog)[begin].e = (int32_t)prog->size();
+      prog->push_back({OP_STRUCT_END, ordinal, idx, 0, flags, 0});
+      return FORY_OK;
+    }
+    case KIND_LIST: {
+      int32_t item = nd.children[0];
+      const Node& it = p.nodes[item];
+      if (it.kind != KIND_FIXED && it.kind != KIND_BOOL) {
+        *err = "device path supports list<fixed-width> only (got element type id " +
+               std::to_string(it.type_id) + ")";
+        return FORY_ERR_UNSUPPORTED;
+      }
+      int32_t iflags = (it.nullable ? 1 : 0) | (it.kind == KIND_BOOL ? 2 : 0);
+      prog->push_back({OP_LIST, ordinal, idx, item, flags, it.width | (iflags << 8)});
+      return FORY_OK;
+    }
+  }
+  *err = "unknown field kind";
+  return FORY_ERR_ENCODER;
+}
+
+int build_plan(const fory_field_desc* fields, int32_t num_desc, Plan* p, std::string* err) {
+  if (num_desc < 0 || (num_desc > 0 && fields == nullptr)) {
+    *err = "fields is null or num_desc < 0";
+    return FORY_ERR_INVALID_ARGUMENT;
+  }
+  p->desc.assign(fields, fields + num_desc);
+  p->nodes.assign(num_desc, Node());
+  p->top.clear();
+  int32_t at = 0;
+  while (at < num_desc) {
+    p->top.push_back(at);
+    int32_t nx = 0;
+    int rc = parse_node(fields, num_desc, at, p, 0, &nx, err);
+    if (rc) return rc;
+    at = nx;
+  }
+  int64_t h = 17;  // DataTypes.computeSchemaHash (DataTypes.java:499-505)
+  for (int32_t t : p->top) h = hash_node(h, *p, t);
+  p->schema_hash = h;
+  p->bitmap_bytes = bitmap_bytes((int64_t)p->top.size());
+  p->fixed_size = p->bitmap_bytes + 8 * (int32_t)p->top.size();
+  p->fixed_width = true;
+  for (int32_t t : p->top) {
+    int k = p->nodes[t].kind;
+    if (k != KIND_FIXED && k != KIND_BOOL) p->fixed_width = false;
+  }
+  p->program.clear();
+  if (!p->fixed_width) {
+    for (size_t k = 0; k < p->top.size(); ++k) {
+      int rc = compile_field(*p, p->top[k], (int32_t)k, &p->program, err);
+      if (rc) return rc;
+    }
+  }
+  return FORY_OK;
+}
+
+}  // namespace fory_amd

@@ -1,0 +1,91 @@
+// plan.h — host-side layout planner for the MI355X row-format path.
+//
+// Restates, once per schema, what the reference computes once per bean class
+// in Encoders.bean (java/fory-format/.../encoder/Encoders.java:75-78,155):
+//   - field order/nullability come from the caller (TypeInference order,
+//     TypeInference.java:141-254; Descriptor.java:415-423)
+//   - DataTypes.getTypeWidth            (DataTypes.java:68-133,225-227)
+//   - BinaryRowWriter fixed size        (BinaryRowWriter.java:46-52)
+//   - BitUtils.calculateBitmapWidthInBytes (BitUtils.java:175-177)
+//   - DataTypes.computeSchemaHash       (DataTypes.java:499-544)
+// and compiles the per-record write/read sequence the JIT codec would
+// generate (RowEncoderBuilder.java:177-270, BaseBinaryEncoderBuilder.java:149-490)
+// into a small op program executed by one GPU lane per record.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/fory_rowfmt.h"
+
+namespace fory_amd {
+
+// Field kinds the device path distinguishes.
+enum FieldKind : int32_t {
+  KIND_FIXED = 0,   // 1/2/4/8-byte value stored zero-extended in an 8-byte slot
+  KIND_BOOL = 1,    // 1 byte 0/1 (MemoryBuffer.putBoolean)
+  KIND_BYTES = 2,   // utf8 / binary: (offset<<32|size) slot + padded bytes
+  KIND_STRUCT = 3,  // nested row inline in the variable section
+  KIND_LIST = 4,    // BinaryArray inline in the variable section
+};
+
+// Per top-level field of a fixed-width plan (read by the tiled kernels).
+struct FixedFieldDev {
+  const uint8_t* values;    // column values (bound per call)
+  const uint8_t* validity;  // Arrow validity (nullable fields only), may be null
+  uint8_t* out_values;      // decode target
+  uint8_t* out_validity;    // decode target
+  int32_t width;            // 1,2,4,8
+  int32_t flags;            // bit0 nullable, bit1 bool
+};
+
+// Op program for varlen plans: executed per record by one lane.
+enum OpCode : int32_t {
+  OP_FIXED = 0,        // a=ordinal b=col c=width d=flags(bit0 nullable, bit1 bool)
+  OP_BYTES = 1,        // a=ordinal b=col d=flags
+  OP_STRUCT_BEGIN = 2, // a=ordinal b=col c=nfields d=flags e=index of matching END
+  OP_STRUCT_END = 3,
+  OP_LIST = 4,         // a=ordinal b=col c=item col d=flags e=item width | item flags<<8
+};
+
+struct Op {
+  int32_t code, a, b, c, d, e;
+};
+
+struct ColumnDev {  // per-column device view (bound per call)
+  const uint8_t* values;
+  const int32_t* offsets;
+  const uint8_t* validity;
+  uint8_t* out_values;
+  int32_t* out_offsets;
+  uint8_t* out_validity;
+};
+
+struct Node {
+  int32_t type_id = 0;
+  int32_t nullable = 0;
+  int32_t width = -1;
+  int32_t kind = 0;
+  std::vector<int32_t> children;  // desc indices
+};
+
+struct Plan {
+  std::vector<fory_field_desc> desc;
+  std::vector<Node> nodes;
+  std::vector<int32_t> top;       // desc indices of top-level fields
+  int64_t schema_hash = 17;
+  int32_t bitmap_bytes = 0;
+  int32_t fixed_size = 0;
+  bool fixed_width = true;
+  bool any_nullable = false;
+  std::vector<Op> program;        // varlen plans
+  int32_t max_depth = 0;
+};
+
+// Returns FORY_OK or an error code, with a message in `err`.
+int build_plan(const fory_field_desc* fields, int32_t num_desc, Plan* out, std::string* err);
+
+int32_t type_width(int32_t type_id);
+
+}  // namespace fory_amd

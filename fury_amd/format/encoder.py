@@ -1,0 +1,195 @@
+"""Encoders / RowEncoder — batch mirror of the reference's row-format API.
+
+Reference API (java/fory-format/src/main/java/org/apache/fory/format/encoder):
+  Encoders.bean(Class[, initialBufferSize])  -> RowEncoder   Encoders.java:63-231
+  RowEncoder.schema() / toRow(T) / fromRow(BinaryRow)          RowEncoder.java:26-32
+  Encoder.encode(T) / encode(MemoryBuffer, T) / decode(...)    Encoder.java:27-40
+
+Here the unit of work is a batch of N objects held as device columns:
+  encode(columns, n, frame_mode=FRAME_STREAM)  == N x encode(MemoryBuffer, obj)
+                                                  into one fresh buffer
+  encode(columns, n, frame_mode=FRAME_RAW)     == N x toRow(obj).toBytes()
+  decode(rows, frame_mode=...)                 == N x decode(buffer) / fromRow(row)
+Same bytes, same schema hash, same exceptions (errors.py).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Union
+
+from .. import _lib
+from . import native
+from .infer import infer_schema
+from .native import DeviceColumn, NativePlan
+from .types import ArrowType, Schema
+
+FRAME_RAW = _lib.FRAME_RAW
+FRAME_STREAM = _lib.FRAME_STREAM
+
+
+def _torch_dtype(type_id):
+    import torch
+    return {
+        ArrowType.BOOL: torch.uint8, ArrowType.INT8: torch.int8, ArrowType.INT16: torch.int16,
+        ArrowType.INT32: torch.int32, ArrowType.INT64: torch.int64, ArrowType.FLOAT: torch.float32,
+        ArrowType.DOUBLE: torch.float64, ArrowType.DATE32: torch.int32,
+        ArrowType.TIMESTAMP: torch.int64,
+    }[type_id]
+
+
+@dataclass
+class EncodedRows:
+    """Rows (RAW) or frames (STREAM) of a batch, back to back in one device buffer."""
+    buffer: object                 # uint8 tensor, exactly total bytes
+    offsets: Optional[object]      # int64 tensor [n+1] (None for fixed-width: i*stride)
+    num_rows: int
+    frame_mode: int
+    stride: int = -1               # fixed-width plans: bytes per row/frame
+
+
+class RowEncoder:
+    def __init__(self, schema: Schema, bean_class=None, device="cuda"):
+        self._schema = schema
+        self.bean_class = bean_class
+        self.device = device
+        self.plan = NativePlan(schema)
+        self._ws = None
+
+    # -- RowEncoder.schema() ------------------------------------------------
+    def schema(self) -> Schema:
+        return self._schema
+
+    @property
+    def schema_hash(self) -> int:
+        return self.plan.schema_hash
+
+    def workspace(self, n: int):
+        import torch
+        need = max(256, self.plan.workspace_bytes(n))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    # -- encode ---------------------------------------------------------------
+    def encode(self, columns: List[DeviceColumn], num_rows: int,
+               frame_mode: int = FRAME_STREAM) -> EncodedRows:
+        import torch
+        p = self.plan
+        ws = self.workspace(num_rows)
+        arr = native.column_array(columns)
+        status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if p.fixed_width:
+            stride = p.stride(frame_mode)
+            total = num_rows * stride
+            out = torch.empty(max(16, total), dtype=torch.uint8, device=self.device)
+            native.encode(p, arr, num_rows, frame_mode, None, out, status, ws)
+            native.read_status(status)
+            return EncodedRows(out[:total], None, num_rows, frame_mode, stride)
+        offs = torch.empty(num_rows + 1, dtype=torch.int64, device=self.device)
+        native.encoded_size(p, arr, num_rows, frame_mode, offs, ws)
+        total = int(offs[num_rows].item())
+        out = torch.empty(max(16, total), dtype=torch.uint8, device=self.device)
+        native.encode(p, arr, num_rows, frame_mode, offs, out, status, ws)
+        native.read_status(status)
+        return EncodedRows(out[:total], offs, num_rows, frame_mode)
+
+    def to_rows(self, columns: List[DeviceColumn], num_rows: int) -> EncodedRows:
+        return self.encode(columns, num_rows, FRAME_RAW)
+
+    # -- decode ---------------------------------------------------------------
+    def alloc_fixed_outputs(self, num_rows: int) -> List[DeviceColumn]:
+        import torch
+        cols = []
+        for f in self.plan.fields:
+            vals = torch.empty(max(1, num_rows), dtype=_torch_dtype(f.type.id), device=self.device)
+            val = None
+            if f.nullable:
+                val = torch.zeros(_validity_bytes(num_rows), dtype=torch.uint8, device=self.device)
+            cols.append(DeviceColumn(vals, None, val, num_rows))
+        return cols
+
+    def decode(self, rows: Union[EncodedRows, object], num_rows: Optional[int] = None,
+               frame_mode: Optional[int] = None, offsets=None) -> List[DeviceColumn]:
+        import torch
+        if isinstance(rows, EncodedRows):
+            buf, num_rows, frame_mode, offsets = rows.buffer, rows.num_rows, rows.frame_mode, rows.offsets
+        else:
+            buf = rows
+        if frame_mode is None:
+            frame_mode = FRAME_STREAM
+        p = self.plan
+        ws = self.workspace(num_rows)
+        status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if p.fixed_width:
+            if buf.numel() < num_rows * p.stride(frame_mode):
+                from .errors import IndexOutOfBoundsException
+                raise IndexOutOfBoundsException("row buffer shorter than num_rows * row size")
+            cols = self.alloc_fixed_outputs(num_rows)
+            native.decode(p, buf, None, num_rows, frame_mode, native.column_array(cols), status, ws)
+            native.read_status(status)
+            return cols
+        # varlen: offsets/validity/row-level values first, then sizes, then items/bytes
+        n = num_rows
+        fields = p.fields
+        cols = [DeviceColumn(length=n) for _ in fields]
+        item_of = {}
+        for i, f in enumerate(fields):
+            if f.type.id == ArrowType.LIST:
+                item_of[i + 1] = i
+        for i, f in enumerate(fields):
+            if i in item_of:
+                continue  # sized after decode_sizes
+            t = f.type.id
+            if t in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST):
+                cols[i].offsets = torch.zeros(n + 1, dtype=torch.int32, device=self.device)
+            elif t != ArrowType.STRUCT:
+                cols[i].values = torch.empty(max(1, n), dtype=_torch_dtype(t), device=self.device)
+            if f.nullable:
+                cols[i].validity = torch.zeros(_validity_bytes(n), dtype=torch.uint8, device=self.device)
+        if offsets is None:
+            raise ValueError("varlen schema: row offsets are required to decode")
+        native.decode_sizes(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
+        var_idx = [i for i, f in enumerate(fields)
+                   if f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST)]
+        totals = {}
+        if var_idx and n > 0:
+            last = torch.stack([cols[i].offsets[n] for i in var_idx]).cpu().tolist()
+            totals = dict(zip(var_idx, last))
+        native.read_status(status)
+        for i in var_idx:
+            tot = int(totals.get(i, 0))
+            f = fields[i]
+            if f.type.id == ArrowType.LIST:
+                it = fields[i + 1]
+                cols[i + 1] = DeviceColumn(
+                    torch.empty(max(1, tot), dtype=_torch_dtype(it.type.id), device=self.device), None,
+                    torch.zeros(_validity_bytes(tot), dtype=torch.uint8, device=self.device)
+                    if it.nullable else None, tot)
+            else:
+                cols[i].values = torch.empty(max(1, tot), dtype=torch.uint8, device=self.device)
+        native.decode(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
+        native.read_status(status)
+        return cols
+
+    def from_rows(self, rows: EncodedRows) -> List[DeviceColumn]:
+        return self.decode(rows)
+
+
+def _validity_bytes(n: int) -> int:
+    return max(4, ((n + 7) // 8 + 3) // 4 * 4)
+
+
+class Encoders:
+    """Factory mirror of Encoders (Encoders.java:63-231)."""
+
+    @staticmethod
+    def bean(bean_class_or_schema, initial_buffer_size: int = 16, device="cuda") -> RowEncoder:
+        del initial_buffer_size  # device buffers are sized exactly per batch
+        if isinstance(bean_class_or_schema, Schema):
+            return RowEncoder(bean_class_or_schema, None, device)
+        try:
+            schema = infer_schema(bean_class_or_schema)
+        except Exception as e:  # Encoders.java:227-230
+            from .errors import EncoderException
+            raise EncoderException(f"Create encoder failed, \nbeanClass: {bean_class_or_schema}") from e
+        return RowEncoder(schema, bean_class_or_schema, device)

@@ -1,0 +1,130 @@
+"""Device path: thin wrappers over the C-ABI (libfory_rowfmt.so).
+
+Device memory and streams come from torch (plumbing only); all compute is in
+the HIP kernels behind the C-ABI. Nothing here falls back to the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional
+
+from .. import _lib
+from .errors import raise_for
+from .types import ArrowType, Schema, flatten, preorder
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream_handle(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class NativePlan:
+    """fory_rowfmt_plan_create: layout + schema hash of a schema."""
+
+    def __init__(self, schema: Schema):
+        lib = _lib.load()
+        self.schema = schema
+        self._desc, self._ndesc = flatten(schema)
+        h = ctypes.c_void_p()
+        rc = lib.fory_rowfmt_plan_create(self._desc, self._ndesc, ctypes.byref(h))
+        if rc:
+            raise_for(rc, _lib.last_error())
+        self.handle = h
+        info = _lib.PlanInfo()
+        rc = lib.fory_rowfmt_plan_info(h, ctypes.byref(info))
+        if rc:
+            raise_for(rc, _lib.last_error())
+        self.schema_hash = int(info.schema_hash)
+        self.num_fields = int(info.num_fields)
+        self.num_columns = int(info.num_columns)
+        self.bitmap_bytes = int(info.bitmap_bytes)
+        self.fixed_size = int(info.fixed_size)
+        self.fixed_width = bool(info.fixed_width)
+        self.row_size = int(info.row_size)
+        self.fields = preorder(schema)
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                _lib.load().fory_rowfmt_plan_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+    def stride(self, frame_mode: int) -> int:
+        assert self.fixed_width
+        return self.fixed_size + (12 if frame_mode else 0)
+
+    def workspace_bytes(self, num_rows: int) -> int:
+        return int(_lib.load().fory_rowfmt_workspace_bytes(self.handle, num_rows))
+
+
+@dataclass
+class DeviceColumn:
+    """One pre-order column on the device (torch tensors, contiguous)."""
+    values: object = None     # tensor (any dtype, viewed as bytes)
+    offsets: object = None    # int32 tensor [length+1]
+    validity: object = None   # uint8 tensor [ceil(length/8)] (rounded up to 4 bytes)
+    length: int = 0
+
+
+def column_array(cols: List[DeviceColumn]):
+    arr = (_lib.Column * max(1, len(cols)))()
+    for i, c in enumerate(cols):
+        arr[i].values = _ptr(c.values)
+        arr[i].offsets = _ptr(c.offsets)
+        arr[i].validity = _ptr(c.validity)
+        arr[i].length = c.length
+        arr[i].capacity = 0 if c.values is None else c.values.numel() * c.values.element_size()
+    return arr
+
+
+def _check(rc: int):
+    if rc:
+        raise_for(rc, _lib.last_error())
+
+
+def encoded_size(plan: NativePlan, cols_arr, n: int, frame: int, d_offsets, ws, stream=None):
+    lib = _lib.load()
+    s = stream if stream is not None else _stream_handle()
+    _check(lib.fory_rowfmt_encoded_size(plan.handle, cols_arr, n, frame, _ptr(d_offsets),
+                                        _ptr(ws), ws.numel(), s))
+
+
+def encode(plan: NativePlan, cols_arr, n: int, frame: int, d_offsets, out, status, ws,
+           stream=None, capacity: Optional[int] = None):
+    lib = _lib.load()
+    s = stream if stream is not None else _stream_handle()
+    cap = out.numel() if capacity is None else capacity
+    _check(lib.fory_rowfmt_encode(plan.handle, cols_arr, n, frame, _ptr(d_offsets), _ptr(out), cap,
+                                  _ptr(status), _ptr(ws), ws.numel(), s))
+
+
+def decode_sizes(plan: NativePlan, rows, d_offsets, n: int, frame: int, cols_arr, status, ws,
+                 stream=None):
+    lib = _lib.load()
+    s = stream if stream is not None else _stream_handle()
+    _check(lib.fory_rowfmt_decode_sizes(plan.handle, _ptr(rows), _ptr(d_offsets), n, frame, cols_arr,
+                                        _ptr(status), _ptr(ws), ws.numel(), s))
+
+
+def decode(plan: NativePlan, rows, d_offsets, n: int, frame: int, cols_arr, status, ws, stream=None):
+    lib = _lib.load()
+    s = stream if stream is not None else _stream_handle()
+    _check(lib.fory_rowfmt_decode(plan.handle, _ptr(rows), _ptr(d_offsets), n, frame, cols_arr,
+                                  _ptr(status), _ptr(ws), ws.numel(), s))
+
+
+def read_status(status, stream=None):
+    lib = _lib.load()
+    s = stream if stream is not None else _stream_handle()
+    _check(lib.fory_rowfmt_read_status(_ptr(status), s))
+
+
+def is_varlen(f) -> bool:
+    return f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST)

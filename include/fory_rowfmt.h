@@ -1,0 +1,207 @@
+/*
+ * fory_rowfmt.h — C-ABI of the MI355X bulk row-format encoder/decoder.
+ *
+ * This is the drop-in boundary for Apache Fory's row-format path
+ * (java/fory-format). The reference has no FFI for this path: it is the
+ * pure-Java API
+ *   Encoders.bean(Class)            java/fory-format/.../encoder/Encoders.java:63-231
+ *   RowEncoder<T>.toRow / fromRow   java/fory-format/.../encoder/RowEncoder.java:26-32
+ *   Encoder<T>.encode(MemoryBuffer,T) / decode(MemoryBuffer)
+ *                                   java/fory-format/.../encoder/Encoder.java:27-40,
+ *                                   Encoders.java:177-225
+ * driving BinaryRowWriter / BinaryArrayWriter / BinaryRow once per object.
+ * Each entry point below replaces a per-object loop of those calls with one
+ * batched call over columns (the bean fields of N objects laid out as
+ * Arrow-style columns) and produces the same bytes.
+ * A JNI shim binds these symbols one-to-one.
+ *
+ * Conventions
+ *  - Plain C: pointers, sizes, int status codes. No HIP/torch types; `stream`
+ *    is a hipStream_t passed as void* (NULL = default stream).
+ *  - Every data pointer named d_* is DEVICE memory (hipMalloc'd or
+ *    device-visible pinned host memory). Descriptor arrays (fory_column*,
+ *    fory_field_desc*) live in HOST memory and are copied by the call.
+ *  - Calls only enqueue work on `stream`; they never allocate device memory
+ *    and never synchronise, except fory_rowfmt_read_status (documented).
+ *  - Plans are immutable after creation and may be shared across threads and
+ *    streams. Workspaces may not be shared by concurrent calls.
+ *  - Errors: non-zero fory_status; fory_rowfmt_last_error() returns a
+ *    thread-local message. The Java exception each code maps to is listed.
+ *  - Byte layout: docs/specification/row_format_spec.md is empty
+ *    (":22-24 Coming soon"); the Java writer is the spec. See DESIGN.md.
+ */
+#ifndef FORY_ROWFMT_H_
+#define FORY_ROWFMT_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FORY_ROWFMT_ABI_VERSION 1
+
+/* Status codes (mapped to the reference's exceptions). */
+typedef enum fory_status {
+  FORY_OK = 0,
+  FORY_ERR_INVALID_ARGUMENT = 1,  /* IllegalArgumentException / Preconditions */
+  FORY_ERR_UNSUPPORTED = 2,       /* UnsupportedOperationException
+                                     (DataTypes.java:unsupported, BinaryArrayWriter.java:99-101) */
+  FORY_ERR_CAPACITY = 3,          /* IndexOutOfBoundsException (MemoryBuffer.java:303-309):
+                                     output buffer too small, or a row > 2^31-1 bytes */
+  FORY_ERR_SCHEMA_MISMATCH = 4,   /* ClassNotCompatibleException (Encoders.java:182-190) */
+  FORY_ERR_CORRUPT = 5,           /* malformed frame / row (size field out of range) */
+  FORY_ERR_DEVICE = 6,            /* HIP runtime error */
+  FORY_ERR_ENCODER = 7            /* EncoderException (Encoders.java:227-230): bad schema */
+} fory_status;
+
+/* Arrow type ids — the ordinals of org.apache.fory.format.type.ArrowType
+ * (java/fory-format/.../type/ArrowType.java:25-160), which are also the ids
+ * DataTypes.computeSchemaHash folds in (DataTypes.java:499-544). */
+enum fory_type_id {
+  FORY_TYPE_BOOL = 1,
+  FORY_TYPE_INT8 = 3,
+  FORY_TYPE_INT16 = 5,
+  FORY_TYPE_INT32 = 7,
+  FORY_TYPE_INT64 = 9,
+  FORY_TYPE_FLOAT = 11,
+  FORY_TYPE_DOUBLE = 12,
+  FORY_TYPE_STRING = 13,    /* utf8 */
+  FORY_TYPE_BINARY = 14,
+  FORY_TYPE_DATE32 = 16,
+  FORY_TYPE_TIMESTAMP = 18,
+  FORY_TYPE_LIST = 25,
+  FORY_TYPE_STRUCT = 26
+};
+
+/* One node of the schema, flattened in pre-order. A schema is the sequence of
+ * its top-level fields; a STRUCT node is followed by its `num_children` child
+ * subtrees, a LIST node by exactly one subtree (the element field "item").
+ * Order must be the Java schema order: TypeInference.inferSchema
+ * (TypeInference.java:68-80,238-247) = fields sorted by name
+ * (Descriptor.java:415-423). */
+typedef struct fory_field_desc {
+  int32_t type_id;       /* enum fory_type_id */
+  int32_t nullable;      /* 1 = boxed/String/bean/List (TypeInference.java:182-247) */
+  int32_t num_children;  /* STRUCT: >= 0, LIST: 1, others: 0 */
+  int32_t reserved;      /* must be 0 */
+} fory_field_desc;
+
+/* Column of one field (index = pre-order index of its fory_field_desc).
+ *  fixed-width : values = length * width bytes, little-endian
+ *                (BOOL: 1 byte per value, non-zero = true; FLOAT/DOUBLE raw IEEE bits)
+ *  STRING/BINARY: offsets = length+1 int32 Arrow offsets into values (bytes)
+ *  LIST        : offsets = length+1 int32 Arrow offsets into the child column
+ *  STRUCT      : values/offsets unused; children have the same length
+ *  validity    : Arrow validity bitmap, LSB-first, 1 = valid; NULL = all valid.
+ *                Only read/written for nullable fields.
+ *  length      : number of slots (rows for top-level and struct children,
+ *                total items for a list element column).
+ *  capacity    : bytes available at `values` (decode outputs; ignored on encode) */
+typedef struct fory_column {
+  void* values;
+  int32_t* offsets;
+  uint8_t* validity;
+  int64_t length;
+  int64_t capacity;
+} fory_column;
+
+typedef struct fory_plan fory_plan;
+
+typedef struct fory_plan_info {
+  int64_t schema_hash;       /* DataTypes.computeSchemaHash (DataTypes.java:499-544) */
+  int32_t num_fields;        /* top-level fields */
+  int32_t num_columns;       /* = num_desc (one column per pre-order node) */
+  int32_t bitmap_bytes;      /* BitUtils.calculateBitmapWidthInBytes (BitUtils.java:175-177) */
+  int32_t fixed_size;        /* bitmap + 8*num_fields (BinaryRowWriter.java:46-52) */
+  int32_t fixed_width;       /* 1 if every row has the same size (no varlen/nested fields) */
+  int32_t row_size;          /* fixed_size when fixed_width, else -1 */
+} fory_plan_info;
+
+/* Framing modes for a batch of N rows:
+ *  FORY_FRAME_RAW   : rows back to back; row i = BinaryRowWriter.getRow()
+ *                     bytes of object i (BinaryRowWriter.java:131-136,
+ *                     BinaryRow.toBytes BinaryRow.java:229-231).
+ *  FORY_FRAME_STREAM: frames back to back, exactly what N calls of
+ *                     Encoder.encode(MemoryBuffer, T) write into one buffer
+ *                     (Encoders.java:213-225):
+ *                     [int32 LE 8+rowSize][int64 LE schemaHash][row].     */
+enum fory_frame_mode { FORY_FRAME_RAW = 0, FORY_FRAME_STREAM = 1 };
+
+/* --- library / errors --------------------------------------------------- */
+int32_t fory_rowfmt_abi_version(void);
+const char* fory_rowfmt_last_error(void);   /* thread-local; never NULL */
+
+/* --- plan: replaces TypeInference/BinaryRowWriter(Schema)/computeSchemaHash
+ *     done once per bean class in Encoders.bean (Encoders.java:75-78,155). */
+int fory_rowfmt_plan_create(const fory_field_desc* fields, int32_t num_desc,
+                            fory_plan** out_plan);
+void fory_rowfmt_plan_destroy(fory_plan* plan);
+int fory_rowfmt_plan_info(const fory_plan* plan, fory_plan_info* out_info);
+
+/* Device workspace (bytes) every call below needs for `num_rows` rows. */
+int64_t fory_rowfmt_workspace_bytes(const fory_plan* plan, int64_t num_rows);
+
+/* --- encode: replaces N x { writer.reset(); GeneratedRowEncoder.toRow(obj) }
+ *     (Encoders.java:92-95 / 213-225, RowEncoderBuilder.java:177-208).
+ *
+ * fory_rowfmt_encoded_size: writes d_row_offsets[0..N] (int64, device):
+ * d_row_offsets[i] = byte offset of row/frame i in the output,
+ * d_row_offsets[N] = total bytes. Needed before encode for varlen plans;
+ * for fixed-width plans it is i*stride and may be skipped. */
+int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols,
+                             int64_t num_rows, int32_t frame_mode,
+                             int64_t* d_row_offsets, void* d_workspace,
+                             int64_t workspace_bytes, void* stream);
+
+/* Encode N rows into d_out (device, out_capacity bytes, 16-byte aligned for
+ * fixed-width plans). d_row_offsets from fory_rowfmt_encoded_size is required
+ * for varlen plans, ignored (may be NULL) for fixed-width plans, whose
+ * capacity is checked on the host. A varlen row that would end past
+ * out_capacity is skipped and sets *d_status = FORY_ERR_CAPACITY (d_status
+ * may be NULL). Null slots are written as zeros (the bytes Java produces on
+ * a fresh buffer; BinaryWriter.java:123-126). */
+int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols,
+                       int64_t num_rows, int32_t frame_mode,
+                       const int64_t* d_row_offsets, void* d_out,
+                       int64_t out_capacity, int32_t* d_status,
+                       void* d_workspace, int64_t workspace_bytes,
+                       void* stream);
+
+/* --- decode: replaces N x { Encoder.decode(buffer) | RowEncoder.fromRow(row) }
+ *     (Encoders.java:177-195, RowEncoderBuilder.java:215-318, UnsafeTrait.java:68-197).
+ *
+ * d_row_offsets: N+1 offsets of each row (RAW) or frame (STREAM): required
+ * for varlen plans; ignored (may be NULL) for fixed-width plans, whose rows
+ * are i*stride (16-byte aligned d_rows).
+ *
+ * fory_rowfmt_decode_sizes (varlen plans; no-op for fixed-width): fills the
+ * `offsets` array (num_rows+1 int32, device) of every STRING/BINARY/LIST
+ * output column, so the caller can size `values` (bytes) and list element
+ * columns (offsets[num_rows] items). The device path supports list elements
+ * of fixed width only (FORY_ERR_UNSUPPORTED at plan creation otherwise).
+ *
+ * fory_rowfmt_decode: writes values/offsets/validity of out_cols. Null
+ * values decode to 0 (RowEncoderBuilder.java:239-246 leaves the Java default).
+ * In STREAM mode every frame's int32 size and int64 schema hash are checked
+ * (Encoders.java:177-193); a mismatch sets *d_status (device int32) to
+ * FORY_ERR_SCHEMA_MISMATCH or FORY_ERR_CORRUPT. d_status may be NULL. */
+int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows,
+                             const int64_t* d_row_offsets, int64_t num_rows,
+                             int32_t frame_mode, const fory_column* out_cols,
+                             int32_t* d_status, void* d_workspace,
+                             int64_t workspace_bytes, void* stream);
+int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows,
+                       const int64_t* d_row_offsets, int64_t num_rows,
+                       int32_t frame_mode, const fory_column* out_cols,
+                       int32_t* d_status, void* d_workspace,
+                       int64_t workspace_bytes, void* stream);
+
+/* Synchronises `stream` and returns the status word written by decode
+ * (FORY_OK if none). Sets last_error with the reference's message shape. */
+int fory_rowfmt_read_status(const int32_t* d_status, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FORY_ROWFMT_H_ */

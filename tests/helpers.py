@@ -1,0 +1,150 @@
+"""Shared test helpers: schema catalog and column comparison."""
+from __future__ import annotations
+
+from typing import List
+
+import numpy as np
+
+from fury_amd import workloads as W
+from fury_amd.format.columns import HostColumn, build_columns, unpack_validity
+from fury_amd.format.types import ArrowType, DataType, DataTypes, Field, Schema, preorder
+
+
+def all_types_schema() -> Schema:
+    """Every fixed-width type, nullable (boxed) and not (primitive)."""
+    fields = []
+    for k, name in [(ArrowType.BOOL, "b"), (ArrowType.INT8, "i8"), (ArrowType.INT16, "i16"),
+                    (ArrowType.INT32, "i32"), (ArrowType.INT64, "i64"), (ArrowType.FLOAT, "f32"),
+                    (ArrowType.DOUBLE, "f64"), (ArrowType.DATE32, "d32"), (ArrowType.TIMESTAMP, "ts")]:
+        fields.append(Field(name + "_boxed", DataType(k), True))
+        fields.append(Field(name + "_prim", DataType(k), False))
+    return Schema(sorted(fields, key=lambda f: f.name))
+
+
+def random_fixed_columns(schema: Schema, n: int, seed: int, null_rate: float = 0.3) -> List[HostColumn]:
+    from fury_amd.format.columns import NP_DTYPE, pack_validity
+    rng = np.random.default_rng(seed)
+    cols = []
+    for f in schema.fields:
+        dt = NP_DTYPE[f.type.id]
+        raw = rng.integers(0, 256, size=n * np.dtype(dt).itemsize, dtype=np.uint8)
+        v = raw.view(dt).copy()
+        if f.type.id == ArrowType.BOOL:
+            v = (rng.random(n) < 0.5).astype(np.uint8) * rng.integers(1, 255, size=n).astype(np.uint8)
+        valid = None
+        if f.nullable:
+            valid = pack_validity(rng.random(n) >= null_rate)
+        cols.append(HostColumn(v, None, valid, n))
+    return cols
+
+
+def wide_schema(n: int = 300) -> Schema:
+    return Schema([Field(f"c{i:04d}", DataType([ArrowType.INT64, ArrowType.INT32, ArrowType.INT16,
+                                                 ArrowType.INT8][i % 4]), i % 3 == 0) for i in range(n)])
+
+
+def string_list_rows(n: int, seed: int):
+    """Python rows for a schema with strings (incl. unicode/empty/null) and a list<int32>."""
+    rng = np.random.default_rng(seed)
+    alphabet = ["a", "bc", "é", "中文", "😀", "", "xyz" * 5]
+    rows = []
+    for i in range(n):
+        s = None if rng.random() < 0.2 else "".join(rng.choice(alphabet, size=rng.integers(0, 6)))
+        b = None if rng.random() < 0.2 else bytes(rng.integers(0, 256, size=rng.integers(0, 20), dtype=np.uint8))
+        lst = None if rng.random() < 0.2 else [None if rng.random() < 0.1 else int(x)
+                                               for x in rng.integers(-1000, 1000, size=rng.integers(0, 70))]
+        rows.append({"id": int(i), "name": s, "payload": b, "vals": lst,
+                     "score": None if rng.random() < 0.3 else float(rng.standard_normal())})
+    return rows
+
+
+def string_list_schema() -> Schema:
+    return Schema([
+        Field("id", DataType(ArrowType.INT64), False),
+        Field("name", DataType(ArrowType.STRING), True),
+        Field("payload", DataType(ArrowType.BINARY), True),
+        Field("score", DataType(ArrowType.DOUBLE), True),
+        DataTypes.array_field("vals", Field("item", DataType(ArrowType.INT32), True)),
+    ])
+
+
+def columns_equal(schema: Schema, a: List[HostColumn], b: List[HostColumn]) -> List[str]:
+    """Semantic equality of two pre-order column sets (values compared only where valid)."""
+    errs = []
+    fields = preorder(schema)
+    parent = _struct_parents(schema)
+    eff = {}
+    for i, f in enumerate(fields):
+        ca, cb = a[i], b[i]
+        n = ca.length
+        if ca.length != cb.length:
+            errs.append(f"{i}:{f.name} length {ca.length} != {cb.length}")
+            continue
+        va = unpack_validity(ca.validity if f.nullable else None, n)
+        vb = unpack_validity(cb.validity if f.nullable else None, n)
+        if i in parent:  # a child of a null struct is absent: compare under the parent's validity
+            pv = eff.get(parent[i])
+            if pv is not None:
+                va, vb = va & pv, vb & pv
+        eff[i] = va
+        if not np.array_equal(va, vb):
+            errs.append(f"{i}:{f.name} validity differs at {np.nonzero(va != vb)[0][:5]}")
+            continue
+        t = f.type.id
+        if ca.values is not None and t not in (ArrowType.STRING, ArrowType.BINARY):
+            xa = np.asarray(ca.values)[:n].view(np.uint8).reshape(n, -1) if n else np.zeros((0, 1), np.uint8)
+            xb = np.asarray(cb.values)[:n].view(np.uint8).reshape(n, -1) if n else np.zeros((0, 1), np.uint8)
+            if t == ArrowType.BOOL:
+                xa, xb = (xa != 0), (xb != 0)
+            bad = np.nonzero(np.any(xa != xb, axis=1) & va)[0]
+            if len(bad):
+                errs.append(f"{i}:{f.name} values differ at rows {bad[:5]}")
+        if t in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST):
+            oa = np.asarray(ca.offsets)[: n + 1].astype(np.int64)
+            ob = np.asarray(cb.offsets)[: n + 1].astype(np.int64)
+            la, lb = np.diff(oa), np.diff(ob)
+            bad = np.nonzero((la != lb) & va)[0]
+            if len(bad):
+                errs.append(f"{i}:{f.name} lengths differ at rows {bad[:5]}")
+                continue
+            if t != ArrowType.LIST:
+                for r in np.nonzero(va)[0]:
+                    if bytes(np.asarray(ca.values)[oa[r]:oa[r + 1]]) != bytes(np.asarray(cb.values)[ob[r]:ob[r + 1]]):
+                        errs.append(f"{i}:{f.name} bytes differ at row {r}")
+                        break
+    return errs
+
+
+def catalog():
+    """name -> (schema, host column factory(n, seed))."""
+    return {
+        "struct104": (W.struct_schema(), lambda n, s: W.struct_host_columns(n, seed_base=17 + s)),
+        "struct104_boxed": (W.struct_schema(boxed=True),
+                            lambda n, s: random_fixed_columns(W.struct_schema(boxed=True), n, s)),
+        "all_types": (all_types_schema(), lambda n, s: random_fixed_columns(all_types_schema(), n, s)),
+        "wide300": (wide_schema(), lambda n, s: random_fixed_columns(wide_schema(), n, s)),
+        "mixed40": (W.mixed_schema(), lambda n, s: W.mixed_host_columns(n, seed=23 + s)),
+        "mixed40_nulls": (W.mixed_schema(), lambda n, s: W.mixed_host_columns(n, seed=23 + s, null_rate=0.2)),
+        "nested": (W.nested_schema(), lambda n, s: W.nested_host_columns(n, seed=29 + s)),
+        "nested_nulls": (W.nested_schema(), lambda n, s: W.nested_host_columns(n, seed=29 + s, null_rate=0.25)),
+        "strings_lists": (string_list_schema(),
+                          lambda n, s: build_columns(string_list_schema(), string_list_rows(n, s))),
+    }
+
+
+def _struct_parents(schema: Schema):
+    """pre-order index -> index of its parent STRUCT (struct children only)."""
+    out = {}
+    pos = [0]
+
+    def visit(f, par):
+        me = pos[0]
+        pos[0] += 1
+        if par is not None:
+            out[me] = par
+        for c in f.children:
+            visit(c, me if f.type.id == ArrowType.STRUCT else None)
+
+    for f in schema.fields:
+        visit(f, None)
+    return out

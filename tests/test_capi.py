@@ -1,0 +1,100 @@
+"""CPU: the C-ABI library loads, exports every symbol include/fory_rowfmt.h
+declares, and its host-side planner (no GPU needed) matches the reference:
+schema hash (python/pyfory/format/infer.py golden values), fixed size
+(BinaryRowWriter.java:46-52), bitmap width (BitUtils.java:175-177), and the
+reference's error behaviour for bad schemas."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from fury_amd import _lib
+from fury_amd import workloads as W
+from fury_amd.format import errors
+from fury_amd.format.native import NativePlan
+from fury_amd.format.types import ArrowType, DataType, DataTypes, Field, Schema, flatten
+
+from helpers import all_types_schema, string_list_schema, wide_schema
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                      "fory_rowfmt.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fory_rowfmt_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 11
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_lib.PROTOTYPES), "ctypes prototypes out of sync with the header"
+    assert lib.fory_rowfmt_abi_version() == 1
+
+
+def test_plan_matches_reference(golden):
+    cases = {"struct104": W.struct_schema(), "mixed40": W.mixed_schema(), "nested": W.nested_schema(),
+             "struct_boxed": W.struct_schema(boxed=True)}
+    for name, s in cases.items():
+        p = NativePlan(s)
+        assert p.schema_hash == golden["schema_hash"][name], name
+    p = NativePlan(W.struct_schema())
+    assert (p.num_fields, p.bitmap_bytes, p.fixed_size, p.fixed_width, p.row_size) == (104, 16, 848, True, 848)
+    p = NativePlan(W.mixed_schema())
+    assert (p.num_fields, p.bitmap_bytes, p.fixed_size, p.fixed_width, p.row_size) == (40, 8, 328, False, -1)
+    p = NativePlan(W.nested_schema())
+    assert (p.num_fields, p.num_columns, p.fixed_size, p.fixed_width) == (3, 7, 32, False)
+
+
+def test_edge_plans(golden):
+    s = Schema([Field(f"c{i:03d}", DataType(ArrowType.INT64), False) for i in range(300)])
+    p = NativePlan(s)
+    assert p.schema_hash == golden["schema_hash"]["wide_300"]  # exercises the overflow (>> 2) path
+    assert p.bitmap_bytes == 40 and p.fixed_size == 40 + 2400
+    assert NativePlan(Schema([])).schema_hash == golden["schema_hash"]["empty"]
+    assert NativePlan(Schema([])).fixed_size == 0
+    for s in (all_types_schema(), wide_schema(), string_list_schema()):
+        NativePlan(s)
+
+
+def test_plan_errors():
+    lib = _lib.load()
+    bad_nested = Schema([Field("x", DataType(ArrowType.INT32), False, [Field("y", DataType(ArrowType.INT32))])])
+    with pytest.raises(errors.EncoderException):
+        NativePlan(bad_nested)
+    with pytest.raises(errors.UnsupportedOperationException):
+        NativePlan(Schema([Field("m", DataType(ArrowType.MAP), True)]))
+    with pytest.raises(errors.UnsupportedOperationException):  # device path: list<fixed> only
+        NativePlan(Schema([DataTypes.array_field("l", Field("item", DataType(ArrowType.STRING)))]))
+    # truncated descriptor: a struct promising 2 children with only 1 present
+    desc, n = flatten(Schema([DataTypes.struct_field("s", True, [Field("a", DataType(ArrowType.INT32))])]))
+    desc[0].num_children = 2
+    h = ctypes.c_void_p()
+    assert lib.fory_rowfmt_plan_create(desc, n, ctypes.byref(h)) == _lib.FORY_ERR_ENCODER
+    assert "truncated" in _lib.last_error()
+    desc[0].num_children = 1
+    desc[0].reserved = 5
+    assert lib.fory_rowfmt_plan_create(desc, n, ctypes.byref(h)) == _lib.FORY_ERR_INVALID_ARGUMENT
+
+
+def test_argument_validation_without_gpu():
+    """Calls that fail validation return before touching the device."""
+    lib = _lib.load()
+    p = NativePlan(W.struct_schema())
+    cols = (_lib.Column * 104)()
+    # workspace too small
+    rc = lib.fory_rowfmt_encode(p.handle, cols, 10, 0, None, ctypes.c_void_p(16), 1 << 20, None,
+                                None, 0, None)
+    assert rc == _lib.FORY_ERR_INVALID_ARGUMENT and "workspace" in _lib.last_error()
+    # bad frame mode
+    rc = lib.fory_rowfmt_encode(p.handle, cols, 10, 7, None, None, 0, None, None, 0, None)
+    assert rc == _lib.FORY_ERR_INVALID_ARGUMENT
+    # zero rows: nothing to do
+    rc = lib.fory_rowfmt_encode(p.handle, cols, 0, 1, None, None, 0, None, None, 0, None)
+    assert rc == _lib.FORY_OK
+    assert lib.fory_rowfmt_workspace_bytes(p.handle, 1 << 26) > 104 * 40
