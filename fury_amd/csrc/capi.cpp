@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -91,8 +92,12 @@ int bind_fixed(const Plan& p, const fory_column* cols, int64_t n, bool decode,
       f.values = static_cast<const uint8_t*>(c.values);
       f.validity = nd.nullable ? c.validity : nullptr;
     }
+    f.slot = (int32_t)k;
     (*out)[k] = f;
   }
+  // width groups 8, 4, 2, 1 (stable): see FixedFieldDev
+  std::stable_sort(out->begin(), out->end(),
+                   [](const FixedFieldDev& a, const FixedFieldDev& b) { return a.width > b.width; });
   return FORY_OK;
 }
 
@@ -135,6 +140,15 @@ fory_amd::FixedLaunch fixed_launch(const Plan& p, const void* table, int64_t n, 
   L.num_rows = n;
   L.any_nullable = p.any_nullable ? 1 : 0;
   L.frame = frame;
+  // width-group boundaries of the sorted table (bind_fixed)
+  const int widths[4] = {8, 4, 2, 1};
+  int at = 0;
+  for (int g = 0; g < 4; ++g) {
+    L.group[g] = at;
+    for (int32_t t : p.top)
+      if (p.nodes[t].width == widths[g]) ++at;
+  }
+  L.group[4] = at;
   return L;
 }
 

@@ -19,6 +19,7 @@ struct FixedLaunch {
   int64_t num_rows;
   int32_t any_nullable;
   int32_t frame;
+  int32_t group[5];             // table index where the 8/4/2/1-byte groups start; group[4] = num_fields
 };
 
 hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s);

@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -32,30 +33,44 @@ namespace fory_amd {
 
 namespace {
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native 16-B vector (SROA-friendly)
+
 constexpr int kWG = 256;         // 4 waves
 constexpr int kWaves = kWG / 64;
 
 __device__ __forceinline__ void st32(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 
+// Pointers read from a descriptor table are generic (flat) to the compiler;
+// a flat access forces s_waitcnt vmcnt(0) lgkmcnt(0) before any dependent
+// use. Cast them to the global address space so loads/stores are global_*.
+#define GAS __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ const GAS T* gp(const T* p) { return (const GAS T*)p; }
+template <typename T>
+__device__ __forceinline__ GAS T* gp(T* p) { return (GAS T*)p; }
+
 // Loads the `width` low bytes of element `i` (little-endian, zero-extended).
-__device__ __forceinline__ uint64_t load_elem(const uint8_t* __restrict__ base, int width, int64_t i) {
+__device__ __forceinline__ uint64_t load_elem(const uint8_t* base, int width, int64_t i) {
   switch (width) {
-    case 8: return *reinterpret_cast<const uint64_t*>(base + i * 8);
-    case 4: return *reinterpret_cast<const uint32_t*>(base + i * 4);
-    case 2: return *reinterpret_cast<const uint16_t*>(base + i * 2);
-    default: return base[i];
+    case 8: return *gp(reinterpret_cast<const uint64_t*>(base + i * 8));
+    case 4: return *gp(reinterpret_cast<const uint32_t*>(base + i * 4));
+    case 2: return *gp(reinterpret_cast<const uint16_t*>(base + i * 2));
+    default: return *gp(base + i);
   }
 }
 
-__device__ __forceinline__ void store_elem(uint8_t* __restrict__ base, int width, int64_t i, uint64_t v) {
+__device__ __forceinline__ void store_elem(uint8_t* base, int width, int64_t i, uint64_t v) {
   switch (width) {
-    case 8: *reinterpret_cast<uint64_t*>(base + i * 8) = v; break;
-    case 4: *reinterpret_cast<uint32_t*>(base + i * 4) = (uint32_t)v; break;
-    case 2: *reinterpret_cast<uint16_t*>(base + i * 2) = (uint16_t)v; break;
-    default: base[i] = (uint8_t)v; break;
+    case 8: *gp(reinterpret_cast<uint64_t*>(base + i * 8)) = v; break;
+    case 4: *gp(reinterpret_cast<uint32_t*>(base + i * 4)) = (uint32_t)v; break;
+    case 2: *gp(reinterpret_cast<uint16_t*>(base + i * 2)) = (uint16_t)v; break;
+    default: *gp(base + i) = (uint8_t)v; break;
   }
 }
+
+__device__ __forceinline__ uint8_t load_byte(const uint8_t* p) { return *gp(p); }
+__device__ __forceinline__ void store_byte(uint8_t* p, uint8_t v) { *gp(p) = v; }
 
 __device__ __forceinline__ void set_status(int32_t* status, int32_t code) {
   if (status) atomicCAS(status, 0, code);
@@ -64,15 +79,121 @@ __device__ __forceinline__ void set_status(int32_t* status, int32_t code) {
 // ---------------------------------------------------------------------------
 // Fixed-width encode: columns -> rows (tiled through LDS)
 // ---------------------------------------------------------------------------
-// TR = records per tile (64 -> one field per wave-instruction; 32/16/8 for
-// wide rows -> 64/TR fields per wave-instruction). U = fields each lane keeps
-// in flight before writing LDS (memory-level parallelism).
-template <int TR, bool FRAME>
-__global__ __launch_bounds__(kWG) void encode_fixed_kernel(FixedLaunch L, uint8_t* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int FPW = 64 / TR;       // fields per wave-instruction
+// One tile = TR records. TR = 64: lane = record, one field per wave
+// instruction (descriptor wave-uniform -> scalar loads). TR = 32/16/8 (wide
+// rows): 64/TR fields per wave instruction. The host sorts the field table
+// into width groups (8/4/2/1 bytes) so every load loop has a compile-time
+// width and distinct destination registers: a batch of U column loads is in
+// flight before the first LDS write. Dead lanes of a partial tile re-read
+// record r0 (no divergent branch around the loads).
+
+template <int TR>
+__device__ __forceinline__ int field_of(int fb, int u, int fstep, int fsub) {
+  const int f = fb + u * fstep + fsub;
+  if constexpr (TR == 64) return __builtin_amdgcn_readfirstlane(f);
+  return f;
+}
+
+template <int W>
+__device__ __forceinline__ uint64_t ldw(const uint8_t* base, int64_t i) {
+  if constexpr (W == 8) return *gp(reinterpret_cast<const uint64_t*>(base) + i);
+  if constexpr (W == 4) return *gp(reinterpret_cast<const uint32_t*>(base) + i);
+  if constexpr (W == 2) return *gp(reinterpret_cast<const uint16_t*>(base) + i);
+  return *gp(base + i);
+}
+
+template <int W>
+__device__ __forceinline__ void stw(uint8_t* base, int64_t i, uint64_t v) {
+  if constexpr (W == 8) *gp(reinterpret_cast<uint64_t*>(base) + i) = v;
+  else if constexpr (W == 4) *gp(reinterpret_cast<uint32_t*>(base) + i) = (uint32_t)v;
+  else if constexpr (W == 2) *gp(reinterpret_cast<uint16_t*>(base) + i) = (uint16_t)v;
+  else *gp(base + i) = (uint8_t)v;
+}
+
+// BinaryWriter.setNullAt's input: Arrow validity bit of record idx (nullable fields).
+__device__ __forceinline__ bool input_null(const FixedFieldDev& fd, int64_t idx) {
+  return (fd.flags & 1) && fd.validity && !((load_byte(fd.validity + (idx >> 3)) >> (idx & 7)) & 1);
+}
+
+// Stores a slot into the LDS row image (BinaryRowWriter.write: slot zeroed,
+// value in the low bytes; null -> bit set, slot left zero; bool -> 0/1).
+template <bool FRAME>
+__device__ __forceinline__ void put_slot(uint8_t* row, int hdr_bm, int slot, uint64_t x, bool isnull, int flags) {
+  constexpr int HDR = FRAME ? 12 : 0;
+  if (flags & 2) x = x ? 1 : 0;  // MemoryBuffer.putBoolean
+  if (isnull) {
+    x = 0;
+    atomicOr(reinterpret_cast<uint32_t*>(row + HDR + ((slot >> 5) << 2)), 1u << (slot & 31));
+  }
+  uint8_t* p = row + hdr_bm + 8 * slot;
+  if (FRAME) {  // frame rows start 12 bytes into the frame: slots are only 4-byte aligned
+    st32(p, (uint32_t)x);
+    st32(p + 4, (uint32_t)(x >> 32));
+  } else {
+    *reinterpret_cast<uint64_t*>(p) = x;
+  }
+}
+
+// Frame header [i32 8+rowSize][i64 hash] + zeroed null bitmap of this lane's row.
+template <bool FRAME>
+__device__ __forceinline__ void put_header(uint8_t* row, const FixedLaunch& L) {
+  if (FRAME) {
+    st32(row, (uint32_t)(8 + L.fixed_size));
+    st32(row + 4, (uint32_t)(uint64_t)L.schema_hash);
+    st32(row + 8, (uint32_t)((uint64_t)L.schema_hash >> 32));
+  }
+  constexpr int HDR = FRAME ? 12 : 0;
+  for (int b = 0; b < L.bitmap_bytes; b += 4) st32(row + HDR + b, 0u);
+}
+
+// LDS tile image -> HBM: `bytes` contiguous bytes, 16-B stores, 4 in flight.
+__device__ __forceinline__ void store_tile(const uint8_t* lds, uint8_t* __restrict__ dst, int bytes, int tid) {
+  const int n16 = bytes >> 4;
+  int c = tid;
+  for (; c + 3 * kWG < n16; c += 4 * kWG) {
+    const u32x4 x0 = *reinterpret_cast<const u32x4*>(lds + c * 16);
+    const u32x4 x1 = *reinterpret_cast<const u32x4*>(lds + (c + kWG) * 16);
+    const u32x4 x2 = *reinterpret_cast<const u32x4*>(lds + (c + 2 * kWG) * 16);
+    const u32x4 x3 = *reinterpret_cast<const u32x4*>(lds + (c + 3 * kWG) * 16);
+    *reinterpret_cast<u32x4*>(dst + c * 16) = x0;
+    *reinterpret_cast<u32x4*>(dst + (c + kWG) * 16) = x1;
+    *reinterpret_cast<u32x4*>(dst + (c + 2 * kWG) * 16) = x2;
+    *reinterpret_cast<u32x4*>(dst + (c + 3 * kWG) * 16) = x3;
+  }
+  for (; c < n16; c += kWG) *reinterpret_cast<u32x4*>(dst + c * 16) = *reinterpret_cast<const u32x4*>(lds + c * 16);
+  const int tail4 = (bytes & 15) >> 2;
+  if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
+}
+
+// One width group [g0, g1) of the encode: U loads in flight, then U slots.
+template <int W, int TR, bool FRAME>
+__device__ __forceinline__ void enc_group(const FixedFieldDev* __restrict__ fields, int g0, int g1, int wave, int fsub,
+                                          int64_t idx, uint8_t* row, int hdr_bm) {
+  constexpr int FPW = 64 / TR;
   constexpr int FSTEP = kWaves * FPW;
   constexpr int U = 16;
+  for (int pb = g0 + wave * FPW; pb < g1; pb += FSTEP * U) {
+    uint64_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = field_of<TR>(pb, u, FSTEP, fsub);
+      v[u] = p < g1 ? ldw<W>(fields[p].values, idx) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = field_of<TR>(pb, u, FSTEP, fsub);
+      if (p < g1) {
+        const FixedFieldDev& fd = fields[p];
+        put_slot<FRAME>(row, hdr_bm, fd.slot, v[u], input_null(fd, idx), fd.flags);
+      }
+    }
+  }
+}
+
+template <int TR, bool FRAME>
+__global__ __launch_bounds__(kWG) void encode_fixed_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
+                                                           uint8_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int HDR = FRAME ? 12 : 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -82,83 +203,192 @@ __global__ __launch_bounds__(kWG) void encode_fixed_kernel(FixedLaunch L, uint8_
   const int64_t r0 = (int64_t)blockIdx.x * TR;
   const int64_t left = L.num_rows - r0;
   const int rows = left < TR ? (int)left : TR;
-  const int stride = L.stride;
-  const int nf = L.num_fields;
-  const int bm = L.bitmap_bytes;
-  uint8_t* row = lds + r * stride;
-  const int64_t grow = r0 + r;
-  const bool live = r < rows;
+  const int hdr_bm = HDR + L.bitmap_bytes;
+  uint8_t* row = lds + r * L.stride;
+  const int64_t idx = r < rows ? r0 + r : r0;
 
-  // Phase 0: frame header + zeroed null bitmap, one writer per record.
-  if (wave == 0 && fsub == 0) {
-    if (FRAME) {
-      st32(row, (uint32_t)(8 + L.fixed_size));
-      st32(row + 4, (uint32_t)(uint64_t)L.schema_hash);
-      st32(row + 8, (uint32_t)((uint64_t)L.schema_hash >> 32));
-    }
-    for (int b = 0; b < bm; b += 4) st32(row + HDR + b, 0u);
-  }
-  if (L.any_nullable) __syncthreads();  // null bits are OR-ed into the bitmap below
+  if (wave == 0 && fsub == 0) put_header<FRAME>(row, L);
+  if (L.any_nullable) __syncthreads();  // null bits are OR-ed into the zeroed bitmap
 
-  // Phase 1: column loads (coalesced: lane = record) -> LDS slots.
-  for (int fb = wave * FPW; fb < nf; fb += FSTEP * U) {
-    uint64_t v[U];
-    bool isnull[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int f = fb + u * FSTEP + fsub;
-      v[u] = 0;
-      isnull[u] = false;
-      if (f < nf && live) {
-        const FixedFieldDev fd = L.fields[f];
-        v[u] = load_elem(fd.values, fd.width, grow);
-        if ((fd.flags & 1) && fd.validity)
-          isnull[u] = !((fd.validity[grow >> 3] >> (grow & 7)) & 1);
-        if (fd.flags & 2) v[u] = v[u] ? 1 : 0;  // MemoryBuffer.putBoolean
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int f = fb + u * FSTEP + fsub;
-      if (f < nf) {
-        uint64_t x = v[u];
-        if (isnull[u]) {  // BinaryWriter.setNullAt: bit set, slot left zero
-          x = 0;
-          atomicOr(reinterpret_cast<uint32_t*>(row + HDR + ((f >> 5) << 2)), 1u << (f & 31));
-        }
-        uint8_t* slot = row + HDR + bm + 8 * f;
-        if (FRAME) {  // 4-byte aligned only (frame = 12-byte header)
-          st32(slot, (uint32_t)x);
-          st32(slot + 4, (uint32_t)(x >> 32));
-        } else {
-          *reinterpret_cast<uint64_t*>(slot) = x;
-        }
-      }
-    }
-  }
+  enc_group<8, TR, FRAME>(fields, L.group[0], L.group[1], wave, fsub, idx, row, hdr_bm);
+  enc_group<4, TR, FRAME>(fields, L.group[1], L.group[2], wave, fsub, idx, row, hdr_bm);
+  enc_group<2, TR, FRAME>(fields, L.group[2], L.group[3], wave, fsub, idx, row, hdr_bm);
+  enc_group<1, TR, FRAME>(fields, L.group[3], L.group[4], wave, fsub, idx, row, hdr_bm);
   __syncthreads();
+  store_tile(lds, out + r0 * L.stride, rows * L.stride, tid);
+}
 
-  // Phase 2: the tile's rows are TR*stride contiguous bytes -> 16-B stores.
-  const int64_t bytes = (int64_t)rows * stride;
-  uint8_t* dst = out + r0 * stride;
-  const int n16 = (int)(bytes >> 4);
-  for (int c = tid; c < n16; c += kWG) {
-    const uint4 x = *reinterpret_cast<const uint4*>(lds + c * 16);
-    *reinterpret_cast<uint4*>(dst + c * 16) = x;
+// Persistent, software-pipelined encode (TR = 64). Each wave keeps its share
+// of the next tile's column values in VGPRs (per width group at most
+// 4*M8 / 4*M4 / 4*M2 / 4*M1 fields per schema) while this tile's rows are
+// stored.
+template <int W, typename T, int M>
+__device__ __forceinline__ void pipe_load(T (&v)[M], const FixedFieldDev* __restrict__ fields, int g0, int g1,
+                                          int wave, int64_t idx) {
+#pragma unroll
+  for (int u = 0; u < M; ++u) {
+    const int p = __builtin_amdgcn_readfirstlane(g0 + wave + u * kWaves);
+    if (p < g1) v[u] = (T)ldw<W>(fields[p].values, idx);
   }
-  const int tail4 = (int)(bytes & 15) >> 2;
-  if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
+}
+
+template <bool FRAME, typename T, int M>
+__device__ __forceinline__ void pipe_put(const T (&v)[M], const FixedFieldDev* __restrict__ fields, int g0, int g1,
+                                         int wave, int64_t idx, uint8_t* row, int hdr_bm) {
+#pragma unroll
+  for (int u = 0; u < M; ++u) {
+    const int p = __builtin_amdgcn_readfirstlane(g0 + wave + u * kWaves);
+    if (p < g1) {
+      const FixedFieldDev& fd = fields[p];
+      put_slot<FRAME>(row, hdr_bm, fd.slot, (uint64_t)v[u], input_null(fd, idx), fd.flags);
+    }
+  }
+}
+
+constexpr int kM8 = 16, kM4 = 16, kM2 = 8, kM1 = 8;
+
+template <bool FRAME>
+__global__ __launch_bounds__(kWG, 2) void encode_fixed_pipe_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
+                                                                uint8_t* __restrict__ out, int64_t tiles) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int HDR = FRAME ? 12 : 0;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int stride = L.stride;
+  const int hdr_bm = HDR + L.bitmap_bytes;
+  uint8_t* row = lds + lane * stride;
+  int64_t t = blockIdx.x;
+  if (t >= tiles) return;
+
+  uint64_t v8[kM8];
+  uint32_t v4[kM4], v2[kM2], v1[kM1];
+  int64_t idx = t * 64 + lane < L.num_rows ? t * 64 + lane : t * 64;
+  pipe_load<8>(v8, fields, L.group[0], L.group[1], wave, idx);
+  pipe_load<4>(v4, fields, L.group[1], L.group[2], wave, idx);
+  pipe_load<2>(v2, fields, L.group[2], L.group[3], wave, idx);
+  pipe_load<1>(v1, fields, L.group[3], L.group[4], wave, idx);
+  if (wave == 0) put_header<FRAME>(row, L);  // constant across tiles
+  for (;;) {
+    if (L.any_nullable) {
+      if (wave == 0) put_header<FRAME>(row, L);  // re-zero the bitmap
+      __syncthreads();
+    }
+    pipe_put<FRAME>(v8, fields, L.group[0], L.group[1], wave, idx, row, hdr_bm);
+    pipe_put<FRAME>(v4, fields, L.group[1], L.group[2], wave, idx, row, hdr_bm);
+    pipe_put<FRAME>(v2, fields, L.group[2], L.group[3], wave, idx, row, hdr_bm);
+    pipe_put<FRAME>(v1, fields, L.group[3], L.group[4], wave, idx, row, hdr_bm);
+    __syncthreads();
+    const int64_t r0 = t * 64;
+    const int64_t left = L.num_rows - r0;
+    const int rows = left < 64 ? (int)left : 64;
+    const int64_t tn = t + gridDim.x;
+    if (tn < tiles) {  // next tile's loads go out before this tile's stores
+      idx = tn * 64 + lane < L.num_rows ? tn * 64 + lane : tn * 64;
+      pipe_load<8>(v8, fields, L.group[0], L.group[1], wave, idx);
+      pipe_load<4>(v4, fields, L.group[1], L.group[2], wave, idx);
+      pipe_load<2>(v2, fields, L.group[2], L.group[3], wave, idx);
+      pipe_load<1>(v1, fields, L.group[3], L.group[4], wave, idx);
+    }
+    store_tile(lds, out + r0 * stride, rows * stride, tid);
+    __syncthreads();
+    if (tn >= tiles) break;
+    t = tn;
+  }
 }
 
 // ---------------------------------------------------------------------------
 // Fixed-width decode: rows -> columns
 // ---------------------------------------------------------------------------
-template <int TR, bool FRAME>
-__global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const uint8_t* __restrict__ in,
-                                                           int32_t* status) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+// LDS-DMA of `bytes` contiguous bytes into the LDS image (1 KiB per wave
+// instruction; lanes past the end masked off).
+__device__ __forceinline__ void dma_tile(uint8_t* lds, const uint8_t* __restrict__ src, int bytes, int tid, int wave) {
+  const int n16 = bytes >> 4;
+  for (int c0 = 0; c0 < n16; c0 += kWG) {
+    const int c = c0 + tid;
+    if (c < n16)
+      __builtin_amdgcn_global_load_lds((const GAS void*)(src + (int64_t)c * 16),
+                                       (__attribute__((address_space(3))) void*)(lds + (c0 + wave * 64) * 16), 16,
+                                       0, 0);
+  }
+  const int tail4 = (bytes & 15) >> 2;
+  if (tid < tail4) st32(lds + n16 * 16 + tid * 4, ld32(src + n16 * 16 + tid * 4));
+}
+
+template <bool FRAME>
+__device__ __forceinline__ void check_frame(const uint8_t* row, const FixedLaunch& L, int32_t* status) {
+  // Encoders.decode (Encoders.java:177-190): size, then the schema hash.
+  const uint32_t len = ld32(row);
+  const uint64_t h = (uint64_t)ld32(row + 4) | ((uint64_t)ld32(row + 8) << 32);
+  if (h != (uint64_t)L.schema_hash) set_status(status, FORY_ERR_SCHEMA_MISMATCH);
+  else if (len != (uint32_t)(8 + L.fixed_size)) set_status(status, FORY_ERR_CORRUPT);
+}
+
+// Slot of an LDS row (UnsafeTrait.getX: the low W bytes).
+template <int W, bool FRAME>
+__device__ __forceinline__ uint64_t get_slot(const uint8_t* row, int hdr_bm, int slot) {
+  const uint8_t* p = row + hdr_bm + 8 * slot;
+  if constexpr (W == 8) {
+    if (FRAME) return (uint64_t)ld32(p) | ((uint64_t)ld32(p + 4) << 32);
+    return *reinterpret_cast<const uint64_t*>(p);
+  }
+  return ld32(p);
+}
+
+// Arrow validity of field fd for the TR records of this lane group.
+template <int TR>
+__device__ __forceinline__ void put_validity(const FixedFieldDev& fd, bool isnull, bool live, int r, int fsub,
+                                             int64_t r0, int rows) {
+  const uint64_t m = __ballot(!isnull && live);
+  if (r == 0) {
+    const uint64_t mine = (m >> (fsub * TR)) & (TR == 64 ? ~0ull : ((1ull << TR) - 1));
+    uint8_t* vb = fd.out_validity + (r0 >> 3);
+    const int nb = (rows + 7) >> 3;
+    for (int b = 0; b < nb; ++b) store_byte(vb + b, (uint8_t)(mine >> (8 * b)));
+  }
+}
+
+// Decodes slot values of one width group: null -> 0 (RowEncoderBuilder.java:239-246),
+// bool -> 0/1 (MemoryBuffer.getBoolean), coalesced column stores.
+template <int W, int TR, bool FRAME>
+__device__ __forceinline__ void dec_group(const FixedFieldDev* __restrict__ fields, int g0, int g1, int wave, int fsub,
+                                          int r, const uint8_t* row, int hdr_bm, int hdr, bool live, int64_t grow,
+                                          int64_t r0, int rows) {
   constexpr int FPW = 64 / TR;
   constexpr int FSTEP = kWaves * FPW;
+  constexpr int U = 8;
+  for (int pb = g0 + wave * FPW; pb < g1; pb += FSTEP * U) {
+    uint64_t x[U];
+    bool nul[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = field_of<TR>(pb, u, FSTEP, fsub);
+      x[u] = 0;
+      nul[u] = true;
+      if (p < g1) {
+        const int slot = fields[p].slot;
+        nul[u] = (ld32(row + hdr + ((slot >> 5) << 2)) >> (slot & 31)) & 1;  // BinaryRow.isNullAt
+        x[u] = get_slot<W, FRAME>(row, hdr_bm, slot);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = field_of<TR>(pb, u, FSTEP, fsub);
+      if (p < g1) {
+        const FixedFieldDev& fd = fields[p];
+        uint64_t v = nul[u] ? 0 : x[u];
+        if (fd.flags & 2) v = (v & 0xff) ? 1 : 0;
+        if (live) stw<W>(fd.out_values, grow, v);
+        if ((fd.flags & 1) && fd.out_validity) put_validity<TR>(fd, nul[u], live, r, fsub, r0, rows);
+      }
+    }
+  }
+}
+
+template <int TR, bool FRAME>
+__global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
+                                                           const uint8_t* __restrict__ in, int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int HDR = FRAME ? 12 : 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -169,67 +399,91 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
   const int64_t left = L.num_rows - r0;
   const int rows = left < TR ? (int)left : TR;
   const int stride = L.stride;
-  const int nf = L.num_fields;
-  const int bm = L.bitmap_bytes;
+  const int hdr_bm = HDR + L.bitmap_bytes;
 
-  // Phase 1: tile image HBM -> LDS by LDS-DMA (1 KiB per wave-instruction,
-  // lane-linear destination = the contiguous tile image).
-  const int64_t bytes = (int64_t)rows * stride;
-  const uint8_t* src = in + r0 * stride;
-  const int n16 = (int)(bytes >> 4);
-  const int nfull = n16 & ~(kWG - 1);
-  for (int c0 = 0; c0 < nfull; c0 += kWG) {
-    const int c = c0 + tid;
-    __builtin_amdgcn_global_load_lds(
-        (const __attribute__((address_space(1))) void*)(src + (int64_t)c * 16),
-        (__attribute__((address_space(3))) void*)(lds + (c0 + wave * 64) * 16), 16, 0, 0);
-  }
-  for (int c = nfull + tid; c < n16; c += kWG)
-    *reinterpret_cast<uint4*>(lds + c * 16) = *reinterpret_cast<const uint4*>(src + (int64_t)c * 16);
-  const int tail4 = (int)(bytes & 15) >> 2;
-  if (tid < tail4) st32(lds + n16 * 16 + tid * 4, ld32(src + n16 * 16 + tid * 4));
+  dma_tile(lds, in + r0 * stride, rows * stride, tid, wave);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const uint8_t* row = lds + r * stride;
   const int64_t grow = r0 + r;
   const bool live = r < rows;
+  if (FRAME && wave == 0 && fsub == 0 && live) check_frame<FRAME>(row, L, status);
+  dec_group<8, TR, FRAME>(fields, L.group[0], L.group[1], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<4, TR, FRAME>(fields, L.group[1], L.group[2], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<2, TR, FRAME>(fields, L.group[2], L.group[3], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<1, TR, FRAME>(fields, L.group[3], L.group[4], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+}
 
-  if (FRAME && wave == 0 && fsub == 0 && live) {
-    // Encoders.decode (Encoders.java:177-190): size, then schema hash check.
-    const uint32_t len = ld32(row);
-    const uint64_t h = (uint64_t)ld32(row + 4) | ((uint64_t)ld32(row + 8) << 32);
-    if (h != (uint64_t)L.schema_hash) set_status(status, FORY_ERR_SCHEMA_MISMATCH);
-    else if (len != (uint32_t)(8 + L.fixed_size)) set_status(status, FORY_ERR_CORRUPT);
+// Persistent, software-pipelined decode (TR = 64, tile image <= MAXC*4 KiB):
+// the next tile streams HBM -> VGPRs while this tile's columns are stored,
+// then VGPRs -> LDS (async-stage split).
+template <int MAXC>
+__device__ __forceinline__ void stage_issue(u32x4 (&buf)[MAXC], uint32_t& tail, const uint8_t* __restrict__ src,
+                                            int bytes, int tid) {
+  const int n16 = bytes >> 4;
+  const int last = n16 > 0 ? n16 - 1 : 0;  // lanes past the end re-read the last chunk (no divergence)
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int c = min(k * kWG + tid, last);
+    buf[k] = *reinterpret_cast<const u32x4*>(src + (int64_t)c * 16);
   }
+  if (tid < ((bytes & 15) >> 2)) tail = ld32(src + n16 * 16 + tid * 4);
+}
 
-  // Phase 2: per field, lane = record: slot from LDS -> coalesced column store.
-  for (int fb = wave * FPW; fb < nf; fb += FSTEP) {
-    const int f = fb + fsub;
-    if (f >= nf) continue;
-    const FixedFieldDev fd = L.fields[f];
-    const uint32_t bw = ld32(row + HDR + ((f >> 5) << 2));
-    const bool isnull = (bw >> (f & 31)) & 1;  // BinaryRow.isNullAt
-    const uint8_t* slot = row + HDR + bm + 8 * f;
-    uint64_t x;
-    if (FRAME || fd.width < 8) {
-      x = ld32(slot);
-      if (fd.width == 8) x |= (uint64_t)ld32(slot + 4) << 32;
-    } else {
-      x = *reinterpret_cast<const uint64_t*>(slot);
-    }
-    if (isnull) x = 0;                         // Java default for a null field
-    if (fd.flags & 2) x = (x & 0xff) ? 1 : 0;  // getBoolean: byte != 0
-    if (live) store_elem(fd.out_values, fd.width, grow, x);
-    if ((fd.flags & 1) && fd.out_validity) {
-      const uint64_t m = __ballot(!isnull && live);
-      if (r == 0) {
-        const uint64_t mine = (m >> (fsub * TR)) & (TR == 64 ? ~0ull : ((1ull << TR) - 1));
-        uint8_t* vb = fd.out_validity + (r0 >> 3);
-        const int nb = (rows + 7) >> 3;
-        for (int b = 0; b < nb; ++b) vb[b] = (uint8_t)(mine >> (8 * b));
-      }
-    }
+template <int MAXC>
+__device__ __forceinline__ void stage_commit(const u32x4 (&buf)[MAXC], uint32_t tail, uint8_t* lds, int bytes,
+                                             int tid) {
+  const int n16 = bytes >> 4;
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int c = k * kWG + tid;
+    if (c < n16) *reinterpret_cast<u32x4*>(lds + c * 16) = buf[k];
+  }
+  if (tid < ((bytes & 15) >> 2)) st32(lds + n16 * 16 + tid * 4, tail);
+}
+
+template <bool FRAME, int MAXC>
+__global__ __launch_bounds__(kWG, 2) void decode_fixed_pipe_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
+                                                                const uint8_t* __restrict__ in, int32_t* status,
+                                                                int64_t tiles) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int HDR = FRAME ? 12 : 0;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int stride = L.stride;
+  const int hdr_bm = HDR + L.bitmap_bytes;
+  int64_t t = blockIdx.x;
+  if (t >= tiles) return;
+
+  u32x4 buf[MAXC];
+  uint32_t tail = 0;
+  auto rows_of = [&](int64_t tile) {
+    const int64_t left = L.num_rows - tile * 64;
+    return left < 64 ? (int)left : 64;
+  };
+  stage_issue<MAXC>(buf, tail, in + t * 64 * stride, rows_of(t) * stride, tid);
+  stage_commit<MAXC>(buf, tail, lds, rows_of(t) * stride, tid);
+  __syncthreads();
+  const uint8_t* row = lds + lane * stride;
+  for (;;) {
+    const int64_t tn = t + gridDim.x;
+    if (tn < tiles) stage_issue<MAXC>(buf, tail, in + tn * 64 * stride, rows_of(tn) * stride, tid);
+    const int64_t r0 = t * 64;
+    const int rows = rows_of(t);
+    const bool live = lane < rows;
+    const int64_t grow = r0 + lane;
+    if (FRAME && wave == 0 && live) check_frame<FRAME>(row, L, status);
+    dec_group<8, 64, FRAME>(fields, L.group[0], L.group[1], wave, 0, lane, row, hdr_bm, HDR, live, grow, r0, rows);
+    dec_group<4, 64, FRAME>(fields, L.group[1], L.group[2], wave, 0, lane, row, hdr_bm, HDR, live, grow, r0, rows);
+    dec_group<2, 64, FRAME>(fields, L.group[2], L.group[3], wave, 0, lane, row, hdr_bm, HDR, live, grow, r0, rows);
+    dec_group<1, 64, FRAME>(fields, L.group[3], L.group[4], wave, 0, lane, row, hdr_bm, HDR, live, grow, r0, rows);
+    __syncthreads();
+    if (tn >= tiles) break;
+    stage_commit<MAXC>(buf, tail, lds, rows_of(tn) * stride, tid);
+    __syncthreads();
+    t = tn;
   }
 }
 
@@ -684,17 +938,59 @@ __global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const uint
   }
 }
 
+template <typename K>
+void raise_lds_cap(K* kernel) {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+}
+
+int num_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+    if (cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+// Persistent grid: resident workgroups per CU (occupancy query) x CUs.
+template <typename K>
+int64_t persistent_grid(K* kernel, size_t lds, int64_t tiles) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kWG, lds) != hipSuccess || per_cu <= 0)
+    per_cu = 1;
+  const int64_t g = (int64_t)per_cu * num_cus();
+  return tiles < g ? tiles : g;
+}
+
+int variant() {  // FORY_ROWFMT_PIPE=0 selects the one-tile-per-workgroup kernels (A/B)
+  const char* e = getenv("FORY_ROWFMT_PIPE");
+  return e ? atoi(e) : 1;
+}
+
 template <int TR, bool FRAME>
 hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const int64_t tiles = (L.num_rows + TR - 1) / TR;
   const size_t lds = (size_t)TR * L.stride;
-  static bool init = false;  // raise the dynamic-LDS cap once (160 KiB per CU)
-  if (!init) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_fixed_kernel<TR, FRAME>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    init = true;
+  if constexpr (TR == 64) {
+    const int n8 = L.group[1] - L.group[0], n4 = L.group[2] - L.group[1];
+    const int n2 = L.group[3] - L.group[2], n1 = L.group[4] - L.group[3];
+    if (n8 <= 4 * kM8 && n4 <= 4 * kM4 && n2 <= 4 * kM2 && n1 <= 4 * kM1 && variant() == 1) {
+      auto* k = &encode_fixed_pipe_kernel<FRAME>;
+      static bool init = false;
+      if (!init) { raise_lds_cap(k); init = true; }
+      const int64_t grid = persistent_grid(k, lds, tiles);
+      hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kWG), lds, s, L, L.fields, out, tiles);
+      return hipGetLastError();
+    }
   }
-  hipLaunchKernelGGL((encode_fixed_kernel<TR, FRAME>), dim3((unsigned)tiles), dim3(kWG), lds, s, L, out);
+  auto* k = &encode_fixed_kernel<TR, FRAME>;
+  static bool init = false;
+  if (!init) { raise_lds_cap(k); init = true; }
+  hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(kWG), lds, s, L, L.fields, out);
   return hipGetLastError();
 }
 
@@ -702,14 +998,21 @@ template <int TR, bool FRAME>
 hipError_t launch_decode_tr(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
   const int64_t tiles = (L.num_rows + TR - 1) / TR;
   const size_t lds = (size_t)TR * L.stride;
-  static bool init = false;
-  if (!init) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_fixed_kernel<TR, FRAME>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    init = true;
+  if constexpr (TR == 64) {
+    constexpr int MAXC = 14;
+    if (lds <= (size_t)MAXC * kWG * 16 && variant() == 1) {
+      auto* k = &decode_fixed_pipe_kernel<FRAME, MAXC>;
+      static bool init = false;
+      if (!init) { raise_lds_cap(k); init = true; }
+      const int64_t grid = persistent_grid(k, lds, tiles);
+      hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kWG), lds, s, L, L.fields, in, status, tiles);
+      return hipGetLastError();
+    }
   }
-  hipLaunchKernelGGL((decode_fixed_kernel<TR, FRAME>), dim3((unsigned)tiles), dim3(kWG), lds, s, L, in,
-                     status);
+  auto* k = &decode_fixed_kernel<TR, FRAME>;
+  static bool init = false;
+  if (!init) { raise_lds_cap(k); init = true; }
+  hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(kWG), lds, s, L, L.fields, in, status);
   return hipGetLastError();
 }
 

@@ -38,7 +38,11 @@ struct FixedFieldDev {
   uint8_t* out_validity;    // decode target
   int32_t width;            // 1,2,4,8
   int32_t flags;            // bit0 nullable, bit1 bool
+  int32_t slot;             // schema ordinal (slot index in the row)
+  int32_t pad;
 };
+// The device table is sorted into width groups [8-byte][4-byte][2-byte][1-byte]
+// (stable within a group) so every load loop has a compile-time width.
 
 // Op program for varlen plans: executed per record by one lane.
 enum OpCode : int32_t {

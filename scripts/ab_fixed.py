@@ -1,0 +1,56 @@
+"""A/B of the fixed-width kernel variants (FORY_ROWFMT_PIPE=1 persistent pipelined vs 0
+one-tile-per-workgroup) in ONE process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
+Usage: python scripts/ab_fixed.py [rows] [rounds]"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from fury_amd import workloads as W  # noqa: E402
+from fury_amd.format import native  # noqa: E402
+from fury_amd.format.encoder import RowEncoder  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 64 * 1024 * 1024
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+iters = 5
+vals = W.gen_struct_device(n)
+cols = [native.DeviceColumn(v, None, None, n) for v in vals]
+enc = RowEncoder(W.struct_schema())
+plan = enc.plan
+ws = enc.workspace(n)
+arr = native.column_array(cols)
+status = torch.zeros(1, dtype=torch.int32, device="cuda")
+res = {}
+for frame in (0, 1):
+    out = torch.empty(n * plan.stride(frame), dtype=torch.uint8, device="cuda")
+    dcols = enc.alloc_fixed_outputs(n)
+    darr = native.column_array(dcols)
+    for rnd in range(rounds):
+        for var in ("1", "0"):
+            os.environ["FORY_ROWFMT_PIPE"] = var
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            native.encode(plan, arr, n, frame, None, out, status, ws)
+            native.decode(plan, out, None, n, frame, darr, status, ws)
+            te, td = [], []
+            for _ in range(iters):
+                ev[0].record()
+                native.encode(plan, arr, n, frame, None, out, status, ws)
+                ev[1].record()
+                native.decode(plan, out, None, n, frame, darr, status, ws)
+                ev[2].record()
+                torch.cuda.synchronize()
+                te.append(ev[0].elapsed_time(ev[1]))
+                td.append(ev[1].elapsed_time(ev[2]))
+            ok = all(torch.equal(a.values.view(torch.uint8), b.values.view(torch.uint8)) for a, b in zip(dcols, cols))
+            native.read_status(status)
+            key = f"frame{frame}_pipe{var}"
+            algo = n * (624 + plan.stride(frame))
+            r = res.setdefault(key, {"enc_ms": [], "dec_ms": [], "ok": True})
+            r["enc_ms"].append(round(min(te), 3))
+            r["dec_ms"].append(round(min(td), 3))
+            r["ok"] &= ok
+            r["enc_GBs"] = round(algo / (min(r["enc_ms"]) * 1e-3) / 1e9, 1)
+            r["dec_GBs"] = round(algo / (min(r["dec_ms"]) * 1e-3) / 1e9, 1)
+print(json.dumps(res, indent=1))

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Iteration run: GPU parity tests, then the in-process A/B of kernel variants, then bench.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest exit $rc" >> gpurun_out/pytest_gpu.log; tail -4 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python scripts/ab_fixed.py > gpurun_out/ab.json 2> gpurun_out/ab.err
+rc=$?; echo "ab exit $rc"; cat gpurun_out/ab.json; tail -3 gpurun_out/ab.err
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench.py --steps 10 --warmup 3 --cpu-seconds 8 > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc=$?; echo "bench exit $rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err
+exit $rc

@@ -35,10 +35,19 @@ def encoder_for(name):
     return _ENC[name]
 
 
+@pytest.fixture(params=["1", "0"], ids=["pipe", "tile"])
+def kernel_variant(request, monkeypatch):
+    """Fixed-width kernels: persistent pipelined (1) and one-tile-per-workgroup (0)."""
+    monkeypatch.setenv("FORY_ROWFMT_PIPE", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("frame", [0, 1])
 @pytest.mark.parametrize("n", SIZES)
 @pytest.mark.parametrize("name", list(catalog().keys()))
-def test_encode_decode_parity(name, n, frame):
+def test_encode_decode_parity(name, n, frame, kernel_variant):
+    if kernel_variant == "0" and name.startswith(("mixed", "nested", "strings")):
+        pytest.skip("the variant switch only affects fixed-width schemas")
     schema, make = catalog()[name]
     cols = make(n, n)
     expect, offs = oracle.encode(schema, cols, n, frame)
@@ -114,7 +123,7 @@ def test_capacity_errors():
         native.read_status(status)
 
 
-def test_struct_large_round_trip_and_sampled_parity():
+def test_struct_large_round_trip_and_sampled_parity(kernel_variant):
     """S at 2M rows: device-generated java.util.Random values, round trip exact,
     and 4 sampled tiles compared byte-for-byte with the oracle."""
     n = 2 * 1024 * 1024 + 3
@@ -144,11 +153,5 @@ def test_mixed_and_nested_large_round_trip():
         rows = enc.encode(to_device(cols), n, 1)
         dec = to_host(enc.decode(rows))
         assert columns_equal(schema, cols, dec) == []
-        # sampled parity: first 2000 rows against the oracle
-        k = 2000
-        sub = make(n, 5)
         expect, offs = oracle.encode(schema, cols, n, 1)
-        got = rows.buffer.cpu().numpy()
-        assert np.array_equal(got[: offs[k]], expect[: offs[k]])
-        assert np.array_equal(got, expect)
-        del sub
+        assert np.array_equal(rows.buffer.cpu().numpy(), expect)
