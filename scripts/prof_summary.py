@@ -1,0 +1,48 @@
+"""Summarise a scripts/profile.sh run: per-kernel avg duration (kernel trace) and
+per-launch counter values (PMC passes). HBM bytes follow MI355X_MICROARCH.md §HBM:
+FETCH_SIZE/WRITE_SIZE are in KB; gfx950 FETCH_SIZE reads 1/2 of a 16-B/lane
+streaming read (x2 applied as 'fetch_bytes_x2'; other widths uncalibrated)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+root = sys.argv[1]
+
+
+def rows(pattern):
+    for f in glob.glob(os.path.join(root, pattern), recursive=True):
+        with open(f) as fh:
+            yield from csv.DictReader(fh)
+
+
+def short(name):
+    for k in ("encode_fixed_pipe", "decode_fixed_pipe", "encode_fixed_kernel", "decode_fixed_kernel",
+              "var_encode", "var_decode_kernelILb0", "var_decode_kernelILb1", "var_sizes", "scan_", "fill_offsets"):
+        if k in name:
+            return k + ("<frame>" if "ILb1E" in name and "fixed" in k else "")
+    return name[:60]
+
+
+out = {"kernels": {}, "pmc": {}}
+stats = list(rows("trace/**/*kernel_stats.csv"))
+for r in stats:
+    out["kernels"][short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                        "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
+acc = defaultdict(lambda: defaultdict(list))
+for d in glob.glob(os.path.join(root, "pmc_*")):
+    if not os.path.isdir(d):
+        continue
+    for r in rows(os.path.relpath(d, root) + "/**/*counter_collection.csv"):
+        acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, cs in acc.items():
+    e = {c: sum(v) / len(v) for c, v in cs.items()}
+    if "FETCH_SIZE" in e:
+        e["fetch_bytes"] = e["FETCH_SIZE"] * 1024
+        e["fetch_bytes_x2"] = e["FETCH_SIZE"] * 2048
+    if "WRITE_SIZE" in e:
+        e["write_bytes"] = e["WRITE_SIZE"] * 1024
+    out["pmc"][k] = e
+print(json.dumps(out, indent=1))
