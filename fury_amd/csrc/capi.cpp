@@ -45,7 +45,8 @@ constexpr int64_t kAlign = 256;
 int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
 int64_t table_bytes(const Plan& p) {
-  if (p.fixed_width) return align_up((int64_t)p.top.size() * (int64_t)sizeof(FixedFieldDev));
+  // fixed-width: width-ordered table + slab-ordered copy (encode v4)
+  if (p.fixed_width) return align_up(2 * (int64_t)p.top.size() * (int64_t)sizeof(FixedFieldDev));
   return align_up((int64_t)p.nodes.size() * (int64_t)sizeof(ColumnDev)) +
          align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::Op));
 }
@@ -150,6 +151,44 @@ fory_amd::FixedLaunch fixed_launch(const Plan& p, const void* table, int64_t n, 
   }
   L.group[4] = at;
   return L;
+}
+
+// Column slabs of encode v4 (kernels.hip): rows cut into S 16-byte-aligned
+// byte ranges of <= ~448 bytes; the field table reordered by (slab, width).
+void build_slabs(const Plan& p, const std::vector<FixedFieldDev>& tab, int frame, fory_amd::FixedLaunch* L,
+                 std::vector<FixedFieldDev>* stab) {
+  L->num_slabs = 0;
+  L->slab_fields = nullptr;
+  if (frame || p.any_nullable || (p.fixed_size & 15) || p.top.empty()) return;
+  const int chunks = p.fixed_size / 16;
+  int S = (p.fixed_size + 447) / 448;
+  if (S < 2 || S > 4) return;
+  const int cps = (chunks + S - 1) / S;
+  S = (chunks + cps - 1) / cps;
+  auto slab_of = [&](const FixedFieldDev& f) { return ((p.bitmap_bytes + 8 * f.slot) / 16) / cps; };
+  *stab = tab;
+  std::stable_sort(stab->begin(), stab->end(), [&](const FixedFieldDev& a, const FixedFieldDev& b) {
+    return slab_of(a) < slab_of(b);
+  });
+  const int widths[4] = {8, 4, 2, 1};
+  int at = 0;
+  int pitch = 0;
+  for (int sl = 0; sl < S; ++sl) {
+    fory_amd::FixedLaunch::Slab& d = L->slab[sl];
+    for (int g = 0; g < 4; ++g) {
+      d.group[g] = at;
+      for (const FixedFieldDev& f : *stab)
+        if (slab_of(f) == sl && f.width == widths[g]) ++at;
+    }
+    d.group[4] = at;
+    d.byte0 = sl * cps * 16;
+    const int c1 = std::min(chunks, (sl + 1) * cps);
+    d.nbytes = (c1 - sl * cps) * 16;
+    d.cpr_magic = 0xffffffffu / (uint32_t)(d.nbytes / 16);
+    pitch = std::max(pitch, d.nbytes);
+  }
+  L->num_slabs = S;
+  L->slab_pitch = pitch;
 }
 
 // Var launch: columns table then program in the workspace.
@@ -271,13 +310,17 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
                                          std::to_string(num_rows * stride) + " bytes");
     if (reinterpret_cast<uintptr_t>(d_out) & 15)
       return fail(FORY_ERR_INVALID_ARGUMENT, "d_out must be 16-byte aligned");
-    std::vector<FixedFieldDev> tab;
+    std::vector<FixedFieldDev> tab, stab;
     rc = bind_fixed(p, cols, num_rows, false, &tab);
     if (rc) return rc;
-    rc = upload(d_workspace, tab.data(), (int64_t)(tab.size() * sizeof(FixedFieldDev)), s);
+    fory_amd::FixedLaunch L = fixed_launch(p, d_workspace, num_rows, frame_mode);
+    build_slabs(p, tab, frame_mode, &L, &stab);
+    std::vector<FixedFieldDev> both(tab);
+    both.insert(both.end(), stab.begin(), stab.end());
+    rc = upload(d_workspace, both.data(), (int64_t)(both.size() * sizeof(FixedFieldDev)), s);
     if (rc) return rc;
-    e = fory_amd::launch_encode_fixed(fixed_launch(p, d_workspace, num_rows, frame_mode),
-                                      static_cast<uint8_t*>(d_out), s);
+    if (L.num_slabs) L.slab_fields = static_cast<const FixedFieldDev*>(d_workspace) + tab.size();
+    e = fory_amd::launch_encode_fixed(L, static_cast<uint8_t*>(d_out), s);
     return e == hipSuccess ? FORY_OK : hip_fail(e, "encode_fixed");
   }
   if (p.fixed_width)

@@ -200,7 +200,7 @@ __global__ __launch_bounds__(kWG) void encode_fixed_kernel(FixedLaunch L, const 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane % TR;
   const int fsub = lane / TR;
-  const int64_t r0 = (int64_t)blockIdx.x * TR;
+  const int64_t r0 = (L.tile0 + (int64_t)blockIdx.x) * TR;
   const int64_t left = L.num_rows - r0;
   const int rows = left < TR ? (int)left : TR;
   const int hdr_bm = HDR + L.bitmap_bytes;
@@ -292,6 +292,463 @@ __global__ __launch_bounds__(kWG, 2) void encode_fixed_pipe_kernel(FixedLaunch L
     }
     store_tile(lds, out + r0 * stride, rows * stride, tid);
     __syncthreads();
+    if (tn >= tiles) break;
+    t = tn;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Encode v3: 16-byte column chunks per lane (R records per tile, 4R threads)
+// ---------------------------------------------------------------------------
+// Column reads are the encode's limiter: 4/8-byte loads of 256-byte column
+// segments reach ~1.6 TB/s at two workgroups per CU, while 16-byte loads of
+// >= 512-byte segments reach ~5.9 TB/s (scripts/microbench/colread.hip).
+// So each lane loads one 16-byte chunk of ONE field's column segment
+// (E = 16/w consecutive records) and scatters its E values into the LDS row
+// image. A field of width w spans CPF = R*w/16 chunks per tile; one wave
+// instruction (64 x 16 B) covers FPI = 64/CPF fields. Instructions are
+// numbered per width group (8, 4, 2, 1 bytes); wave v issues v, v+NW, ....
+// Persistent + software-pipelined: tile t+1's chunks are in flight while
+// tile t's rows are stored. Only full tiles; the tail goes to encode_fixed_kernel.
+template <int R>
+__device__ __forceinline__ bool v3_insn_g(int i, const int32_t* group, int* w, int* p0, int* pend) {
+  const int fpi8 = 1024 / (R * 8), fpi4 = 1024 / (R * 4), fpi2 = 1024 / (R * 2), fpi1 = 1024 / R;
+  const int n8 = group[1] - group[0], n4 = group[2] - group[1];
+  const int n2 = group[3] - group[2], n1 = group[4] - group[3];
+  const int i8 = (n8 + fpi8 - 1) / fpi8, i4 = (n4 + fpi4 - 1) / fpi4;
+  const int i2 = (n2 + fpi2 - 1) / fpi2, i1 = (n1 + fpi1 - 1) / fpi1;
+  if (i < i8) { *w = 8; *p0 = group[0] + i * fpi8; *pend = group[1]; return true; }
+  i -= i8;
+  if (i < i4) { *w = 4; *p0 = group[1] + i * fpi4; *pend = group[2]; return true; }
+  i -= i4;
+  if (i < i2) { *w = 2; *p0 = group[2] + i * fpi2; *pend = group[3]; return true; }
+  i -= i2;
+  if (i < i1) { *w = 1; *p0 = group[3] + i * fpi1; *pend = group[4]; return true; }
+  return false;
+}
+
+template <int R>
+__device__ __forceinline__ bool v3_insn(int i, const FixedLaunch& L, int* w, int* p0, int* pend) {
+  return v3_insn_g<R>(i, L.group, w, p0, pend);
+}
+
+template <int R>
+__host__ __device__ inline int v3_insn_count(const int* group) {
+  const int fpi8 = 1024 / (R * 8), fpi4 = 1024 / (R * 4), fpi2 = 1024 / (R * 2), fpi1 = 1024 / R;
+  const int n8 = group[1] - group[0], n4 = group[2] - group[1];
+  const int n2 = group[3] - group[2], n1 = group[4] - group[3];
+  return (n8 + fpi8 - 1) / fpi8 + (n4 + fpi4 - 1) / fpi4 + (n2 + fpi2 - 1) / fpi2 + (n1 + fpi1 - 1) / fpi1;
+}
+
+constexpr int kV3K = 12;  // instructions per wave per tile
+
+template <int R, bool FRAME, bool NULLS, bool PAD>
+__global__ __launch_bounds__(4 * R, 1) void encode_fixed_v3_kernel(FixedLaunch L,
+                                                                    const FixedFieldDev* __restrict__ fields,
+                                                                    uint8_t* __restrict__ out, int64_t tiles) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int WG = 4 * R;
+  constexpr int NW = WG / 64;
+  constexpr int HDR = FRAME ? 12 : 0;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int stride = L.stride;
+  // LDS row pitch: PAD (raw rows) spaces rows by pitch = 4 mod 32 bytes so the
+  // 16 lanes of a ds_write_b64 group (records 2c / 4c of one field) spread
+  // over the banks; the store phase then re-packs rows with 4-byte reads.
+  const int pitch = PAD ? L.pitch : stride;
+  const int hdr_bm = HDR + L.bitmap_bytes;
+  int64_t t = blockIdx.x;
+  if (t >= tiles) return;
+
+  // per-lane descriptors, loop-invariant across tiles
+  const uint8_t* ptr[kV3K];
+  const uint8_t* vptr[kV3K];
+  uint32_t sf[kV3K];  // slot | flags << 16 | active << 20 | rb << 21 (rb = first record of the chunk)
+#pragma unroll
+  for (int k = 0; k < kV3K; ++k) {
+    int w = 8, p0 = 0, pend = 0;
+    const bool ok = v3_insn<R>(wave + k * NW, L, &w, &p0, &pend);
+    const int cpf = R * w / 16;
+    const int p = p0 + lane / cpf, c = lane % cpf;
+    ptr[k] = nullptr;
+    vptr[k] = nullptr;
+    sf[k] = 0;
+    if (ok && p < pend) {
+      const FixedFieldDev& fd = fields[p];
+      ptr[k] = fd.values + c * 16;
+      if (NULLS) vptr[k] = (fd.flags & 1) ? fd.validity : nullptr;
+      sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (1u << 20) | ((uint32_t)(c * (16 / w)) << 21);
+    }
+  }
+  u32x4 d[kV3K];
+  uint32_t vb[kV3K];
+  auto issue = [&](int64_t tile) {
+    const int64_t r0 = tile * R;
+#pragma unroll
+    for (int k = 0; k < kV3K; ++k) {
+      int w = 8, p0, pend;
+      if (!v3_insn<R>(wave + k * NW, L, &w, &p0, &pend)) continue;  // uniform
+      if (sf[k] & (1u << 20)) {
+        d[k] = *gp(reinterpret_cast<const u32x4*>(ptr[k] + r0 * w));
+        if (NULLS) {
+          vb[k] = 0xffffffffu;
+          if (vptr[k]) {
+            const int64_t rec = r0 + (sf[k] >> 21);
+            vb[k] = w == 1 ? *gp(reinterpret_cast<const uint16_t*>(vptr[k] + (rec >> 3)))
+                           : (uint32_t)load_byte(vptr[k] + (rec >> 3)) >> (rec & 7);
+          }
+        }
+      }
+    }
+  };
+
+  issue(t);
+  if (tid < R) put_header<FRAME>(lds + tid * pitch, L);  // constant across tiles
+  for (;;) {
+    if (NULLS) {
+      if (tid < R) put_header<FRAME>(lds + tid * pitch, L);  // re-zero the bitmaps
+      __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < kV3K; ++k) {
+      int w = 8, p0, pend;
+      if (!v3_insn<R>(wave + k * NW, L, &w, &p0, &pend)) continue;
+      if (!(sf[k] & (1u << 20))) continue;
+      const int slot = sf[k] & 0xffff, flags = (sf[k] >> 16) & 0xf, rb = sf[k] >> 21;
+      uint8_t* row = lds + rb * pitch;
+      const uint32_t nb = NULLS ? ~vb[k] : 0u;  // 1 = null
+      const u32x4 x = d[k];
+      if (w == 8) {
+        put_slot<FRAME>(row, hdr_bm, slot, (uint64_t)x.x | ((uint64_t)x.y << 32), nb & 1, flags);
+        put_slot<FRAME>(row + pitch, hdr_bm, slot, (uint64_t)x.z | ((uint64_t)x.w << 32), (nb >> 1) & 1, flags);
+      } else if (w == 4) {
+        put_slot<FRAME>(row, hdr_bm, slot, x.x, nb & 1, flags);
+        put_slot<FRAME>(row + pitch, hdr_bm, slot, x.y, (nb >> 1) & 1, flags);
+        put_slot<FRAME>(row + 2 * pitch, hdr_bm, slot, x.z, (nb >> 2) & 1, flags);
+        put_slot<FRAME>(row + 3 * pitch, hdr_bm, slot, x.w, (nb >> 3) & 1, flags);
+      } else if (w == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          put_slot<FRAME>(row + e * pitch, hdr_bm, slot, (x[e >> 1] >> (16 * (e & 1))) & 0xffff, (nb >> e) & 1, flags);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          put_slot<FRAME>(row + e * pitch, hdr_bm, slot, (x[e >> 2] >> (8 * (e & 3))) & 0xff, (nb >> e) & 1, flags);
+      }
+    }
+    __syncthreads();
+    const int64_t tn = t + gridDim.x;
+    if (tn < tiles) issue(tn);  // next tile's column chunks go out before this tile's rows
+    {
+      uint8_t* dst = out + t * R * stride;
+      const int bytes = R * stride;
+      const int n16 = bytes >> 4;
+      int c = tid;
+      if constexpr (PAD) {
+        // tile byte o -> LDS (o / stride) * pitch + o % stride, 4 bytes at a time
+        for (; c < n16; c += WG) {
+          u32x4 y;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t o = (uint32_t)(c * 16 + 4 * i);
+            uint32_t j = __umulhi(o, L.stride_magic);
+            uint32_t r = o - j * (uint32_t)stride;
+            if (r >= (uint32_t)stride) { ++j; r -= stride; }
+            y[i] = ld32(lds + j * pitch + r);
+          }
+          *reinterpret_cast<u32x4*>(dst + c * 16) = y;
+        }
+      }
+      for (; c + 3 * WG < n16; c += 4 * WG) {
+        const u32x4 y0 = *reinterpret_cast<const u32x4*>(lds + c * 16);
+        const u32x4 y1 = *reinterpret_cast<const u32x4*>(lds + (c + WG) * 16);
+        const u32x4 y2 = *reinterpret_cast<const u32x4*>(lds + (c + 2 * WG) * 16);
+        const u32x4 y3 = *reinterpret_cast<const u32x4*>(lds + (c + 3 * WG) * 16);
+        *reinterpret_cast<u32x4*>(dst + c * 16) = y0;
+        *reinterpret_cast<u32x4*>(dst + (c + WG) * 16) = y1;
+        *reinterpret_cast<u32x4*>(dst + (c + 2 * WG) * 16) = y2;
+        *reinterpret_cast<u32x4*>(dst + (c + 3 * WG) * 16) = y3;
+      }
+      for (; c < n16; c += WG) *reinterpret_cast<u32x4*>(dst + c * 16) = *reinterpret_cast<const u32x4*>(lds + c * 16);
+      const int tail4 = (bytes & 15) >> 2;
+      if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
+    }
+    __syncthreads();
+    if (tn >= tiles) break;
+    t = tn;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Encode v5: v3 with a depth-2 load pipeline
+// ---------------------------------------------------------------------------
+// Two tiles of column chunks are in flight per workgroup (register sets A/B,
+// the loop unrolled by 2 so both stay static). Every lane issues exactly K
+// loads per tile (inactive lanes / absent instructions re-read a valid dummy
+// address), so hipcc can wait with a counted vmcnt for the older set while
+// the younger set stays in flight. Order per stage: write X -> barrier ->
+// store this tile's rows -> issue X for tile + 2*grid -> barrier.
+template <int R, int K>
+__device__ __forceinline__ void v5_issue(const uint8_t* const (&ptr)[K], const int (&wk)[K], int64_t r0,
+                                         u32x4 (&d)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) d[k] = *gp(reinterpret_cast<const u32x4*>(ptr[k] + r0 * wk[k]));
+}
+
+template <int R, int K, bool FRAME, bool PAD>
+__device__ __forceinline__ void v5_write(uint8_t* lds, int pitch, int hdr_bm, const int (&wk)[K],
+                                         const uint32_t (&sf)[K], const u32x4 (&d)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int w = wk[k];
+    if (!(sf[k] & (1u << 20))) continue;
+    const int slot = sf[k] & 0xffff, flags = (sf[k] >> 16) & 0xf, rb = sf[k] >> 21;
+    uint8_t* row = lds + rb * pitch;
+    const u32x4 x = d[k];
+    if (w == 8) {
+      put_slot<FRAME>(row, hdr_bm, slot, (uint64_t)x.x | ((uint64_t)x.y << 32), false, flags);
+      put_slot<FRAME>(row + pitch, hdr_bm, slot, (uint64_t)x.z | ((uint64_t)x.w << 32), false, flags);
+    } else if (w == 4) {
+      put_slot<FRAME>(row, hdr_bm, slot, x.x, false, flags);
+      put_slot<FRAME>(row + pitch, hdr_bm, slot, x.y, false, flags);
+      put_slot<FRAME>(row + 2 * pitch, hdr_bm, slot, x.z, false, flags);
+      put_slot<FRAME>(row + 3 * pitch, hdr_bm, slot, x.w, false, flags);
+    } else if (w == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        put_slot<FRAME>(row + e * pitch, hdr_bm, slot, (x[e >> 1] >> (16 * (e & 1))) & 0xffff, false, flags);
+    } else if (w == 1) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        put_slot<FRAME>(row + e * pitch, hdr_bm, slot, (x[e >> 2] >> (8 * (e & 3))) & 0xff, false, flags);
+    }
+  }
+}
+
+template <int R, bool PAD>
+__device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* lds, int pitch, uint8_t* dst, int tid) {
+  constexpr int WG = 4 * R;
+  const int stride = L.stride;
+  const int bytes = R * stride;
+  const int n16 = bytes >> 4;
+  int c = tid;
+  if constexpr (PAD) {
+    for (; c < n16; c += WG) {
+      u32x4 y;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t o = (uint32_t)(c * 16 + 4 * i);
+        uint32_t j = __umulhi(o, L.stride_magic);
+        uint32_t r = o - j * (uint32_t)stride;
+        if (r >= (uint32_t)stride) { ++j; r -= stride; }
+        y[i] = ld32(lds + j * pitch + r);
+      }
+      *gp(reinterpret_cast<u32x4*>(dst + c * 16)) = y;
+    }
+  } else {
+    for (; c < n16; c += WG)
+      *gp(reinterpret_cast<u32x4*>(dst + c * 16)) = *reinterpret_cast<const u32x4*>(lds + c * 16);
+    const int tail4 = (bytes & 15) >> 2;
+    if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
+  }
+}
+
+template <int R, int K, bool FRAME, bool PAD>
+__global__ __launch_bounds__(4 * R, 1) void encode_fixed_v5_kernel(FixedLaunch L,
+                                                                    const FixedFieldDev* __restrict__ fields,
+                                                                    uint8_t* __restrict__ out, int64_t tiles) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int NW = 4 * R / 64;
+  constexpr int HDR = FRAME ? 12 : 0;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int stride = L.stride;
+  const int pitch = PAD ? L.pitch : stride;
+  const int hdr_bm = HDR + L.bitmap_bytes;
+  int64_t t = blockIdx.x;
+  if (t >= tiles) return;
+
+  const uint8_t* dummy = fields[L.group[0]].values;  // any valid column (never null: num_rows > 0)
+  const uint8_t* ptr[K];
+  int wk[K];
+  uint32_t sf[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    int w = 0, p0 = 0, pend = 0;
+    const bool ok = v3_insn<R>(wave + k * NW, L, &w, &p0, &pend);
+    wk[k] = ok ? w : 0;
+    const int cpf = R * (ok ? w : 8) / 16;
+    const int p = p0 + lane / cpf, c = lane % cpf;
+    ptr[k] = dummy;
+    sf[k] = 0;
+    if (ok && p < pend) {
+      const FixedFieldDev& fd = fields[p];
+      ptr[k] = fd.values + c * 16;
+      sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (1u << 20) | ((uint32_t)(c * (16 / w)) << 21);
+    } else {
+      wk[k] = ok ? w : 0;
+    }
+  }
+  if (tid < R) put_header<FRAME>(lds + tid * pitch, L);  // constant across tiles (no nullable fields)
+  u32x4 dA[K], dB[K];
+  const int64_t last = tiles - 1;
+  v5_issue<R, K>(ptr, wk, t * R, dA);
+  v5_issue<R, K>(ptr, wk, min(t + (int64_t)gridDim.x, last) * R, dB);
+  for (;;) {
+    v5_write<R, K, FRAME, PAD>(lds, pitch, hdr_bm, wk, sf, dA);
+    __syncthreads();
+    v5_store<R, PAD>(L, lds, pitch, out + t * R * stride, tid);
+    v5_issue<R, K>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dA);
+    __syncthreads();
+    t += gridDim.x;
+    if (t >= tiles) break;
+    v5_write<R, K, FRAME, PAD>(lds, pitch, hdr_bm, wk, sf, dB);
+    __syncthreads();
+    v5_store<R, PAD>(L, lds, pitch, out + t * R * stride, tid);
+    v5_issue<R, K>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dB);
+    __syncthreads();
+    t += gridDim.x;
+    if (t >= tiles) break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Encode v4: v3's 16-byte column chunks, tiles split into column slabs
+// ---------------------------------------------------------------------------
+// v3's full-row LDS image (R * stride bytes) caps residency at 2 workgroups
+// per CU, and each workgroup alternates LDS-write / barrier / store phases, so
+// the CU idles on HBM between them. v4 cuts every row into S 16-byte-aligned
+// byte slabs (e.g. [0, 432) and [432, 848) of an 848-byte row) and runs one
+// (tile, slab) stage at a time through an R x slab_pitch image: LDS per
+// workgroup drops S-fold, 4-5 workgroups share a CU and hide each other's
+// phases. Stages are software-pipelined: stage k+1's column chunks are in
+// flight while stage k's slab is stored. A slab's rows leave as R runs of
+// nbytes (16-B stores); row lines split across slabs are completed in L2 by
+// the next stage of the same workgroup. Raw rows only (8-byte slots, rows a
+// multiple of 16 bytes), no nullable fields.
+constexpr int kV4K = 8;  // instructions per wave per slab
+
+template <int R, int S>
+__device__ __forceinline__ void v4_desc(const FixedLaunch& L, const FixedFieldDev* __restrict__ fields, int wave,
+                                        int lane, int s, const uint8_t* (&ptr)[kV4K], uint32_t (&sf)[kV4K]) {
+  constexpr int NW = 4 * R / 64;
+#pragma unroll
+  for (int k = 0; k < kV4K; ++k) {
+    int w = 8, p0 = 0, pend = 0;
+    const bool ok = v3_insn_g<R>(wave + k * NW, L.slab[s].group, &w, &p0, &pend);
+    const int cpf = R * w / 16;
+    const int p = p0 + lane / cpf, c = lane % cpf;
+    ptr[k] = nullptr;
+    sf[k] = 0;
+    if (ok && p < pend) {
+      const FixedFieldDev& fd = fields[p];
+      // byte of the slot inside the slab image row
+      const int sb = L.bitmap_bytes + 8 * fd.slot - L.slab[s].byte0;
+      ptr[k] = fd.values + c * 16;
+      sf[k] = (uint32_t)sb | ((uint32_t)fd.flags << 12) | (1u << 16) | ((uint32_t)(c * (16 / w)) << 17);
+    }
+  }
+}
+
+template <int R>
+__device__ __forceinline__ void v4_issue(const FixedLaunch& L, int s, int wave, int64_t r0,
+                                         const uint8_t* const (&ptr)[kV4K], const uint32_t (&sf)[kV4K],
+                                         u32x4 (&d)[kV4K]) {
+  constexpr int NW = 4 * R / 64;
+#pragma unroll
+  for (int k = 0; k < kV4K; ++k) {
+    int w = 8, p0, pend;
+    if (!v3_insn_g<R>(wave + k * NW, L.slab[s].group, &w, &p0, &pend)) continue;  // uniform
+    if (sf[k] & (1u << 16)) d[k] = *gp(reinterpret_cast<const u32x4*>(ptr[k] + r0 * w));
+  }
+}
+
+__device__ __forceinline__ void v4_put(uint8_t* p, uint64_t x, int flags) {
+  if (flags & 2) x = x ? 1 : 0;  // MemoryBuffer.putBoolean
+  *reinterpret_cast<uint64_t*>(p) = x;
+}
+
+template <int R>
+__device__ __forceinline__ void v4_write(const FixedLaunch& L, int s, int wave, uint8_t* lds, int sp,
+                                         const uint32_t (&sf)[kV4K], const u32x4 (&d)[kV4K]) {
+  constexpr int NW = 4 * R / 64;
+#pragma unroll
+  for (int k = 0; k < kV4K; ++k) {
+    int w = 8, p0, pend;
+    if (!v3_insn_g<R>(wave + k * NW, L.slab[s].group, &w, &p0, &pend)) continue;
+    if (!(sf[k] & (1u << 16))) continue;
+    const int sb = sf[k] & 0xfff, flags = (sf[k] >> 12) & 0xf, rb = sf[k] >> 17;
+    uint8_t* p = lds + rb * sp + sb;
+    const u32x4 x = d[k];
+    if (w == 8) {
+      v4_put(p, (uint64_t)x.x | ((uint64_t)x.y << 32), flags);
+      v4_put(p + sp, (uint64_t)x.z | ((uint64_t)x.w << 32), flags);
+    } else if (w == 4) {
+      v4_put(p, x.x, flags);
+      v4_put(p + sp, x.y, flags);
+      v4_put(p + 2 * sp, x.z, flags);
+      v4_put(p + 3 * sp, x.w, flags);
+    } else if (w == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v4_put(p + e * sp, (x[e >> 1] >> (16 * (e & 1))) & 0xffff, flags);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v4_put(p + e * sp, (x[e >> 2] >> (8 * (e & 3))) & 0xff, flags);
+    }
+  }
+}
+
+// Slab s of tile rows [r0, r0+R): R runs of nbytes from the LDS image.
+template <int R>
+__device__ __forceinline__ void v4_store(const FixedLaunch& L, int s, const uint8_t* lds, int sp, uint8_t* out,
+                                         int64_t r0, int tid) {
+  constexpr int WG = 4 * R;
+  const uint32_t cpr = (uint32_t)L.slab[s].nbytes >> 4;
+  const int n16 = R * (int)cpr;
+  uint8_t* base = out + r0 * L.stride + L.slab[s].byte0;
+  for (int q = tid; q < n16; q += WG) {
+    uint32_t j = __umulhi((uint32_t)q, L.slab[s].cpr_magic);
+    uint32_t c = (uint32_t)q - j * cpr;
+    if (c >= cpr) { ++j; c -= cpr; }
+    const u32x4 y = *reinterpret_cast<const u32x4*>(lds + j * sp + c * 16);
+    *gp(reinterpret_cast<u32x4*>(base + (int64_t)j * L.stride + c * 16)) = y;
+  }
+}
+
+template <int R, int S>
+__global__ __launch_bounds__(4 * R, 4) void encode_fixed_v4_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
+                                                                  uint8_t* __restrict__ out, int64_t tiles) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sp = L.slab_pitch;
+  int64_t t = blockIdx.x;
+  if (t >= tiles) return;
+
+  const uint8_t* ptr[S][kV4K];
+  uint32_t sf[S][kV4K];
+#pragma unroll
+  for (int s = 0; s < S; ++s) v4_desc<R, S>(L, fields, wave, lane, s, ptr[s], sf[s]);
+  u32x4 d[kV4K];
+  v4_issue<R>(L, 0, wave, t * R, ptr[0], sf[0], d);
+  for (;;) {
+    const int64_t tn = t + gridDim.x;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      if (s == 0 && tid < R) {  // slab 0 holds the null bitmap: zero it (no nullable fields here)
+        for (int b = 0; b < L.bitmap_bytes; b += 8) *reinterpret_cast<uint64_t*>(lds + tid * sp + b) = 0;
+      }
+      v4_write<R>(L, s, wave, lds, sp, sf[s], d);
+      __syncthreads();
+      if (s + 1 < S) v4_issue<R>(L, s + 1, wave, t * R, ptr[s + 1], sf[s + 1], d);
+      else if (tn < tiles) v4_issue<R>(L, 0, wave, tn * R, ptr[0], sf[0], d);
+      v4_store<R>(L, s, lds, sp, out, t * R, tid);
+      __syncthreads();
+    }
     if (tn >= tiles) break;
     t = tn;
   }
@@ -395,7 +852,7 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane % TR;
   const int fsub = lane / TR;
-  const int64_t r0 = (int64_t)blockIdx.x * TR;
+  const int64_t r0 = (L.tile0 + (int64_t)blockIdx.x) * TR;
   const int64_t left = L.num_rows - r0;
   const int rows = left < TR ? (int)left : TR;
   const int stride = L.stride;
@@ -958,17 +1415,124 @@ int num_cus() {
 
 // Persistent grid: resident workgroups per CU (occupancy query) x CUs.
 template <typename K>
-int64_t persistent_grid(K* kernel, size_t lds, int64_t tiles) {
+int64_t persistent_grid(K* kernel, size_t lds, int64_t tiles, int wg = kWG) {
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kWG, lds) != hipSuccess || per_cu <= 0)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, wg, lds) != hipSuccess || per_cu <= 0)
     per_cu = 1;
   const int64_t g = (int64_t)per_cu * num_cus();
   return tiles < g ? tiles : g;
 }
 
-int variant() {  // FORY_ROWFMT_PIPE=0 selects the one-tile-per-workgroup kernels (A/B)
+// Kernel variant for A/B runs (FORY_ROWFMT_PIPE): 0 one tile per workgroup,
+// 1 persistent pipelined (lane = record), 2 / 3 encode v3 with R = 64 / 128,
+// 4 encode v4 column slabs, 5 / 6 (default) encode v5 depth-2 pipeline with
+// R = 64 / 128 (fallbacks: v3 for nullable schemas, one-tile kernel).
+int variant() {
   const char* e = getenv("FORY_ROWFMT_PIPE");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 6;
+}
+
+template <int R, bool FRAME, bool NULLS, bool PAD>
+hipError_t launch_encode_v3(const FixedLaunch& L, uint8_t* out, hipStream_t s, bool* done) {
+  *done = false;
+  if (v3_insn_count<R>(L.group) > kV3K * (4 * R / 64)) return hipSuccess;  // too many fields: fall back
+  const int64_t full = L.num_rows / R;
+  if (full > 0) {
+    auto* k = &encode_fixed_v3_kernel<R, FRAME, NULLS, PAD>;
+    static bool init = false;
+    if (!init) { raise_lds_cap(k); init = true; }
+    const size_t lds = (size_t)R * (PAD ? L.pitch : L.stride);
+    const int64_t grid = persistent_grid(k, lds, full, 4 * R);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(4 * R), lds, s, L, L.fields, out, full);
+  }
+  if (L.num_rows > full * R) {  // tail (< R records): one-tile kernel from tile full*R/64
+    FixedLaunch T = L;
+    T.tile0 = full * R / 64;
+    auto* k = &encode_fixed_kernel<64, FRAME>;
+    static bool init2 = false;
+    if (!init2) { raise_lds_cap(k); init2 = true; }
+    const int64_t tail_tiles = (L.num_rows - full * R + 63) / 64;
+    hipLaunchKernelGGL(k, dim3((unsigned)tail_tiles), dim3(kWG), (size_t)64 * L.stride, s, T, L.fields, out);
+  }
+  *done = true;
+  return hipGetLastError();
+}
+
+template <int R, int S>
+hipError_t launch_encode_v4(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
+  const int64_t full = L.num_rows / R;
+  if (full > 0) {
+    auto* k = &encode_fixed_v4_kernel<R, S>;
+    static bool init = false;
+    if (!init) { raise_lds_cap(k); init = true; }
+    const size_t lds = (size_t)R * L.slab_pitch;
+    const int64_t grid = persistent_grid(k, lds, full, 4 * R);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(4 * R), lds, s, L, L.slab_fields, out, full);
+  }
+  if (L.num_rows > full * R) {  // tail (< R records): one-tile kernel
+    FixedLaunch T = L;
+    T.tile0 = full * R / 64;
+    auto* k = &encode_fixed_kernel<64, false>;
+    static bool init2 = false;
+    if (!init2) { raise_lds_cap(k); init2 = true; }
+    const int64_t tail_tiles = (L.num_rows - full * R + 63) / 64;
+    hipLaunchKernelGGL(k, dim3((unsigned)tail_tiles), dim3(kWG), (size_t)64 * L.stride, s, T, L.fields, out);
+  }
+  return hipGetLastError();
+}
+
+template <int R, int K, bool FRAME, bool PAD>
+hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
+  const int64_t full = L.num_rows / R;
+  if (full > 0) {
+    auto* k = &encode_fixed_v5_kernel<R, K, FRAME, PAD>;
+    static bool init = false;
+    if (!init) { raise_lds_cap(k); init = true; }
+    const size_t lds = (size_t)R * (PAD ? L.pitch : L.stride);
+    const int64_t grid = persistent_grid(k, lds, full, 4 * R);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(4 * R), lds, s, L, L.fields, out, full);
+  }
+  if (L.num_rows > full * R) {
+    FixedLaunch T = L;
+    T.tile0 = full * R / 64;
+    auto* k = &encode_fixed_kernel<64, FRAME>;
+    static bool init2 = false;
+    if (!init2) { raise_lds_cap(k); init2 = true; }
+    const int64_t tail_tiles = (L.num_rows - full * R + 63) / 64;
+    hipLaunchKernelGGL(k, dim3((unsigned)tail_tiles), dim3(kWG), (size_t)64 * L.stride, s, T, L.fields, out);
+  }
+  return hipGetLastError();
+}
+
+// v5 (depth-2 pipeline): not-null schemas, <= K load instructions per wave.
+template <bool FRAME>
+hipError_t try_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s, int R, bool* done) {
+  *done = false;
+  if (L.any_nullable) return hipSuccess;
+  FixedLaunch P = L;
+  P.pitch = L.stride + ((4 - L.stride % 32) + 32) % 32;
+  P.stride_magic = 0xffffffffu / (uint32_t)L.stride;
+  const bool pad = !FRAME && !getenv("FORY_ROWFMT_NOPAD");
+  const int per_wave64 = (v3_insn_count<64>(L.group) + 3) / 4;
+  const int per_wave128 = (v3_insn_count<128>(L.group) + 7) / 8;
+  hipError_t e = hipSuccess;
+  if (R == 64 && per_wave64 <= 12) {
+    e = pad ? launch_encode_v5<64, 12, FRAME, true>(P, out, s) : launch_encode_v5<64, 12, FRAME, false>(P, out, s);
+    *done = true;
+  } else if (R == 128 && per_wave128 <= 12) {
+    e = pad ? launch_encode_v5<128, 12, FRAME, true>(P, out, s) : launch_encode_v5<128, 12, FRAME, false>(P, out, s);
+    *done = true;
+  }
+  return e;
+}
+
+// v4 applies to raw rows of not-null schemas whose row size is a multiple of
+// 16 and whose slabs fit kV4K instructions per wave.
+bool v4_ok(const FixedLaunch& L) {
+  if (L.frame || L.any_nullable || L.num_slabs < 2 || L.num_slabs > 4 || (L.fixed_size & 15)) return false;
+  for (int s = 0; s < L.num_slabs; ++s)
+    if (v3_insn_count<64>(L.slab[s].group) > kV4K * 4) return false;
+  return L.slab_fields != nullptr;
 }
 
 template <int TR, bool FRAME>
@@ -976,13 +1540,60 @@ hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const int64_t tiles = (L.num_rows + TR - 1) / TR;
   const size_t lds = (size_t)TR * L.stride;
   if constexpr (TR == 64) {
+    const int var = variant();
+    if (var == 5 || var == 6) {  // v5: depth-2 pipeline, R = 64 (5) / 128 (6)
+      bool done = false;
+      hipError_t e = try_encode_v5<FRAME>(L, out, s, var == 5 ? 64 : 128, &done);
+      if (done || e != hipSuccess) return e;
+      if (!L.any_nullable) {  // too many fields per wave for v5: v3
+        e = launch_encode_v3<64, FRAME, false, false>(L, out, s, &done);
+        if (done || e != hipSuccess) return e;
+      }
+    }
+    if (var == 4 && !FRAME && v4_ok(L)) {
+      switch (L.num_slabs) {
+        case 2: return launch_encode_v4<64, 2>(L, out, s);
+        case 3: return launch_encode_v4<64, 3>(L, out, s);
+        default: return launch_encode_v4<64, 4>(L, out, s);
+      }
+    }
+    if (var == 4) {  // frames / nullable / odd rows: v3 (R = 64 for frames, 128 otherwise)
+      bool done = false;
+      hipError_t e = hipSuccess;
+      if (!L.any_nullable) {
+        FixedLaunch P = L;
+        P.pitch = L.stride + ((4 - L.stride % 32) + 32) % 32;
+        P.stride_magic = 0xffffffffu / (uint32_t)L.stride;
+        e = FRAME ? launch_encode_v3<64, FRAME, false, false>(L, out, s, &done)
+                  : launch_encode_v3<128, FRAME, false, false>(L, out, s, &done);
+        if (done || e != hipSuccess) return e;
+      }
+    }
+    if (var == 2 || var == 3) {
+      bool done = false;
+      hipError_t e = hipSuccess;
+      // v3 covers not-null schemas (the nullable form spills: falls back below)
+      if (!L.any_nullable) {
+        // raw rows (8-byte aligned slots): padded LDS pitch; frames: pitch = stride
+        FixedLaunch P = L;
+        P.pitch = L.stride + ((4 - L.stride % 32) + 32) % 32;  // pitch = 4 (mod 32) bytes
+        P.stride_magic = 0xffffffffu / (uint32_t)L.stride;
+        if (FRAME || getenv("FORY_ROWFMT_NOPAD"))
+          e = var == 3 ? launch_encode_v3<128, FRAME, false, false>(L, out, s, &done)
+                       : launch_encode_v3<64, FRAME, false, false>(L, out, s, &done);
+        else
+          e = var == 3 ? launch_encode_v3<128, FRAME, false, true>(P, out, s, &done)
+                       : launch_encode_v3<64, FRAME, false, true>(P, out, s, &done);
+        if (done || e != hipSuccess) return e;
+      }
+    }
     const int n8 = L.group[1] - L.group[0], n4 = L.group[2] - L.group[1];
     const int n2 = L.group[3] - L.group[2], n1 = L.group[4] - L.group[3];
-    if (n8 <= 4 * kM8 && n4 <= 4 * kM4 && n2 <= 4 * kM2 && n1 <= 4 * kM1 && variant() == 1) {
+    if (n8 <= 4 * kM8 && n4 <= 4 * kM4 && n2 <= 4 * kM2 && n1 <= 4 * kM1 && var == 1) {
       auto* k = &encode_fixed_pipe_kernel<FRAME>;
       static bool init = false;
       if (!init) { raise_lds_cap(k); init = true; }
-      const int64_t grid = persistent_grid(k, lds, tiles);
+      const int64_t grid = persistent_grid(k, lds, tiles, kWG);
       hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kWG), lds, s, L, L.fields, out, tiles);
       return hipGetLastError();
     }

@@ -1,0 +1,26 @@
+"""profiles/pmc_latest.json from a scripts/profile.sh summary: per-launch HBM bytes of the
+bench's encode and decode kernels = FETCH_SIZE*1024*2 (gfx950 half-count correction,
+MI355X_MICROARCH.md §HBM; calibrated here: it equals the algorithmic read bytes exactly)
++ WRITE_SIZE*1024. Usage: python scripts/pmc_to_traffic.py SUMMARY KEY [OUT]"""
+import json
+import sys
+
+summ = json.load(open(sys.argv[1]))
+key = sys.argv[2]
+out = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_latest.json"
+try:
+    cur = json.load(open(out))
+except (OSError, ValueError):
+    cur = {}
+ent = {}
+for name, e in summ["pmc"].items():
+    role = "encode" if name.startswith("encode") or name.startswith("var_encode") else \
+        "decode" if name.startswith("decode") or name.startswith("var_decode_kernelILb1") else None
+    if role and "fetch_bytes_x2" in e and "write_bytes" in e:
+        ent[role] = int(e["fetch_bytes_x2"] + e["write_bytes"])
+        ent[role + "_kernel"] = name
+        ent[role + "_fetch_bytes_x2"] = int(e["fetch_bytes_x2"])
+        ent[role + "_write_bytes"] = int(e["write_bytes"])
+cur[key] = ent
+json.dump(cur, open(out, "w"), indent=1, sort_keys=True)
+print(json.dumps(ent))

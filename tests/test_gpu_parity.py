@@ -35,10 +35,15 @@ def encoder_for(name):
     return _ENC[name]
 
 
-@pytest.fixture(params=["1", "0"], ids=["pipe", "tile"])
+@pytest.fixture(params=["6", "5", "5n", "4", "3", "3n", "2", "1", "0"],
+                ids=["v5r128", "v5r64", "v5r64nopad", "v4", "v3r128", "v3r128nopad", "v3r64", "pipe", "tile"])
 def kernel_variant(request, monkeypatch):
-    """Fixed-width kernels: persistent pipelined (1) and one-tile-per-workgroup (0)."""
-    monkeypatch.setenv("FORY_ROWFMT_PIPE", request.param)
+    """Fixed-width kernel variants (FORY_ROWFMT_PIPE): 4 encode v4 (column slabs, the
+    default), 3/2 encode v3 (16-B column chunks, 128/64 records per tile), 1 persistent
+    pipelined, 0 one tile per workgroup."""
+    monkeypatch.setenv("FORY_ROWFMT_PIPE", request.param[0])
+    if request.param.endswith("n"):
+        monkeypatch.setenv("FORY_ROWFMT_NOPAD", "1")
     return request.param
 
 
@@ -46,7 +51,7 @@ def kernel_variant(request, monkeypatch):
 @pytest.mark.parametrize("n", SIZES)
 @pytest.mark.parametrize("name", list(catalog().keys()))
 def test_encode_decode_parity(name, n, frame, kernel_variant):
-    if kernel_variant == "0" and name.startswith(("mixed", "nested", "strings")):
+    if kernel_variant != "4" and name.startswith(("mixed", "nested", "strings")):
         pytest.skip("the variant switch only affects fixed-width schemas")
     schema, make = catalog()[name]
     cols = make(n, n)
