@@ -19,11 +19,10 @@ def rows(pattern):
 
 
 def short(name):
-    for k in ("encode_fixed_pipe", "decode_fixed_pipe", "encode_fixed_kernel", "decode_fixed_kernel",
-              "var_encode", "var_decode_kernelILb0", "var_decode_kernelILb1", "var_sizes", "scan_", "fill_offsets"):
-        if k in name:
-            return k + ("<frame>" if "ILb1E" in name and "fixed" in k else "")
-    return name[:60]
+    import re
+    m = re.search(r"(encode_fixed_\w*?kernel|decode_fixed_\w*?kernel|var_encode_kernel|var_decode_kernelILb[01]|"
+                  r"var_sizes_kernel|scan_\w+?_kernel|fill_offsets_kernel)", name)
+    return m.group(1) if m else name[:60]
 
 
 out = {"kernels": {}, "pmc": {}}
