@@ -527,9 +527,8 @@ __device__ __forceinline__ void v5_write(uint8_t* lds, int pitch, int hdr_bm, co
   }
 }
 
-template <int R, bool PAD>
+template <int R, int WG, bool PAD>
 __device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* lds, int pitch, uint8_t* dst, int tid) {
-  constexpr int WG = 4 * R;
   const int stride = L.stride;
   const int bytes = R * stride;
   const int n16 = bytes >> 4;
@@ -555,12 +554,12 @@ __device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* ld
   }
 }
 
-template <int R, int K, bool FRAME, bool PAD>
-__global__ __launch_bounds__(4 * R, 1) void encode_fixed_v5_kernel(FixedLaunch L,
-                                                                    const FixedFieldDev* __restrict__ fields,
-                                                                    uint8_t* __restrict__ out, int64_t tiles) {
+template <int R, int WG, int K, bool FRAME, bool PAD>
+__global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
+                                                                 const FixedFieldDev* __restrict__ fields,
+                                                                 uint8_t* __restrict__ out, int64_t tiles) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int NW = 4 * R / 64;
+  constexpr int NW = WG / 64;
   constexpr int HDR = FRAME ? 12 : 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -579,7 +578,7 @@ __global__ __launch_bounds__(4 * R, 1) void encode_fixed_v5_kernel(FixedLaunch L
   for (int k = 0; k < K; ++k) {
     int w = 0, p0 = 0, pend = 0;
     const bool ok = v3_insn<R>(wave + k * NW, L, &w, &p0, &pend);
-    wk[k] = ok ? w : 0;
+    wk[k] = ok ? w : 0;  // absent instruction: width 0 -> re-reads the dummy address
     const int cpf = R * (ok ? w : 8) / 16;
     const int p = p0 + lane / cpf, c = lane % cpf;
     ptr[k] = dummy;
@@ -588,8 +587,6 @@ __global__ __launch_bounds__(4 * R, 1) void encode_fixed_v5_kernel(FixedLaunch L
       const FixedFieldDev& fd = fields[p];
       ptr[k] = fd.values + c * 16;
       sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (1u << 20) | ((uint32_t)(c * (16 / w)) << 21);
-    } else {
-      wk[k] = ok ? w : 0;
     }
   }
   if (tid < R) put_header<FRAME>(lds + tid * pitch, L);  // constant across tiles (no nullable fields)
@@ -600,14 +597,14 @@ __global__ __launch_bounds__(4 * R, 1) void encode_fixed_v5_kernel(FixedLaunch L
   for (;;) {
     v5_write<R, K, FRAME, PAD>(lds, pitch, hdr_bm, wk, sf, dA);
     __syncthreads();
-    v5_store<R, PAD>(L, lds, pitch, out + t * R * stride, tid);
+    v5_store<R, WG, PAD>(L, lds, pitch, out + t * R * stride, tid);
     v5_issue<R, K>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dA);
     __syncthreads();
     t += gridDim.x;
     if (t >= tiles) break;
     v5_write<R, K, FRAME, PAD>(lds, pitch, hdr_bm, wk, sf, dB);
     __syncthreads();
-    v5_store<R, PAD>(L, lds, pitch, out + t * R * stride, tid);
+    v5_store<R, WG, PAD>(L, lds, pitch, out + t * R * stride, tid);
     v5_issue<R, K>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dB);
     __syncthreads();
     t += gridDim.x;
@@ -870,6 +867,95 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
   dec_group<4, TR, FRAME>(fields, L.group[1], L.group[2], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
   dec_group<2, TR, FRAME>(fields, L.group[2], L.group[3], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
   dec_group<1, TR, FRAME>(fields, L.group[3], L.group[4], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+}
+
+// Decode v2: one tile of TR records (TR a multiple of 64) per workgroup of WG
+// threads; lane = record within a 64-record half; wave instruction i covers
+// field i / (TR/64), records (i % (TR/64)) * 64 + lane. Same LDS-DMA image and
+// per-field batching as decode_fixed_kernel, more waves / larger column runs.
+template <int TR, int WG, bool FRAME>
+__global__ __launch_bounds__(WG) void decode_fixed_v2_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
+                                                             const uint8_t* __restrict__ in, int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int NW = WG / 64;
+  constexpr int H = TR / 64;  // 64-record halves per tile
+  constexpr int HDR = FRAME ? 12 : 0;
+  constexpr int U = 8;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t r0 = (L.tile0 + (int64_t)blockIdx.x) * TR;
+  const int64_t left = L.num_rows - r0;
+  const int rows = left < TR ? (int)left : TR;
+  const int stride = L.stride;
+  const int hdr_bm = HDR + L.bitmap_bytes;
+  {  // tile image HBM -> LDS (LDS-DMA, 1 KiB per wave instruction)
+    const uint8_t* src = in + r0 * stride;
+    const int bytes = rows * stride;
+    const int n16 = bytes >> 4;
+    for (int c0 = 0; c0 < n16; c0 += WG) {
+      const int c = c0 + tid;
+      if (c < n16)
+        __builtin_amdgcn_global_load_lds((const GAS void*)(src + (int64_t)c * 16),
+                                         (__attribute__((address_space(3))) void*)(lds + (c0 + wave * 64) * 16), 16,
+                                         0, 0);
+    }
+    const int tail4 = (bytes & 15) >> 2;
+    if (tid < tail4) st32(lds + n16 * 16 + tid * 4, ld32(src + n16 * 16 + tid * 4));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (FRAME) {
+    for (int r = tid; r < rows; r += WG) check_frame<FRAME>(lds + r * stride, L, status);
+  }
+  const int nins = L.num_fields * H;
+  for (int ib = wave; ib < nins; ib += NW * U) {
+    uint64_t x[U];
+    bool nul[U];
+    int rr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = __builtin_amdgcn_readfirstlane(ib + u * NW);
+      const int p = i / H, h = i % H;
+      rr[u] = h * 64 + lane;
+      x[u] = 0;
+      nul[u] = true;
+      if (i < nins) {
+        const uint8_t* row = lds + rr[u] * stride;
+        const int slot = fields[p].slot;
+        const int w = fields[p].width;
+        nul[u] = (ld32(row + HDR + ((slot >> 5) << 2)) >> (slot & 31)) & 1;
+        const uint8_t* sp = row + hdr_bm + 8 * slot;
+        if (w == 8) x[u] = (FRAME ? ((uint64_t)ld32(sp) | ((uint64_t)ld32(sp + 4) << 32))
+                                  : *reinterpret_cast<const uint64_t*>(sp));
+        else x[u] = ld32(sp);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = __builtin_amdgcn_readfirstlane(ib + u * NW);
+      if (i < nins) {
+        const int p = i / H;
+        const FixedFieldDev& fd = fields[p];
+        const bool live = rr[u] < rows;
+        uint64_t v = nul[u] ? 0 : x[u];
+        if (fd.flags & 2) v = (v & 0xff) ? 1 : 0;
+        if (live) {
+          switch (fd.width) {
+            case 8: stw<8>(fd.out_values, r0 + rr[u], v); break;
+            case 4: stw<4>(fd.out_values, r0 + rr[u], v); break;
+            case 2: stw<2>(fd.out_values, r0 + rr[u], v); break;
+            default: stw<1>(fd.out_values, r0 + rr[u], v); break;
+          }
+        }
+        if ((fd.flags & 1) && fd.out_validity) {
+          const int h = i % H;
+          const int hrows = rows - h * 64 < 64 ? rows - h * 64 : 64;
+          if (hrows > 0) put_validity<64>(fd, nul[u], live, lane, 0, r0 + h * 64, hrows);
+        }
+      }
+    }
+  }
 }
 
 // Persistent, software-pipelined decode (TR = 64, tile image <= MAXC*4 KiB):
@@ -1425,11 +1511,11 @@ int64_t persistent_grid(K* kernel, size_t lds, int64_t tiles, int wg = kWG) {
 
 // Kernel variant for A/B runs (FORY_ROWFMT_PIPE): 0 one tile per workgroup,
 // 1 persistent pipelined (lane = record), 2 / 3 encode v3 with R = 64 / 128,
-// 4 encode v4 column slabs, 5 / 6 (default) encode v5 depth-2 pipeline with
-// R = 64 / 128 (fallbacks: v3 for nullable schemas, one-tile kernel).
+// 4 encode v4 column slabs, 5..8 encode v5 depth-2 pipeline (8 = default:
+// R = 64, 512 threads; see try_encode_v5), fallbacks: v3, one-tile kernel.
 int variant() {
   const char* e = getenv("FORY_ROWFMT_PIPE");
-  return e ? atoi(e) : 6;
+  return e ? atoi(e) : 8;
 }
 
 template <int R, bool FRAME, bool NULLS, bool PAD>
@@ -1481,16 +1567,16 @@ hipError_t launch_encode_v4(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int R, int K, bool FRAME, bool PAD>
+template <int R, int WG, int K, bool FRAME, bool PAD>
 hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const int64_t full = L.num_rows / R;
   if (full > 0) {
-    auto* k = &encode_fixed_v5_kernel<R, K, FRAME, PAD>;
+    auto* k = &encode_fixed_v5_kernel<R, WG, K, FRAME, PAD>;
     static bool init = false;
     if (!init) { raise_lds_cap(k); init = true; }
     const size_t lds = (size_t)R * (PAD ? L.pitch : L.stride);
-    const int64_t grid = persistent_grid(k, lds, full, 4 * R);
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(4 * R), lds, s, L, L.fields, out, full);
+    const int64_t grid = persistent_grid(k, lds, full, WG);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(WG), lds, s, L, L.fields, out, full);
   }
   if (L.num_rows > full * R) {
     FixedLaunch T = L;
@@ -1505,24 +1591,29 @@ hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
 }
 
 // v5 (depth-2 pipeline): not-null schemas, <= K load instructions per wave.
+// v5 shapes: 5 = R64/WG256, 6 = R128/WG512 (default), 7 = R128/WG1024, 8 = R64/WG512.
 template <bool FRAME>
-hipError_t try_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s, int R, bool* done) {
+hipError_t try_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s, int var, bool* done) {
   *done = false;
   if (L.any_nullable) return hipSuccess;
   FixedLaunch P = L;
   P.pitch = L.stride + ((4 - L.stride % 32) + 32) % 32;
   P.stride_magic = 0xffffffffu / (uint32_t)L.stride;
-  const bool pad = !FRAME && !getenv("FORY_ROWFMT_NOPAD");
-  const int per_wave64 = (v3_insn_count<64>(L.group) + 3) / 4;
-  const int per_wave128 = (v3_insn_count<128>(L.group) + 7) / 8;
+  // LDS pitch padding (raw rows): measured neutral-to-negative for the
+  // 512-thread shapes, so off unless FORY_ROWFMT_PAD=1.
+  const bool pad = !FRAME && getenv("FORY_ROWFMT_PAD") && !getenv("FORY_ROWFMT_NOPAD");
+  const int i64 = v3_insn_count<64>(L.group), i128 = v3_insn_count<128>(L.group);
   hipError_t e = hipSuccess;
-  if (R == 64 && per_wave64 <= 12) {
-    e = pad ? launch_encode_v5<64, 12, FRAME, true>(P, out, s) : launch_encode_v5<64, 12, FRAME, false>(P, out, s);
-    *done = true;
-  } else if (R == 128 && per_wave128 <= 12) {
-    e = pad ? launch_encode_v5<128, 12, FRAME, true>(P, out, s) : launch_encode_v5<128, 12, FRAME, false>(P, out, s);
-    *done = true;
-  }
+#define V5(R, WG, K)                                                                             \
+  do {                                                                                           \
+    e = pad ? launch_encode_v5<R, WG, K, FRAME, true>(P, out, s) : launch_encode_v5<R, WG, K, FRAME, false>(P, out, s); \
+    *done = true;                                                                                \
+  } while (0)
+  if (var == 5 && (i64 + 3) / 4 <= 12) V5(64, 256, 12);
+  else if (var == 6 && (i128 + 7) / 8 <= 12) V5(128, 512, 12);
+  else if (var == 7 && (i128 + 15) / 16 <= 6) V5(128, 1024, 6);
+  else if (var == 8 && (i64 + 7) / 8 <= 6) V5(64, 512, 6);
+#undef V5
   return e;
 }
 
@@ -1541,9 +1632,9 @@ hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const size_t lds = (size_t)TR * L.stride;
   if constexpr (TR == 64) {
     const int var = variant();
-    if (var == 5 || var == 6) {  // v5: depth-2 pipeline, R = 64 (5) / 128 (6)
+    if (var >= 5 && var <= 8) {  // v5: depth-2 pipeline (shapes: try_encode_v5)
       bool done = false;
-      hipError_t e = try_encode_v5<FRAME>(L, out, s, var == 5 ? 64 : 128, &done);
+      hipError_t e = try_encode_v5<FRAME>(L, out, s, var, &done);
       if (done || e != hipSuccess) return e;
       if (!L.any_nullable) {  // too many fields per wave for v5: v3
         e = launch_encode_v3<64, FRAME, false, false>(L, out, s, &done);
@@ -1605,11 +1696,30 @@ hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int TR, int WG, bool FRAME>
+hipError_t launch_decode_v2(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
+  const int64_t tiles = (L.num_rows + TR - 1) / TR;
+  auto* k = &decode_fixed_v2_kernel<TR, WG, FRAME>;
+  static bool init = false;
+  if (!init) { raise_lds_cap(k); init = true; }
+  hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(WG), (size_t)TR * L.stride, s, L, L.fields, in, status);
+  return hipGetLastError();
+}
+
+int dec_variant() {  // FORY_ROWFMT_DEC: 0 decode_fixed_kernel (default), 1..3 decode v2 shapes
+  const char* e = getenv("FORY_ROWFMT_DEC");
+  return e ? atoi(e) : 0;
+}
+
 template <int TR, bool FRAME>
 hipError_t launch_decode_tr(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
   const int64_t tiles = (L.num_rows + TR - 1) / TR;
   const size_t lds = (size_t)TR * L.stride;
   if constexpr (TR == 64) {
+    const int dv = dec_variant();
+    if (dv == 1 && 64 * L.stride <= 80 * 1024) return launch_decode_v2<64, 512, FRAME>(L, in, status, s);
+    if (dv == 2 && 128 * L.stride <= 160 * 1024) return launch_decode_v2<128, 512, FRAME>(L, in, status, s);
+    if (dv == 3 && 128 * L.stride <= 160 * 1024) return launch_decode_v2<128, 1024, FRAME>(L, in, status, s);
     constexpr int MAXC = 14;
     if (lds <= (size_t)MAXC * kWG * 16 && variant() == 1) {
       auto* k = &decode_fixed_pipe_kernel<FRAME, MAXC>;

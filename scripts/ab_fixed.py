@@ -28,12 +28,17 @@ for frame in (0, 1):
     dcols = enc.alloc_fixed_outputs(n)
     darr = native.column_array(dcols)
     for rnd in range(rounds):
-        for var in ("6", "5", "4", "3", "2"):
-            os.environ["FORY_ROWFMT_PIPE"] = var[0]
-            if var.endswith("n"):
-                os.environ["FORY_ROWFMT_NOPAD"] = "1"
+        for var in ("8", "8p", "6", "d1", "d2", "d3"):
+            os.environ.pop("FORY_ROWFMT_DEC", None)
+            os.environ.pop("FORY_ROWFMT_PAD", None)
+            if var.startswith("d"):
+                os.environ["FORY_ROWFMT_DEC"] = var[1]
+                var_env = "8"
             else:
-                os.environ.pop("FORY_ROWFMT_NOPAD", None)
+                var_env = var[0]
+            if var.endswith("p"):
+                os.environ["FORY_ROWFMT_PAD"] = "1"
+            os.environ["FORY_ROWFMT_PIPE"] = var_env
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             native.encode(plan, arr, n, frame, None, out, status, ws)
             native.decode(plan, out, None, n, frame, darr, status, ws)
@@ -69,7 +74,8 @@ for f, c in zip(W.struct_schema().fields, cols):
 harr = native.column_array(hot)
 out = torch.empty(n * plan.stride(0), dtype=torch.uint8, device="cuda")
 os.environ.pop("FORY_ROWFMT_NOPAD", None)
-for var in ("6", "5", "4", "3", "2"):
+os.environ.pop("FORY_ROWFMT_DEC", None)
+for var in ("8", "6"):
     os.environ["FORY_ROWFMT_PIPE"] = var
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     native.encode(plan, harr, n, 0, None, out, status, ws)

@@ -127,6 +127,53 @@ __global__ __launch_bounds__(256) void enc_traffic(Cols c, long nrows, unsigned 
   }
 }
 
+// The decode's HBM traffic without LDS: per tile of R records, read R*848
+// contiguous bytes (16 B/lane), then store the 104 column segments either
+// lane = record (4/8-B stores, W=0) or as 16-B chunks (W=16).
+template <int R, int W>
+__global__ __launch_bounds__(256) void dec_traffic(Cols c, long nrows, const unsigned char* __restrict__ rows) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long tiles = nrows / R;
+  for (long t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const long r0 = t * R;
+    const unsigned char* s = rows + r0 * 848;
+    unsigned acc = 0;
+    const int n16 = R * 848 / 16;
+    u32x4 v[(R * 848 / 16 + 255) / 256];
+#pragma unroll
+    for (int k = 0; k < (R * 848 / 16 + 255) / 256; ++k) {
+      const int q = k * 256 + tid;
+      u32x4 x = {0, 0, 0, 0};
+      if (q < n16) x = *(const u32x4*)(s + q * 16);
+      v[k] = x;
+    }
+#pragma unroll
+    for (int k = 0; k < (R * 848 / 16 + 255) / 256; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    if (W == 16) {
+      constexpr int C8 = R * 8 / 16, C4 = R * 4 / 16;
+      constexpr int I8 = 52 * C8 / 64, I4 = 52 * C4 / 64;
+      for (int i = wave; i < I8 + I4; i += 4) {
+        u32x4 y = {acc, acc, acc, acc};
+        if (i < I8) {
+          const int q = i * 64 + lane;
+          *(u32x4*)(c.p[2 * (q / C8) + 1] + r0 * 8 + (q % C8) * 16) = y;
+        } else {
+          const int q = (i - I8) * 64 + lane;
+          *(u32x4*)(c.p[2 * (q / C4)] + r0 * 4 + (q % C4) * 16) = y;
+        }
+      }
+    } else {
+      for (int f = wave; f < 104; f += 4) {
+        for (int k = 0; k < R / 64; ++k) {
+          const long r = r0 + lane + 64 * k;
+          if (f & 1) *(unsigned long long*)(c.p[f] + r * 8) = acc;
+          else *(unsigned*)(c.p[f] + r * 4) = acc;
+        }
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void writerows(unsigned char* __restrict__ out, long nrows, int stride) {
   const long tiles = nrows / 64;
   const int tid = threadIdx.x;
@@ -201,6 +248,14 @@ int main(int argc, char** argv) {
   for (int wpc : {2, 4, 8}) {
     const int g = cus * wpc;
     float ms;
+    ms = time_ms([&] { hipLaunchKernelGGL((dec_traffic<64, 0>), dim3(g), dim3(256), 0, 0, c, n, rows); });
+    printf("{\"test\":\"dec_traffic R64 lane=row\",\"wg_per_cu\":%d,\"ms\":%.3f,\"GBs\":%.1f}\n", wpc, ms, (colbytes + rowbytes) / ms / 1e6);
+    ms = time_ms([&] { hipLaunchKernelGGL((dec_traffic<64, 16>), dim3(g), dim3(256), 0, 0, c, n, rows); });
+    printf("{\"test\":\"dec_traffic R64 16B\",\"wg_per_cu\":%d,\"ms\":%.3f,\"GBs\":%.1f}\n", wpc, ms, (colbytes + rowbytes) / ms / 1e6);
+    ms = time_ms([&] { hipLaunchKernelGGL((dec_traffic<128, 16>), dim3(g), dim3(256), 0, 0, c, n, rows); });
+    printf("{\"test\":\"dec_traffic R128 16B\",\"wg_per_cu\":%d,\"ms\":%.3f,\"GBs\":%.1f}\n", wpc, ms, (colbytes + rowbytes) / ms / 1e6);
+    ms = time_ms([&] { hipLaunchKernelGGL((dec_traffic<128, 0>), dim3(g), dim3(256), 0, 0, c, n, rows); });
+    printf("{\"test\":\"dec_traffic R128 lane=row\",\"wg_per_cu\":%d,\"ms\":%.3f,\"GBs\":%.1f}\n", wpc, ms, (colbytes + rowbytes) / ms / 1e6);
     ms = time_ms([&] { hipLaunchKernelGGL((enc_traffic<64>), dim3(g), dim3(256), 0, 0, c, n, rows); });
     printf("{\"test\":\"enc_traffic R64\",\"wg_per_cu\":%d,\"ms\":%.3f,\"GBs\":%.1f}\n", wpc, ms, (colbytes + rowbytes) / ms / 1e6);
     ms = time_ms([&] { hipLaunchKernelGGL((enc_traffic<128>), dim3(g), dim3(256), 0, 0, c, n, rows); });
