@@ -191,6 +191,23 @@ void build_slabs(const Plan& p, const std::vector<FixedFieldDev>& tab, int frame
   L->slab_pitch = pitch;
 }
 
+// LDS budget of one 64-record tile image for the varlen tile engine: 1.25x an
+// estimated row (fixed part, nested struct rows, ~24 bytes per string,
+// ~4 elements per list), in [8, 64] KiB. Tiles above it take the per-record
+// global path (correct, slower); FORY_ROWFMT_VARCAP overrides.
+int var_tile_cap(const Plan& p, int frame) {
+  int64_t est = p.fixed_size + (frame ? 12 : 0);
+  for (size_t k = 0; k < p.nodes.size(); ++k) {
+    const fory_amd::Node& nd = p.nodes[k];
+    if (nd.kind == fory_amd::KIND_BYTES) est += 24;
+    else if (nd.kind == fory_amd::KIND_LIST) est += 16 + 4 * 8;
+    else if (nd.kind == fory_amd::KIND_STRUCT)  // child rows live in the variable region
+      est += ((int64_t)(nd.children.size() + 63) / 64) * 8 + 8 * (int64_t)nd.children.size();
+  }
+  int64_t cap = (64 * est * 5 / 4 + 1023) / 1024 * 1024;
+  return (int)std::min<int64_t>(std::max<int64_t>(cap, 8 * 1024), 64 * 1024);
+}
+
 // Var launch: columns table then program in the workspace.
 int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, void* ws,
                 hipStream_t s, fory_amd::VarLaunch* L) {
@@ -212,6 +229,7 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   L->schema_hash = p.schema_hash;
   L->num_rows = n;
   L->frame = frame;
+  L->tile_cap = var_tile_cap(p, frame);
   return FORY_OK;
 }
 

@@ -51,6 +51,7 @@ struct VarLaunch {
   int64_t schema_hash;
   int64_t num_rows;
   int32_t frame;
+  int32_t tile_cap;             // LDS bytes per 64-record tile image (tile engine)
 };
 
 // sizes -> d_row_offsets[0..n-1] (row/frame byte sizes), then exclusive scan.

@@ -554,7 +554,11 @@ __device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* ld
   }
 }
 
-template <int R, int WG, int K, bool FRAME, bool PAD>
+// ONESHOT: one tile per workgroup, grid = tiles (no pipeline). Workgroups are
+// dispatched in tile order, so the addresses in flight chip-wide stay a
+// compact window; persistent grids drift apart (scripts/microbench/copybw.hip:
+// one-shot 16-B copy 6.25 TB/s vs 5.2-5.6 TB/s for grid-stride loops).
+template <int R, int WG, int K, bool FRAME, bool PAD, bool ONESHOT = false>
 __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
                                                                  const FixedFieldDev* __restrict__ fields,
                                                                  uint8_t* __restrict__ out, int64_t tiles) {
@@ -591,6 +595,13 @@ __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
   }
   if (tid < R) put_header<FRAME>(lds + tid * pitch, L);  // constant across tiles (no nullable fields)
   u32x4 dA[K], dB[K];
+  if constexpr (ONESHOT) {
+    v5_issue<R, K>(ptr, wk, t * R, dA);
+    v5_write<R, K, FRAME, PAD>(lds, pitch, hdr_bm, wk, sf, dA);
+    __syncthreads();
+    v5_store<R, WG, PAD>(L, lds, pitch, out + t * R * stride, tid);
+    return;
+  }
   const int64_t last = tiles - 1;
   v5_issue<R, K>(ptr, wk, t * R, dA);
   v5_issue<R, K>(ptr, wk, min(t + (int64_t)gridDim.x, last) * R, dB);
@@ -1178,12 +1189,42 @@ __device__ __forceinline__ void set_null_bit(uint8_t* bitmap, int32_t ordinal) {
   bitmap[ordinal >> 3] |= (uint8_t)(1u << (ordinal & 7));  // BitUtils.set
 }
 
-// Copies n bytes (any alignment) and zero-pads to round8(n) (BinaryWriter.writeUnaligned).
+// Copies n bytes from global `src` (any alignment) to `dst` (4-byte aligned;
+// LDS image or global row) and zero-pads to round8(n): BinaryWriter.writeUnaligned
+// + zeroOutPaddingBytes (BinaryWriter.java:117-121,162-194). Source dwords are
+// read aligned (each holds at least one byte of the string, so never crosses
+// the column's end) and funnel-shifted.
 __device__ __forceinline__ void copy_padded(uint8_t* dst, const uint8_t* src, int64_t n) {
+  const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
+  const int sb = (int)(sa & 3);
+  const uint8_t* s0 = reinterpret_cast<const uint8_t*>(sa - sb);
+  const int64_t n4 = (n + 3) & ~int64_t(3);
+  for (int64_t k = 0, q = 0; k < n4; k += 4, ++q) {
+    const uint32_t a = *gp(reinterpret_cast<const uint32_t*>(s0 + 4 * q));
+    const int64_t lastb = sb + (k + 4 < n ? k + 4 : n) - 1;  // last needed byte, relative to s0
+    const uint32_t b = (lastb >> 2) > q ? *gp(reinterpret_cast<const uint32_t*>(s0 + 4 * q + 4)) : 0u;
+    uint32_t w = sb ? (a >> (8 * sb)) | (b << (32 - 8 * sb)) : a;
+    const int64_t valid = n - k;
+    if (valid < 4) w &= (1u << (8 * valid)) - 1u;
+    st32(dst + k, w);
+  }
+  if (round8(n) > n4) st32(dst + n4, 0);
+}
+
+// Copies n bytes from `src` (row bytes: LDS image or global, any alignment)
+// to the global column buffer `dst` (any alignment): byte head up to a 4-byte
+// aligned destination, dword body, byte tail.
+__device__ __forceinline__ void copy_out(uint8_t* dst, const uint8_t* src, int64_t n) {
   int64_t k = 0;
-  for (; k < n; ++k) dst[k] = src[k];
-  const int64_t e = round8(n);
-  for (; k < e; ++k) dst[k] = 0;
+  const int64_t head0 = (int64_t)((4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3);
+  const int64_t head = head0 < n ? head0 : n;
+  for (; k < head; ++k) store_byte(dst + k, src[k]);
+  for (; k + 4 <= n; k += 4) {
+    const uint32_t w = (uint32_t)src[k] | ((uint32_t)src[k + 1] << 8) | ((uint32_t)src[k + 2] << 16) |
+                       ((uint32_t)src[k + 3] << 24);
+    *gp(reinterpret_cast<uint32_t*>(dst + k)) = w;
+  }
+  for (; k < n; ++k) store_byte(dst + k, src[k]);
 }
 
 // Row/frame size of record i (BinaryRowWriter.reset + all appends).
@@ -1220,20 +1261,16 @@ __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, int64_t* si
   sizes[i] = size;
 }
 
-__global__ __launch_bounds__(kWG) void var_encode_kernel(VarLaunch L, const int64_t* __restrict__ offs,
-                                                         uint8_t* __restrict__ out, int64_t capacity,
-                                                         int32_t* status) {
-  const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
-  if (i >= L.num_rows) return;
-  const int64_t beg = offs[i], end = offs[i + 1];
-  if (end > capacity || beg < 0 || end < beg) {
-    set_status(status, FORY_ERR_CAPACITY);
-    return;
-  }
-  uint8_t* base = out + beg;
+constexpr int kFixBatch = 8;  // consecutive OP_FIXED ops whose loads are issued together
+
+// Encodes record i into `base` (its frame in STREAM mode, else its row;
+// `size` bytes; an LDS tile image or global memory). Generated toRow
+// (RowEncoderBuilder.java:177-208) with BaseBinaryEncoderBuilder's per-type
+// branches (:149-490) as an op program.
+__device__ void enc_record(const VarLaunch& L, int64_t i, uint8_t* base, int64_t size) {
   uint8_t* row = base;
   if (L.frame) {  // Encoders.encode(MemoryBuffer,T): [i32 8+rowSize][i64 hash]
-    st32(base, (uint32_t)(end - beg - 4));
+    st32(base, (uint32_t)(size - 4));
     gst64(base + 4, (uint64_t)L.schema_hash);
     row = base + 12;
   }
@@ -1254,16 +1291,35 @@ __global__ __launch_bounds__(kWG) void var_encode_kernel(VarLaunch L, const int6
       else if (op.code == OP_STRUCT_END) absent--;
       continue;
     }
-    uint8_t* slot = row + st_start[depth] + st_hdr[depth] + 8 * op.a;
+    uint8_t* slots = row + st_start[depth] + st_hdr[depth];
+    uint8_t* slot = slots + 8 * op.a;
     uint8_t* bitmap = row + st_start[depth];
     const bool isnull = (op.d & 1) && !col_valid(c, i);
     switch (op.code) {
-      case OP_FIXED: {
-        uint64_t v = 0;
-        if (isnull) set_null_bit(bitmap, op.a);
-        else v = load_elem(c.values, op.c, i);
-        if (op.d & 2) v = v ? 1 : 0;
-        gst64(slot, v);
+      case OP_FIXED: {  // BinaryRowWriter.write(ordinal, v) / setNullAt, batched
+        int cnt = 1;
+        while (cnt < kFixBatch && pc + cnt < L.num_ops && L.prog[pc + cnt].code == OP_FIXED) ++cnt;
+        uint64_t v[kFixBatch];
+#pragma unroll
+        for (int k = 0; k < kFixBatch; ++k) {
+          v[k] = 0;
+          if (k < cnt) {
+            const Op o = L.prog[pc + k];
+            const ColumnDev& cc = L.cols[o.b];
+            if (!(o.d & 1) || col_valid(cc, i)) v[k] = load_elem(cc.values, o.c, i);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < kFixBatch; ++k) {
+          if (k < cnt) {
+            const Op o = L.prog[pc + k];
+            if ((o.d & 1) && !col_valid(L.cols[o.b], i)) set_null_bit(bitmap, o.a);
+            uint64_t x = v[k];
+            if (o.d & 2) x = x ? 1 : 0;
+            gst64(slots + 8 * o.a, x);
+          }
+        }
+        pc += cnt - 1;
         break;
       }
       case OP_BYTES: {
@@ -1295,11 +1351,11 @@ __global__ __launch_bounds__(kWG) void var_encode_kernel(VarLaunch L, const int6
         break;
       }
       case OP_STRUCT_END: {
-        const int64_t size = wi - st_start[depth];
+        const int64_t sz = wi - st_start[depth];
         const int32_t rel = st_start[depth] - st_start[depth - 1];
         const int32_t ord = st_ord[depth];
         depth--;
-        gst64(row + st_start[depth] + st_hdr[depth] + 8 * ord, ((uint64_t)(uint32_t)rel << 32) | (uint32_t)size);
+        gst64(row + st_start[depth] + st_hdr[depth] + 8 * ord, ((uint64_t)(uint32_t)rel << 32) | (uint32_t)sz);
         break;
       }
       case OP_LIST: {
@@ -1319,21 +1375,32 @@ __global__ __launch_bounds__(kWG) void var_encode_kernel(VarLaunch L, const int6
         gst64(arr, (uint64_t)n);
         for (int b = 8; b < ahdr; b += 8) gst64(arr + b, 0);
         uint8_t* data = arr + ahdr;
-        for (int64_t j = 0; j < n; ++j) {
-          const bool enull = (iflags & 1) && !col_valid(it, e0 + j);
-          uint64_t v = 0;
-          if (enull) arr[8 + (j >> 3)] |= (uint8_t)(1u << (j & 7));
-          else v = load_elem(it.values, w, e0 + j);
-          if (iflags & 2) v = v ? 1 : 0;
-          switch (w) {
-            case 8: gst64(data + 8 * j, v); break;
-            case 4: st32(data + 4 * j, (uint32_t)v); break;
-            case 2: data[2 * j] = (uint8_t)v; data[2 * j + 1] = (uint8_t)(v >> 8); break;
-            default: data[j] = (uint8_t)v; break;
-          }
-        }
         const int64_t dsz = n * w, fixed_part = round8(dsz);
-        for (int64_t k = dsz; k < fixed_part; ++k) data[k] = 0;
+        if (w == 8 && !(iflags & 3)) {  // fromPrimitiveArray fast path: 8-byte elements, no nulls
+          for (int64_t j = 0; j < n; j += 4) {
+            uint64_t x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = j + u < n ? load_elem(it.values, 8, e0 + j + u) : 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (j + u < n) gst64(data + 8 * (j + u), x[u]);
+          }
+        } else {
+          for (int64_t j = 0; j < n; ++j) {
+            const bool enull = (iflags & 1) && !col_valid(it, e0 + j);
+            uint64_t v = 0;
+            if (enull) arr[8 + (j >> 3)] |= (uint8_t)(1u << (j & 7));
+            else v = load_elem(it.values, w, e0 + j);
+            if (iflags & 2) v = v ? 1 : 0;
+            switch (w) {
+              case 8: gst64(data + 8 * j, v); break;
+              case 4: st32(data + 4 * j, (uint32_t)v); break;
+              case 2: data[2 * j] = (uint8_t)v; data[2 * j + 1] = (uint8_t)(v >> 8); break;
+              default: data[j] = (uint8_t)v; break;
+            }
+          }
+          for (int64_t k = dsz; k < fixed_part; ++k) data[k] = 0;
+        }
         wi += ahdr + fixed_part;
         gst64(slot, ((uint64_t)(astart - st_start[depth]) << 32) | (uint32_t)(wi - astart));
         break;
@@ -1342,18 +1409,17 @@ __global__ __launch_bounds__(kWG) void var_encode_kernel(VarLaunch L, const int6
   }
 }
 
-// Decode, pass 1: lengths of every varlen column of record i into
-// out_offsets[i+1] (bytes for STRING/BINARY, elements for LIST).
-// Pass 2 (WRITE=true): values, validity, list items.
+// Decodes record i from `base` (frame or row; `row_len` bytes; LDS image or
+// global). Pass 1 (WRITE = false): lengths of every varlen column into
+// out_offsets[i+1] (bytes for STRING/BINARY, elements for LIST). Pass 2:
+// values, validity, list items. Generated fromRow (RowEncoderBuilder.java:
+// 215-318) over BinaryRow/UnsafeTrait getters (UnsafeTrait.java:68-197).
+// Called by all 64 lanes of a wave whose records are consecutive (ballots).
 template <bool WRITE>
-__global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const uint8_t* __restrict__ in,
-                                                         const int64_t* __restrict__ offs, int32_t* status) {
-  const int64_t i0 = (int64_t)blockIdx.x * kWG + threadIdx.x;
-  const bool live = i0 < L.num_rows;
+__device__ void dec_record(const VarLaunch& L, int64_t i0, bool live, const uint8_t* base, int64_t row_len,
+                           int32_t* status) {
   const int64_t i = live ? i0 : 0;
-  const uint8_t* base = in + offs[i];
   const uint8_t* row = base;
-  int64_t row_len = offs[i + 1] - offs[i];
   bool bad = !live;
   if (live && L.frame) {
     const uint32_t len = ld32(base);
@@ -1368,9 +1434,50 @@ __global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const uint
   st_start[0] = 0;
   st_hdr[0] = L.bitmap_bytes;
   int absent = bad ? 1 << 20 : 0;  // >0: this record's subtree is null/absent
+  const int lane = threadIdx.x & 63;
   for (int pc = 0; pc < L.num_ops; ++pc) {
     const Op op = L.prog[pc];
     const ColumnDev& c = L.cols[op.b];
+    if (WRITE && op.code == OP_FIXED) {  // batch of consecutive fixed fields: reads first, then stores
+      int cnt = 1;
+      while (cnt < kFixBatch && pc + cnt < L.num_ops && L.prog[pc + cnt].code == OP_FIXED) ++cnt;
+      uint64_t v[kFixBatch];
+      bool nul[kFixBatch];
+#pragma unroll
+      for (int k = 0; k < kFixBatch; ++k) {
+        v[k] = 0;
+        nul[k] = true;
+        if (k < cnt && !absent) {
+          const Op o = L.prog[pc + k];
+          const uint8_t* bm = row + st_start[depth];
+          nul[k] = (bm[o.a >> 3] >> (o.a & 7)) & 1;  // BinaryRow.isNullAt
+          if (!nul[k]) v[k] = gld64(row + st_start[depth] + st_hdr[depth] + 8 * o.a);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kFixBatch; ++k) {
+        if (k < cnt) {
+          const Op o = L.prog[pc + k];
+          const ColumnDev& cc = L.cols[o.b];
+          if ((o.d & 1) && cc.out_validity) {
+            const uint64_t m = __ballot(live && !nul[k]);
+            const int64_t w0 = i0 - lane;
+            if (lane == 0 && w0 < L.num_rows) {
+              const int64_t nrow = L.num_rows - w0 < 64 ? L.num_rows - w0 : 64;
+              uint8_t* vb = cc.out_validity + (w0 >> 3);
+              for (int b = 0; b < (int)((nrow + 7) >> 3); ++b) store_byte(vb + b, (uint8_t)(m >> (8 * b)));
+            }
+          }
+          if (live) {
+            uint64_t x = nul[k] ? 0 : v[k];
+            if (o.d & 2) x = (x & 0xff) ? 1 : 0;
+            store_elem(cc.out_values, o.c, i, x);
+          }
+        }
+      }
+      pc += cnt - 1;
+      continue;
+    }
     bool isnull = true;
     const uint8_t* slot = nullptr;
     if (!absent) {
@@ -1381,21 +1488,15 @@ __global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const uint
     // Row-level validity of this column (rows of a wave are consecutive).
     if (WRITE && (op.d & 1) && c.out_validity && op.code != OP_STRUCT_END) {
       const uint64_t m = __ballot(live && !isnull);
-      const int lane = threadIdx.x & 63;
       const int64_t w0 = i0 - lane;
       if (lane == 0 && w0 < L.num_rows) {
         const int64_t nrow = L.num_rows - w0 < 64 ? L.num_rows - w0 : 64;
         uint8_t* vb = c.out_validity + (w0 >> 3);
-        for (int b = 0; b < (int)((nrow + 7) >> 3); ++b) vb[b] = (uint8_t)(m >> (8 * b));
+        for (int b = 0; b < (int)((nrow + 7) >> 3); ++b) store_byte(vb + b, (uint8_t)(m >> (8 * b)));
       }
     }
     switch (op.code) {
-      case OP_FIXED: {
-        if (WRITE && live) {
-          uint64_t v = isnull ? 0 : gld64(slot);
-          if (op.d & 2) v = (v & 0xff) ? 1 : 0;
-          store_elem(c.out_values, op.c, i, v);
-        }
+      case OP_FIXED: {  // pass 1 only (WRITE batches above)
         break;
       }
       case OP_BYTES: {
@@ -1404,15 +1505,11 @@ __global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const uint
           const uint64_t os = gld64(slot);
           rel = (int32_t)(os >> 32);
           n = (int32_t)(uint32_t)os;
-          if (n < 0 || rel < 0 || rel + n > row_len) { set_status(status, FORY_ERR_CORRUPT); n = 0; }
+          if (n < 0 || rel < 0 || st_start[depth] + rel + n > row_len) { set_status(status, FORY_ERR_CORRUPT); n = 0; }
         }
         if (live) {
           if (!WRITE) c.out_offsets[i + 1] = (int32_t)n;
-          else {
-            uint8_t* dst = c.out_values + c.out_offsets[i];
-            const uint8_t* s = row + st_start[depth] + rel;
-            for (int64_t k = 0; k < n; ++k) dst[k] = s[k];
-          }
+          else if (n > 0) copy_out(c.out_values + c.out_offsets[i], row + st_start[depth] + rel, n);
         }
         break;
       }
@@ -1423,6 +1520,11 @@ __global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const uint
         }
         const uint64_t os = gld64(slot);
         const int64_t rel = (int32_t)(os >> 32);
+        if (rel < 0 || st_start[depth] + rel + bitmap_bytes(op.c) + 8LL * op.c > row_len) {
+          set_status(status, FORY_ERR_CORRUPT);
+          absent++;
+          break;
+        }
         depth++;
         st_start[depth] = st_start[depth - 1] + (int32_t)rel;
         st_hdr[depth] = bitmap_bytes(op.c);
@@ -1437,9 +1539,16 @@ __global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const uint
         if (!isnull) {
           const uint64_t os = gld64(slot);
           rel = (int32_t)(os >> 32);
-          n = (int64_t)gld64(row + st_start[depth] + rel);  // BinaryArray.pointTo
-          n = (int32_t)n;
-          if (n < 0 || rel + 8 > row_len) { set_status(status, FORY_ERR_CORRUPT); n = 0; }
+          if (rel < 0 || st_start[depth] + rel + 8 > row_len) {
+            set_status(status, FORY_ERR_CORRUPT);
+          } else {
+            n = (int32_t)(int64_t)gld64(row + st_start[depth] + rel);  // BinaryArray.pointTo
+            const int w = op.e & 0xff;
+            if (n < 0 || st_start[depth] + rel + 8 + bitmap_bytes(n) + n * w > row_len) {
+              set_status(status, FORY_ERR_CORRUPT);
+              n = 0;
+            }
+          }
         }
         if (live) {
           if (!WRITE) {
@@ -1451,26 +1560,41 @@ __global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const uint
             const uint8_t* arr = row + st_start[depth] + rel;
             const int32_t ahdr = 8 + bitmap_bytes(n);
             const int64_t e0 = c.out_offsets[i];
-            for (int64_t j = 0; j < n; ++j) {
-              const bool en = (arr[8 + (j >> 3)] >> (j & 7)) & 1;  // BinaryArray.isNullAt
-              uint64_t v = 0;
-              if (!en) {
-                const uint8_t* p = arr + ahdr + j * w;
-                switch (w) {
-                  case 8: v = gld64(p); break;
-                  case 4: v = ld32(p); break;
-                  case 2: v = (uint64_t)p[0] | ((uint64_t)p[1] << 8); break;
-                  default: v = p[0]; break;
-                }
+            if (w == 8 && !(iflags & 3)) {  // BinaryArray.toLongArray fast path
+              for (int64_t j = 0; j < n; j += 4) {
+                uint64_t x[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) x[u] = j + u < n ? gld64(arr + ahdr + 8 * (j + u)) : 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                  if (j + u < n) {
+                    // BinaryArray null bits still apply for a not-null item field written by a peer
+                    const bool en = (arr[8 + ((j + u) >> 3)] >> ((j + u) & 7)) & 1;
+                    store_elem(it.out_values, 8, e0 + j + u, en ? 0 : x[u]);
+                  }
               }
-              if (iflags & 2) v = (v & 0xff) ? 1 : 0;
-              store_elem(it.out_values, w, e0 + j, v);
-              if ((iflags & 1) && it.out_validity) {
-                const int64_t q = e0 + j;
-                const uint32_t bit = 1u << (q & 31);
-                uint32_t* word = reinterpret_cast<uint32_t*>(it.out_validity) + (q >> 5);
-                if (en) atomicAnd(word, ~bit);
-                else atomicOr(word, bit);
+            } else {
+              for (int64_t j = 0; j < n; ++j) {
+                const bool en = (arr[8 + (j >> 3)] >> (j & 7)) & 1;  // BinaryArray.isNullAt
+                uint64_t v = 0;
+                if (!en) {
+                  const uint8_t* p = arr + ahdr + j * w;
+                  switch (w) {
+                    case 8: v = gld64(p); break;
+                    case 4: v = ld32(p); break;
+                    case 2: v = (uint64_t)p[0] | ((uint64_t)p[1] << 8); break;
+                    default: v = p[0]; break;
+                  }
+                }
+                if (iflags & 2) v = (v & 0xff) ? 1 : 0;
+                store_elem(it.out_values, w, e0 + j, v);
+                if ((iflags & 1) && it.out_validity) {
+                  const int64_t q = e0 + j;
+                  const uint32_t bit = 1u << (q & 31);
+                  uint32_t* word = reinterpret_cast<uint32_t*>(it.out_validity) + (q >> 5);
+                  if (en) atomicAnd(word, ~bit);
+                  else atomicOr(word, bit);
+                }
               }
             }
           }
@@ -1479,6 +1603,140 @@ __global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const uint
       }
     }
   }
+}
+
+// Global-memory interpreters (one lane per record): tiles whose rows exceed
+// the LDS budget, and the FORY_ROWFMT_VARTILE=0 A/B baseline.
+__global__ __launch_bounds__(kWG) void var_encode_kernel(VarLaunch L, const int64_t* __restrict__ offs,
+                                                         uint8_t* __restrict__ out, int64_t capacity,
+                                                         int32_t* status) {
+  const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (i >= L.num_rows) return;
+  const int64_t beg = offs[i], end = offs[i + 1];
+  if (end > capacity || beg < 0 || end < beg) {
+    set_status(status, FORY_ERR_CAPACITY);
+    return;
+  }
+  enc_record(L, i, out + beg, end - beg);
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const uint8_t* __restrict__ in,
+                                                         const int64_t* __restrict__ offs, int32_t* status) {
+  const int64_t i0 = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  const bool live = i0 < L.num_rows;
+  const int64_t i = live ? i0 : 0;
+  dec_record<WRITE>(L, i0, live, in + offs[i], offs[i + 1] - offs[i], status);
+}
+
+// Tile engine: one wave per tile of 64 consecutive records. The tile's bytes
+// [offs[r0], offs[r0+64]) are one contiguous run of the output/input, so the
+// wave assembles (encode) or stages (decode) them in an LDS image placed at
+// the run's 16-byte phase, and HBM sees aligned 16-B stores/loads instead of
+// 64 lanes each touching its own row. Tiles bigger than the LDS budget (or
+// with malformed offsets) fall back to the per-record global interpreter.
+__device__ __forceinline__ bool var_tile_bounds(const int64_t* offs, int64_t n, int64_t r0, int lane, int64_t* B0,
+                                                int64_t* B1, int64_t* beg, int64_t* end, bool* live) {
+  const int rows = n - r0 < 64 ? (int)(n - r0) : 64;
+  *live = lane < rows;
+  *B0 = offs[r0];
+  *B1 = offs[r0 + rows];
+  *beg = *live ? offs[r0 + lane] : *B0;
+  *end = *live ? offs[r0 + lane + 1] : *B0;
+  const bool ok = !*live || (*beg >= *B0 && *end >= *beg && *end <= *B1);
+  return __ballot(!ok) == 0 && ((*B0 | *B1) & 3) == 0 && *B1 >= *B0;
+}
+
+__global__ __launch_bounds__(64) void var_encode_tile_kernel(VarLaunch L, const int64_t* __restrict__ offs,
+                                                             uint8_t* __restrict__ out, int64_t capacity,
+                                                             int32_t* status, int cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  int64_t B0, B1, beg, end;
+  bool live;
+  const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
+  if (live && (end > capacity || beg < 0 || end < beg)) set_status(status, FORY_ERR_CAPACITY);
+  if (__ballot(live && (end > capacity || beg < 0 || end < beg))) return;
+  const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
+  const int64_t total = mis + (B1 - B0);
+  if (!sane || total > cap) {
+    if (live) enc_record(L, r0 + lane, out + beg, end - beg);
+    return;
+  }
+  if (live) enc_record(L, r0 + lane, lds + mis + (beg - B0), end - beg);
+  __syncthreads();
+  uint8_t* g = out + B0 - mis;  // 16-byte aligned
+  const int tot = (int)total;
+  const int nch = (tot + 15) >> 4;
+  for (int c = lane; c < nch; c += 64) {
+    const int lo = c * 16;
+    if (lo >= mis && lo + 16 <= tot) {
+      *gp(reinterpret_cast<u32x4*>(g + lo)) = *reinterpret_cast<const u32x4*>(lds + lo);
+    } else {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int o = lo + 4 * d;
+        if (o >= mis && o + 4 <= tot) *gp(reinterpret_cast<uint32_t*>(g + o)) = ld32(lds + o);
+      }
+    }
+  }
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(64) void var_decode_tile_kernel(VarLaunch L, const uint8_t* __restrict__ in,
+                                                             const int64_t* __restrict__ offs, int32_t* status,
+                                                             int cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  int64_t B0, B1, beg, end;
+  bool live;
+  const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
+  const int mis = (int)(reinterpret_cast<uintptr_t>(in + B0) & 15);
+  const int64_t total = mis + (B1 - B0);
+  if (!sane || total > cap) {
+    dec_record<WRITE>(L, r0 + lane, live, in + beg, end - beg, status);
+    return;
+  }
+  const uint8_t* g = in + B0 - mis;  // 16-byte aligned
+  const int tot = (int)total;
+  const int nch = (tot + 15) >> 4;
+  int c = lane;
+  for (; c + 192 < nch; c += 256) {  // 4 chunks in flight per lane
+    u32x4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int lo = (c + 64 * u) * 16;
+      if (lo >= mis && lo + 16 <= tot) {
+        x[u] = *gp(reinterpret_cast<const u32x4*>(g + lo));
+      } else {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int o = lo + 4 * d;
+          x[u][d] = (o >= mis && o + 4 <= tot) ? *gp(reinterpret_cast<const uint32_t*>(g + o)) : 0u;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) *reinterpret_cast<u32x4*>(lds + (c + 64 * u) * 16) = x[u];
+  }
+  for (; c < nch; c += 64) {
+    const int lo = c * 16;
+    u32x4 x;
+    if (lo >= mis && lo + 16 <= tot) {
+      x = *gp(reinterpret_cast<const u32x4*>(g + lo));
+    } else {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int o = lo + 4 * d;
+        x[d] = (o >= mis && o + 4 <= tot) ? *gp(reinterpret_cast<const uint32_t*>(g + o)) : 0u;
+      }
+    }
+    *reinterpret_cast<u32x4*>(lds + lo) = x;
+  }
+  __syncthreads();
+  dec_record<WRITE>(L, r0 + lane, live, lds + mis + (beg - B0), end - beg, status);
 }
 
 template <typename K>
@@ -1567,15 +1825,15 @@ hipError_t launch_encode_v4(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int R, int WG, int K, bool FRAME, bool PAD>
+template <int R, int WG, int K, bool FRAME, bool PAD, bool ONESHOT = false>
 hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const int64_t full = L.num_rows / R;
   if (full > 0) {
-    auto* k = &encode_fixed_v5_kernel<R, WG, K, FRAME, PAD>;
+    auto* k = &encode_fixed_v5_kernel<R, WG, K, FRAME, PAD, ONESHOT>;
     static bool init = false;
     if (!init) { raise_lds_cap(k); init = true; }
     const size_t lds = (size_t)R * (PAD ? L.pitch : L.stride);
-    const int64_t grid = persistent_grid(k, lds, full, WG);
+    const int64_t grid = ONESHOT ? full : persistent_grid(k, lds, full, WG);
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(WG), lds, s, L, L.fields, out, full);
   }
   if (L.num_rows > full * R) {
@@ -1613,6 +1871,16 @@ hipError_t try_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s, int 
   else if (var == 6 && (i128 + 7) / 8 <= 12) V5(128, 512, 12);
   else if (var == 7 && (i128 + 15) / 16 <= 6) V5(128, 1024, 6);
   else if (var == 8 && (i64 + 7) / 8 <= 6) V5(64, 512, 6);
+  else if (var == 9 && (i64 + 7) / 8 <= 6) {  // one-shot shapes
+    e = launch_encode_v5<64, 512, 6, FRAME, false, true>(P, out, s);
+    *done = true;
+  } else if (var == 10 && (i64 + 3) / 4 <= 12) {
+    e = launch_encode_v5<64, 256, 12, FRAME, false, true>(P, out, s);
+    *done = true;
+  } else if (var == 11 && (i128 + 7) / 8 <= 12) {
+    e = launch_encode_v5<128, 512, 12, FRAME, false, true>(P, out, s);
+    *done = true;
+  }
 #undef V5
   return e;
 }
@@ -1632,7 +1900,7 @@ hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const size_t lds = (size_t)TR * L.stride;
   if constexpr (TR == 64) {
     const int var = variant();
-    if (var >= 5 && var <= 8) {  // v5: depth-2 pipeline (shapes: try_encode_v5)
+    if (var >= 5 && var <= 11) {  // v5: depth-2 pipeline / one-shot (shapes: try_encode_v5)
       bool done = false;
       hipError_t e = try_encode_v5<FRAME>(L, out, s, var, &done);
       if (done || e != hipSuccess) return e;
@@ -1706,7 +1974,7 @@ hipError_t launch_decode_v2(const FixedLaunch& L, const uint8_t* in, int32_t* st
   return hipGetLastError();
 }
 
-int dec_variant() {  // FORY_ROWFMT_DEC: 0 decode_fixed_kernel (default), 1..3 decode v2 shapes
+int dec_variant() {  // FORY_ROWFMT_DEC: 0 decode_fixed_kernel (default), 1..3 decode v2 shapes, 4 TR=32
   const char* e = getenv("FORY_ROWFMT_DEC");
   return e ? atoi(e) : 0;
 }
@@ -1720,6 +1988,14 @@ hipError_t launch_decode_tr(const FixedLaunch& L, const uint8_t* in, int32_t* st
     if (dv == 1 && 64 * L.stride <= 80 * 1024) return launch_decode_v2<64, 512, FRAME>(L, in, status, s);
     if (dv == 2 && 128 * L.stride <= 160 * 1024) return launch_decode_v2<128, 512, FRAME>(L, in, status, s);
     if (dv == 3 && 128 * L.stride <= 160 * 1024) return launch_decode_v2<128, 1024, FRAME>(L, in, status, s);
+    if (dv == 4) {  // 32-record tiles: more workgroups per CU
+      auto* k = &decode_fixed_kernel<32, FRAME>;
+      static bool init32 = false;
+      if (!init32) { raise_lds_cap(k); init32 = true; }
+      hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 31) / 32)), dim3(kWG), (size_t)32 * L.stride, s, L,
+                         L.fields, in, status);
+      return hipGetLastError();
+    }
     constexpr int MAXC = 14;
     if (lds <= (size_t)MAXC * kWG * 16 && variant() == 1) {
       auto* k = &decode_fixed_pipe_kernel<FRAME, MAXC>;
@@ -1823,31 +2099,64 @@ hipError_t launch_var_sizes(const VarLaunch& L, int64_t* d_row_offsets, hipStrea
   return hipGetLastError();
 }
 
+// FORY_ROWFMT_VARTILE=0: per-record global interpreters only (A/B baseline).
+bool var_tiles() {
+  const char* e = getenv("FORY_ROWFMT_VARTILE");
+  return !e || atoi(e) != 0;
+}
+
+int var_cap(const VarLaunch& L) {
+  const char* e = getenv("FORY_ROWFMT_VARCAP");
+  const int cap = e ? atoi(e) : L.tile_cap;
+  return cap < 1024 ? 1024 : (cap > 160 * 1024 ? 160 * 1024 : cap);
+}
+
+template <typename K>
+void var_tile_launch(K* k, const VarLaunch&, int) {
+  static bool init = false;  // one per kernel instantiation
+  if (!init) { raise_lds_cap(k); init = true; }
+}
+
 hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity,
                              int32_t* status, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
+  if (var_tiles()) {
+    const int cap = var_cap(L);
+    var_tile_launch(&var_encode_tile_kernel, L, cap);
+    hipLaunchKernelGGL(var_encode_tile_kernel, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64), (size_t)cap, s,
+                       L, offs, out, capacity, status, cap);
+    return hipGetLastError();
+  }
   const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
   hipLaunchKernelGGL(var_encode_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, offs, out, capacity,
                      status);
   return hipGetLastError();
 }
 
+template <bool WRITE>
+hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int32_t* status,
+                                  hipStream_t s) {
+  if (L.num_rows <= 0) return hipSuccess;
+  if (var_tiles()) {
+    const int cap = var_cap(L);
+    var_tile_launch(&var_decode_tile_kernel<WRITE>, L, cap);
+    hipLaunchKernelGGL(var_decode_tile_kernel<WRITE>, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64),
+                       (size_t)cap, s, L, rows, offs, status, cap);
+    return hipGetLastError();
+  }
+  const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
+  hipLaunchKernelGGL(var_decode_kernel<WRITE>, dim3((unsigned)blocks), dim3(kWG), 0, s, L, rows, offs, status);
+  return hipGetLastError();
+}
+
 hipError_t launch_var_decode_lengths(const VarLaunch& L, const uint8_t* rows, const int64_t* offs,
                                      int32_t* status, hipStream_t s) {
-  if (L.num_rows <= 0) return hipSuccess;
-  const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
-  hipLaunchKernelGGL(var_decode_kernel<false>, dim3((unsigned)blocks), dim3(kWG), 0, s, L, rows, offs,
-                     status);
-  return hipGetLastError();
+  return launch_var_decode_pass<false>(L, rows, offs, status, s);
 }
 
 hipError_t launch_var_decode(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int32_t* status,
                              hipStream_t s) {
-  if (L.num_rows <= 0) return hipSuccess;
-  const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
-  hipLaunchKernelGGL(var_decode_kernel<true>, dim3((unsigned)blocks), dim3(kWG), 0, s, L, rows, offs,
-                     status);
-  return hipGetLastError();
+  return launch_var_decode_pass<true>(L, rows, offs, status, s);
 }
 
 }  // namespace fory_amd

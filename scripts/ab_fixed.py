@@ -28,14 +28,14 @@ for frame in (0, 1):
     dcols = enc.alloc_fixed_outputs(n)
     darr = native.column_array(dcols)
     for rnd in range(rounds):
-        for var in ("8", "8p", "6", "d1", "d2", "d3"):
+        for var in ("8", "9", "10", "11", "6", "d1", "d4"):
             os.environ.pop("FORY_ROWFMT_DEC", None)
             os.environ.pop("FORY_ROWFMT_PAD", None)
             if var.startswith("d"):
                 os.environ["FORY_ROWFMT_DEC"] = var[1]
                 var_env = "8"
             else:
-                var_env = var[0]
+                var_env = var.rstrip("p")
             if var.endswith("p"):
                 os.environ["FORY_ROWFMT_PAD"] = "1"
             os.environ["FORY_ROWFMT_PIPE"] = var_env
@@ -75,7 +75,7 @@ harr = native.column_array(hot)
 out = torch.empty(n * plan.stride(0), dtype=torch.uint8, device="cuda")
 os.environ.pop("FORY_ROWFMT_NOPAD", None)
 os.environ.pop("FORY_ROWFMT_DEC", None)
-for var in ("8", "6"):
+for var in ("8", "9", "10"):
     os.environ["FORY_ROWFMT_PIPE"] = var
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     native.encode(plan, harr, n, 0, None, out, status, ws)
