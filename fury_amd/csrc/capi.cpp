@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -48,7 +49,9 @@ int64_t table_bytes(const Plan& p) {
   // fixed-width: width-ordered table + slab-ordered copy (encode v4)
   if (p.fixed_width) return align_up(2 * (int64_t)p.top.size() * (int64_t)sizeof(FixedFieldDev));
   return align_up((int64_t)p.nodes.size() * (int64_t)sizeof(ColumnDev)) +
-         align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::Op));
+         align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::Op)) +
+         align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::VarFieldDev)) +
+         align_up((int64_t)p.top.size() * (int64_t)sizeof(FixedFieldDev));
 }
 
 bool use_tiled(const Plan& p, int frame) {
@@ -191,7 +194,7 @@ void build_slabs(const Plan& p, const std::vector<FixedFieldDev>& tab, int frame
   L->slab_pitch = pitch;
 }
 
-// LDS budget of one 64-record tile image for the varlen tile engine: 1.25x an
+// LDS budget of one 64-record tile image for the varlen tile engine: 1.125x an
 // estimated row (fixed part, nested struct rows, ~24 bytes per string,
 // ~4 elements per list), in [8, 64] KiB. Tiles above it take the per-record
 // global path (correct, slower); FORY_ROWFMT_VARCAP overrides.
@@ -204,7 +207,7 @@ int var_tile_cap(const Plan& p, int frame) {
     else if (nd.kind == fory_amd::KIND_STRUCT)  // child rows live in the variable region
       est += ((int64_t)(nd.children.size() + 63) / 64) * 8 + 8 * (int64_t)nd.children.size();
   }
-  int64_t cap = (64 * est * 5 / 4 + 1023) / 1024 * 1024;
+  int64_t cap = (64 * est * 9 / 8 + 1023) / 1024 * 1024;
   return (int)std::min<int64_t>(std::max<int64_t>(cap, 8 * 1024), 64 * 1024);
 }
 
@@ -215,11 +218,80 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   int rc = bind_var(p, cols, n, &cd);
   if (rc) return rc;
   const int64_t col_bytes = align_up((int64_t)cd.size() * (int64_t)sizeof(ColumnDev));
+  const int64_t prog_bytes = align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::Op));
+  const int64_t idx_bytes = align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::VarFieldDev));
+  // flat plans: var-field descriptors (field order) and the width-sorted fixed-field table
+  std::vector<fory_amd::VarFieldDev> var;
+  std::vector<FixedFieldDev> fix;
+  bool flat = true;
+  for (size_t k = 0; k < p.program.size(); ++k) {
+    const fory_amd::Op& op = p.program[k];
+    if (op.code == fory_amd::OP_FIXED) {
+      const fory_column& c = cols[op.b];
+      FixedFieldDev f{};
+      f.values = static_cast<const uint8_t*>(c.values);
+      f.out_values = static_cast<uint8_t*>(c.values);
+      f.validity = (op.d & 1) ? c.validity : nullptr;
+      f.out_validity = (op.d & 1) ? c.validity : nullptr;
+      f.width = op.c;
+      f.flags = op.d;
+      f.slot = op.a;
+      fix.push_back(f);
+    } else if (op.code == fory_amd::OP_BYTES || op.code == fory_amd::OP_LIST) {
+      const fory_column& c = cols[op.b];
+      fory_amd::VarFieldDev v{};
+      v.offsets = c.offsets;
+      v.out_offsets = c.offsets;
+      v.validity = (op.d & 1) ? c.validity : nullptr;
+      v.out_validity = (op.d & 1) ? c.validity : nullptr;
+      v.slot = op.a;
+      v.flags = op.d;
+      if (op.code == fory_amd::OP_LIST) {
+        const fory_column& it = cols[op.c];
+        v.is_list = 1;
+        v.w = op.e & 0xff;
+        v.iflags = op.e >> 8;
+        v.values = static_cast<const uint8_t*>(it.values);
+        v.out_values = static_cast<uint8_t*>(it.values);
+        v.item_validity = (v.iflags & 1) ? it.validity : nullptr;
+        v.out_item_validity = (v.iflags & 1) ? it.validity : nullptr;
+      } else {
+        v.w = 1;
+        v.values = static_cast<const uint8_t*>(c.values);
+        v.out_values = static_cast<uint8_t*>(c.values);
+      }
+      var.push_back(v);
+    } else {
+      flat = false;
+    }
+  }
+  std::stable_sort(fix.begin(), fix.end(),
+                   [](const FixedFieldDev& a, const FixedFieldDev& b) { return a.width > b.width; });
   std::vector<uint8_t> host((size_t)table_bytes(p), 0);
   std::memcpy(host.data(), cd.data(), cd.size() * sizeof(ColumnDev));
   std::memcpy(host.data() + col_bytes, p.program.data(), p.program.size() * sizeof(fory_amd::Op));
+  std::memcpy(host.data() + col_bytes + prog_bytes, var.data(), var.size() * sizeof(fory_amd::VarFieldDev));
+  std::memcpy(host.data() + col_bytes + prog_bytes + idx_bytes, fix.data(), fix.size() * sizeof(FixedFieldDev));
   rc = upload(ws, host.data(), (int64_t)host.size(), s);
   if (rc) return rc;
+  uint8_t* wsb = static_cast<uint8_t*>(ws);
+  L->flat = flat && var.size() <= 32 ? 1 : 0;
+  L->num_var = (int32_t)var.size();
+  L->vf = reinterpret_cast<const fory_amd::VarFieldDev*>(wsb + col_bytes + prog_bytes);
+  L->fix = reinterpret_cast<const FixedFieldDev*>(wsb + col_bytes + prog_bytes + idx_bytes);
+  {
+    const int widths[4] = {8, 4, 2, 1};
+    int at = 0;
+    for (int g = 0; g < 4; ++g) {
+      L->fix_group[g] = at;
+      for (const FixedFieldDev& f : fix)
+        if (f.width == widths[g]) ++at;
+    }
+    L->fix_group[4] = at;
+  }
+  L->prof = fory_amd::var_prof_buffer((n + 63) / 64);
+  const char* stg = getenv("FORY_ROWFMT_VARSTG");
+  L->stg_bytes = stg ? std::max(256, std::min(16384, atoi(stg))) & ~15 : 2048;
   L->cols = static_cast<const ColumnDev*>(ws);
   L->prog = reinterpret_cast<const fory_amd::Op*>(static_cast<uint8_t*>(ws) + col_bytes);
   L->num_ops = (int32_t)p.program.size();
@@ -242,6 +314,12 @@ int64_t* partials_ptr(const Plan& p, void* ws) {
 extern "C" {
 
 int32_t fory_rowfmt_abi_version(void) { return FORY_ROWFMT_ABI_VERSION; }
+
+// Debug only (not in the public header): copies the flat-kernel phase timeline
+// recorded under FORY_ROWFMT_VARPROF=1 (8 s_memrealtime stamps per tile).
+int64_t fory_rowfmt_debug_timeline(uint64_t* host, int64_t max_words) {
+  return fory_amd::var_prof_copy(host, max_words);
+}
 
 const char* fory_rowfmt_last_error(void) { return g_err.c_str(); }
 

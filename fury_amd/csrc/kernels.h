@@ -52,6 +52,15 @@ struct VarLaunch {
   int64_t num_rows;
   int32_t frame;
   int32_t tile_cap;             // LDS bytes per 64-record tile image (tile engine)
+  // Flat plans (every top-level field FIXED/BOOL, STRING/BINARY or LIST<fixed>;
+  // the program is one op per field): cooperative tile kernels.
+  int32_t flat;
+  int32_t num_var;              // top-level OP_BYTES / OP_LIST ops, field order
+  int32_t stg_bytes;            // LDS staging per wave for one field's span
+  int32_t fix_group[5];         // width groups [8][4][2][1] of `fix`
+  const FixedFieldDev* fix;     // device: top-level fixed fields, width-sorted
+  const VarFieldDev* vf;        // device: top-level var fields, field order
+  uint64_t* prof;               // debug (FORY_ROWFMT_VARPROF): 8 timestamps per tile, else null
 };
 
 // sizes -> d_row_offsets[0..n-1] (row/frame byte sizes), then exclusive scan.
@@ -68,6 +77,10 @@ hipError_t launch_var_decode(const VarLaunch& L, const uint8_t* rows,
 // Exclusive scan of n int64 values in place; data[n] receives the total.
 // partials: >= scan_partials(n) int64 of workspace.
 int64_t scan_partials(int64_t n);
+
+// Debug timeline buffer for the flat tile kernels (FORY_ROWFMT_VARPROF=1).
+uint64_t* var_prof_buffer(int64_t tiles);
+int64_t var_prof_copy(uint64_t* host, int64_t max_words);
 hipError_t launch_scan_i64(int64_t* data, int64_t n, int64_t* partials, hipStream_t s);
 // Arrow offsets: offs[1..n] hold lengths; writes offs[0]=0 and inclusive
 // prefix into offs[1..n] (int32). Overflow past INT32_MAX sets *status.

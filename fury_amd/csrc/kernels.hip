@@ -1228,14 +1228,14 @@ __device__ __forceinline__ void copy_out(uint8_t* dst, const uint8_t* src, int64
 }
 
 // Row/frame size of record i (BinaryRowWriter.reset + all appends).
-__global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, int64_t* sizes) {
+__global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, int64_t* sizes) {
   const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
   if (i >= L.num_rows) return;
   int64_t size = L.fixed_size + (L.frame ? 12 : 0);
   int absent_depth = 0;  // >0: inside a null struct
   for (int pc = 0; pc < L.num_ops; ++pc) {
-    const Op op = L.prog[pc];
-    const ColumnDev& c = L.cols[op.b];
+    const Op op = prog[pc];
+    const ColumnDev& c = cols[op.b];
     switch (op.code) {
       case OP_FIXED:
         break;
@@ -1267,7 +1267,7 @@ constexpr int kFixBatch = 8;  // consecutive OP_FIXED ops whose loads are issued
 // `size` bytes; an LDS tile image or global memory). Generated toRow
 // (RowEncoderBuilder.java:177-208) with BaseBinaryEncoderBuilder's per-type
 // branches (:149-490) as an op program.
-__device__ void enc_record(const VarLaunch& L, int64_t i, uint8_t* base, int64_t size) {
+__device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, int64_t i, uint8_t* base, int64_t size) {
   uint8_t* row = base;
   if (L.frame) {  // Encoders.encode(MemoryBuffer,T): [i32 8+rowSize][i64 hash]
     st32(base, (uint32_t)(size - 4));
@@ -1284,8 +1284,8 @@ __device__ void enc_record(const VarLaunch& L, int64_t i, uint8_t* base, int64_t
   int64_t wi = L.fixed_size;  // writerIndex relative to row (BinaryRowWriter.reset)
   for (int b = 0; b < L.bitmap_bytes; b += 8) gst64(row + b, 0);
   for (int pc = 0; pc < L.num_ops; ++pc) {
-    const Op op = L.prog[pc];
-    const ColumnDev& c = L.cols[op.b];
+    const Op op = prog[pc];
+    const ColumnDev& c = cols[op.b];
     if (absent) {
       if (op.code == OP_STRUCT_BEGIN) absent++;
       else if (op.code == OP_STRUCT_END) absent--;
@@ -1298,22 +1298,22 @@ __device__ void enc_record(const VarLaunch& L, int64_t i, uint8_t* base, int64_t
     switch (op.code) {
       case OP_FIXED: {  // BinaryRowWriter.write(ordinal, v) / setNullAt, batched
         int cnt = 1;
-        while (cnt < kFixBatch && pc + cnt < L.num_ops && L.prog[pc + cnt].code == OP_FIXED) ++cnt;
+        while (cnt < kFixBatch && pc + cnt < L.num_ops && prog[pc + cnt].code == OP_FIXED) ++cnt;
         uint64_t v[kFixBatch];
 #pragma unroll
         for (int k = 0; k < kFixBatch; ++k) {
           v[k] = 0;
           if (k < cnt) {
-            const Op o = L.prog[pc + k];
-            const ColumnDev& cc = L.cols[o.b];
+            const Op o = prog[pc + k];
+            const ColumnDev& cc = cols[o.b];
             if (!(o.d & 1) || col_valid(cc, i)) v[k] = load_elem(cc.values, o.c, i);
           }
         }
 #pragma unroll
         for (int k = 0; k < kFixBatch; ++k) {
           if (k < cnt) {
-            const Op o = L.prog[pc + k];
-            if ((o.d & 1) && !col_valid(L.cols[o.b], i)) set_null_bit(bitmap, o.a);
+            const Op o = prog[pc + k];
+            if ((o.d & 1) && !col_valid(cols[o.b], i)) set_null_bit(bitmap, o.a);
             uint64_t x = v[k];
             if (o.d & 2) x = x ? 1 : 0;
             gst64(slots + 8 * o.a, x);
@@ -1365,7 +1365,7 @@ __device__ void enc_record(const VarLaunch& L, int64_t i, uint8_t* base, int64_t
           break;
         }
         // BinaryArrayWriter.reset(n) + per-element write (BinaryArrayWriter.java:93-158)
-        const ColumnDev& it = L.cols[op.c];
+        const ColumnDev& it = cols[op.c];
         const int w = op.e & 0xff;
         const int iflags = op.e >> 8;
         const int64_t e0 = c.offsets[i], n = (int64_t)c.offsets[i + 1] - e0;
@@ -1416,7 +1416,7 @@ __device__ void enc_record(const VarLaunch& L, int64_t i, uint8_t* base, int64_t
 // 215-318) over BinaryRow/UnsafeTrait getters (UnsafeTrait.java:68-197).
 // Called by all 64 lanes of a wave whose records are consecutive (ballots).
 template <bool WRITE>
-__device__ void dec_record(const VarLaunch& L, int64_t i0, bool live, const uint8_t* base, int64_t row_len,
+__device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, int64_t i0, bool live, const uint8_t* base, int64_t row_len,
                            int32_t* status) {
   const int64_t i = live ? i0 : 0;
   const uint8_t* row = base;
@@ -1436,11 +1436,11 @@ __device__ void dec_record(const VarLaunch& L, int64_t i0, bool live, const uint
   int absent = bad ? 1 << 20 : 0;  // >0: this record's subtree is null/absent
   const int lane = threadIdx.x & 63;
   for (int pc = 0; pc < L.num_ops; ++pc) {
-    const Op op = L.prog[pc];
-    const ColumnDev& c = L.cols[op.b];
+    const Op op = prog[pc];
+    const ColumnDev& c = cols[op.b];
     if (WRITE && op.code == OP_FIXED) {  // batch of consecutive fixed fields: reads first, then stores
       int cnt = 1;
-      while (cnt < kFixBatch && pc + cnt < L.num_ops && L.prog[pc + cnt].code == OP_FIXED) ++cnt;
+      while (cnt < kFixBatch && pc + cnt < L.num_ops && prog[pc + cnt].code == OP_FIXED) ++cnt;
       uint64_t v[kFixBatch];
       bool nul[kFixBatch];
 #pragma unroll
@@ -1448,7 +1448,7 @@ __device__ void dec_record(const VarLaunch& L, int64_t i0, bool live, const uint
         v[k] = 0;
         nul[k] = true;
         if (k < cnt && !absent) {
-          const Op o = L.prog[pc + k];
+          const Op o = prog[pc + k];
           const uint8_t* bm = row + st_start[depth];
           nul[k] = (bm[o.a >> 3] >> (o.a & 7)) & 1;  // BinaryRow.isNullAt
           if (!nul[k]) v[k] = gld64(row + st_start[depth] + st_hdr[depth] + 8 * o.a);
@@ -1457,8 +1457,8 @@ __device__ void dec_record(const VarLaunch& L, int64_t i0, bool live, const uint
 #pragma unroll
       for (int k = 0; k < kFixBatch; ++k) {
         if (k < cnt) {
-          const Op o = L.prog[pc + k];
-          const ColumnDev& cc = L.cols[o.b];
+          const Op o = prog[pc + k];
+          const ColumnDev& cc = cols[o.b];
           if ((o.d & 1) && cc.out_validity) {
             const uint64_t m = __ballot(live && !nul[k]);
             const int64_t w0 = i0 - lane;
@@ -1554,7 +1554,7 @@ __device__ void dec_record(const VarLaunch& L, int64_t i0, bool live, const uint
           if (!WRITE) {
             c.out_offsets[i + 1] = (int32_t)n;
           } else if (n > 0) {
-            const ColumnDev& it = L.cols[op.c];
+            const ColumnDev& it = cols[op.c];
             const int w = op.e & 0xff;
             const int iflags = op.e >> 8;
             const uint8_t* arr = row + st_start[depth] + rel;
@@ -1607,7 +1607,7 @@ __device__ void dec_record(const VarLaunch& L, int64_t i0, bool live, const uint
 
 // Global-memory interpreters (one lane per record): tiles whose rows exceed
 // the LDS budget, and the FORY_ROWFMT_VARTILE=0 A/B baseline.
-__global__ __launch_bounds__(kWG) void var_encode_kernel(VarLaunch L, const int64_t* __restrict__ offs,
+__global__ __launch_bounds__(kWG) void var_encode_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, const int64_t* __restrict__ offs,
                                                          uint8_t* __restrict__ out, int64_t capacity,
                                                          int32_t* status) {
   const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
@@ -1617,16 +1617,16 @@ __global__ __launch_bounds__(kWG) void var_encode_kernel(VarLaunch L, const int6
     set_status(status, FORY_ERR_CAPACITY);
     return;
   }
-  enc_record(L, i, out + beg, end - beg);
+  enc_record(L, prog, cols, i, out + beg, end - beg);
 }
 
 template <bool WRITE>
-__global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const uint8_t* __restrict__ in,
+__global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, const uint8_t* __restrict__ in,
                                                          const int64_t* __restrict__ offs, int32_t* status) {
   const int64_t i0 = (int64_t)blockIdx.x * kWG + threadIdx.x;
   const bool live = i0 < L.num_rows;
   const int64_t i = live ? i0 : 0;
-  dec_record<WRITE>(L, i0, live, in + offs[i], offs[i + 1] - offs[i], status);
+  dec_record<WRITE>(L, prog, cols, i0, live, in + offs[i], offs[i + 1] - offs[i], status);
 }
 
 // Tile engine: one wave per tile of 64 consecutive records. The tile's bytes
@@ -1647,7 +1647,7 @@ __device__ __forceinline__ bool var_tile_bounds(const int64_t* offs, int64_t n, 
   return __ballot(!ok) == 0 && ((*B0 | *B1) & 3) == 0 && *B1 >= *B0;
 }
 
-__global__ __launch_bounds__(64) void var_encode_tile_kernel(VarLaunch L, const int64_t* __restrict__ offs,
+__global__ __launch_bounds__(64) void var_encode_tile_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, const int64_t* __restrict__ offs,
                                                              uint8_t* __restrict__ out, int64_t capacity,
                                                              int32_t* status, int cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1660,11 +1660,11 @@ __global__ __launch_bounds__(64) void var_encode_tile_kernel(VarLaunch L, const 
   if (__ballot(live && (end > capacity || beg < 0 || end < beg))) return;
   const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
   const int64_t total = mis + (B1 - B0);
-  if (!sane || total > cap) {
-    if (live) enc_record(L, r0 + lane, out + beg, end - beg);
+  if (!sane || (mis & 3) || total > cap) {
+    if (live) enc_record(L, prog, cols, r0 + lane, out + beg, end - beg);
     return;
   }
-  if (live) enc_record(L, r0 + lane, lds + mis + (beg - B0), end - beg);
+  if (live) enc_record(L, prog, cols, r0 + lane, lds + mis + (beg - B0), end - beg);
   __syncthreads();
   uint8_t* g = out + B0 - mis;  // 16-byte aligned
   const int tot = (int)total;
@@ -1684,7 +1684,7 @@ __global__ __launch_bounds__(64) void var_encode_tile_kernel(VarLaunch L, const 
 }
 
 template <bool WRITE>
-__global__ __launch_bounds__(64) void var_decode_tile_kernel(VarLaunch L, const uint8_t* __restrict__ in,
+__global__ __launch_bounds__(64) void var_decode_tile_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, const uint8_t* __restrict__ in,
                                                              const int64_t* __restrict__ offs, int32_t* status,
                                                              int cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1695,8 +1695,8 @@ __global__ __launch_bounds__(64) void var_decode_tile_kernel(VarLaunch L, const 
   const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
   const int mis = (int)(reinterpret_cast<uintptr_t>(in + B0) & 15);
   const int64_t total = mis + (B1 - B0);
-  if (!sane || total > cap) {
-    dec_record<WRITE>(L, r0 + lane, live, in + beg, end - beg, status);
+  if (!sane || (mis & 3) || total > cap) {
+    dec_record<WRITE>(L, prog, cols, r0 + lane, live, in + beg, end - beg, status);
     return;
   }
   const uint8_t* g = in + B0 - mis;  // 16-byte aligned
@@ -1736,7 +1736,502 @@ __global__ __launch_bounds__(64) void var_decode_tile_kernel(VarLaunch L, const 
     *reinterpret_cast<u32x4*>(lds + lo) = x;
   }
   __syncthreads();
-  dec_record<WRITE>(L, r0 + lane, live, lds + mis + (beg - B0), end - beg, status);
+  dec_record<WRITE>(L, prog, cols, r0 + lane, live, lds + mis + (beg - B0), end - beg, status);
+}
+
+// ---------------------------------------------------------------------------
+// Flat varlen tile kernels: every top-level field FIXED/BOOL, STRING/BINARY or
+// LIST<fixed> (VarLaunch::flat). One workgroup of NW (4 or 8) waves per 64-record
+// tile; lane = record within each wave.
+//   encode: wave 0 writes headers, null bitmaps and the variable-region layout
+//   (slot words; payload offsets into LDS `pos`) while all waves fill fixed
+//   slots with batched column loads; then each wave takes whole var fields:
+//   the tile's span of a string/list column is contiguous in its Arrow
+//   buffer, so the wave loads it coalesced into an LDS staging buffer and
+//   every lane copies its record's bytes LDS -> LDS; finally the row image
+//   leaves as aligned 16-B stores.
+//   decode: the mirror image (coalesced row staging in, per-field output
+//   spans staged in LDS and stored coalesced).
+// Spans larger than the staging buffer, bool/nullable list items and tiles
+// bigger than the LDS image take per-lane paths with the same results.
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ void wave_lds_sync() {
+  // LDS ops of one wave execute in order; keep the compiler from reordering.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// LDS -> LDS copy of n bytes (src any alignment, dst 4-byte aligned), zero
+// padded to round8(n). Reads up to 4 bytes past the source span (staging slack).
+__device__ __forceinline__ void lds_copy_padded(uint8_t* dst, const uint8_t* src, int64_t n) {
+  const int sb = (int)(reinterpret_cast<uintptr_t>(src) & 3);
+  const uint8_t* s0 = src - sb;
+  const int64_t n4 = (n + 3) & ~int64_t(3);
+  for (int64_t k = 0; k < n4; k += 4) {
+    const uint32_t a = ld32(s0 + k);
+    uint32_t w = a;
+    if (sb) w = (a >> (8 * sb)) | (ld32(s0 + k + 4) << (32 - 8 * sb));
+    if (n - k < 4) w &= (1u << (8 * (n - k))) - 1u;
+    st32(dst + k, w);
+  }
+  if (round8(n) > n4) st32(dst + n4, 0);
+}
+
+__device__ __forceinline__ void st64_lds(uint8_t* p, uint64_t v) {  // 4-byte aligned LDS
+  st32(p, (uint32_t)v);
+  st32(p + 4, (uint32_t)(v >> 32));
+}
+
+__device__ __forceinline__ void write_validity64(uint8_t* validity, int64_t r0, int rows, uint64_t m) {
+  for (int b = 0; b < (rows + 7) >> 3; ++b) store_byte(validity + (r0 >> 3) + b, (uint8_t)(m >> (8 * b)));
+}
+
+// Fixed fields of width W (one width group of L.fix): column -> slot, batches of
+// kFixBatch loads per wave issued together (branch-free: clamped field index,
+// row 0 for idle lanes, nulls selected to 0 afterwards).
+template <int W, int NW>
+__device__ __forceinline__ void flat_enc_fixed(const FixedFieldDev* __restrict__ fix, int g0, int g1, int wave, bool live, int64_t i,
+                                               uint8_t* slots) {
+  const int64_t ii = live ? i : 0;
+  for (int k0 = g0 + wave * kFixBatch; k0 < g1; k0 += NW * kFixBatch) {
+    uint64_t v[kFixBatch];
+    uint32_t vb[kFixBatch];
+#pragma unroll
+    for (int k = 0; k < kFixBatch; ++k) {
+      const FixedFieldDev& f = fix[min(k0 + k, g1 - 1)];
+      v[k] = ldw<W>(f.values, ii);
+      vb[k] = f.validity ? load_byte(f.validity + (ii >> 3)) : 0xffu;
+    }
+#pragma unroll
+    for (int k = 0; k < kFixBatch; ++k) {
+      if (k0 + k < g1 && live) {
+        const FixedFieldDev& f = fix[k0 + k];
+        uint64_t x = ((vb[k] >> (ii & 7)) & 1) ? v[k] : 0;
+        if (f.flags & 2) x = x ? 1 : 0;
+        st64_lds(slots + 8 * f.slot, x);
+      }
+    }
+  }
+}
+
+// Loads the tile's span of var field f (string bytes or list items) into the
+// wave's staging buffer; returns false when it must take the per-lane path.
+__device__ __forceinline__ bool flat_stage(const VarFieldDev& f, int stg_bytes, int64_t r0, int rows, int lane,
+                                           uint8_t* stg, int* phase_out, int64_t* s0_out) {
+  const int64_t s0 = f.offsets[r0], s1 = f.offsets[r0 + rows];
+  const int64_t S = (s1 - s0) * f.w;
+  *s0_out = s0;
+  if ((f.iflags & 3) != 0 || S < 0 || S + 32 > stg_bytes) return false;
+  const uint8_t* gsrc = f.values + s0 * f.w;
+  const int phase = (int)(reinterpret_cast<uintptr_t>(gsrc) & 15);
+  *phase_out = phase;
+  const uint8_t* ga = gsrc - phase;
+  const int nch = (int)((phase + S + 15) >> 4);
+  for (int cc = lane; cc < nch; cc += 64)
+    *reinterpret_cast<u32x4*>(stg + cc * 16) = *gp(reinterpret_cast<const u32x4*>(ga + cc * 16));
+  return true;
+}
+
+// Copies record i's payload of var field f into its row image (staged: from
+// LDS; else per lane from global, incl. item null bits and bool items).
+__device__ __forceinline__ void flat_place(const VarFieldDev& f, bool staged, const uint8_t* stg, int phase,
+                                           int64_t s0, int p, bool live, int64_t i, uint8_t* row) {
+  if (!live || p < 0) return;
+  const int w = f.w;
+  const int64_t e0 = f.offsets[i], n = (int64_t)f.offsets[i + 1] - e0;
+  uint8_t* dst = row + p + (f.is_list ? 8 + bitmap_bytes(n) : 0);
+  if (staged) {
+    lds_copy_padded(dst, stg + phase + (e0 - s0) * w, n * w);
+  } else if (!f.is_list) {
+    copy_padded(dst, f.values + e0, n);
+  } else {
+    uint8_t* arr = row + p;
+    for (int64_t j = 0; j < n; ++j) {
+      const bool enull = f.item_validity && !((f.item_validity[(e0 + j) >> 3] >> ((e0 + j) & 7)) & 1);
+      uint64_t x = 0;
+      if (enull) arr[8 + (j >> 3)] |= (uint8_t)(1u << (j & 7));
+      else x = load_elem(f.values, w, e0 + j);
+      if (f.iflags & 2) x = x ? 1 : 0;
+      switch (w) {
+        case 8: st64_lds(dst + 8 * j, x); break;
+        case 4: st32(dst + 4 * j, (uint32_t)x); break;
+        case 2: dst[2 * j] = (uint8_t)x; dst[2 * j + 1] = (uint8_t)(x >> 8); break;
+        default: dst[j] = (uint8_t)x; break;
+      }
+    }
+    for (int64_t k = n * w; k < round8(n * w); ++k) dst[k] = 0;
+  }
+}
+
+// PROF: thread 0 stamps s_memrealtime (100 MHz) at phase boundaries into
+// L.prof[tile * 8 + k] (debug timeline, FORY_ROWFMT_VARPROF=1).
+#define FLAT_STAMP(k)                                                                            \
+  do {                                                                                          \
+    if (PROF && tid == 0) L.prof[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
+
+template <bool FRAME, int NW, bool PROF = false>
+__global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
+                                                                  const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
+                                                                  const int64_t* __restrict__ offs,
+                                                                  uint8_t* __restrict__ out, int64_t capacity,
+                                                                  int32_t* status, int cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int HDR = FRAME ? 12 : 0;
+  const int stg_bytes = L.stg_bytes;
+  uint8_t* img = lds;
+  int32_t* pos = reinterpret_cast<int32_t*>(lds + cap + NW * stg_bytes);  // [num_var][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  FLAT_STAMP(0);
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  int64_t B0, B1, beg, end;
+  bool live;
+  const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
+  const bool capbad = live && (end > capacity || beg < 0 || end < beg);
+  if (__ballot(capbad)) {
+    if (wave == 0 && capbad) set_status(status, FORY_ERR_CAPACITY);
+    return;
+  }
+  const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
+  const int64_t total = mis + (B1 - B0);
+  if (!sane || (mis & 3) || total > cap) {
+    if (wave == 0 && live) enc_record(L, prog, cols, r0 + lane, out + beg, end - beg);
+    return;
+  }
+  const int64_t i = r0 + lane;
+  const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
+  uint8_t* fp = img + mis + (int)(beg - B0);
+  uint8_t* row = fp + HDR;
+  uint8_t* slots = row + L.bitmap_bytes;
+  // this wave's first var field: span loads in flight across the layout phase
+  uint8_t* stg = lds + cap + wave * stg_bytes;
+  int phase = 0;
+  int64_t s0 = 0;
+  bool staged = false;
+  if (wave < L.num_var) staged = flat_stage(vf[wave], stg_bytes, r0, rows, lane, stg, &phase, &s0);
+  FLAT_STAMP(1);
+  if (wave == 0) {
+    // Encoders.encode frame header; BinaryRowWriter.reset zeroes the bitmap (BinaryRowWriter.java:76-84)
+    if (live) {
+      if (FRAME) {
+        st32(fp, (uint32_t)(end - beg - 4));
+        st64_lds(fp + 4, (uint64_t)L.schema_hash);
+      }
+      for (int b = 0; b < L.bitmap_bytes; b += 4) st32(row + b, 0);
+    }
+    // null bits of nullable fixed fields (this wave only: no bitmap races)
+    const int nfix = L.fix_group[4];
+    for (int k0 = 0; k0 < nfix; k0 += kFixBatch) {
+      uint32_t vb[kFixBatch];
+      const int64_t ii = live ? i : 0;
+#pragma unroll
+      for (int k = 0; k < kFixBatch; ++k) {
+        const FixedFieldDev& f = fix[min(k0 + k, nfix - 1)];
+        vb[k] = f.validity ? load_byte(f.validity + (ii >> 3)) : 0xffu;
+      }
+#pragma unroll
+      for (int k = 0; k < kFixBatch; ++k)
+        if (k0 + k < nfix && live && !((vb[k] >> (ii & 7)) & 1)) set_null_bit(row, fix[k0 + k].slot);
+    }
+    // variable-region layout in field order (writeUnaligned / BinaryArrayWriter.reset)
+    int64_t wi = L.fixed_size;
+    for (int v0 = 0; v0 < L.num_var; v0 += kFixBatch) {
+      int64_t e0[kFixBatch], e1[kFixBatch];
+      uint32_t vb[kFixBatch];
+      const int64_t ii = live ? i : 0;
+#pragma unroll
+      for (int k = 0; k < kFixBatch; ++k) {
+        const VarFieldDev& f = vf[min(v0 + k, L.num_var - 1)];
+        e0[k] = f.offsets[ii];
+        e1[k] = f.offsets[ii + 1];
+        vb[k] = f.validity ? load_byte(f.validity + (ii >> 3)) : 0xffu;
+      }
+#pragma unroll
+      for (int k = 0; k < kFixBatch; ++k) {
+        if (v0 + k >= L.num_var) break;
+        const VarFieldDev& f = vf[v0 + k];
+        int32_t p = -1;
+        if (live) {
+          uint8_t* slot = slots + 8 * f.slot;
+          const int64_t nn = e1[k] - e0[k];
+          if (!((vb[k] >> (ii & 7)) & 1)) {
+            set_null_bit(row, f.slot);
+            st64_lds(slot, 0);
+          } else if (!f.is_list) {
+            st64_lds(slot, ((uint64_t)wi << 32) | (uint32_t)nn);
+            p = (int32_t)wi;
+            wi += round8(nn);
+          } else {  // LIST: [i64 n][null bitmap][n * w bytes, padded to 8]
+            const int32_t ahdr = 8 + bitmap_bytes(nn);
+            const int64_t size = ahdr + round8(nn * f.w);
+            st64_lds(row + wi, (uint64_t)nn);
+            for (int b = 8; b < ahdr; b += 4) st32(row + wi + b, 0);
+            st64_lds(slot, ((uint64_t)wi << 32) | (uint32_t)size);
+            p = (int32_t)wi;
+            wi += size;
+          }
+        }
+        pos[(v0 + k) * 64 + lane] = p;
+      }
+    }
+  }
+  FLAT_STAMP(2);
+  // fixed slots (all waves): BinaryRowWriter.write(ordinal, v), null -> 0
+  flat_enc_fixed<8, NW>(fix, L.fix_group[0], L.fix_group[1], wave, live, i, slots);
+  flat_enc_fixed<4, NW>(fix, L.fix_group[1], L.fix_group[2], wave, live, i, slots);
+  flat_enc_fixed<2, NW>(fix, L.fix_group[2], L.fix_group[3], wave, live, i, slots);
+  flat_enc_fixed<1, NW>(fix, L.fix_group[3], L.fix_group[4], wave, live, i, slots);
+  if (PROF) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  FLAT_STAMP(3);
+  __syncthreads();
+  FLAT_STAMP(4);
+  // variable payloads: one field per wave at a time (the first one already staged)
+  for (int v = wave; v < L.num_var; v += NW) {
+    if (v != wave) {
+      wave_lds_sync();  // staging reused
+      staged = flat_stage(vf[v], stg_bytes, r0, rows, lane, stg, &phase, &s0);
+    }
+    wave_lds_sync();
+    flat_place(vf[v], staged, stg, phase, s0, pos[v * 64 + lane], live, i, row);
+  }
+  if (PROF) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  FLAT_STAMP(5);
+  __syncthreads();
+  FLAT_STAMP(6);
+  uint8_t* g = out + B0 - mis;  // 16-byte aligned
+  const int tot = (int)total;
+  const int nch = (tot + 15) >> 4;
+  for (int cc = tid; cc < nch; cc += 64 * NW) {
+    const int lo = cc * 16;
+    if (lo >= mis && lo + 16 <= tot) {
+      *gp(reinterpret_cast<u32x4*>(g + lo)) = *reinterpret_cast<const u32x4*>(img + lo);
+    } else {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int o = lo + 4 * d;
+        if (o >= mis && o + 4 <= tot) *gp(reinterpret_cast<uint32_t*>(g + o)) = ld32(img + o);
+      }
+    }
+  }
+  if (PROF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  FLAT_STAMP(7);
+}
+
+// Reads a var field's slot of a staged record: returns payload (rel, n) with
+// n = bytes (STRING/BINARY) or elements (LIST); n = 0 when null/corrupt.
+__device__ __forceinline__ bool flat_var_slot(const VarLaunch& L, const VarFieldDev& f, const uint8_t* row,
+                                              int64_t row_len, int64_t* rel, int64_t* n, bool report,
+                                              int32_t* status) {
+  *rel = 0;
+  *n = 0;
+  if ((row[f.slot >> 3] >> (f.slot & 7)) & 1) return true;  // BinaryRow.isNullAt
+  const uint8_t* sp = row + L.bitmap_bytes + 8 * f.slot;
+  const uint64_t os = ld32(sp) | ((uint64_t)ld32(sp + 4) << 32);
+  const int64_t r = (int32_t)(os >> 32);
+  if (!f.is_list) {
+    const int64_t len = (int32_t)(uint32_t)os;
+    if (len < 0 || r < 0 || r + len > row_len) {
+      if (report) set_status(status, FORY_ERR_CORRUPT);
+      return false;
+    }
+    *rel = r;
+    *n = len;
+    return false;
+  }
+  if (r < 0 || r + 8 > row_len) {
+    if (report) set_status(status, FORY_ERR_CORRUPT);
+    return false;
+  }
+  const int64_t cnt = (int32_t)ld32(row + r);  // BinaryArray.pointTo: numElements
+  if (cnt < 0 || r + 8 + bitmap_bytes(cnt) + cnt * f.w > row_len) {
+    if (report) set_status(status, FORY_ERR_CORRUPT);
+    return false;
+  }
+  *rel = r;
+  *n = cnt;
+  return false;
+}
+
+// Fixed fields of width W: slot (LDS) -> column, validity by ballot.
+template <int W, int NW>
+__device__ __forceinline__ void flat_dec_fixed(const VarLaunch& L, const FixedFieldDev* __restrict__ fix, int g0, int g1, int wave, int lane, bool live,
+                                               bool bad, int64_t i, int64_t r0, int rows, const uint8_t* row) {
+  for (int k0 = g0 + wave * kFixBatch; k0 < g1; k0 += NW * kFixBatch) {
+#pragma unroll
+    for (int k = 0; k < kFixBatch; ++k) {
+      if (k0 + k < g1) {
+        const FixedFieldDev& f = fix[k0 + k];
+        const bool nul = bad || ((row[f.slot >> 3] >> (f.slot & 7)) & 1);
+        const uint8_t* sp = row + L.bitmap_bytes + 8 * f.slot;
+        uint64_t x = 0;
+        if (!nul) x = (uint64_t)ld32(sp) | ((uint64_t)ld32(sp + 4) << 32);
+        if (f.flags & 2) x = (x & 0xff) ? 1 : 0;
+        if (f.out_validity) {
+          const uint64_t m = __ballot(live && !nul);
+          if (lane == 0) write_validity64(f.out_validity, r0, rows, m);
+        }
+        if (live) stw<W>(f.out_values, i, x);
+      }
+    }
+  }
+}
+
+template <bool FRAME, bool WRITE, int NW>
+__global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
+                                                                  const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
+                                                                  const uint8_t* __restrict__ in,
+                                                                       const int64_t* __restrict__ offs,
+                                                                       int32_t* status, int cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int HDR = FRAME ? 12 : 0;
+  const int stg_bytes = L.stg_bytes;
+  uint8_t* img = lds;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  int64_t B0, B1, beg, end;
+  bool live;
+  const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
+  const int mis = (int)(reinterpret_cast<uintptr_t>(in + B0) & 15);
+  const int64_t total = mis + (B1 - B0);
+  if (!sane || (mis & 3) || total > cap) {
+    if (wave == 0) dec_record<WRITE>(L, prog, cols, r0 + lane, live, in + beg, end - beg, status);
+    return;
+  }
+  {  // stage the tile's rows (coalesced 16-B loads; edge chunks by dword)
+    const uint8_t* g = in + B0 - mis;
+    const int tot = (int)total;
+    const int nch = (tot + 15) >> 4;
+    for (int cc = tid; cc < nch; cc += 64 * NW) {
+      const int lo = cc * 16;
+      u32x4 x;
+      if (lo >= mis && lo + 16 <= tot) {
+        x = *gp(reinterpret_cast<const u32x4*>(g + lo));
+      } else {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int o = lo + 4 * d;
+          x[d] = (o >= mis && o + 4 <= tot) ? *gp(reinterpret_cast<const uint32_t*>(g + o)) : 0u;
+        }
+      }
+      *reinterpret_cast<u32x4*>(img + lo) = x;
+    }
+  }
+  __syncthreads();
+  const int64_t i = r0 + lane;
+  const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
+  const uint8_t* fp = img + mis + (int)(beg - B0);
+  const uint8_t* row = fp + HDR;
+  int64_t row_len = end - beg;
+  bool bad = !live;
+  if (live && FRAME) {  // Encoders.decode: length + schema hash (Encoders.java:177-200)
+    const uint32_t len = ld32(fp);
+    const uint64_t h = (uint64_t)ld32(fp + 4) | ((uint64_t)ld32(fp + 8) << 32);
+    const bool report = WRITE && wave == 0;
+    if (h != (uint64_t)L.schema_hash) {
+      if (report) set_status(status, FORY_ERR_SCHEMA_MISMATCH);
+      bad = true;
+    } else if ((int64_t)len + 4 != row_len || len < (uint32_t)(8 + L.fixed_size)) {
+      if (report) set_status(status, FORY_ERR_CORRUPT);
+      bad = true;
+    }
+    row_len -= 12;
+  }
+  if (!WRITE) {  // pass 1: payload lengths -> out_offsets[i+1]
+    for (int v = wave; v < L.num_var; v += NW) {
+      int64_t rel = 0, n = 0;
+      if (!bad) flat_var_slot(L, vf[v], row, row_len, &rel, &n, true, status);
+      if (live) vf[v].out_offsets[i + 1] = (int32_t)n;
+    }
+    return;
+  }
+  // fixed fields: slot -> column (UnsafeTrait.getInt32/... ; null -> 0), validity by ballot
+  flat_dec_fixed<8, NW>(L, fix, L.fix_group[0], L.fix_group[1], wave, lane, live, bad, i, r0, rows, row);
+  flat_dec_fixed<4, NW>(L, fix, L.fix_group[1], L.fix_group[2], wave, lane, live, bad, i, r0, rows, row);
+  flat_dec_fixed<2, NW>(L, fix, L.fix_group[2], L.fix_group[3], wave, lane, live, bad, i, r0, rows, row);
+  flat_dec_fixed<1, NW>(L, fix, L.fix_group[3], L.fix_group[4], wave, lane, live, bad, i, r0, rows, row);
+  // var fields: one per wave at a time, output span staged in LDS
+  uint8_t* stg = lds + cap + wave * stg_bytes;
+  for (int v = wave; v < L.num_var; v += NW) {
+    const VarFieldDev& f = vf[v];
+    const bool islist = f.is_list;
+    const int w = f.w;
+    const int iflags = f.iflags;
+    int64_t rel = 0, n = 0;
+    bool nul = true;
+    if (!bad) nul = flat_var_slot(L, f, row, row_len, &rel, &n, false, status);
+    if (f.out_validity) {
+      const uint64_t m = __ballot(live && !nul);
+      if (lane == 0) write_validity64(f.out_validity, r0, rows, m);
+    }
+    const int64_t O0 = f.out_offsets[r0], O1 = f.out_offsets[r0 + rows];
+    const int64_t S = (O1 - O0) * w;
+    uint8_t* gdst = f.out_values + O0 * w;
+    const int phase = (int)(reinterpret_cast<uintptr_t>(gdst) & 15);
+    const int64_t e0 = live ? (int64_t)f.out_offsets[i] : 0;
+    const uint8_t* src = row + rel + (islist ? 8 + bitmap_bytes(n) : 0);
+    if ((iflags & 3) == 0 && S >= 0 && S + 32 <= stg_bytes) {
+      if (live && n > 0) {
+        uint8_t* d = stg + phase + (e0 - O0) * w;
+        if (!islist) {
+          for (int64_t k = 0; k < n; ++k) d[k] = src[k];
+        } else {  // BinaryArray.toXArray; a peer's null item bits read as 0
+          const uint8_t* abm = row + rel + 8;
+          for (int64_t j = 0; j < n; ++j) {
+            const bool en = (abm[j >> 3] >> (j & 7)) & 1;
+            for (int b = 0; b < w; ++b) d[j * w + b] = en ? 0 : src[j * w + b];
+          }
+        }
+      }
+      wave_lds_sync();
+      uint8_t* g = gdst - phase;
+      const int tot = (int)(phase + S);
+      const int nch = (tot + 15) >> 4;
+      for (int cc = lane; cc < nch; cc += 64) {
+        const int lo = cc * 16;
+        if (lo >= phase && lo + 16 <= tot) {
+          *gp(reinterpret_cast<u32x4*>(g + lo)) = *reinterpret_cast<const u32x4*>(stg + lo);
+        } else {
+          for (int b = 0; b < 16; ++b) {
+            const int o2 = lo + b;
+            if (o2 >= phase && o2 < tot) store_byte(g + o2, stg[o2]);
+          }
+        }
+      }
+      wave_lds_sync();
+    } else if (live && n > 0) {
+      if (!islist) {
+        copy_out(f.out_values + e0, src, n);
+      } else {
+        const uint8_t* arr = row + rel;
+        for (int64_t j = 0; j < n; ++j) {
+          const bool en = (arr[8 + (j >> 3)] >> (j & 7)) & 1;
+          uint64_t x = 0;
+          if (!en) {
+            const uint8_t* pp = src + j * w;
+            switch (w) {
+              case 8: x = (uint64_t)ld32(pp) | ((uint64_t)ld32(pp + 4) << 32); break;
+              case 4: x = ld32(pp); break;
+              case 2: x = (uint64_t)pp[0] | ((uint64_t)pp[1] << 8); break;
+              default: x = pp[0]; break;
+            }
+          }
+          if (iflags & 2) x = (x & 0xff) ? 1 : 0;
+          store_elem(f.out_values, w, e0 + j, x);
+          if (f.out_item_validity) {
+            const int64_t q = e0 + j;
+            const uint32_t bit = 1u << (q & 31);
+            uint32_t* word = reinterpret_cast<uint32_t*>(f.out_item_validity) + (q >> 5);
+            if (en) atomicAnd(word, ~bit);
+            else atomicOr(word, bit);
+          }
+        }
+      }
+    }
+  }
 }
 
 template <typename K>
@@ -2095,7 +2590,7 @@ hipError_t launch_scan_offsets_i32(int32_t* offs, int64_t n, int64_t* partials, 
 hipError_t launch_var_sizes(const VarLaunch& L, int64_t* d_row_offsets, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
   const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
-  hipLaunchKernelGGL(var_sizes_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, d_row_offsets);
+  hipLaunchKernelGGL(var_sizes_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.prog, L.cols, d_row_offsets);
   return hipGetLastError();
 }
 
@@ -2117,19 +2612,88 @@ void var_tile_launch(K* k, const VarLaunch&, int) {
   if (!init) { raise_lds_cap(k); init = true; }
 }
 
+uint64_t* g_prof = nullptr;
+int64_t g_prof_words = 0;
+
+uint64_t* var_prof_buffer(int64_t tiles) {
+  const char* e = getenv("FORY_ROWFMT_VARPROF");
+  if (!e || atoi(e) == 0) return nullptr;
+  if (tiles * 8 > g_prof_words) {
+    if (g_prof) (void)hipFree(g_prof);
+    g_prof = nullptr;
+    g_prof_words = 0;
+    if (hipMalloc(&g_prof, (size_t)tiles * 8 * sizeof(uint64_t)) != hipSuccess) return nullptr;
+    g_prof_words = tiles * 8;
+  }
+  return g_prof;
+}
+
+int64_t var_prof_copy(uint64_t* host, int64_t max_words) {
+  if (!g_prof) return 0;
+  const int64_t n = max_words < g_prof_words ? max_words : g_prof_words;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(host, g_prof, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return n;
+}
+
+// FORY_ROWFMT_VARFLAT=0: generic tile interpreter for flat plans too (A/B).
+bool var_flat(const VarLaunch& L) {
+  const char* e = getenv("FORY_ROWFMT_VARFLAT");
+  return L.flat && (!e || atoi(e) != 0);
+}
+
+int flat_nw() {  // FORY_ROWFMT_VARNW: waves per 64-record tile (4 or 8)
+  const char* e = getenv("FORY_ROWFMT_VARNW");
+  return e && atoi(e) == 8 ? 8 : 4;
+}
+
+size_t flat_lds(const VarLaunch& L, int cap, int nw) {
+  return (size_t)cap + (size_t)nw * L.stg_bytes + (size_t)L.num_var * 64 * sizeof(int32_t);
+}
+
+template <bool FRAME, int NW>
+void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
+                     int cap, hipStream_t s) {
+  auto* k = L.prof ? &var_encode_flat_kernel<FRAME, NW, true> : &var_encode_flat_kernel<FRAME, NW, false>;
+  var_tile_launch(k, L, cap);
+  hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds(L, cap, NW), s, L, L.prog,
+                     L.cols, L.fix, L.vf, offs, out, capacity, status, cap);
+}
+
+template <bool FRAME, bool WRITE, int NW>
+void launch_flat_dec(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int32_t* status, int cap,
+                     hipStream_t s) {
+  auto* k = &var_decode_flat_kernel<FRAME, WRITE, NW>;
+  var_tile_launch(k, L, cap);
+  hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds(L, cap, NW), s, L, L.prog,
+                     L.cols, L.fix, L.vf, rows, offs, status, cap);
+}
+
 hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity,
                              int32_t* status, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
+  if (var_tiles() && var_flat(L)) {
+    const int cap = var_cap(L);
+    const int nw = flat_nw();
+    if (L.frame) {
+      if (nw == 8) launch_flat_enc<true, 8>(L, offs, out, capacity, status, cap, s);
+      else launch_flat_enc<true, 4>(L, offs, out, capacity, status, cap, s);
+    } else {
+      if (nw == 8) launch_flat_enc<false, 8>(L, offs, out, capacity, status, cap, s);
+      else launch_flat_enc<false, 4>(L, offs, out, capacity, status, cap, s);
+    }
+    return hipGetLastError();
+  }
   if (var_tiles()) {
     const int cap = var_cap(L);
     var_tile_launch(&var_encode_tile_kernel, L, cap);
     hipLaunchKernelGGL(var_encode_tile_kernel, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64), (size_t)cap, s,
-                       L, offs, out, capacity, status, cap);
+                       L, L.prog, L.cols, offs, out, capacity, status, cap);
     return hipGetLastError();
   }
   const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
-  hipLaunchKernelGGL(var_encode_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, offs, out, capacity,
-                     status);
+  hipLaunchKernelGGL(var_encode_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.prog, L.cols, offs, out,
+                     capacity, status);
   return hipGetLastError();
 }
 
@@ -2137,15 +2701,28 @@ template <bool WRITE>
 hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int32_t* status,
                                   hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
+  if (var_tiles() && var_flat(L)) {
+    const int cap = var_cap(L);
+    const int nw = flat_nw();
+    if (L.frame) {
+      if (nw == 8) launch_flat_dec<true, WRITE, 8>(L, rows, offs, status, cap, s);
+      else launch_flat_dec<true, WRITE, 4>(L, rows, offs, status, cap, s);
+    } else {
+      if (nw == 8) launch_flat_dec<false, WRITE, 8>(L, rows, offs, status, cap, s);
+      else launch_flat_dec<false, WRITE, 4>(L, rows, offs, status, cap, s);
+    }
+    return hipGetLastError();
+  }
   if (var_tiles()) {
     const int cap = var_cap(L);
     var_tile_launch(&var_decode_tile_kernel<WRITE>, L, cap);
     hipLaunchKernelGGL(var_decode_tile_kernel<WRITE>, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64),
-                       (size_t)cap, s, L, rows, offs, status, cap);
+                       (size_t)cap, s, L, L.prog, L.cols, rows, offs, status, cap);
     return hipGetLastError();
   }
   const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
-  hipLaunchKernelGGL(var_decode_kernel<WRITE>, dim3((unsigned)blocks), dim3(kWG), 0, s, L, rows, offs, status);
+  hipLaunchKernelGGL(var_decode_kernel<WRITE>, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.prog, L.cols, rows, offs,
+                     status);
   return hipGetLastError();
 }
 

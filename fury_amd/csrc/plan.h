@@ -57,6 +57,25 @@ struct Op {
   int32_t code, a, b, c, d, e;
 };
 
+// Flat plans: one top-level STRING/BINARY or LIST<fixed> field (bound per call;
+// read with scalar loads by the flat tile kernels).
+struct VarFieldDev {
+  const int32_t* offsets;        // Arrow offsets: bytes (STRING/BINARY) or items (LIST)
+  const uint8_t* values;         // string bytes / item values
+  const uint8_t* validity;       // field validity (nullable) or null
+  const uint8_t* item_validity;  // LIST item validity (nullable items) or null
+  int32_t* out_offsets;          // decode targets (same buffers, output side)
+  uint8_t* out_values;
+  uint8_t* out_validity;
+  uint8_t* out_item_validity;
+  int32_t slot;                  // schema ordinal
+  int32_t is_list;
+  int32_t w;                     // item width (1 for bytes)
+  int32_t iflags;                // item flags: bit0 nullable, bit1 bool
+  int32_t flags;                 // field flags: bit0 nullable
+  int32_t pad[3];
+};
+
 struct ColumnDev {  // per-column device view (bound per call)
   const uint8_t* values;
   const int32_t* offsets;

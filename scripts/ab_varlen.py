@@ -24,13 +24,16 @@ plan = enc.plan
 ws = enc.workspace(n)
 arr = native.column_array(cols)
 status = torch.zeros(1, dtype=torch.int32, device=dev)
-variants = {"global": {"FORY_ROWFMT_VARTILE": "0"}, "tile": {}, "tile16k": {"FORY_ROWFMT_VARCAP": "16384"},
-            "tile32k": {"FORY_ROWFMT_VARCAP": "32768"}, "tile48k": {"FORY_ROWFMT_VARCAP": "49152"}}
+variants = {"global": {"FORY_ROWFMT_VARTILE": "0"}, "tile": {"FORY_ROWFMT_VARFLAT": "0"}, "flat": {},
+            "flat_nw8": {"FORY_ROWFMT_VARNW": "8"}, "flat_stg4k": {"FORY_ROWFMT_VARSTG": "4096"},
+            "flat_cap40k": {"FORY_ROWFMT_VARCAP": "40960"}, "flat_nw8_cap40k": {"FORY_ROWFMT_VARNW": "8",
+                                                                                "FORY_ROWFMT_VARCAP": "40960"}}
 res = {}
 
 
 def set_env(envs):
-    for k in ("FORY_ROWFMT_VARTILE", "FORY_ROWFMT_VARCAP"):
+    for k in ("FORY_ROWFMT_VARTILE", "FORY_ROWFMT_VARCAP", "FORY_ROWFMT_VARFLAT", "FORY_ROWFMT_VARNW",
+              "FORY_ROWFMT_VARSTG"):
         os.environ.pop(k, None)
     os.environ.update(envs)
 

@@ -12,3 +12,8 @@ for cfg in mixed40 nested; do
   python -c "import json,sys;d=json.load(open('gpurun_out/ab_$cfg.json'));[print(k,v) for k,v in d.items()]" || exit 1
   [ $rc -eq 0 ] || exit $rc
 done
+timeout -k 10 300 python scripts/var_timeline.py mixed40 > gpurun_out/timeline_mixed.json 2> gpurun_out/timeline.err
+rc=$?; echo "timeline exit $rc"; python -c "
+import json; d=json.load(open('gpurun_out/timeline_mixed.json'))
+for k,v in d.items(): print(k, {a:(b['median_us'] if isinstance(b,dict) else b) for a,b in v.items()})"
+exit $rc

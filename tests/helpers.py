@@ -115,6 +115,39 @@ def columns_equal(schema: Schema, a: List[HostColumn], b: List[HostColumn]) -> L
     return errs
 
 
+def flat_mix_rows(n: int, seed: int):
+    """Flat varlen rows: short and long strings (spans beyond one staging buffer),
+    list<int64>/list<int16> with not-null items, list<bool>, bool / int8 fields."""
+    rng = np.random.default_rng(seed)
+    rows = []
+    for i in range(n):
+        long_len = int(rng.integers(0, 300)) if rng.random() < 0.5 else int(rng.integers(0, 8))
+        rows.append({
+            "a": bool(rng.random() < 0.5),
+            "b": int(rng.integers(-128, 128)),
+            "c": None if rng.random() < 0.1 else "".join(chr(int(x)) for x in rng.integers(97, 123, size=rng.integers(0, 12))),
+            "d": "".join(chr(int(x)) for x in rng.integers(65, 91, size=long_len)),
+            "e": None if rng.random() < 0.15 else [int(x) for x in rng.integers(-2**62, 2**62, size=rng.integers(0, 20))],
+            "f": [int(x) for x in rng.integers(-30000, 30000, size=rng.integers(0, 9))],
+            "g": [bool(x) for x in rng.integers(0, 2, size=rng.integers(0, 5))],
+            "h": int(rng.integers(-2**31, 2**31)),
+        })
+    return rows
+
+
+def flat_mix_schema() -> Schema:
+    return Schema([
+        Field("a", DataType(ArrowType.BOOL), False),
+        Field("b", DataType(ArrowType.INT8), False),
+        Field("c", DataType(ArrowType.STRING), True),
+        Field("d", DataType(ArrowType.STRING), False),
+        DataTypes.array_field("e", Field("item", DataType(ArrowType.INT64), False)),
+        Field("f", DataType(ArrowType.LIST), False, [Field("item", DataType(ArrowType.INT16), False)]),
+        Field("g", DataType(ArrowType.LIST), False, [Field("item", DataType(ArrowType.BOOL), False)]),
+        Field("h", DataType(ArrowType.INT32), False),
+    ])
+
+
 def catalog():
     """name -> (schema, host column factory(n, seed))."""
     return {
@@ -129,6 +162,7 @@ def catalog():
         "nested_nulls": (W.nested_schema(), lambda n, s: W.nested_host_columns(n, seed=29 + s, null_rate=0.25)),
         "strings_lists": (string_list_schema(),
                           lambda n, s: build_columns(string_list_schema(), string_list_rows(n, s))),
+        "flat_mix": (flat_mix_schema(), lambda n, s: build_columns(flat_mix_schema(), flat_mix_rows(n, s))),
     }
 
 

@@ -20,6 +20,7 @@ from fury_amd.format import (ClassNotCompatibleException, CorruptRowException,  
 from fury_amd.format.columns import to_device, to_host  # noqa: E402
 from fury_amd.format.encoder import EncodedRows, RowEncoder  # noqa: E402
 from fury_amd.format import native  # noqa: E402
+from fury_amd.format.types import ArrowType  # noqa: E402
 
 from helpers import catalog, columns_equal  # noqa: E402
 
@@ -55,12 +56,28 @@ def kernel_variant(request, monkeypatch):
     return request.param
 
 
-@pytest.mark.parametrize("frame", [0, 1])
-@pytest.mark.parametrize("n", SIZES)
-@pytest.mark.parametrize("name", list(catalog().keys()))
-def test_encode_decode_parity(name, n, frame, kernel_variant):
-    if kernel_variant != "8" and name.startswith(("mixed", "nested", "strings")):
-        pytest.skip("the variant switch only affects fixed-width schemas")
+VARLEN = [k for k, (sch, _) in catalog().items()
+          if any(f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.STRUCT)
+                 for f in sch.fields)]
+FIXED = [k for k in catalog() if k not in VARLEN]
+
+
+@pytest.fixture(params=["flat", "flat_nw8", "flat_stg256", "tile", "global", "smallcap"])
+def varlen_engine(request, monkeypatch):
+    """Varlen engines: flat cooperative tile kernels (default for flat plans), the
+    generic one-wave tile interpreter (FORY_ROWFMT_VARFLAT=0), the per-record global
+    interpreter (FORY_ROWFMT_VARTILE=0), and a 2 KiB LDS image so most tiles take the
+    per-record fallback inside the tile kernels; flat with 8 waves per tile, and with a
+    256-byte staging buffer (most spans take the per-lane copy)."""
+    env = {"flat": {}, "flat_nw8": {"FORY_ROWFMT_VARNW": "8"}, "flat_stg256": {"FORY_ROWFMT_VARSTG": "256"},
+           "tile": {"FORY_ROWFMT_VARFLAT": "0"}, "global": {"FORY_ROWFMT_VARTILE": "0"},
+           "smallcap": {"FORY_ROWFMT_VARCAP": "2048"}}[request.param]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+def check_parity(name, n, frame):
     schema, make = catalog()[name]
     cols = make(n, n)
     expect, offs = oracle.encode(schema, cols, n, frame)
@@ -81,6 +98,47 @@ def test_encode_decode_parity(name, n, frame, kernel_variant):
     d_offs = None if rows.offsets is None else torch.from_numpy(offs).cuda()
     dec2 = to_host(enc.decode(buf, n, frame, d_offs))
     assert columns_equal(schema, ref, dec2) == []
+
+
+@pytest.mark.parametrize("frame", [0, 1])
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("name", FIXED)
+def test_encode_decode_parity(name, n, frame, kernel_variant):
+    check_parity(name, n, frame)
+
+
+@pytest.mark.parametrize("frame", [0, 1])
+@pytest.mark.parametrize("n", SIZES + [5000])
+@pytest.mark.parametrize("name", VARLEN)
+def test_varlen_parity(name, n, frame, varlen_engine):
+    check_parity(name, n, frame)
+
+
+@pytest.mark.parametrize("shift", [4, 8, 12])
+@pytest.mark.parametrize("name", ["mixed40_nulls", "flat_mix", "nested_nulls"])
+def test_varlen_unaligned_buffers(name, shift, varlen_engine):
+    """Rows written to / read from buffers at a 4-byte (not 16-byte) aligned address."""
+    schema, make = catalog()[name]
+    n = 777
+    cols = make(n, 11)
+    enc = encoder_for(name)
+    dcols = to_device(cols)
+    arr = native.column_array(dcols)
+    ws = enc.workspace(n)
+    for frame in (0, 1):
+        expect, offs = oracle.encode(schema, cols, n, frame)
+        d_offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        native.encoded_size(enc.plan, arr, n, frame, d_offs, ws)
+        big = torch.zeros(expect.nbytes + 64, dtype=torch.uint8, device="cuda")
+        out = big[shift:]
+        status = torch.zeros(1, dtype=torch.int32, device="cuda")
+        native.encode(enc.plan, arr, n, frame, d_offs, out, status, ws)
+        native.read_status(status)
+        got = out[:expect.nbytes].cpu().numpy()
+        assert np.array_equal(got, expect), frame
+        assert int(big[:shift].sum().item()) == 0 and int(big[shift + expect.nbytes:].sum().item()) == 0
+        dec = to_host(enc.decode(out[:expect.nbytes], n, frame, d_offs))
+        assert columns_equal(schema, cols, dec) == []
 
 
 def test_schema_mismatch_raises():
@@ -158,8 +216,8 @@ def test_struct_large_round_trip_and_sampled_parity(kernel_variant):
             assert torch.equal(a.values[:n].view(torch.uint8), b.values.view(torch.uint8))
 
 
-def test_mixed_and_nested_large_round_trip():
-    for name, n in (("mixed40_nulls", 300_000), ("nested_nulls", 300_000)):
+def test_mixed_and_nested_large_round_trip(varlen_engine):
+    for name, n in (("mixed40_nulls", 300_000), ("nested_nulls", 300_000), ("flat_mix", 100_000)):
         schema, make = catalog()[name]
         cols = make(n, 5)
         enc = encoder_for(name)
