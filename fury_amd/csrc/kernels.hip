@@ -1283,9 +1283,14 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
   int absent = 0;
   int64_t wi = L.fixed_size;  // writerIndex relative to row (BinaryRowWriter.reset)
   for (int b = 0; b < L.bitmap_bytes; b += 8) gst64(row + b, 0);
-  for (int pc = 0; pc < L.num_ops; ++pc) {
+  // pc and the fixed-batch length stay wave-uniform (advanced outside the
+  // per-lane branches) so the program and column tables load as scalars.
+  for (int pc = 0, cnt = 1; pc < L.num_ops; pc += cnt) {
     const Op op = prog[pc];
     const ColumnDev& c = cols[op.b];
+    cnt = 1;
+    if (op.code == OP_FIXED)
+      while (cnt < kFixBatch && pc + cnt < L.num_ops && prog[pc + cnt].code == OP_FIXED) ++cnt;
     if (absent) {
       if (op.code == OP_STRUCT_BEGIN) absent++;
       else if (op.code == OP_STRUCT_END) absent--;
@@ -1297,8 +1302,6 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
     const bool isnull = (op.d & 1) && !col_valid(c, i);
     switch (op.code) {
       case OP_FIXED: {  // BinaryRowWriter.write(ordinal, v) / setNullAt, batched
-        int cnt = 1;
-        while (cnt < kFixBatch && pc + cnt < L.num_ops && prog[pc + cnt].code == OP_FIXED) ++cnt;
         uint64_t v[kFixBatch];
 #pragma unroll
         for (int k = 0; k < kFixBatch; ++k) {
@@ -1319,7 +1322,6 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
             gst64(slots + 8 * o.a, x);
           }
         }
-        pc += cnt - 1;
         break;
       }
       case OP_BYTES: {

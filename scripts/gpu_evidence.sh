@@ -14,4 +14,8 @@ timeout -k 10 400 python bench.py ${BENCH_ARGS:---steps 10 --warmup 3} > gpurun_
 rc=$?; echo "bench exit $rc"; cat gpurun_out/bench.json; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python bench.py --frame --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bench_frame.json 2> gpurun_out/bench_frame.err
 rc=$?; echo "bench frame exit $rc"; cat gpurun_out/bench_frame.json
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+for cfg in mixed40 nested; do
+  timeout -k 10 400 python bench.py --config $cfg --steps 10 --warmup 3 --cpu-seconds 8 > gpurun_out/bench_$cfg.json 2> gpurun_out/bench_$cfg.err
+  rc=$?; echo "bench $cfg exit $rc"; cat gpurun_out/bench_$cfg.json; [ $rc -eq 0 ] || exit $rc
+done

@@ -21,12 +21,16 @@ def rows(pattern):
 def short(name):
     import re
     m = re.search(r"(encode_fixed_\w*?kernel|decode_fixed_\w*?kernel|var_encode_kernel|var_decode_kernelILb[01]|"
-                  r"var_encode_tile_kernel|var_decode_tile_kernelILb[01]|"
+                  r"var_encode_tile_kernel|var_decode_tile_kernelILb[01]|var_encode_flat_kernel|var_decode_flat_kernel|"
                   r"var_sizes_kernel|scan_\w+?_kernel|fill_offsets_kernel)", name)
     if m:
         k = m.group(1)
         if k.startswith("var_decode") and not k.endswith(("0", "1")):
-            k += "ILb1" if "<true>" in name else ("ILb0" if "<false>" in name else "")
+            if k == "var_decode_flat_kernel":
+                k += "<pass2>" if re.search(r"<(true|false), true", name) or "ILb1ELb1E" in name or "ILb0ELb1E" in name \
+                    else "<pass1>"
+            else:
+                k += "ILb1" if "<true>" in name else ("ILb0" if "<false>" in name else "")
         return k
     return name[:60]
 
