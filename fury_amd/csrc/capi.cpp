@@ -309,6 +309,12 @@ int64_t* partials_ptr(const Plan& p, void* ws) {
   return reinterpret_cast<int64_t*>(static_cast<uint8_t*>(ws) + table_bytes(p));
 }
 
+// Per-tile payload totals of the flat decode (after the scan partials).
+int64_t* tile_totals_ptr(const Plan& p, void* ws, int64_t n) {
+  return reinterpret_cast<int64_t*>(static_cast<uint8_t*>(ws) + table_bytes(p) +
+                                    align_up((fory_amd::scan_partials(n) + 2) * 8));
+}
+
 }  // namespace
 
 extern "C" {
@@ -359,7 +365,8 @@ int fory_rowfmt_plan_info(const fory_plan* plan, fory_plan_info* info) {
 int64_t fory_rowfmt_workspace_bytes(const fory_plan* plan, int64_t num_rows) {
   if (!plan) return -1;
   const int64_t n = num_rows < 0 ? 0 : num_rows;
-  return table_bytes(plan->p) + align_up((fory_amd::scan_partials(n) + 2) * 8);
+  return table_bytes(plan->p) + align_up((fory_amd::scan_partials(n) + 2) * 8) +
+         align_up(fory_amd::var_tile_totals_words((int64_t)plan->p.top.size(), n) * 8);
 }
 
 int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols, int64_t num_rows,
@@ -455,8 +462,10 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
   rc = prepare_var(p, out_cols, num_rows, frame_mode, d_workspace, s, &L);
   if (rc) return rc;
   hipError_t e = fory_amd::launch_var_decode_lengths(L, static_cast<const uint8_t*>(d_rows), d_row_offsets,
-                                                     d_status, s);
+                                                     tile_totals_ptr(p, d_workspace, num_rows),
+                                                     partials_ptr(p, d_workspace), d_status, s);
   if (e != hipSuccess) return hip_fail(e, "var_decode_lengths");
+  if (fory_amd::var_decode_tiled_offsets(L)) return FORY_OK;  // tile bases written; decode fills the rest
   for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
     const int k = p.nodes[idx].kind;
     if (k != fory_amd::KIND_BYTES && k != fory_amd::KIND_LIST) continue;

@@ -67,10 +67,15 @@ struct VarLaunch {
 hipError_t launch_var_sizes(const VarLaunch& L, int64_t* d_row_offsets, hipStream_t s);
 hipError_t launch_var_encode(const VarLaunch& L, const int64_t* d_row_offsets, uint8_t* out,
                              int64_t capacity, int32_t* status, hipStream_t s);
-// decode: per-row lengths of every varlen column into out_offsets[i+1]
+// decode sizes. Flat plans on the tile engine: per-tile payload totals into
+// tile_tot (var_tile_totals_words int64), scanned here, tile bases scattered
+// to out_offsets[64 t] and out_offsets[n]; the values pass fills the rest.
+// Otherwise: per-row lengths into out_offsets[i+1] (caller scans per column).
 hipError_t launch_var_decode_lengths(const VarLaunch& L, const uint8_t* rows,
-                                     const int64_t* d_row_offsets, int32_t* status,
-                                     hipStream_t s);
+                                     const int64_t* d_row_offsets, int64_t* tile_tot,
+                                     int64_t* partials, int32_t* status, hipStream_t s);
+bool var_decode_tiled_offsets(const VarLaunch& L);
+int64_t var_tile_totals_words(int64_t num_var, int64_t n);
 hipError_t launch_var_decode(const VarLaunch& L, const uint8_t* rows,
                              const int64_t* d_row_offsets, int32_t* status, hipStream_t s);
 

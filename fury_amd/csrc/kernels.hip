@@ -2022,6 +2022,37 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   FLAT_STAMP(7);
 }
 
+__device__ __forceinline__ int64_t wave_incl_scan64(int64_t x, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+__device__ __forceinline__ int64_t wave_sum64(int64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+  return x;
+}
+
+// Tile prefixes -> Arrow offsets at tile starts: out_offsets[64 t] for every
+// tile t and out_offsets[n] (= total) of each flat var field; the values pass
+// fills the records in between (tile base + in-wave prefix).
+__global__ __launch_bounds__(kWG) void flat_tile_bases_kernel(const VarFieldDev* __restrict__ vf, int num_var,
+                                                              const int64_t* __restrict__ tile_tot, int64_t n,
+                                                              int32_t* status) {
+  const int64_t tiles = (n + 63) / 64;
+  const int64_t k = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (k >= num_var * (tiles + 1)) return;
+  const int v = (int)(k / (tiles + 1));
+  const int64_t t = k - v * (tiles + 1);
+  const int64_t off = tile_tot[k];
+  if (off > 0x7fffffffLL) set_status(status, FORY_ERR_CAPACITY);  // int32 Arrow offsets
+  vf[v].out_offsets[t == tiles ? n : t * 64] = (int32_t)off;
+}
+
 // Reads a var field's slot of a staged record: returns payload (rel, n) with
 // n = bytes (STRING/BINARY) or elements (LIST); n = 0 when null/corrupt.
 __device__ __forceinline__ bool flat_var_slot(const VarLaunch& L, const VarFieldDev& f, const uint8_t* row,
@@ -2085,8 +2116,9 @@ template <bool FRAME, bool WRITE, int NW>
 __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
                                                                   const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
                                                                   const uint8_t* __restrict__ in,
-                                                                       const int64_t* __restrict__ offs,
-                                                                       int32_t* status, int cap) {
+                                                                  const int64_t* __restrict__ offs,
+                                                                  int64_t* __restrict__ tile_tot, int32_t* status,
+                                                                  int cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int HDR = FRAME ? 12 : 0;
   const int stg_bytes = L.stg_bytes;
@@ -2099,8 +2131,33 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
   const int mis = (int)(reinterpret_cast<uintptr_t>(in + B0) & 15);
   const int64_t total = mis + (B1 - B0);
-  if (!sane || (mis & 3) || total > cap) {
-    if (wave == 0) dec_record<WRITE>(L, prog, cols, r0 + lane, live, in + beg, end - beg, status);
+  const int64_t tiles = (L.num_rows + 63) / 64;
+  if (!sane || (mis & 3) || total > cap) {  // per-lane path on global rows (one wave)
+    if (wave == 0) {
+      const uint8_t* fp = in + beg;
+      const uint8_t* row = fp + HDR;
+      int64_t row_len = end - beg;
+      bool bad = !live;
+      if (live && FRAME) {
+        const uint32_t len = ld32(fp);
+        const uint64_t h = (uint64_t)ld32(fp + 4) | ((uint64_t)ld32(fp + 8) << 32);
+        bad = h != (uint64_t)L.schema_hash || (int64_t)len + 4 != row_len || len < (uint32_t)(8 + L.fixed_size);
+        row_len -= 12;
+      }
+      for (int v = 0; v < L.num_var; ++v) {
+        int64_t rel = 0, n = 0;
+        if (!bad) flat_var_slot(L, vf[v], row, row_len, &rel, &n, !WRITE, status);
+        if (!WRITE) {
+          const int64_t sum = wave_sum64(n);
+          if (lane == 0) tile_tot[v * (tiles + 1) + blockIdx.x] = sum;
+        } else {
+          const int64_t base = vf[v].out_offsets[r0];
+          const int64_t excl = wave_incl_scan64(n, lane) - n;
+          if (live) vf[v].out_offsets[r0 + lane] = (int32_t)(base + excl);
+        }
+      }
+      if (WRITE) dec_record<true>(L, prog, cols, r0 + lane, live, in + beg, end - beg, status);
+    }
     return;
   }
   {  // stage the tile's rows (coalesced 16-B loads; edge chunks by dword)
@@ -2142,11 +2199,12 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
     }
     row_len -= 12;
   }
-  if (!WRITE) {  // pass 1: payload lengths -> out_offsets[i+1]
+  if (!WRITE) {  // pass 1: per-tile payload totals (scanned over tiles by the host launcher)
     for (int v = wave; v < L.num_var; v += NW) {
       int64_t rel = 0, n = 0;
       if (!bad) flat_var_slot(L, vf[v], row, row_len, &rel, &n, true, status);
-      if (live) vf[v].out_offsets[i + 1] = (int32_t)n;
+      const int64_t sum = wave_sum64(n);
+      if (lane == 0) tile_tot[v * (tiles + 1) + blockIdx.x] = sum;
     }
     return;
   }
@@ -2169,11 +2227,15 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
       const uint64_t m = __ballot(live && !nul);
       if (lane == 0) write_validity64(f.out_validity, r0, rows, m);
     }
-    const int64_t O0 = f.out_offsets[r0], O1 = f.out_offsets[r0 + rows];
+    // Arrow offsets of this tile: base (tile prefix written by decode_sizes) + in-wave prefix
+    const int64_t O0 = f.out_offsets[r0];
+    const int64_t incl = wave_incl_scan64(n, lane);
+    const int64_t O1 = O0 + __shfl(incl, 63);
+    const int64_t e0 = O0 + incl - n;
+    if (live) f.out_offsets[i] = (int32_t)e0;
     const int64_t S = (O1 - O0) * w;
     uint8_t* gdst = f.out_values + O0 * w;
     const int phase = (int)(reinterpret_cast<uintptr_t>(gdst) & 15);
-    const int64_t e0 = live ? (int64_t)f.out_offsets[i] : 0;
     const uint8_t* src = row + rel + (islist ? 8 + bitmap_bytes(n) : 0);
     if ((iflags & 3) == 0 && S >= 0 && S + 32 <= stg_bytes) {
       if (live && n > 0) {
@@ -2663,12 +2725,13 @@ void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int6
 }
 
 template <bool FRAME, bool WRITE, int NW>
-void launch_flat_dec(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int32_t* status, int cap,
-                     hipStream_t s) {
+void launch_flat_dec(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int64_t* tile_tot,
+                     int32_t* status, int cap, hipStream_t s) {
   auto* k = &var_decode_flat_kernel<FRAME, WRITE, NW>;
   var_tile_launch(k, L, cap);
-  hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds(L, cap, NW), s, L, L.prog,
-                     L.cols, L.fix, L.vf, rows, offs, status, cap);
+  const size_t lds = WRITE ? flat_lds(L, cap, NW) : (size_t)cap;  // pass 1 needs only the row image
+  hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
+                     L.vf, rows, offs, tile_tot, status, cap);
 }
 
 hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity,
@@ -2700,18 +2763,18 @@ hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* o
 }
 
 template <bool WRITE>
-hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int32_t* status,
-                                  hipStream_t s) {
+hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int64_t* tile_tot,
+                                  int32_t* status, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
   if (var_tiles() && var_flat(L)) {
     const int cap = var_cap(L);
     const int nw = flat_nw();
     if (L.frame) {
-      if (nw == 8) launch_flat_dec<true, WRITE, 8>(L, rows, offs, status, cap, s);
-      else launch_flat_dec<true, WRITE, 4>(L, rows, offs, status, cap, s);
+      if (nw == 8) launch_flat_dec<true, WRITE, 8>(L, rows, offs, tile_tot, status, cap, s);
+      else launch_flat_dec<true, WRITE, 4>(L, rows, offs, tile_tot, status, cap, s);
     } else {
-      if (nw == 8) launch_flat_dec<false, WRITE, 8>(L, rows, offs, status, cap, s);
-      else launch_flat_dec<false, WRITE, 4>(L, rows, offs, status, cap, s);
+      if (nw == 8) launch_flat_dec<false, WRITE, 8>(L, rows, offs, tile_tot, status, cap, s);
+      else launch_flat_dec<false, WRITE, 4>(L, rows, offs, tile_tot, status, cap, s);
     }
     return hipGetLastError();
   }
@@ -2728,14 +2791,28 @@ hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const
   return hipGetLastError();
 }
 
+bool var_decode_tiled_offsets(const VarLaunch& L) { return L.num_rows > 0 && var_tiles() && var_flat(L); }
+
+int64_t var_tile_totals_words(int64_t num_var, int64_t n) { return num_var * ((n + 63) / 64 + 1); }
+
 hipError_t launch_var_decode_lengths(const VarLaunch& L, const uint8_t* rows, const int64_t* offs,
-                                     int32_t* status, hipStream_t s) {
-  return launch_var_decode_pass<false>(L, rows, offs, status, s);
+                                     int64_t* tile_tot, int64_t* partials, int32_t* status, hipStream_t s) {
+  hipError_t e = launch_var_decode_pass<false>(L, rows, offs, tile_tot, status, s);
+  if (e != hipSuccess || !var_decode_tiled_offsets(L)) return e;
+  const int64_t tiles = (L.num_rows + 63) / 64;
+  for (int v = 0; v < L.num_var; ++v) {  // exclusive scan of each field's tile totals
+    e = launch_scan_i64(tile_tot + v * (tiles + 1), tiles, partials, s);
+    if (e != hipSuccess) return e;
+  }
+  const int64_t words = (int64_t)L.num_var * (tiles + 1);
+  hipLaunchKernelGGL(flat_tile_bases_kernel, dim3((unsigned)((words + kWG - 1) / kWG)), dim3(kWG), 0, s, L.vf,
+                     L.num_var, tile_tot, L.num_rows, status);
+  return hipGetLastError();
 }
 
 hipError_t launch_var_decode(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int32_t* status,
                              hipStream_t s) {
-  return launch_var_decode_pass<true>(L, rows, offs, status, s);
+  return launch_var_decode_pass<true>(L, rows, offs, nullptr, status, s);
 }
 
 }  // namespace fory_amd

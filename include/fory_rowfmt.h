@@ -175,11 +175,17 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols,
  * for varlen plans; ignored (may be NULL) for fixed-width plans, whose rows
  * are i*stride (16-byte aligned d_rows).
  *
- * fory_rowfmt_decode_sizes (varlen plans; no-op for fixed-width): fills the
- * `offsets` array (num_rows+1 int32, device) of every STRING/BINARY/LIST
- * output column, so the caller can size `values` (bytes) and list element
- * columns (offsets[num_rows] items). The device path supports list elements
- * of fixed width only (FORY_ERR_UNSUPPORTED at plan creation otherwise).
+ * fory_rowfmt_decode_sizes (varlen plans; no-op for fixed-width): writes
+ * offsets[num_rows] (the total: bytes, or items for LIST) of every
+ * STRING/BINARY/LIST output column's `offsets` array (num_rows+1 int32,
+ * device), so the caller can size `values` and list element columns. The
+ * rest of `offsets` is complete after fory_rowfmt_decode (for plans whose
+ * top-level fields are all fixed/string/binary/list, decode_sizes writes
+ * tile-start prefixes at offsets[64*k] and decode fills the records in
+ * between): pass the same rows, row offsets and column arrays to both calls
+ * and do not modify `offsets` in between. The device path supports list
+ * elements of fixed width only (FORY_ERR_UNSUPPORTED at plan creation
+ * otherwise).
  *
  * fory_rowfmt_decode: writes values/offsets/validity of out_cols. Null
  * values decode to 0 (RowEncoderBuilder.java:239-246 leaves the Java default).
