@@ -33,7 +33,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="struct104", choices=["struct104", "mixed40", "nested"])
+    ap.add_argument("--config", default="struct104", choices=["struct104", "mixed40", "mixed40_long", "nested"])
     ap.add_argument("--rows", type=int, default=0, help="rows per GPU (default: config size)")
     ap.add_argument("--frame", action="store_true", help="frame-stream mode instead of raw rows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -43,7 +43,8 @@ def parse():
     return ap.parse_args()
 
 
-DEFAULT_ROWS = {"struct104": 64 * 1024 * 1024, "mixed40": 16 * 1024 * 1024, "nested": 8 * 1024 * 1024}
+DEFAULT_ROWS = {"struct104": 64 * 1024 * 1024, "mixed40": 16 * 1024 * 1024, "nested": 8 * 1024 * 1024,
+                "mixed40_long": 8 * 1024 * 1024}  # mixed40_long: strings 0..128 B (robustness, not a BASELINE config)
 
 
 def setup_dist(args):
@@ -78,9 +79,10 @@ def make_batch(config, n, row0, device):
         cols = [DeviceColumn(v, None, None, n) for v in vals]
         col_bytes = sum(v.numel() * v.element_size() for v in vals)
     else:
-        mk = W.mixed_host_columns if config == "mixed40" else W.nested_host_columns
-        seed = (23 if config == "mixed40" else 29) + row0
-        host = mk(n, seed=seed)
+        mixed = config.startswith("mixed40")
+        mk = W.mixed_host_columns if mixed else W.nested_host_columns
+        seed = (23 if mixed else 29) + row0
+        host = mk(n, seed=seed, max_len=128) if config == "mixed40_long" else mk(n, seed=seed)
         cols = to_device(host, device)
         col_bytes = 0
         for c in host:
@@ -89,7 +91,8 @@ def make_batch(config, n, row0, device):
                     col_bytes += a.nbytes
         # string/item value buffers carry 8 bytes of generator padding: not algorithmic
     torch.cuda.synchronize()
-    return schema if config == "struct104" else (W.mixed_schema() if config == "mixed40" else W.nested_schema()), cols, col_bytes
+    return schema if config == "struct104" else (W.mixed_schema() if config.startswith("mixed40")
+                                                 else W.nested_schema()), cols, col_bytes
 
 
 def cpu_baseline(config, frame, seconds):
@@ -101,9 +104,9 @@ def cpu_baseline(config, frame, seconds):
         schema = W.struct_schema()
         n = 200_000
         cols = W.struct_host_columns(n)
-    elif config == "mixed40":
+    elif config.startswith("mixed40"):
         schema, n = W.mixed_schema(), 200_000
-        cols = W.mixed_host_columns(n)
+        cols = W.mixed_host_columns(n, max_len=128 if config == "mixed40_long" else 32)
     else:
         schema, n = W.nested_schema(), 200_000
         cols = W.nested_host_columns(n)

@@ -194,20 +194,23 @@ void build_slabs(const Plan& p, const std::vector<FixedFieldDev>& tab, int frame
   L->slab_pitch = pitch;
 }
 
-// LDS budget of one 64-record tile image for the varlen tile engine: 1.125x an
-// estimated row (fixed part, nested struct rows, ~24 bytes per string,
-// ~4 elements per list), in [8, 64] KiB. Tiles above it take the per-record
-// global path (correct, slower); FORY_ROWFMT_VARCAP overrides.
+int32_t* spill_ptr(const Plan& p, void* ws, int64_t n);
+
+// LDS budget of one 64-record tile image for the varlen tile engine: 64 x an
+// estimated row (fixed part, nested struct rows, ~32 bytes per string,
+// ~16 elements per list), in [8, 64] KiB; small enough to keep several
+// workgroups per CU. Bigger tiles spill to a second launch with a 96 KiB
+// image (kSpillCap); FORY_ROWFMT_VARCAP overrides.
 int var_tile_cap(const Plan& p, int frame) {
   int64_t est = p.fixed_size + (frame ? 12 : 0);
   for (size_t k = 0; k < p.nodes.size(); ++k) {
     const fory_amd::Node& nd = p.nodes[k];
-    if (nd.kind == fory_amd::KIND_BYTES) est += 24;
-    else if (nd.kind == fory_amd::KIND_LIST) est += 16 + 4 * 8;
+    if (nd.kind == fory_amd::KIND_BYTES) est += 32;
+    else if (nd.kind == fory_amd::KIND_LIST) est += 16 + 16 * std::max<int64_t>(1, p.nodes[nd.children[0]].width);
     else if (nd.kind == fory_amd::KIND_STRUCT)  // child rows live in the variable region
       est += ((int64_t)(nd.children.size() + 63) / 64) * 8 + 8 * (int64_t)nd.children.size();
   }
-  int64_t cap = (64 * est * 9 / 8 + 1023) / 1024 * 1024;
+  int64_t cap = (64 * est + 1023) / 1024 * 1024;
   return (int)std::min<int64_t>(std::max<int64_t>(cap, 8 * 1024), 64 * 1024);
 }
 
@@ -290,6 +293,8 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
     L->fix_group[4] = at;
   }
   L->prof = fory_amd::var_prof_buffer((n + 63) / 64);
+  L->spill_count = spill_ptr(p, ws, n);
+  L->spill = L->spill_count + 4;
   const char* stg = getenv("FORY_ROWFMT_VARSTG");
   L->stg_bytes = stg ? std::max(256, std::min(16384, atoi(stg))) & ~15 : 2048;
   L->cols = static_cast<const ColumnDev*>(ws);
@@ -313,6 +318,12 @@ int64_t* partials_ptr(const Plan& p, void* ws) {
 int64_t* tile_totals_ptr(const Plan& p, void* ws, int64_t n) {
   return reinterpret_cast<int64_t*>(static_cast<uint8_t*>(ws) + table_bytes(p) +
                                     align_up((fory_amd::scan_partials(n) + 2) * 8));
+}
+
+// Spill list of the tile engines (after the tile totals): [count][pad x3][tiles].
+int32_t* spill_ptr(const Plan& p, void* ws, int64_t n) {
+  return reinterpret_cast<int32_t*>(reinterpret_cast<uint8_t*>(tile_totals_ptr(p, ws, n)) +
+                                    align_up(fory_amd::var_tile_totals_words((int64_t)p.top.size(), n) * 8));
 }
 
 }  // namespace
@@ -366,7 +377,8 @@ int64_t fory_rowfmt_workspace_bytes(const fory_plan* plan, int64_t num_rows) {
   if (!plan) return -1;
   const int64_t n = num_rows < 0 ? 0 : num_rows;
   return table_bytes(plan->p) + align_up((fory_amd::scan_partials(n) + 2) * 8) +
-         align_up(fory_amd::var_tile_totals_words((int64_t)plan->p.top.size(), n) * 8);
+         align_up(fory_amd::var_tile_totals_words((int64_t)plan->p.top.size(), n) * 8) +
+         align_up(fory_amd::var_spill_words(n) * 4);
 }
 
 int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols, int64_t num_rows,

@@ -61,6 +61,8 @@ struct VarLaunch {
   const FixedFieldDev* fix;     // device: top-level fixed fields, width-sorted
   const VarFieldDev* vf;        // device: top-level var fields, field order
   uint64_t* prof;               // debug (FORY_ROWFMT_VARPROF): 8 timestamps per tile, else null
+  int32_t* spill;               // workspace: tiles spilled to the big-image launch (ceil(n/64))
+  int32_t* spill_count;         // workspace: number of spilled tiles
 };
 
 // sizes -> d_row_offsets[0..n-1] (row/frame byte sizes), then exclusive scan.
@@ -76,6 +78,7 @@ hipError_t launch_var_decode_lengths(const VarLaunch& L, const uint8_t* rows,
                                      int64_t* partials, int32_t* status, hipStream_t s);
 bool var_decode_tiled_offsets(const VarLaunch& L);
 int64_t var_tile_totals_words(int64_t num_var, int64_t n);
+int64_t var_spill_words(int64_t n);
 hipError_t launch_var_decode(const VarLaunch& L, const uint8_t* rows,
                              const int64_t* d_row_offsets, int32_t* status, hipStream_t s);
 

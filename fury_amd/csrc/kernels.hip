@@ -1631,6 +1631,17 @@ __global__ __launch_bounds__(kWG) void var_decode_kernel(VarLaunch L, const Op* 
   dec_record<WRITE>(L, prog, cols, i0, live, in + offs[i], offs[i + 1] - offs[i], status);
 }
 
+// Tiles whose image exceeds a launch's LDS budget are appended to `list`
+// (atomic `count`) by the main launch and processed by a small persistent
+// launch of the same kernel with a big image (`cap` = its budget); only tiles
+// beyond that (or with misaligned bases) take the per-record global path.
+struct SpillArgs {
+  int32_t* list;
+  int32_t* count;
+  int32_t cap;  // LDS image budget of the spill launch
+  int32_t pad;
+};
+
 // Tile engine: one wave per tile of 64 consecutive records. The tile's bytes
 // [offs[r0], offs[r0+64]) are one contiguous run of the output/input, so the
 // wave assembles (encode) or stages (decode) them in an LDS image placed at
@@ -1649,12 +1660,14 @@ __device__ __forceinline__ bool var_tile_bounds(const int64_t* offs, int64_t n, 
   return __ballot(!ok) == 0 && ((*B0 | *B1) & 3) == 0 && *B1 >= *B0;
 }
 
+template <bool SPILL>
 __global__ __launch_bounds__(64) void var_encode_tile_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, const int64_t* __restrict__ offs,
                                                              uint8_t* __restrict__ out, int64_t capacity,
-                                                             int32_t* status, int cap) {
+                                                             int32_t* status, int cap, SpillArgs sp) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  auto body = [&](int64_t tile) {
+  const int64_t r0 = tile * 64;
   int64_t B0, B1, beg, end;
   bool live;
   const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
@@ -1663,6 +1676,10 @@ __global__ __launch_bounds__(64) void var_encode_tile_kernel(VarLaunch L, const 
   const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
   const int64_t total = mis + (B1 - B0);
   if (!sane || (mis & 3) || total > cap) {
+    if (!SPILL && sane && !(mis & 3) && total <= sp.cap) {  // spill: the big-image launch takes it
+      if (threadIdx.x == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
+      return;
+    }
     if (live) enc_record(L, prog, cols, r0 + lane, out + beg, end - beg);
     return;
   }
@@ -1683,21 +1700,37 @@ __global__ __launch_bounds__(64) void var_encode_tile_kernel(VarLaunch L, const 
       }
     }
   }
+  };
+  if (!SPILL) {
+    body(blockIdx.x);
+    return;
+  }
+  const int64_t count = *sp.count;  // tiles the main launch spilled
+  for (int64_t k = blockIdx.x; k < count; k += gridDim.x) {
+    body(sp.list[k]);
+    __syncthreads();
+  }
 }
 
-template <bool WRITE>
+
+template <bool WRITE, bool SPILL>
 __global__ __launch_bounds__(64) void var_decode_tile_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, const uint8_t* __restrict__ in,
                                                              const int64_t* __restrict__ offs, int32_t* status,
-                                                             int cap) {
+                                                             int cap, SpillArgs sp) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  auto body = [&](int64_t tile) {
+  const int64_t r0 = tile * 64;
   int64_t B0, B1, beg, end;
   bool live;
   const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
   const int mis = (int)(reinterpret_cast<uintptr_t>(in + B0) & 15);
   const int64_t total = mis + (B1 - B0);
   if (!sane || (mis & 3) || total > cap) {
+    if (!SPILL && sane && !(mis & 3) && total <= sp.cap) {  // spill: the big-image launch takes it
+      if (threadIdx.x == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
+      return;
+    }
     dec_record<WRITE>(L, prog, cols, r0 + lane, live, in + beg, end - beg, status);
     return;
   }
@@ -1739,7 +1772,18 @@ __global__ __launch_bounds__(64) void var_decode_tile_kernel(VarLaunch L, const 
   }
   __syncthreads();
   dec_record<WRITE>(L, prog, cols, r0 + lane, live, lds + mis + (beg - B0), end - beg, status);
+  };
+  if (!SPILL) {
+    body(blockIdx.x);
+    return;
+  }
+  const int64_t count = *sp.count;  // tiles the main launch spilled
+  for (int64_t k = blockIdx.x; k < count; k += gridDim.x) {
+    body(sp.list[k]);
+    __syncthreads();
+  }
 }
+
 
 // ---------------------------------------------------------------------------
 // Flat varlen tile kernels: every top-level field FIXED/BOOL, STRING/BINARY or
@@ -1871,15 +1915,15 @@ __device__ __forceinline__ void flat_place(const VarFieldDev& f, bool staged, co
 // L.prof[tile * 8 + k] (debug timeline, FORY_ROWFMT_VARPROF=1).
 #define FLAT_STAMP(k)                                                                            \
   do {                                                                                          \
-    if (PROF && tid == 0) L.prof[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();      \
+    if (PROF && tid == 0) L.prof[tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime();            \
   } while (0)
 
-template <bool FRAME, int NW, bool PROF = false>
+template <bool FRAME, int NW, bool PROF, bool SPILL>
 __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
                                                                   const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
                                                                   const int64_t* __restrict__ offs,
                                                                   uint8_t* __restrict__ out, int64_t capacity,
-                                                                  int32_t* status, int cap) {
+                                                                  int32_t* status, int cap, SpillArgs sp) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int HDR = FRAME ? 12 : 0;
   const int stg_bytes = L.stg_bytes;
@@ -1887,8 +1931,9 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   int32_t* pos = reinterpret_cast<int32_t*>(lds + cap + NW * stg_bytes);  // [num_var][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  auto body = [&](int64_t tile) {
   FLAT_STAMP(0);
-  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  const int64_t r0 = tile * 64;
   int64_t B0, B1, beg, end;
   bool live;
   const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
@@ -1900,6 +1945,10 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
   const int64_t total = mis + (B1 - B0);
   if (!sane || (mis & 3) || total > cap) {
+    if (!SPILL && sane && !(mis & 3) && total <= sp.cap) {  // spill: the big-image launch takes it
+      if (threadIdx.x == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
+      return;
+    }
     if (wave == 0 && live) enc_record(L, prog, cols, r0 + lane, out + beg, end - beg);
     return;
   }
@@ -2020,7 +2069,18 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   }
   if (PROF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   FLAT_STAMP(7);
+  };
+  if (!SPILL) {
+    body(blockIdx.x);
+    return;
+  }
+  const int64_t count = *sp.count;  // tiles the main launch spilled
+  for (int64_t k = blockIdx.x; k < count; k += gridDim.x) {
+    body(sp.list[k]);
+    __syncthreads();
+  }
 }
+
 
 __device__ __forceinline__ int64_t wave_incl_scan64(int64_t x, int lane) {
 #pragma unroll
@@ -2112,20 +2172,21 @@ __device__ __forceinline__ void flat_dec_fixed(const VarLaunch& L, const FixedFi
   }
 }
 
-template <bool FRAME, bool WRITE, int NW>
+template <bool FRAME, bool WRITE, int NW, bool SPILL>
 __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
                                                                   const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
                                                                   const uint8_t* __restrict__ in,
                                                                   const int64_t* __restrict__ offs,
                                                                   int64_t* __restrict__ tile_tot, int32_t* status,
-                                                                  int cap) {
+                                                                  int cap, SpillArgs sp) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int HDR = FRAME ? 12 : 0;
   const int stg_bytes = L.stg_bytes;
   uint8_t* img = lds;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  auto body = [&](int64_t tile) {
+  const int64_t r0 = tile * 64;
   int64_t B0, B1, beg, end;
   bool live;
   const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
@@ -2133,6 +2194,10 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   const int64_t total = mis + (B1 - B0);
   const int64_t tiles = (L.num_rows + 63) / 64;
   if (!sane || (mis & 3) || total > cap) {  // per-lane path on global rows (one wave)
+    if (!SPILL && sane && !(mis & 3) && total <= sp.cap) {  // spill: the big-image launch takes it
+      if (threadIdx.x == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
+      return;
+    }
     if (wave == 0) {
       const uint8_t* fp = in + beg;
       const uint8_t* row = fp + HDR;
@@ -2149,7 +2214,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
         if (!bad) flat_var_slot(L, vf[v], row, row_len, &rel, &n, !WRITE, status);
         if (!WRITE) {
           const int64_t sum = wave_sum64(n);
-          if (lane == 0) tile_tot[v * (tiles + 1) + blockIdx.x] = sum;
+          if (lane == 0) tile_tot[v * (tiles + 1) + tile] = sum;
         } else {
           const int64_t base = vf[v].out_offsets[r0];
           const int64_t excl = wave_incl_scan64(n, lane) - n;
@@ -2204,7 +2269,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
       int64_t rel = 0, n = 0;
       if (!bad) flat_var_slot(L, vf[v], row, row_len, &rel, &n, true, status);
       const int64_t sum = wave_sum64(n);
-      if (lane == 0) tile_tot[v * (tiles + 1) + blockIdx.x] = sum;
+      if (lane == 0) tile_tot[v * (tiles + 1) + tile] = sum;
     }
     return;
   }
@@ -2296,7 +2361,18 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
       }
     }
   }
+  };
+  if (!SPILL) {
+    body(blockIdx.x);
+    return;
+  }
+  const int64_t count = *sp.count;  // tiles the main launch spilled
+  for (int64_t k = blockIdx.x; k < count; k += gridDim.x) {
+    body(sp.list[k]);
+    __syncthreads();
+  }
 }
+
 
 template <typename K>
 void raise_lds_cap(K* kernel) {
@@ -2715,30 +2791,80 @@ size_t flat_lds(const VarLaunch& L, int cap, int nw) {
   return (size_t)cap + (size_t)nw * L.stg_bytes + (size_t)L.num_var * 64 * sizeof(int32_t);
 }
 
+// LDS image of the spill launches: 3x the main image, in [32, 96] KiB
+// (FORY_ROWFMT_SPILLCAP overrides, for tests).
+int spill_cap(int cap) {
+  const char* e = getenv("FORY_ROWFMT_SPILLCAP");
+  int c = e ? atoi(e) : 3 * cap;
+  if (!e) c = c < 32 * 1024 ? 32 * 1024 : (c > 96 * 1024 ? 96 * 1024 : c);
+  return c < 1024 ? 1024 : (c > 128 * 1024 ? 128 * 1024 : c);
+}
+
+SpillArgs spill_args(const VarLaunch& L, int cap) { return SpillArgs{L.spill, L.spill_count, spill_cap(cap), 0}; }
+
+// Persistent spill grid: resident workgroups at the spill image size.
+template <typename K>
+unsigned spill_grid(K* k, const VarLaunch& L, size_t lds, int wg) {
+  return (unsigned)persistent_grid(k, lds, (L.num_rows + 63) / 64, wg);
+}
+
+template <bool FRAME, int NW, bool PROF>
+void launch_flat_enc_t(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
+                       int cap, hipStream_t s) {
+  const SpillArgs sp = spill_args(L, cap);
+  (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
+  auto* k = &var_encode_flat_kernel<FRAME, NW, PROF, false>;
+  var_tile_launch(k, L, cap);
+  hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds(L, cap, NW), s, L, L.prog,
+                     L.cols, L.fix, L.vf, offs, out, capacity, status, cap, sp);
+  auto* k2 = &var_encode_flat_kernel<FRAME, NW, PROF, true>;
+  var_tile_launch(k2, L, sp.cap);
+  hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
+                     flat_lds(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, offs, out, capacity, status, sp.cap,
+                     sp);
+}
+
 template <bool FRAME, int NW>
 void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                      int cap, hipStream_t s) {
-  auto* k = L.prof ? &var_encode_flat_kernel<FRAME, NW, true> : &var_encode_flat_kernel<FRAME, NW, false>;
-  var_tile_launch(k, L, cap);
-  hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds(L, cap, NW), s, L, L.prog,
-                     L.cols, L.fix, L.vf, offs, out, capacity, status, cap);
+  if (L.prof) launch_flat_enc_t<FRAME, NW, true>(L, offs, out, capacity, status, cap, s);
+  else launch_flat_enc_t<FRAME, NW, false>(L, offs, out, capacity, status, cap, s);
 }
 
 template <bool FRAME, bool WRITE, int NW>
 void launch_flat_dec(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int64_t* tile_tot,
                      int32_t* status, int cap, hipStream_t s) {
-  auto* k = &var_decode_flat_kernel<FRAME, WRITE, NW>;
+  const SpillArgs sp = spill_args(L, cap);
+  (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
+  auto* k = &var_decode_flat_kernel<FRAME, WRITE, NW, false>;
   var_tile_launch(k, L, cap);
   const size_t lds = WRITE ? flat_lds(L, cap, NW) : (size_t)cap;  // pass 1 needs only the row image
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
-                     L.vf, rows, offs, tile_tot, status, cap);
+                     L.vf, rows, offs, tile_tot, status, cap, sp);
+  auto* k2 = &var_decode_flat_kernel<FRAME, WRITE, NW, true>;
+  var_tile_launch(k2, L, sp.cap);
+  const size_t lds2 = WRITE ? flat_lds(L, sp.cap, NW) : (size_t)sp.cap;
+  hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, lds2, 64 * NW)), dim3(64 * NW), lds2, s, L, L.prog, L.cols, L.fix,
+                     L.vf, rows, offs, tile_tot, status, sp.cap, sp);
+}
+
+// Encode: the caller's capacity (normally encoded_size's total) gives the mean
+// row size for free; the image holds 64 of them + 15 % unless the plan's
+// static estimate is larger (capped at 64 KiB).
+int enc_cap(const VarLaunch& L, int64_t capacity) {
+  int cap = var_cap(L);
+  if (getenv("FORY_ROWFMT_VARCAP") || L.num_rows < 64) return cap;
+  const int64_t mean = capacity / L.num_rows;
+  const int64_t hint = (64 * mean * 115 / 100 + 1023) / 1024 * 1024;
+  if (hint > cap) cap = (int)(hint < 64 * 1024 ? hint : 64 * 1024);
+  return cap;
 }
 
 hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity,
                              int32_t* status, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
   if (var_tiles() && var_flat(L)) {
-    const int cap = var_cap(L);
+    const int cap = enc_cap(L, capacity);
     const int nw = flat_nw();
     if (L.frame) {
       if (nw == 8) launch_flat_enc<true, 8>(L, offs, out, capacity, status, cap, s);
@@ -2750,10 +2876,16 @@ hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* o
     return hipGetLastError();
   }
   if (var_tiles()) {
-    const int cap = var_cap(L);
-    var_tile_launch(&var_encode_tile_kernel, L, cap);
-    hipLaunchKernelGGL(var_encode_tile_kernel, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64), (size_t)cap, s,
-                       L, L.prog, L.cols, offs, out, capacity, status, cap);
+    const int cap = enc_cap(L, capacity);
+    const SpillArgs sp = spill_args(L, cap);
+    (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
+    var_tile_launch(&var_encode_tile_kernel<false>, L, cap);
+    hipLaunchKernelGGL(var_encode_tile_kernel<false>, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64),
+                       (size_t)cap, s, L, L.prog, L.cols, offs, out, capacity, status, cap, sp);
+    var_tile_launch(&var_encode_tile_kernel<true>, L, sp.cap);
+    hipLaunchKernelGGL(var_encode_tile_kernel<true>,
+                       dim3(spill_grid(&var_encode_tile_kernel<true>, L, (size_t)sp.cap, 64)), dim3(64),
+                       (size_t)sp.cap, s, L, L.prog, L.cols, offs, out, capacity, status, sp.cap, sp);
     return hipGetLastError();
   }
   const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
@@ -2780,9 +2912,15 @@ hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const
   }
   if (var_tiles()) {
     const int cap = var_cap(L);
-    var_tile_launch(&var_decode_tile_kernel<WRITE>, L, cap);
-    hipLaunchKernelGGL(var_decode_tile_kernel<WRITE>, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64),
-                       (size_t)cap, s, L, L.prog, L.cols, rows, offs, status, cap);
+    const SpillArgs sp = spill_args(L, cap);
+    (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
+    var_tile_launch(&var_decode_tile_kernel<WRITE, false>, L, cap);
+    hipLaunchKernelGGL((var_decode_tile_kernel<WRITE, false>), dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64),
+                       (size_t)cap, s, L, L.prog, L.cols, rows, offs, status, cap, sp);
+    var_tile_launch(&var_decode_tile_kernel<WRITE, true>, L, sp.cap);
+    hipLaunchKernelGGL((var_decode_tile_kernel<WRITE, true>),
+                       dim3(spill_grid(&var_decode_tile_kernel<WRITE, true>, L, (size_t)sp.cap, 64)), dim3(64),
+                       (size_t)sp.cap, s, L, L.prog, L.cols, rows, offs, status, sp.cap, sp);
     return hipGetLastError();
   }
   const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
@@ -2794,6 +2932,8 @@ hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const
 bool var_decode_tiled_offsets(const VarLaunch& L) { return L.num_rows > 0 && var_tiles() && var_flat(L); }
 
 int64_t var_tile_totals_words(int64_t num_var, int64_t n) { return num_var * ((n + 63) / 64 + 1); }
+
+int64_t var_spill_words(int64_t n) { return (n + 63) / 64 + 4; }
 
 hipError_t launch_var_decode_lengths(const VarLaunch& L, const uint8_t* rows, const int64_t* offs,
                                      int64_t* tile_tot, int64_t* partials, int32_t* status, hipStream_t s) {

@@ -25,15 +25,14 @@ ws = enc.workspace(n)
 arr = native.column_array(cols)
 status = torch.zeros(1, dtype=torch.int32, device=dev)
 variants = {"global": {"FORY_ROWFMT_VARTILE": "0"}, "tile": {"FORY_ROWFMT_VARFLAT": "0"}, "flat": {},
-            "flat_nw8": {"FORY_ROWFMT_VARNW": "8"}, "flat_stg4k": {"FORY_ROWFMT_VARSTG": "4096"},
-            "flat_cap40k": {"FORY_ROWFMT_VARCAP": "40960"}, "flat_nw8_cap40k": {"FORY_ROWFMT_VARNW": "8",
-                                                                                "FORY_ROWFMT_VARCAP": "40960"}}
+            "cap12k": {"FORY_ROWFMT_VARCAP": "12288"}, "cap24k": {"FORY_ROWFMT_VARCAP": "24576"},
+            "flat_nw8": {"FORY_ROWFMT_VARNW": "8"}, "flat_cap48k": {"FORY_ROWFMT_VARCAP": "49152"}}
 res = {}
 
 
 def set_env(envs):
     for k in ("FORY_ROWFMT_VARTILE", "FORY_ROWFMT_VARCAP", "FORY_ROWFMT_VARFLAT", "FORY_ROWFMT_VARNW",
-              "FORY_ROWFMT_VARSTG"):
+              "FORY_ROWFMT_VARSTG", "FORY_ROWFMT_SPILLCAP"):
         os.environ.pop(k, None)
     os.environ.update(envs)
 
@@ -68,7 +67,7 @@ for frame in (0, 1):
                 ref_rows = out.clone()
             else:
                 rows_ok = bool(torch.equal(out, ref_rows))
-            dec_ok = all(col_bytes_equal(a, b) for a, b in zip(dcols, cols)) if config == "mixed40" else None
+            dec_ok = all(col_bytes_equal(a, b) for a, b in zip(dcols, cols)) if config.startswith("mixed40") else None
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             te, td = [], []
             for _ in range(iters):

@@ -62,16 +62,20 @@ VARLEN = [k for k, (sch, _) in catalog().items()
 FIXED = [k for k in catalog() if k not in VARLEN]
 
 
-@pytest.fixture(params=["flat", "flat_nw8", "flat_stg256", "tile", "global", "smallcap"])
+@pytest.fixture(params=["flat", "flat_nw8", "flat_stg256", "tile", "global", "spill", "nocap", "tile_nocap"])
 def varlen_engine(request, monkeypatch):
     """Varlen engines: flat cooperative tile kernels (default for flat plans), the
     generic one-wave tile interpreter (FORY_ROWFMT_VARFLAT=0), the per-record global
-    interpreter (FORY_ROWFMT_VARTILE=0), and a 2 KiB LDS image so most tiles take the
-    per-record fallback inside the tile kernels; flat with 8 waves per tile, and with a
+    interpreter (FORY_ROWFMT_VARTILE=0); a 2 KiB LDS image so tiles spill to the second
+    (big-image) launch; 2 KiB for both launches so tiles take the per-record global path
+    inside the tile kernels (flat and generic); flat with 8 waves per tile, and with a
     256-byte staging buffer (most spans take the per-lane copy)."""
     env = {"flat": {}, "flat_nw8": {"FORY_ROWFMT_VARNW": "8"}, "flat_stg256": {"FORY_ROWFMT_VARSTG": "256"},
            "tile": {"FORY_ROWFMT_VARFLAT": "0"}, "global": {"FORY_ROWFMT_VARTILE": "0"},
-           "smallcap": {"FORY_ROWFMT_VARCAP": "2048"}}[request.param]
+           "spill": {"FORY_ROWFMT_VARCAP": "2048"},
+           "nocap": {"FORY_ROWFMT_VARCAP": "2048", "FORY_ROWFMT_SPILLCAP": "2048"},
+           "tile_nocap": {"FORY_ROWFMT_VARFLAT": "0", "FORY_ROWFMT_VARCAP": "2048",
+                          "FORY_ROWFMT_SPILLCAP": "2048"}}[request.param]
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     return request.param
