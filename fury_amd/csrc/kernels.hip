@@ -490,11 +490,15 @@ __global__ __launch_bounds__(4 * R, 1) void encode_fixed_v3_kernel(FixedLaunch L
 // address), so hipcc can wait with a counted vmcnt for the older set while
 // the younger set stays in flight. Order per stage: write X -> barrier ->
 // store this tile's rows -> issue X for tile + 2*grid -> barrier.
-template <int R, int K>
+template <int R, int K, int NT = 0>
 __device__ __forceinline__ void v5_issue(const uint8_t* const (&ptr)[K], const int (&wk)[K], int64_t r0,
                                          u32x4 (&d)[K]) {
 #pragma unroll
-  for (int k = 0; k < K; ++k) d[k] = *gp(reinterpret_cast<const u32x4*>(ptr[k] + r0 * wk[k]));
+  for (int k = 0; k < K; ++k) {
+    const GAS u32x4* a = gp(reinterpret_cast<const u32x4*>(ptr[k] + r0 * wk[k]));
+    if constexpr (NT & 1) d[k] = __builtin_nontemporal_load(a);  // once-read column stream
+    else d[k] = *a;
+  }
 }
 
 template <int R, int K, bool FRAME, bool PAD>
@@ -527,7 +531,7 @@ __device__ __forceinline__ void v5_write(uint8_t* lds, int pitch, int hdr_bm, co
   }
 }
 
-template <int R, int WG, bool PAD>
+template <int R, int WG, bool PAD, int NT = 0>
 __device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* lds, int pitch, uint8_t* dst, int tid) {
   const int stride = L.stride;
   const int bytes = R * stride;
@@ -547,8 +551,11 @@ __device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* ld
       *gp(reinterpret_cast<u32x4*>(dst + c * 16)) = y;
     }
   } else {
-    for (; c < n16; c += WG)
-      *gp(reinterpret_cast<u32x4*>(dst + c * 16)) = *reinterpret_cast<const u32x4*>(lds + c * 16);
+    for (; c < n16; c += WG) {
+      const u32x4 y = *reinterpret_cast<const u32x4*>(lds + c * 16);
+      if constexpr (NT & 2) __builtin_nontemporal_store(y, gp(reinterpret_cast<u32x4*>(dst + c * 16)));
+      else *gp(reinterpret_cast<u32x4*>(dst + c * 16)) = y;
+    }
     const int tail4 = (bytes & 15) >> 2;
     if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
   }
@@ -558,7 +565,7 @@ __device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* ld
 // dispatched in tile order, so the addresses in flight chip-wide stay a
 // compact window; persistent grids drift apart (scripts/microbench/copybw.hip:
 // one-shot 16-B copy 6.25 TB/s vs 5.2-5.6 TB/s for grid-stride loops).
-template <int R, int WG, int K, bool FRAME, bool PAD, bool ONESHOT = false>
+template <int R, int WG, int K, bool FRAME, bool PAD, bool ONESHOT = false, int NT = 0>
 __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
                                                                  const FixedFieldDev* __restrict__ fields,
                                                                  uint8_t* __restrict__ out, int64_t tiles) {
@@ -596,27 +603,27 @@ __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
   if (tid < R) put_header<FRAME>(lds + tid * pitch, L);  // constant across tiles (no nullable fields)
   u32x4 dA[K], dB[K];
   if constexpr (ONESHOT) {
-    v5_issue<R, K>(ptr, wk, t * R, dA);
+    v5_issue<R, K, NT>(ptr, wk, t * R, dA);
     v5_write<R, K, FRAME, PAD>(lds, pitch, hdr_bm, wk, sf, dA);
     __syncthreads();
-    v5_store<R, WG, PAD>(L, lds, pitch, out + t * R * stride, tid);
+    v5_store<R, WG, PAD, NT>(L, lds, pitch, out + t * R * stride, tid);
     return;
   }
   const int64_t last = tiles - 1;
-  v5_issue<R, K>(ptr, wk, t * R, dA);
-  v5_issue<R, K>(ptr, wk, min(t + (int64_t)gridDim.x, last) * R, dB);
+  v5_issue<R, K, NT>(ptr, wk, t * R, dA);
+  v5_issue<R, K, NT>(ptr, wk, min(t + (int64_t)gridDim.x, last) * R, dB);
   for (;;) {
     v5_write<R, K, FRAME, PAD>(lds, pitch, hdr_bm, wk, sf, dA);
     __syncthreads();
-    v5_store<R, WG, PAD>(L, lds, pitch, out + t * R * stride, tid);
-    v5_issue<R, K>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dA);
+    v5_store<R, WG, PAD, NT>(L, lds, pitch, out + t * R * stride, tid);
+    v5_issue<R, K, NT>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dA);
     __syncthreads();
     t += gridDim.x;
     if (t >= tiles) break;
     v5_write<R, K, FRAME, PAD>(lds, pitch, hdr_bm, wk, sf, dB);
     __syncthreads();
-    v5_store<R, WG, PAD>(L, lds, pitch, out + t * R * stride, tid);
-    v5_issue<R, K>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dB);
+    v5_store<R, WG, PAD, NT>(L, lds, pitch, out + t * R * stride, tid);
+    v5_issue<R, K, NT>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dB);
     __syncthreads();
     t += gridDim.x;
     if (t >= tiles) break;
@@ -767,6 +774,8 @@ __global__ __launch_bounds__(4 * R, 4) void encode_fixed_v4_kernel(FixedLaunch L
 // ---------------------------------------------------------------------------
 // LDS-DMA of `bytes` contiguous bytes into the LDS image (1 KiB per wave
 // instruction; lanes past the end masked off).
+// NT & 4: non-temporal policy (aux = 2) on the once-read row stream.
+template <int NT = 0>
 __device__ __forceinline__ void dma_tile(uint8_t* lds, const uint8_t* __restrict__ src, int bytes, int tid, int wave) {
   const int n16 = bytes >> 4;
   for (int c0 = 0; c0 < n16; c0 += kWG) {
@@ -774,7 +783,7 @@ __device__ __forceinline__ void dma_tile(uint8_t* lds, const uint8_t* __restrict
     if (c < n16)
       __builtin_amdgcn_global_load_lds((const GAS void*)(src + (int64_t)c * 16),
                                        (__attribute__((address_space(3))) void*)(lds + (c0 + wave * 64) * 16), 16,
-                                       0, 0);
+                                       0, (NT & 4) ? 2 : 0);
   }
   const int tail4 = (bytes & 15) >> 2;
   if (tid < tail4) st32(lds + n16 * 16 + tid * 4, ld32(src + n16 * 16 + tid * 4));
@@ -815,7 +824,7 @@ __device__ __forceinline__ void put_validity(const FixedFieldDev& fd, bool isnul
 
 // Decodes slot values of one width group: null -> 0 (RowEncoderBuilder.java:239-246),
 // bool -> 0/1 (MemoryBuffer.getBoolean), coalesced column stores.
-template <int W, int TR, bool FRAME>
+template <int W, int TR, bool FRAME, int NT = 0>
 __device__ __forceinline__ void dec_group(const FixedFieldDev* __restrict__ fields, int g0, int g1, int wave, int fsub,
                                           int r, const uint8_t* row, int hdr_bm, int hdr, bool live, int64_t grow,
                                           int64_t r0, int rows) {
@@ -843,14 +852,21 @@ __device__ __forceinline__ void dec_group(const FixedFieldDev* __restrict__ fiel
         const FixedFieldDev& fd = fields[p];
         uint64_t v = nul[u] ? 0 : x[u];
         if (fd.flags & 2) v = (v & 0xff) ? 1 : 0;
-        if (live) stw<W>(fd.out_values, grow, v);
+        if (live) {
+          if constexpr ((NT & 8) && W >= 4) {  // non-temporal column stores
+            if constexpr (W == 8) __builtin_nontemporal_store(v, gp(reinterpret_cast<uint64_t*>(fd.out_values)) + grow);
+            else __builtin_nontemporal_store((uint32_t)v, gp(reinterpret_cast<uint32_t*>(fd.out_values)) + grow);
+          } else {
+            stw<W>(fd.out_values, grow, v);
+          }
+        }
         if ((fd.flags & 1) && fd.out_validity) put_validity<TR>(fd, nul[u], live, r, fsub, r0, rows);
       }
     }
   }
 }
 
-template <int TR, bool FRAME>
+template <int TR, bool FRAME, int NT = 0>
 __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
                                                            const uint8_t* __restrict__ in, int32_t* status) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -866,7 +882,7 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
   const int stride = L.stride;
   const int hdr_bm = HDR + L.bitmap_bytes;
 
-  dma_tile(lds, in + r0 * stride, rows * stride, tid, wave);
+  dma_tile<NT>(lds, in + r0 * stride, rows * stride, tid, wave);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -874,10 +890,10 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
   const int64_t grow = r0 + r;
   const bool live = r < rows;
   if (FRAME && wave == 0 && fsub == 0 && live) check_frame<FRAME>(row, L, status);
-  dec_group<8, TR, FRAME>(fields, L.group[0], L.group[1], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
-  dec_group<4, TR, FRAME>(fields, L.group[1], L.group[2], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
-  dec_group<2, TR, FRAME>(fields, L.group[2], L.group[3], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
-  dec_group<1, TR, FRAME>(fields, L.group[3], L.group[4], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<8, TR, FRAME, NT>(fields, L.group[0], L.group[1], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<4, TR, FRAME, NT>(fields, L.group[1], L.group[2], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<2, TR, FRAME, NT>(fields, L.group[2], L.group[3], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<1, TR, FRAME, NT>(fields, L.group[3], L.group[4], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
 }
 
 // Decode v2: one tile of TR records (TR a multiple of 64) per workgroup of WG
@@ -2460,11 +2476,21 @@ hipError_t launch_encode_v4(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int R, int WG, int K, bool FRAME, bool PAD, bool ONESHOT = false>
+// Cache-policy bits (FORY_ROWFMT_NT, for A/B): 1 nt column loads / 2 nt row
+// stores (encode v5), 4 nt LDS-DMA row loads / 8 nt column stores (decode).
+// Default 2|4|8: at 64M Struct104 rows nt row stores take encode 18.43 ->
+// 18.03 ms, nt loads + stores take decode 17.72 -> 17.52 ms; nt column loads
+// in encode are slower (18.60 ms) (scripts/ab_nt.py, profiles/r01/ab_nt.json).
+int nt_mode() {
+  const char* e = getenv("FORY_ROWFMT_NT");
+  return e ? atoi(e) : 14;
+}
+
+template <int R, int WG, int K, bool FRAME, bool PAD, bool ONESHOT = false, int NT = 0>
 hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const int64_t full = L.num_rows / R;
   if (full > 0) {
-    auto* k = &encode_fixed_v5_kernel<R, WG, K, FRAME, PAD, ONESHOT>;
+    auto* k = &encode_fixed_v5_kernel<R, WG, K, FRAME, PAD, ONESHOT, NT>;
     static bool init = false;
     if (!init) { raise_lds_cap(k); init = true; }
     const size_t lds = (size_t)R * (PAD ? L.pitch : L.stride);
@@ -2505,7 +2531,15 @@ hipError_t try_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s, int 
   if (var == 5 && (i64 + 3) / 4 <= 12) V5(64, 256, 12);
   else if (var == 6 && (i128 + 7) / 8 <= 12) V5(128, 512, 12);
   else if (var == 7 && (i128 + 15) / 16 <= 6) V5(128, 1024, 6);
-  else if (var == 8 && (i64 + 7) / 8 <= 6) V5(64, 512, 6);
+  else if (var == 8 && (i64 + 7) / 8 <= 6 && !pad) {
+    switch (nt_mode() & 3) {
+      case 1: e = launch_encode_v5<64, 512, 6, FRAME, false, false, 1>(P, out, s); break;
+      case 2: e = launch_encode_v5<64, 512, 6, FRAME, false, false, 2>(P, out, s); break;
+      case 3: e = launch_encode_v5<64, 512, 6, FRAME, false, false, 3>(P, out, s); break;
+      default: e = launch_encode_v5<64, 512, 6, FRAME, false, false, 0>(P, out, s); break;
+    }
+    *done = true;
+  } else if (var == 8 && (i64 + 7) / 8 <= 6) V5(64, 512, 6);
   else if (var == 9 && (i64 + 7) / 8 <= 6) {  // one-shot shapes
     e = launch_encode_v5<64, 512, 6, FRAME, false, true>(P, out, s);
     *done = true;
@@ -2642,8 +2676,15 @@ hipError_t launch_decode_tr(const FixedLaunch& L, const uint8_t* in, int32_t* st
     }
   }
   auto* k = &decode_fixed_kernel<TR, FRAME>;
-  static bool init = false;
-  if (!init) { raise_lds_cap(k); init = true; }
+  int nt = 0;
+  if constexpr (TR == 64) {
+    nt = (nt_mode() & 12) >> 2;
+    if (nt == 1) k = &decode_fixed_kernel<TR, FRAME, 4>;
+    else if (nt == 2) k = &decode_fixed_kernel<TR, FRAME, 8>;
+    else if (nt == 3) k = &decode_fixed_kernel<TR, FRAME, 12>;
+  }
+  static bool init[4] = {false, false, false, false};
+  if (!init[nt]) { raise_lds_cap(k); init[nt] = true; }
   hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(kWG), lds, s, L, L.fields, in, status);
   return hipGetLastError();
 }
