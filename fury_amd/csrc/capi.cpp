@@ -51,7 +51,16 @@ int64_t table_bytes(const Plan& p) {
   return align_up((int64_t)p.nodes.size() * (int64_t)sizeof(ColumnDev)) +
          align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::Op)) +
          align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::VarFieldDev)) +
-         align_up((int64_t)p.top.size() * (int64_t)sizeof(FixedFieldDev));
+         align_up((int64_t)p.program.size() * (int64_t)sizeof(FixedFieldDev)) +
+         align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::StructDev));
+}
+
+// STRING/BINARY/LIST fields at any struct level (the tile kernels' var fields).
+int64_t num_var_ops(const Plan& p) {
+  int64_t n = 0;
+  for (const fory_amd::Op& op : p.program)
+    if (op.code == fory_amd::OP_BYTES || op.code == fory_amd::OP_LIST) ++n;
+  return n;
 }
 
 bool use_tiled(const Plan& p, int frame) {
@@ -223,13 +232,32 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   const int64_t col_bytes = align_up((int64_t)cd.size() * (int64_t)sizeof(ColumnDev));
   const int64_t prog_bytes = align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::Op));
   const int64_t idx_bytes = align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::VarFieldDev));
-  // flat plans: var-field descriptors (field order) and the width-sorted fixed-field table
+  const int64_t fix_bytes = align_up((int64_t)p.program.size() * (int64_t)sizeof(FixedFieldDev));
+  // tile kernels: var-field descriptors (program order), the width-sorted
+  // fixed-field table and the struct table, each field tagged with its
+  // enclosing struct (0 = the row)
   std::vector<fory_amd::VarFieldDev> var;
   std::vector<FixedFieldDev> fix;
-  bool flat = true;
+  std::vector<fory_amd::StructDev> st;
+  std::vector<int32_t> stack{0};
   for (size_t k = 0; k < p.program.size(); ++k) {
     const fory_amd::Op& op = p.program[k];
-    if (op.code == fory_amd::OP_FIXED) {
+    const int32_t parent = stack.back();
+    if (op.code == fory_amd::OP_STRUCT_BEGIN) {
+      const fory_column& c = cols[op.b];
+      fory_amd::StructDev sd{};
+      sd.validity = (op.d & 1) ? c.validity : nullptr;
+      sd.out_validity = (op.d & 1) ? c.validity : nullptr;
+      sd.parent = parent;
+      sd.slot = op.a;
+      sd.nfields = op.c;
+      sd.hdr = (int32_t)(((op.c + 63) / 64) * 8);
+      sd.flags = op.d;
+      st.push_back(sd);
+      stack.push_back((int32_t)st.size());
+    } else if (op.code == fory_amd::OP_STRUCT_END) {
+      stack.pop_back();
+    } else if (op.code == fory_amd::OP_FIXED) {
       const fory_column& c = cols[op.b];
       FixedFieldDev f{};
       f.values = static_cast<const uint8_t*>(c.values);
@@ -239,6 +267,7 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
       f.width = op.c;
       f.flags = op.d;
       f.slot = op.a;
+      f.parent = parent;
       fix.push_back(f);
     } else if (op.code == fory_amd::OP_BYTES || op.code == fory_amd::OP_LIST) {
       const fory_column& c = cols[op.b];
@@ -249,6 +278,7 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
       v.out_validity = (op.d & 1) ? c.validity : nullptr;
       v.slot = op.a;
       v.flags = op.d;
+      v.parent = parent;
       if (op.code == fory_amd::OP_LIST) {
         const fory_column& it = cols[op.c];
         v.is_list = 1;
@@ -264,24 +294,26 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
         v.out_values = static_cast<uint8_t*>(c.values);
       }
       var.push_back(v);
-    } else {
-      flat = false;
     }
   }
   std::stable_sort(fix.begin(), fix.end(),
                    [](const FixedFieldDev& a, const FixedFieldDev& b) { return a.width > b.width; });
   std::vector<uint8_t> host((size_t)table_bytes(p), 0);
+  const int64_t o_var = col_bytes + prog_bytes, o_fix = o_var + idx_bytes, o_st = o_fix + fix_bytes;
   std::memcpy(host.data(), cd.data(), cd.size() * sizeof(ColumnDev));
   std::memcpy(host.data() + col_bytes, p.program.data(), p.program.size() * sizeof(fory_amd::Op));
-  std::memcpy(host.data() + col_bytes + prog_bytes, var.data(), var.size() * sizeof(fory_amd::VarFieldDev));
-  std::memcpy(host.data() + col_bytes + prog_bytes + idx_bytes, fix.data(), fix.size() * sizeof(FixedFieldDev));
+  std::memcpy(host.data() + o_var, var.data(), var.size() * sizeof(fory_amd::VarFieldDev));
+  std::memcpy(host.data() + o_fix, fix.data(), fix.size() * sizeof(FixedFieldDev));
+  std::memcpy(host.data() + o_st, st.data(), st.size() * sizeof(fory_amd::StructDev));
   rc = upload(ws, host.data(), (int64_t)host.size(), s);
   if (rc) return rc;
   uint8_t* wsb = static_cast<uint8_t*>(ws);
-  L->flat = flat && var.size() <= 32 ? 1 : 0;
+  L->flat = var.size() <= 32 && st.size() <= (size_t)fory_amd::kMaxTileStructs ? 1 : 0;
   L->num_var = (int32_t)var.size();
-  L->vf = reinterpret_cast<const fory_amd::VarFieldDev*>(wsb + col_bytes + prog_bytes);
-  L->fix = reinterpret_cast<const FixedFieldDev*>(wsb + col_bytes + prog_bytes + idx_bytes);
+  L->num_struct = (int32_t)st.size();
+  L->vf = reinterpret_cast<const fory_amd::VarFieldDev*>(wsb + o_var);
+  L->fix = reinterpret_cast<const FixedFieldDev*>(wsb + o_fix);
+  L->st = reinterpret_cast<const fory_amd::StructDev*>(wsb + o_st);
   {
     const int widths[4] = {8, 4, 2, 1};
     int at = 0;
@@ -323,7 +355,7 @@ int64_t* tile_totals_ptr(const Plan& p, void* ws, int64_t n) {
 // Spill list of the tile engines (after the tile totals): [count][pad x3][tiles].
 int32_t* spill_ptr(const Plan& p, void* ws, int64_t n) {
   return reinterpret_cast<int32_t*>(reinterpret_cast<uint8_t*>(tile_totals_ptr(p, ws, n)) +
-                                    align_up(fory_amd::var_tile_totals_words((int64_t)p.top.size(), n) * 8));
+                                    align_up(fory_amd::var_tile_totals_words(num_var_ops(p), n) * 8));
 }
 
 }  // namespace
@@ -377,7 +409,7 @@ int64_t fory_rowfmt_workspace_bytes(const fory_plan* plan, int64_t num_rows) {
   if (!plan) return -1;
   const int64_t n = num_rows < 0 ? 0 : num_rows;
   return table_bytes(plan->p) + align_up((fory_amd::scan_partials(n) + 2) * 8) +
-         align_up(fory_amd::var_tile_totals_words((int64_t)plan->p.top.size(), n) * 8) +
+         align_up(fory_amd::var_tile_totals_words(num_var_ops(plan->p), n) * 8) +
          align_up(fory_amd::var_spill_words(n) * 4);
 }
 

@@ -58,8 +58,10 @@ struct VarLaunch {
   int32_t num_var;              // top-level OP_BYTES / OP_LIST ops, field order
   int32_t stg_bytes;            // LDS staging per wave for one field's span
   int32_t fix_group[5];         // width groups [8][4][2][1] of `fix`
-  const FixedFieldDev* fix;     // device: top-level fixed fields, width-sorted
-  const VarFieldDev* vf;        // device: top-level var fields, field order
+  const FixedFieldDev* fix;     // device: fixed fields (any struct level), width-sorted
+  const VarFieldDev* vf;        // device: var fields (any struct level), program order
+  const StructDev* st;          // device: nested struct fields, pre-order (id = index + 1)
+  int32_t num_struct;
   uint64_t* prof;               // debug (FORY_ROWFMT_VARPROF): 8 timestamps per tile, else null
   int32_t* spill;               // workspace: tiles spilled to the big-image launch (ceil(n/64))
   int32_t* spill_count;         // workspace: number of spilled tiles

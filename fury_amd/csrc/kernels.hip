@@ -1841,6 +1841,23 @@ __device__ __forceinline__ void lds_copy_padded(uint8_t* dst, const uint8_t* src
   if (round8(n) > n4) st32(dst + n4, 0);
 }
 
+// LDS -> LDS copy of n bytes, any alignments: byte head to a 4-byte aligned
+// dst, funnel-shifted dwords, byte tail. Reads up to 4 bytes past the source.
+__device__ __forceinline__ void lds_copy_any(uint8_t* dst, const uint8_t* src, int n) {
+  int k = (int)((4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3);
+  if (k > n) k = n;
+  for (int j = 0; j < k; ++j) dst[j] = src[j];
+  const uint8_t* s = src + k;
+  const int sb = (int)(reinterpret_cast<uintptr_t>(s) & 3);
+  const uint8_t* s0 = s - sb;
+  const int m = (n - k) & ~3;
+  for (int j = 0; j < m; j += 4) {
+    const uint32_t a = ld32(s0 + j);
+    st32(dst + k + j, sb ? (a >> (8 * sb)) | (ld32(s0 + j + 4) << (32 - 8 * sb)) : a);
+  }
+  for (int j = k + m; j < n; ++j) dst[j] = src[j];
+}
+
 __device__ __forceinline__ void st64_lds(uint8_t* p, uint64_t v) {  // 4-byte aligned LDS
   st32(p, (uint32_t)v);
   st32(p + 4, (uint32_t)(v >> 32));
@@ -1853,9 +1870,11 @@ __device__ __forceinline__ void write_validity64(uint8_t* validity, int64_t r0, 
 // Fixed fields of width W (one width group of L.fix): column -> slot, batches of
 // kFixBatch loads per wave issued together (branch-free: clamped field index,
 // row 0 for idle lanes, nulls selected to 0 afterwards).
+// Fields of nested structs go to their child row (sbase, -1 = absent: skipped).
 template <int W, int NW>
-__device__ __forceinline__ void flat_enc_fixed(const FixedFieldDev* __restrict__ fix, int g0, int g1, int wave, bool live, int64_t i,
-                                               uint8_t* slots) {
+__device__ __forceinline__ void flat_enc_fixed(const VarLaunch& L, const FixedFieldDev* __restrict__ fix, int g0, int g1,
+                                               int wave, int lane, bool live, int64_t i, uint8_t* row,
+                                               const StructDev* __restrict__ st, const int32_t* sbase) {
   const int64_t ii = live ? i : 0;
   for (int k0 = g0 + wave * kFixBatch; k0 < g1; k0 += NW * kFixBatch) {
     uint64_t v[kFixBatch];
@@ -1872,7 +1891,12 @@ __device__ __forceinline__ void flat_enc_fixed(const FixedFieldDev* __restrict__
         const FixedFieldDev& f = fix[k0 + k];
         uint64_t x = ((vb[k] >> (ii & 7)) & 1) ? v[k] : 0;
         if (f.flags & 2) x = x ? 1 : 0;
-        st64_lds(slots + 8 * f.slot, x);
+        if (!f.parent) {
+          st64_lds(row + L.bitmap_bytes + 8 * f.slot, x);
+        } else {
+          const int32_t b = sbase[f.parent * 64 + lane];
+          if (b >= 0) st64_lds(row + b + st[f.parent - 1].hdr + 8 * f.slot, x);
+        }
       }
     }
   }
@@ -1885,7 +1909,7 @@ __device__ __forceinline__ bool flat_stage(const VarFieldDev& f, int stg_bytes, 
   const int64_t s0 = f.offsets[r0], s1 = f.offsets[r0 + rows];
   const int64_t S = (s1 - s0) * f.w;
   *s0_out = s0;
-  if ((f.iflags & 3) != 0 || S < 0 || S + 32 > stg_bytes) return false;
+  if ((f.iflags & 2) != 0 || S < 0 || S + 32 > stg_bytes) return false;  // bool items: per lane (0/1)
   const uint8_t* gsrc = f.values + s0 * f.w;
   const int phase = (int)(reinterpret_cast<uintptr_t>(gsrc) & 15);
   *phase_out = phase;
@@ -1906,6 +1930,15 @@ __device__ __forceinline__ void flat_place(const VarFieldDev& f, bool staged, co
   uint8_t* dst = row + p + (f.is_list ? 8 + bitmap_bytes(n) : 0);
   if (staged) {
     lds_copy_padded(dst, stg + phase + (e0 - s0) * w, n * w);
+    if (f.item_validity) {  // BinaryArrayWriter.setNullAt: item bit set, element left 0
+      uint8_t* abm = row + p + 8;
+      for (int64_t j = 0; j < n; ++j) {
+        const int64_t q = e0 + j;
+        if ((load_byte(f.item_validity + (q >> 3)) >> (q & 7)) & 1) continue;
+        abm[j >> 3] |= (uint8_t)(1u << (j & 7));
+        for (int b = 0; b < w; ++b) dst[j * w + b] = 0;
+      }
+    }
   } else if (!f.is_list) {
     copy_padded(dst, f.values + e0, n);
   } else {
@@ -1927,6 +1960,128 @@ __device__ __forceinline__ void flat_place(const VarFieldDev& f, bool staged, co
   }
 }
 
+// Layout of record i for plans with nested struct fields (wave 0 of the encode
+// tile kernel): the per-record program walk of enc_record without the value
+// copies. One writerIndex is shared by the row and its child rows
+// (BinaryRowWriter(schema, parent), BinaryRowWriter.java:54-62): a struct
+// field's child row starts at the writerIndex its field is reached
+// (serializeForBean, BaseBinaryEncoderBuilder.java:436-490), its fixed part
+// is reserved and zero-bitmapped there, its var payloads follow, and the
+// parent slot gets (offset relative to the parent, child size) at the END op.
+// Outputs: null bits and var/struct slot words in the LDS row image,
+// pos[v][lane] (payload offset from the row, -1 = none), sbase[s][lane]
+// (child row offset from the row, -1 = null/absent struct).
+__device__ __forceinline__ void flat_enc_layout_nested(const VarLaunch& L, const Op* __restrict__ prog,
+                                                       const ColumnDev* __restrict__ cols, bool live, int64_t i,
+                                                       int lane, uint8_t* row, int32_t* pos, int32_t* sbase) {
+  int32_t st_start[kMaxDepth], st_hdr[kMaxDepth];
+  int depth = 0;
+  st_start[0] = 0;
+  st_hdr[0] = L.bitmap_bytes;
+  int absent = live ? 0 : 1 << 20;
+  const int64_t ii = live ? i : 0;
+  int64_t wi = L.fixed_size;
+  int vi = 0, si = 0;  // wave-uniform: var field / struct ids in program order
+  for (int pc = 0; pc < L.num_ops; ++pc) {
+    const Op op = prog[pc];
+    const ColumnDev& c = cols[op.b];
+    const bool isnull = (op.d & 1) && !col_valid(c, ii);
+    uint8_t* base = row + st_start[depth];
+    uint8_t* slot = base + st_hdr[depth] + 8 * op.a;
+    switch (op.code) {
+      case OP_FIXED:  // BinaryWriter.setNullAt; the value phase writes the slot
+        if (!absent && isnull) set_null_bit(base, op.a);
+        break;
+      case OP_BYTES:
+      case OP_LIST: {
+        int32_t p = -1;
+        if (!absent) {
+          if (isnull) {
+            set_null_bit(base, op.a);
+            st64_lds(slot, 0);
+          } else {
+            const int64_t nn = (int64_t)c.offsets[ii + 1] - c.offsets[ii];
+            const int64_t rel = wi - st_start[depth];
+            if (op.code == OP_BYTES) {  // writeUnaligned: (offset<<32 | size), padded payload
+              st64_lds(slot, ((uint64_t)rel << 32) | (uint32_t)nn);
+              p = (int32_t)wi;
+              wi += round8(nn);
+            } else {  // BinaryArrayWriter.reset(n): [i64 n][null bitmap][n * w bytes, padded to 8]
+              const int32_t ahdr = 8 + bitmap_bytes(nn);
+              const int64_t size = ahdr + round8(nn * (op.e & 0xff));
+              st64_lds(row + wi, (uint64_t)nn);
+              for (int b = 8; b < ahdr; b += 4) st32(row + wi + b, 0);
+              st64_lds(slot, ((uint64_t)rel << 32) | (uint32_t)size);
+              p = (int32_t)wi;
+              wi += size;
+            }
+          }
+        }
+        pos[vi * 64 + lane] = p;
+        ++vi;
+        break;
+      }
+      case OP_STRUCT_BEGIN: {
+        ++si;
+        int32_t b = -1;
+        if (absent) {
+          ++absent;
+        } else if (isnull) {
+          set_null_bit(base, op.a);
+          st64_lds(slot, 0);
+          absent = 1;
+        } else {
+          ++depth;
+          st_start[depth] = (int32_t)wi;
+          st_hdr[depth] = bitmap_bytes(op.c);
+          for (int k = 0; k < st_hdr[depth]; k += 4) st32(row + wi + k, 0);
+          b = (int32_t)wi;
+          wi += st_hdr[depth] + 8LL * op.c;
+        }
+        sbase[si * 64 + lane] = b;
+        break;
+      }
+      case OP_STRUCT_END:
+        if (absent) {
+          --absent;
+        } else {
+          const int64_t sz = wi - st_start[depth];
+          const int32_t rel = st_start[depth] - st_start[depth - 1];
+          --depth;
+          st64_lds(row + st_start[depth] + st_hdr[depth] + 8 * op.a, ((uint64_t)(uint32_t)rel << 32) | (uint32_t)sz);
+        }
+        break;
+    }
+  }
+}
+
+// Child-row offsets of the staged record (decode; wave 0): struct s's row
+// starts at its parent's start + the offset in its slot (BinaryRow.getStruct,
+// UnsafeTrait.java:160-175); -1 when it or an ancestor is null. Struct ids are
+// pre-order, so parents come first. Writes the struct columns' validity.
+template <bool WRITE>
+__device__ __forceinline__ void flat_dec_struct_bases(const VarLaunch& L, const StructDev* __restrict__ st, bool bad,
+                                                      bool live, int lane, int64_t r0, int rows, const uint8_t* row,
+                                                      int64_t row_len, int32_t* sbase, int32_t* status) {
+  for (int s = 1; s <= L.num_struct; ++s) {
+    const StructDev& sd = st[s - 1];
+    const int32_t pb = sd.parent ? sbase[sd.parent * 64 + lane] : (bad ? -1 : 0);
+    const int32_t ph = sd.parent ? st[sd.parent - 1].hdr : L.bitmap_bytes;
+    int32_t b = -1;
+    if (pb >= 0 && !((row[pb + (sd.slot >> 3)] >> (sd.slot & 7)) & 1)) {
+      const uint8_t* sp = row + pb + ph + 8 * sd.slot;
+      const int64_t rel = (int32_t)ld32(sp + 4);
+      if (rel < 0 || pb + rel + sd.hdr + 8LL * sd.nfields > row_len) set_status(status, FORY_ERR_CORRUPT);
+      else b = (int32_t)(pb + rel);
+    }
+    sbase[s * 64 + lane] = b;
+    if (WRITE && sd.out_validity) {
+      const uint64_t m = __ballot(live && b >= 0);
+      if (lane == 0) write_validity64(sd.out_validity, r0, rows, m);
+    }
+  }
+}
+
 // PROF: thread 0 stamps s_memrealtime (100 MHz) at phase boundaries into
 // L.prof[tile * 8 + k] (debug timeline, FORY_ROWFMT_VARPROF=1).
 #define FLAT_STAMP(k)                                                                            \
@@ -1937,6 +2092,7 @@ __device__ __forceinline__ void flat_place(const VarFieldDev& f, bool staged, co
 template <bool FRAME, int NW, bool PROF, bool SPILL>
 __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
                                                                   const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
+                                                                  const StructDev* __restrict__ st,
                                                                   const int64_t* __restrict__ offs,
                                                                   uint8_t* __restrict__ out, int64_t capacity,
                                                                   int32_t* status, int cap, SpillArgs sp) {
@@ -1945,6 +2101,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   const int stg_bytes = L.stg_bytes;
   uint8_t* img = lds;
   int32_t* pos = reinterpret_cast<int32_t*>(lds + cap + NW * stg_bytes);  // [num_var][64]
+  int32_t* sbase = pos + L.num_var * 64;                                  // [1 + num_struct][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   auto body = [&](int64_t tile) {
@@ -1989,6 +2146,9 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
       }
       for (int b = 0; b < L.bitmap_bytes; b += 4) st32(row + b, 0);
     }
+    if (L.num_struct) {  // nested struct fields: program walk
+      flat_enc_layout_nested(L, prog, cols, live, i, lane, row, pos, sbase);
+    } else {
     // null bits of nullable fixed fields (this wave only: no bitmap races)
     const int nfix = L.fix_group[4];
     for (int k0 = 0; k0 < nfix; k0 += kFixBatch) {
@@ -2044,13 +2204,15 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
         pos[(v0 + k) * 64 + lane] = p;
       }
     }
+    }
   }
   FLAT_STAMP(2);
+  if (L.num_struct) __syncthreads();  // nested fixed slots need the child-row offsets
   // fixed slots (all waves): BinaryRowWriter.write(ordinal, v), null -> 0
-  flat_enc_fixed<8, NW>(fix, L.fix_group[0], L.fix_group[1], wave, live, i, slots);
-  flat_enc_fixed<4, NW>(fix, L.fix_group[1], L.fix_group[2], wave, live, i, slots);
-  flat_enc_fixed<2, NW>(fix, L.fix_group[2], L.fix_group[3], wave, live, i, slots);
-  flat_enc_fixed<1, NW>(fix, L.fix_group[3], L.fix_group[4], wave, live, i, slots);
+  flat_enc_fixed<8, NW>(L, fix, L.fix_group[0], L.fix_group[1], wave, lane, live, i, row, st, sbase);
+  flat_enc_fixed<4, NW>(L, fix, L.fix_group[1], L.fix_group[2], wave, lane, live, i, row, st, sbase);
+  flat_enc_fixed<2, NW>(L, fix, L.fix_group[2], L.fix_group[3], wave, lane, live, i, row, st, sbase);
+  flat_enc_fixed<1, NW>(L, fix, L.fix_group[3], L.fix_group[4], wave, lane, live, i, row, st, sbase);
   if (PROF) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   FLAT_STAMP(3);
   __syncthreads();
@@ -2129,20 +2291,41 @@ __global__ __launch_bounds__(kWG) void flat_tile_bases_kernel(const VarFieldDev*
   vf[v].out_offsets[t == tiles ? n : t * 64] = (int32_t)off;
 }
 
-// Reads a var field's slot of a staged record: returns payload (rel, n) with
-// n = bytes (STRING/BINARY) or elements (LIST); n = 0 when null/corrupt.
-__device__ __forceinline__ bool flat_var_slot(const VarLaunch& L, const VarFieldDev& f, const uint8_t* row,
+// Start and null-bitmap bytes of the row or child row holding a field of
+// struct `parent` (0 = the row; sbase: child-row offsets, -1 = absent).
+__device__ __forceinline__ int32_t field_base(const VarLaunch& L, const StructDev* __restrict__ st, int parent,
+                                              const int32_t* sbase, int lane, int32_t* hdr) {
+  if (!parent) {
+    *hdr = L.bitmap_bytes;
+    return 0;
+  }
+  *hdr = st[parent - 1].hdr;
+  return sbase[parent * 64 + lane];
+}
+
+// Reads a var field's slot of a staged record: returns payload (rel from the
+// row start, n) with n = bytes (STRING/BINARY) or elements (LIST); n = 0 when
+// null/absent/corrupt. Returns true when null or absent.
+__device__ __forceinline__ bool flat_var_slot(const VarLaunch& L, const VarFieldDev& f, const StructDev* __restrict__ st,
+                                              const int32_t* sbase, int lane, const uint8_t* row,
                                               int64_t row_len, int64_t* rel, int64_t* n, bool report,
                                               int32_t* status) {
   *rel = 0;
   *n = 0;
-  if ((row[f.slot >> 3] >> (f.slot & 7)) & 1) return true;  // BinaryRow.isNullAt
-  const uint8_t* sp = row + L.bitmap_bytes + 8 * f.slot;
+  int32_t hdr;
+  const int32_t base = field_base(L, st, f.parent, sbase, lane, &hdr);
+  if (base < 0) return true;  // inside a null struct
+  if ((row[base + (f.slot >> 3)] >> (f.slot & 7)) & 1) return true;  // BinaryRow.isNullAt
+  const uint8_t* sp = row + base + hdr + 8 * f.slot;
   const uint64_t os = ld32(sp) | ((uint64_t)ld32(sp + 4) << 32);
-  const int64_t r = (int32_t)(os >> 32);
+  const int64_t r = base + (int64_t)(int32_t)(os >> 32);  // offsets are relative to the enclosing row
+  if ((int32_t)(os >> 32) < 0) {
+    if (report) set_status(status, FORY_ERR_CORRUPT);
+    return false;
+  }
   if (!f.is_list) {
     const int64_t len = (int32_t)(uint32_t)os;
-    if (len < 0 || r < 0 || r + len > row_len) {
+    if (len < 0 || r + len > row_len) {
       if (report) set_status(status, FORY_ERR_CORRUPT);
       return false;
     }
@@ -2150,7 +2333,7 @@ __device__ __forceinline__ bool flat_var_slot(const VarLaunch& L, const VarField
     *n = len;
     return false;
   }
-  if (r < 0 || r + 8 > row_len) {
+  if (r + 8 > row_len) {
     if (report) set_status(status, FORY_ERR_CORRUPT);
     return false;
   }
@@ -2167,14 +2350,17 @@ __device__ __forceinline__ bool flat_var_slot(const VarLaunch& L, const VarField
 // Fixed fields of width W: slot (LDS) -> column, validity by ballot.
 template <int W, int NW>
 __device__ __forceinline__ void flat_dec_fixed(const VarLaunch& L, const FixedFieldDev* __restrict__ fix, int g0, int g1, int wave, int lane, bool live,
-                                               bool bad, int64_t i, int64_t r0, int rows, const uint8_t* row) {
+                                               bool bad, int64_t i, int64_t r0, int rows, const uint8_t* row,
+                                               const StructDev* __restrict__ st, const int32_t* sbase) {
   for (int k0 = g0 + wave * kFixBatch; k0 < g1; k0 += NW * kFixBatch) {
 #pragma unroll
     for (int k = 0; k < kFixBatch; ++k) {
       if (k0 + k < g1) {
         const FixedFieldDev& f = fix[k0 + k];
-        const bool nul = bad || ((row[f.slot >> 3] >> (f.slot & 7)) & 1);
-        const uint8_t* sp = row + L.bitmap_bytes + 8 * f.slot;
+        int32_t hdr;
+        const int32_t base = field_base(L, st, f.parent, sbase, lane, &hdr);
+        const bool nul = bad || base < 0 || ((row[base + (f.slot >> 3)] >> (f.slot & 7)) & 1);
+        const uint8_t* sp = row + (base < 0 ? 0 : base) + hdr + 8 * f.slot;
         uint64_t x = 0;
         if (!nul) x = (uint64_t)ld32(sp) | ((uint64_t)ld32(sp + 4) << 32);
         if (f.flags & 2) x = (x & 0xff) ? 1 : 0;
@@ -2191,6 +2377,7 @@ __device__ __forceinline__ void flat_dec_fixed(const VarLaunch& L, const FixedFi
 template <bool FRAME, bool WRITE, int NW, bool SPILL>
 __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
                                                                   const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
+                                                                  const StructDev* __restrict__ st,
                                                                   const uint8_t* __restrict__ in,
                                                                   const int64_t* __restrict__ offs,
                                                                   int64_t* __restrict__ tile_tot, int32_t* status,
@@ -2199,6 +2386,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   constexpr int HDR = FRAME ? 12 : 0;
   const int stg_bytes = L.stg_bytes;
   uint8_t* img = lds;
+  int32_t* sbase = reinterpret_cast<int32_t*>(lds + cap + (WRITE ? NW * stg_bytes : 0));  // [1 + num_struct][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   auto body = [&](int64_t tile) {
@@ -2225,9 +2413,14 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
         bad = h != (uint64_t)L.schema_hash || (int64_t)len + 4 != row_len || len < (uint32_t)(8 + L.fixed_size);
         row_len -= 12;
       }
+      if (L.num_struct) {
+        const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
+        flat_dec_struct_bases<false>(L, st, bad, live, lane, r0, rows, row, row_len, sbase, status);
+        wave_lds_sync();
+      }
       for (int v = 0; v < L.num_var; ++v) {
         int64_t rel = 0, n = 0;
-        if (!bad) flat_var_slot(L, vf[v], row, row_len, &rel, &n, !WRITE, status);
+        if (!bad) flat_var_slot(L, vf[v], st, sbase, lane, row, row_len, &rel, &n, !WRITE, status);
         if (!WRITE) {
           const int64_t sum = wave_sum64(n);
           if (lane == 0) tile_tot[v * (tiles + 1) + tile] = sum;
@@ -2280,20 +2473,24 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
     }
     row_len -= 12;
   }
+  if (L.num_struct) {  // child-row offsets (+ struct validity) for every wave
+    if (wave == 0) flat_dec_struct_bases<WRITE>(L, st, bad, live, lane, r0, rows, row, row_len, sbase, status);
+    __syncthreads();
+  }
   if (!WRITE) {  // pass 1: per-tile payload totals (scanned over tiles by the host launcher)
     for (int v = wave; v < L.num_var; v += NW) {
       int64_t rel = 0, n = 0;
-      if (!bad) flat_var_slot(L, vf[v], row, row_len, &rel, &n, true, status);
+      if (!bad) flat_var_slot(L, vf[v], st, sbase, lane, row, row_len, &rel, &n, true, status);
       const int64_t sum = wave_sum64(n);
       if (lane == 0) tile_tot[v * (tiles + 1) + tile] = sum;
     }
     return;
   }
   // fixed fields: slot -> column (UnsafeTrait.getInt32/... ; null -> 0), validity by ballot
-  flat_dec_fixed<8, NW>(L, fix, L.fix_group[0], L.fix_group[1], wave, lane, live, bad, i, r0, rows, row);
-  flat_dec_fixed<4, NW>(L, fix, L.fix_group[1], L.fix_group[2], wave, lane, live, bad, i, r0, rows, row);
-  flat_dec_fixed<2, NW>(L, fix, L.fix_group[2], L.fix_group[3], wave, lane, live, bad, i, r0, rows, row);
-  flat_dec_fixed<1, NW>(L, fix, L.fix_group[3], L.fix_group[4], wave, lane, live, bad, i, r0, rows, row);
+  flat_dec_fixed<8, NW>(L, fix, L.fix_group[0], L.fix_group[1], wave, lane, live, bad, i, r0, rows, row, st, sbase);
+  flat_dec_fixed<4, NW>(L, fix, L.fix_group[1], L.fix_group[2], wave, lane, live, bad, i, r0, rows, row, st, sbase);
+  flat_dec_fixed<2, NW>(L, fix, L.fix_group[2], L.fix_group[3], wave, lane, live, bad, i, r0, rows, row, st, sbase);
+  flat_dec_fixed<1, NW>(L, fix, L.fix_group[3], L.fix_group[4], wave, lane, live, bad, i, r0, rows, row, st, sbase);
   // var fields: one per wave at a time, output span staged in LDS
   uint8_t* stg = lds + cap + wave * stg_bytes;
   for (int v = wave; v < L.num_var; v += NW) {
@@ -2303,7 +2500,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
     const int iflags = f.iflags;
     int64_t rel = 0, n = 0;
     bool nul = true;
-    if (!bad) nul = flat_var_slot(L, f, row, row_len, &rel, &n, false, status);
+    if (!bad) nul = flat_var_slot(L, f, st, sbase, lane, row, row_len, &rel, &n, false, status);
     if (f.out_validity) {
       const uint64_t m = __ballot(live && !nul);
       if (lane == 0) write_validity64(f.out_validity, r0, rows, m);
@@ -2318,16 +2515,24 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
     uint8_t* gdst = f.out_values + O0 * w;
     const int phase = (int)(reinterpret_cast<uintptr_t>(gdst) & 15);
     const uint8_t* src = row + rel + (islist ? 8 + bitmap_bytes(n) : 0);
-    if ((iflags & 3) == 0 && S >= 0 && S + 32 <= stg_bytes) {
+    if ((iflags & 2) == 0 && S >= 0 && S + 32 <= stg_bytes) {
       if (live && n > 0) {
         uint8_t* d = stg + phase + (e0 - O0) * w;
         if (!islist) {
-          for (int64_t k = 0; k < n; ++k) d[k] = src[k];
-        } else {  // BinaryArray.toXArray; a peer's null item bits read as 0
+          lds_copy_any(d, src, (int)n);
+        } else {  // BinaryArray.toXArray; null items (BinaryArray.isNullAt) read as 0
           const uint8_t* abm = row + rel + 8;
-          for (int64_t j = 0; j < n; ++j) {
-            const bool en = (abm[j >> 3] >> (j & 7)) & 1;
-            for (int b = 0; b < w; ++b) d[j * w + b] = en ? 0 : src[j * w + b];
+          if (w == 8 || w == 4) {  // src 4-byte aligned (8-padded row offsets), d w-aligned
+            for (int64_t j = 0; j < n; ++j) {
+              const bool en = (abm[j >> 3] >> (j & 7)) & 1;
+              st32(d + j * w, en ? 0u : ld32(src + j * w));
+              if (w == 8) st32(d + j * w + 4, en ? 0u : ld32(src + j * w + 4));
+            }
+          } else {
+            for (int64_t j = 0; j < n; ++j) {
+              const bool en = (abm[j >> 3] >> (j & 7)) & 1;
+              for (int b = 0; b < w; ++b) d[j * w + b] = en ? 0 : src[j * w + b];
+            }
           }
         }
       }
@@ -2347,6 +2552,32 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
         }
       }
       wave_lds_sync();
+      if (islist && f.out_item_validity) {  // the span's item validity, assembled in LDS (staging reused)
+        uint32_t* bw = reinterpret_cast<uint32_t*>(stg);
+        const int64_t W0 = O0 >> 5;
+        const int nwd = O1 > O0 ? (int)(((O1 - 1) >> 5) - W0 + 1) : 0;
+        for (int k = lane; k < nwd; k += 64) bw[k] = 0;
+        wave_lds_sync();
+        if (live && n > 0) {
+          const uint8_t* abm = row + rel + 8;
+          for (int64_t j = 0; j < n; ++j)
+            if (!((abm[j >> 3] >> (j & 7)) & 1)) atomicOr(&bw[((e0 + j) >> 5) - W0], 1u << ((e0 + j) & 31));
+        }
+        wave_lds_sync();
+        uint32_t* gv = reinterpret_cast<uint32_t*>(f.out_item_validity) + W0;
+        for (int k = lane; k < nwd; k += 64) {
+          const int64_t lo = (W0 + k) * 32, hi = lo + 32;
+          const int b0 = O0 > lo ? (int)(O0 - lo) : 0, b1 = O1 < hi ? (int)(O1 - lo) : 32;
+          const uint32_t span = (b1 - b0 == 32) ? ~0u : (((1u << (b1 - b0)) - 1u) << b0);
+          if (span == ~0u) {
+            *gp(gv + k) = bw[k];
+          } else {  // word shared with a neighbouring tile: touch only this span's bits
+            atomicAnd(gv + k, ~span);
+            atomicOr(gv + k, bw[k]);
+          }
+        }
+        wave_lds_sync();
+      }
     } else if (live && n > 0) {
       if (!islist) {
         copy_out(f.out_values + e0, src, n);
@@ -2828,8 +3059,14 @@ int flat_nw() {  // FORY_ROWFMT_VARNW: waves per 64-record tile (4 or 8)
   return e && atoi(e) == 8 ? 8 : 4;
 }
 
+size_t sbase_lds(const VarLaunch& L) {
+  return L.num_struct ? (size_t)(1 + L.num_struct) * 64 * sizeof(int32_t) : 0;
+}
+
+// LDS of the flat tile kernels: row image, per-wave staging, payload offsets
+// (encode) and child-row offsets (nested plans).
 size_t flat_lds(const VarLaunch& L, int cap, int nw) {
-  return (size_t)cap + (size_t)nw * L.stg_bytes + (size_t)L.num_var * 64 * sizeof(int32_t);
+  return (size_t)cap + (size_t)nw * L.stg_bytes + (size_t)L.num_var * 64 * sizeof(int32_t) + sbase_lds(L);
 }
 
 // LDS image of the spill launches: 3x the main image, in [32, 96] KiB
@@ -2857,11 +3094,11 @@ void launch_flat_enc_t(const VarLaunch& L, const int64_t* offs, uint8_t* out, in
   auto* k = &var_encode_flat_kernel<FRAME, NW, PROF, false>;
   var_tile_launch(k, L, cap);
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds(L, cap, NW), s, L, L.prog,
-                     L.cols, L.fix, L.vf, offs, out, capacity, status, cap, sp);
+                     L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, cap, sp);
   auto* k2 = &var_encode_flat_kernel<FRAME, NW, PROF, true>;
   var_tile_launch(k2, L, sp.cap);
   hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
-                     flat_lds(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, offs, out, capacity, status, sp.cap,
+                     flat_lds(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, sp.cap,
                      sp);
 }
 
@@ -2879,14 +3116,14 @@ void launch_flat_dec(const VarLaunch& L, const uint8_t* rows, const int64_t* off
   (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
   auto* k = &var_decode_flat_kernel<FRAME, WRITE, NW, false>;
   var_tile_launch(k, L, cap);
-  const size_t lds = WRITE ? flat_lds(L, cap, NW) : (size_t)cap;  // pass 1 needs only the row image
+  const size_t lds = WRITE ? flat_lds(L, cap, NW) : (size_t)cap + sbase_lds(L);  // pass 1: row image (+ struct offsets)
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
-                     L.vf, rows, offs, tile_tot, status, cap, sp);
+                     L.vf, L.st, rows, offs, tile_tot, status, cap, sp);
   auto* k2 = &var_decode_flat_kernel<FRAME, WRITE, NW, true>;
   var_tile_launch(k2, L, sp.cap);
-  const size_t lds2 = WRITE ? flat_lds(L, sp.cap, NW) : (size_t)sp.cap;
+  const size_t lds2 = WRITE ? flat_lds(L, sp.cap, NW) : (size_t)sp.cap + sbase_lds(L);
   hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, lds2, 64 * NW)), dim3(64 * NW), lds2, s, L, L.prog, L.cols, L.fix,
-                     L.vf, rows, offs, tile_tot, status, sp.cap, sp);
+                     L.vf, L.st, rows, offs, tile_tot, status, sp.cap, sp);
 }
 
 // Encode: the caller's capacity (normally encoded_size's total) gives the mean

@@ -38,8 +38,8 @@ struct FixedFieldDev {
   uint8_t* out_validity;    // decode target
   int32_t width;            // 1,2,4,8
   int32_t flags;            // bit0 nullable, bit1 bool
-  int32_t slot;             // schema ordinal (slot index in the row)
-  int32_t pad;
+  int32_t slot;             // schema ordinal (slot index in the row / enclosing struct)
+  int32_t parent;           // varlen tile kernels: enclosing struct id (0 = the row itself)
 };
 // The device table is sorted into width groups [8-byte][4-byte][2-byte][1-byte]
 // (stable within a group) so every load loop has a compile-time width.
@@ -73,8 +73,24 @@ struct VarFieldDev {
   int32_t w;                     // item width (1 for bytes)
   int32_t iflags;                // item flags: bit0 nullable, bit1 bool
   int32_t flags;                 // field flags: bit0 nullable
-  int32_t pad[3];
+  int32_t parent;                // enclosing struct id (0 = the row itself)
+  int32_t pad[2];
 };
+
+// Nested struct fields of a tile-engine plan, in pre-order (id = index + 1; id
+// 0 is the top-level row). A struct's child row is written inline at the
+// writerIndex its field is reached (BaseBinaryEncoderBuilder.java:436-490).
+struct StructDev {
+  const uint8_t* validity;       // struct column validity (nullable) or null
+  uint8_t* out_validity;         // decode target
+  int32_t parent;                // enclosing struct id
+  int32_t slot;                  // ordinal in the parent
+  int32_t hdr;                   // child null-bitmap bytes
+  int32_t nfields;               // child field count
+  int32_t flags;                 // bit0 nullable
+  int32_t pad;
+};
+constexpr int kMaxTileStructs = 16;  // struct fields a tile-engine plan may hold
 
 struct ColumnDev {  // per-column device view (bound per call)
   const uint8_t* values;

@@ -57,13 +57,15 @@ def validity_bytes(n: int) -> int:
     return max(4, ((n + 7) // 8 + 3) // 4 * 4)
 
 
-def _build(f: Field, vals: Sequence[Any], out: List[HostColumn]):
-    """Appends the pre-order columns of field f for python values `vals`."""
+def _build(f: Field, vals: Sequence[Any], out: List[HostColumn], absent: Optional[np.ndarray] = None):
+    """Appends the pre-order columns of field f for python values `vals`
+    (`absent`: slots under a null parent struct, where a not-null field may be None)."""
     n = len(vals)
     valid = np.array([v is not None for v in vals], dtype=bool)
     col = HostColumn(length=n)
     col.validity = pack_validity(valid) if f.nullable else None
-    if not f.nullable and not valid.all():
+    bad = ~valid if absent is None else (~valid & ~absent)
+    if not f.nullable and bad.any():
         raise ValueError(f"null value for not-null field {f.name}")
     t = f.type.id
     out.append(col)
@@ -96,8 +98,9 @@ def _build(f: Field, vals: Sequence[Any], out: List[HostColumn]):
         col.offsets = offs
         _build(f.children[0], items, out)
     elif t == ArrowType.STRUCT:
+        gone = ~valid if absent is None else (~valid | absent)
         for c in f.children:
-            _build(c, [None if v is None else v[c.name] for v in vals], out)
+            _build(c, [None if v is None else v[c.name] for v in vals], out, gone)
     else:
         raise NotImplementedError(f"type {f.type} not supported")
 

@@ -148,6 +148,61 @@ def flat_mix_schema() -> Schema:
     ])
 
 
+def deep_nested_rows(n: int, seed: int):
+    """Rows of deep_nested_schema: null structs at two levels, strings and lists
+    inside child rows, an all-fixed child struct, empty strings/lists."""
+    rng = np.random.default_rng(seed)
+    rows = []
+
+    def s(k):
+        return "".join(chr(int(x)) for x in rng.integers(97, 123, size=rng.integers(0, k)))
+
+    for i in range(n):
+        q = None if rng.random() < 0.2 else {
+            "s": s(20),
+            "v": None if rng.random() < 0.2 else [None if rng.random() < 0.1 else int(x)
+                                                  for x in rng.integers(-9999, 9999, size=rng.integers(0, 40))],
+            "w": None if rng.random() < 0.3 else int(rng.integers(-30000, 30000)),
+        }
+        p = None if rng.random() < 0.15 else {
+            "k": bool(rng.random() < 0.5),
+            "name": None if rng.random() < 0.2 else s(12),
+            "q": q,
+        }
+        rows.append({
+            "id": int(rng.integers(-2**62, 2**62)),
+            "p": p,
+            "r": {"x": float(rng.standard_normal()),
+                  "y": [int(x) for x in rng.integers(-2**62, 2**62, size=rng.integers(0, 10))]},
+            "t": {"u": int(rng.integers(-2**31, 2**31)), "z": float(rng.standard_normal())},
+            "tag": s(30),
+        })
+    return rows
+
+
+def deep_nested_schema() -> Schema:
+    q = DataTypes.struct_field("q", True, [
+        Field("s", DataType(ArrowType.STRING), False),
+        DataTypes.array_field("v", Field("item", DataType(ArrowType.INT32), True)),
+        Field("w", DataType(ArrowType.INT16), True),
+    ])
+    p = DataTypes.struct_field("p", True, [
+        Field("k", DataType(ArrowType.BOOL), False),
+        Field("name", DataType(ArrowType.STRING), True),
+        q,
+    ])
+    r = DataTypes.struct_field("r", False, [
+        Field("x", DataType(ArrowType.DOUBLE), False),
+        Field("y", DataType(ArrowType.LIST), False, [Field("item", DataType(ArrowType.INT64), False)]),
+    ])
+    t = DataTypes.struct_field("t", False, [
+        Field("u", DataType(ArrowType.INT32), False),
+        Field("z", DataType(ArrowType.FLOAT), False),
+    ])
+    return Schema([Field("id", DataType(ArrowType.INT64), False), p, r, t,
+                   Field("tag", DataType(ArrowType.STRING), False)])
+
+
 def catalog():
     """name -> (schema, host column factory(n, seed))."""
     return {
@@ -163,6 +218,8 @@ def catalog():
         "strings_lists": (string_list_schema(),
                           lambda n, s: build_columns(string_list_schema(), string_list_rows(n, s))),
         "flat_mix": (flat_mix_schema(), lambda n, s: build_columns(flat_mix_schema(), flat_mix_rows(n, s))),
+        "deep_nested": (deep_nested_schema(),
+                        lambda n, s: build_columns(deep_nested_schema(), deep_nested_rows(n, s))),
     }
 
 
