@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--frame", action="store_true", help="frame-stream mode instead of raw rows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=16, help="host threads of the CPU baseline")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_latest.json"),
                     help="per-launch HBM traffic from a rocprofv3 PMC run of this command")
     return ap.parse_args()
@@ -95,9 +96,13 @@ def make_batch(config, n, row0, device):
                                                  else W.nested_schema()), cols, col_bytes
 
 
-def cpu_baseline(config, frame, seconds):
-    """The oracle (scalar C port of the Java writer/reader, 1 thread) on a bounded sample."""
-    import numpy as np
+def cpu_baseline(config, frame, seconds, threads=1):
+    """The oracle (scalar C port of the Java writer/reader) on a bounded sample of the
+    workload: `threads` host threads, each with its own encoder state and buffers,
+    running encode+decode round trips of the same 200K-record sample (the oracle's C
+    calls release the GIL), as the JVM path would run one Encoders.bean encoder per
+    core thread."""
+    import threading
     from oracle import oracle
     from fury_amd import workloads as W
     if config == "struct104":
@@ -110,20 +115,31 @@ def cpu_baseline(config, frame, seconds):
     else:
         schema, n = W.nested_schema(), 200_000
         cols = W.nested_host_columns(n)
-    reps = 0
-    row_bytes = 0
+    oracle.load()
+    tallies = [[0, 0] for _ in range(threads)]  # [reps, row bytes] per thread
     t0 = time.perf_counter()
-    while True:
-        buf, offs = oracle.encode(schema, cols, n, 1 if frame else 0)
-        oracle.decode(schema, buf, offs, n, 1 if frame else 0)
-        reps += 1
-        row_bytes += 2 * int(offs[-1])
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": row_bytes / el / 2**30, "unit": "GiB/s", "cores": 1, "kind": "port",
+
+    def worker(k):
+        while True:
+            buf, offs = oracle.encode(schema, cols, n, 1 if frame else 0)
+            oracle.decode(schema, buf, offs, n, 1 if frame else 0)
+            tallies[k][0] += 1
+            tallies[k][1] += 2 * int(offs[-1])
+            if time.perf_counter() - t0 >= seconds:
+                break
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    el = time.perf_counter() - t0
+    reps = sum(t[0] for t in tallies)
+    row_bytes = sum(t[1] for t in tallies)
+    return {"value": row_bytes / el / 2**30, "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{reps} x (encode+decode) of {n} {config} rows "
-                      f"({'frame' if frame else 'raw'}), oracle/rowfmt_oracle.c scalar, {el:.1f} s",
+                      f"({'frame' if frame else 'raw'}) on {threads} thread(s), "
+                      f"oracle/rowfmt_oracle.c scalar per thread, {el:.1f} s",
             "rows_per_s": reps * n / el}
 
 
@@ -244,7 +260,12 @@ def main():
         "step_hbm_frac": round(2 * algo / ((enc_avg + dec_avg) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(config, frame, args.cpu_seconds)
+        # all host cores of this GPU's share (the box allots 16 per GPU), then one core
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        res["cpu_baseline"] = cpu_baseline(config, frame, args.cpu_seconds, threads)
+        single = cpu_baseline(config, frame, args.cpu_seconds / 2, 1)
+        res["cpu_baseline"]["single_core"] = {"value": single["value"], "unit": "GiB/s",
+                                              "rows_per_s": single["rows_per_s"], "sample": single["sample"]}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:

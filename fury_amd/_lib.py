@@ -92,6 +92,19 @@ PROTOTYPES = {
          ctypes.c_void_p],
     ),
     "fory_rowfmt_read_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "fory_rowfmt_host_ctx_create": (
+        ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),
+    "fory_rowfmt_host_ctx_destroy": (None, [ctypes.c_void_p]),
+    "fory_rowfmt_host_encode": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.POINTER(Column), ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+         ctypes.c_int64]),
+    "fory_rowfmt_host_decode": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+         ctypes.POINTER(Column)]),
+    "fory_rowfmt_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "fory_rowfmt_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
 }
 
 _lib = None

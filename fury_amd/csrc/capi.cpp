@@ -372,6 +372,18 @@ int64_t fory_rowfmt_debug_timeline(uint64_t* host, int64_t max_words) {
 
 const char* fory_rowfmt_last_error(void) { return g_err.c_str(); }
 
+// Library-internal (host.cpp): shares last_error and the planner's column layout.
+int fory_rowfmt_internal_set_error(int code, const char* msg) { return fail(code, msg); }
+
+int fory_rowfmt_internal_column_layout(const fory_plan* plan, int32_t* width, int32_t* nullable) {
+  const Plan& p = plan->p;
+  for (size_t i = 0; i < p.nodes.size(); ++i) {
+    width[i] = p.nodes[i].width;
+    nullable[i] = p.nodes[i].nullable;
+  }
+  return FORY_OK;
+}
+
 int fory_rowfmt_plan_create(const fory_field_desc* fields, int32_t num_desc, fory_plan** out_plan) {
   if (!out_plan) return fail(FORY_ERR_INVALID_ARGUMENT, "out_plan is null");
   *out_plan = nullptr;

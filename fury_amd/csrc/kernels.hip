@@ -1904,37 +1904,55 @@ __device__ __forceinline__ void flat_enc_fixed(const VarLaunch& L, const FixedFi
 
 // Loads the tile's span of var field f (string bytes or list items) into the
 // wave's staging buffer; returns false when it must take the per-lane path.
+// Nullable list items: the span's item-validity bytes follow the values (from
+// stg + staged_vofs(phase, S), starting at byte (s0 >> 3) & ~3 of the bitmap).
+__device__ __forceinline__ int staged_vofs(int phase, int64_t S) { return (int)((phase + S + 4 + 15) & ~15); }
+
 __device__ __forceinline__ bool flat_stage(const VarFieldDev& f, int stg_bytes, int64_t r0, int rows, int lane,
-                                           uint8_t* stg, int* phase_out, int64_t* s0_out) {
+                                           uint8_t* stg, int* phase_out, int64_t* s0_out, int* vofs_out) {
   const int64_t s0 = f.offsets[r0], s1 = f.offsets[r0 + rows];
   const int64_t S = (s1 - s0) * f.w;
   *s0_out = s0;
   if ((f.iflags & 2) != 0 || S < 0 || S + 32 > stg_bytes) return false;  // bool items: per lane (0/1)
   const uint8_t* gsrc = f.values + s0 * f.w;
   const int phase = (int)(reinterpret_cast<uintptr_t>(gsrc) & 15);
+  int64_t A = 0, nvw = 0;
+  if (f.item_validity) {
+    A = (s0 >> 3) & ~int64_t(3);
+    nvw = s1 > s0 ? (((s1 + 7) >> 3) - A + 3) >> 2 : 0;
+    if (staged_vofs(phase, S) + 4 * nvw > stg_bytes) return false;
+  }
   *phase_out = phase;
+  *vofs_out = staged_vofs(phase, S);
   const uint8_t* ga = gsrc - phase;
   const int nch = (int)((phase + S + 15) >> 4);
   for (int cc = lane; cc < nch; cc += 64)
     *reinterpret_cast<u32x4*>(stg + cc * 16) = *gp(reinterpret_cast<const u32x4*>(ga + cc * 16));
+  if (nvw) {
+    uint32_t* sv = reinterpret_cast<uint32_t*>(stg + staged_vofs(phase, S));
+    const uint32_t* gv = reinterpret_cast<const uint32_t*>(f.item_validity + A);
+    for (int k = lane; k < nvw; k += 64) sv[k] = *gp(gv + k);
+  }
   return true;
 }
 
 // Copies record i's payload of var field f into its row image (staged: from
 // LDS; else per lane from global, incl. item null bits and bool items).
 __device__ __forceinline__ void flat_place(const VarFieldDev& f, bool staged, const uint8_t* stg, int phase,
-                                           int64_t s0, int p, bool live, int64_t i, uint8_t* row) {
+                                           int64_t s0, int vofs, int p, bool live, int64_t i, uint8_t* row) {
   if (!live || p < 0) return;
   const int w = f.w;
   const int64_t e0 = f.offsets[i], n = (int64_t)f.offsets[i + 1] - e0;
   uint8_t* dst = row + p + (f.is_list ? 8 + bitmap_bytes(n) : 0);
   if (staged) {
     lds_copy_padded(dst, stg + phase + (e0 - s0) * w, n * w);
-    if (f.item_validity) {  // BinaryArrayWriter.setNullAt: item bit set, element left 0
+    if (f.item_validity && n > 0) {  // BinaryArrayWriter.setNullAt: item bit set, element left 0
+      const uint8_t* sv = stg + vofs;
+      const int64_t A = (s0 >> 3) & ~int64_t(3);  // first staged bitmap byte
       uint8_t* abm = row + p + 8;
       for (int64_t j = 0; j < n; ++j) {
         const int64_t q = e0 + j;
-        if ((load_byte(f.item_validity + (q >> 3)) >> (q & 7)) & 1) continue;
+        if ((sv[(q >> 3) - A] >> (q & 7)) & 1) continue;
         abm[j >> 3] |= (uint8_t)(1u << (j & 7));
         for (int b = 0; b < w; ++b) dst[j * w + b] = 0;
       }
@@ -1973,84 +1991,111 @@ __device__ __forceinline__ void flat_place(const VarFieldDev& f, bool staged, co
 // (child row offset from the row, -1 = null/absent struct).
 __device__ __forceinline__ void flat_enc_layout_nested(const VarLaunch& L, const Op* __restrict__ prog,
                                                        const ColumnDev* __restrict__ cols, bool live, int64_t i,
-                                                       int lane, uint8_t* row, int32_t* pos, int32_t* sbase) {
-  int32_t st_start[kMaxDepth], st_hdr[kMaxDepth];
-  int depth = 0;
-  st_start[0] = 0;
-  st_hdr[0] = L.bitmap_bytes;
+                                                       const StructDev* __restrict__ st, int lane, uint8_t* row,
+                                                       int32_t* pos, int32_t* sbase) {
+  // the enclosing struct `cur` is wave-uniform (only absence is per record): no
+  // per-lane writer stack, starts live in sbase, headers in the struct table
+  int cur = 0;
+  int32_t cstart = 0, chdr = L.bitmap_bytes;  // this lane's current row start / header bytes
   int absent = live ? 0 : 1 << 20;
   const int64_t ii = live ? i : 0;
   int64_t wi = L.fixed_size;
   int vi = 0, si = 0;  // wave-uniform: var field / struct ids in program order
-  for (int pc = 0; pc < L.num_ops; ++pc) {
-    const Op op = prog[pc];
-    const ColumnDev& c = cols[op.b];
-    const bool isnull = (op.d & 1) && !col_valid(c, ii);
-    uint8_t* base = row + st_start[depth];
-    uint8_t* slot = base + st_hdr[depth] + 8 * op.a;
-    switch (op.code) {
-      case OP_FIXED:  // BinaryWriter.setNullAt; the value phase writes the slot
-        if (!absent && isnull) set_null_bit(base, op.a);
-        break;
-      case OP_BYTES:
-      case OP_LIST: {
-        int32_t p = -1;
-        if (!absent) {
-          if (isnull) {
-            set_null_bit(base, op.a);
-            st64_lds(slot, 0);
-          } else {
-            const int64_t nn = (int64_t)c.offsets[ii + 1] - c.offsets[ii];
-            const int64_t rel = wi - st_start[depth];
-            if (op.code == OP_BYTES) {  // writeUnaligned: (offset<<32 | size), padded payload
-              st64_lds(slot, ((uint64_t)rel << 32) | (uint32_t)nn);
-              p = (int32_t)wi;
-              wi += round8(nn);
-            } else {  // BinaryArrayWriter.reset(n): [i64 n][null bitmap][n * w bytes, padded to 8]
-              const int32_t ahdr = 8 + bitmap_bytes(nn);
-              const int64_t size = ahdr + round8(nn * (op.e & 0xff));
-              st64_lds(row + wi, (uint64_t)nn);
-              for (int b = 8; b < ahdr; b += 4) st32(row + wi + b, 0);
-              st64_lds(slot, ((uint64_t)rel << 32) | (uint32_t)size);
-              p = (int32_t)wi;
-              wi += size;
+  for (int pc0 = 0; pc0 < L.num_ops; pc0 += kFixBatch) {
+    // this batch's per-record inputs (validity bits, var-field lengths), loads issued together
+    bool nul[kFixBatch];
+    int32_t nn[kFixBatch];
+#pragma unroll
+    for (int k = 0; k < kFixBatch; ++k) {
+      nul[k] = false;
+      nn[k] = 0;
+      if (pc0 + k < L.num_ops) {
+        const Op op = prog[pc0 + k];
+        const ColumnDev& c = cols[op.b];
+        if ((op.d & 1) && op.code != OP_STRUCT_END && c.validity)
+          nul[k] = !((load_byte(c.validity + (ii >> 3)) >> (ii & 7)) & 1);
+        if (op.code == OP_BYTES || op.code == OP_LIST) nn[k] = c.offsets[ii + 1] - c.offsets[ii];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kFixBatch; ++k) {
+      if (pc0 + k >= L.num_ops) break;
+      const Op op = prog[pc0 + k];
+      const bool isnull = nul[k];
+      uint8_t* base = row + cstart;
+      uint8_t* slot = base + chdr + 8 * op.a;
+      switch (op.code) {
+        case OP_FIXED:  // BinaryWriter.setNullAt; the value phase writes the slot
+          if (!absent && isnull) set_null_bit(base, op.a);
+          break;
+        case OP_BYTES:
+        case OP_LIST: {
+          int32_t p = -1;
+          if (!absent) {
+            if (isnull) {
+              set_null_bit(base, op.a);
+              st64_lds(slot, 0);
+            } else {
+              const int64_t n = nn[k];
+              const int64_t rel = wi - cstart;
+              if (op.code == OP_BYTES) {  // writeUnaligned: (offset<<32 | size), padded payload
+                st64_lds(slot, ((uint64_t)rel << 32) | (uint32_t)n);
+                p = (int32_t)wi;
+                wi += round8(n);
+              } else {  // BinaryArrayWriter.reset(n): [i64 n][null bitmap][n * w bytes, padded to 8]
+                const int32_t ahdr = 8 + bitmap_bytes(n);
+                const int64_t size = ahdr + round8(n * (op.e & 0xff));
+                st64_lds(row + wi, (uint64_t)n);
+                for (int b = 8; b < ahdr; b += 4) st32(row + wi + b, 0);
+                st64_lds(slot, ((uint64_t)rel << 32) | (uint32_t)size);
+                p = (int32_t)wi;
+                wi += size;
+              }
             }
           }
+          pos[vi * 64 + lane] = p;
+          ++vi;
+          break;
         }
-        pos[vi * 64 + lane] = p;
-        ++vi;
-        break;
+        case OP_STRUCT_BEGIN: {
+          ++si;
+          cur = si;
+          int32_t b = -1;
+          if (absent) {
+            ++absent;
+          } else if (isnull) {
+            set_null_bit(base, op.a);
+            st64_lds(slot, 0);
+            absent = 1;
+          } else {
+            const int32_t h = bitmap_bytes(op.c);
+            for (int q = 0; q < h; q += 4) st32(row + wi + q, 0);
+            b = (int32_t)wi;
+            cstart = b;
+            chdr = h;
+            wi += h + 8LL * op.c;
+          }
+          sbase[si * 64 + lane] = b;
+          break;
+        }
+        case OP_STRUCT_END: {
+          cur = __builtin_amdgcn_readfirstlane(cur);  // uniform by construction: scalar table loads
+          const int par = st[cur - 1].parent;
+          const int32_t pstart = par ? sbase[par * 64 + lane] : 0;
+          const int32_t phdr = par ? st[par - 1].hdr : L.bitmap_bytes;
+          if (absent) {
+            --absent;
+          } else {
+            const int64_t sz = wi - cstart;
+            const int32_t rel = cstart - pstart;
+            st64_lds(row + pstart + phdr + 8 * op.a, ((uint64_t)(uint32_t)rel << 32) | (uint32_t)sz);
+          }
+          cur = par;
+          cstart = pstart;  // (unused while absent)
+          chdr = phdr;
+          break;
+        }
       }
-      case OP_STRUCT_BEGIN: {
-        ++si;
-        int32_t b = -1;
-        if (absent) {
-          ++absent;
-        } else if (isnull) {
-          set_null_bit(base, op.a);
-          st64_lds(slot, 0);
-          absent = 1;
-        } else {
-          ++depth;
-          st_start[depth] = (int32_t)wi;
-          st_hdr[depth] = bitmap_bytes(op.c);
-          for (int k = 0; k < st_hdr[depth]; k += 4) st32(row + wi + k, 0);
-          b = (int32_t)wi;
-          wi += st_hdr[depth] + 8LL * op.c;
-        }
-        sbase[si * 64 + lane] = b;
-        break;
-      }
-      case OP_STRUCT_END:
-        if (absent) {
-          --absent;
-        } else {
-          const int64_t sz = wi - st_start[depth];
-          const int32_t rel = st_start[depth] - st_start[depth - 1];
-          --depth;
-          st64_lds(row + st_start[depth] + st_hdr[depth] + 8 * op.a, ((uint64_t)(uint32_t)rel << 32) | (uint32_t)sz);
-        }
-        break;
     }
   }
 }
@@ -2132,10 +2177,10 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   uint8_t* slots = row + L.bitmap_bytes;
   // this wave's first var field: span loads in flight across the layout phase
   uint8_t* stg = lds + cap + wave * stg_bytes;
-  int phase = 0;
+  int phase = 0, vofs = 0;
   int64_t s0 = 0;
   bool staged = false;
-  if (wave < L.num_var) staged = flat_stage(vf[wave], stg_bytes, r0, rows, lane, stg, &phase, &s0);
+  if (wave < L.num_var) staged = flat_stage(vf[wave], stg_bytes, r0, rows, lane, stg, &phase, &s0, &vofs);
   FLAT_STAMP(1);
   if (wave == 0) {
     // Encoders.encode frame header; BinaryRowWriter.reset zeroes the bitmap (BinaryRowWriter.java:76-84)
@@ -2147,7 +2192,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
       for (int b = 0; b < L.bitmap_bytes; b += 4) st32(row + b, 0);
     }
     if (L.num_struct) {  // nested struct fields: program walk
-      flat_enc_layout_nested(L, prog, cols, live, i, lane, row, pos, sbase);
+      flat_enc_layout_nested(L, prog, cols, live, i, st, lane, row, pos, sbase);
     } else {
     // null bits of nullable fixed fields (this wave only: no bitmap races)
     const int nfix = L.fix_group[4];
@@ -2221,10 +2266,10 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   for (int v = wave; v < L.num_var; v += NW) {
     if (v != wave) {
       wave_lds_sync();  // staging reused
-      staged = flat_stage(vf[v], stg_bytes, r0, rows, lane, stg, &phase, &s0);
+      staged = flat_stage(vf[v], stg_bytes, r0, rows, lane, stg, &phase, &s0, &vofs);
     }
     wave_lds_sync();
-    flat_place(vf[v], staged, stg, phase, s0, pos[v * 64 + lane], live, i, row);
+    flat_place(vf[v], staged, stg, phase, s0, vofs, pos[v * 64 + lane], live, i, row);
   }
   if (PROF) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   FLAT_STAMP(5);

@@ -128,3 +128,60 @@ def read_status(status, stream=None):
 
 def is_varlen(f) -> bool:
     return f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST)
+
+
+def _np_ptr(a) -> Optional[int]:
+    return None if a is None else a.ctypes.data
+
+
+class HostPipeline:
+    """fory_rowfmt_host_*: host-memory batches (numpy arrays, e.g. the Arrow view of
+    off-heap MemoryBuffers) through the device kernels with the C++ chunk pipeline.
+    Fixed-width plans (ABI 1)."""
+
+    def __init__(self, plan: NativePlan, chunk_rows: int = 1 << 20, device: int = 0):
+        lib = _lib.load()
+        self.plan = plan
+        h = ctypes.c_void_p()
+        _check(lib.fory_rowfmt_host_ctx_create(plan.handle, device, chunk_rows, ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.load().fory_rowfmt_host_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _host_array(cols):
+        arr = (_lib.Column * max(1, len(cols)))()
+        for i, c in enumerate(cols):
+            arr[i].values = _np_ptr(c.values)
+            arr[i].offsets = _np_ptr(c.offsets)
+            arr[i].validity = _np_ptr(c.validity)
+            arr[i].length = c.length
+            arr[i].capacity = 0 if c.values is None else c.values.nbytes
+        return arr
+
+    def encode(self, host_cols, n: int, frame: int, out) -> None:
+        """host_cols: HostColumn list (numpy); out: uint8 numpy array of >= n*stride bytes."""
+        _check(_lib.load().fory_rowfmt_host_encode(self.handle, self._host_array(host_cols), n, frame,
+                                                   _np_ptr(out), out.nbytes))
+
+    def decode(self, rows, n: int, frame: int, host_out_cols) -> None:
+        _check(_lib.load().fory_rowfmt_host_decode(self.handle, _np_ptr(rows), rows.nbytes, n, frame,
+                                                   self._host_array(host_out_cols)))
+
+
+def host_register(a) -> None:
+    """Pins a numpy array's memory in place (hipHostRegister)."""
+    _check(_lib.load().fory_rowfmt_host_register(a.ctypes.data, a.nbytes))
+
+
+def host_unregister(a) -> None:
+    _check(_lib.load().fory_rowfmt_host_unregister(a.ctypes.data))

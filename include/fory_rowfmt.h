@@ -207,6 +207,39 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows,
  * (FORY_OK if none). Sets last_error with the reference's message shape. */
 int fory_rowfmt_read_status(const int32_t* d_status, void* stream);
 
+/* --- host path: replaces N x Encoder.encode(MemoryBuffer, T) /
+ *     Encoder.decode(MemoryBuffer) over OFF-HEAP host buffers
+ *     (Encoders.java:177-225; MemoryBuffer.getUnsafeAddress,
+ *     java/fory-core/.../memory/MemoryBuffer.java:287-297) — the path's real
+ *     endpoints (JVM buffers on their way to / from an RPC socket).
+ *
+ * A host context owns one device, three HIP streams and two sets of device
+ * chunk buffers (columns, rows, workspace), allocated once at creation. Each
+ * call splits the batch into chunks of chunk_rows records (rounded up to a
+ * multiple of 64) and pipelines H2D of chunk k+1 || kernel of chunk k || D2H
+ * of chunk k-1. Calls are synchronous: they return when the host output is
+ * complete (or with the first error). All pointers are HOST memory; register
+ * long-lived buffers (fory_rowfmt_host_register = hipHostRegister) for full
+ * PCIe rate. The plan must outlive the context; a context serves one call at
+ * a time. ABI 1: fixed-width plans only (FORY_ERR_UNSUPPORTED at creation
+ * otherwise). Output bytes equal fory_rowfmt_encode's / decode's. */
+typedef struct fory_host_ctx fory_host_ctx;
+int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t chunk_rows,
+                                fory_host_ctx** out_ctx);
+void fory_rowfmt_host_ctx_destroy(fory_host_ctx* ctx);
+/* host_cols: values (+ validity for nullable fields) in host memory; rows
+ * written back to back into host_out (out_capacity bytes; FORY_ERR_CAPACITY
+ * before any work if n * stride does not fit: IndexOutOfBoundsException). */
+int fory_rowfmt_host_encode(fory_host_ctx* ctx, const fory_column* host_cols, int64_t num_rows,
+                            int32_t frame_mode, void* host_out, int64_t out_capacity);
+/* host_rows: rows_bytes of rows/frames; host_out_cols: values (+ validity)
+ * targets in host memory. STREAM mode checks every frame's size and schema
+ * hash (FORY_ERR_SCHEMA_MISMATCH: ClassNotCompatibleException). */
+int fory_rowfmt_host_decode(fory_host_ctx* ctx, const void* host_rows, int64_t rows_bytes,
+                            int64_t num_rows, int32_t frame_mode, const fory_column* host_out_cols);
+int fory_rowfmt_host_register(void* host_ptr, int64_t bytes);
+int fory_rowfmt_host_unregister(void* host_ptr);
+
 #ifdef __cplusplus
 }
 #endif

@@ -98,3 +98,17 @@ def test_argument_validation_without_gpu():
     rc = lib.fory_rowfmt_encode(p.handle, cols, 0, 1, None, None, 0, None, None, 0, None)
     assert rc == _lib.FORY_OK
     assert lib.fory_rowfmt_workspace_bytes(p.handle, 1 << 26) > 104 * 40
+
+
+def test_host_path_validation_without_gpu():
+    """The host pipeline rejects varlen plans and bad arguments before touching the device."""
+    from fury_amd.format.native import HostPipeline
+    with pytest.raises(errors.UnsupportedOperationException):
+        HostPipeline(NativePlan(W.mixed_schema()))
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.fory_rowfmt_host_ctx_create(None, 0, 1024, ctypes.byref(h)) == _lib.FORY_ERR_INVALID_ARGUMENT
+    cols = (_lib.Column * 1)()
+    assert lib.fory_rowfmt_host_encode(None, cols, 1, 0, None, 0) == _lib.FORY_ERR_INVALID_ARGUMENT
+    assert lib.fory_rowfmt_host_decode(None, None, 0, 1, 0, cols) == _lib.FORY_ERR_INVALID_ARGUMENT
+    assert lib.fory_rowfmt_host_register(None, 16) == _lib.FORY_ERR_INVALID_ARGUMENT
