@@ -329,6 +329,10 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   L->spill = L->spill_count + 4;
   const char* stg = getenv("FORY_ROWFMT_VARSTG");
   L->stg_bytes = stg ? std::max(256, std::min(16384, atoi(stg))) & ~15 : 2048;
+  int64_t nested_fixed = 0;
+  for (const fory_amd::StructDev& sd : st) nested_fixed += sd.hdr + 8LL * sd.nfields;
+  for (const fory_amd::VarFieldDev& v : var) nested_fixed += v.is_list ? 8 : 0;
+  L->nested_fixed = (int32_t)nested_fixed;
   L->cols = static_cast<const ColumnDev*>(ws);
   L->prog = reinterpret_cast<const fory_amd::Op*>(static_cast<uint8_t*>(ws) + col_bytes);
   L->num_ops = (int32_t)p.program.size();

@@ -52,11 +52,13 @@ struct VarLaunch {
   int64_t num_rows;
   int32_t frame;
   int32_t tile_cap;             // LDS bytes per 64-record tile image (tile engine)
-  // Flat plans (every top-level field FIXED/BOOL, STRING/BINARY or LIST<fixed>;
-  // the program is one op per field): cooperative tile kernels.
+  // Cooperative tile kernels (every plan the device path accepts, up to 32 var
+  // fields and kMaxTileStructs nested structs; name kept from when they took
+  // flat plans only).
   int32_t flat;
-  int32_t num_var;              // top-level OP_BYTES / OP_LIST ops, field order
-  int32_t stg_bytes;            // LDS staging per wave for one field's span
+  int32_t num_var;              // OP_BYTES / OP_LIST ops at any struct level, program order
+  int32_t stg_bytes;            // LDS staging per wave (slot) for one record group's span
+  int32_t nested_fixed;         // fixed bytes of child rows + list headers per record (staging estimate)
   int32_t fix_group[5];         // width groups [8][4][2][1] of `fix`
   const FixedFieldDev* fix;     // device: fixed fields (any struct level), width-sorted
   const VarFieldDev* vf;        // device: var fields (any struct level), program order

@@ -1818,6 +1818,10 @@ __global__ __launch_bounds__(64) void var_decode_tile_kernel(VarLaunch L, const 
 // bigger than the LDS image take per-lane paths with the same results.
 // ---------------------------------------------------------------------------
 
+// Waves that place var fields in the encode tile kernel: waves 1..NW-1 (wave 0
+// lays the rows out) when every field gets a wave of its own, else all NW.
+__host__ __device__ __forceinline__ int var_placers(int num_var, int nw) { return num_var < nw ? nw - 1 : nw; }
+
 __device__ __forceinline__ void wave_lds_sync() {
   // LDS ops of one wave execute in order; keep the compiler from reordering.
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1902,53 +1906,65 @@ __device__ __forceinline__ void flat_enc_fixed(const VarLaunch& L, const FixedFi
   }
 }
 
-// Loads the tile's span of var field f (string bytes or list items) into the
-// wave's staging buffer; returns false when it must take the per-lane path.
-// Nullable list items: the span's item-validity bytes follow the values (from
-// stg + staged_vofs(phase, S), starting at byte (s0 >> 3) & ~3 of the bitmap).
+// Var payloads are staged per RECORD GROUP: records [lo, hi) of the tile whose
+// span of var field f (string bytes or list items, contiguous in the Arrow
+// buffer) fits the wave's staging buffer, with the span's item-validity bytes
+// behind it (nullable list items). A record too big on its own, and bool items
+// (0/1 normalisation), take the per-lane path. e0/e1: the lane's item range
+// (nondecreasing over lanes; dead lanes hold the tile's end).
 __device__ __forceinline__ int staged_vofs(int phase, int64_t S) { return (int)((phase + S + 4 + 15) & ~15); }
 
-__device__ __forceinline__ bool flat_stage(const VarFieldDev& f, int stg_bytes, int64_t r0, int rows, int lane,
-                                           uint8_t* stg, int* phase_out, int64_t* s0_out, int* vofs_out) {
-  const int64_t s0 = f.offsets[r0], s1 = f.offsets[r0 + rows];
-  const int64_t S = (s1 - s0) * f.w;
-  *s0_out = s0;
-  if ((f.iflags & 2) != 0 || S < 0 || S + 32 > stg_bytes) return false;  // bool items: per lane (0/1)
-  const uint8_t* gsrc = f.values + s0 * f.w;
+__device__ __forceinline__ int flat_group(const VarFieldDev& f, int64_t e0, int64_t e1, int lo, int rows, int lane,
+                                          int stg_bytes, bool* fits) {
+  const int64_t base = __shfl(e0, lo);
+  int64_t need = (e1 - base) * f.w + 16 + 4 + 16;  // phase + funnel-copy slack + vofs rounding
+  if (f.item_validity) need += ((e1 + 7) >> 3) - ((base >> 3) & ~int64_t(3)) + 4;
+  const bool ok = (f.iflags & 2) == 0 && lane >= lo && lane < rows && need <= stg_bytes;
+  const uint64_t m = __ballot(ok) >> lo;  // a prefix of the lanes from lo (e1 nondecreasing)
+  const int cnt = ~m == 0 ? 64 - lo : (int)__builtin_ctzll(~m);
+  *fits = cnt > 0;
+  return lo + (cnt > 0 ? cnt : 1);
+}
+
+// Items [sa, sb) of f (and their validity bytes) -> staging, by LDS-DMA (1 KiB
+// per wave instruction; asynchronous: wait vmcnt(0) before reading).
+__device__ __forceinline__ void flat_stage_span(const VarFieldDev& f, int64_t sa, int64_t sb, int lane, uint8_t* stg,
+                                                int* phase_out, int* vofs_out) {
+  const int64_t S = (sb - sa) * f.w;
+  const uint8_t* gsrc = f.values + sa * f.w;
   const int phase = (int)(reinterpret_cast<uintptr_t>(gsrc) & 15);
-  int64_t A = 0, nvw = 0;
-  if (f.item_validity) {
-    A = (s0 >> 3) & ~int64_t(3);
-    nvw = s1 > s0 ? (((s1 + 7) >> 3) - A + 3) >> 2 : 0;
-    if (staged_vofs(phase, S) + 4 * nvw > stg_bytes) return false;
-  }
   *phase_out = phase;
   *vofs_out = staged_vofs(phase, S);
   const uint8_t* ga = gsrc - phase;
   const int nch = (int)((phase + S + 15) >> 4);
-  for (int cc = lane; cc < nch; cc += 64)
-    *reinterpret_cast<u32x4*>(stg + cc * 16) = *gp(reinterpret_cast<const u32x4*>(ga + cc * 16));
-  if (nvw) {
-    uint32_t* sv = reinterpret_cast<uint32_t*>(stg + staged_vofs(phase, S));
-    const uint32_t* gv = reinterpret_cast<const uint32_t*>(f.item_validity + A);
-    for (int k = lane; k < nvw; k += 64) sv[k] = *gp(gv + k);
+  for (int c0 = 0; c0 < nch; c0 += 64)
+    if (c0 + lane < nch)
+      __builtin_amdgcn_global_load_lds((const GAS void*)(ga + (int64_t)(c0 + lane) * 16),
+                                       (__attribute__((address_space(3))) void*)(stg + c0 * 16), 16, 0, 0);
+  if (f.item_validity && sb > sa) {
+    const int64_t A = (sa >> 3) & ~int64_t(3);
+    const int nvw = (int)((((sb + 7) >> 3) - A + 3) >> 2);
+    const uint8_t* gv = f.item_validity + A;
+    for (int k0 = 0; k0 < nvw; k0 += 64)
+      if (k0 + lane < nvw)
+        __builtin_amdgcn_global_load_lds((const GAS void*)(gv + (int64_t)(k0 + lane) * 4),
+                                         (__attribute__((address_space(3))) void*)(stg + *vofs_out + k0 * 4), 4, 0, 0);
   }
-  return true;
 }
 
-// Copies record i's payload of var field f into its row image (staged: from
-// LDS; else per lane from global, incl. item null bits and bool items).
+// Copies the lane's payload of var field f (items e0 .. e0+n) into its row image
+// at row + p (staged: from LDS, the group's span starting at item `base`; else
+// per lane from global, incl. item null bits and bool items).
 __device__ __forceinline__ void flat_place(const VarFieldDev& f, bool staged, const uint8_t* stg, int phase,
-                                           int64_t s0, int vofs, int p, bool live, int64_t i, uint8_t* row) {
-  if (!live || p < 0) return;
+                                           int64_t base, int vofs, int p, int64_t e0, int64_t n, uint8_t* row) {
+  if (p < 0) return;
   const int w = f.w;
-  const int64_t e0 = f.offsets[i], n = (int64_t)f.offsets[i + 1] - e0;
   uint8_t* dst = row + p + (f.is_list ? 8 + bitmap_bytes(n) : 0);
   if (staged) {
-    lds_copy_padded(dst, stg + phase + (e0 - s0) * w, n * w);
+    lds_copy_padded(dst, stg + phase + (e0 - base) * w, n * w);
     if (f.item_validity && n > 0) {  // BinaryArrayWriter.setNullAt: item bit set, element left 0
       const uint8_t* sv = stg + vofs;
-      const int64_t A = (s0 >> 3) & ~int64_t(3);  // first staged bitmap byte
+      const int64_t A = (base >> 3) & ~int64_t(3);  // first staged bitmap byte
       uint8_t* abm = row + p + 8;
       for (int64_t j = 0; j < n; ++j) {
         const int64_t q = e0 + j;
@@ -2145,10 +2161,14 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   constexpr int HDR = FRAME ? 12 : 0;
   const int stg_bytes = L.stg_bytes;
   uint8_t* img = lds;
-  int32_t* pos = reinterpret_cast<int32_t*>(lds + cap + NW * stg_bytes);  // [num_var][64]
-  int32_t* sbase = pos + L.num_var * 64;                                  // [1 + num_struct][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // var placement: up to 3 fields per wave stay off wave 0 (it lays the rows out)
+  const int nplc = var_placers(L.num_var, NW);
+  const int pi = nplc < NW ? wave - 1 : (wave + NW - 1) % NW;  // placer index (-1: none)
+  const int nslot = L.num_var < nplc ? L.num_var : nplc;  // staging slots: one per placing wave
+  int32_t* pos = reinterpret_cast<int32_t*>(lds + cap + nslot * stg_bytes);  // [num_var][64]
+  int32_t* sbase = pos + L.num_var * 64;                                  // [1 + num_struct][64]
   auto body = [&](int64_t tile) {
   FLAT_STAMP(0);
   const int64_t r0 = tile * 64;
@@ -2175,12 +2195,21 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   uint8_t* fp = img + mis + (int)(beg - B0);
   uint8_t* row = fp + HDR;
   uint8_t* slots = row + L.bitmap_bytes;
-  // this wave's first var field: span loads in flight across the layout phase
-  uint8_t* stg = lds + cap + wave * stg_bytes;
-  int phase = 0, vofs = 0;
-  int64_t s0 = 0;
-  bool staged = false;
-  if (wave < L.num_var) staged = flat_stage(vf[wave], stg_bytes, r0, rows, lane, stg, &phase, &s0, &vofs);
+  // var field v is placed by wave (v + 1) % NW: wave 0 lays the rows out while
+  // the other waves' first record groups stream into staging (LDS-DMA)
+  const int v_first = pi < 0 ? L.num_var : pi;
+  uint8_t* stg = lds + cap + (pi < 0 ? 0 : pi) * stg_bytes;
+  int pf_hi = 0, pf_phase = 0, pf_vofs = 0;
+  bool pf_fits = false;
+  int64_t pf_e0 = 0, pf_e1 = 0;
+  if (wave != 0 && v_first < L.num_var) {
+    const VarFieldDev& f = vf[v_first];
+    const int64_t ee = f.offsets[r0 + rows];
+    pf_e0 = live ? f.offsets[i] : ee;
+    pf_e1 = live ? f.offsets[i + 1] : ee;
+    pf_hi = flat_group(f, pf_e0, pf_e1, 0, rows, lane, stg_bytes, &pf_fits);
+    if (pf_fits) flat_stage_span(f, __shfl(pf_e0, 0), __shfl(pf_e1, pf_hi - 1), lane, stg, &pf_phase, &pf_vofs);
+  }
   FLAT_STAMP(1);
   if (wave == 0) {
     // Encoders.encode frame header; BinaryRowWriter.reset zeroes the bitmap (BinaryRowWriter.java:76-84)
@@ -2262,14 +2291,39 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   FLAT_STAMP(3);
   __syncthreads();
   FLAT_STAMP(4);
-  // variable payloads: one field per wave at a time (the first one already staged)
-  for (int v = wave; v < L.num_var; v += NW) {
-    if (v != wave) {
-      wave_lds_sync();  // staging reused
-      staged = flat_stage(vf[v], stg_bytes, r0, rows, lane, stg, &phase, &s0, &vofs);
+  // variable payloads: one field per wave at a time, record group by record group
+  for (int v = v_first; v < L.num_var; v += nplc) {
+    const VarFieldDev& f = vf[v];
+    int64_t e0 = pf_e0, e1 = pf_e1;
+    if (v != v_first || wave == 0) {
+      const int64_t ee = f.offsets[r0 + rows];
+      e0 = live ? f.offsets[i] : ee;
+      e1 = live ? f.offsets[i + 1] : ee;
     }
-    wave_lds_sync();
-    flat_place(vf[v], staged, stg, phase, s0, vofs, pos[v * 64 + lane], live, i, row);
+    const int p = live ? pos[v * 64 + lane] : -1;
+    for (int lo = 0; lo < rows;) {
+      bool fits;
+      int hi, phase = 0, vofs = 0;
+      if (v == v_first && wave != 0 && lo == 0) {  // prefetched group
+        hi = pf_hi;
+        fits = pf_fits;
+        phase = pf_phase;
+        vofs = pf_vofs;
+      } else {
+        hi = flat_group(f, e0, e1, lo, rows, lane, stg_bytes, &fits);
+        if (fits) {
+          wave_lds_sync();  // staging reused
+          flat_stage_span(f, __shfl(e0, lo), __shfl(e1, hi - 1), lane, stg, &phase, &vofs);
+        }
+      }
+      if (fits) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wave_lds_sync();
+      }
+      const int64_t base = __shfl(e0, lo);  // (all lanes: no shuffle in divergent code)
+      if (lane >= lo && lane < hi) flat_place(f, fits, stg, phase, base, vofs, p, e0, e1 - e0, row);
+      lo = hi;
+    }
   }
   if (PROF) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   FLAT_STAMP(5);
@@ -3114,6 +3168,47 @@ size_t flat_lds(const VarLaunch& L, int cap, int nw) {
   return (size_t)cap + (size_t)nw * L.stg_bytes + (size_t)L.num_var * 64 * sizeof(int32_t) + sbase_lds(L);
 }
 
+// Encode: staging only for the min(NW, num_var) waves that place var fields.
+size_t flat_lds_enc(const VarLaunch& L, int cap, int nw) {
+  const int np = var_placers(L.num_var, nw);
+  const int nslot = L.num_var < np ? L.num_var : np;
+  return (size_t)cap + (size_t)nslot * L.stg_bytes + (size_t)L.num_var * 64 * sizeof(int32_t) + sbase_lds(L);
+}
+
+// Encode staging per slot sized from the caller's capacity (normally the exact
+// encoded size): 1.5x the mean per-field span of a 64-record tile, in [2, 16] KiB,
+// so most tiles stage each field in one record group -- but never at the cost of
+// resident workgroups (hipOccupancy with the kernel's registers and LDS):
+// FORY_ROWFMT_VARSTG overrides.
+template <typename K>
+int enc_stg_bytes(K* k, const VarLaunch& L, int64_t capacity, int cap, int nw) {
+  if (getenv("FORY_ROWFMT_VARSTG") || L.num_rows < 64 || L.num_var == 0) return L.stg_bytes;
+  const int64_t var_row = capacity / L.num_rows - L.fixed_size - (L.frame ? 12 : 0) - L.nested_fixed;
+  const int64_t per = var_row > 0 ? 64 * var_row / L.num_var : 0;
+  int b = (int)((per * 3 / 2 + 512 + 255) & ~int64_t(255));
+  b = b < 2048 ? 2048 : (b > 16384 ? 16384 : b);
+  auto occ = [&](int stg) {
+    VarLaunch T = L;
+    T.stg_bytes = stg;
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(k), 64 * nw,
+                                                     flat_lds_enc(T, cap, nw)) != hipSuccess)
+      return -1;
+    return blocks;
+  };
+  // memo of the last answer per instantiation (same plan shape -> same answer)
+  static int m_cap = -1, m_b = -1, m_nv = -1, m_ns = -1, m_res = 2048;
+  if (m_cap == cap && m_b == b && m_nv == L.num_var && m_ns == L.num_struct) return m_res;
+  const int want = occ(2048);
+  int r = 2048;
+  if (want > 0) {
+    r = b;
+    while (r > 2048 && occ(r) < want) r -= 256;
+  }
+  m_cap = cap, m_b = b, m_nv = L.num_var, m_ns = L.num_struct, m_res = r;
+  return r;
+}
+
 // LDS image of the spill launches: 3x the main image, in [32, 96] KiB
 // (FORY_ROWFMT_SPILLCAP overrides, for tests).
 int spill_cap(int cap) {
@@ -3132,18 +3227,20 @@ unsigned spill_grid(K* k, const VarLaunch& L, size_t lds, int wg) {
 }
 
 template <bool FRAME, int NW, bool PROF>
-void launch_flat_enc_t(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
+void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                        int cap, hipStream_t s) {
-  const SpillArgs sp = spill_args(L, cap);
-  (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
+  const SpillArgs sp = spill_args(L0, cap);
+  (void)hipMemsetAsync(L0.spill_count, 0, sizeof(int32_t), s);
   auto* k = &var_encode_flat_kernel<FRAME, NW, PROF, false>;
-  var_tile_launch(k, L, cap);
-  hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds(L, cap, NW), s, L, L.prog,
+  var_tile_launch(k, L0, cap);
+  VarLaunch L = L0;
+  L.stg_bytes = enc_stg_bytes(k, L0, capacity, cap, NW);
+  hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds_enc(L, cap, NW), s, L, L.prog,
                      L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, cap, sp);
   auto* k2 = &var_encode_flat_kernel<FRAME, NW, PROF, true>;
   var_tile_launch(k2, L, sp.cap);
-  hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
-                     flat_lds(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, sp.cap,
+  hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds_enc(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
+                     flat_lds_enc(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, sp.cap,
                      sp);
 }
 
