@@ -127,7 +127,8 @@ int bind_var(const Plan& p, const fory_column* cols, int64_t n, std::vector<Colu
     d.out_offsets = c.offsets;
     d.out_validity = nd.nullable ? c.validity : nullptr;
     if (n > 0) {
-      if ((nd.kind == fory_amd::KIND_BYTES || nd.kind == fory_amd::KIND_LIST) && !c.offsets)
+      if ((nd.kind == fory_amd::KIND_BYTES || nd.kind == fory_amd::KIND_LIST || nd.kind == fory_amd::KIND_MAP) &&
+          !c.offsets)
         return fail(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(idx) + " needs offsets");
     }
     (*out)[idx] = d;
@@ -216,6 +217,8 @@ int var_tile_cap(const Plan& p, int frame) {
     const fory_amd::Node& nd = p.nodes[k];
     if (nd.kind == fory_amd::KIND_BYTES) est += 32;
     else if (nd.kind == fory_amd::KIND_LIST) est += 16 + 16 * std::max<int64_t>(1, p.nodes[nd.children[0]].width);
+    else if (nd.kind == fory_amd::KIND_MAP)  // [i64][keys][values], ~16 entries
+      est += 40 + 16 * (p.nodes[nd.children[0]].width + p.nodes[nd.children[1]].width);
     else if (nd.kind == fory_amd::KIND_STRUCT)  // child rows live in the variable region
       est += ((int64_t)(nd.children.size() + 63) / 64) * 8 + 8 * (int64_t)nd.children.size();
   }
@@ -308,7 +311,10 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   rc = upload(ws, host.data(), (int64_t)host.size(), s);
   if (rc) return rc;
   uint8_t* wsb = static_cast<uint8_t*>(ws);
-  L->flat = var.size() <= 32 && st.size() <= (size_t)fory_amd::kMaxTileStructs ? 1 : 0;
+  bool has_map = false;
+  for (const fory_amd::Op& op : p.program) has_map |= op.code == fory_amd::OP_MAP;
+  // maps run on the generic tile interpreter (enc_record / dec_record)
+  L->flat = !has_map && var.size() <= 32 && st.size() <= (size_t)fory_amd::kMaxTileStructs ? 1 : 0;
   L->num_var = (int32_t)var.size();
   L->num_struct = (int32_t)st.size();
   L->vf = reinterpret_cast<const fory_amd::VarFieldDev*>(wsb + o_var);
@@ -509,7 +515,8 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
       hipStream_t s0 = static_cast<hipStream_t>(stream);
       for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
         const int k = p.nodes[idx].kind;
-        if ((k == fory_amd::KIND_BYTES || k == fory_amd::KIND_LIST) && out_cols && out_cols[idx].offsets)
+        if ((k == fory_amd::KIND_BYTES || k == fory_amd::KIND_LIST || k == fory_amd::KIND_MAP) && out_cols &&
+            out_cols[idx].offsets)
           (void)hipMemsetAsync(out_cols[idx].offsets, 0, sizeof(int32_t), s0);
       }
     }
@@ -528,7 +535,7 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
   if (fory_amd::var_decode_tiled_offsets(L)) return FORY_OK;  // tile bases written; decode fills the rest
   for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
     const int k = p.nodes[idx].kind;
-    if (k != fory_amd::KIND_BYTES && k != fory_amd::KIND_LIST) continue;
+    if (k != fory_amd::KIND_BYTES && k != fory_amd::KIND_LIST && k != fory_amd::KIND_MAP) continue;
     e = fory_amd::launch_scan_offsets_i32(out_cols[idx].offsets, num_rows, partials_ptr(p, d_workspace),
                                           d_status, s);
     if (e != hipSuccess) return hip_fail(e, "scan offsets");

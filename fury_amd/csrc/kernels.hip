@@ -1272,6 +1272,12 @@ __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* _
           size += 8 + bitmap_bytes(n) + round8(n * w);
         }
         break;
+      case OP_MAP:  // [i64 keyArrayBytes][key array][value array]
+        if (!absent_depth && (!(op.d & 1) || col_valid(c, i))) {
+          const int64_t n = (int64_t)c.offsets[i + 1] - c.offsets[i];
+          size += 8 + 2 * (8 + bitmap_bytes(n)) + round8(n * (op.e & 0xff)) + round8(n * ((op.e >> 8) & 0xff));
+        }
+        break;
     }
   }
   sizes[i] = size;
@@ -1421,6 +1427,51 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
         }
         wi += ahdr + fixed_part;
         gst64(slot, ((uint64_t)(astart - st_start[depth]) << 32) | (uint32_t)(wi - astart));
+        break;
+      }
+      case OP_MAP: {
+        if (isnull) {
+          set_null_bit(bitmap, op.a);
+          gst64(slot, 0);
+          break;
+        }
+        // serializeForMap (BaseBinaryEncoderBuilder.java:370-427): reserve 8 bytes,
+        // key array (serializeForArray of keySet), back-patch its size
+        // (writeDirectly(offset, size), BinaryWriter.java:239-241), value array,
+        // then setOffsetAndSize(ordinal, offset, writerIndex - offset).
+        const int64_t e0 = c.offsets[i], n = (int64_t)c.offsets[i + 1] - e0;
+        const int64_t mstart = wi;
+        wi += 8;
+        int64_t keybytes = 0;
+        for (int part = 0; part < 2; ++part) {  // keys, then values
+          const ColumnDev& it = cols[op.c + part];
+          const int w = (op.e >> (8 * part)) & 0xff;
+          const int iflags = (op.e >> (16 + 8 * part)) & 0xff;
+          uint8_t* arr = row + wi;
+          const int32_t ahdr = 8 + bitmap_bytes(n);
+          gst64(arr, (uint64_t)n);  // BinaryArrayWriter.reset(n) (BinaryArrayWriter.java:93-118)
+          for (int b = 8; b < ahdr; b += 8) gst64(arr + b, 0);
+          uint8_t* data = arr + ahdr;
+          const int64_t fixed_part = round8(n * w);
+          for (int64_t j = 0; j < n; ++j) {
+            const bool enull = (iflags & 1) && !col_valid(it, e0 + j);
+            uint64_t v = 0;
+            if (enull) arr[8 + (j >> 3)] |= (uint8_t)(1u << (j & 7));
+            else v = load_elem(it.values, w, e0 + j);
+            if (iflags & 2) v = v ? 1 : 0;
+            switch (w) {
+              case 8: gst64(data + 8 * j, v); break;
+              case 4: st32(data + 4 * j, (uint32_t)v); break;
+              case 2: data[2 * j] = (uint8_t)v; data[2 * j + 1] = (uint8_t)(v >> 8); break;
+              default: data[j] = (uint8_t)v; break;
+            }
+          }
+          for (int64_t k = n * w; k < fixed_part; ++k) data[k] = 0;
+          wi += ahdr + fixed_part;
+          if (part == 0) keybytes = ahdr + fixed_part;
+        }
+        gst64(row + mstart, (uint64_t)keybytes);
+        gst64(slot, ((uint64_t)(mstart - st_start[depth]) << 32) | (uint32_t)(wi - mstart));
         break;
       }
     }
@@ -1592,6 +1643,71 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
                   }
               }
             } else {
+              for (int64_t j = 0; j < n; ++j) {
+                const bool en = (arr[8 + (j >> 3)] >> (j & 7)) & 1;  // BinaryArray.isNullAt
+                uint64_t v = 0;
+                if (!en) {
+                  const uint8_t* p = arr + ahdr + j * w;
+                  switch (w) {
+                    case 8: v = gld64(p); break;
+                    case 4: v = ld32(p); break;
+                    case 2: v = (uint64_t)p[0] | ((uint64_t)p[1] << 8); break;
+                    default: v = p[0]; break;
+                  }
+                }
+                if (iflags & 2) v = (v & 0xff) ? 1 : 0;
+                store_elem(it.out_values, w, e0 + j, v);
+                if ((iflags & 1) && it.out_validity) {
+                  const int64_t q = e0 + j;
+                  const uint32_t bit = 1u << (q & 31);
+                  uint32_t* word = reinterpret_cast<uint32_t*>(it.out_validity) + (q >> 5);
+                  if (en) atomicAnd(word, ~bit);
+                  else atomicOr(word, bit);
+                }
+              }
+            }
+          }
+        }
+        break;
+      }
+      case OP_MAP: {  // BinaryMap.pointTo (BinaryMap.java:62-77): keys + values arrays
+        int64_t n = 0, rel = 0, kat = 0, vat = 0;
+        if (!isnull) {
+          const uint64_t os = gld64(slot);
+          rel = (int32_t)(os >> 32);
+          const int64_t msz = (int32_t)(uint32_t)os;
+          const int64_t at = st_start[depth] + rel;
+          if (rel < 0 || msz < 8 || at + msz > row_len) {
+            set_status(status, FORY_ERR_CORRUPT);
+          } else {
+            const int64_t kbytes = (int32_t)ld32(row + at);  // buf.getInt32(offset)
+            kat = at + 8;
+            vat = kat + kbytes;
+            const int kw = op.e & 0xff, vw = (op.e >> 8) & 0xff;
+            if (kbytes < 8 || vat + 8 > at + msz) {
+              set_status(status, FORY_ERR_CORRUPT);
+            } else {
+              n = (int32_t)(int64_t)gld64(row + kat);
+              const int64_t nv = (int32_t)(int64_t)gld64(row + vat);
+              if (n < 0 || n != nv || kat + 8 + bitmap_bytes(n) + n * kw > vat ||
+                  vat + 8 + bitmap_bytes(n) + n * vw > at + msz) {
+                set_status(status, FORY_ERR_CORRUPT);  // keys.numElements() != values.numElements()
+                n = 0;
+              }
+            }
+          }
+        }
+        if (live) {
+          if (!WRITE) {
+            c.out_offsets[i + 1] = (int32_t)n;
+          } else if (n > 0) {
+            const int64_t e0 = c.out_offsets[i];
+            for (int part = 0; part < 2; ++part) {
+              const ColumnDev& it = cols[op.c + part];
+              const int w = (op.e >> (8 * part)) & 0xff;
+              const int iflags = (op.e >> (16 + 8 * part)) & 0xff;
+              const uint8_t* arr = row + (part ? vat : kat);
+              const int32_t ahdr = 8 + bitmap_bytes(n);
               for (int64_t j = 0; j < n; ++j) {
                 const bool en = (arr[8 + (j >> 3)] >> (j & 7)) & 1;  // BinaryArray.isNullAt
                 uint64_t v = 0;

@@ -32,7 +32,7 @@ static bool supported_type(int32_t t) {
     case FORY_TYPE_BOOL: case FORY_TYPE_INT8: case FORY_TYPE_INT16: case FORY_TYPE_INT32:
     case FORY_TYPE_INT64: case FORY_TYPE_FLOAT: case FORY_TYPE_DOUBLE: case FORY_TYPE_STRING:
     case FORY_TYPE_BINARY: case FORY_TYPE_DATE32: case FORY_TYPE_TIMESTAMP: case FORY_TYPE_LIST:
-    case FORY_TYPE_STRUCT:
+    case FORY_TYPE_STRUCT: case FORY_TYPE_MAP:
       return true;
     default:
       return false;
@@ -69,7 +69,12 @@ static int parse_node(const fory_field_desc* d, int32_t n, int32_t at, Plan* p, 
     *err = "list field must have exactly one child (DataTypes.arrayField)";
     return FORY_ERR_ENCODER;
   }
-  if (f.type_id != FORY_TYPE_LIST && f.type_id != FORY_TYPE_STRUCT && f.num_children != 0) {
+  if (f.type_id == FORY_TYPE_MAP && f.num_children != 2) {
+    *err = "map field must have exactly two children: key and value (DataTypes.mapField)";
+    return FORY_ERR_ENCODER;
+  }
+  if (f.type_id != FORY_TYPE_LIST && f.type_id != FORY_TYPE_STRUCT && f.type_id != FORY_TYPE_MAP &&
+      f.num_children != 0) {
     // DataTypes.java:533-538 "field type should not be nested"
     *err = "field type should not be nested, but got type id " + std::to_string(f.type_id);
     return FORY_ERR_ENCODER;
@@ -79,6 +84,7 @@ static int parse_node(const fory_field_desc* d, int32_t n, int32_t at, Plan* p, 
     case FORY_TYPE_STRING: case FORY_TYPE_BINARY: nd.kind = KIND_BYTES; break;
     case FORY_TYPE_STRUCT: nd.kind = KIND_STRUCT; break;
     case FORY_TYPE_LIST: nd.kind = KIND_LIST; break;
+    case FORY_TYPE_MAP: nd.kind = KIND_MAP; break;
     default: nd.kind = KIND_FIXED; break;
   }
   int32_t cur = at + 1;
@@ -145,6 +151,24 @@ static int compile_field(const Plan& p, int32_t idx, int32_t ordinal, std::vecto
       }
       int32_t iflags = (it.nullable ? 1 : 0) | (it.kind == KIND_BOOL ? 2 : 0);
       prog->push_back({OP_LIST, ordinal, idx, item, flags, it.width | (iflags << 8)});
+      return FORY_OK;
+    }
+    case KIND_MAP: {  // serializeForMap (BaseBinaryEncoderBuilder.java:370-427)
+      const int32_t key = nd.children[0], val = nd.children[1];
+      const Node& k = p.nodes[key];
+      const Node& v = p.nodes[val];
+      if (k.nullable) {
+        *err = "Map's keys must be non-nullable";  // DataTypes.mapField (DataTypes.java:419)
+        return FORY_ERR_ENCODER;
+      }
+      if ((k.kind != KIND_FIXED && k.kind != KIND_BOOL) || (v.kind != KIND_FIXED && v.kind != KIND_BOOL)) {
+        *err = "device path supports map<fixed-width, fixed-width> only (got key type id " +
+               std::to_string(k.type_id) + ", value type id " + std::to_string(v.type_id) + ")";
+        return FORY_ERR_UNSUPPORTED;
+      }
+      const int32_t kf = k.kind == KIND_BOOL ? 2 : 0;
+      const int32_t vf = (v.nullable ? 1 : 0) | (v.kind == KIND_BOOL ? 2 : 0);
+      prog->push_back({OP_MAP, ordinal, idx, key, flags, k.width | (v.width << 8) | (kf << 16) | (vf << 24)});
       return FORY_OK;
     }
   }

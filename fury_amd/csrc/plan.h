@@ -28,6 +28,7 @@ enum FieldKind : int32_t {
   KIND_BYTES = 2,   // utf8 / binary: (offset<<32|size) slot + padded bytes
   KIND_STRUCT = 3,  // nested row inline in the variable section
   KIND_LIST = 4,    // BinaryArray inline in the variable section
+  KIND_MAP = 5,     // BinaryMap inline: [i64 keyArrayBytes][key BinaryArray][value BinaryArray]
 };
 
 // Per top-level field of a fixed-width plan (read by the tiled kernels).
@@ -51,6 +52,8 @@ enum OpCode : int32_t {
   OP_STRUCT_BEGIN = 2, // a=ordinal b=col c=nfields d=flags e=index of matching END
   OP_STRUCT_END = 3,
   OP_LIST = 4,         // a=ordinal b=col c=item col d=flags e=item width | item flags<<8
+  OP_MAP = 5,          // a=ordinal b=col c=key col (value col = c+1) d=flags
+                       // e=key width | value width<<8 | key flags<<16 | value flags<<24
 };
 
 struct Op {

@@ -97,6 +97,19 @@ def _build(f: Field, vals: Sequence[Any], out: List[HostColumn], absent: Optiona
             offs[i + 1] = len(items)
         col.offsets = offs
         _build(f.children[0], items, out)
+    elif t == ArrowType.MAP:  # Arrow map: entry offsets + key / value columns (entries struct elided)
+        offs = np.zeros(n + 1, dtype=np.int32)
+        keys: List[Any] = []
+        vals_: List[Any] = []
+        for i, v in enumerate(vals):
+            if v is not None:
+                pairs = list(v.items()) if isinstance(v, dict) else list(v)
+                keys.extend(k for k, _ in pairs)
+                vals_.extend(x for _, x in pairs)
+            offs[i + 1] = len(keys)
+        col.offsets = offs
+        _build(f.children[0], keys, out)
+        _build(f.children[1], vals_, out)
     elif t == ArrowType.STRUCT:
         gone = ~valid if absent is None else (~valid | absent)
         for c in f.children:

@@ -132,15 +132,18 @@ class RowEncoder:
         n = num_rows
         fields = p.fields
         cols = [DeviceColumn(length=n) for _ in fields]
-        item_of = {}
+        item_of = {}  # element columns sized after decode_sizes: list items, map keys + values
         for i, f in enumerate(fields):
             if f.type.id == ArrowType.LIST:
                 item_of[i + 1] = i
+            elif f.type.id == ArrowType.MAP:
+                item_of[i + 1] = i
+                item_of[i + 2] = i
         for i, f in enumerate(fields):
             if i in item_of:
                 continue  # sized after decode_sizes
             t = f.type.id
-            if t in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST):
+            if t in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP):
                 cols[i].offsets = torch.zeros(n + 1, dtype=torch.int32, device=self.device)
             elif t != ArrowType.STRUCT:
                 cols[i].values = torch.empty(max(1, n), dtype=_torch_dtype(t), device=self.device)
@@ -150,7 +153,7 @@ class RowEncoder:
             raise ValueError("varlen schema: row offsets are required to decode")
         native.decode_sizes(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
         var_idx = [i for i, f in enumerate(fields)
-                   if f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST)]
+                   if f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP)]
         totals = {}
         if var_idx and n > 0:
             last = torch.stack([cols[i].offsets[n] for i in var_idx]).cpu().tolist()
@@ -159,12 +162,13 @@ class RowEncoder:
         for i in var_idx:
             tot = int(totals.get(i, 0))
             f = fields[i]
-            if f.type.id == ArrowType.LIST:
-                it = fields[i + 1]
-                cols[i + 1] = DeviceColumn(
-                    torch.empty(max(1, tot), dtype=_torch_dtype(it.type.id), device=self.device), None,
-                    torch.zeros(_validity_bytes(tot), dtype=torch.uint8, device=self.device)
-                    if it.nullable else None, tot)
+            if f.type.id in (ArrowType.LIST, ArrowType.MAP):
+                for k in ((i + 1,) if f.type.id == ArrowType.LIST else (i + 1, i + 2)):
+                    it = fields[k]
+                    cols[k] = DeviceColumn(
+                        torch.empty(max(1, tot), dtype=_torch_dtype(it.type.id), device=self.device), None,
+                        torch.zeros(_validity_bytes(tot), dtype=torch.uint8, device=self.device)
+                        if it.nullable else None, tot)
             else:
                 cols[i].values = torch.empty(max(1, tot), dtype=torch.uint8, device=self.device)
         native.decode(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)

@@ -164,6 +164,18 @@ class DataTypes:
         return Field(name, DataType(ArrowType.LIST), True, [item])
 
     @staticmethod
+    def map_field(name: str, key: Field, value: Field) -> Field:
+        """DataTypes.mapField (DataTypes.java:404-424): nullable map, key not nullable. The
+        entries struct of Arrow's map type is elided: children are [key, value], the
+        fields the schema hash visits (DataTypes.java:522-527)."""
+        if key.nullable:
+            from .errors import IllegalArgumentException
+            raise IllegalArgumentException("Map's keys must be non-nullable")
+        return Field(name, DataType(ArrowType.MAP), True,
+                     [Field("key", key.type, False, key.children), Field("value", value.type, value.nullable,
+                                                                          value.children)])
+
+    @staticmethod
     def struct_field(name: str, nullable: bool, children: Sequence[Field]) -> Field:
         return Field(name, DataType(ArrowType.STRUCT), nullable, list(children))
 

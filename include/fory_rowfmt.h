@@ -71,19 +71,23 @@ enum fory_type_id {
   FORY_TYPE_DATE32 = 16,
   FORY_TYPE_TIMESTAMP = 18,
   FORY_TYPE_LIST = 25,
-  FORY_TYPE_STRUCT = 26
+  FORY_TYPE_STRUCT = 26,
+  FORY_TYPE_MAP = 30
 };
 
 /* One node of the schema, flattened in pre-order. A schema is the sequence of
  * its top-level fields; a STRUCT node is followed by its `num_children` child
- * subtrees, a LIST node by exactly one subtree (the element field "item").
+ * subtrees, a LIST node by exactly one subtree (the element field "item"), a
+ * MAP node by exactly two: the key field (not nullable, DataTypes.mapField
+ * DataTypes.java:418-424) and the value field — Arrow's entries struct is
+ * elided, as in the schema hash (DataTypes.java:522-527).
  * Order must be the Java schema order: TypeInference.inferSchema
  * (TypeInference.java:68-80,238-247) = fields sorted by name
  * (Descriptor.java:415-423). */
 typedef struct fory_field_desc {
   int32_t type_id;       /* enum fory_type_id */
   int32_t nullable;      /* 1 = boxed/String/bean/List (TypeInference.java:182-247) */
-  int32_t num_children;  /* STRUCT: >= 0, LIST: 1, others: 0 */
+  int32_t num_children;  /* STRUCT: >= 0, LIST: 1, MAP: 2, others: 0 */
   int32_t reserved;      /* must be 0 */
 } fory_field_desc;
 
@@ -92,6 +96,8 @@ typedef struct fory_field_desc {
  *                (BOOL: 1 byte per value, non-zero = true; FLOAT/DOUBLE raw IEEE bits)
  *  STRING/BINARY: offsets = length+1 int32 Arrow offsets into values (bytes)
  *  LIST        : offsets = length+1 int32 Arrow offsets into the child column
+ *  MAP         : offsets = length+1 int32 Arrow offsets into the key and value
+ *                columns (entries); key/value columns hold one slot per entry
  *  STRUCT      : values/offsets unused; children have the same length
  *  validity    : Arrow validity bitmap, LSB-first, 1 = valid; NULL = all valid.
  *                Only read/written for nullable fields.
@@ -176,16 +182,16 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols,
  * are i*stride (16-byte aligned d_rows).
  *
  * fory_rowfmt_decode_sizes (varlen plans; no-op for fixed-width): writes
- * offsets[num_rows] (the total: bytes, or items for LIST) of every
- * STRING/BINARY/LIST output column's `offsets` array (num_rows+1 int32,
+ * offsets[num_rows] (the total: bytes, or items for LIST, entries for MAP) of
+ * every STRING/BINARY/LIST/MAP output column's `offsets` array (num_rows+1 int32,
  * device), so the caller can size `values` and list element columns. The
  * rest of `offsets` is complete after fory_rowfmt_decode (for plans whose
  * top-level fields are all fixed/string/binary/list, decode_sizes writes
  * tile-start prefixes at offsets[64*k] and decode fills the records in
  * between): pass the same rows, row offsets and column arrays to both calls
  * and do not modify `offsets` in between. The device path supports list
- * elements of fixed width only (FORY_ERR_UNSUPPORTED at plan creation
- * otherwise).
+ * elements and map keys/values of fixed width only (FORY_ERR_UNSUPPORTED at
+ * plan creation otherwise).
  *
  * fory_rowfmt_decode: writes values/offsets/validity of out_cols. Null
  * values decode to 0 (RowEncoderBuilder.java:239-246 leaves the Java default).

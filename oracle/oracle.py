@@ -147,7 +147,7 @@ def decode(schema, buf: np.ndarray, offsets: Optional[np.ndarray], n: int, frame
         elif t in (ArrowType.STRING, ArrowType.BINARY):
             c.offsets = np.zeros(ln + 1, dtype=np.int32)
             c.values = np.zeros(max(1, int(nbytes[i])), dtype=np.uint8)
-        elif t == ArrowType.LIST:
+        elif t in (ArrowType.LIST, ArrowType.MAP):
             c.offsets = np.zeros(ln + 1, dtype=np.int32)
         if f.nullable:
             c.validity = np.zeros(validity_bytes(ln), dtype=np.uint8)

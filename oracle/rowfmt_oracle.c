@@ -13,6 +13,8 @@
  *   - row writer           F/row/binary/writer/BinaryRowWriter.java:46-136
  *   - writer base          F/row/binary/writer/BinaryWriter.java:40-194
  *   - array writer         F/row/binary/writer/BinaryArrayWriter.java:93-206
+ *   - map layout           F/row/binary/BinaryMap.java:30-77 (writer:
+ *                          F/encoder/BaseBinaryEncoderBuilder.java:370-427)
  *   - per-type dispatch    F/encoder/BaseBinaryEncoderBuilder.java:149-490
  *   - framing              F/encoder/Encoders.java:177-225
  *   - readers              F/row/binary/BinaryRow.java:110-123,
@@ -292,6 +294,36 @@ static void write_list_body(owriter* parent, int64_t ordinal, const otree* t, in
   w_set_offset_and_size(parent, ordinal, off, b->wi - off);
 }
 
+static void write_map_body(owriter* parent, int64_t ordinal, const otree* t, int idx,
+                           const fory_column* cols, int64_t i) {
+  /* serializeForMap (BaseBinaryEncoderBuilder.java:370-427): offset = writerIndex;
+   * writeDirectly(-1) reserves 8 bytes (BinaryWriter.java:232-236); the key set
+   * and the values are written as two BinaryArrays (serializeForArray); the key
+   * array's size is back-patched at offset (writeDirectly(offset, size) :239-241);
+   * then setOffsetAndSize(ordinal, offset, writerIndex - offset). Entries are the
+   * Arrow map's entries [offsets[i], offsets[i+1]) in order. */
+  const onode* nd = &t->nodes[idx];
+  const fory_column* c = &cols[idx];
+  int64_t b0 = c->offsets[i], n = c->offsets[i + 1] - b0;
+  obuf* b = parent->b;
+  int64_t off = b->wi;
+  grow(b, 8);
+  put64(b, off, (uint64_t)-1);
+  b->wi += 8;
+  int64_t key_bytes = 0;
+  for (int part = 0; part < 2; part++) {
+    int child = nd->child[part];
+    const onode* it = &t->nodes[child];
+    int64_t a0 = b->wi;
+    owriter aw;
+    array_reset(&aw, b, n, it->width < 0 ? 8 : it->width);
+    for (int64_t j = 0; j < n; j++) write_value(&aw, j, t, child, cols, b0 + j);
+    if (part == 0) key_bytes = b->wi - a0;
+  }
+  put64(b, off, (uint64_t)key_bytes);
+  w_set_offset_and_size(parent, ordinal, off, b->wi - off);
+}
+
 static void write_value(owriter* w, int64_t ordinal, const otree* t, int idx,
                         const fory_column* cols, int64_t i) {
   const onode* nd = &t->nodes[idx];
@@ -334,6 +366,9 @@ static void write_value(owriter* w, int64_t ordinal, const otree* t, int idx,
       return;
     case FORY_TYPE_LIST:
       write_list_body(w, ordinal, t, idx, cols, i);
+      return;
+    case FORY_TYPE_MAP:
+      write_map_body(w, ordinal, t, idx, cols, i);
       return;
     default:
       b->overflow = 2;
@@ -480,6 +515,28 @@ static void read_value(odec* D, const otree* t, int idx, const fory_column* cols
       for (int64_t j = 0; j < n; j++) {
         int nul = (int)((rd(D, at + 8 + (j >> 3), 1) >> (j & 7)) & 1); /* BinaryArray.isNullAt :128-130 */
         read_value(D, t, item, cols, first + j, nul, at + hdr + j * es, at);
+      }
+      D->cursor[idx] = first + n;
+      if (!D->sizing) c->offsets[i + 1] = (int32_t)(first + n);
+      return;
+    }
+    case FORY_TYPE_MAP: { /* getMap + BinaryMap.pointTo (BinaryMap.java:62-77) */
+      int64_t kbytes = (int32_t)rd(D, at, 4);  /* buf.getInt32(offset) */
+      int64_t kat = at + 8, vat = at + 8 + kbytes;
+      if (kbytes < 8 || vat + 8 > at + size) { D->bad = 1; return; }
+      int64_t n = (int32_t)rd(D, kat, 8), nv = (int32_t)rd(D, vat, 8);
+      if (n < 0 || n != nv) { D->bad = 1; return; } /* UnsupportedOperationException */
+      int64_t first = D->cursor[idx];
+      int64_t hdr = 8 + bitmap_bytes(n);
+      for (int part = 0; part < 2; part++) {
+        int child = nd->child[part];
+        const onode* it = &t->nodes[child];
+        int64_t es = it->width < 0 ? 8 : it->width;
+        int64_t aat = part ? vat : kat;
+        for (int64_t j = 0; j < n; j++) {
+          int nul = (int)((rd(D, aat + 8 + (j >> 3), 1) >> (j & 7)) & 1);
+          read_value(D, t, child, cols, first + j, nul, aat + hdr + j * es, aat);
+        }
       }
       D->cursor[idx] = first + n;
       if (!D->sizing) c->offsets[i + 1] = (int32_t)(first + n);

@@ -68,11 +68,15 @@ def main():
             typ = pa.list_(to_pa(f.children[0]))
         elif t == ArrowType.STRUCT:
             typ = pa.struct([to_pa(c) for c in f.children])
+        elif t == ArrowType.MAP:
+            typ = pa.map_(to_pa(f.children[0]).type, to_pa(f.children[1]).type)
         else:
             raise ValueError(t)
         return pa.field(f.name, typ, nullable=f.nullable)
 
     from fury_amd.format.types import DataType, DataTypes, Field, Schema
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from helpers import deep_nested_schema, maps_schema
 
     edge = {
         "empty": Schema([]),
@@ -84,6 +88,8 @@ def main():
             Field("u", DataType(ArrowType.INT64))])])]),
         "wide_300": Schema([Field(f"c{i:03d}", DataType(ArrowType.INT64), False) for i in range(300)]),
         "struct_boxed": W.struct_schema(100, boxed=True),
+        "maps": maps_schema(),
+        "deep_nested": deep_nested_schema(),
     }
     schemas = {"struct104": W.struct_schema(), "mixed40": W.mixed_schema(),
                "nested": W.nested_schema(), **edge}

@@ -99,7 +99,7 @@ def columns_equal(schema: Schema, a: List[HostColumn], b: List[HostColumn]) -> L
             bad = np.nonzero(np.any(xa != xb, axis=1) & va)[0]
             if len(bad):
                 errs.append(f"{i}:{f.name} values differ at rows {bad[:5]}")
-        if t in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST):
+        if t in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP):
             oa = np.asarray(ca.offsets)[: n + 1].astype(np.int64)
             ob = np.asarray(cb.offsets)[: n + 1].astype(np.int64)
             la, lb = np.diff(oa), np.diff(ob)
@@ -107,7 +107,7 @@ def columns_equal(schema: Schema, a: List[HostColumn], b: List[HostColumn]) -> L
             if len(bad):
                 errs.append(f"{i}:{f.name} lengths differ at rows {bad[:5]}")
                 continue
-            if t != ArrowType.LIST:
+            if t not in (ArrowType.LIST, ArrowType.MAP):
                 for r in np.nonzero(va)[0]:
                     if bytes(np.asarray(ca.values)[oa[r]:oa[r + 1]]) != bytes(np.asarray(cb.values)[ob[r]:ob[r + 1]]):
                         errs.append(f"{i}:{f.name} bytes differ at row {r}")
@@ -203,6 +203,47 @@ def deep_nested_schema() -> Schema:
                    Field("tag", DataType(ArrowType.STRING), False)])
 
 
+def maps_rows(n: int, seed: int):
+    """Rows of maps_schema: null / empty / up to 70 entries (bitmap beyond one word),
+    null values, bool values, a map inside a nullable struct."""
+    rng = np.random.default_rng(seed)
+    rows = []
+    for i in range(n):
+        def m(k, null_p=0.1, vals=lambda: int(rng.integers(-2**62, 2**62))):
+            if rng.random() < null_p:
+                return None
+            keys = rng.choice(10**6, size=int(rng.integers(0, k)), replace=False)
+            return {int(x): (None if rng.random() < 0.15 else vals()) for x in keys}
+        s = None if rng.random() < 0.2 else {
+            "flags": m(6, vals=lambda: bool(rng.random() < 0.5)),
+            "w": int(rng.integers(-999, 999)),
+        }
+        rows.append({
+            "a": int(rng.integers(-2**31, 2**31)),
+            "counts": m(70),
+            "s": s,
+            "scores": None if rng.random() < 0.1 else {int(x): float(rng.standard_normal())
+                                                       for x in rng.choice(1000, size=rng.integers(0, 5),
+                                                                           replace=False)},
+        })
+    return rows
+
+
+def maps_schema() -> Schema:
+    return Schema([
+        Field("a", DataType(ArrowType.INT32), False),
+        DataTypes.map_field("counts", Field("key", DataType(ArrowType.INT32), False),
+                            Field("value", DataType(ArrowType.INT64), True)),
+        DataTypes.struct_field("s", True, [
+            DataTypes.map_field("flags", Field("key", DataType(ArrowType.INT64), False),
+                                Field("value", DataType(ArrowType.BOOL), True)),
+            Field("w", DataType(ArrowType.INT16), False),
+        ]),
+        DataTypes.map_field("scores", Field("key", DataType(ArrowType.INT16), False),
+                            Field("value", DataType(ArrowType.DOUBLE), False)),
+    ])
+
+
 def catalog():
     """name -> (schema, host column factory(n, seed))."""
     return {
@@ -220,6 +261,7 @@ def catalog():
         "flat_mix": (flat_mix_schema(), lambda n, s: build_columns(flat_mix_schema(), flat_mix_rows(n, s))),
         "deep_nested": (deep_nested_schema(),
                         lambda n, s: build_columns(deep_nested_schema(), deep_nested_rows(n, s))),
+        "maps": (maps_schema(), lambda n, s: build_columns(maps_schema(), maps_rows(n, s))),
     }
 
 

@@ -67,8 +67,14 @@ def test_plan_errors():
     bad_nested = Schema([Field("x", DataType(ArrowType.INT32), False, [Field("y", DataType(ArrowType.INT32))])])
     with pytest.raises(errors.EncoderException):
         NativePlan(bad_nested)
-    with pytest.raises(errors.UnsupportedOperationException):
+    with pytest.raises(errors.EncoderException):  # a map needs [key, value] children
         NativePlan(Schema([Field("m", DataType(ArrowType.MAP), True)]))
+    with pytest.raises(errors.UnsupportedOperationException):  # device path: map<fixed, fixed> only
+        NativePlan(Schema([DataTypes.map_field("m", Field("key", DataType(ArrowType.STRING), False),
+                                               Field("value", DataType(ArrowType.INT32), True))]))
+    with pytest.raises(errors.EncoderException):  # Map's keys must be non-nullable (DataTypes.java:419)
+        NativePlan(Schema([Field("m", DataType(ArrowType.MAP), True, [Field("key", DataType(ArrowType.INT32), True),
+                                                                       Field("value", DataType(ArrowType.INT32))])]))
     with pytest.raises(errors.UnsupportedOperationException):  # device path: list<fixed> only
         NativePlan(Schema([DataTypes.array_field("l", Field("item", DataType(ArrowType.STRING)))]))
     # truncated descriptor: a struct promising 2 children with only 1 present

@@ -57,7 +57,7 @@ def kernel_variant(request, monkeypatch):
 
 
 VARLEN = [k for k, (sch, _) in catalog().items()
-          if any(f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.STRUCT)
+          if any(f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.STRUCT, ArrowType.MAP)
                  for f in sch.fields)]
 FIXED = [k for k in catalog() if k not in VARLEN]
 
@@ -119,7 +119,7 @@ def test_varlen_parity(name, n, frame, varlen_engine):
 
 
 @pytest.mark.parametrize("shift", [4, 8, 12])
-@pytest.mark.parametrize("name", ["mixed40_nulls", "flat_mix", "nested_nulls"])
+@pytest.mark.parametrize("name", ["mixed40_nulls", "flat_mix", "nested_nulls", "deep_nested", "maps"])
 def test_varlen_unaligned_buffers(name, shift, varlen_engine):
     """Rows written to / read from buffers at a 4-byte (not 16-byte) aligned address."""
     schema, make = catalog()[name]
