@@ -9,6 +9,8 @@ for Python classes whose annotations name Java field types:
   nullable other:         String (utf8), LocalDate (date32), Timestamp / Instant
                           (timestamp), Binary (binary)
   List[X] / X[]           list (nullable) with element field "item"
+  Dict[K, V] / Map<K,V>   map (nullable): key field "key" forced not-null, value "value"
+                          (TypeInference.java:228-237, DataTypes.mapField :404-424)
   any annotated class     nested bean -> nullable struct
 
 Field order = names sorted with String.compareTo (Descriptor.java:415-423);
@@ -86,6 +88,11 @@ def _infer_field(name: str, tp, walked: List[type]) -> Field:
         (elem,) = typing.get_args(tp)
         item = _infer_field("item", elem, walked)
         return DataTypes.array_field(name, item)
+    if origin in (dict, Dict):
+        kt, vt = typing.get_args(tp)
+        key = _infer_field("key", kt, walked)
+        key = Field(key.name, key.type, False, key.children)  # Map's keys must be non-nullable
+        return DataTypes.map_field(name, key, _infer_field("value", vt, walked))
     if isinstance(tp, type) and issubclass(tp, _JavaType):
         return Field(name, DataType(tp.type_id), tp.nullable)
     if isinstance(tp, type) and getattr(tp, "__annotations__", None):

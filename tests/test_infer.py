@@ -82,3 +82,29 @@ def test_encoders_bean_wraps_errors():
 
     with pytest.raises(EncoderException):
         Encoders.bean(Bad)
+
+
+def test_infer_map_field(golden):
+    """Dict[K, V] infers a map with a not-null key (TypeInference.java:228-237) and hashes
+    like the reference's map schema."""
+    import typing
+
+    from fury_amd.format import infer
+    from fury_amd.format.native import NativePlan
+    from fury_amd.format.types import ArrowType
+
+    class S:
+        flags: typing.Dict[infer.Long, infer.Boolean]
+        w: infer.jshort
+
+    class Maps:
+        a: infer.jint
+        counts: typing.Dict[infer.Integer, infer.Long]
+        s: S
+        scores: typing.Dict[infer.Short, infer.jdouble]
+
+    schema = infer.infer_schema(Maps)
+    m = schema.fields[1]
+    assert m.type.id == ArrowType.MAP and m.nullable
+    assert [c.name for c in m.children] == ["key", "value"] and not m.children[0].nullable
+    assert NativePlan(schema).schema_hash == golden["schema_hash"]["maps"]
