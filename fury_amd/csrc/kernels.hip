@@ -896,6 +896,104 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
   dec_group<1, TR, FRAME, NT>(fields, L.group[3], L.group[4], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
 }
 
+// Decode v3: the mirror of encode v3/v5 — each lane assembles one 16-byte chunk
+// of ONE field's column segment (16/w consecutive records of the tile) from the
+// LDS row image and stores it with one 16-B store: 39 store instructions per
+// 64-record Struct104 tile instead of 104 per-lane 4/8-byte ones. One full
+// 64-record tile per workgroup (tail: decode_fixed_kernel), not-null schemas
+// only (nullable fields need per-record validity bits: decode_fixed_kernel).
+// Null bits are still honoured (RowEncoderBuilder.java:239-246 reads isNullAt
+// for every field): a set bit decodes to 0. Descriptors are loaded per lane
+// before the tile's LDS-DMA wait, so their latency hides under it.
+template <bool FRAME, int K, int NT>
+__global__ __launch_bounds__(kWG) void decode_fixed_v3_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
+                                                              const uint8_t* __restrict__ in, int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int HDR = FRAME ? 12 : 0;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t r0 = (L.tile0 + (int64_t)blockIdx.x) * 64;
+  const int stride = L.stride;
+  const int hdr_bm = HDR + L.bitmap_bytes;
+  uint8_t* optr[K];
+  int wk[K], rb[K], slot[K], flg[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    int w = 0, p0 = 0, pend = 0;
+    const bool ok = v3_insn<64>(wave + k * kWaves, L, &w, &p0, &pend);
+    const int cpf = ok ? 4 * w : 32;
+    const int p = p0 + lane / cpf, c = lane % cpf;
+    wk[k] = 0;
+    optr[k] = nullptr;
+    rb[k] = slot[k] = flg[k] = 0;
+    if (ok && p < pend) {
+      const FixedFieldDev& fd = fields[p];
+      wk[k] = w;
+      optr[k] = fd.out_values + (r0 * w + c * 16);
+      rb[k] = c * (16 / w);
+      slot[k] = fd.slot;
+      flg[k] = fd.flags;
+    }
+  }
+  dma_tile<NT>(lds, in + r0 * stride, 64 * stride, tid, wave);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (FRAME && wave == 0) check_frame<FRAME>(lds + lane * stride, L, status);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int w = wk[k];
+    if (!w) continue;
+    const uint8_t* row = lds + rb[k] * stride;
+    const int s = slot[k];
+    const int bmo = HDR + ((s >> 5) << 2), bit = s & 31;
+    const uint8_t* sp = row + hdr_bm + 8 * s;
+    u32x4 y;
+    if (w == 8) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const bool nul = (ld32(row + e * stride + bmo) >> bit) & 1;
+        y[2 * e] = nul ? 0u : ld32(sp + e * stride);
+        y[2 * e + 1] = nul ? 0u : ld32(sp + e * stride + 4);
+      }
+    } else if (w == 4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool nul = (ld32(row + e * stride + bmo) >> bit) & 1;
+        y[e] = nul ? 0u : ld32(sp + e * stride);
+      }
+    } else if (w == 2) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = 2 * q + h;
+          const bool nul = (ld32(row + e * stride + bmo) >> bit) & 1;
+          v |= (nul ? 0u : (ld32(sp + e * stride) & 0xffffu)) << (16 * h);
+        }
+        y[q] = v;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int e = 4 * q + h;
+          const bool nul = (ld32(row + e * stride + bmo) >> bit) & 1;
+          uint32_t b = nul ? 0u : (ld32(sp + e * stride) & 0xffu);
+          if (flg[k] & 2) b = b ? 1u : 0u;  // MemoryBuffer.getBoolean
+          v |= b << (8 * h);
+        }
+        y[q] = v;
+      }
+    }
+    if constexpr (NT & 8) __builtin_nontemporal_store(y, gp(reinterpret_cast<u32x4*>(optr[k])));
+    else *gp(reinterpret_cast<u32x4*>(optr[k])) = y;
+  }
+}
+
 // Decode v2: one tile of TR records (TR a multiple of 64) per workgroup of WG
 // threads; lane = record within a 64-record half; wave instruction i covers
 // field i / (TR/64), records (i % (TR/64)) * 64 + lane. Same LDS-DMA image and
@@ -3089,7 +3187,33 @@ hipError_t launch_decode_v2(const FixedLaunch& L, const uint8_t* in, int32_t* st
   return hipGetLastError();
 }
 
-int dec_variant() {  // FORY_ROWFMT_DEC: 0 decode_fixed_kernel (default), 1..3 decode v2 shapes, 4 TR=32
+template <bool FRAME>
+hipError_t launch_decode_v3(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s, bool* done) {
+  constexpr int K = 12;
+  *done = false;
+  if (L.any_nullable || v3_insn_count<64>(L.group) > K * kWaves) return hipSuccess;
+  const int64_t full = L.num_rows / 64;
+  const size_t lds = (size_t)64 * L.stride;
+  if (full > 0) {
+    auto* k = (nt_mode() & 12) == 12 ? &decode_fixed_v3_kernel<FRAME, K, 12> : &decode_fixed_v3_kernel<FRAME, K, 0>;
+    static bool init[2] = {false, false};
+    const int ix = (nt_mode() & 12) == 12;
+    if (!init[ix]) { raise_lds_cap(k); init[ix] = true; }
+    hipLaunchKernelGGL(k, dim3((unsigned)full), dim3(kWG), lds, s, L, L.fields, in, status);
+  }
+  if (L.num_rows > full * 64) {  // tail tile
+    FixedLaunch T = L;
+    T.tile0 = full;
+    auto* k = &decode_fixed_kernel<64, FRAME>;
+    static bool init2 = false;
+    if (!init2) { raise_lds_cap(k); init2 = true; }
+    hipLaunchKernelGGL(k, dim3(1), dim3(kWG), lds, s, T, L.fields, in, status);
+  }
+  *done = true;
+  return hipGetLastError();
+}
+
+int dec_variant() {  // FORY_ROWFMT_DEC: 0 decode_fixed_kernel (default), 1..3 decode v2 shapes, 4 TR=32, 5 decode v3
   const char* e = getenv("FORY_ROWFMT_DEC");
   return e ? atoi(e) : 0;
 }
@@ -3100,6 +3224,11 @@ hipError_t launch_decode_tr(const FixedLaunch& L, const uint8_t* in, int32_t* st
   const size_t lds = (size_t)TR * L.stride;
   if constexpr (TR == 64) {
     const int dv = dec_variant();
+    if (dv == 5) {
+      bool done = false;
+      hipError_t e = launch_decode_v3<FRAME>(L, in, status, s, &done);
+      if (done || e != hipSuccess) return e;
+    }
     if (dv == 1 && 64 * L.stride <= 80 * 1024) return launch_decode_v2<64, 512, FRAME>(L, in, status, s);
     if (dv == 2 && 128 * L.stride <= 160 * 1024) return launch_decode_v2<128, 512, FRAME>(L, in, status, s);
     if (dv == 3 && 128 * L.stride <= 160 * 1024) return launch_decode_v2<128, 1024, FRAME>(L, in, status, s);

@@ -36,10 +36,10 @@ def encoder_for(name):
     return _ENC[name]
 
 
-@pytest.fixture(params=["8", "8p", "6", "7", "5", "9", "10", "11", "4", "3", "2", "1", "0", "d1", "d2", "d3", "d4"],
+@pytest.fixture(params=["8", "8p", "6", "7", "5", "9", "10", "11", "4", "3", "2", "1", "0", "d1", "d2", "d3", "d4", "d5"],
                 ids=["v5r64w512", "v5r64w512pad", "v5r128", "v5r128w1024", "v5r64", "once_r64w512", "once_r64w256",
                      "once_r128w512", "v4", "v3r128", "v3r64", "pipe", "tile", "dec_v2r64w512", "dec_v2r128",
-                     "dec_v2r128w1024", "dec_tr32"])
+                     "dec_v2r128w1024", "dec_tr32", "dec_v3"])
 def kernel_variant(request, monkeypatch):
     """Fixed-width kernel variants. FORY_ROWFMT_PIPE: 8 (default) / 6 / 7 / 5 encode v5
     (depth-2 pipeline; R64-WG512 / R128-WG512 / R128-WG1024 / R64-WG256), 9 / 10 / 11
