@@ -1965,41 +1965,13 @@ __global__ __launch_bounds__(64) void var_decode_tile_kernel(VarLaunch L, const 
     return;
   }
   const uint8_t* g = in + B0 - mis;  // 16-byte aligned
-  const int tot = (int)total;
-  const int nch = (tot + 15) >> 4;
-  int c = lane;
-  for (; c + 192 < nch; c += 256) {  // 4 chunks in flight per lane
-    u32x4 x[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int lo = (c + 64 * u) * 16;
-      if (lo >= mis && lo + 16 <= tot) {
-        x[u] = *gp(reinterpret_cast<const u32x4*>(g + lo));
-      } else {
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const int o = lo + 4 * d;
-          x[u][d] = (o >= mis && o + 4 <= tot) ? *gp(reinterpret_cast<const uint32_t*>(g + o)) : 0u;
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) *reinterpret_cast<u32x4*>(lds + (c + 64 * u) * 16) = x[u];
+  const int nch = (int)((total + 15) >> 4);
+  for (int c0 = 0; c0 < nch; c0 += 64) {  // LDS-DMA, 1 KiB per instruction, all in flight
+    if (c0 + lane < nch)
+      __builtin_amdgcn_global_load_lds((const GAS void*)(g + (int64_t)(c0 + lane) * 16),
+                                       (__attribute__((address_space(3))) void*)(lds + c0 * 16), 16, 0, 2);
   }
-  for (; c < nch; c += 64) {
-    const int lo = c * 16;
-    u32x4 x;
-    if (lo >= mis && lo + 16 <= tot) {
-      x = *gp(reinterpret_cast<const u32x4*>(g + lo));
-    } else {
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int o = lo + 4 * d;
-        x[d] = (o >= mis && o + 4 <= tot) ? *gp(reinterpret_cast<const uint32_t*>(g + o)) : 0u;
-      }
-    }
-    *reinterpret_cast<u32x4*>(lds + lo) = x;
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   dec_record<WRITE>(L, prog, cols, r0 + lane, live, lds + mis + (beg - B0), end - beg, status);
   };
@@ -2089,12 +2061,20 @@ __device__ __forceinline__ void write_validity64(uint8_t* validity, int64_t r0, 
 // kFixBatch loads per wave issued together (branch-free: clamped field index,
 // row 0 for idle lanes, nulls selected to 0 afterwards).
 // Fields of nested structs go to their child row (sbase, -1 = absent: skipped).
+// Batch j (numbered across the width groups from j0) belongs to wave
+// fix_owner(j): waves 1..NW-1 first, since wave 0 lays the rows out meanwhile.
+__device__ __forceinline__ int fix_owner(int j, int nbatch, int nw) {
+  return nbatch <= 2 * (nw - 1) ? 1 + j % (nw - 1) : j % nw;
+}
+
 template <int W, int NW>
 __device__ __forceinline__ void flat_enc_fixed(const VarLaunch& L, const FixedFieldDev* __restrict__ fix, int g0, int g1,
-                                               int wave, int lane, bool live, int64_t i, uint8_t* row,
-                                               const StructDev* __restrict__ st, const int32_t* sbase) {
+                                               int j0, int nbatch, int wave, int lane, bool live, int64_t i,
+                                               uint8_t* row, const StructDev* __restrict__ st,
+                                               const int32_t* sbase) {
   const int64_t ii = live ? i : 0;
-  for (int k0 = g0 + wave * kFixBatch; k0 < g1; k0 += NW * kFixBatch) {
+  for (int k0 = g0, j = j0; k0 < g1; k0 += kFixBatch, ++j) {
+    if (fix_owner(j, nbatch, NW) != wave) continue;
     uint64_t v[kFixBatch];
     uint32_t vb[kFixBatch];
 #pragma unroll
@@ -2497,10 +2477,15 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   FLAT_STAMP(2);
   if (L.num_struct) __syncthreads();  // nested fixed slots need the child-row offsets
   // fixed slots (all waves): BinaryRowWriter.write(ordinal, v), null -> 0
-  flat_enc_fixed<8, NW>(L, fix, L.fix_group[0], L.fix_group[1], wave, lane, live, i, row, st, sbase);
-  flat_enc_fixed<4, NW>(L, fix, L.fix_group[1], L.fix_group[2], wave, lane, live, i, row, st, sbase);
-  flat_enc_fixed<2, NW>(L, fix, L.fix_group[2], L.fix_group[3], wave, lane, live, i, row, st, sbase);
-  flat_enc_fixed<1, NW>(L, fix, L.fix_group[3], L.fix_group[4], wave, lane, live, i, row, st, sbase);
+  {
+    int jb[5];
+    jb[0] = 0;
+    for (int g = 0; g < 4; ++g) jb[g + 1] = jb[g] + (L.fix_group[g + 1] - L.fix_group[g] + kFixBatch - 1) / kFixBatch;
+    flat_enc_fixed<8, NW>(L, fix, L.fix_group[0], L.fix_group[1], jb[0], jb[4], wave, lane, live, i, row, st, sbase);
+    flat_enc_fixed<4, NW>(L, fix, L.fix_group[1], L.fix_group[2], jb[1], jb[4], wave, lane, live, i, row, st, sbase);
+    flat_enc_fixed<2, NW>(L, fix, L.fix_group[2], L.fix_group[3], jb[2], jb[4], wave, lane, live, i, row, st, sbase);
+    flat_enc_fixed<1, NW>(L, fix, L.fix_group[3], L.fix_group[4], jb[3], jb[4], wave, lane, live, i, row, st, sbase);
+  }
   if (PROF) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   FLAT_STAMP(3);
   __syncthreads();
@@ -2702,7 +2687,14 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   int32_t* sbase = reinterpret_cast<int32_t*>(lds + cap + (WRITE ? NW * stg_bytes : 0));  // [1 + num_struct][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // debug timeline (FORY_ROWFMT_VARPROF=1, values pass only): thread 0 stamps
+  // s_memrealtime at phase boundaries (uniform branch when off)
+#define DEC_STAMP(k)                                                                             \
+  do {                                                                                          \
+    if (WRITE && L.prof && tid == 0) L.prof[tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime();  \
+  } while (0)
   auto body = [&](int64_t tile) {
+  DEC_STAMP(0);
   const int64_t r0 = tile * 64;
   int64_t B0, B1, beg, end;
   bool live;
@@ -2747,26 +2739,26 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
     }
     return;
   }
-  {  // stage the tile's rows (coalesced 16-B loads; edge chunks by dword)
+  // tile-start Arrow offsets of every var field (written by decode_sizes): loaded
+  // now so their latency hides under the staging loads (lane v holds field v's)
+  int64_t obase = 0;
+  if (WRITE && lane < L.num_var) obase = vf[lane].out_offsets[r0];
+  {  // stage the tile's rows: LDS-DMA of whole 16-B chunks (1 KiB per wave
+     // instruction, all in flight at once, nt policy for the once-read rows); the
+     // edge chunks' bytes outside the tile (same 16-B blocks) are never read
     const uint8_t* g = in + B0 - mis;
-    const int tot = (int)total;
-    const int nch = (tot + 15) >> 4;
-    for (int cc = tid; cc < nch; cc += 64 * NW) {
-      const int lo = cc * 16;
-      u32x4 x;
-      if (lo >= mis && lo + 16 <= tot) {
-        x = *gp(reinterpret_cast<const u32x4*>(g + lo));
-      } else {
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const int o = lo + 4 * d;
-          x[d] = (o >= mis && o + 4 <= tot) ? *gp(reinterpret_cast<const uint32_t*>(g + o)) : 0u;
-        }
-      }
-      *reinterpret_cast<u32x4*>(img + lo) = x;
+    const int nch = (int)((total + 15) >> 4);
+    for (int c0 = 0; c0 < nch; c0 += 64 * NW) {
+      const int cc = c0 + tid;
+      if (cc < nch)
+        __builtin_amdgcn_global_load_lds((const GAS void*)(g + (int64_t)cc * 16),
+                                         (__attribute__((address_space(3))) void*)(img + (c0 + wave * 64) * 16), 16,
+                                         0, 2);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  DEC_STAMP(1);
   const int64_t i = r0 + lane;
   const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
   const uint8_t* fp = img + mis + (int)(beg - B0);
@@ -2799,11 +2791,14 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
     }
     return;
   }
+  DEC_STAMP(2);
   // fixed fields: slot -> column (UnsafeTrait.getInt32/... ; null -> 0), validity by ballot
   flat_dec_fixed<8, NW>(L, fix, L.fix_group[0], L.fix_group[1], wave, lane, live, bad, i, r0, rows, row, st, sbase);
   flat_dec_fixed<4, NW>(L, fix, L.fix_group[1], L.fix_group[2], wave, lane, live, bad, i, r0, rows, row, st, sbase);
   flat_dec_fixed<2, NW>(L, fix, L.fix_group[2], L.fix_group[3], wave, lane, live, bad, i, r0, rows, row, st, sbase);
   flat_dec_fixed<1, NW>(L, fix, L.fix_group[3], L.fix_group[4], wave, lane, live, bad, i, r0, rows, row, st, sbase);
+  if (WRITE && L.prof) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  DEC_STAMP(3);
   // var fields: one per wave at a time, output span staged in LDS
   uint8_t* stg = lds + cap + wave * stg_bytes;
   for (int v = wave; v < L.num_var; v += NW) {
@@ -2819,7 +2814,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
       if (lane == 0) write_validity64(f.out_validity, r0, rows, m);
     }
     // Arrow offsets of this tile: base (tile prefix written by decode_sizes) + in-wave prefix
-    const int64_t O0 = f.out_offsets[r0];
+    const int64_t O0 = __shfl(obase, v);
     const int64_t incl = wave_incl_scan64(n, lane);
     const int64_t O1 = O0 + __shfl(incl, 63);
     const int64_t e0 = O0 + incl - n;
@@ -2921,6 +2916,14 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
       }
     }
   }
+  if (WRITE && L.prof) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    DEC_STAMP(4);
+    __syncthreads();
+    DEC_STAMP(5);
+    DEC_STAMP(6);
+    DEC_STAMP(7);
+  }
   };
   if (!SPILL) {
     body(blockIdx.x);
@@ -2931,6 +2934,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
     body(sp.list[k]);
     __syncthreads();
   }
+#undef DEC_STAMP
 }
 
 

@@ -1,4 +1,5 @@
-"""Phase timeline of the flat varlen encode kernel (debug, FORY_ROWFMT_VARPROF=1):
+"""Phase timeline of the flat varlen encode kernel and of the decode values pass
+(debug, FORY_ROWFMT_VARPROF=1):
 per-tile durations of each phase (s_memrealtime, 100 MHz), tile lifetime and the
 average number of tiles resident. Usage: python scripts/var_timeline.py [config] [rows]"""
 import ctypes
@@ -53,4 +54,33 @@ for frame in (0, 1):
         r[nm] = {"median_us": round(float(np.median(d[:, k])), 2), "p90_us": round(float(np.percentile(d[:, k], 90)), 2),
                  "mean_us": round(float(d[:, k].mean()), 2)}
     res[f"{config}_frame{frame}"] = r
+
+def summarize(t, names):
+    t = t[t[:, 7] > 0]
+    d = np.diff(t, axis=1) * 10 / 1000.0  # us
+    life = (t[:, 7] - t[:, 0]) * 10 / 1000.0
+    span = (t[:, 7].max() - t[:, 0].min()) * 10 / 1000.0
+    r = {"tiles_stamped": int(len(t)), "kernel_span_us": round(float(span), 1),
+         "tile_life_us_median": round(float(np.median(life)), 2),
+         "avg_resident_tiles": round(float(life.sum() / span), 1)}
+    for k, nm in enumerate(names):
+        if nm:
+            r[nm] = {"median_us": round(float(np.median(d[:, k])), 2), "mean_us": round(float(d[:, k].mean()), 2)}
+    return r
+
+
+dnames = ["stage rows", "frame/struct bases", "fixed fields", "var fields", "barrier", None, None]
+for frame in (0, 1):
+    offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    native.encoded_size(plan, arr, n, frame, offs, ws)
+    total = int(offs[n].item())
+    out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    native.encode(plan, arr, n, frame, offs, out, status, ws)
+    for _ in range(3):
+        enc.decode(out[:total], n, frame, offs)
+    torch.cuda.synchronize()
+    tiles = (n + 63) // 64
+    buf = np.zeros(tiles * 8, dtype=np.uint64)
+    got = lib.fory_rowfmt_debug_timeline(buf.ctypes.data, buf.size)
+    res[f"{config}_decode_frame{frame}"] = summarize(buf[:got].reshape(-1, 8).astype(np.int64), dnames)
 print(json.dumps(res, indent=1))
