@@ -2404,6 +2404,20 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
     pf_hi = flat_group(f, pf_e0, pf_e1, 0, rows, lane, stg_bytes, &pf_fits);
     if (pf_fits) flat_stage_span(f, __shfl(pf_e0, 0), __shfl(pf_e1, pf_hi - 1), lane, stg, &pf_phase, &pf_vofs);
   }
+  // item ranges of this wave's later var fields, loaded before the layout barrier
+  constexpr int kPre = 3;
+  int64_t pe0[kPre], pe1[kPre];
+#pragma unroll
+  for (int k = 0; k < kPre; ++k) {
+    const int v = v_first + (k + 1) * nplc;
+    pe0[k] = pe1[k] = 0;
+    if (v < L.num_var) {
+      const VarFieldDev& f = vf[v];
+      const int64_t ee = f.offsets[r0 + rows];
+      pe0[k] = live ? f.offsets[i] : ee;
+      pe1[k] = live ? f.offsets[i + 1] : ee;
+    }
+  }
   FLAT_STAMP(1);
   if (wave == 0) {
     // Encoders.encode frame header; BinaryRowWriter.reset zeroes the bitmap (BinaryRowWriter.java:76-84)
@@ -2491,10 +2505,14 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   __syncthreads();
   FLAT_STAMP(4);
   // variable payloads: one field per wave at a time, record group by record group
-  for (int v = v_first; v < L.num_var; v += nplc) {
+  for (int v = v_first, kv = 0; v < L.num_var; v += nplc, ++kv) {
     const VarFieldDev& f = vf[v];
     int64_t e0 = pf_e0, e1 = pf_e1;
-    if (v != v_first || wave == 0) {
+    if (kv >= 1 && kv <= kPre) {
+#pragma unroll
+      for (int k = 0; k < kPre; ++k)
+        if (kv == k + 1) e0 = pe0[k], e1 = pe1[k];
+    } else if (kv > kPre || wave == 0) {
       const int64_t ee = f.offsets[r0 + rows];
       e0 = live ? f.offsets[i] : ee;
       e1 = live ? f.offsets[i + 1] : ee;
