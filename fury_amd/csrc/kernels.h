@@ -59,6 +59,7 @@ struct VarLaunch {
   int32_t num_var;              // OP_BYTES / OP_LIST ops at any struct level, program order
   int32_t stg_bytes;            // LDS staging per wave (slot) for one record group's span
   int32_t nested_fixed;         // fixed bytes of child rows + list headers per record (staging estimate)
+  int32_t var_est_row;          // widest var field's static payload estimate per record (decode staging)
   int32_t fix_group[5];         // width groups [8][4][2][1] of `fix`
   const FixedFieldDev* fix;     // device: fixed fields (any struct level), width-sorted
   const VarFieldDev* vf;        // device: var fields (any struct level), program order

@@ -2702,7 +2702,8 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   constexpr int HDR = FRAME ? 12 : 0;
   const int stg_bytes = L.stg_bytes;
   uint8_t* img = lds;
-  int32_t* sbase = reinterpret_cast<int32_t*>(lds + cap + (WRITE ? NW * stg_bytes : 0));  // [1 + num_struct][64]
+  const int nslot = L.num_var < NW ? L.num_var : NW;  // staging slots: waves with var fields (v = wave + k NW)
+  int32_t* sbase = reinterpret_cast<int32_t*>(lds + cap + (WRITE ? nslot * stg_bytes : 0));  // [1 + num_struct][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // debug timeline (FORY_ROWFMT_VARPROF=1, values pass only): thread 0 stamps
@@ -3493,6 +3494,43 @@ unsigned spill_grid(K* k, const VarLaunch& L, size_t lds, int wg) {
   return (unsigned)persistent_grid(k, lds, (L.num_rows + 63) / 64, wg);
 }
 
+// Decode values pass: staging only for the waves that own var fields.
+size_t flat_lds_dec(const VarLaunch& L, int cap, int nw) {
+  const int nslot = L.num_var < nw ? L.num_var : nw;
+  return (size_t)cap + (size_t)nslot * L.stg_bytes + sbase_lds(L);
+}
+
+// Decode staging per slot: the output span of a 64-record tile of the widest
+// var field at the plan's static estimate (var_est_row: ~32 B per string,
+// 16 items per list, +25 %), in [2, 16] KiB, under the same occupancy guard as
+// the encode slots (FORY_ROWFMT_VARSTG overrides). Spans that still do not fit
+// take the per-lane path.
+template <typename K>
+int dec_stg_bytes(K* k, const VarLaunch& L, int cap, int nw) {
+  if (getenv("FORY_ROWFMT_VARSTG") || L.num_var == 0) return L.stg_bytes;
+  int b = (int)(((int64_t)64 * L.var_est_row * 5 / 4 + 512 + 255) & ~int64_t(255));
+  b = b < 2048 ? 2048 : (b > 16384 ? 16384 : b);
+  auto occ = [&](int stg) {
+    VarLaunch T = L;
+    T.stg_bytes = stg;
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(k), 64 * nw,
+                                                     flat_lds_dec(T, cap, nw)) != hipSuccess)
+      return -1;
+    return blocks;
+  };
+  static int m_cap = -1, m_b = -1, m_nv = -1, m_ns = -1, m_res = 2048;
+  if (m_cap == cap && m_b == b && m_nv == L.num_var && m_ns == L.num_struct) return m_res;
+  const int want = occ(2048);
+  int r = 2048;
+  if (want > 0) {
+    r = b;
+    while (r > 2048 && occ(r) < want) r -= 256;
+  }
+  m_cap = cap, m_b = b, m_nv = L.num_var, m_ns = L.num_struct, m_res = r;
+  return r;
+}
+
 template <bool FRAME, int NW, bool PROF>
 void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                        int cap, hipStream_t s) {
@@ -3519,18 +3557,20 @@ void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int6
 }
 
 template <bool FRAME, bool WRITE, int NW>
-void launch_flat_dec(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int64_t* tile_tot,
+void launch_flat_dec(const VarLaunch& L0, const uint8_t* rows, const int64_t* offs, int64_t* tile_tot,
                      int32_t* status, int cap, hipStream_t s) {
-  const SpillArgs sp = spill_args(L, cap);
-  (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
+  const SpillArgs sp = spill_args(L0, cap);
+  (void)hipMemsetAsync(L0.spill_count, 0, sizeof(int32_t), s);
   auto* k = &var_decode_flat_kernel<FRAME, WRITE, NW, false>;
-  var_tile_launch(k, L, cap);
-  const size_t lds = WRITE ? flat_lds(L, cap, NW) : (size_t)cap + sbase_lds(L);  // pass 1: row image (+ struct offsets)
+  var_tile_launch(k, L0, cap);
+  VarLaunch L = L0;
+  if (WRITE) L.stg_bytes = dec_stg_bytes(k, L0, cap, NW);
+  const size_t lds = WRITE ? flat_lds_dec(L, cap, NW) : (size_t)cap + sbase_lds(L);  // pass 1: row image (+ struct offsets)
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
                      L.vf, L.st, rows, offs, tile_tot, status, cap, sp);
   auto* k2 = &var_decode_flat_kernel<FRAME, WRITE, NW, true>;
   var_tile_launch(k2, L, sp.cap);
-  const size_t lds2 = WRITE ? flat_lds(L, sp.cap, NW) : (size_t)sp.cap + sbase_lds(L);
+  const size_t lds2 = WRITE ? flat_lds_dec(L, sp.cap, NW) : (size_t)sp.cap + sbase_lds(L);
   hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, lds2, 64 * NW)), dim3(64 * NW), lds2, s, L, L.prog, L.cols, L.fix,
                      L.vf, L.st, rows, offs, tile_tot, status, sp.cap, sp);
 }
