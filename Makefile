@@ -7,7 +7,15 @@ ORACLE := oracle/_build/liboracle.so
 SRCS := fury_amd/csrc/kernels.hip fury_amd/csrc/capi.cpp fury_amd/csrc/plan.cpp fury_amd/csrc/host.cpp
 HDRS := fury_amd/csrc/kernels.h fury_amd/csrc/plan.h include/fory_rowfmt.h
 
-all: $(LIB) $(ORACLE)
+CAPI_TEST := tests/c/capi_roundtrip
+
+all: $(LIB) $(ORACLE) $(CAPI_TEST)
+
+# C driver of the C-ABI (GPU test tests/test_gpu_capi_c.py): plain C + HIP runtime C API
+$(CAPI_TEST): tests/c/capi_roundtrip.c include/fory_rowfmt.h $(LIB) $(ORACLE)
+	gcc -O2 -std=c11 -Wall -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude $< -o $@ \
+	  -Lfury_amd/lib -lfory_rowfmt -Loracle/_build -loracle -L/opt/rocm/lib -lamdhip64 \
+	  -Wl,-rpath,'$$ORIGIN/../../fury_amd/lib:$$ORIGIN/../../oracle/_build:/opt/rocm/lib'
 
 fury_amd/lib/%.o: fury_amd/csrc/%.hip $(HDRS)
 	@mkdir -p fury_amd/lib
@@ -25,6 +33,6 @@ $(ORACLE): oracle/rowfmt_oracle.c include/fory_rowfmt.h
 	gcc -O2 -std=c11 -Wall -Wextra -fPIC -shared -o $@ $<
 
 clean:
-	rm -rf fury_amd/lib oracle/_build
+	rm -rf fury_amd/lib oracle/_build $(CAPI_TEST)
 
 .PHONY: all clean

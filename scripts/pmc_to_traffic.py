@@ -14,8 +14,11 @@ except (OSError, ValueError):
     cur = {}
 ent = {}
 for name, e in summ["pmc"].items():
+    if "<spill>" in name:
+        continue
     role = "encode" if name.startswith("encode") or name.startswith("var_encode") else \
-        "decode" if name.startswith("decode") or name.startswith("var_decode_kernelILb1") else None
+        "decode" if name.startswith("decode") or name.startswith("var_decode_kernelILb1") or \
+        name == "var_decode_flat_kernel<pass2>" else None
     if role and "fetch_bytes_x2" in e and "write_bytes" in e:
         ent[role] = int(e["fetch_bytes_x2"] + e["write_bytes"])
         ent[role + "_kernel"] = name

@@ -25,6 +25,12 @@ def short(name):
                   r"var_sizes_kernel|scan_\w+?_kernel|fill_offsets_kernel)", name)
     if m:
         k = m.group(1)
+        t = re.search(r"var_(?:en|de)code_flat_kernel<([^>]*)>", name)
+        if t and t.group(1).split(",")[-1].strip() == "true":
+            k += "<spill>"  # the small big-image launch: kept apart from the main launch's averages
+            if k.startswith("var_decode_flat_kernel"):
+                k = "var_decode_flat_kernel<spill>"
+            return k
         if k.startswith("var_decode") and not k.endswith(("0", "1")):
             if k == "var_decode_flat_kernel":
                 k += "<pass2>" if re.search(r"<(true|false), true", name) or "ILb1ELb1E" in name or "ILb0ELb1E" in name \
