@@ -311,8 +311,8 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   rc = upload(ws, host.data(), (int64_t)host.size(), s);
   if (rc) return rc;
   uint8_t* wsb = static_cast<uint8_t*>(ws);
-  bool has_map = false;
-  for (const fory_amd::Op& op : p.program) has_map |= op.code == fory_amd::OP_MAP;
+  bool has_map = false;  // (and lists of structs)
+  for (const fory_amd::Op& op : p.program) has_map |= op.code == fory_amd::OP_MAP || op.code == fory_amd::OP_LIST_STRUCT;
   // maps run on the generic tile interpreter (enc_record / dec_record)
   L->flat = !has_map && var.size() <= 32 && st.size() <= (size_t)fory_amd::kMaxTileStructs ? 1 : 0;
   L->num_var = (int32_t)var.size();

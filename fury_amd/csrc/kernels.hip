@@ -1370,6 +1370,22 @@ __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* _
           size += 8 + bitmap_bytes(n) + round8(n * w);
         }
         break;
+      case OP_LIST_STRUCT: {  // [i64 n][bitmap][n slots][child row per non-null element]
+        if (!absent_depth && (!(op.d & 1) || col_valid(c, i))) {
+          const int64_t e0 = c.offsets[i], n = (int64_t)c.offsets[i + 1] - e0;
+          const int nf = op.e - pc - 1;
+          const int64_t ssize = bitmap_bytes(nf) + 8LL * nf;
+          int64_t m = n;
+          if (op.d & 4) {
+            const ColumnDev& sc = cols[op.c];
+            m = 0;
+            for (int64_t j = 0; j < n; ++j) m += col_valid(sc, e0 + j);
+          }
+          size += 8 + bitmap_bytes(n) + 8 * n + m * ssize;
+        }
+        pc = op.e - 1;
+        break;
+      }
       case OP_MAP:  // [i64 keyArrayBytes][key array][value array]
         if (!absent_depth && (!(op.d & 1) || col_valid(c, i))) {
           const int64_t n = (int64_t)c.offsets[i + 1] - c.offsets[i];
@@ -1411,6 +1427,7 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
     cnt = 1;
     if (op.code == OP_FIXED)
       while (cnt < kFixBatch && pc + cnt < L.num_ops && prog[pc + cnt].code == OP_FIXED) ++cnt;
+    if (op.code == OP_LIST_STRUCT) cnt = op.e - pc;  // the element fields are its sub-program
     if (absent) {
       if (op.code == OP_STRUCT_BEGIN) absent++;
       else if (op.code == OP_STRUCT_END) absent--;
@@ -1524,6 +1541,51 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
           for (int64_t k = dsz; k < fixed_part; ++k) data[k] = 0;
         }
         wi += ahdr + fixed_part;
+        gst64(slot, ((uint64_t)(astart - st_start[depth]) << 32) | (uint32_t)(wi - astart));
+        break;
+      }
+      case OP_LIST_STRUCT: {
+        if (isnull) {
+          set_null_bit(bitmap, op.a);
+          gst64(slot, 0);
+          break;
+        }
+        // BinaryArrayWriter.reset(n) with 8-byte element slots, then per element
+        // serializeForBean (BaseBinaryEncoderBuilder.java:436-490): child row at the
+        // writerIndex, element slot = (offset from the array start, child size);
+        // a null element only sets its bit (slot 0).
+        const ColumnDev& sc = cols[op.c];
+        const int nf = op.e - pc - 1;
+        const int32_t shdr = bitmap_bytes(nf);
+        const int64_t ssize = shdr + 8LL * nf;
+        const int64_t e0 = c.offsets[i], n = (int64_t)c.offsets[i + 1] - e0;
+        const int64_t astart = wi;
+        const int32_t ahdr = 8 + bitmap_bytes(n);
+        uint8_t* arr = row + astart;
+        gst64(arr, (uint64_t)n);
+        for (int b = 8; b < ahdr; b += 8) gst64(arr + b, 0);
+        wi += ahdr + 8 * n;
+        for (int64_t j = 0; j < n; ++j) {
+          const int64_t q = e0 + j;
+          if ((op.d & 4) && !col_valid(sc, q)) {
+            arr[8 + (j >> 3)] |= (uint8_t)(1u << (j & 7));
+            gst64(arr + ahdr + 8 * j, 0);
+            continue;
+          }
+          uint8_t* srow = row + wi;
+          for (int b = 0; b < shdr; b += 8) gst64(srow + b, 0);
+          for (int f = 0; f < nf; ++f) {  // BinaryRowWriter.write / setNullAt of each field
+            const Op o = prog[pc + 1 + f];
+            const ColumnDev& cc = cols[o.b];
+            uint64_t v = 0;
+            if ((o.d & 1) && !col_valid(cc, q)) set_null_bit(srow, f);
+            else v = load_elem(cc.values, o.c, q);
+            if (o.d & 2) v = v ? 1 : 0;
+            gst64(srow + shdr + 8 * f, v);
+          }
+          gst64(arr + ahdr + 8 * j, ((uint64_t)(wi - astart) << 32) | (uint32_t)ssize);
+          wi += ssize;
+        }
         gst64(slot, ((uint64_t)(astart - st_start[depth]) << 32) | (uint32_t)(wi - astart));
         break;
       }
@@ -1766,6 +1828,72 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
             }
           }
         }
+        break;
+      }
+      case OP_LIST_STRUCT: {  // getArray + per element getStruct (UnsafeTrait.java:160-186)
+        const int nf = op.e - pc - 1;
+        const int32_t shdr = bitmap_bytes(nf);
+        const int64_t ssize = shdr + 8LL * nf;
+        int64_t n = 0, at = 0;
+        if (!isnull) {
+          const uint64_t os = gld64(slot);
+          at = st_start[depth] + (int32_t)(os >> 32);
+          if ((int32_t)(os >> 32) < 0 || at + 8 > row_len) {
+            set_status(status, FORY_ERR_CORRUPT);
+          } else {
+            n = (int32_t)(int64_t)gld64(row + at);
+            if (n < 0 || at + 8 + bitmap_bytes(n) + 8 * n > row_len) {
+              set_status(status, FORY_ERR_CORRUPT);
+              n = 0;
+            }
+          }
+        }
+        if (live) {
+          if (!WRITE) {
+            c.out_offsets[i + 1] = (int32_t)n;
+          } else if (n > 0) {
+            const ColumnDev& sc = cols[op.c];
+            const uint8_t* arr = row + at;
+            const int32_t ahdr = 8 + bitmap_bytes(n);
+            const int64_t e0 = c.out_offsets[i];
+            for (int64_t j = 0; j < n; ++j) {
+              const int64_t q = e0 + j;
+              bool en = (arr[8 + (j >> 3)] >> (j & 7)) & 1;  // BinaryArray.isNullAt
+              const uint8_t* srow = nullptr;
+              if (!en) {
+                const uint64_t os2 = gld64(arr + ahdr + 8 * j);
+                const int64_t r2 = (int32_t)(os2 >> 32);
+                if (r2 < 0 || at + r2 + ssize > row_len) {
+                  set_status(status, FORY_ERR_CORRUPT);
+                  en = true;
+                } else {
+                  srow = arr + r2;
+                }
+              }
+              const uint32_t bit = 1u << (q & 31);
+              if ((op.d & 4) && sc.out_validity) {
+                uint32_t* word = reinterpret_cast<uint32_t*>(sc.out_validity) + (q >> 5);
+                if (en) atomicAnd(word, ~bit);
+                else atomicOr(word, bit);
+              }
+              for (int f = 0; f < nf; ++f) {
+                const Op o = prog[pc + 1 + f];
+                const ColumnDev& cc = cols[o.b];
+                const bool nul = en || ((srow[f >> 3] >> (f & 7)) & 1);
+                uint64_t v = 0;
+                if (!nul) v = gld64(srow + shdr + 8 * f);
+                if (o.d & 2) v = (v & 0xff) ? 1 : 0;
+                store_elem(cc.out_values, o.c, q, v);
+                if ((o.d & 1) && cc.out_validity) {
+                  uint32_t* word = reinterpret_cast<uint32_t*>(cc.out_validity) + (q >> 5);
+                  if (nul) atomicAnd(word, ~bit);
+                  else atomicOr(word, bit);
+                }
+              }
+            }
+          }
+        }
+        pc = op.e - 1;  // the element fields were this op's sub-program
         break;
       }
       case OP_MAP: {  // BinaryMap.pointTo (BinaryMap.java:62-77): keys + values arrays

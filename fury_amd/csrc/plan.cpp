@@ -144,6 +144,29 @@ static int compile_field(const Plan& p, int32_t idx, int32_t ordinal, std::vecto
     case KIND_LIST: {
       int32_t item = nd.children[0];
       const Node& it = p.nodes[item];
+      if (it.kind == KIND_STRUCT) {
+        // List<Bean> (serializeForArrayByWriter, BaseBinaryEncoderBuilder.java:293-351, with
+        // serializeForBean per element :436-490): element slots hold (offset, size) of
+        // child rows appended after the array's fixed part. Device path: bean fields
+        // of fixed width only.
+        for (int32_t ch : it.children) {
+          const Node& cn = p.nodes[ch];
+          if (cn.kind != KIND_FIXED && cn.kind != KIND_BOOL) {
+            *err = "device path supports list<struct of fixed-width fields> only (got field type id " +
+                   std::to_string(cn.type_id) + ")";
+            return FORY_ERR_UNSUPPORTED;
+          }
+        }
+        const size_t begin = prog->size();
+        prog->push_back({OP_LIST_STRUCT, ordinal, idx, item, flags | (it.nullable ? 4 : 0), 0});
+        for (size_t k = 0; k < it.children.size(); ++k) {
+          const Node& cn = p.nodes[it.children[k]];
+          const int32_t cf = (cn.nullable ? 1 : 0) | (cn.kind == KIND_BOOL ? 2 : 0);
+          prog->push_back({OP_FIXED, (int32_t)k, it.children[k], cn.width, cf, 0});
+        }
+        (*prog)[begin].e = (int32_t)prog->size();
+        return FORY_OK;
+      }
       if (it.kind != KIND_FIXED && it.kind != KIND_BOOL) {
         *err = "device path supports list<fixed-width> only (got element type id " +
                std::to_string(it.type_id) + ")";

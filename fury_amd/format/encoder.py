@@ -132,13 +132,16 @@ class RowEncoder:
         n = num_rows
         fields = p.fields
         cols = [DeviceColumn(length=n) for _ in fields]
-        item_of = {}  # element columns sized after decode_sizes: list items, map keys + values
+        # element columns sized after decode_sizes: list item subtrees (a list of structs:
+        # the struct and its fields), map keys + values
+        item_of = {}
+        sub = {}  # list/map column -> its element columns (pre-order)
         for i, f in enumerate(fields):
-            if f.type.id == ArrowType.LIST:
-                item_of[i + 1] = i
-            elif f.type.id == ArrowType.MAP:
-                item_of[i + 1] = i
-                item_of[i + 2] = i
+            if f.type.id in (ArrowType.LIST, ArrowType.MAP):
+                size = sum(_subtree_size(c) for c in f.children)
+                sub[i] = list(range(i + 1, i + 1 + size))
+                for k in sub[i]:
+                    item_of[k] = i
         for i, f in enumerate(fields):
             if i in item_of:
                 continue  # sized after decode_sizes
@@ -163,10 +166,12 @@ class RowEncoder:
             tot = int(totals.get(i, 0))
             f = fields[i]
             if f.type.id in (ArrowType.LIST, ArrowType.MAP):
-                for k in ((i + 1,) if f.type.id == ArrowType.LIST else (i + 1, i + 2)):
+                for k in sub[i]:
                     it = fields[k]
+                    vals = None if it.type.id == ArrowType.STRUCT else \
+                        torch.empty(max(1, tot), dtype=_torch_dtype(it.type.id), device=self.device)
                     cols[k] = DeviceColumn(
-                        torch.empty(max(1, tot), dtype=_torch_dtype(it.type.id), device=self.device), None,
+                        vals, None,
                         torch.zeros(_validity_bytes(tot), dtype=torch.uint8, device=self.device)
                         if it.nullable else None, tot)
             else:
@@ -177,6 +182,10 @@ class RowEncoder:
 
     def from_rows(self, rows: EncodedRows) -> List[DeviceColumn]:
         return self.decode(rows)
+
+
+def _subtree_size(f) -> int:
+    return 1 + sum(_subtree_size(c) for c in f.children)
 
 
 def _validity_bytes(n: int) -> int:

@@ -76,7 +76,7 @@ def main():
 
     from fury_amd.format.types import DataType, DataTypes, Field, Schema
     sys.path.insert(0, os.path.join(REPO, "tests"))
-    from helpers import deep_nested_schema, maps_schema
+    from helpers import deep_nested_schema, list_struct_schema, maps_schema
 
     edge = {
         "empty": Schema([]),
@@ -90,6 +90,7 @@ def main():
         "struct_boxed": W.struct_schema(100, boxed=True),
         "maps": maps_schema(),
         "deep_nested": deep_nested_schema(),
+        "list_struct": list_struct_schema(),
     }
     schemas = {"struct104": W.struct_schema(), "mixed40": W.mixed_schema(),
                "nested": W.nested_schema(), **edge}

@@ -244,6 +244,38 @@ def maps_schema() -> Schema:
     ])
 
 
+def list_struct_rows(n: int, seed: int):
+    """Rows of list_struct_schema: List<Bean> with null elements, null / empty lists,
+    more than 64 elements (element bitmap beyond one word), nullable bean fields."""
+    rng = np.random.default_rng(seed)
+    rows = []
+    for i in range(n):
+        items = None
+        if rng.random() >= 0.15:
+            k = int(rng.integers(0, 70)) if rng.random() < 0.1 else int(rng.integers(0, 6))
+            items = [None if rng.random() < 0.1 else {
+                "a": int(rng.integers(-2**31, 2**31)),
+                "b": None if rng.random() < 0.3 else int(rng.integers(-2**62, 2**62)),
+                "c": bool(rng.random() < 0.5),
+                "d": float(rng.standard_normal()),
+            } for _ in range(k)]
+        rows.append({"id": int(rng.integers(-2**62, 2**62)), "items": items,
+                     "tag": "".join(chr(int(x)) for x in rng.integers(97, 123, size=rng.integers(0, 10)))})
+    return rows
+
+
+def list_struct_schema() -> Schema:
+    bean = DataTypes.struct_field("item", True, [
+        Field("a", DataType(ArrowType.INT32), False),
+        Field("b", DataType(ArrowType.INT64), True),
+        Field("c", DataType(ArrowType.BOOL), False),
+        Field("d", DataType(ArrowType.FLOAT), False),
+    ])
+    return Schema([Field("id", DataType(ArrowType.INT64), False),
+                   Field("items", DataType(ArrowType.LIST), True, [bean]),
+                   Field("tag", DataType(ArrowType.STRING), True)])
+
+
 def catalog():
     """name -> (schema, host column factory(n, seed))."""
     return {
@@ -262,6 +294,8 @@ def catalog():
         "deep_nested": (deep_nested_schema(),
                         lambda n, s: build_columns(deep_nested_schema(), deep_nested_rows(n, s))),
         "maps": (maps_schema(), lambda n, s: build_columns(maps_schema(), maps_rows(n, s))),
+        "list_struct": (list_struct_schema(),
+                        lambda n, s: build_columns(list_struct_schema(), list_struct_rows(n, s))),
     }
 
 

@@ -119,7 +119,7 @@ def test_varlen_parity(name, n, frame, varlen_engine):
 
 
 @pytest.mark.parametrize("shift", [4, 8, 12])
-@pytest.mark.parametrize("name", ["mixed40_nulls", "flat_mix", "nested_nulls", "deep_nested", "maps"])
+@pytest.mark.parametrize("name", ["mixed40_nulls", "flat_mix", "nested_nulls", "deep_nested", "maps", "list_struct"])
 def test_varlen_unaligned_buffers(name, shift, varlen_engine):
     """Rows written to / read from buffers at a 4-byte (not 16-byte) aligned address."""
     schema, make = catalog()[name]

@@ -108,3 +108,29 @@ def test_infer_map_field(golden):
     assert m.type.id == ArrowType.MAP and m.nullable
     assert [c.name for c in m.children] == ["key", "value"] and not m.children[0].nullable
     assert NativePlan(schema).schema_hash == golden["schema_hash"]["maps"]
+
+
+def test_infer_list_of_beans(golden):
+    """List[Bean] infers a list whose item is a nullable struct (TypeInference.java:222-227,
+    DataTypes.arrayField); the device plan accepts beans of fixed-width fields."""
+    import typing
+
+    from fury_amd.format import infer
+    from fury_amd.format.native import NativePlan
+    from fury_amd.format.types import ArrowType
+
+    class Item:
+        a: infer.jint
+        b: infer.Long
+        c: infer.jboolean
+        d: infer.jfloat
+
+    class Holder:
+        id: infer.jlong
+        items: typing.List[Item]
+        tag: infer.String
+
+    schema = infer.infer_schema(Holder)
+    lst = schema.fields[1]
+    assert lst.type.id == ArrowType.LIST and lst.children[0].type.id == ArrowType.STRUCT
+    assert NativePlan(schema).schema_hash == golden["schema_hash"]["list_struct"]
