@@ -24,6 +24,7 @@ FORY_ERR_ENCODER = 7
 
 FRAME_RAW = 0
 FRAME_STREAM = 1
+FRAME_COLLECTION = 2
 
 
 class FieldDesc(ctypes.Structure):

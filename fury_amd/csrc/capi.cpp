@@ -71,8 +71,15 @@ int check_common(const fory_plan* plan, const fory_column* cols, int64_t n, int 
                  void* ws, int64_t ws_bytes) {
   if (!plan) return fail(FORY_ERR_INVALID_ARGUMENT, "plan is null");
   if (n < 0) return fail(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
-  if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM)
-    return fail(FORY_ERR_INVALID_ARGUMENT, "frame_mode must be 0 (raw) or 1 (stream)");
+  if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM && frame != FORY_FRAME_COLLECTION)
+    return fail(FORY_ERR_INVALID_ARGUMENT, "frame_mode must be 0 (raw), 1 (stream) or 2 (collection)");
+  if (frame == FORY_FRAME_COLLECTION) {
+    const Plan& p = plan->p;
+    const int k = p.top.size() == 1 ? p.nodes[p.top[0]].kind : -1;
+    if (k != fory_amd::KIND_LIST && k != fory_amd::KIND_MAP)
+      return fail(FORY_ERR_INVALID_ARGUMENT,
+                  "collection frames need a plan of exactly one list or map field (ArrayEncoder / MapEncoder)");
+  }
   if (n > 0 && !cols) return fail(FORY_ERR_INVALID_ARGUMENT, "cols is null");
   const int64_t need = fory_rowfmt_workspace_bytes(plan, n);
   if (n > 0 && (!ws || ws_bytes < need))
@@ -314,7 +321,10 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   bool has_map = false;  // (and lists of structs)
   for (const fory_amd::Op& op : p.program) has_map |= op.code == fory_amd::OP_MAP || op.code == fory_amd::OP_LIST_STRUCT;
   // maps run on the generic tile interpreter (enc_record / dec_record)
-  L->flat = !has_map && var.size() <= 32 && st.size() <= (size_t)fory_amd::kMaxTileStructs ? 1 : 0;
+  L->flat = !has_map && frame != FORY_FRAME_COLLECTION && var.size() <= 32 &&
+                    st.size() <= (size_t)fory_amd::kMaxTileStructs
+                ? 1
+                : 0;
   L->num_var = (int32_t)var.size();
   L->num_struct = (int32_t)st.size();
   L->vf = reinterpret_cast<const fory_amd::VarFieldDev*>(wsb + o_var);

@@ -1345,7 +1345,10 @@ __device__ __forceinline__ void copy_out(uint8_t* dst, const uint8_t* src, int64
 __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, int64_t* sizes) {
   const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
   if (i >= L.num_rows) return;
-  int64_t size = L.fixed_size + (L.frame ? 12 : 0);
+  // FORY_FRAME_COLLECTION (ArrayEncoder/MapEncoder.encode(MemoryBuffer, T), Encoders.java:418-431,
+  // 559-572): [i32 size][the single field's BinaryArray / BinaryMap], no row around it
+  const bool coll = L.frame == FORY_FRAME_COLLECTION;
+  int64_t size = coll ? 4 : L.fixed_size + (L.frame ? 12 : 0);
   int absent_depth = 0;  // >0: inside a null struct
   for (int pc = 0; pc < L.num_ops; ++pc) {
     const Op op = prog[pc];
@@ -1354,7 +1357,7 @@ __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* _
       case OP_FIXED:
         break;
       case OP_BYTES:
-        if (!absent_depth && (!(op.d & 1) || col_valid(c, i))) size += round8((int64_t)c.offsets[i + 1] - c.offsets[i]);
+        if (!absent_depth && (!(op.d & 1) || coll || col_valid(c, i))) size += round8((int64_t)c.offsets[i + 1] - c.offsets[i]);
         break;
       case OP_STRUCT_BEGIN:
         if (absent_depth || ((op.d & 1) && !col_valid(c, i))) absent_depth++;
@@ -1364,14 +1367,14 @@ __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* _
         if (absent_depth) absent_depth--;
         break;
       case OP_LIST:
-        if (!absent_depth && (!(op.d & 1) || col_valid(c, i))) {
+        if (!absent_depth && (!(op.d & 1) || coll || col_valid(c, i))) {
           const int64_t n = (int64_t)c.offsets[i + 1] - c.offsets[i];
           const int w = op.e & 0xff;
           size += 8 + bitmap_bytes(n) + round8(n * w);
         }
         break;
       case OP_LIST_STRUCT: {  // [i64 n][bitmap][n slots][child row per non-null element]
-        if (!absent_depth && (!(op.d & 1) || col_valid(c, i))) {
+        if (!absent_depth && (!(op.d & 1) || coll || col_valid(c, i))) {
           const int64_t e0 = c.offsets[i], n = (int64_t)c.offsets[i + 1] - e0;
           const int nf = op.e - pc - 1;
           const int64_t ssize = bitmap_bytes(nf) + 8LL * nf;
@@ -1387,7 +1390,7 @@ __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* _
         break;
       }
       case OP_MAP:  // [i64 keyArrayBytes][key array][value array]
-        if (!absent_depth && (!(op.d & 1) || col_valid(c, i))) {
+        if (!absent_depth && (!(op.d & 1) || coll || col_valid(c, i))) {
           const int64_t n = (int64_t)c.offsets[i + 1] - c.offsets[i];
           size += 8 + 2 * (8 + bitmap_bytes(n)) + round8(n * (op.e & 0xff)) + round8(n * ((op.e >> 8) & 0xff));
         }
@@ -1399,13 +1402,25 @@ __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* _
 
 constexpr int kFixBatch = 8;  // consecutive OP_FIXED ops whose loads are issued together
 
+// A var/struct/list/map slot store; slot == null for the top-level field of a
+// collection frame, which has none.
+__device__ __forceinline__ void slot_put(uint8_t* slot, uint64_t v) {
+  if (slot) gst64(slot, v);
+}
+
 // Encodes record i into `base` (its frame in STREAM mode, else its row;
 // `size` bytes; an LDS tile image or global memory). Generated toRow
 // (RowEncoderBuilder.java:177-208) with BaseBinaryEncoderBuilder's per-type
 // branches (:149-490) as an op program.
 __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, int64_t i, uint8_t* base, int64_t size) {
   uint8_t* row = base;
-  if (L.frame) {  // Encoders.encode(MemoryBuffer,T): [i32 8+rowSize][i64 hash]
+  // collection frames: the payload sits where the single field's var data would
+  // (row + fixed_size); the row's bitmap and slot are never written
+  const bool coll = L.frame == FORY_FRAME_COLLECTION;
+  if (coll) {
+    st32(base, (uint32_t)(size - 4));
+    row = base + 4 - L.fixed_size;
+  } else if (L.frame) {  // Encoders.encode(MemoryBuffer,T): [i32 8+rowSize][i64 hash]
     st32(base, (uint32_t)(size - 4));
     gst64(base + 4, (uint64_t)L.schema_hash);
     row = base + 12;
@@ -1418,7 +1433,8 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
   st_ord[0] = 0;
   int absent = 0;
   int64_t wi = L.fixed_size;  // writerIndex relative to row (BinaryRowWriter.reset)
-  for (int b = 0; b < L.bitmap_bytes; b += 8) gst64(row + b, 0);
+  if (!coll)
+    for (int b = 0; b < L.bitmap_bytes; b += 8) gst64(row + b, 0);
   // pc and the fixed-batch length stay wave-uniform (advanced outside the
   // per-lane branches) so the program and column tables load as scalars.
   for (int pc = 0, cnt = 1; pc < L.num_ops; pc += cnt) {
@@ -1434,9 +1450,13 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
       continue;
     }
     uint8_t* slots = row + st_start[depth] + st_hdr[depth];
-    uint8_t* slot = slots + 8 * op.a;
     uint8_t* bitmap = row + st_start[depth];
-    const bool isnull = (op.d & 1) && !col_valid(c, i);
+    // collection frames: the top-level field has no slot (slot = null: its writes
+    // are skipped) and is never null (a null collection is written from its
+    // offsets, i.e. empty; Java's toArray(null) would throw)
+    const bool top_coll = coll && depth == 0;
+    uint8_t* slot = top_coll ? nullptr : slots + 8 * op.a;
+    const bool isnull = !top_coll && (op.d & 1) && !col_valid(c, i);
     switch (op.code) {
       case OP_FIXED: {  // BinaryRowWriter.write(ordinal, v) / setNullAt, batched
         uint64_t v[kFixBatch];
@@ -1464,19 +1484,19 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
       case OP_BYTES: {
         if (isnull) {
           set_null_bit(bitmap, op.a);
-          gst64(slot, 0);
+          slot_put(slot, 0);
           break;
         }
         const int64_t s0 = c.offsets[i], n = (int64_t)c.offsets[i + 1] - s0;
         copy_padded(row + wi, c.values + s0, n);
-        gst64(slot, ((uint64_t)(wi - st_start[depth]) << 32) | (uint32_t)n);
+        slot_put(slot, ((uint64_t)(wi - st_start[depth]) << 32) | (uint32_t)n);
         wi += round8(n);
         break;
       }
       case OP_STRUCT_BEGIN: {
         if (isnull) {
           set_null_bit(bitmap, op.a);
-          gst64(slot, 0);
+          slot_put(slot, 0);
           absent = 1;
           break;
         }
@@ -1500,7 +1520,7 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
       case OP_LIST: {
         if (isnull) {
           set_null_bit(bitmap, op.a);
-          gst64(slot, 0);
+          slot_put(slot, 0);
           break;
         }
         // BinaryArrayWriter.reset(n) + per-element write (BinaryArrayWriter.java:93-158)
@@ -1541,13 +1561,13 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
           for (int64_t k = dsz; k < fixed_part; ++k) data[k] = 0;
         }
         wi += ahdr + fixed_part;
-        gst64(slot, ((uint64_t)(astart - st_start[depth]) << 32) | (uint32_t)(wi - astart));
+        slot_put(slot, ((uint64_t)(astart - st_start[depth]) << 32) | (uint32_t)(wi - astart));
         break;
       }
       case OP_LIST_STRUCT: {
         if (isnull) {
           set_null_bit(bitmap, op.a);
-          gst64(slot, 0);
+          slot_put(slot, 0);
           break;
         }
         // BinaryArrayWriter.reset(n) with 8-byte element slots, then per element
@@ -1586,13 +1606,13 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
           gst64(arr + ahdr + 8 * j, ((uint64_t)(wi - astart) << 32) | (uint32_t)ssize);
           wi += ssize;
         }
-        gst64(slot, ((uint64_t)(astart - st_start[depth]) << 32) | (uint32_t)(wi - astart));
+        slot_put(slot, ((uint64_t)(astart - st_start[depth]) << 32) | (uint32_t)(wi - astart));
         break;
       }
       case OP_MAP: {
         if (isnull) {
           set_null_bit(bitmap, op.a);
-          gst64(slot, 0);
+          slot_put(slot, 0);
           break;
         }
         // serializeForMap (BaseBinaryEncoderBuilder.java:370-427): reserve 8 bytes,
@@ -1631,7 +1651,7 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
           if (part == 0) keybytes = ahdr + fixed_part;
         }
         gst64(row + mstart, (uint64_t)keybytes);
-        gst64(slot, ((uint64_t)(mstart - st_start[depth]) << 32) | (uint32_t)(wi - mstart));
+        slot_put(slot, ((uint64_t)(mstart - st_start[depth]) << 32) | (uint32_t)(wi - mstart));
         break;
       }
     }
@@ -1650,7 +1670,16 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
   const int64_t i = live ? i0 : 0;
   const uint8_t* row = base;
   bool bad = !live;
-  if (live && L.frame) {
+  const bool coll = L.frame == FORY_FRAME_COLLECTION;
+  if (live && coll) {  // ArrayEncoder/MapEncoder.decode(MemoryBuffer): [i32 size][payload] (Encoders.java:394-404)
+    const uint32_t len = ld32(base);
+    if ((int64_t)len + 4 != row_len || len < 8) {
+      if (WRITE) set_status(status, FORY_ERR_CORRUPT);
+      bad = true;
+    }
+    row = base + 4 - L.fixed_size;  // the payload sits where the field's var data would
+    row_len += L.fixed_size - 4;
+  } else if (live && L.frame) {
     const uint32_t len = ld32(base);
     const uint64_t h = gld64(base + 4);
     if (h != (uint64_t)L.schema_hash) { if (WRITE) set_status(status, FORY_ERR_SCHEMA_MISMATCH); bad = true; }
@@ -1708,12 +1737,17 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
       continue;
     }
     bool isnull = true;
-    const uint8_t* slot = nullptr;
+    const uint8_t* slot = nullptr;  // null + !isnull: the top-level payload of a collection frame
     if (!absent) {
-      const uint8_t* bm = row + st_start[depth];
-      isnull = (bm[op.a >> 3] >> (op.a & 7)) & 1;  // BinaryRow.isNullAt
-      slot = row + st_start[depth] + st_hdr[depth] + 8 * op.a;
+      if (coll && depth == 0) {
+        isnull = false;
+      } else {
+        const uint8_t* bm = row + st_start[depth];
+        isnull = (bm[op.a >> 3] >> (op.a & 7)) & 1;  // BinaryRow.isNullAt
+        slot = row + st_start[depth] + st_hdr[depth] + 8 * op.a;
+      }
     }
+    const uint64_t coll_os = ((uint64_t)L.fixed_size << 32) | (uint32_t)(row_len - L.fixed_size);
     // Row-level validity of this column (rows of a wave are consecutive).
     if (WRITE && (op.d & 1) && c.out_validity && op.code != OP_STRUCT_END) {
       const uint64_t m = __ballot(live && !isnull);
@@ -1731,7 +1765,7 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
       case OP_BYTES: {
         int64_t n = 0, rel = 0;
         if (!isnull) {
-          const uint64_t os = gld64(slot);
+          const uint64_t os = (slot ? gld64(slot) : coll_os);
           rel = (int32_t)(os >> 32);
           n = (int32_t)(uint32_t)os;
           if (n < 0 || rel < 0 || st_start[depth] + rel + n > row_len) { set_status(status, FORY_ERR_CORRUPT); n = 0; }
@@ -1747,7 +1781,7 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
           absent++;
           break;
         }
-        const uint64_t os = gld64(slot);
+        const uint64_t os = (slot ? gld64(slot) : coll_os);
         const int64_t rel = (int32_t)(os >> 32);
         if (rel < 0 || st_start[depth] + rel + bitmap_bytes(op.c) + 8LL * op.c > row_len) {
           set_status(status, FORY_ERR_CORRUPT);
@@ -1766,7 +1800,7 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
       case OP_LIST: {
         int64_t n = 0, rel = 0;
         if (!isnull) {
-          const uint64_t os = gld64(slot);
+          const uint64_t os = (slot ? gld64(slot) : coll_os);
           rel = (int32_t)(os >> 32);
           if (rel < 0 || st_start[depth] + rel + 8 > row_len) {
             set_status(status, FORY_ERR_CORRUPT);
@@ -1836,7 +1870,7 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
         const int64_t ssize = shdr + 8LL * nf;
         int64_t n = 0, at = 0;
         if (!isnull) {
-          const uint64_t os = gld64(slot);
+          const uint64_t os = (slot ? gld64(slot) : coll_os);
           at = st_start[depth] + (int32_t)(os >> 32);
           if ((int32_t)(os >> 32) < 0 || at + 8 > row_len) {
             set_status(status, FORY_ERR_CORRUPT);
@@ -1899,7 +1933,7 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
       case OP_MAP: {  // BinaryMap.pointTo (BinaryMap.java:62-77): keys + values arrays
         int64_t n = 0, rel = 0, kat = 0, vat = 0;
         if (!isnull) {
-          const uint64_t os = gld64(slot);
+          const uint64_t os = (slot ? gld64(slot) : coll_os);
           rel = (int32_t)(os >> 32);
           const int64_t msz = (int32_t)(uint32_t)os;
           const int64_t at = st_start[depth] + rel;

@@ -9,7 +9,8 @@ from .columns import HostColumn, build_columns, pack_validity, unpack_validity  
 
 def __getattr__(name):
     # The device path (Encoders/RowEncoder) imports torch lazily.
-    if name in ("Encoders", "RowEncoder", "EncodedRows", "FRAME_RAW", "FRAME_STREAM"):
+    if name in ("Encoders", "RowEncoder", "CollectionEncoder", "EncodedRows", "FRAME_RAW", "FRAME_STREAM",
+                "FRAME_COLLECTION"):
         from . import encoder
         return getattr(encoder, name)
     raise AttributeError(name)

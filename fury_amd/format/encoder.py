@@ -10,6 +10,8 @@ Here the unit of work is a batch of N objects held as device columns:
                                                   into one fresh buffer
   encode(columns, n, frame_mode=FRAME_RAW)     == N x toRow(obj).toBytes()
   decode(rows, frame_mode=...)                 == N x decode(buffer) / fromRow(row)
+  Encoders.array_encoder / map_encoder         == N x ArrayEncoder / MapEncoder
+                                                  .encode(MemoryBuffer, collection)
 Same bytes, same schema hash, same exceptions (errors.py).
 """
 from __future__ import annotations
@@ -25,6 +27,7 @@ from .types import ArrowType, Schema
 
 FRAME_RAW = _lib.FRAME_RAW
 FRAME_STREAM = _lib.FRAME_STREAM
+FRAME_COLLECTION = _lib.FRAME_COLLECTION
 
 
 def _torch_dtype(type_id):
@@ -192,8 +195,37 @@ def _validity_bytes(n: int) -> int:
     return max(4, ((n + 7) // 8 + 3) // 4 * 4)
 
 
+class CollectionEncoder(RowEncoder):
+    """ArrayEncoder / MapEncoder mirror (Encoders.java:276-580): a batch of N collections
+    held as a one-field schema (the collection column); encode/decode default to the
+    collection frames [i32 size][BinaryArray | BinaryMap] (FRAME_COLLECTION)."""
+
+    def field(self):
+        return self.plan.schema.fields[0]
+
+    def encode(self, columns, num_rows, frame_mode=FRAME_COLLECTION):
+        return super().encode(columns, num_rows, frame_mode)
+
+    def decode(self, rows, num_rows=None, frame_mode=None, offsets=None):
+        if not isinstance(rows, EncodedRows) and frame_mode is None:
+            frame_mode = FRAME_COLLECTION
+        return super().decode(rows, num_rows, frame_mode, offsets)
+
+
 class Encoders:
     """Factory mirror of Encoders (Encoders.java:63-231)."""
+
+    @staticmethod
+    def array_encoder(element_field, device="cuda") -> CollectionEncoder:
+        """Encoders.arrayEncoder (Encoders.java:276-330,357-432) for Collection<element>."""
+        from .types import DataTypes
+        return CollectionEncoder(Schema([DataTypes.array_field("", element_field)]), None, device)
+
+    @staticmethod
+    def map_encoder(key_field, value_field, device="cuda") -> CollectionEncoder:
+        """Encoders.mapEncoder (Encoders.java:434-580) for Map<key, value>."""
+        from .types import DataTypes
+        return CollectionEncoder(Schema([DataTypes.map_field("", key_field, value_field)]), None, device)
 
     @staticmethod
     def bean(bean_class_or_schema, initial_buffer_size: int = 16, device="cuda") -> RowEncoder:

@@ -132,7 +132,16 @@ typedef struct fory_plan_info {
  *                     Encoder.encode(MemoryBuffer, T) write into one buffer
  *                     (Encoders.java:213-225):
  *                     [int32 LE 8+rowSize][int64 LE schemaHash][row].     */
-enum fory_frame_mode { FORY_FRAME_RAW = 0, FORY_FRAME_STREAM = 1 };
+enum fory_frame_mode { FORY_FRAME_RAW = 0, FORY_FRAME_STREAM = 1, FORY_FRAME_COLLECTION = 2 };
+/*  FORY_FRAME_COLLECTION: the standalone collection encoders — N calls of
+ *                     ArrayEncoder / MapEncoder .encode(MemoryBuffer, T)
+ *                     (Encoders.arrayEncoder / mapEncoder, Encoders.java:418-431,
+ *                     559-572): [int32 LE size][BinaryArray | BinaryMap].
+ *                     Only for plans of exactly one top-level LIST or MAP field
+ *                     (the collection); no schema hash. A null collection is
+ *                     written from its offsets (empty for Arrow-style nulls);
+ *                     decoding yields not-null collections. Decode checks
+ *                     size == frame length - 4 (FORY_ERR_CORRUPT otherwise). */
 
 /* --- library / errors --------------------------------------------------- */
 int32_t fory_rowfmt_abi_version(void);

@@ -275,27 +275,40 @@ static void write_struct_body(owriter* parent, int64_t ordinal, const otree* t, 
   w_set_offset_and_size(parent, ordinal, off, b->wi - off);
 }
 
-static void write_list_body(owriter* parent, int64_t ordinal, const otree* t, int idx,
-                            const fory_column* cols, int64_t i) {
-  /* BaseBinaryEncoderBuilder :240-249 (offset, serializeForArray, size,
-   * setOffsetAndSize) + serializeForArrayByWriter :293-351 (reset(n), then
-   * serializeFor(j, elem, arrayWriter, ...) per element) */
+/* The BinaryArray of list idx's entry i at the writerIndex: serializeForArrayByWriter
+ * :293-351 (reset(n), then serializeFor(j, elem, arrayWriter, ...) per element). */
+static void write_list_payload(obuf* b, const otree* t, int idx, const fory_column* cols, int64_t i) {
   const onode* nd = &t->nodes[idx];
   const fory_column* c = &cols[idx];
   int item = nd->child[0];
   const onode* it = &t->nodes[item];
   int64_t b0 = c->offsets[i], b1 = c->offsets[i + 1];
   int64_t n = b1 - b0;
-  obuf* b = parent->b;
-  int64_t off = b->wi;
   owriter aw;
   array_reset(&aw, b, n, it->width < 0 ? 8 : it->width); /* BinaryArrayWriter ctor :75-85 */
   for (int64_t j = 0; j < n; j++) write_value(&aw, j, t, item, cols, b0 + j);
+}
+
+static void write_list_body(owriter* parent, int64_t ordinal, const otree* t, int idx,
+                            const fory_column* cols, int64_t i) {
+  /* BaseBinaryEncoderBuilder :240-249 (offset, serializeForArray, size, setOffsetAndSize) */
+  obuf* b = parent->b;
+  int64_t off = b->wi;
+  write_list_payload(b, t, idx, cols, i);
   w_set_offset_and_size(parent, ordinal, off, b->wi - off);
 }
 
+static void write_map_payload(obuf* b, const otree* t, int idx, const fory_column* cols, int64_t i);
+
 static void write_map_body(owriter* parent, int64_t ordinal, const otree* t, int idx,
                            const fory_column* cols, int64_t i) {
+  obuf* b = parent->b;
+  int64_t off = b->wi;
+  write_map_payload(b, t, idx, cols, i);
+  w_set_offset_and_size(parent, ordinal, off, b->wi - off);
+}
+
+static void write_map_payload(obuf* b, const otree* t, int idx, const fory_column* cols, int64_t i) {
   /* serializeForMap (BaseBinaryEncoderBuilder.java:370-427): offset = writerIndex;
    * writeDirectly(-1) reserves 8 bytes (BinaryWriter.java:232-236); the key set
    * and the values are written as two BinaryArrays (serializeForArray); the key
@@ -305,7 +318,6 @@ static void write_map_body(owriter* parent, int64_t ordinal, const otree* t, int
   const onode* nd = &t->nodes[idx];
   const fory_column* c = &cols[idx];
   int64_t b0 = c->offsets[i], n = c->offsets[i + 1] - b0;
-  obuf* b = parent->b;
   int64_t off = b->wi;
   grow(b, 8);
   put64(b, off, (uint64_t)-1);
@@ -321,7 +333,6 @@ static void write_map_body(owriter* parent, int64_t ordinal, const otree* t, int
     if (part == 0) key_bytes = b->wi - a0;
   }
   put64(b, off, (uint64_t)key_bytes);
-  w_set_offset_and_size(parent, ordinal, off, b->wi - off);
 }
 
 static void write_value(owriter* w, int64_t ordinal, const otree* t, int idx,
@@ -396,6 +407,20 @@ int64_t oracle_encode(const fory_field_desc* d, int n_desc, const fory_column* c
   for (int64_t i = 0; i < nrows; i++) {
     if (row_offsets) row_offsets[i] = b.wi;
     int64_t frame = b.wi;
+    if (frame_mode == 2) {
+      /* ArrayEncoder / MapEncoder.encode(MemoryBuffer, T) (Encoders.java:418-431,
+       * 559-572): writeInt32(-1), the collection's BinaryArray / BinaryMap at the
+       * writerIndex (toArray / toMap), back-patched size. A null collection is
+       * written from its offsets (the device path's documented policy). */
+      const onode* top = t.ntop == 1 ? &t.nodes[t.top[0]] : NULL;
+      if (!top || (top->type_id != FORY_TYPE_LIST && top->type_id != FORY_TYPE_MAP)) { free_tree(&t); return -2; }
+      put32(&b, b.wi, 0xFFFFFFFFu); b.wi += 4;
+      if (top->type_id == FORY_TYPE_LIST) write_list_payload(&b, &t, t.top[0], cols, i);
+      else write_map_payload(&b, &t, t.top[0], cols, i);
+      put32(&b, frame, (uint32_t)(b.wi - frame - 4));
+      if (b.overflow == 2) { free_tree(&t); return -2; }
+      continue;
+    }
     if (frame_mode) {
       put32(&b, b.wi, 0xFFFFFFFFu); b.wi += 4;        /* writeInt32(-1) */
       put64(&b, b.wi, (uint64_t)hash); b.wi += 8;     /* writeInt64(schemaHash) */
@@ -464,6 +489,9 @@ static void null_value(odec* D, const otree* t, int idx, const fory_column* cols
 /* Read one value of node idx whose slot is at `slot_at` inside the row or
  * array starting at `base` (relative offsets are relative to it) and write
  * it to output slot i. */
+static void read_payload(odec* D, const otree* t, int idx, const fory_column* cols, int64_t i, int64_t at,
+                         int64_t size);
+
 static void read_value(odec* D, const otree* t, int idx, const fory_column* cols,
                        int64_t i, int is_null, int64_t slot_at, int64_t base) {
   const onode* nd = &t->nodes[idx];
@@ -483,7 +511,15 @@ static void read_value(odec* D, const otree* t, int idx, const fory_column* cols
   uint64_t os = rd(D, slot_at, 8);
   int64_t rel = (int32_t)(os >> 32);   /* (int)(offsetAndSize >> 32) */
   int64_t size = (int32_t)os;          /* (int)offsetAndSize */
-  int64_t at = base + rel;
+  read_payload(D, t, idx, cols, i, base + rel, size);
+}
+
+/* The var payload of node idx at [at, at+size) -> output slot i (the part of
+ * read_value after the slot; also the whole record of a collection frame). */
+static void read_payload(odec* D, const otree* t, int idx, const fory_column* cols, int64_t i, int64_t at,
+                         int64_t size) {
+  const onode* nd = &t->nodes[idx];
+  const fory_column* c = &cols[idx];
   if (size < 0 || at < 0 || at + size > D->len) { D->bad = 1; return; }
   switch (nd->type_id) {
     case FORY_TYPE_STRING: case FORY_TYPE_BINARY: { /* getBinary :116-137 */
@@ -572,6 +608,19 @@ int oracle_decode(const fory_field_desc* d, int n_desc, const uint8_t* buf, int6
   for (int64_t i = 0; i < nrows && !rc; i++) {
     int64_t start = row_offsets ? row_offsets[i] : pos;
     int64_t row_at = start;
+    if (frame_mode == 2) {  /* ArrayEncoder / MapEncoder.decode: [i32 size][payload] (Encoders.java:394-404) */
+      int64_t size = (int32_t)rd(&D, start, 4);
+      int64_t end = row_offsets ? row_offsets[i + 1] : start + 4 + size;
+      if (D.bad || size < 8 || start + 4 + size != end || end > len) { rc = 5; break; }
+      if (i == 0 && !sizing) cols[t.top[0]].offsets[0] = 0;
+      D.slots[t.top[0]]++;
+      if (t.nodes[t.top[0]].nullable && !sizing) set_valid(&cols[t.top[0]], i, 1);  /* never null */
+      read_payload(&D, &t, t.top[0], cols, i, start + 4, size);
+      pos = end;
+      if (D.bad == 2) rc = 3;
+      else if (D.bad) rc = 5;
+      continue;
+    }
     if (frame_mode) {
       int64_t size = (int32_t)rd(&D, start, 4);       /* buffer.readInt32() */
       int64_t peer = (int64_t)rd(&D, start + 4, 8);   /* buffer.readInt64() */

@@ -315,3 +315,27 @@ def _struct_parents(schema: Schema):
     for f in schema.fields:
         visit(f, None)
     return out
+
+
+def collection_cases(n=300, seed=5):
+    """One-field schemas of the standalone collection encoders (Encoders.arrayEncoder /
+    mapEncoder) and their rows: list<Long>, List<Bean>, Map<Integer, Long>."""
+    rng = np.random.default_rng(seed)
+
+    def bean():
+        return {"a": int(rng.integers(-2**31, 2**31)), "b": None if rng.random() < 0.3 else int(rng.integers(-2**62, 2**62)),
+                "c": bool(rng.random() < 0.5), "d": float(np.float32(rng.standard_normal()))}
+
+    longs = Schema([DataTypes.array_field("", Field("item", DataType(ArrowType.INT64), True))])
+    beans = Schema([list_struct_schema().fields[1]])
+    amap = Schema([maps_schema().fields[1]])
+    out = []
+    for schema, gen in [
+        (longs, lambda: {"": [None if rng.random() < 0.1 else int(x) for x in rng.integers(-9, 9, size=rng.integers(0, 70))]}),
+        (beans, lambda: {"items": [None if rng.random() < 0.2 else bean() for _ in range(int(rng.integers(0, 5)))]}),
+        (amap, lambda: {"counts": {int(k): (None if rng.random() < 0.2 else int(k) * 3)
+                                   for k in rng.choice(1000, size=rng.integers(0, 9), replace=False)}}),
+    ]:
+        rows = [gen() for _ in range(n)]
+        out.append((schema, build_columns(schema, rows)))
+    return out

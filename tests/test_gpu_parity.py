@@ -18,11 +18,11 @@ from fury_amd import workloads as W  # noqa: E402
 from fury_amd.format import (ClassNotCompatibleException, CorruptRowException,  # noqa: E402
                              IndexOutOfBoundsException)
 from fury_amd.format.columns import to_device, to_host  # noqa: E402
-from fury_amd.format.encoder import EncodedRows, RowEncoder  # noqa: E402
+from fury_amd.format.encoder import CollectionEncoder, EncodedRows, Encoders, RowEncoder  # noqa: E402
 from fury_amd.format import native  # noqa: E402
 from fury_amd.format.types import ArrowType  # noqa: E402
 
-from helpers import catalog, columns_equal  # noqa: E402
+from helpers import catalog, collection_cases, columns_equal  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -116,6 +116,30 @@ def test_encode_decode_parity(name, n, frame, kernel_variant):
 @pytest.mark.parametrize("name", VARLEN)
 def test_varlen_parity(name, n, frame, varlen_engine):
     check_parity(name, n, frame)
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 65, 4097])
+def test_collection_frame_parity(n, varlen_engine):
+    """ArrayEncoder / MapEncoder frames (Encoders.java:418-431, 559-572): device bytes ==
+    oracle bytes for list<Long>, List<Bean> and Map<Integer, Long>, and both decode back."""
+    for schema, cols in collection_cases(n, 7 + n):
+        f = schema.fields[0]
+        if f.type.id == ArrowType.MAP:
+            enc = Encoders.map_encoder(f.children[0], f.children[1])
+        else:
+            enc = Encoders.array_encoder(f.children[0])
+        assert enc.plan.schema_hash == CollectionEncoder(schema).plan.schema_hash  # names do not hash
+        expect, offs = oracle.encode(schema, cols, n, 2)
+        rows = enc.encode(to_device(cols), n)
+        got = rows.buffer.cpu().numpy()
+        assert got.nbytes == expect.nbytes
+        bad = np.nonzero(got != expect)[0]
+        assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+        assert np.array_equal(rows.offsets.cpu().numpy(), offs)
+        assert columns_equal(schema, cols, to_host(enc.decode(rows))) == []
+        buf = torch.from_numpy(np.concatenate([expect, np.zeros(16, np.uint8)])).cuda()
+        dec = to_host(enc.decode(buf, n, None, torch.from_numpy(offs).cuda()))
+        assert columns_equal(schema, cols, dec) == []
 
 
 @pytest.mark.parametrize("shift", [4, 8, 12])
