@@ -121,7 +121,25 @@ int bind_fixed(const Plan& p, const fory_column* cols, int64_t n, bool decode,
   return FORY_OK;
 }
 
-int bind_var(const Plan& p, const fory_column* cols, int64_t n, std::vector<ColumnDev>* out) {
+// String/binary list elements and map keys/values: their columns are indexed by
+// element, so decode sizes them in a second lengths pass (decode_sizes).
+std::vector<int32_t> elem_bytes_cols(const Plan& p) {
+  std::vector<int32_t> out;
+  for (const fory_amd::Op& op : p.program) {
+    if (op.code == fory_amd::OP_LIST && ((op.e >> 8) & 4)) out.push_back(op.c);
+    if (op.code == fory_amd::OP_MAP) {
+      if ((op.e >> 16) & 4) out.push_back(op.c);
+      if ((op.e >> 24) & 4) out.push_back(op.c + 1);
+    }
+  }
+  return out;
+}
+
+// sizes_pass: element string/binary columns may come without offsets (decode_sizes
+// before the caller knows the element count).
+int bind_var(const Plan& p, const fory_column* cols, int64_t n, std::vector<ColumnDev>* out,
+             bool sizes_pass = false) {
+  std::vector<int32_t> elem = sizes_pass ? elem_bytes_cols(p) : std::vector<int32_t>();
   out->resize(p.nodes.size());
   for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
     const fory_amd::Node& nd = p.nodes[idx];
@@ -135,7 +153,7 @@ int bind_var(const Plan& p, const fory_column* cols, int64_t n, std::vector<Colu
     d.out_validity = nd.nullable ? c.validity : nullptr;
     if (n > 0) {
       if ((nd.kind == fory_amd::KIND_BYTES || nd.kind == fory_amd::KIND_LIST || nd.kind == fory_amd::KIND_MAP) &&
-          !c.offsets)
+          !c.offsets && std::find(elem.begin(), elem.end(), (int32_t)idx) == elem.end())
         return fail(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(idx) + " needs offsets");
     }
     (*out)[idx] = d;
@@ -235,9 +253,9 @@ int var_tile_cap(const Plan& p, int frame) {
 
 // Var launch: columns table then program in the workspace.
 int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, void* ws,
-                hipStream_t s, fory_amd::VarLaunch* L) {
+                hipStream_t s, fory_amd::VarLaunch* L, bool sizes_pass = false) {
   std::vector<ColumnDev> cd;
-  int rc = bind_var(p, cols, n, &cd);
+  int rc = bind_var(p, cols, n, &cd, sizes_pass);
   if (rc) return rc;
   const int64_t col_bytes = align_up((int64_t)cd.size() * (int64_t)sizeof(ColumnDev));
   const int64_t prog_bytes = align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::Op));
@@ -319,8 +337,11 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   if (rc) return rc;
   uint8_t* wsb = static_cast<uint8_t*>(ws);
   bool has_map = false;  // (and lists of structs)
-  for (const fory_amd::Op& op : p.program) has_map |= op.code == fory_amd::OP_MAP || op.code == fory_amd::OP_LIST_STRUCT;
-  // maps run on the generic tile interpreter (enc_record / dec_record)
+  for (const fory_amd::Op& op : p.program)
+    has_map |= op.code == fory_amd::OP_MAP || op.code == fory_amd::OP_LIST_STRUCT ||
+               (op.code == fory_amd::OP_LIST && ((op.e >> 8) & 4));
+  // maps, lists of structs and lists of strings run on the generic tile interpreter
+  // (enc_record / dec_record)
   L->flat = !has_map && frame != FORY_FRAME_COLLECTION && var.size() <= 32 &&
                     st.size() <= (size_t)fory_amd::kMaxTileStructs
                 ? 1
@@ -362,6 +383,7 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   L->num_rows = n;
   L->frame = frame;
   L->tile_cap = var_tile_cap(p, frame);
+  L->level2 = 0;
   return FORY_OK;
 }
 
@@ -379,6 +401,16 @@ int64_t* tile_totals_ptr(const Plan& p, void* ws, int64_t n) {
 int32_t* spill_ptr(const Plan& p, void* ws, int64_t n) {
   return reinterpret_cast<int32_t*>(reinterpret_cast<uint8_t*>(tile_totals_ptr(p, ws, n)) +
                                     align_up(fory_amd::var_tile_totals_words(num_var_ops(p), n) * 8));
+}
+
+// Scan partials of the element string/binary columns (after the spill list): the
+// element count is unknown when the workspace is sized, so their offsets are
+// scanned in segments of kScanTile x (words - 1) elements (one segment in practice).
+int64_t elem_partials_words(const Plan& p, int64_t n) { return elem_bytes_cols(p).empty() ? 0 : n / 8 + 8; }
+
+int64_t* elem_partials_ptr(const Plan& p, void* ws, int64_t n) {
+  return reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(spill_ptr(p, ws, n)) +
+                                    align_up(fory_amd::var_spill_words(n) * 4));
 }
 
 }  // namespace
@@ -445,7 +477,7 @@ int64_t fory_rowfmt_workspace_bytes(const fory_plan* plan, int64_t num_rows) {
   const int64_t n = num_rows < 0 ? 0 : num_rows;
   return table_bytes(plan->p) + align_up((fory_amd::scan_partials(n) + 2) * 8) +
          align_up(fory_amd::var_tile_totals_words(num_var_ops(plan->p), n) * 8) +
-         align_up(fory_amd::var_spill_words(n) * 4);
+         align_up(fory_amd::var_spill_words(n) * 4) + align_up(elem_partials_words(plan->p, n) * 8);
 }
 
 int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols, int64_t num_rows,
@@ -539,19 +571,43 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
     return fail(FORY_ERR_INVALID_ARGUMENT, "varlen schema: d_rows and d_row_offsets required");
   hipStream_t s = static_cast<hipStream_t>(stream);
   fory_amd::VarLaunch L{};
-  rc = prepare_var(p, out_cols, num_rows, frame_mode, d_workspace, s, &L);
+  rc = prepare_var(p, out_cols, num_rows, frame_mode, d_workspace, s, &L, true);
   if (rc) return rc;
   hipError_t e = fory_amd::launch_var_decode_lengths(L, static_cast<const uint8_t*>(d_rows), d_row_offsets,
                                                      tile_totals_ptr(p, d_workspace, num_rows),
                                                      partials_ptr(p, d_workspace), d_status, s);
   if (e != hipSuccess) return hip_fail(e, "var_decode_lengths");
   if (fory_amd::var_decode_tiled_offsets(L)) return FORY_OK;  // tile bases written; decode fills the rest
+  const std::vector<int32_t> elem = elem_bytes_cols(p);
+  auto is_elem = [&](size_t idx) { return std::find(elem.begin(), elem.end(), (int32_t)idx) != elem.end(); };
   for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
     const int k = p.nodes[idx].kind;
     if (k != fory_amd::KIND_BYTES && k != fory_amd::KIND_LIST && k != fory_amd::KIND_MAP) continue;
+    if (is_elem(idx)) continue;
     e = fory_amd::launch_scan_offsets_i32(out_cols[idx].offsets, num_rows, partials_ptr(p, d_workspace),
                                           d_status, s);
     if (e != hipSuccess) return hip_fail(e, "scan offsets");
+  }
+  // pass 2: element string/binary columns whose offsets the caller has allocated
+  // (length = the container's element total from pass 1)
+  bool level2 = false;
+  for (int32_t idx : elem) {
+    if (!out_cols[idx].offsets) continue;
+    if (out_cols[idx].length < 0) return fail(FORY_ERR_INVALID_ARGUMENT, "element column length < 0");
+    level2 = true;
+  }
+  if (!level2) return FORY_OK;
+  L.level2 = 1;
+  e = fory_amd::launch_var_decode_lengths(L, static_cast<const uint8_t*>(d_rows), d_row_offsets,
+                                          tile_totals_ptr(p, d_workspace, num_rows), partials_ptr(p, d_workspace),
+                                          d_status, s);
+  if (e != hipSuccess) return hip_fail(e, "var_decode_lengths (elements)");
+  for (int32_t idx : elem) {
+    if (!out_cols[idx].offsets) continue;
+    e = fory_amd::launch_scan_offsets_i32_segmented(out_cols[idx].offsets, out_cols[idx].length,
+                                                    elem_partials_ptr(p, d_workspace, num_rows),
+                                                    elem_partials_words(p, num_rows), d_status, s);
+    if (e != hipSuccess) return hip_fail(e, "scan element offsets");
   }
   return FORY_OK;
 }

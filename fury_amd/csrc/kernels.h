@@ -68,6 +68,8 @@ struct VarLaunch {
   uint64_t* prof;               // debug (FORY_ROWFMT_VARPROF): 8 timestamps per tile, else null
   int32_t* spill;               // workspace: tiles spilled to the big-image launch (ceil(n/64))
   int32_t* spill_count;         // workspace: number of spilled tiles
+  int32_t level2;               // decode lengths pass 2: sizes of string/binary list/map
+                                // elements (container offsets already scanned)
 };
 
 // sizes -> d_row_offsets[0..n-1] (row/frame byte sizes), then exclusive scan.
@@ -99,5 +101,9 @@ hipError_t launch_scan_i64(int64_t* data, int64_t n, int64_t* partials, hipStrea
 // prefix into offs[1..n] (int32). Overflow past INT32_MAX sets *status.
 hipError_t launch_scan_offsets_i32(int32_t* offs, int64_t n, int64_t* partials,
                                    int32_t* status, hipStream_t s);
+// The same over an offsets array of any length with a partials buffer of
+// partial_words int64 (segments of 4096 x (partial_words - 1) items, carried).
+hipError_t launch_scan_offsets_i32_segmented(int32_t* offs, int64_t n, int64_t* partials, int64_t partial_words,
+                                             int32_t* status, hipStream_t s);
 
 }  // namespace fory_amd

@@ -1240,7 +1240,9 @@ __global__ __launch_bounds__(kWG) void scan_partials_kernel(int64_t* partials, i
   if (threadIdx.x == 0) partials[nb] = carry;
 }
 
-template <int MODE>
+// SEG (MODE 1): a segment of a longer offsets array: data[0] already holds the
+// previous segment's last offset (the carry; 0 for the first) and is left as is.
+template <int MODE, bool SEG = false>
 __global__ __launch_bounds__(kWG) void scan_down_kernel(void* data, int64_t n, const int64_t* partials,
                                                         int32_t* status) {
   __shared__ int64_t smem[kWaves];
@@ -1254,6 +1256,7 @@ __global__ __launch_bounds__(kWG) void scan_down_kernel(void* data, int64_t n, c
   }
   int64_t tot;
   int64_t pre = block_excl_scan(s, smem, &tot) + partials[blockIdx.x];
+  if (SEG) pre += reinterpret_cast<const int32_t*>(data)[0];
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
     if (base + k < n) {
@@ -1269,7 +1272,7 @@ __global__ __launch_bounds__(kWG) void scan_down_kernel(void* data, int64_t n, c
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (MODE == 0) reinterpret_cast<int64_t*>(data)[n] = partials[gridDim.x];
-    else reinterpret_cast<int32_t*>(data)[0] = 0;
+    else if (!SEG) reinterpret_cast<int32_t*>(data)[0] = 0;
   }
 }
 
@@ -1341,6 +1344,18 @@ __device__ __forceinline__ void copy_out(uint8_t* dst, const uint8_t* src, int64
   for (; k < n; ++k) store_byte(dst + k, src[k]);
 }
 
+// Bytes of a BinaryArray of n elements of column `it` starting at element e0
+// (BinaryArrayWriter.reset(n) + appends, BinaryArrayWriter.java:93-118): header,
+// bitmap, fixed part padded to 8, and for string/binary elements (iflags bit2)
+// each non-null element's bytes padded to 8.
+__device__ __forceinline__ int64_t array_bytes(const ColumnDev& it, int w, int iflags, int64_t e0, int64_t n) {
+  int64_t s = 8 + bitmap_bytes(n) + round8(n * w);
+  if (iflags & 4)
+    for (int64_t j = 0; j < n; ++j)
+      if (!(iflags & 1) || col_valid(it, e0 + j)) s += round8((int64_t)it.offsets[e0 + j + 1] - it.offsets[e0 + j]);
+  return s;
+}
+
 // Row/frame size of record i (BinaryRowWriter.reset + all appends).
 __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, int64_t* sizes) {
   const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
@@ -1368,9 +1383,8 @@ __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* _
         break;
       case OP_LIST:
         if (!absent_depth && (!(op.d & 1) || coll || col_valid(c, i))) {
-          const int64_t n = (int64_t)c.offsets[i + 1] - c.offsets[i];
-          const int w = op.e & 0xff;
-          size += 8 + bitmap_bytes(n) + round8(n * w);
+          const int64_t e0 = c.offsets[i], n = (int64_t)c.offsets[i + 1] - e0;
+          size += array_bytes(cols[op.c], op.e & 0xff, op.e >> 8, e0, n);
         }
         break;
       case OP_LIST_STRUCT: {  // [i64 n][bitmap][n slots][child row per non-null element]
@@ -1391,8 +1405,9 @@ __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* _
       }
       case OP_MAP:  // [i64 keyArrayBytes][key array][value array]
         if (!absent_depth && (!(op.d & 1) || coll || col_valid(c, i))) {
-          const int64_t n = (int64_t)c.offsets[i + 1] - c.offsets[i];
-          size += 8 + 2 * (8 + bitmap_bytes(n)) + round8(n * (op.e & 0xff)) + round8(n * ((op.e >> 8) & 0xff));
+          const int64_t e0 = c.offsets[i], n = (int64_t)c.offsets[i + 1] - e0;
+          size += 8 + array_bytes(cols[op.c], op.e & 0xff, (op.e >> 16) & 0xff, e0, n) +
+                  array_bytes(cols[op.c + 1], (op.e >> 8) & 0xff, (op.e >> 24) & 0xff, e0, n);
         }
         break;
     }
@@ -1406,6 +1421,71 @@ constexpr int kFixBatch = 8;  // consecutive OP_FIXED ops whose loads are issued
 // collection frame, which has none.
 __device__ __forceinline__ void slot_put(uint8_t* slot, uint64_t v) {
   if (slot) gst64(slot, v);
+}
+
+// A BinaryArray of string/binary elements at row + wi: reset(n) with 8-byte element
+// slots (BinaryArrayWriter.java:75-85,93-118), then per element write(j, bytes) ->
+// writeUnaligned (BinaryWriter.java:162-194): bytes appended at the writerIndex,
+// zero-padded to 8, slot = (offset from the array start, size); a null element sets
+// its bit, slot 0. Returns the new writerIndex.
+__device__ __forceinline__ int64_t enc_bytes_array(uint8_t* row, int64_t wi, const ColumnDev& it, int iflags,
+                                                   int64_t e0, int64_t n) {
+  const int64_t astart = wi;
+  uint8_t* arr = row + astart;
+  const int32_t ahdr = 8 + bitmap_bytes(n);
+  gst64(arr, (uint64_t)n);
+  for (int b = 8; b < ahdr; b += 8) gst64(arr + b, 0);
+  wi += ahdr + 8 * n;
+  for (int64_t j = 0; j < n; ++j) {
+    uint8_t* eslot = arr + ahdr + 8 * j;
+    if ((iflags & 1) && !col_valid(it, e0 + j)) {
+      arr[8 + (j >> 3)] |= (uint8_t)(1u << (j & 7));
+      gst64(eslot, 0);
+      continue;
+    }
+    const int64_t s0 = it.offsets[e0 + j], len = (int64_t)it.offsets[e0 + j + 1] - s0;
+    copy_padded(row + wi, it.values + s0, len);
+    gst64(eslot, ((uint64_t)(wi - astart) << 32) | (uint32_t)len);
+    wi += round8(len);
+  }
+  return wi;
+}
+
+// Reads a BinaryArray of string/binary elements at row + at (n elements, bounds
+// row_len): BinaryArray.isNullAt + getString/getBinary per element (UnsafeTrait.java:
+// 68-197, offsets relative to the array). LENGTHS: element sizes into
+// it.out_offsets[e0 + j + 1] (the caller scans them); else bytes to
+// it.out_values + it.out_offsets[e0 + j] and item validity.
+template <bool LENGTHS>
+__device__ __forceinline__ void dec_bytes_array(const uint8_t* row, int64_t row_len, int64_t at, int64_t n,
+                                                const ColumnDev& it, int iflags, int64_t e0, int32_t* status) {
+  const uint8_t* arr = row + at;
+  const int32_t ahdr = 8 + bitmap_bytes(n);
+  for (int64_t j = 0; j < n; ++j) {
+    const int64_t q = e0 + j;
+    bool en = (arr[8 + (j >> 3)] >> (j & 7)) & 1;
+    int64_t len = 0, rel = 0;
+    if (!en) {
+      const uint64_t os = gld64(arr + ahdr + 8 * j);
+      rel = (int32_t)(os >> 32);
+      len = (int32_t)(uint32_t)os;
+      if (rel < 0 || len < 0 || at + rel + len > row_len) {
+        set_status(status, FORY_ERR_CORRUPT);
+        len = 0;
+      }
+    }
+    if (LENGTHS) {
+      it.out_offsets[q + 1] = (int32_t)len;
+    } else {
+      if (len > 0) copy_out(it.out_values + it.out_offsets[q], arr + rel, len);
+      if ((iflags & 1) && it.out_validity) {
+        const uint32_t bit = 1u << (q & 31);
+        uint32_t* word = reinterpret_cast<uint32_t*>(it.out_validity) + (q >> 5);
+        if (en) atomicAnd(word, ~bit);
+        else atomicOr(word, bit);
+      }
+    }
+  }
 }
 
 // Encodes record i into `base` (its frame in STREAM mode, else its row;
@@ -1529,6 +1609,11 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
         const int iflags = op.e >> 8;
         const int64_t e0 = c.offsets[i], n = (int64_t)c.offsets[i + 1] - e0;
         const int64_t astart = wi;
+        if (iflags & 4) {  // string/binary elements
+          wi = enc_bytes_array(row, wi, it, iflags, e0, n);
+          slot_put(slot, ((uint64_t)(astart - st_start[depth]) << 32) | (uint32_t)(wi - astart));
+          break;
+        }
         const int32_t ahdr = 8 + bitmap_bytes(n);
         uint8_t* arr = row + astart;
         gst64(arr, (uint64_t)n);
@@ -1627,6 +1712,12 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
           const ColumnDev& it = cols[op.c + part];
           const int w = (op.e >> (8 * part)) & 0xff;
           const int iflags = (op.e >> (16 + 8 * part)) & 0xff;
+          if (iflags & 4) {  // string/binary keys or values
+            const int64_t a0 = wi;
+            wi = enc_bytes_array(row, wi, it, iflags, e0, n);
+            if (part == 0) keybytes = wi - a0;
+            continue;
+          }
           uint8_t* arr = row + wi;
           const int32_t ahdr = 8 + bitmap_bytes(n);
           gst64(arr, (uint64_t)n);  // BinaryArrayWriter.reset(n) (BinaryArrayWriter.java:93-118)
@@ -1771,8 +1862,11 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
           if (n < 0 || rel < 0 || st_start[depth] + rel + n > row_len) { set_status(status, FORY_ERR_CORRUPT); n = 0; }
         }
         if (live) {
-          if (!WRITE) c.out_offsets[i + 1] = (int32_t)n;
-          else if (n > 0) copy_out(c.out_values + c.out_offsets[i], row + st_start[depth] + rel, n);
+          if (!WRITE) {
+            if (!L.level2) c.out_offsets[i + 1] = (int32_t)n;
+          } else if (n > 0) {
+            copy_out(c.out_values + c.out_offsets[i], row + st_start[depth] + rel, n);
+          }
         }
         break;
       }
@@ -1814,12 +1908,16 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
           }
         }
         if (live) {
+          const ColumnDev& it = cols[op.c];
+          const int iflags = op.e >> 8;
           if (!WRITE) {
-            c.out_offsets[i + 1] = (int32_t)n;
+            if (!L.level2) c.out_offsets[i + 1] = (int32_t)n;
+            else if ((iflags & 4) && it.out_offsets && n > 0)  // element sizes (list offsets final)
+              dec_bytes_array<true>(row, row_len, st_start[depth] + rel, n, it, iflags, c.out_offsets[i], status);
+          } else if (n > 0 && (iflags & 4)) {
+            dec_bytes_array<false>(row, row_len, st_start[depth] + rel, n, it, iflags, c.out_offsets[i], status);
           } else if (n > 0) {
-            const ColumnDev& it = cols[op.c];
             const int w = op.e & 0xff;
-            const int iflags = op.e >> 8;
             const uint8_t* arr = row + st_start[depth] + rel;
             const int32_t ahdr = 8 + bitmap_bytes(n);
             const int64_t e0 = c.out_offsets[i];
@@ -1884,7 +1982,7 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
         }
         if (live) {
           if (!WRITE) {
-            c.out_offsets[i + 1] = (int32_t)n;
+            if (!L.level2) c.out_offsets[i + 1] = (int32_t)n;
           } else if (n > 0) {
             const ColumnDev& sc = cols[op.c];
             const uint8_t* arr = row + at;
@@ -1959,13 +2057,26 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
         }
         if (live) {
           if (!WRITE) {
-            c.out_offsets[i + 1] = (int32_t)n;
+            if (!L.level2) {
+              c.out_offsets[i + 1] = (int32_t)n;
+            } else if (n > 0) {  // string/binary key or value sizes (entry offsets final)
+              for (int part = 0; part < 2; ++part) {
+                const ColumnDev& it = cols[op.c + part];
+                const int iflags = (op.e >> (16 + 8 * part)) & 0xff;
+                if ((iflags & 4) && it.out_offsets)
+                  dec_bytes_array<true>(row, row_len, part ? vat : kat, n, it, iflags, c.out_offsets[i], status);
+              }
+            }
           } else if (n > 0) {
             const int64_t e0 = c.out_offsets[i];
             for (int part = 0; part < 2; ++part) {
               const ColumnDev& it = cols[op.c + part];
               const int w = (op.e >> (8 * part)) & 0xff;
               const int iflags = (op.e >> (16 + 8 * part)) & 0xff;
+              if (iflags & 4) {
+                dec_bytes_array<false>(row, row_len, part ? vat : kat, n, it, iflags, e0, status);
+                continue;
+              }
               const uint8_t* arr = row + (part ? vat : kat);
               const int32_t ahdr = 8 + bitmap_bytes(n);
               for (int64_t j = 0; j < n; ++j) {
@@ -3525,6 +3636,23 @@ hipError_t launch_scan_offsets_i32(int32_t* offs, int64_t n, int64_t* partials, 
   hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kWG), 0, s, partials, nb);
   hipLaunchKernelGGL(scan_down_kernel<1>, dim3((unsigned)nb), dim3(kWG), 0, s, (void*)offs, n,
                      (const int64_t*)partials, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_offsets_i32_segmented(int32_t* offs, int64_t n, int64_t* partials, int64_t partial_words,
+                                             int32_t* status, hipStream_t s) {
+  (void)hipMemsetAsync(offs, 0, sizeof(int32_t), s);
+  const int64_t seg = kScanTile * (partial_words - 1);
+  if (n <= 0) return hipGetLastError();
+  if (seg <= 0) return hipErrorInvalidValue;
+  for (int64_t a = 0; a < n; a += seg) {
+    const int64_t m = n - a < seg ? n - a : seg;
+    const int64_t nb = (m + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(scan_reduce_kernel<1>, dim3((unsigned)nb), dim3(kWG), 0, s, (void*)(offs + a), m, partials);
+    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kWG), 0, s, partials, nb);
+    hipLaunchKernelGGL((scan_down_kernel<1, true>), dim3((unsigned)nb), dim3(kWG), 0, s, (void*)(offs + a), m,
+                       (const int64_t*)partials, status);
+  }
   return hipGetLastError();
 }
 

@@ -118,6 +118,13 @@ static int64_t hash_node(int64_t h, const Plan& p, int32_t idx) {
 
 static int32_t bitmap_bytes(int64_t n) { return (int32_t)(((n + 63) / 64) * 8); }
 
+// Array element flags (OP_LIST / OP_MAP parts): bit0 nullable, bit1 bool, bit2
+// string/binary (8-byte (offset, size) slot + padded bytes after the fixed part).
+static int32_t elem_flags(const Node& it) {
+  return (it.nullable ? 1 : 0) | (it.kind == KIND_BOOL ? 2 : 0) | (it.kind == KIND_BYTES ? 4 : 0);
+}
+static int32_t elem_width(const Node& it) { return it.kind == KIND_BYTES ? 8 : it.width; }
+
 static int compile_field(const Plan& p, int32_t idx, int32_t ordinal, std::vector<Op>* prog,
                          std::string* err) {
   const Node& nd = p.nodes[idx];
@@ -167,13 +174,16 @@ static int compile_field(const Plan& p, int32_t idx, int32_t ordinal, std::vecto
         (*prog)[begin].e = (int32_t)prog->size();
         return FORY_OK;
       }
-      if (it.kind != KIND_FIXED && it.kind != KIND_BOOL) {
-        *err = "device path supports list<fixed-width> only (got element type id " +
+      if (it.kind != KIND_FIXED && it.kind != KIND_BOOL && it.kind != KIND_BYTES) {
+        *err = "device path supports list<fixed-width | string | binary | struct> only (got element type id " +
                std::to_string(it.type_id) + ")";
         return FORY_ERR_UNSUPPORTED;
       }
-      int32_t iflags = (it.nullable ? 1 : 0) | (it.kind == KIND_BOOL ? 2 : 0);
-      prog->push_back({OP_LIST, ordinal, idx, item, flags, it.width | (iflags << 8)});
+      // string/binary elements: 8-byte (offset, size) element slots, the bytes appended
+      // after the array's fixed part (BinaryArrayWriter elemSize 8, :75-85; write(int,
+      // String) through writeUnaligned, BinaryWriter.java:162-194)
+      const int32_t iflags = elem_flags(it);
+      prog->push_back({OP_LIST, ordinal, idx, item, flags, elem_width(it) | (iflags << 8)});
       return FORY_OK;
     }
     case KIND_MAP: {  // serializeForMap (BaseBinaryEncoderBuilder.java:370-427)
@@ -184,14 +194,15 @@ static int compile_field(const Plan& p, int32_t idx, int32_t ordinal, std::vecto
         *err = "Map's keys must be non-nullable";  // DataTypes.mapField (DataTypes.java:419)
         return FORY_ERR_ENCODER;
       }
-      if ((k.kind != KIND_FIXED && k.kind != KIND_BOOL) || (v.kind != KIND_FIXED && v.kind != KIND_BOOL)) {
-        *err = "device path supports map<fixed-width, fixed-width> only (got key type id " +
+      auto scalar = [](const Node& x) { return x.kind == KIND_FIXED || x.kind == KIND_BOOL || x.kind == KIND_BYTES; };
+      if (!scalar(k) || !scalar(v)) {
+        *err = "device path supports map keys/values of fixed width, string or binary only (got key type id " +
                std::to_string(k.type_id) + ", value type id " + std::to_string(v.type_id) + ")";
         return FORY_ERR_UNSUPPORTED;
       }
-      const int32_t kf = k.kind == KIND_BOOL ? 2 : 0;
-      const int32_t vf = (v.nullable ? 1 : 0) | (v.kind == KIND_BOOL ? 2 : 0);
-      prog->push_back({OP_MAP, ordinal, idx, key, flags, k.width | (v.width << 8) | (kf << 16) | (vf << 24)});
+      const int32_t kf = elem_flags(k), vf = elem_flags(v);
+      prog->push_back({OP_MAP, ordinal, idx, key, flags,
+                       elem_width(k) | (elem_width(v) << 8) | (kf << 16) | (vf << 24)});
       return FORY_OK;
     }
   }

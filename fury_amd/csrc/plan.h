@@ -54,6 +54,7 @@ enum OpCode : int32_t {
   OP_LIST = 4,         // a=ordinal b=col c=item col d=flags e=item width | item flags<<8
   OP_MAP = 5,          // a=ordinal b=col c=key col (value col = c+1) d=flags
                        // e=key width | value width<<8 | key flags<<16 | value flags<<24
+                       // item flags: bit0 nullable, bit1 bool, bit2 string/binary (width 8)
   OP_LIST_STRUCT = 6,  // list<struct of fixed fields>: a=ordinal b=list col c=struct col
                        // d=list flags | struct nullable<<2, e=pc after the element fields;
                        // followed by one OP_FIXED per struct field (a=child ordinal)

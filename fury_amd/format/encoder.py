@@ -158,27 +158,38 @@ class RowEncoder:
         if offsets is None:
             raise ValueError("varlen schema: row offsets are required to decode")
         native.decode_sizes(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
-        var_idx = [i for i, f in enumerate(fields)
-                   if f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP)]
+        var_idx = [i for i, f in enumerate(fields) if i not in item_of and
+                   f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP)]
         totals = {}
         if var_idx and n > 0:
             last = torch.stack([cols[i].offsets[n] for i in var_idx]).cpu().tolist()
             totals = dict(zip(var_idx, last))
         native.read_status(status)
+        elem_bytes = []  # string/binary list elements / map keys+values: sized by a second pass
         for i in var_idx:
             tot = int(totals.get(i, 0))
             f = fields[i]
             if f.type.id in (ArrowType.LIST, ArrowType.MAP):
                 for k in sub[i]:
                     it = fields[k]
-                    vals = None if it.type.id == ArrowType.STRUCT else \
-                        torch.empty(max(1, tot), dtype=_torch_dtype(it.type.id), device=self.device)
+                    vals, offs = None, None
+                    if it.type.id in (ArrowType.STRING, ArrowType.BINARY):
+                        offs = torch.zeros(tot + 1, dtype=torch.int32, device=self.device)
+                        elem_bytes.append(k)
+                    elif it.type.id != ArrowType.STRUCT:
+                        vals = torch.empty(max(1, tot), dtype=_torch_dtype(it.type.id), device=self.device)
                     cols[k] = DeviceColumn(
-                        vals, None,
+                        vals, offs,
                         torch.zeros(_validity_bytes(tot), dtype=torch.uint8, device=self.device)
                         if it.nullable else None, tot)
             else:
                 cols[i].values = torch.empty(max(1, tot), dtype=torch.uint8, device=self.device)
+        if elem_bytes:
+            native.decode_sizes(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
+            last = torch.stack([cols[k].offsets[cols[k].length] for k in elem_bytes]).cpu().tolist()
+            native.read_status(status)
+            for k, tot in zip(elem_bytes, last):
+                cols[k].values = torch.empty(max(1, int(tot)), dtype=torch.uint8, device=self.device)
         native.decode(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
         native.read_status(status)
         return cols

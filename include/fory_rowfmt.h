@@ -198,9 +198,18 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols,
  * top-level fields are all fixed/string/binary/list, decode_sizes writes
  * tile-start prefixes at offsets[64*k] and decode fills the records in
  * between): pass the same rows, row offsets and column arrays to both calls
- * and do not modify `offsets` in between. The device path supports list
- * elements and map keys/values of fixed width only (FORY_ERR_UNSUPPORTED at
- * plan creation otherwise).
+ * and do not modify `offsets` in between.
+ *
+ * String/binary list elements and map keys/values (columns indexed by element):
+ * their offsets array has (element total + 1) entries, known only after a first
+ * decode_sizes. Pass such a column with offsets = NULL to the first call (it
+ * is skipped), then allocate offsets (length = the container's element total,
+ * offsets[length] of the container column) and call decode_sizes again: the
+ * second call also writes the element sizes and scans them (element
+ * offsets[length] = total bytes). The device path supports list elements of
+ * fixed width, string, binary or struct-of-fixed-width, and map keys/values of
+ * fixed width, string or binary (FORY_ERR_UNSUPPORTED at plan creation
+ * otherwise).
  *
  * fory_rowfmt_decode: writes values/offsets/validity of out_cols. Null
  * values decode to 0 (RowEncoderBuilder.java:239-246 leaves the Java default).

@@ -76,7 +76,7 @@ def main():
 
     from fury_amd.format.types import DataType, DataTypes, Field, Schema
     sys.path.insert(0, os.path.join(REPO, "tests"))
-    from helpers import deep_nested_schema, list_struct_schema, maps_schema
+    from helpers import deep_nested_schema, list_struct_schema, maps_schema, string_elems_schema
 
     edge = {
         "empty": Schema([]),
@@ -91,6 +91,7 @@ def main():
         "maps": maps_schema(),
         "deep_nested": deep_nested_schema(),
         "list_struct": list_struct_schema(),
+        "string_elems": string_elems_schema(),
     }
     schemas = {"struct104": W.struct_schema(), "mixed40": W.mixed_schema(),
                "nested": W.nested_schema(), **edge}

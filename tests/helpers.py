@@ -264,6 +264,61 @@ def list_struct_rows(n: int, seed: int):
     return rows
 
 
+def string_elems_schema() -> Schema:
+    """List<String>, List<byte[]>, Map<String, String>, Map<String, Integer> inside a
+    nullable bean, Map<Long, byte[]>: string/binary array elements and map keys/values
+    (BinaryArrayWriter with 8-byte (offset, size) element slots)."""
+    return Schema([
+        Field("id", DataType(ArrowType.INT64), False),
+        DataTypes.array_field("names", Field("item", DataType(ArrowType.STRING), True)),
+        DataTypes.array_field("blobs", Field("item", DataType(ArrowType.BINARY), False)),
+        DataTypes.map_field("attrs", Field("key", DataType(ArrowType.STRING), False),
+                            Field("value", DataType(ArrowType.STRING), True)),
+        DataTypes.struct_field("s", True, [
+            DataTypes.map_field("idx", Field("key", DataType(ArrowType.STRING), False),
+                                Field("value", DataType(ArrowType.INT32), True)),
+            Field("z", DataType(ArrowType.INT16), False),
+        ]),
+        DataTypes.map_field("codes", Field("key", DataType(ArrowType.INT64), False),
+                            Field("value", DataType(ArrowType.BINARY), True)),
+    ])
+
+
+def string_elems_rows(n: int, seed: int):
+    """Rows of string_elems_schema: null / empty containers, null elements and values,
+    empty and multi-byte UTF-8 strings, one container in ten beyond 64 elements."""
+    rng = np.random.default_rng(seed)
+    alphabet = "abcdefghijklmnopqrstuvwxyz0123456789 éü中文"
+
+    def text(k=20):
+        return "".join(alphabet[int(x)] for x in rng.integers(0, len(alphabet), size=rng.integers(0, k)))
+
+    def count():
+        return int(rng.integers(0, 70)) if rng.random() < 0.1 else int(rng.integers(0, 6))
+
+    def smap(val, null_p=0.1):
+        if rng.random() < null_p:
+            return None
+        return {f"{text(6)}#{j}": (None if rng.random() < 0.15 else val()) for j in range(count())}
+
+    rows = []
+    for _ in range(n):
+        rows.append({
+            "id": int(rng.integers(-2**62, 2**62)),
+            "names": None if rng.random() < 0.1 else [None if rng.random() < 0.15 else text() for _ in range(count())],
+            "blobs": None if rng.random() < 0.1 else [bytes(rng.integers(0, 256, size=rng.integers(0, 30),
+                                                                         dtype=np.uint8)) for _ in range(count())],
+            "attrs": smap(lambda: text(40)),
+            "s": None if rng.random() < 0.2 else {"idx": smap(lambda: int(rng.integers(-2**31, 2**31))),
+                                                  "z": int(rng.integers(-999, 999))},
+            "codes": None if rng.random() < 0.1 else {
+                int(k): (None if rng.random() < 0.2 else bytes(rng.integers(0, 256, size=rng.integers(0, 12),
+                                                                             dtype=np.uint8)))
+                for k in rng.choice(10**6, size=count(), replace=False)},
+        })
+    return rows
+
+
 def list_struct_schema() -> Schema:
     bean = DataTypes.struct_field("item", True, [
         Field("a", DataType(ArrowType.INT32), False),
@@ -296,6 +351,8 @@ def catalog():
         "maps": (maps_schema(), lambda n, s: build_columns(maps_schema(), maps_rows(n, s))),
         "list_struct": (list_struct_schema(),
                         lambda n, s: build_columns(list_struct_schema(), list_struct_rows(n, s))),
+        "string_elems": (string_elems_schema(),
+                         lambda n, s: build_columns(string_elems_schema(), string_elems_rows(n, s))),
     }
 
 
@@ -319,7 +376,8 @@ def _struct_parents(schema: Schema):
 
 def collection_cases(n=300, seed=5):
     """One-field schemas of the standalone collection encoders (Encoders.arrayEncoder /
-    mapEncoder) and their rows: list<Long>, List<Bean>, Map<Integer, Long>."""
+    mapEncoder) and their rows: list<Long>, List<Bean>, Map<Integer, Long>, List<String>,
+    Map<String, String>."""
     rng = np.random.default_rng(seed)
 
     def bean():
@@ -329,6 +387,8 @@ def collection_cases(n=300, seed=5):
     longs = Schema([DataTypes.array_field("", Field("item", DataType(ArrowType.INT64), True))])
     beans = Schema([list_struct_schema().fields[1]])
     amap = Schema([maps_schema().fields[1]])
+    names = Schema([string_elems_schema().fields[1]])
+    attrs = Schema([string_elems_schema().fields[3]])
     out = []
     for schema, gen in [
         (longs, lambda: {"": [None if rng.random() < 0.1 else int(x) for x in rng.integers(-9, 9, size=rng.integers(0, 70))]}),
@@ -337,5 +397,10 @@ def collection_cases(n=300, seed=5):
                                    for k in rng.choice(1000, size=rng.integers(0, 9), replace=False)}}),
     ]:
         rows = [gen() for _ in range(n)]
+        out.append((schema, build_columns(schema, rows)))
+    # List<String> / Map<String, String> collections
+    for schema, key in ((names, "names"), (attrs, "attrs")):
+        empty = [] if key == "names" else {}
+        rows = [{key: empty if r[key] is None else r[key]} for r in string_elems_rows(n, seed)]
         out.append((schema, build_columns(schema, rows)))
     return out

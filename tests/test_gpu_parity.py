@@ -143,7 +143,8 @@ def test_collection_frame_parity(n, varlen_engine):
 
 
 @pytest.mark.parametrize("shift", [4, 8, 12])
-@pytest.mark.parametrize("name", ["mixed40_nulls", "flat_mix", "nested_nulls", "deep_nested", "maps", "list_struct"])
+@pytest.mark.parametrize("name", ["mixed40_nulls", "flat_mix", "nested_nulls", "deep_nested", "maps", "list_struct",
+                                  "string_elems"])
 def test_varlen_unaligned_buffers(name, shift, varlen_engine):
     """Rows written to / read from buffers at a 4-byte (not 16-byte) aligned address."""
     schema, make = catalog()[name]
