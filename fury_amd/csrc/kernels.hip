@@ -2279,7 +2279,12 @@ __global__ __launch_bounds__(64) void var_decode_tile_kernel(VarLaunch L, const 
 
 // Waves that place var fields in the encode tile kernel: waves 1..NW-1 (wave 0
 // lays the rows out) when every field gets a wave of its own, else all NW.
-__host__ __device__ __forceinline__ int var_placers(int num_var, int nw) { return num_var < nw ? nw - 1 : nw; }
+// Waves that place var payloads in the encode tile kernel: all NW when num_var >= NW
+// (wave 0 takes its fields after the layout); FORY_ROWFMT_VARPL=0 keeps wave 0 to
+// the layout (waves 1..NW-1 place everything: Mixed encode 6.42 -> 6.77 ms, so off).
+__host__ __device__ __forceinline__ int var_placers(int num_var, int nw, int pl_all) {
+  return pl_all && num_var >= nw ? nw : nw - 1;
+}
 
 __device__ __forceinline__ void wave_lds_sync() {
   // LDS ops of one wave execute in order; keep the compiler from reordering.
@@ -2631,7 +2636,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // var placement: up to 3 fields per wave stay off wave 0 (it lays the rows out)
-  const int nplc = var_placers(L.num_var, NW);
+  const int nplc = var_placers(L.num_var, NW, L.pl_all);
   const int pi = nplc < NW ? wave - 1 : (wave + NW - 1) % NW;  // placer index (-1: none)
   const int nslot = L.num_var < nplc ? L.num_var : nplc;  // staging slots: one per placing wave
   int32_t* pos = reinterpret_cast<int32_t*>(lds + cap + nslot * stg_bytes);  // [num_var][64]
@@ -3728,7 +3733,7 @@ size_t flat_lds(const VarLaunch& L, int cap, int nw) {
 
 // Encode: staging only for the min(NW, num_var) waves that place var fields.
 size_t flat_lds_enc(const VarLaunch& L, int cap, int nw) {
-  const int np = var_placers(L.num_var, nw);
+  const int np = var_placers(L.num_var, nw, L.pl_all);
   const int nslot = L.num_var < np ? L.num_var : np;
   return (size_t)cap + (size_t)nslot * L.stg_bytes + (size_t)L.num_var * 64 * sizeof(int32_t) + sbase_lds(L);
 }
@@ -3755,15 +3760,15 @@ int enc_stg_bytes(K* k, const VarLaunch& L, int64_t capacity, int cap, int nw) {
     return blocks;
   };
   // memo of the last answer per instantiation (same plan shape -> same answer)
-  static int m_cap = -1, m_b = -1, m_nv = -1, m_ns = -1, m_res = 2048;
-  if (m_cap == cap && m_b == b && m_nv == L.num_var && m_ns == L.num_struct) return m_res;
+  static int m_cap = -1, m_b = -1, m_nv = -1, m_ns = -1, m_pl = -1, m_res = 2048;
+  if (m_cap == cap && m_b == b && m_nv == L.num_var && m_ns == L.num_struct && m_pl == L.pl_all) return m_res;
   const int want = occ(2048);
   int r = 2048;
   if (want > 0) {
     r = b;
     while (r > 2048 && occ(r) < want) r -= 256;
   }
-  m_cap = cap, m_b = b, m_nv = L.num_var, m_ns = L.num_struct, m_res = r;
+  m_cap = cap, m_b = b, m_nv = L.num_var, m_ns = L.num_struct, m_pl = L.pl_all, m_res = r;
   return r;
 }
 
@@ -3829,7 +3834,9 @@ void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, i
   auto* k = &var_encode_flat_kernel<FRAME, NW, PROF, false>;
   var_tile_launch(k, L0, cap);
   VarLaunch L = L0;
-  L.stg_bytes = enc_stg_bytes(k, L0, capacity, cap, NW);
+  const char* pl = getenv("FORY_ROWFMT_VARPL");
+  L.pl_all = pl ? atoi(pl) : 1;
+  L.stg_bytes = enc_stg_bytes(k, L, capacity, cap, NW);
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds_enc(L, cap, NW), s, L, L.prog,
                      L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, cap, sp);
   auto* k2 = &var_encode_flat_kernel<FRAME, NW, PROF, true>;
