@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libfory_rowfmt.so")
+# FORY_ROWFMT_LIB: another build of the same library (A/B of two builds on one box)
+LIB_PATH = os.environ.get("FORY_ROWFMT_LIB") or os.path.join(_HERE, "lib", "libfory_rowfmt.so")
 
 # fory_status (include/fory_rowfmt.h)
 FORY_OK = 0

@@ -2644,6 +2644,46 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
   auto body = [&](int64_t tile) {
   FLAT_STAMP(0);
   const int64_t r0 = tile * 64;
+  const int64_t i = r0 + lane;
+  const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
+  const bool lv = lane < rows;  // == live below
+  // Item ranges this wave needs, loaded BEFORE the row bounds (they do not depend on
+  // them) so the two round trips overlap: the first var field it places, its later
+  // fields, and (wave 0 of a struct-free plan) the layout's first batch of var fields.
+  const int v_first = pi < 0 ? L.num_var : pi;
+  int64_t pf_e0 = 0, pf_e1 = 0;
+  if (wave != 0 && v_first < L.num_var) {
+    const VarFieldDev& f = vf[v_first];
+    const int64_t ee = f.offsets[r0 + rows];
+    pf_e0 = lv ? f.offsets[i] : ee;
+    pf_e1 = lv ? f.offsets[i + 1] : ee;
+  }
+  constexpr int kPre = 3;
+  int64_t pe0[kPre], pe1[kPre];
+#pragma unroll
+  for (int k = 0; k < kPre; ++k) {
+    const int v = v_first + (k + 1) * nplc;
+    pe0[k] = pe1[k] = 0;
+    if (v < L.num_var) {
+      const VarFieldDev& f = vf[v];
+      const int64_t ee = f.offsets[r0 + rows];
+      pe0[k] = lv ? f.offsets[i] : ee;
+      pe1[k] = lv ? f.offsets[i + 1] : ee;
+    }
+  }
+  const bool pre_layout = wave == 0 && !L.num_struct && L.num_var > 0;
+  int64_t le0[kFixBatch], le1[kFixBatch];
+  uint32_t lvb[kFixBatch];
+  if (pre_layout) {
+    const int64_t ii = lv ? i : 0;
+#pragma unroll
+    for (int k = 0; k < kFixBatch; ++k) {
+      const VarFieldDev& f = vf[min(k, L.num_var - 1)];
+      le0[k] = f.offsets[ii];
+      le1[k] = f.offsets[ii + 1];
+      lvb[k] = f.validity ? load_byte(f.validity + (ii >> 3)) : 0xffu;
+    }
+  }
   int64_t B0, B1, beg, end;
   bool live;
   const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
@@ -2662,39 +2702,18 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
     if (wave == 0 && live) enc_record(L, prog, cols, r0 + lane, out + beg, end - beg);
     return;
   }
-  const int64_t i = r0 + lane;
-  const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
   uint8_t* fp = img + mis + (int)(beg - B0);
   uint8_t* row = fp + HDR;
   uint8_t* slots = row + L.bitmap_bytes;
   // var field v is placed by wave (v + 1) % NW: wave 0 lays the rows out while
   // the other waves' first record groups stream into staging (LDS-DMA)
-  const int v_first = pi < 0 ? L.num_var : pi;
   uint8_t* stg = lds + cap + (pi < 0 ? 0 : pi) * stg_bytes;
   int pf_hi = 0, pf_phase = 0, pf_vofs = 0;
   bool pf_fits = false;
-  int64_t pf_e0 = 0, pf_e1 = 0;
   if (wave != 0 && v_first < L.num_var) {
     const VarFieldDev& f = vf[v_first];
-    const int64_t ee = f.offsets[r0 + rows];
-    pf_e0 = live ? f.offsets[i] : ee;
-    pf_e1 = live ? f.offsets[i + 1] : ee;
     pf_hi = flat_group(f, pf_e0, pf_e1, 0, rows, lane, stg_bytes, &pf_fits);
     if (pf_fits) flat_stage_span(f, __shfl(pf_e0, 0), __shfl(pf_e1, pf_hi - 1), lane, stg, &pf_phase, &pf_vofs);
-  }
-  // item ranges of this wave's later var fields, loaded before the layout barrier
-  constexpr int kPre = 3;
-  int64_t pe0[kPre], pe1[kPre];
-#pragma unroll
-  for (int k = 0; k < kPre; ++k) {
-    const int v = v_first + (k + 1) * nplc;
-    pe0[k] = pe1[k] = 0;
-    if (v < L.num_var) {
-      const VarFieldDev& f = vf[v];
-      const int64_t ee = f.offsets[r0 + rows];
-      pe0[k] = live ? f.offsets[i] : ee;
-      pe1[k] = live ? f.offsets[i + 1] : ee;
-    }
   }
   FLAT_STAMP(1);
   if (wave == 0) {
@@ -2731,6 +2750,12 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
       const int64_t ii = live ? i : 0;
 #pragma unroll
       for (int k = 0; k < kFixBatch; ++k) {
+        if (v0 == 0) {  // loaded before the row bounds
+          e0[k] = le0[k];
+          e1[k] = le1[k];
+          vb[k] = lvb[k];
+          continue;
+        }
         const VarFieldDev& f = vf[min(v0 + k, L.num_var - 1)];
         e0[k] = f.offsets[ii];
         e1[k] = f.offsets[ii + 1];
