@@ -387,6 +387,32 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   return FORY_OK;
 }
 
+// Mean row/frame bytes of a decode batch, for the tile image size of the flat decode
+// kernels (fit_cap), estimated from the output capacities the caller sized from
+// decode_sizes (string bytes, list items): fixed part + child rows + per var field
+// its mean payload and padding. No device read. 0 (static estimate) when a capacity
+// is missing or the batch is small.
+int64_t decode_mean_row(const Plan& p, const fory_amd::VarLaunch& L, const fory_column* cols, int64_t n, int frame) {
+  if (!L.flat || n < 4096 || !cols) return 0;
+  double row = p.fixed_size + (frame ? 12 : 0);
+  for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
+    const fory_amd::Node& nd = p.nodes[idx];
+    if (nd.kind == fory_amd::KIND_STRUCT) {
+      row += ((nd.children.size() + 63) / 64) * 8.0 + 8.0 * nd.children.size();
+    } else if (nd.kind == fory_amd::KIND_BYTES) {
+      if (cols[idx].capacity <= 0) return 0;
+      row += (double)cols[idx].capacity / n + 3.5;  // + mean zero padding to 8
+    } else if (nd.kind == fory_amd::KIND_LIST) {
+      const int32_t item = nd.children[0];
+      const int w = p.nodes[item].width > 0 ? p.nodes[item].width : 8;
+      if (cols[item].capacity <= 0) return 0;
+      const double items = (double)cols[item].capacity / w / n;
+      row += 8 + 8.0 * ((int64_t)items / 64 + 1) + items * w + 3.5;
+    }
+  }
+  return (int64_t)row;
+}
+
 int64_t* partials_ptr(const Plan& p, void* ws) {
   return reinterpret_cast<int64_t*>(static_cast<uint8_t*>(ws) + table_bytes(p));
 }
@@ -640,6 +666,7 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows, const int64_t*
   fory_amd::VarLaunch L{};
   rc = prepare_var(p, out_cols, num_rows, frame_mode, d_workspace, s, &L);
   if (rc) return rc;
+  L.mean_row = decode_mean_row(p, L, out_cols, num_rows, frame_mode);
   e = fory_amd::launch_var_decode(L, static_cast<const uint8_t*>(d_rows), d_row_offsets, d_status, s);
   return e == hipSuccess ? FORY_OK : hip_fail(e, "var_decode");
 }

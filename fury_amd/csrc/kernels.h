@@ -68,6 +68,7 @@ struct VarLaunch {
   uint64_t* prof;               // debug (FORY_ROWFMT_VARPROF): 8 timestamps per tile, else null
   int32_t* spill;               // workspace: tiles spilled to the big-image launch (ceil(n/64))
   int32_t* spill_count;         // workspace: number of spilled tiles
+  int64_t mean_row;             // decode: mean row/frame bytes of the batch (tile image sizing), 0 = unknown
   int32_t pl_all;               // encode tile kernel: wave 0 places var payloads too (A/B)
   int32_t level2;               // decode lengths pass 2: sizes of string/binary list/map
                                 // elements (container offsets already scanned)

@@ -3705,6 +3705,19 @@ int var_cap(const VarLaunch& L) {
   return cap < 1024 ? 1024 : (cap > 160 * 1024 ? 160 * 1024 : cap);
 }
 
+// Tile image of the cooperative kernels from the batch's mean row (bytes per row or
+// frame): 64 rows + 4 % + the 16-B phase, 256-B granular, in [4, 64] KiB. Tiles
+// above it go to the spill launch; the image is the largest LDS item, so sizing it
+// to the data instead of the plan's static estimate is what sets the resident
+// workgroups per CU (Mixed: 37 KiB static -> 32 KiB, 3 -> 4 workgroups per CU).
+int fit_cap(const VarLaunch& L, int64_t mean_row) {
+  if (getenv("FORY_ROWFMT_VARCAP") || getenv("FORY_ROWFMT_VARFIT") || mean_row <= 0 || L.num_rows < 64)
+    return var_cap(L);
+  int64_t need = (64 * mean_row * 104 / 100 + 16 + 255) & ~int64_t(255);
+  need = need < 4096 ? 4096 : (need > 64 * 1024 ? 64 * 1024 : need);
+  return (int)need;
+}
+
 template <typename K>
 void var_tile_launch(K* k, const VarLaunch&, int) {
   static bool init = false;  // one per kernel instantiation
@@ -3787,11 +3800,17 @@ int enc_stg_bytes(K* k, const VarLaunch& L, int64_t capacity, int cap, int nw) {
   // memo of the last answer per instantiation (same plan shape -> same answer)
   static int m_cap = -1, m_b = -1, m_nv = -1, m_ns = -1, m_pl = -1, m_res = 2048;
   if (m_cap == cap && m_b == b && m_nv == L.num_var && m_ns == L.num_struct && m_pl == L.pl_all) return m_res;
-  const int want = occ(2048);
-  int r = 2048;
+  // the most resident workgroups any slot size in [1, 2] KiB reaches, then the
+  // largest slot (up to b) that keeps them
+  int want = -1;
+  for (int t = 2048; t >= 1024; t -= 256) {
+    const int o = occ(t);
+    want = o > want ? o : want;
+  }
+  int r = 1024;
   if (want > 0) {
     r = b;
-    while (r > 2048 && occ(r) < want) r -= 256;
+    while (r > 1024 && occ(r) < want) r -= 256;
   }
   m_cap = cap, m_b = b, m_nv = L.num_var, m_ns = L.num_struct, m_pl = L.pl_all, m_res = r;
   return r;
@@ -3841,27 +3860,59 @@ int dec_stg_bytes(K* k, const VarLaunch& L, int cap, int nw) {
   };
   static int m_cap = -1, m_b = -1, m_nv = -1, m_ns = -1, m_res = 2048;
   if (m_cap == cap && m_b == b && m_nv == L.num_var && m_ns == L.num_struct) return m_res;
-  const int want = occ(2048);
-  int r = 2048;
+  // the most resident workgroups any slot size in [1, 2] KiB reaches, then the
+  // largest slot (up to b) that keeps them
+  int want = -1;
+  for (int t = 2048; t >= 1024; t -= 256) {
+    const int o = occ(t);
+    want = o > want ? o : want;
+  }
+  int r = 1024;
   if (want > 0) {
     r = b;
-    while (r > 2048 && occ(r) < want) r -= 256;
+    while (r > 1024 && occ(r) < want) r -= 256;
   }
   m_cap = cap, m_b = b, m_nv = L.num_var, m_ns = L.num_struct, m_res = r;
   return r;
 }
 
+// Grows a data-fitted tile image (fit_cap) in 256-B steps, up to +20 %, while the
+// resident workgroups per CU stay the same: spill margin that costs no occupancy.
+// Memoised per kernel instantiation (same inputs -> same answer).
+template <typename K, typename F>
+int grow_cap(K* k, int threads, int cap, int key, F lds_of) {
+  if (getenv("FORY_ROWFMT_VARCAP") || getenv("FORY_ROWFMT_VARFIT")) return cap;
+  static int m_cap = -1, m_key = -1, m_res = 0;
+  if (m_cap == cap && m_key == key) return m_res;
+  auto occ = [&](int c) {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(k), threads, lds_of(c)) !=
+        hipSuccess)
+      return -1;
+    return b;
+  };
+  const int b0 = occ(cap);
+  int c = cap;
+  const int limit = cap * 6 / 5 < 64 * 1024 ? cap * 6 / 5 : 64 * 1024;
+  if (b0 > 0)
+    while (c + 256 <= limit && occ(c + 256) >= b0) c += 256;
+  m_cap = cap, m_key = key, m_res = c;
+  return c;
+}
+
 template <bool FRAME, int NW, bool PROF>
 void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                        int cap, hipStream_t s) {
-  const SpillArgs sp = spill_args(L0, cap);
-  (void)hipMemsetAsync(L0.spill_count, 0, sizeof(int32_t), s);
   auto* k = &var_encode_flat_kernel<FRAME, NW, PROF, false>;
   var_tile_launch(k, L0, cap);
   VarLaunch L = L0;
   const char* pl = getenv("FORY_ROWFMT_VARPL");
   L.pl_all = pl ? atoi(pl) : 1;
   L.stg_bytes = enc_stg_bytes(k, L, capacity, cap, NW);
+  cap = grow_cap(k, 64 * NW, cap, L.stg_bytes * 4096 + L.num_var * 64 + L.num_struct,
+                 [&](int c) { return flat_lds_enc(L, c, NW); });
+  const SpillArgs sp = spill_args(L, cap);
+  (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds_enc(L, cap, NW), s, L, L.prog,
                      L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, cap, sp);
   auto* k2 = &var_encode_flat_kernel<FRAME, NW, PROF, true>;
@@ -3881,12 +3932,15 @@ void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int6
 template <bool FRAME, bool WRITE, int NW>
 void launch_flat_dec(const VarLaunch& L0, const uint8_t* rows, const int64_t* offs, int64_t* tile_tot,
                      int32_t* status, int cap, hipStream_t s) {
-  const SpillArgs sp = spill_args(L0, cap);
-  (void)hipMemsetAsync(L0.spill_count, 0, sizeof(int32_t), s);
   auto* k = &var_decode_flat_kernel<FRAME, WRITE, NW, false>;
   var_tile_launch(k, L0, cap);
   VarLaunch L = L0;
   if (WRITE) L.stg_bytes = dec_stg_bytes(k, L0, cap, NW);
+  if (WRITE && L.mean_row > 0)
+    cap = grow_cap(k, 64 * NW, cap, L.stg_bytes * 4096 + L.num_var * 64 + L.num_struct,
+                   [&](int c) { return flat_lds_dec(L, c, NW); });
+  const SpillArgs sp = spill_args(L, cap);
+  (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
   const size_t lds = WRITE ? flat_lds_dec(L, cap, NW) : (size_t)cap + sbase_lds(L);  // pass 1: row image (+ struct offsets)
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
                      L.vf, L.st, rows, offs, tile_tot, status, cap, sp);
@@ -3898,15 +3952,10 @@ void launch_flat_dec(const VarLaunch& L0, const uint8_t* rows, const int64_t* of
 }
 
 // Encode: the caller's capacity (normally encoded_size's total) gives the mean
-// row size for free; the image holds 64 of them + 15 % unless the plan's
-// static estimate is larger (capped at 64 KiB).
+// row size for free (fit_cap).
 int enc_cap(const VarLaunch& L, int64_t capacity) {
-  int cap = var_cap(L);
-  if (getenv("FORY_ROWFMT_VARCAP") || L.num_rows < 64) return cap;
-  const int64_t mean = capacity / L.num_rows;
-  const int64_t hint = (64 * mean * 115 / 100 + 1023) / 1024 * 1024;
-  if (hint > cap) cap = (int)(hint < 64 * 1024 ? hint : 64 * 1024);
-  return cap;
+  if (L.num_rows < 64) return var_cap(L);
+  return fit_cap(L, capacity / L.num_rows);
 }
 
 hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity,
@@ -3948,7 +3997,7 @@ hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const
                                   int32_t* status, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
   if (var_tiles() && var_flat(L)) {
-    const int cap = var_cap(L);
+    const int cap = fit_cap(L, L.mean_row);
     const int nw = flat_nw();
     if (L.frame) {
       if (nw == 8) launch_flat_dec<true, WRITE, 8>(L, rows, offs, tile_tot, status, cap, s);
