@@ -24,6 +24,8 @@
 // per record, with a device-wide scan for row offsets.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include <cstdint>
 #include <cstdlib>
 
@@ -2622,8 +2624,12 @@ __device__ __forceinline__ void flat_dec_struct_bases(const VarLaunch& L, const 
     if (PROF && tid == 0) L.prof[tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime();            \
   } while (0)
 
+// Encode tile kernel body, compiled as two kernels: the default register budget
+// (Mixed-like plans are LDS-limited at 4 workgroups per CU anyway) and a lean one for
+// 5 waves per SIMD (small-row plans such as Nested are register-limited: encode
+// 1.49 -> 1.26 ms; its spills would cost Mixed 27 %). launch_flat_enc_t picks by occupancy.
 template <bool FRAME, int NW, bool PROF, bool SPILL>
-__global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
+__device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
                                                                   const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
                                                                   const StructDev* __restrict__ st,
                                                                   const int64_t* __restrict__ offs,
@@ -2877,6 +2883,22 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(VarLaunch L, c
     __syncthreads();
   }
 }
+
+#define FORY_VAR_ENC_PARAMS                                                                              \
+  VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,                          \
+      const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,                         \
+      const StructDev* __restrict__ st, const int64_t* __restrict__ offs, uint8_t* __restrict__ out,    \
+      int64_t capacity, int32_t* status, int cap, SpillArgs sp
+template <bool FRAME, int NW, bool PROF, bool SPILL>
+__global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(FORY_VAR_ENC_PARAMS) {
+  var_encode_flat_body<FRAME, NW, PROF, SPILL>(L, prog, cols, fix, vf, st, offs, out, capacity, status, cap, sp);
+}
+template <bool FRAME, int NW, bool PROF, bool SPILL>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(5, 8))) void var_encode_flat_lean_kernel(
+    FORY_VAR_ENC_PARAMS) {
+  var_encode_flat_body<FRAME, NW, PROF, SPILL>(L, prog, cols, fix, vf, st, offs, out, capacity, status, cap, sp);
+}
+#undef FORY_VAR_ENC_PARAMS
 
 
 __device__ __forceinline__ int64_t wave_incl_scan64(int64_t x, int lane) {
@@ -3720,8 +3742,13 @@ int fit_cap(const VarLaunch& L, int64_t mean_row) {
 
 template <typename K>
 void var_tile_launch(K* k, const VarLaunch&, int) {
-  static bool init = false;  // one per kernel instantiation
-  if (!init) { raise_lds_cap(k); init = true; }
+  // once per kernel (kernels of one signature share this instantiation)
+  static const void* done[16] = {};
+  static int nd = 0;
+  for (int i = 0; i < nd; ++i)
+    if (done[i] == reinterpret_cast<const void*>(k)) return;
+  raise_lds_cap(k);
+  if (nd < 16) done[nd++] = reinterpret_cast<const void*>(k);
 }
 
 uint64_t* g_prof = nullptr;
@@ -3798,8 +3825,11 @@ int enc_stg_bytes(K* k, const VarLaunch& L, int64_t capacity, int cap, int nw) {
     return blocks;
   };
   // memo of the last answer per instantiation (same plan shape -> same answer)
+  static const void* m_k = nullptr;
   static int m_cap = -1, m_b = -1, m_nv = -1, m_ns = -1, m_pl = -1, m_res = 2048;
-  if (m_cap == cap && m_b == b && m_nv == L.num_var && m_ns == L.num_struct && m_pl == L.pl_all) return m_res;
+  if (m_k == (const void*)k && m_cap == cap && m_b == b && m_nv == L.num_var && m_ns == L.num_struct &&
+      m_pl == L.pl_all)
+    return m_res;
   // the most resident workgroups any slot size in [1, 2] KiB reaches, then the
   // largest slot (up to b) that keeps them
   int want = -1;
@@ -3812,7 +3842,7 @@ int enc_stg_bytes(K* k, const VarLaunch& L, int64_t capacity, int cap, int nw) {
     r = b;
     while (r > 1024 && occ(r) < want) r -= 256;
   }
-  m_cap = cap, m_b = b, m_nv = L.num_var, m_ns = L.num_struct, m_pl = L.pl_all, m_res = r;
+  m_k = (const void*)k, m_cap = cap, m_b = b, m_nv = L.num_var, m_ns = L.num_struct, m_pl = L.pl_all, m_res = r;
   return r;
 }
 
@@ -3882,8 +3912,9 @@ int dec_stg_bytes(K* k, const VarLaunch& L, int cap, int nw) {
 template <typename K, typename F>
 int grow_cap(K* k, int threads, int cap, int key, F lds_of) {
   if (getenv("FORY_ROWFMT_VARCAP") || getenv("FORY_ROWFMT_VARFIT")) return cap;
+  static const void* m_k = nullptr;
   static int m_cap = -1, m_key = -1, m_res = 0;
-  if (m_cap == cap && m_key == key) return m_res;
+  if (m_k == (const void*)k && m_cap == cap && m_key == key) return m_res;
   auto occ = [&](int c) {
     int b = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(k), threads, lds_of(c)) !=
@@ -3896,26 +3927,60 @@ int grow_cap(K* k, int threads, int cap, int key, F lds_of) {
   const int limit = cap * 6 / 5 < 64 * 1024 ? cap * 6 / 5 : 64 * 1024;
   if (b0 > 0)
     while (c + 256 <= limit && occ(c + 256) >= b0) c += 256;
-  m_cap = cap, m_key = key, m_res = c;
+  m_k = (const void*)k, m_cap = cap, m_key = key, m_res = c;
   return c;
+}
+
+// FORY_ROWFMT_VARDIAG=1: the tile kernels' LDS sizing and resulting residency, to stderr.
+template <typename K>
+void var_diag(const char* what, K* k, int threads, int cap, int stg, size_t lds) {
+  static const bool on = getenv("FORY_ROWFMT_VARDIAG") != nullptr;
+  if (!on) return;
+  int b = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(k), threads, lds);
+  fprintf(stderr, "[fory_rowfmt] %s tile kernel: image %d B, staging %d B/slot, LDS %zu B, %d workgroups/CU\n", what,
+          cap, stg, lds, b);
 }
 
 template <bool FRAME, int NW, bool PROF>
 void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                        int cap, hipStream_t s) {
-  auto* k = &var_encode_flat_kernel<FRAME, NW, PROF, false>;
-  var_tile_launch(k, L0, cap);
   VarLaunch L = L0;
   const char* pl = getenv("FORY_ROWFMT_VARPL");
   L.pl_all = pl ? atoi(pl) : 1;
-  L.stg_bytes = enc_stg_bytes(k, L, capacity, cap, NW);
-  cap = grow_cap(k, 64 * NW, cap, L.stg_bytes * 4096 + L.num_var * 64 + L.num_struct,
-                 [&](int c) { return flat_lds_enc(L, c, NW); });
+  // default or lean kernel: whichever keeps more workgroups per CU resident with its
+  // own staging / image sizing (ties: default; FORY_ROWFMT_VARLEAN=0/1 forces)
+  auto* kd = &var_encode_flat_kernel<FRAME, NW, PROF, false>;
+  auto* kl = &var_encode_flat_lean_kernel<FRAME, NW, PROF, false>;
+  var_tile_launch(kd, L0, cap);
+  var_tile_launch(kl, L0, cap);
+  auto size_for = [&](decltype(kd) kk, int* stg, int* c) {
+    VarLaunch T = L;
+    *stg = enc_stg_bytes(kk, T, capacity, cap, NW);
+    T.stg_bytes = *stg;
+    *c = grow_cap(kk, 64 * NW, cap, *stg * 4096 + L.num_var * 64 + L.num_struct,
+                  [&](int x) { return flat_lds_enc(T, x, NW); });
+    T.stg_bytes = *stg;
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(kk), 64 * NW,
+                                                     flat_lds_enc(T, *c, NW)) != hipSuccess)
+      b = 0;
+    return b;
+  };
+  int stg_d = 0, cap_d = cap, stg_l = 0, cap_l = cap;
+  const int occ_d = size_for(kd, &stg_d, &cap_d);
+  const int occ_l = size_for(kl, &stg_l, &cap_l);
+  const char* lean_env = getenv("FORY_ROWFMT_VARLEAN");
+  const bool lean = lean_env ? atoi(lean_env) != 0 : occ_l > occ_d;
+  auto* k = lean ? kl : kd;
+  L.stg_bytes = lean ? stg_l : stg_d;
+  cap = lean ? cap_l : cap_d;
   const SpillArgs sp = spill_args(L, cap);
   (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
+  var_diag(lean ? "encode (lean)" : "encode", k, 64 * NW, cap, L.stg_bytes, flat_lds_enc(L, cap, NW));
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds_enc(L, cap, NW), s, L, L.prog,
                      L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, cap, sp);
-  auto* k2 = &var_encode_flat_kernel<FRAME, NW, PROF, true>;
+  auto* k2 = lean ? &var_encode_flat_lean_kernel<FRAME, NW, PROF, true> : &var_encode_flat_kernel<FRAME, NW, PROF, true>;
   var_tile_launch(k2, L, sp.cap);
   hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds_enc(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
                      flat_lds_enc(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, sp.cap,
@@ -3942,6 +4007,7 @@ void launch_flat_dec(const VarLaunch& L0, const uint8_t* rows, const int64_t* of
   const SpillArgs sp = spill_args(L, cap);
   (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
   const size_t lds = WRITE ? flat_lds_dec(L, cap, NW) : (size_t)cap + sbase_lds(L);  // pass 1: row image (+ struct offsets)
+  var_diag(WRITE ? "decode" : "decode lengths", k, 64 * NW, cap, L.stg_bytes, lds);
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
                      L.vf, L.st, rows, offs, tile_tot, status, cap, sp);
   auto* k2 = &var_decode_flat_kernel<FRAME, WRITE, NW, true>;
