@@ -105,6 +105,15 @@ PROTOTYPES = {
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
          ctypes.POINTER(Column)]),
+    "fory_rowfmt_host_encode_var": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.POINTER(Column), ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64,
+         ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),
+    "fory_rowfmt_host_decode_var_sizes": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+         ctypes.c_void_p]),
+    "fory_rowfmt_host_decode_var": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Column)]),
     "fory_rowfmt_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "fory_rowfmt_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
 }

@@ -465,6 +465,21 @@ int fory_rowfmt_internal_column_layout(const fory_plan* plan, int32_t* width, in
   return FORY_OK;
 }
 
+// kind (FieldKind), width, nullable and parent node (-1: top level) of every pre-order node.
+int fory_rowfmt_internal_node_layout(const fory_plan* plan, int32_t* kind, int32_t* width, int32_t* nullable,
+                                     int32_t* parent) {
+  const Plan& p = plan->p;
+  for (size_t i = 0; i < p.nodes.size(); ++i) {
+    kind[i] = p.nodes[i].kind;
+    width[i] = p.nodes[i].width;
+    nullable[i] = p.nodes[i].nullable;
+    parent[i] = -1;
+  }
+  for (size_t i = 0; i < p.nodes.size(); ++i)
+    for (int32_t ch : p.nodes[i].children) parent[ch] = (int32_t)i;
+  return FORY_OK;
+}
+
 int fory_rowfmt_plan_create(const fory_field_desc* fields, int32_t num_desc, fory_plan** out_plan) {
   if (!out_plan) return fail(FORY_ERR_INVALID_ARGUMENT, "out_plan is null");
   *out_plan = nullptr;

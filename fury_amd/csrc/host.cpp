@@ -48,6 +48,24 @@ struct fory_host_ctx {
   int64_t ws_bytes = 0;
   hipStream_t s_in = nullptr, s_k = nullptr, s_out = nullptr;
   hipEvent_t ev_in[2] = {}, ev_k[2] = {}, ev_out[2] = {};
+  // varlen plans (whole batch per call; device buffers kept and grown)
+  bool varlen = false;
+  std::vector<int32_t> kind, parent;
+  uint8_t* dbuf = nullptr;   // columns, row offsets, workspace, status
+  int64_t dbuf_bytes = 0;
+  uint8_t* drows = nullptr;  // rows / frames
+  int64_t drows_bytes = 0;
+  uint8_t* dout = nullptr;   // decode: output columns
+  int64_t dout_bytes = 0;
+  // decode state between host_decode_var_sizes and host_decode_var
+  int64_t dec_n = -1;
+  int32_t dec_frame = 0;
+  int64_t dec_r0 = 0;
+  std::vector<int64_t> dec_count, dec_bytes;
+  std::vector<fory_column> dec_cols;
+  int64_t* dec_offs = nullptr;
+  void* dec_ws = nullptr;
+  int32_t* dec_status = nullptr;
 };
 
 namespace {
@@ -65,6 +83,8 @@ int hip_check(hipError_t e, const char* what) {
 // is thread-local there; column widths/nullability of a fixed-width plan.
 extern "C" int fory_rowfmt_internal_set_error(int code, const char* msg);
 extern "C" int fory_rowfmt_internal_column_layout(const fory_plan* plan, int32_t* width, int32_t* nullable);
+extern "C" int fory_rowfmt_internal_node_layout(const fory_plan* plan, int32_t* kind, int32_t* width,
+                                                int32_t* nullable, int32_t* parent);
 
 namespace {
 
@@ -90,9 +110,26 @@ int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t c
   fory_plan_info info{};
   int rc = fory_rowfmt_plan_info(plan, &info);
   if (rc) return rc;
-  if (!info.fixed_width)
-    return fail_host(FORY_ERR_UNSUPPORTED, "host path: fixed-width plans only (ABI 1); varlen plans use the device "
-                                           "entry points with caller-staged buffers");
+  if (!info.fixed_width) {  // varlen: fory_rowfmt_host_encode_var / host_decode_var_sizes / host_decode_var
+    fory_host_ctx* c = new fory_host_ctx();
+    c->plan = plan;
+    c->info = info;
+    c->device = device;
+    c->varlen = true;
+    c->kind.resize(info.num_columns);
+    c->parent.resize(info.num_columns);
+    c->width.resize(info.num_columns);
+    c->nullable.resize(info.num_columns);
+    fory_rowfmt_internal_node_layout(plan, c->kind.data(), c->width.data(), c->nullable.data(), c->parent.data());
+    rc = hip_check(hipSetDevice(device), "hipSetDevice");
+    if (!rc) rc = hip_check(hipStreamCreateWithFlags(&c->s_k, hipStreamNonBlocking), "hipStreamCreate");
+    if (rc) {
+      fory_rowfmt_host_ctx_destroy(c);
+      return rc;
+    }
+    *out = c;
+    return FORY_OK;
+  }
   if (chunk_rows <= 0) chunk_rows = 1 << 20;
   chunk_rows = (chunk_rows + 63) / 64 * 64;  // whole 64-record tiles: validity slices are byte aligned
   fory_host_ctx* c = new fory_host_ctx();
@@ -162,6 +199,8 @@ void fory_rowfmt_host_ctx_destroy(fory_host_ctx* c) {
   for (hipStream_t s : {c->s_in, c->s_k, c->s_out})
     if (s) (void)hipStreamDestroy(s);
   if (c->arena) (void)hipFree(c->arena);
+  for (uint8_t* b : {c->dbuf, c->drows, c->dout})
+    if (b) (void)hipFree(b);
   delete c;
 }
 
@@ -178,6 +217,7 @@ int fory_rowfmt_host_unregister(void* host_ptr) {
 int fory_rowfmt_host_encode(fory_host_ctx* c, const fory_column* host_cols, int64_t n, int32_t frame,
                             void* host_out, int64_t out_capacity) {
   if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+  if (c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "varlen plan: use fory_rowfmt_host_encode_var");
   if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM)
     return fail_host(FORY_ERR_INVALID_ARGUMENT, "frame_mode must be 0 (raw) or 1 (stream)");
   if (n < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
@@ -244,6 +284,7 @@ int fory_rowfmt_host_encode(fory_host_ctx* c, const fory_column* host_cols, int6
 int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t rows_bytes, int64_t n, int32_t frame,
                             const fory_column* host_out_cols) {
   if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+  if (c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "varlen plan: use fory_rowfmt_host_decode_var");
   if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM)
     return fail_host(FORY_ERR_INVALID_ARGUMENT, "frame_mode must be 0 (raw) or 1 (stream)");
   if (n < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
@@ -305,6 +346,309 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
     if (rc) return rc;
   }
   return FORY_OK;
+}
+
+
+// ---------------------------------------------------------------------------
+// Varlen plans (strings, lists, maps, nested structs, collection frames): the
+// whole batch per call. Row sizes are data-dependent, so the chunk pipeline's
+// fixed strides do not apply; device buffers live in the context and grow.
+// ---------------------------------------------------------------------------
+
+}  // extern "C"
+
+namespace {
+
+constexpr int32_t kKindFixed = 0, kKindBool = 1, kKindBytes = 2, kKindStruct = 3, kKindList = 4, kKindMap = 5;
+
+bool has_offsets(int32_t k) { return k == kKindBytes || k == kKindList || k == kKindMap; }
+
+// Grows a context-owned device buffer (synchronising the context's stream first).
+int ensure(fory_host_ctx* c, uint8_t** buf, int64_t* have, int64_t need) {
+  if (need <= *have) return FORY_OK;
+  int rc = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize");
+  if (rc) return rc;
+  if (*buf) (void)hipFree(*buf);
+  *buf = nullptr;
+  *have = 0;
+  const int64_t sz = align_up(need + need / 4);
+  rc = hip_check(hipMalloc(buf, (size_t)sz), "hipMalloc(host ctx varlen buffers)");
+  if (!rc) *have = sz;
+  return rc;
+}
+
+// Carves per-column device regions (values, offsets, validity) for the element
+// counts / value bytes given, then row offsets (n+1 int64), the workspace and the
+// status word; returns the bytes needed when base is null.
+int64_t carve(fory_host_ctx* c, uint8_t* base, const std::vector<int64_t>& cnt, const std::vector<int64_t>& vbytes,
+              const std::vector<char>& want_validity, int64_t n, std::vector<fory_column>* cols, int64_t** d_offs,
+              void** ws, int64_t ws_bytes, int32_t** status) {
+  int64_t at = 0;
+  const int N = (int)cnt.size();
+  if (cols) cols->assign(N, fory_column{});
+  for (int i = 0; i < N; ++i) {
+    fory_column d{};
+    d.length = cnt[i];
+    if (vbytes[i] > 0 || c->kind[i] == kKindFixed || c->kind[i] == kKindBool || c->kind[i] == kKindBytes) {
+      d.values = base ? base + at : nullptr;
+      d.capacity = vbytes[i];
+      at += align_up(vbytes[i] > 0 ? vbytes[i] : 1);
+    }
+    if (has_offsets(c->kind[i]) && cnt[i] >= 0) {
+      d.offsets = base ? reinterpret_cast<int32_t*>(base + at) : nullptr;
+      at += align_up((cnt[i] + 1) * 4);
+    }
+    if (want_validity[i]) {
+      d.validity = base ? base + at : nullptr;
+      at += align_up(validity_bytes(cnt[i] > 0 ? cnt[i] : 1));
+    }
+    if (cols) (*cols)[i] = d;
+  }
+  if (d_offs) *d_offs = base ? reinterpret_cast<int64_t*>(base + at) : nullptr;
+  at += align_up((n + 1) * 8);
+  if (ws) *ws = base ? base + at : nullptr;
+  at += align_up(ws_bytes);
+  if (status) *status = base ? reinterpret_cast<int32_t*>(base + at) : nullptr;
+  at += kAlign;
+  return at;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fory_rowfmt_host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, int32_t frame,
+                                void* host_out, int64_t out_capacity, int64_t* host_row_offsets,
+                                int64_t* out_bytes) {
+  if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+  if (!c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "fixed-width plan: use fory_rowfmt_host_encode");
+  if (n < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
+  if (out_bytes) *out_bytes = 0;
+  if (n == 0) {
+    if (host_row_offsets) host_row_offsets[0] = 0;
+    return FORY_OK;
+  }
+  if (!host_cols || !host_out) return fail_host(FORY_ERR_INVALID_ARGUMENT, "host columns or output is null");
+  const int N = c->info.num_columns;
+  // element count and value bytes of every column, from the host offsets
+  std::vector<int64_t> cnt(N, 0), vbytes(N, 0);
+  std::vector<char> want_validity(N, 0);
+  for (int i = 0; i < N; ++i) {
+    const int p = c->parent[i];
+    if (p < 0) cnt[i] = n;
+    else if (c->kind[p] == kKindStruct) cnt[i] = cnt[p];
+    else cnt[i] = cnt[p] > 0 ? host_cols[p].offsets[cnt[p]] : 0;  // list items / map entries
+    const fory_column& h = host_cols[i];
+    if (has_offsets(c->kind[i]) && !h.offsets)
+      return fail_host(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(i) + " needs offsets");
+    if (c->kind[i] == kKindFixed || c->kind[i] == kKindBool) vbytes[i] = cnt[i] * c->width[i];
+    else if (c->kind[i] == kKindBytes) vbytes[i] = cnt[i] > 0 ? h.offsets[cnt[i]] : 0;
+    if (vbytes[i] > 0 && !h.values)
+      return fail_host(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(i) + " has no values");
+    want_validity[i] = c->nullable[i] && h.validity;
+  }
+  int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
+  if (rc) return rc;
+  const int64_t ws_bytes = fory_rowfmt_workspace_bytes(c->plan, n);
+  rc = ensure(c, &c->dbuf, &c->dbuf_bytes, carve(c, nullptr, cnt, vbytes, want_validity, n, nullptr, nullptr,
+                                                 nullptr, ws_bytes, nullptr));
+  if (rc) return rc;
+  std::vector<fory_column> d;
+  int64_t* d_offs = nullptr;
+  void* ws = nullptr;
+  int32_t* status = nullptr;
+  carve(c, c->dbuf, cnt, vbytes, want_validity, n, &d, &d_offs, &ws, ws_bytes, &status);
+  for (int i = 0; i < N && !rc; ++i) {  // H2D of every column
+    const fory_column& h = host_cols[i];
+    if (d[i].values && vbytes[i] > 0)
+      rc = hip_check(hipMemcpyAsync(d[i].values, h.values, (size_t)vbytes[i], hipMemcpyHostToDevice, c->s_k), "H2D");
+    if (!rc && d[i].offsets)
+      rc = hip_check(hipMemcpyAsync(d[i].offsets, h.offsets, (size_t)(cnt[i] + 1) * 4, hipMemcpyHostToDevice, c->s_k),
+                     "H2D offsets");
+    if (!rc && d[i].validity)
+      rc = hip_check(hipMemcpyAsync(d[i].validity, h.validity, (size_t)((cnt[i] + 7) / 8), hipMemcpyHostToDevice,
+                                    c->s_k), "H2D validity");
+  }
+  if (!rc) rc = hip_check(hipMemsetAsync(status, 0, 4, c->s_k), "hipMemsetAsync");
+  if (!rc) rc = fory_rowfmt_encoded_size(c->plan, d.data(), n, frame, d_offs, ws, ws_bytes, c->s_k);
+  int64_t total = 0;
+  if (!rc) rc = hip_check(hipMemcpyAsync(&total, d_offs + n, 8, hipMemcpyDeviceToHost, c->s_k), "D2H total");
+  if (!rc) rc = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize");
+  if (rc) return rc;
+  if (out_bytes) *out_bytes = total;
+  if (total > out_capacity)  // MemoryBuffer bounds check (MemoryBuffer.java:303-309)
+    return fail_host(FORY_ERR_CAPACITY, "output capacity " + std::to_string(out_capacity) + " < " +
+                                            std::to_string(total) + " bytes");
+  rc = ensure(c, &c->drows, &c->drows_bytes, total + 16);
+  if (!rc) rc = fory_rowfmt_encode(c->plan, d.data(), n, frame, d_offs, c->drows, total, status, ws, ws_bytes, c->s_k);
+  if (!rc && total > 0)
+    rc = hip_check(hipMemcpyAsync(host_out, c->drows, (size_t)total, hipMemcpyDeviceToHost, c->s_k), "D2H rows");
+  if (!rc && host_row_offsets)
+    rc = hip_check(hipMemcpyAsync(host_row_offsets, d_offs, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, c->s_k),
+                   "D2H row offsets");
+  if (!rc) rc = fory_rowfmt_read_status(status, c->s_k);  // synchronises the stream
+  return rc;
+}
+
+int fory_rowfmt_host_decode_var_sizes(fory_host_ctx* c, const void* host_rows, const int64_t* host_row_offsets,
+                                      int64_t n, int32_t frame, int64_t* host_counts, int64_t* host_bytes) {
+  if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+  if (!c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "fixed-width plan: use fory_rowfmt_host_decode");
+  if (n < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
+  if (!host_row_offsets || !host_counts || !host_bytes || (n > 0 && !host_rows))
+    return fail_host(FORY_ERR_INVALID_ARGUMENT, "host rows, row offsets or size outputs null");
+  const int N = c->info.num_columns;
+  c->dec_n = -1;
+  const int64_t r0 = host_row_offsets[0], r1 = host_row_offsets[n];
+  if (r1 < r0 || r0 < 0) return fail_host(FORY_ERR_CORRUPT, "row offsets decrease");
+  int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
+  if (rc) return rc;
+  // rows at their 16-byte phase, so the device sees the host buffer's alignment
+  rc = ensure(c, &c->drows, &c->drows_bytes, (r1 - r0) + 32);
+  if (rc) return rc;
+  uint8_t* drow0 = c->drows + (r0 & 15);
+  if (r1 > r0)
+    rc = hip_check(hipMemcpyAsync(drow0, static_cast<const uint8_t*>(host_rows) + r0, (size_t)(r1 - r0),
+                                  hipMemcpyHostToDevice, c->s_k), "H2D rows");
+  // element counts: top level n; struct fields as their struct; list/map elements
+  // from the container totals (pass 1), string/binary elements' bytes (pass 2)
+  std::vector<int64_t> cnt(N, -1), vbytes(N, 0);
+  std::vector<char> want_validity(N, 0);
+  for (int i = 0; i < N; ++i) want_validity[i] = c->nullable[i] != 0;
+  auto resolve = [&]() {
+    for (int i = 0; i < N; ++i) {
+      const int p = c->parent[i];
+      if (cnt[i] >= 0) continue;
+      if (p < 0) cnt[i] = n;
+      else if (cnt[p] >= 0 && c->kind[p] == kKindStruct) cnt[i] = cnt[p];
+    }
+  };
+  resolve();
+  const int64_t ws_bytes = fory_rowfmt_workspace_bytes(c->plan, n);
+  std::vector<fory_column> d;
+  int64_t* d_offs = nullptr;
+  void* ws = nullptr;
+  int32_t* status = nullptr;
+  for (int pass = 0; pass < 3 && !rc; ++pass) {
+    // layout for the counts known so far (unknown: no buffers, length 0)
+    std::vector<int64_t> kc(N);
+    for (int i = 0; i < N; ++i) kc[i] = cnt[i] < 0 ? -1 : cnt[i];
+    std::vector<int64_t> vb0(N, 0);
+    std::vector<char> wv(N, 0);
+    rc = ensure(c, &c->dbuf, &c->dbuf_bytes, carve(c, nullptr, kc, vb0, wv, n, nullptr, nullptr, nullptr, ws_bytes,
+                                                   nullptr));
+    if (rc) break;
+    carve(c, c->dbuf, kc, vb0, wv, n, &d, &d_offs, &ws, ws_bytes, &status);
+    for (int i = 0; i < N; ++i) {
+      d[i].values = nullptr;
+      d[i].capacity = 0;
+      if (kc[i] < 0) d[i] = fory_column{};
+    }
+    // the row offsets' place moves with the layout: copy them for every pass
+    rc = hip_check(hipMemcpyAsync(d_offs, host_row_offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->s_k),
+                   "H2D row offsets");
+    if (!rc) rc = hip_check(hipMemsetAsync(status, 0, 4, c->s_k), "hipMemsetAsync");
+    if (!rc)
+      rc = fory_rowfmt_decode_sizes(c->plan, drow0 - r0, d_offs, n, frame, d.data(), status, ws, ws_bytes, c->s_k);
+    std::vector<int32_t> tot(N, 0);
+    for (int i = 0; i < N && !rc; ++i)
+      if (d[i].offsets && kc[i] >= 0)
+        rc = hip_check(hipMemcpyAsync(&tot[i], d[i].offsets + kc[i], 4, hipMemcpyDeviceToHost, c->s_k), "D2H totals");
+    if (!rc) rc = fory_rowfmt_read_status(status, c->s_k);
+    if (rc) break;
+    bool changed = false;
+    for (int i = 0; i < N; ++i) {
+      if (!has_offsets(c->kind[i]) || kc[i] < 0) continue;
+      if (c->kind[i] == kKindBytes) vbytes[i] = tot[i];
+      else
+        for (int j = 0; j < N; ++j)  // direct children of a list/map: its element total
+          if (c->parent[j] == i && cnt[j] < 0) cnt[j] = tot[i], changed = true;
+    }
+    resolve();
+    if (!changed) break;
+  }
+  if (rc) return rc;
+  for (int i = 0; i < N; ++i) {
+    if (cnt[i] < 0) cnt[i] = 0;
+    if (c->kind[i] == kKindFixed || c->kind[i] == kKindBool) vbytes[i] = cnt[i] * c->width[i];
+    host_counts[i] = cnt[i];
+    host_bytes[i] = vbytes[i];
+  }
+  c->dec_n = n;
+  c->dec_frame = frame;
+  c->dec_r0 = r0;
+  c->dec_count = cnt;
+  c->dec_bytes = vbytes;
+  c->dec_cols = d;  // the last pass's device offsets (tile bases / totals for decode)
+  c->dec_offs = d_offs;
+  c->dec_ws = ws;
+  c->dec_status = status;
+  return FORY_OK;
+}
+
+int fory_rowfmt_host_decode_var(fory_host_ctx* c, const fory_column* host_out_cols) {
+  if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+  if (!c->varlen || c->dec_n < 0)
+    return fail_host(FORY_ERR_INVALID_ARGUMENT, "call fory_rowfmt_host_decode_var_sizes first");
+  const int N = c->info.num_columns;
+  const int64_t n = c->dec_n;
+  if (n > 0 && !host_out_cols) return fail_host(FORY_ERR_INVALID_ARGUMENT, "host output columns null");
+  for (int i = 0; i < N && n > 0; ++i) {
+    const fory_column& h = host_out_cols[i];
+    if (c->dec_bytes[i] > 0 && (!h.values || (h.capacity > 0 && h.capacity < c->dec_bytes[i])))
+      return fail_host(FORY_ERR_CAPACITY, "output column " + std::to_string(i) + " values missing or too small");
+    if (has_offsets(c->kind[i]) && !h.offsets)
+      return fail_host(FORY_ERR_INVALID_ARGUMENT, "output column " + std::to_string(i) + " needs offsets");
+  }
+  if (n == 0) {
+    for (int i = 0; i < N; ++i)
+      if (host_out_cols && host_out_cols[i].offsets) host_out_cols[i].offsets[0] = 0;
+    return FORY_OK;
+  }
+  int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
+  if (rc) return rc;
+  std::vector<char> wv(N, 0);
+  for (int i = 0; i < N; ++i) wv[i] = c->nullable[i] && host_out_cols[i].validity;
+  const int64_t ws_bytes = fory_rowfmt_workspace_bytes(c->plan, n);
+  // output columns in their own buffer (the row offsets / workspace stay in dbuf)
+  rc = ensure(c, &c->dout, &c->dout_bytes, carve(c, nullptr, c->dec_count, c->dec_bytes, wv, 0, nullptr, nullptr,
+                                                 nullptr, 0, nullptr));
+  if (rc) return rc;
+  std::vector<fory_column> d;
+  carve(c, c->dout, c->dec_count, c->dec_bytes, wv, 0, &d, nullptr, nullptr, 0, nullptr);
+  const std::vector<int64_t>& kc = c->dec_count;
+  const std::vector<fory_column>& dsz = c->dec_cols;
+  int64_t* d_offs = c->dec_offs;
+  void* ws = c->dec_ws;
+  int32_t* status = c->dec_status;
+  // the sizes pass wrote the offsets into dbuf's column regions: copy them over
+  for (int i = 0; i < N && !rc; ++i) {
+    if (d[i].offsets && dsz[i].offsets)
+      rc = hip_check(hipMemcpyAsync(d[i].offsets, dsz[i].offsets, (size_t)(kc[i] + 1) * 4, hipMemcpyDeviceToDevice,
+                                    c->s_k), "D2D offsets");
+    if (!rc && d[i].validity)
+      rc = hip_check(hipMemsetAsync(d[i].validity, 0, (size_t)validity_bytes(kc[i] > 0 ? kc[i] : 1), c->s_k),
+                     "hipMemsetAsync");
+  }
+  if (!rc) rc = hip_check(hipMemsetAsync(status, 0, 4, c->s_k), "hipMemsetAsync");
+  uint8_t* drow0 = c->drows + (c->dec_r0 & 15);
+  if (!rc)
+    rc = fory_rowfmt_decode(c->plan, drow0 - c->dec_r0, d_offs, n, c->dec_frame, d.data(), status, ws, ws_bytes,
+                            c->s_k);
+  for (int i = 0; i < N && !rc; ++i) {  // D2H of every column
+    const fory_column& h = host_out_cols[i];
+    if (d[i].values && c->dec_bytes[i] > 0)
+      rc = hip_check(hipMemcpyAsync(h.values, d[i].values, (size_t)c->dec_bytes[i], hipMemcpyDeviceToHost, c->s_k),
+                     "D2H values");
+    if (!rc && d[i].offsets)
+      rc = hip_check(hipMemcpyAsync(h.offsets, d[i].offsets, (size_t)(kc[i] + 1) * 4, hipMemcpyDeviceToHost, c->s_k),
+                     "D2H offsets");
+    if (!rc && d[i].validity)
+      rc = hip_check(hipMemcpyAsync(h.validity, d[i].validity, (size_t)((kc[i] + 7) / 8), hipMemcpyDeviceToHost,
+                                    c->s_k), "D2H validity");
+  }
+  if (!rc) rc = fory_rowfmt_read_status(status, c->s_k);
+  return rc;
 }
 
 }  // extern "C"

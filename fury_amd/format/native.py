@@ -136,8 +136,9 @@ def _np_ptr(a) -> Optional[int]:
 
 class HostPipeline:
     """fory_rowfmt_host_*: host-memory batches (numpy arrays, e.g. the Arrow view of
-    off-heap MemoryBuffers) through the device kernels with the C++ chunk pipeline.
-    Fixed-width plans (ABI 1)."""
+    off-heap MemoryBuffers) through the device kernels: the C++ chunk pipeline for
+    fixed-width plans (encode/decode), whole batches for varlen plans (encode_var /
+    decode_var)."""
 
     def __init__(self, plan: NativePlan, chunk_rows: int = 1 << 20, device: int = 0):
         lib = _lib.load()
@@ -176,6 +177,53 @@ class HostPipeline:
     def decode(self, rows, n: int, frame: int, host_out_cols) -> None:
         _check(_lib.load().fory_rowfmt_host_decode(self.handle, _np_ptr(rows), rows.nbytes, n, frame,
                                                    self._host_array(host_out_cols)))
+
+    # -- varlen plans: whole batch per call --------------------------------
+    def encode_var(self, host_cols, n: int, frame: int, out=None):
+        """Returns (rows uint8 array, row offsets int64[n+1]); grows `out` on capacity errors."""
+        import numpy as np
+        lib = _lib.load()
+        arr = self._host_array(host_cols)
+        offs = np.zeros(n + 1, np.int64)
+        total = ctypes.c_int64(0)
+        if out is None:
+            out = np.zeros(1, np.uint8)
+        rc = lib.fory_rowfmt_host_encode_var(self.handle, arr, n, frame, _np_ptr(out), out.nbytes,
+                                             _np_ptr(offs), ctypes.byref(total))
+        if rc == _lib.FORY_ERR_CAPACITY and total.value > out.nbytes:  # MemoryBuffer grows and retries
+            out = np.zeros(total.value, np.uint8)
+            rc = lib.fory_rowfmt_host_encode_var(self.handle, arr, n, frame, _np_ptr(out), out.nbytes,
+                                                 _np_ptr(offs), ctypes.byref(total))
+        _check(rc)
+        return out[:total.value], offs
+
+    def decode_var(self, rows, offsets, n: int, frame: int):
+        """Host rows -> host columns (HostColumn list, pre-order)."""
+        import numpy as np
+        from .columns import HostColumn, NP_DTYPE, validity_bytes
+        from .types import ArrowType, preorder
+        lib = _lib.load()
+        fields = preorder(self.plan.schema)
+        counts = np.zeros(max(1, len(fields)), np.int64)
+        nbytes = np.zeros(max(1, len(fields)), np.int64)
+        offs = np.ascontiguousarray(offsets, dtype=np.int64)
+        _check(lib.fory_rowfmt_host_decode_var_sizes(self.handle, _np_ptr(rows), _np_ptr(offs), n, frame,
+                                                     _np_ptr(counts), _np_ptr(nbytes)))
+        cols = []
+        for i, f in enumerate(fields):
+            k, t = int(counts[i]), f.type.id
+            c = HostColumn(length=k)
+            if t in (ArrowType.STRING, ArrowType.BINARY):
+                c.values = np.zeros(max(1, int(nbytes[i])), np.uint8)
+            elif t in NP_DTYPE:
+                c.values = np.zeros(max(1, k), NP_DTYPE[t])
+            if t in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP):
+                c.offsets = np.zeros(k + 1, np.int32)
+            if f.nullable:
+                c.validity = np.zeros(validity_bytes(k), np.uint8)
+            cols.append(c)
+        _check(lib.fory_rowfmt_host_decode_var(self.handle, self._host_array(cols)))
+        return cols
 
 
 def host_register(a) -> None:

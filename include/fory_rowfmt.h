@@ -245,8 +245,9 @@ int fory_rowfmt_read_status(const int32_t* d_status, void* stream);
  * complete (or with the first error). All pointers are HOST memory; register
  * long-lived buffers (fory_rowfmt_host_register = hipHostRegister) for full
  * PCIe rate. The plan must outlive the context; a context serves one call at
- * a time. ABI 1: fixed-width plans only (FORY_ERR_UNSUPPORTED at creation
- * otherwise). Output bytes equal fory_rowfmt_encode's / decode's. */
+ * a time. Fixed-width plans use the chunk pipeline (host_encode / host_decode);
+ * varlen plans the _var entry points below. Output bytes equal
+ * fory_rowfmt_encode's / decode's. */
 typedef struct fory_host_ctx fory_host_ctx;
 int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t chunk_rows,
                                 fory_host_ctx** out_ctx);
@@ -261,6 +262,29 @@ int fory_rowfmt_host_encode(fory_host_ctx* ctx, const fory_column* host_cols, in
  * hash (FORY_ERR_SCHEMA_MISMATCH: ClassNotCompatibleException). */
 int fory_rowfmt_host_decode(fory_host_ctx* ctx, const void* host_rows, int64_t rows_bytes,
                             int64_t num_rows, int32_t frame_mode, const fory_column* host_out_cols);
+/* Varlen plans (strings, lists, maps, nested structs; also FORY_FRAME_COLLECTION):
+ * the whole batch per call (row sizes are data-dependent, so there are no fixed
+ * chunk strides); the context keeps its device buffers and grows them as needed.
+ * host_encode_var: host columns (Arrow layout, as fory_rowfmt_encode) -> rows /
+ * frames back to back in host_out; *out_bytes receives the total (also on
+ * FORY_ERR_CAPACITY, so the caller can grow its buffer), host_row_offsets (n+1,
+ * may be NULL) the row/frame starts. */
+int fory_rowfmt_host_encode_var(fory_host_ctx* ctx, const fory_column* host_cols, int64_t num_rows,
+                                int32_t frame_mode, void* host_out, int64_t out_capacity,
+                                int64_t* host_row_offsets, int64_t* out_bytes);
+/* Decode of host rows in two calls (the caller allocates in between):
+ * host_decode_var_sizes stages the rows (host_row_offsets: n+1 starts, required)
+ * on the device and writes per pre-order column its element count
+ * (host_counts: rows for top-level fields, items / entries below a list or map)
+ * and value bytes (host_bytes: count x width, or the string/binary bytes; 0 for
+ * struct/list/map). host_decode_var then decodes that staged batch into
+ * host_out_cols: values (>= host_bytes), offsets (count + 1 int32) for
+ * string/binary/list/map, validity ((count + 7) / 8 bytes) for nullable fields.
+ * Errors as fory_rowfmt_decode (schema hash, corrupt frame). */
+int fory_rowfmt_host_decode_var_sizes(fory_host_ctx* ctx, const void* host_rows,
+                                      const int64_t* host_row_offsets, int64_t num_rows,
+                                      int32_t frame_mode, int64_t* host_counts, int64_t* host_bytes);
+int fory_rowfmt_host_decode_var(fory_host_ctx* ctx, const fory_column* host_out_cols);
 int fory_rowfmt_host_register(void* host_ptr, int64_t bytes);
 int fory_rowfmt_host_unregister(void* host_ptr);
 

@@ -116,10 +116,7 @@ def test_argument_validation_without_gpu():
 
 
 def test_host_path_validation_without_gpu():
-    """The host pipeline rejects varlen plans and bad arguments before touching the device."""
-    from fury_amd.format.native import HostPipeline
-    with pytest.raises(errors.UnsupportedOperationException):
-        HostPipeline(NativePlan(W.mixed_schema()))
+    """The host path rejects bad arguments before touching the device."""
     lib = _lib.load()
     h = ctypes.c_void_p()
     assert lib.fory_rowfmt_host_ctx_create(None, 0, 1024, ctypes.byref(h)) == _lib.FORY_ERR_INVALID_ARGUMENT
@@ -127,3 +124,8 @@ def test_host_path_validation_without_gpu():
     assert lib.fory_rowfmt_host_encode(None, cols, 1, 0, None, 0) == _lib.FORY_ERR_INVALID_ARGUMENT
     assert lib.fory_rowfmt_host_decode(None, None, 0, 1, 0, cols) == _lib.FORY_ERR_INVALID_ARGUMENT
     assert lib.fory_rowfmt_host_register(None, 16) == _lib.FORY_ERR_INVALID_ARGUMENT
+    total = ctypes.c_int64(0)
+    assert lib.fory_rowfmt_host_encode_var(None, cols, 1, 0, None, 0, None, ctypes.byref(total)) == \
+        _lib.FORY_ERR_INVALID_ARGUMENT
+    assert lib.fory_rowfmt_host_decode_var_sizes(None, None, None, 1, 0, None, None) == _lib.FORY_ERR_INVALID_ARGUMENT
+    assert lib.fory_rowfmt_host_decode_var(None, cols) == _lib.FORY_ERR_INVALID_ARGUMENT
