@@ -4,8 +4,9 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
 LIB := fury_amd/lib/libfory_rowfmt.so
 ORACLE := oracle/_build/liboracle.so
-SRCS := fury_amd/csrc/kernels.hip fury_amd/csrc/capi.cpp fury_amd/csrc/plan.cpp fury_amd/csrc/host.cpp
-HDRS := fury_amd/csrc/kernels.h fury_amd/csrc/plan.h include/fory_rowfmt.h
+KOBJS := fury_amd/lib/fixed.o fury_amd/lib/scan.o fury_amd/lib/varlen.o fury_amd/lib/launch_state.o \
+         fury_amd/lib/capi.o fury_amd/lib/plan.o fury_amd/lib/host.o
+HDRS := fury_amd/csrc/kernels.h fury_amd/csrc/kcommon.h fury_amd/csrc/plan.h include/fory_rowfmt.h
 
 CAPI_TEST := tests/c/capi_roundtrip
 
@@ -25,7 +26,7 @@ fury_amd/lib/%.o: fury_amd/csrc/%.cpp $(HDRS)
 	@mkdir -p fury_amd/lib
 	$(HIPCC) $(HIPFLAGS) -x hip -c -o $@ $<
 
-$(LIB): fury_amd/lib/kernels.o fury_amd/lib/capi.o fury_amd/lib/plan.o fury_amd/lib/host.o
+$(LIB): $(KOBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 $(ORACLE): oracle/rowfmt_oracle.c include/fory_rowfmt.h

@@ -5,20 +5,37 @@ Metric (BASELINE.json): "row-format encode+decode GiB/s (device-resident),
 64M Struct(100 prim) rows" = (row bytes written by encode + row bytes read by
 decode) / (t_encode + t_decode) / 2^30, summed over all ranks.
 
-One step = encode the whole per-GPU batch (columns -> rows, RAW rows =
-BinaryRow.toBytes of each object; --frame for the Encoder.encode(MemoryBuffer,T)
+One step = encode every record of the job (columns -> rows; RAW rows =
+BinaryRow.toBytes of each object, --frame for the Encoder.encode(MemoryBuffer,T)
 frame stream) + decode it back (rows -> columns), inputs resident in HBM.
-Multi-GPU: one process per GPU (torchrun), each encodes/decodes its own shard
-of records (weak scaling: rows per GPU fixed); no data-path collective — only a
-barrier and a MAX of the elapsed time.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config struct104|mixed40|nested]
+Struct104 (default): BASELINE config C4 — a FIXED total of 256Mi records
+(strong scaling), split into contiguous per-rank ranges (fury_amd.shard), no
+data-path collective. A rank processes its range in resident windows of at most
+64Mi records (the 64M-row headline batch; 256Mi rows' columns + rows + decoded
+columns would need 565 GB, a window needs 141 GB of the 288 GB HBM), so at N=1
+a step is 4 windows of the headline batch, at N=4 one, at N=8 one 32Mi window.
+Every window is a full encode + decode of 64Mi (32Mi) records; a rank's windows
+reuse one set of resident columns (the byte shuffle's memory traffic does not
+depend on the values of a fixed-width schema). A second timed loop reports the
+weak-scaling extra (64Mi records per rank, one window) under "weak".
+
+Multi-GPU: `python bench.py --gpus N` starts `torch.distributed.run` with N
+ranks as a child process (before anything touches the GPU) and exits with its
+code; under torchrun (WORLD_SIZE set) each rank takes cuda:LOCAL_RANK. Fewer
+visible GPUs than N is an error, never a silent 1-GPU run. Timing: barrier +
+synchronize on both sides, MAX of the elapsed time over ranks.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+                       [--config struct104|mixed40|mixed40_long|nested] [--frame]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
+import subprocess
 import sys
 import time
 
@@ -26,6 +43,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+MI = 1024 * 1024
 
 
 def parse():
@@ -34,8 +52,18 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="struct104", choices=["struct104", "mixed40", "mixed40_long", "nested"])
-    ap.add_argument("--rows", type=int, default=0, help="rows per GPU (default: config size)")
+    ap.add_argument("--total-rows", type=int, default=0,
+                    help="records of the whole job, split over the ranks (default: C4 256Mi for struct104, "
+                         "the config size for the varlen configs)")
+    ap.add_argument("--rows", type=int, default=0, help="(compat) records per GPU: total = rows x gpus")
+    ap.add_argument("--window-rows", type=int, default=64 * MI, help="max resident records per rank window")
+    ap.add_argument("--weak-rows", type=int, default=64 * MI,
+                    help="records per rank of the weak-scaling extra (struct104; 0 = skip)")
     ap.add_argument("--frame", action="store_true", help="frame-stream mode instead of raw rows")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group backend (gloo: rehearsal of the multi-rank path)")
+    ap.add_argument("--oversubscribe", action="store_true",
+                    help="allow more ranks than visible GPUs (rank -> cuda:(local_rank %% count)); rehearsal only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads of the CPU baseline")
@@ -44,8 +72,27 @@ def parse():
     return ap.parse_args()
 
 
-DEFAULT_ROWS = {"struct104": 64 * 1024 * 1024, "mixed40": 16 * 1024 * 1024, "nested": 8 * 1024 * 1024,
-                "mixed40_long": 8 * 1024 * 1024}  # mixed40_long: strings 0..128 B (robustness, not a BASELINE config)
+DEFAULT_TOTAL = {"struct104": 256 * MI, "mixed40": 16 * MI, "nested": 8 * MI,
+                 "mixed40_long": 8 * MI}  # mixed40_long: strings 0..128 B (robustness, not a BASELINE config)
+
+
+def launch_ranks(args) -> int:
+    """Parent of an N-rank run: torchrun as a child process (no GPU touched here;
+    device_count() does not initialise the GPU)."""
+    import socket
+    import torch
+    have = torch.cuda.device_count()
+    if have < args.gpus and not args.oversubscribe:
+        print(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible; refusing to measure fewer ranks",
+              file=sys.stderr)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def setup_dist(args):
@@ -53,23 +100,47 @@ def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    have = torch.cuda.device_count()
+    if have < world and not args.oversubscribe:
+        raise SystemExit(f"bench.py: {world} ranks but only {have} GPU(s) visible")
+    dev = local % max(1, have)
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return dist, world, rank, local
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
+        # n_gpus = ranks that actually initialised
+        one = torch.ones(1, dtype=torch.int64, device="cuda" if args.backend == "nccl" else "cpu")
+        dist.all_reduce(one)
+        if int(one.item()) != world:
+            raise SystemExit("bench.py: not every rank initialised")
+    return dist, world, rank, dev
 
 
 def barrier(dist):
     import torch
+    torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
 
 
+def max_over_ranks(dist, x: float, backend: str) -> float:
+    import torch
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def make_batch(config, n, row0, device):
-    """Device columns + algorithmic byte counts for the config."""
+    """Device columns + algorithmic column byte count for the config."""
     import torch
     from fury_amd import workloads as W
     from fury_amd.format.columns import to_device
@@ -79,21 +150,64 @@ def make_batch(config, n, row0, device):
         vals = W.gen_struct_device(n, seed_base=17 + row0, device=device)
         cols = [DeviceColumn(v, None, None, n) for v in vals]
         col_bytes = sum(v.numel() * v.element_size() for v in vals)
-    else:
-        mixed = config.startswith("mixed40")
-        mk = W.mixed_host_columns if mixed else W.nested_host_columns
-        seed = (23 if mixed else 29) + row0
-        host = mk(n, seed=seed, max_len=128) if config == "mixed40_long" else mk(n, seed=seed)
-        cols = to_device(host, device)
-        col_bytes = 0
-        for c in host:
-            for a in (c.values, c.offsets, c.validity):
-                if a is not None:
-                    col_bytes += a.nbytes
-        # string/item value buffers carry 8 bytes of generator padding: not algorithmic
+        torch.cuda.synchronize()
+        return schema, cols, col_bytes
+    mixed = config.startswith("mixed40")
+    mk = W.mixed_host_columns if mixed else W.nested_host_columns
+    seed = (23 if mixed else 29) + row0
+    host = mk(n, seed=seed, max_len=128) if config == "mixed40_long" else mk(n, seed=seed)
+    cols = to_device(host, device)
+    col_bytes = 0
+    for c in host:
+        for a in (c.values, c.offsets, c.validity):
+            if a is not None:
+                col_bytes += a.nbytes
+    # string/item value buffers carry 8 bytes of generator padding: not algorithmic
     torch.cuda.synchronize()
-    return schema if config == "struct104" else (W.mixed_schema() if config.startswith("mixed40")
-                                                 else W.nested_schema()), cols, col_bytes
+    return (W.mixed_schema() if mixed else W.nested_schema()), cols, col_bytes
+
+
+def prefix_cols(cols, n):
+    """The first n records of fixed-width device columns (views, no copy)."""
+    from fury_amd.format.native import DeviceColumn
+    return [DeviceColumn(c.values[:n], None, None if c.validity is None else c.validity, n) for c in cols]
+
+
+def check_round_trip(plan, cols, dcols, n):
+    """decode(encode(x)) == x on the measured batch: values, offsets, validity of every column."""
+    import torch
+    from fury_amd.format.types import ArrowType
+    for i, (a, b) in enumerate(zip(cols, dcols)):
+        f = plan.fields[i]
+        k = a.length
+        if b.length != k:
+            return f"column {i}: length {b.length} != {k}"
+        if a.offsets is not None:
+            if not torch.equal(a.offsets[:k + 1].to(torch.int64), b.offsets[:k + 1].to(torch.int64)):
+                return f"column {i}: offsets differ"
+        if a.values is not None and f.type.id != ArrowType.STRUCT:
+            if f.type.id in (ArrowType.STRING, ArrowType.BINARY):
+                nb = int(a.offsets[k].item()) if k > 0 else 0
+            else:
+                nb = k * a.values.element_size()
+            va = a.values.view(torch.uint8)[:nb]
+            vb = b.values.view(torch.uint8)[:nb]
+            if f.nullable and a.validity is not None and f.type.id not in (ArrowType.STRING, ArrowType.BINARY):
+                # null slots decode to 0; compare valid slots only
+                w = a.values.element_size()
+                bits = torch.arange(k, device=a.values.device)
+                valid = ((a.validity[bits // 8] >> (bits % 8).to(torch.uint8)) & 1).bool()
+                mask = valid.repeat_interleave(w)
+                va, vb = va[mask], vb[mask]
+            if not torch.equal(va, vb):
+                return f"column {i}: values differ"
+        if f.nullable and a.validity is not None and k > 0:
+            bits = torch.arange(k, device=a.validity.device)
+            ga = (a.validity[bits // 8] >> (bits % 8).to(torch.uint8)) & 1
+            gb = (b.validity[bits // 8] >> (bits % 8).to(torch.uint8)) & 1
+            if not torch.equal(ga, gb):
+                return f"column {i}: validity differs"
+    return None
 
 
 def cpu_baseline(config, frame, seconds, threads=1):
@@ -143,132 +257,249 @@ def cpu_baseline(config, frame, seconds, threads=1):
             "rows_per_s": reps * n / el}
 
 
+def jdk_probe():
+    """The reference's own CPU path needs a JVM (java/fory-format); record what the box has."""
+    java = shutil.which("java")
+    out = {"java": java, "javac": shutil.which("javac")}
+    if java:
+        try:
+            r = subprocess.run([java, "-version"], capture_output=True, text=True, timeout=20)
+            out["version"] = (r.stderr or r.stdout).strip().splitlines()[0] if (r.stderr or r.stdout) else ""
+        except (OSError, subprocess.SubprocessError) as e:
+            out["version"] = f"probe failed: {e}"
+    return out
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     import torch
-    dist, world, rank, local = setup_dist(args)
-    device = torch.device("cuda", local)
+    dist, world, rank, dev = setup_dist(args)
+    device = torch.device("cuda", dev)
     from fury_amd.format.encoder import RowEncoder
     from fury_amd.format import native
+    from fury_amd.shard import shard_range
 
     config = args.config
-    n = args.rows or DEFAULT_ROWS[config]
     frame = 1 if args.frame else 0
-    schema, cols, col_bytes = make_batch(config, n, rank * n, device)
+    total_rows = args.total_rows or (args.rows * world if args.rows else DEFAULT_TOTAL[config])
+    b, e = shard_range(total_rows, world, rank)
+    share = e - b
+    fixed = config == "struct104"
+    window = min(args.window_rows, share) if fixed else share
+    nwin = (share + window - 1) // window if window > 0 else 0
+    weak_rows = args.weak_rows if fixed else 0
+    alloc = max(window, weak_rows)
+    schema, cols_all, col_bytes_all = make_batch(config, alloc, b, device)
     enc = RowEncoder(schema, device=device)
     plan = enc.plan
-    ws = enc.workspace(n)
-    arr = native.column_array(cols)
+    ws = enc.workspace(alloc)
     status = torch.zeros(1, dtype=torch.int32, device=device)
     stream = torch.cuda.current_stream(device).cuda_stream
 
-    # output rows (sized once; varlen sizes via the device scan)
+    # ------------------------------------------------------------------ fixed width
     if plan.fixed_width:
-        total = n * plan.stride(frame)
-        offs = None
+        stride = plan.stride(frame)
+        out = torch.empty(max(16, alloc * stride), dtype=torch.uint8, device=device)
+        dcols_all = enc.alloc_fixed_outputs(alloc)
+        col_row = col_bytes_all // alloc  # column bytes per record (624 for Struct104)
+        # windows of this rank's share: (records, input cols, output cols)
+        wins = []
+        left = share
+        while left > 0:
+            m = min(window, left)
+            wins.append(m)
+            left -= m
+        arrs = {}
+
+        def arrays(m):
+            if m not in arrs:
+                arrs[m] = (native.column_array(prefix_cols(cols_all, m)), native.column_array(prefix_cols(dcols_all, m)))
+            return arrs[m]
+
+        def step(evs=None):
+            for j, m in enumerate(wins):
+                a_in, a_out = arrays(m)
+                ev = evs[j] if evs is not None else None
+                if ev:
+                    ev[0].record()
+                native.encode(plan, a_in, m, frame, None, out, status, ws, stream)
+                if ev:
+                    ev[1].record()
+                native.decode(plan, out, None, m, frame, a_out, status, ws, stream)
+                if ev:
+                    ev[2].record()
+
+        for _ in range(args.warmup):
+            step()
+        native.read_status(status, stream)
+        if wins:
+            bad = check_round_trip(plan, prefix_cols(cols_all, wins[0]), prefix_cols(dcols_all, wins[0]), wins[0])
+            if bad:
+                raise SystemExit(f"round-trip mismatch on the benchmark batch: {bad}")
+        evs = [[[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in wins] for _ in range(args.steps)]
+        recs = [(m, ev) for step_evs in evs for m, ev in zip(wins, step_evs)]
+        barrier(dist)
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(evs[k])
+        barrier(dist)
+        el = max_over_ranks(dist, time.perf_counter() - t0, args.backend)
+        native.read_status(status, stream)
+        enc_ms = [ev[0].elapsed_time(ev[1]) for _, ev in recs]
+        dec_ms = [ev[1].elapsed_time(ev[2]) for _, ev in recs]
+        # dominant kernel: per-launch algorithmic bytes / average launch time (full windows)
+        wmax = max(wins) if wins else 0
+        full = [i for i, (m, _) in enumerate(recs) if m == wmax]
+        enc_avg = sum(enc_ms[i] for i in full) / max(1, len(full))
+        dec_avg = sum(dec_ms[i] for i in full) / max(1, len(full))
+        algo = wmax * (col_row + stride)
+        dom, dom_ms = ("encode", enc_avg) if enc_avg >= dec_avg else ("decode", dec_avg)
+        achieved = algo / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+        value = 2 * total_rows * stride * args.steps / el / 2**30
+        res_weak = None
+        if weak_rows > 0:  # weak-scaling extra: weak_rows records per rank, one window
+            a_in, a_out = arrays(weak_rows)
+            for _ in range(max(1, args.warmup // 2)):
+                native.encode(plan, a_in, weak_rows, frame, None, out, status, ws, stream)
+                native.decode(plan, out, None, weak_rows, frame, a_out, status, ws, stream)
+            barrier(dist)
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                native.encode(plan, a_in, weak_rows, frame, None, out, status, ws, stream)
+                native.decode(plan, out, None, weak_rows, frame, a_out, status, ws, stream)
+            barrier(dist)
+            elw = max_over_ranks(dist, time.perf_counter() - t1, args.backend)
+            native.read_status(status, stream)
+            res_weak = {"value": round(world * 2 * weak_rows * stride * args.steps / elw / 2**30, 3),
+                        "unit": "GiB/s", "scaling": "weak", "rows_per_gpu": weak_rows,
+                        "ms_per_step": round(elw * 1000 / args.steps, 4)}
+        row_bytes_step = total_rows * stride
+        res = {
+            "metric": "row-format encode+decode GiB/s (device-resident), 64M Struct(100 prim) rows",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el * 1000 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (java.util.Random per record, as Struct.createPOJO)",
+            "config": {"workload": f"struct104 {'frame-stream' if frame else 'raw rows'}: BASELINE C4, "
+                                   f"{total_rows} records split over {world} rank(s), windows of <= "
+                                   f"{args.window_rows} records (the 64M-row headline batch)",
+                       "total_rows": total_rows, "rows_per_gpu": share, "windows_per_gpu": len(wins),
+                       "window_rows": wmax, "row_bytes_total": row_bytes_step,
+                       "column_bytes_per_record": col_row, "frame_mode": "stream" if frame else "raw",
+                       "schema_hash": plan.schema_hash,
+                       "parallelism": f"record-sharded x{world} (contiguous ranges), no collective"},
+            "kernels_ms": {"encode_avg": round(enc_avg, 4), "decode_avg": round(dec_avg, 4),
+                           "encode_min": round(min(enc_ms), 4) if enc_ms else None,
+                           "decode_min": round(min(dec_ms), 4) if dec_ms else None},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": pmc_traffic(args.pmc, config, wmax, frame, dom),
+                         "traffic_source": "profiles/pmc_latest.json (rocprofv3 --pmc pass of this command)",
+                         "algorithmic_bytes_per_launch": algo},
+            "step_hbm_frac": round(2 * algo / ((enc_avg + dec_avg) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            if enc_avg + dec_avg > 0 else None,
+        }
+        if res_weak:
+            res["weak"] = res_weak
+    # ------------------------------------------------------------------ varlen
     else:
+        n = share
+        cols = cols_all
+        col_bytes = col_bytes_all
+        arr = native.column_array(cols)
         offs = torch.empty(n + 1, dtype=torch.int64, device=device)
         native.encoded_size(plan, arr, n, frame, offs, ws, stream)
         total = int(offs[n].item())
-    out = torch.empty(max(16, total), dtype=torch.uint8, device=device)
-    # decode targets
-    if plan.fixed_width:
-        dcols = enc.alloc_fixed_outputs(n)
-    else:
+        out = torch.empty(max(16, total), dtype=torch.uint8, device=device)
         native.encode(plan, arr, n, frame, offs, out, status, ws, stream)
         dcols = enc.decode(out[:total], n, frame, offs)
-    darr = native.column_array(dcols)
+        darr = native.column_array(dcols)
 
-    def step(ev=None):
-        # events: 0 | encoded_size | 3 | encode | 1 | decode_sizes | 4 | decode | 2
-        if ev:
-            ev[0].record()
-        if not plan.fixed_width:
+        def step(ev=None):
+            # events: 0 | encoded_size | 3 | encode | 1 | decode_sizes | 4 | decode | 2
+            if ev:
+                ev[0].record()
             native.encoded_size(plan, arr, n, frame, offs, ws, stream)
-        if ev:
-            ev[3].record()
-        native.encode(plan, arr, n, frame, offs, out, status, ws, stream)
-        if ev:
-            ev[1].record()
-        if not plan.fixed_width:
+            if ev:
+                ev[3].record()
+            native.encode(plan, arr, n, frame, offs, out, status, ws, stream)
+            if ev:
+                ev[1].record()
             native.decode_sizes(plan, out, offs, n, frame, darr, status, ws, stream)
-        if ev:
-            ev[4].record()
-        native.decode(plan, out, offs, n, frame, darr, status, ws, stream)
-        if ev:
-            ev[2].record()
+            if ev:
+                ev[4].record()
+            native.decode(plan, out, offs, n, frame, darr, status, ws, stream)
+            if ev:
+                ev[2].record()
 
-    for _ in range(args.warmup):
-        step()
-    native.read_status(status, stream)
-    # correctness guard on the measured data: decode(encode(x)) == x (fixed-width configs)
-    if plan.fixed_width:
-        for a, b in zip(dcols, cols):
-            if not torch.equal(a.values[:n].view(torch.uint8), b.values.view(torch.uint8)):
-                raise SystemExit("round-trip mismatch on the benchmark batch")
-
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
-    barrier(dist)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(evs[k])
-    barrier(dist)
-    el = time.perf_counter() - t0
-    native.read_status(status, stream)
-    t = torch.tensor([el], dtype=torch.float64, device=device)
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
-    enc_ms = sorted(e[0].elapsed_time(e[1]) for e in evs)
-    dec_ms = sorted(e[1].elapsed_time(e[2]) for e in evs)
-    enc_avg = sum(enc_ms) / len(enc_ms)
-    dec_avg = sum(dec_ms) / len(dec_ms)
-    # the encode / decode calls alone (varlen plans: without their sizing passes)
-    enc_k = sum(e[3].elapsed_time(e[1]) for e in evs) / len(evs)
-    dec_k = sum(e[4].elapsed_time(e[2]) for e in evs) / len(evs)
-
-    row_bytes = total  # per GPU per direction
-    value = world * 2 * row_bytes * args.steps / el / 2**30
-    # roofline of the dominant kernel: algorithmic bytes (columns + rows) / its avg duration
-    algo = col_bytes + row_bytes
-    dom, dom_ms = ("encode", enc_k) if enc_k >= dec_k else ("decode", dec_k)
-    achieved = algo / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    try:
-        with open(args.pmc) as fh:
-            pmc = json.load(fh)
-        key = f"{config}:{n}:{frame}"
-        if key in pmc:
-            traffic = pmc[key].get(dom)
-    except (OSError, ValueError):
-        pass
-    res = {
-        "metric": "row-format encode+decode GiB/s (device-resident), 64M Struct(100 prim) rows",
-        "value": round(value, 3),
-        "unit": "GiB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(el * 1000 / args.steps, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (java.util.Random per record, as Struct.createPOJO)" if config == "struct104"
-                else "synthetic (numpy seeded)",
-        "config": {"workload": f"{config} {'frame-stream' if frame else 'raw rows'}, {n} rows per GPU",
-                   "rows_per_gpu": n, "row_bytes_total_per_gpu": row_bytes,
-                   "column_bytes_per_gpu": col_bytes, "frame_mode": "stream" if frame else "raw",
-                   "schema_hash": plan.schema_hash, "parallelism": f"record-sharded x{world}, no collective"},
-        "kernels_ms": {"encode_avg": round(enc_avg, 4), "decode_avg": round(dec_avg, 4),
-                       "encode_min": round(enc_ms[0], 4), "decode_min": round(dec_ms[0], 4),
-                       "encode_call_avg": round(enc_k, 4), "decode_call_avg": round(dec_k, 4)},
-        "roofline": {"bound": "hbm", "kernel": dom if plan.fixed_width else dom + " call (sizing pass excluded)",
-                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_launch": algo},
-        "step_hbm_frac": round(2 * algo / ((enc_avg + dec_avg) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-    }
+        for _ in range(args.warmup):
+            step()
+        native.read_status(status, stream)
+        bad = check_round_trip(plan, cols, dcols, n)
+        if bad:
+            raise SystemExit(f"round-trip mismatch on the benchmark batch: {bad}")
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+        barrier(dist)
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(evs[k])
+        barrier(dist)
+        el = max_over_ranks(dist, time.perf_counter() - t0, args.backend)
+        native.read_status(status, stream)
+        enc_avg = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)  # sizes + scan + encode
+        dec_avg = sum(e[1].elapsed_time(e[2]) for e in evs) / len(evs)  # decode_sizes + decode
+        enc_k = sum(e[3].elapsed_time(e[1]) for e in evs) / len(evs)    # encode call alone
+        dec_k = sum(e[4].elapsed_time(e[2]) for e in evs) / len(evs)    # decode call alone
+        algo = col_bytes + total
+        dom, dom_ms = ("encode", enc_avg) if enc_avg >= dec_avg else ("decode", dec_avg)
+        achieved = algo / (dom_ms * 1e-3) / 1e9
+        row_bytes_all = total
+        if dist is not None:
+            t = torch.tensor([float(total)], dtype=torch.float64,
+                             device="cuda" if args.backend == "nccl" else "cpu")
+            dist.all_reduce(t)
+            row_bytes_all = int(t.item())
+        value = 2 * row_bytes_all * args.steps / el / 2**30
+        res = {
+            "metric": "row-format encode+decode GiB/s (device-resident), 64M Struct(100 prim) rows",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el * 1000 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (numpy seeded)",
+            "config": {"workload": f"{config} {'frame-stream' if frame else 'raw rows'}, {total_rows} records "
+                                   f"split over {world} rank(s)",
+                       "total_rows": total_rows, "rows_per_gpu": n, "row_bytes_total_per_gpu": total,
+                       "column_bytes_per_gpu": col_bytes, "frame_mode": "stream" if frame else "raw",
+                       "schema_hash": plan.schema_hash,
+                       "parallelism": f"record-sharded x{world} (contiguous ranges), no collective"},
+            "kernels_ms": {"encode_avg": round(enc_avg, 4), "decode_avg": round(dec_avg, 4),
+                           "encode_call_avg": round(enc_k, 4), "decode_call_avg": round(dec_k, 4)},
+            "roofline": {"bound": "hbm", "kernel": dom + " (sizing passes included)",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "call_frac": {"encode": round(algo / (enc_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                       "decode": round(algo / (dec_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                         "traffic": pmc_traffic(args.pmc, config, n, frame, dom),
+                         "traffic_source": "profiles/pmc_latest.json (rocprofv3 --pmc pass of this command)",
+                         "algorithmic_bytes_per_launch": algo},
+            "step_hbm_frac": round(2 * algo / ((enc_avg + dec_avg) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # all host cores of this GPU's share (the box allots 16 per GPU), then one core
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
@@ -276,10 +507,24 @@ def main():
         single = cpu_baseline(config, frame, args.cpu_seconds / 2, 1)
         res["cpu_baseline"]["single_core"] = {"value": single["value"], "unit": "GiB/s",
                                               "rows_per_s": single["rows_per_s"], "sample": single["sample"]}
+        res["cpu_baseline"]["reference_jvm"] = jdk_probe()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def pmc_traffic(path, config, n, frame, dom):
+    try:
+        with open(path) as fh:
+            pmc = json.load(fh)
+        key = f"{config}:{n}:{frame}"
+        if key in pmc:
+            return pmc[key].get(dom)
+    except (OSError, ValueError):
+        pass
+    return None
 
 
 if __name__ == "__main__":

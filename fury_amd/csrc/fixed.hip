@@ -1,0 +1,538 @@
+// fixed.hip — gfx950 (CDNA4) kernels for fixed-width row-format schemas.
+//
+// Byte layout restated from the Java writer (the spec doc is empty,
+// docs/specification/row_format_spec.md:22-24). F = java/fory-format/src/
+// main/java/org/apache/fory/format:
+//   row   = [null bitmap ((n+63)/64)*8 B, bit i = byte i>>3 bit i&7, 1 = null]
+//           [n x 8-B slots]                              F/row/binary/writer/BinaryRowWriter.java:46-124
+//   fixed = value in the slot's low bytes, zero-extended            BinaryRowWriter.java:92-124
+//   frame = [i32 8+rowSize][i64 schemaHash][row]                   F/encoder/Encoders.java:213-225
+//
+// Fixed-width schemas (every top-level field 1/2/4/8 bytes) take the tiled
+// path: tiles of records, columns read with coalesced loads, scattered into an
+// LDS image of the tile's rows, and the whole tile (TR * stride contiguous
+// bytes) leaves with 16-B stores. Decode is the inverse: the tile image comes
+// in through LDS-DMA (global_load_lds_dwordx4), each lane reads its record's
+// slots from LDS and stores coalesced columns. No MFMA: this is byte shuffling
+// bound by HBM.
+//
+// Kernels: encode_fixed_v5_kernel (persistent, depth-2 pipelined, 16-byte
+// column chunks; not-null schemas) with encode_fixed_kernel for the tail,
+// nullable schemas and wide rows; decode_fixed_kernel. Rejected variants of
+// round 1 (pipe, v3, v4, one-shot, decode v2/v3/pipe) are gone from the
+// product library; their measurements are in DESIGN.md §6.1.
+#include "kcommon.h"
+
+namespace fory_amd {
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Fixed-width encode: columns -> rows (tiled through LDS)
+// ---------------------------------------------------------------------------
+// One tile = TR records. TR = 64: lane = record, one field per wave
+// instruction (descriptor wave-uniform -> scalar loads). TR = 32/16/8 (wide
+// rows): 64/TR fields per wave instruction. The host sorts the field table
+// into width groups (8/4/2/1 bytes) so every load loop has a compile-time
+// width and distinct destination registers: a batch of U column loads is in
+// flight before the first LDS write. Dead lanes of a partial tile re-read
+// record r0 (no divergent branch around the loads).
+
+template <int TR>
+__device__ __forceinline__ int field_of(int fb, int u, int fstep, int fsub) {
+  const int f = fb + u * fstep + fsub;
+  if constexpr (TR == 64) return __builtin_amdgcn_readfirstlane(f);
+  return f;
+}
+
+// BinaryWriter.setNullAt's input: Arrow validity bit of record idx (nullable fields).
+__device__ __forceinline__ bool input_null(const FixedFieldDev& fd, int64_t idx) {
+  return (fd.flags & 1) && fd.validity && !((load_byte(fd.validity + (idx >> 3)) >> (idx & 7)) & 1);
+}
+
+// Stores a slot into the LDS row image (BinaryRowWriter.write: slot zeroed,
+// value in the low bytes; null -> bit set, slot left zero; bool -> 0/1).
+template <bool FRAME>
+__device__ __forceinline__ void put_slot(uint8_t* row, int hdr_bm, int slot, uint64_t x, bool isnull, int flags) {
+  constexpr int HDR = FRAME ? 12 : 0;
+  if (flags & 2) x = x ? 1 : 0;  // MemoryBuffer.putBoolean
+  if (isnull) {
+    x = 0;
+    atomicOr(reinterpret_cast<uint32_t*>(row + HDR + ((slot >> 5) << 2)), 1u << (slot & 31));
+  }
+  uint8_t* p = row + hdr_bm + 8 * slot;
+  if (FRAME) {  // frame rows start 12 bytes into the frame: slots are only 4-byte aligned
+    st32(p, (uint32_t)x);
+    st32(p + 4, (uint32_t)(x >> 32));
+  } else {
+    *reinterpret_cast<uint64_t*>(p) = x;
+  }
+}
+
+// Frame header [i32 8+rowSize][i64 hash] + zeroed null bitmap of this lane's row.
+template <bool FRAME>
+__device__ __forceinline__ void put_header(uint8_t* row, const FixedLaunch& L) {
+  if (FRAME) {
+    st32(row, (uint32_t)(8 + L.fixed_size));
+    st32(row + 4, (uint32_t)(uint64_t)L.schema_hash);
+    st32(row + 8, (uint32_t)((uint64_t)L.schema_hash >> 32));
+  }
+  constexpr int HDR = FRAME ? 12 : 0;
+  for (int b = 0; b < L.bitmap_bytes; b += 4) st32(row + HDR + b, 0u);
+}
+
+// LDS tile image -> HBM: `bytes` contiguous bytes, 16-B stores, 4 in flight.
+__device__ __forceinline__ void store_tile(const uint8_t* lds, uint8_t* __restrict__ dst, int bytes, int tid) {
+  const int n16 = bytes >> 4;
+  int c = tid;
+  for (; c + 3 * kWG < n16; c += 4 * kWG) {
+    const u32x4 x0 = *reinterpret_cast<const u32x4*>(lds + c * 16);
+    const u32x4 x1 = *reinterpret_cast<const u32x4*>(lds + (c + kWG) * 16);
+    const u32x4 x2 = *reinterpret_cast<const u32x4*>(lds + (c + 2 * kWG) * 16);
+    const u32x4 x3 = *reinterpret_cast<const u32x4*>(lds + (c + 3 * kWG) * 16);
+    *reinterpret_cast<u32x4*>(dst + c * 16) = x0;
+    *reinterpret_cast<u32x4*>(dst + (c + kWG) * 16) = x1;
+    *reinterpret_cast<u32x4*>(dst + (c + 2 * kWG) * 16) = x2;
+    *reinterpret_cast<u32x4*>(dst + (c + 3 * kWG) * 16) = x3;
+  }
+  for (; c < n16; c += kWG) *reinterpret_cast<u32x4*>(dst + c * 16) = *reinterpret_cast<const u32x4*>(lds + c * 16);
+  const int tail4 = (bytes & 15) >> 2;
+  if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
+}
+
+// One width group [g0, g1) of the encode: U loads in flight, then U slots.
+template <int W, int TR, bool FRAME>
+__device__ __forceinline__ void enc_group(const FixedFieldDev* __restrict__ fields, int g0, int g1, int wave, int fsub,
+                                          int64_t idx, uint8_t* row, int hdr_bm) {
+  constexpr int FPW = 64 / TR;
+  constexpr int FSTEP = kWaves * FPW;
+  constexpr int U = 16;
+  for (int pb = g0 + wave * FPW; pb < g1; pb += FSTEP * U) {
+    uint64_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = field_of<TR>(pb, u, FSTEP, fsub);
+      v[u] = p < g1 ? ldw<W>(fields[p].values, idx) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = field_of<TR>(pb, u, FSTEP, fsub);
+      if (p < g1) {
+        const FixedFieldDev& fd = fields[p];
+        put_slot<FRAME>(row, hdr_bm, fd.slot, v[u], input_null(fd, idx), fd.flags);
+      }
+    }
+  }
+}
+
+template <int TR, bool FRAME>
+__global__ __launch_bounds__(kWG) void encode_fixed_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
+                                                           uint8_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int HDR = FRAME ? 12 : 0;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane % TR;
+  const int fsub = lane / TR;
+  const int64_t r0 = (L.tile0 + (int64_t)blockIdx.x) * TR;
+  const int64_t left = L.num_rows - r0;
+  const int rows = left < TR ? (int)left : TR;
+  const int hdr_bm = HDR + L.bitmap_bytes;
+  uint8_t* row = lds + r * L.stride;
+  const int64_t idx = r < rows ? r0 + r : r0;
+
+  if (wave == 0 && fsub == 0) put_header<FRAME>(row, L);
+  if (L.any_nullable) __syncthreads();  // null bits are OR-ed into the zeroed bitmap
+
+  enc_group<8, TR, FRAME>(fields, L.group[0], L.group[1], wave, fsub, idx, row, hdr_bm);
+  enc_group<4, TR, FRAME>(fields, L.group[1], L.group[2], wave, fsub, idx, row, hdr_bm);
+  enc_group<2, TR, FRAME>(fields, L.group[2], L.group[3], wave, fsub, idx, row, hdr_bm);
+  enc_group<1, TR, FRAME>(fields, L.group[3], L.group[4], wave, fsub, idx, row, hdr_bm);
+  __syncthreads();
+  store_tile(lds, out + r0 * L.stride, rows * L.stride, tid);
+}
+
+// Chunk instructions of the 16-byte-chunk encode (v5 below): instruction i of a
+// tile of R records, numbered per width group (8, 4, 2, 1 bytes): its width and
+// its first field; wave v issues v, v + NW, ....
+template <int R>
+__device__ __forceinline__ bool v3_insn_g(int i, const int32_t* group, int* w, int* p0, int* pend) {
+  const int fpi8 = 1024 / (R * 8), fpi4 = 1024 / (R * 4), fpi2 = 1024 / (R * 2), fpi1 = 1024 / R;
+  const int n8 = group[1] - group[0], n4 = group[2] - group[1];
+  const int n2 = group[3] - group[2], n1 = group[4] - group[3];
+  const int i8 = (n8 + fpi8 - 1) / fpi8, i4 = (n4 + fpi4 - 1) / fpi4;
+  const int i2 = (n2 + fpi2 - 1) / fpi2, i1 = (n1 + fpi1 - 1) / fpi1;
+  if (i < i8) { *w = 8; *p0 = group[0] + i * fpi8; *pend = group[1]; return true; }
+  i -= i8;
+  if (i < i4) { *w = 4; *p0 = group[1] + i * fpi4; *pend = group[2]; return true; }
+  i -= i4;
+  if (i < i2) { *w = 2; *p0 = group[2] + i * fpi2; *pend = group[3]; return true; }
+  i -= i2;
+  if (i < i1) { *w = 1; *p0 = group[3] + i * fpi1; *pend = group[4]; return true; }
+  return false;
+}
+
+template <int R>
+__device__ __forceinline__ bool v3_insn(int i, const FixedLaunch& L, int* w, int* p0, int* pend) {
+  return v3_insn_g<R>(i, L.group, w, p0, pend);
+}
+
+template <int R>
+__host__ __device__ inline int v3_insn_count(const int* group) {
+  const int fpi8 = 1024 / (R * 8), fpi4 = 1024 / (R * 4), fpi2 = 1024 / (R * 2), fpi1 = 1024 / R;
+  const int n8 = group[1] - group[0], n4 = group[2] - group[1];
+  const int n2 = group[3] - group[2], n1 = group[4] - group[3];
+  return (n8 + fpi8 - 1) / fpi8 + (n4 + fpi4 - 1) / fpi4 + (n2 + fpi2 - 1) / fpi2 + (n1 + fpi1 - 1) / fpi1;
+}
+
+// ---------------------------------------------------------------------------
+// Encode v5: 16-byte column chunks per lane, depth-2 load pipeline
+// ---------------------------------------------------------------------------
+// Column reads are the encode's limiter: 4/8-byte loads of 256-byte column
+// segments reach ~1.6 TB/s at two workgroups per CU, while 16-byte loads of
+// >= 512-byte segments reach ~5.9 TB/s (scripts/microbench/colread.hip). So each
+// lane loads one 16-byte chunk of ONE field's column segment (E = 16/w
+// consecutive records) and scatters its E values into the LDS row image. A
+// field of width w spans CPF = R*w/16 chunks per tile; one wave instruction
+// (64 x 16 B) covers FPI = 64/CPF fields (v3_insn_g numbers the instructions per
+// width group). Persistent workgroups; two tiles of column chunks are in flight
+// per workgroup (register sets A/B, the loop unrolled by 2 so both stay
+// static). Every lane issues exactly K loads per tile (inactive lanes / absent
+// instructions re-read a valid dummy address), so hipcc waits with a counted
+// vmcnt for the older set while the younger set stays in flight. Order per
+// stage: write X -> barrier -> store this tile's rows -> issue X for tile +
+// 2*grid -> barrier. Not-null schemas only (the nullable form spills).
+template <int R, int K>
+__device__ __forceinline__ void v5_issue(const uint8_t* const (&ptr)[K], const int (&wk)[K], int64_t r0,
+                                         u32x4 (&d)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) d[k] = *gp(reinterpret_cast<const u32x4*>(ptr[k] + r0 * wk[k]));
+}
+
+template <int R, int K, bool FRAME>
+__device__ __forceinline__ void v5_write(uint8_t* lds, int stride, int hdr_bm, const int (&wk)[K],
+                                         const uint32_t (&sf)[K], const u32x4 (&d)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int w = wk[k];
+    if (!(sf[k] & (1u << 20))) continue;
+    const int slot = sf[k] & 0xffff, flags = (sf[k] >> 16) & 0xf, rb = sf[k] >> 21;
+    uint8_t* row = lds + rb * stride;
+    const u32x4 x = d[k];
+    if (w == 8) {
+      put_slot<FRAME>(row, hdr_bm, slot, (uint64_t)x.x | ((uint64_t)x.y << 32), false, flags);
+      put_slot<FRAME>(row + stride, hdr_bm, slot, (uint64_t)x.z | ((uint64_t)x.w << 32), false, flags);
+    } else if (w == 4) {
+      put_slot<FRAME>(row, hdr_bm, slot, x.x, false, flags);
+      put_slot<FRAME>(row + stride, hdr_bm, slot, x.y, false, flags);
+      put_slot<FRAME>(row + 2 * stride, hdr_bm, slot, x.z, false, flags);
+      put_slot<FRAME>(row + 3 * stride, hdr_bm, slot, x.w, false, flags);
+    } else if (w == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        put_slot<FRAME>(row + e * stride, hdr_bm, slot, (x[e >> 1] >> (16 * (e & 1))) & 0xffff, false, flags);
+    } else if (w == 1) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        put_slot<FRAME>(row + e * stride, hdr_bm, slot, (x[e >> 2] >> (8 * (e & 3))) & 0xff, false, flags);
+    }
+  }
+}
+
+// The tile's rows (R * stride contiguous bytes) leave with non-temporal 16-B
+// stores: the once-written row stream does not displace L2 lines
+// (18.43 -> 18.03 ms at 64M Struct104 rows).
+template <int R, int WG>
+__device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* lds, uint8_t* dst, int tid) {
+  const int bytes = R * L.stride;
+  const int n16 = bytes >> 4;
+  for (int c = tid; c < n16; c += WG)
+    __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(lds + c * 16), gp(reinterpret_cast<u32x4*>(dst + c * 16)));
+  const int tail4 = (bytes & 15) >> 2;
+  if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
+}
+
+template <int R, int WG, int K, bool FRAME>
+__global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
+                                                                 const FixedFieldDev* __restrict__ fields,
+                                                                 uint8_t* __restrict__ out, int64_t tiles) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int NW = WG / 64;
+  constexpr int HDR = FRAME ? 12 : 0;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int stride = L.stride;
+  const int hdr_bm = HDR + L.bitmap_bytes;
+  int64_t t = blockIdx.x;
+  if (t >= tiles) return;
+
+  const uint8_t* dummy = fields[L.group[0]].values;  // any valid column (never null: num_rows > 0)
+  const uint8_t* ptr[K];
+  int wk[K];
+  uint32_t sf[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    int w = 0, p0 = 0, pend = 0;
+    const bool ok = v3_insn<R>(wave + k * NW, L, &w, &p0, &pend);
+    wk[k] = ok ? w : 0;  // absent instruction: width 0 -> re-reads the dummy address
+    const int cpf = R * (ok ? w : 8) / 16;
+    const int p = p0 + lane / cpf, c = lane % cpf;
+    ptr[k] = dummy;
+    sf[k] = 0;
+    if (ok && p < pend) {
+      const FixedFieldDev& fd = fields[p];
+      ptr[k] = fd.values + c * 16;
+      sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (1u << 20) | ((uint32_t)(c * (16 / w)) << 21);
+    }
+  }
+  if (tid < R) put_header<FRAME>(lds + tid * stride, L);  // constant across tiles (no nullable fields)
+  u32x4 dA[K], dB[K];
+  const int64_t last = tiles - 1;
+  v5_issue<R, K>(ptr, wk, t * R, dA);
+  v5_issue<R, K>(ptr, wk, min(t + (int64_t)gridDim.x, last) * R, dB);
+  for (;;) {
+    v5_write<R, K, FRAME>(lds, stride, hdr_bm, wk, sf, dA);
+    __syncthreads();
+    v5_store<R, WG>(L, lds, out + t * R * stride, tid);
+    v5_issue<R, K>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dA);
+    __syncthreads();
+    t += gridDim.x;
+    if (t >= tiles) break;
+    v5_write<R, K, FRAME>(lds, stride, hdr_bm, wk, sf, dB);
+    __syncthreads();
+    v5_store<R, WG>(L, lds, out + t * R * stride, tid);
+    v5_issue<R, K>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dB);
+    __syncthreads();
+    t += gridDim.x;
+    if (t >= tiles) break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fixed-width decode: rows -> columns
+// ---------------------------------------------------------------------------
+// LDS-DMA of `bytes` contiguous bytes into the LDS image (1 KiB per wave
+// instruction; lanes past the end masked off).
+// NT & 4: non-temporal policy (aux = 2) on the once-read row stream.
+template <int NT = 0>
+__device__ __forceinline__ void dma_tile(uint8_t* lds, const uint8_t* __restrict__ src, int bytes, int tid, int wave) {
+  const int n16 = bytes >> 4;
+  for (int c0 = 0; c0 < n16; c0 += kWG) {
+    const int c = c0 + tid;
+    if (c < n16)
+      __builtin_amdgcn_global_load_lds((const GAS void*)(src + (int64_t)c * 16),
+                                       (__attribute__((address_space(3))) void*)(lds + (c0 + wave * 64) * 16), 16,
+                                       0, (NT & 4) ? 2 : 0);
+  }
+  const int tail4 = (bytes & 15) >> 2;
+  if (tid < tail4) st32(lds + n16 * 16 + tid * 4, ld32(src + n16 * 16 + tid * 4));
+}
+
+template <bool FRAME>
+__device__ __forceinline__ void check_frame(const uint8_t* row, const FixedLaunch& L, int32_t* status) {
+  // Encoders.decode (Encoders.java:177-190): size, then the schema hash.
+  const uint32_t len = ld32(row);
+  const uint64_t h = (uint64_t)ld32(row + 4) | ((uint64_t)ld32(row + 8) << 32);
+  if (h != (uint64_t)L.schema_hash) set_status(status, FORY_ERR_SCHEMA_MISMATCH);
+  else if (len != (uint32_t)(8 + L.fixed_size)) set_status(status, FORY_ERR_CORRUPT);
+}
+
+// Slot of an LDS row (UnsafeTrait.getX: the low W bytes).
+template <int W, bool FRAME>
+__device__ __forceinline__ uint64_t get_slot(const uint8_t* row, int hdr_bm, int slot) {
+  const uint8_t* p = row + hdr_bm + 8 * slot;
+  if constexpr (W == 8) {
+    if (FRAME) return (uint64_t)ld32(p) | ((uint64_t)ld32(p + 4) << 32);
+    return *reinterpret_cast<const uint64_t*>(p);
+  }
+  return ld32(p);
+}
+
+// Arrow validity of field fd for the TR records of this lane group.
+template <int TR>
+__device__ __forceinline__ void put_validity(const FixedFieldDev& fd, bool isnull, bool live, int r, int fsub,
+                                             int64_t r0, int rows) {
+  const uint64_t m = __ballot(!isnull && live);
+  if (r == 0) {
+    const uint64_t mine = (m >> (fsub * TR)) & (TR == 64 ? ~0ull : ((1ull << TR) - 1));
+    uint8_t* vb = fd.out_validity + (r0 >> 3);
+    const int nb = (rows + 7) >> 3;
+    for (int b = 0; b < nb; ++b) store_byte(vb + b, (uint8_t)(mine >> (8 * b)));
+  }
+}
+
+// Decodes slot values of one width group: null -> 0 (RowEncoderBuilder.java:239-246),
+// bool -> 0/1 (MemoryBuffer.getBoolean), coalesced column stores.
+template <int W, int TR, bool FRAME, int NT = 0>
+__device__ __forceinline__ void dec_group(const FixedFieldDev* __restrict__ fields, int g0, int g1, int wave, int fsub,
+                                          int r, const uint8_t* row, int hdr_bm, int hdr, bool live, int64_t grow,
+                                          int64_t r0, int rows) {
+  constexpr int FPW = 64 / TR;
+  constexpr int FSTEP = kWaves * FPW;
+  constexpr int U = 8;
+  for (int pb = g0 + wave * FPW; pb < g1; pb += FSTEP * U) {
+    uint64_t x[U];
+    bool nul[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = field_of<TR>(pb, u, FSTEP, fsub);
+      x[u] = 0;
+      nul[u] = true;
+      if (p < g1) {
+        const int slot = fields[p].slot;
+        nul[u] = (ld32(row + hdr + ((slot >> 5) << 2)) >> (slot & 31)) & 1;  // BinaryRow.isNullAt
+        x[u] = get_slot<W, FRAME>(row, hdr_bm, slot);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = field_of<TR>(pb, u, FSTEP, fsub);
+      if (p < g1) {
+        const FixedFieldDev& fd = fields[p];
+        uint64_t v = nul[u] ? 0 : x[u];
+        if (fd.flags & 2) v = (v & 0xff) ? 1 : 0;
+        if (live) {
+          if constexpr ((NT & 8) && W >= 4) {  // non-temporal column stores
+            if constexpr (W == 8) __builtin_nontemporal_store(v, gp(reinterpret_cast<uint64_t*>(fd.out_values)) + grow);
+            else __builtin_nontemporal_store((uint32_t)v, gp(reinterpret_cast<uint32_t*>(fd.out_values)) + grow);
+          } else {
+            stw<W>(fd.out_values, grow, v);
+          }
+        }
+        if ((fd.flags & 1) && fd.out_validity) put_validity<TR>(fd, nul[u], live, r, fsub, r0, rows);
+      }
+    }
+  }
+}
+
+template <int TR, bool FRAME, int NT = 0>
+__global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
+                                                           const uint8_t* __restrict__ in, int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int HDR = FRAME ? 12 : 0;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane % TR;
+  const int fsub = lane / TR;
+  const int64_t r0 = (L.tile0 + (int64_t)blockIdx.x) * TR;
+  const int64_t left = L.num_rows - r0;
+  const int rows = left < TR ? (int)left : TR;
+  const int stride = L.stride;
+  const int hdr_bm = HDR + L.bitmap_bytes;
+
+  dma_tile<NT>(lds, in + r0 * stride, rows * stride, tid, wave);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const uint8_t* row = lds + r * stride;
+  const int64_t grow = r0 + r;
+  const bool live = r < rows;
+  if (FRAME && wave == 0 && fsub == 0 && live) check_frame<FRAME>(row, L, status);
+  dec_group<8, TR, FRAME, NT>(fields, L.group[0], L.group[1], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<4, TR, FRAME, NT>(fields, L.group[1], L.group[2], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<2, TR, FRAME, NT>(fields, L.group[2], L.group[3], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<1, TR, FRAME, NT>(fields, L.group[3], L.group[4], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+}
+
+// ---------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------
+// Encode v5: R = 64 records per tile, 512 threads, <= 6 chunk loads per wave per
+// tile (Struct104: 39 load instructions over 8 waves), nt row stores.
+constexpr int kV5R = 64, kV5WG = 512, kV5K = 6;
+
+template <bool FRAME>
+hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
+  const int64_t full = L.num_rows / kV5R;
+  if (full > 0) {
+    auto* k = &encode_fixed_v5_kernel<kV5R, kV5WG, kV5K, FRAME>;
+    raise_lds_cap(k);
+    const size_t lds = (size_t)kV5R * L.stride;
+    const int64_t grid = persistent_grid(k, lds, full, kV5WG);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kV5WG), lds, s, L, L.fields, out, full);
+  }
+  if (L.num_rows > full * kV5R) {  // tail (< R records): one-tile kernel
+    FixedLaunch T = L;
+    T.tile0 = full * kV5R / 64;
+    auto* k = &encode_fixed_kernel<64, FRAME>;
+    raise_lds_cap(k);
+    const int64_t tail_tiles = (L.num_rows - full * kV5R + 63) / 64;
+    hipLaunchKernelGGL(k, dim3((unsigned)tail_tiles), dim3(kWG), (size_t)64 * L.stride, s, T, L.fields, out);
+  }
+  return hipGetLastError();
+}
+
+template <int TR, bool FRAME>
+hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
+  const int64_t tiles = (L.num_rows + TR - 1) / TR;
+  const size_t lds = (size_t)TR * L.stride;
+  if constexpr (TR == 64) {
+    // v5: not-null schemas whose chunk instructions fit K per wave
+    if (!L.any_nullable && (v3_insn_count<kV5R>(L.group) + kV5WG / 64 - 1) / (kV5WG / 64) <= kV5K)
+      return launch_encode_v5<FRAME>(L, out, s);
+  }
+  auto* k = &encode_fixed_kernel<TR, FRAME>;
+  raise_lds_cap(k);
+  hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(kWG), lds, s, L, L.fields, out);
+  return hipGetLastError();
+}
+
+template <int TR, bool FRAME>
+hipError_t launch_decode_tr(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
+  const int64_t tiles = (L.num_rows + TR - 1) / TR;
+  const size_t lds = (size_t)TR * L.stride;
+  // TR = 64: non-temporal LDS-DMA row loads + column stores (17.72 -> 17.52 ms at 64M Struct104)
+  auto* k = TR == 64 ? &decode_fixed_kernel<TR, FRAME, 12> : &decode_fixed_kernel<TR, FRAME, 0>;
+  raise_lds_cap(k);
+  hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(kWG), lds, s, L, L.fields, in, status);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// Records per tile: 64 (one field per wave-instruction) while a tile fits
+// 80 KiB of LDS (two workgroups per CU), else fewer records, more fields.
+static int pick_tr(int stride) {
+  if (64 * stride <= 80 * 1024) return 64;
+  if (32 * stride <= 80 * 1024) return 32;
+  if (16 * stride <= 80 * 1024) return 16;
+  if (8 * stride <= 160 * 1024) return 8;
+  return 0;
+}
+
+hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
+  if (L.num_rows <= 0) return hipSuccess;
+  switch (pick_tr(L.stride) * 2 + (L.frame ? 1 : 0)) {
+    case 128: return launch_encode_tr<64, false>(L, out, s);
+    case 129: return launch_encode_tr<64, true>(L, out, s);
+    case 64: return launch_encode_tr<32, false>(L, out, s);
+    case 65: return launch_encode_tr<32, true>(L, out, s);
+    case 32: return launch_encode_tr<16, false>(L, out, s);
+    case 33: return launch_encode_tr<16, true>(L, out, s);
+    case 16: return launch_encode_tr<8, false>(L, out, s);
+    case 17: return launch_encode_tr<8, true>(L, out, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_decode_fixed(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
+  if (L.num_rows <= 0) return hipSuccess;
+  switch (pick_tr(L.stride) * 2 + (L.frame ? 1 : 0)) {
+    case 128: return launch_decode_tr<64, false>(L, in, status, s);
+    case 129: return launch_decode_tr<64, true>(L, in, status, s);
+    case 64: return launch_decode_tr<32, false>(L, in, status, s);
+    case 65: return launch_decode_tr<32, true>(L, in, status, s);
+    case 32: return launch_decode_tr<16, false>(L, in, status, s);
+    case 33: return launch_decode_tr<16, true>(L, in, status, s);
+    case 16: return launch_decode_tr<8, false>(L, in, status, s);
+    case 17: return launch_decode_tr<8, true>(L, in, status, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+bool fixed_tiled_supported(int stride) { return pick_tr(stride) != 0; }
+
+}  // namespace fory_amd

@@ -364,8 +364,11 @@ constexpr int32_t kKindFixed = 0, kKindBool = 1, kKindBytes = 2, kKindStruct = 3
 bool has_offsets(int32_t k) { return k == kKindBytes || k == kKindList || k == kKindMap; }
 
 // Grows a context-owned device buffer (synchronising the context's stream first).
+// Regrowing dbuf or drows frees what a staged decode (host_decode_var_sizes ->
+// host_decode_var) points into, so it also drops that staged state.
 int ensure(fory_host_ctx* c, uint8_t** buf, int64_t* have, int64_t need) {
   if (need <= *have) return FORY_OK;
+  if (buf == &c->dbuf || buf == &c->drows) c->dec_n = -1;
   int rc = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize");
   if (rc) return rc;
   if (*buf) (void)hipFree(*buf);
@@ -429,6 +432,9 @@ int fory_rowfmt_host_encode_var(fory_host_ctx* c, const fory_column* host_cols, 
     return FORY_OK;
   }
   if (!host_cols || !host_out) return fail_host(FORY_ERR_INVALID_ARGUMENT, "host columns or output is null");
+  // the encode reuses the device buffers a staged decode lives in: a later
+  // host_decode_var must be preceded by a fresh host_decode_var_sizes
+  c->dec_n = -1;
   const int N = c->info.num_columns;
   // element count and value bytes of every column, from the host offsets
   std::vector<int64_t> cnt(N, 0), vbytes(N, 0);
@@ -510,6 +516,9 @@ int fory_rowfmt_host_decode_var_sizes(fory_host_ctx* c, const void* host_rows, c
   if (r1 > r0)
     rc = hip_check(hipMemcpyAsync(drow0, static_cast<const uint8_t*>(host_rows) + r0, (size_t)(r1 - r0),
                                   hipMemcpyHostToDevice, c->s_k), "H2D rows");
+  // row offsets relative to the staged run (its first byte at drow0)
+  std::vector<int64_t> rel_offs((size_t)n + 1);
+  for (int64_t k = 0; k <= n; ++k) rel_offs[(size_t)k] = host_row_offsets[k] - r0;
   // element counts: top level n; struct fields as their struct; list/map elements
   // from the container totals (pass 1), string/binary elements' bytes (pass 2)
   std::vector<int64_t> cnt(N, -1), vbytes(N, 0);
@@ -545,11 +554,11 @@ int fory_rowfmt_host_decode_var_sizes(fory_host_ctx* c, const void* host_rows, c
       if (kc[i] < 0) d[i] = fory_column{};
     }
     // the row offsets' place moves with the layout: copy them for every pass
-    rc = hip_check(hipMemcpyAsync(d_offs, host_row_offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->s_k),
+    rc = hip_check(hipMemcpyAsync(d_offs, rel_offs.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->s_k),
                    "H2D row offsets");
     if (!rc) rc = hip_check(hipMemsetAsync(status, 0, 4, c->s_k), "hipMemsetAsync");
     if (!rc)
-      rc = fory_rowfmt_decode_sizes(c->plan, drow0 - r0, d_offs, n, frame, d.data(), status, ws, ws_bytes, c->s_k);
+      rc = fory_rowfmt_decode_sizes(c->plan, drow0, d_offs, n, frame, d.data(), status, ws, ws_bytes, c->s_k);
     std::vector<int32_t> tot(N, 0);
     for (int i = 0; i < N && !rc; ++i)
       if (d[i].offsets && kc[i] >= 0)
@@ -633,8 +642,7 @@ int fory_rowfmt_host_decode_var(fory_host_ctx* c, const fory_column* host_out_co
   if (!rc) rc = hip_check(hipMemsetAsync(status, 0, 4, c->s_k), "hipMemsetAsync");
   uint8_t* drow0 = c->drows + (c->dec_r0 & 15);
   if (!rc)
-    rc = fory_rowfmt_decode(c->plan, drow0 - c->dec_r0, d_offs, n, c->dec_frame, d.data(), status, ws, ws_bytes,
-                            c->s_k);
+    rc = fory_rowfmt_decode(c->plan, drow0, d_offs, n, c->dec_frame, d.data(), status, ws, ws_bytes, c->s_k);
   for (int i = 0; i < N && !rc; ++i) {  // D2H of every column
     const fory_column& h = host_out_cols[i];
     if (d[i].values && c->dec_bytes[i] > 0)

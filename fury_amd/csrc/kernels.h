@@ -1,4 +1,5 @@
-// kernels.h — launchers for the gfx950 row-format kernels (kernels.hip).
+// kernels.h — launchers for the gfx950 row-format kernels (fixed.hip, scan.hip,
+// varlen.hip; launch state in launch_state.cpp).
 #pragma once
 
 #include <hip/hip_runtime.h>

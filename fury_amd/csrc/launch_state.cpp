@@ -1,0 +1,88 @@
+// launch_state.cpp — per-device launch state of the kernel files, thread-safe.
+//
+// The C-ABI promises that plans may be shared across threads and streams
+// (include/fory_rowfmt.h) and the host path keeps one context per device, so
+// a process can drive several GPUs from several host threads. Everything a
+// launch caches about a device lives here behind one mutex, keyed by the
+// device current on the calling thread:
+//   - the 160 KiB dynamic-LDS attribute of every kernel (hipFuncSetAttribute),
+//     set once per (kernel, device) before that kernel's first launch there;
+//   - the CU count (hipGetDeviceProperties) per device;
+//   - occupancy answers (hipOccupancyMaxActiveBlocksPerMultiprocessor) per
+//     (kernel, device, threads, LDS bytes) — the tile kernels size their LDS
+//     images and staging slots by querying many candidate sizes.
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <set>
+#include <tuple>
+#include <utility>
+
+namespace fory_amd {
+
+namespace {
+
+std::mutex g_mu;
+
+int current_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  return dev;
+}
+
+std::set<std::pair<const void*, int>>& lds_done() {
+  static std::set<std::pair<const void*, int>> s;
+  return s;
+}
+
+std::map<int, int>& cus_cache() {
+  static std::map<int, int> m;
+  return m;
+}
+
+std::map<std::tuple<const void*, int, int, size_t>, int>& occ_cache() {
+  static std::map<std::tuple<const void*, int, int, size_t>, int> m;
+  return m;
+}
+
+}  // namespace
+
+void ensure_lds_cap(const void* kernel) {
+  const int dev = current_device();
+  std::lock_guard<std::mutex> lock(g_mu);
+  if (!lds_done().insert({kernel, dev}).second) return;
+  (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+int num_cus() {
+  const int dev = current_device();
+  std::lock_guard<std::mutex> lock(g_mu);
+  auto it = cus_cache().find(dev);
+  if (it != cus_cache().end()) return it->second;
+  int cus = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+  if (cus <= 0) cus = 256;
+  cus_cache()[dev] = cus;
+  return cus;
+}
+
+int occupancy(const void* kernel, int threads, size_t lds) {
+  const int dev = current_device();
+  const auto key = std::make_tuple(kernel, dev, threads, lds);
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
+    auto it = occ_cache().find(key);
+    if (it != occ_cache().end()) return it->second;
+  }
+  // the attribute must be in place before the query (LDS above the 64 KiB default)
+  ensure_lds_cap(kernel);
+  int blocks = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kernel, threads, lds) != hipSuccess) blocks = 0;
+  std::lock_guard<std::mutex> lock(g_mu);
+  occ_cache()[key] = blocks;
+  return blocks;
+}
+
+}  // namespace fory_amd

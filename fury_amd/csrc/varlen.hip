@@ -1,1282 +1,27 @@
-// kernels.hip — gfx950 (CDNA4) kernels for Fory's row format.
+// varlen.hip — gfx950 kernels for varlen / nested row-format schemas
+// (strings, binary, lists, maps, nested structs, collection frames).
 //
-// Byte layout restated from the Java writer (the spec doc is empty,
-// docs/specification/row_format_spec.md:22-24). F = java/fory-format/src/
-// main/java/org/apache/fory/format:
-//   row   = [null bitmap ((n+63)/64)*8 B, bit i = byte i>>3 bit i&7, 1 = null]
-//           [n x 8-B slots][variable section]      F/row/binary/writer/BinaryRowWriter.java:46-124
-//   fixed = value in the slot's low bytes, zero-extended            BinaryRowWriter.java:92-124
+// Byte layout restated from the Java writer (F = java/fory-format/src/main/java/
+// org/apache/fory/format):
 //   var   = slot (relOffset<<32 | size), data appended in ordinal
-//           order, zero-padded to 8                                F/.../writer/BinaryWriter.java:106-194
-//   array = [i64 n][bitmap][n x elemSize padded to 8]              F/.../writer/BinaryArrayWriter.java:93-118
+//           order, zero-padded to 8                                F/row/binary/writer/BinaryWriter.java:106-194
+//   array = [i64 n][bitmap][n x elemSize padded to 8]              F/row/binary/writer/BinaryArrayWriter.java:93-118
+//   map   = [i64 keyArrayBytes][key array][value array]            F/row/binary/BinaryMap.java:30-77
+//   struct= child row inline at the field's writerIndex           F/encoder/BaseBinaryEncoderBuilder.java:436-490
 //   frame = [i32 8+rowSize][i64 schemaHash][row]                   F/encoder/Encoders.java:213-225
 //
-// Fixed-width schemas (every top-level field 1/2/4/8 bytes) take the tiled
-// path: one workgroup per tile of TR records, one lane per record. Columns
-// are read with coalesced per-lane loads (lane = record, consecutive
-// addresses), scattered into an LDS image of the tile's rows, and the whole
-// tile (TR * stride contiguous bytes) leaves with 16-B stores. Decode is the
-// inverse: the tile image comes in through LDS-DMA (global_load_lds_dwordx4),
-// each lane reads its record's slots from LDS and stores coalesced columns.
-// No MFMA: this is byte shuffling bound by HBM.
-//
-// Varlen / nested schemas run a per-record op program (plan.cpp) in one lane
-// per record, with a device-wide scan for row offsets.
-#include <hip/hip_runtime.h>
+// Row sizes come from a sizes pass + device scan (row offsets); the encode and
+// decode run either the cooperative tile kernels (one workgroup per 64-record
+// tile, row image in LDS), the generic one-wave tile interpreter (maps, List<Bean>,
+// string list elements, collection frames) or the per-record global interpreter
+// (tiles beyond every LDS budget).
+#include <mutex>
 
-#include <cstdio>
-
-#include <cstdint>
-#include <cstdlib>
-
-#include "kernels.h"
+#include "kcommon.h"
 
 namespace fory_amd {
 
 namespace {
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native 16-B vector (SROA-friendly)
-
-constexpr int kWG = 256;         // 4 waves
-constexpr int kWaves = kWG / 64;
-
-__device__ __forceinline__ void st32(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
-__device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
-
-// Pointers read from a descriptor table are generic (flat) to the compiler;
-// a flat access forces s_waitcnt vmcnt(0) lgkmcnt(0) before any dependent
-// use. Cast them to the global address space so loads/stores are global_*.
-#define GAS __attribute__((address_space(1)))
-template <typename T>
-__device__ __forceinline__ const GAS T* gp(const T* p) { return (const GAS T*)p; }
-template <typename T>
-__device__ __forceinline__ GAS T* gp(T* p) { return (GAS T*)p; }
-
-// Loads the `width` low bytes of element `i` (little-endian, zero-extended).
-__device__ __forceinline__ uint64_t load_elem(const uint8_t* base, int width, int64_t i) {
-  switch (width) {
-    case 8: return *gp(reinterpret_cast<const uint64_t*>(base + i * 8));
-    case 4: return *gp(reinterpret_cast<const uint32_t*>(base + i * 4));
-    case 2: return *gp(reinterpret_cast<const uint16_t*>(base + i * 2));
-    default: return *gp(base + i);
-  }
-}
-
-__device__ __forceinline__ void store_elem(uint8_t* base, int width, int64_t i, uint64_t v) {
-  switch (width) {
-    case 8: *gp(reinterpret_cast<uint64_t*>(base + i * 8)) = v; break;
-    case 4: *gp(reinterpret_cast<uint32_t*>(base + i * 4)) = (uint32_t)v; break;
-    case 2: *gp(reinterpret_cast<uint16_t*>(base + i * 2)) = (uint16_t)v; break;
-    default: *gp(base + i) = (uint8_t)v; break;
-  }
-}
-
-__device__ __forceinline__ uint8_t load_byte(const uint8_t* p) { return *gp(p); }
-__device__ __forceinline__ void store_byte(uint8_t* p, uint8_t v) { *gp(p) = v; }
-
-__device__ __forceinline__ void set_status(int32_t* status, int32_t code) {
-  if (status) atomicCAS(status, 0, code);
-}
-
-// ---------------------------------------------------------------------------
-// Fixed-width encode: columns -> rows (tiled through LDS)
-// ---------------------------------------------------------------------------
-// One tile = TR records. TR = 64: lane = record, one field per wave
-// instruction (descriptor wave-uniform -> scalar loads). TR = 32/16/8 (wide
-// rows): 64/TR fields per wave instruction. The host sorts the field table
-// into width groups (8/4/2/1 bytes) so every load loop has a compile-time
-// width and distinct destination registers: a batch of U column loads is in
-// flight before the first LDS write. Dead lanes of a partial tile re-read
-// record r0 (no divergent branch around the loads).
-
-template <int TR>
-__device__ __forceinline__ int field_of(int fb, int u, int fstep, int fsub) {
-  const int f = fb + u * fstep + fsub;
-  if constexpr (TR == 64) return __builtin_amdgcn_readfirstlane(f);
-  return f;
-}
-
-template <int W>
-__device__ __forceinline__ uint64_t ldw(const uint8_t* base, int64_t i) {
-  if constexpr (W == 8) return *gp(reinterpret_cast<const uint64_t*>(base) + i);
-  if constexpr (W == 4) return *gp(reinterpret_cast<const uint32_t*>(base) + i);
-  if constexpr (W == 2) return *gp(reinterpret_cast<const uint16_t*>(base) + i);
-  return *gp(base + i);
-}
-
-template <int W>
-__device__ __forceinline__ void stw(uint8_t* base, int64_t i, uint64_t v) {
-  if constexpr (W == 8) *gp(reinterpret_cast<uint64_t*>(base) + i) = v;
-  else if constexpr (W == 4) *gp(reinterpret_cast<uint32_t*>(base) + i) = (uint32_t)v;
-  else if constexpr (W == 2) *gp(reinterpret_cast<uint16_t*>(base) + i) = (uint16_t)v;
-  else *gp(base + i) = (uint8_t)v;
-}
-
-// BinaryWriter.setNullAt's input: Arrow validity bit of record idx (nullable fields).
-__device__ __forceinline__ bool input_null(const FixedFieldDev& fd, int64_t idx) {
-  return (fd.flags & 1) && fd.validity && !((load_byte(fd.validity + (idx >> 3)) >> (idx & 7)) & 1);
-}
-
-// Stores a slot into the LDS row image (BinaryRowWriter.write: slot zeroed,
-// value in the low bytes; null -> bit set, slot left zero; bool -> 0/1).
-template <bool FRAME>
-__device__ __forceinline__ void put_slot(uint8_t* row, int hdr_bm, int slot, uint64_t x, bool isnull, int flags) {
-  constexpr int HDR = FRAME ? 12 : 0;
-  if (flags & 2) x = x ? 1 : 0;  // MemoryBuffer.putBoolean
-  if (isnull) {
-    x = 0;
-    atomicOr(reinterpret_cast<uint32_t*>(row + HDR + ((slot >> 5) << 2)), 1u << (slot & 31));
-  }
-  uint8_t* p = row + hdr_bm + 8 * slot;
-  if (FRAME) {  // frame rows start 12 bytes into the frame: slots are only 4-byte aligned
-    st32(p, (uint32_t)x);
-    st32(p + 4, (uint32_t)(x >> 32));
-  } else {
-    *reinterpret_cast<uint64_t*>(p) = x;
-  }
-}
-
-// Frame header [i32 8+rowSize][i64 hash] + zeroed null bitmap of this lane's row.
-template <bool FRAME>
-__device__ __forceinline__ void put_header(uint8_t* row, const FixedLaunch& L) {
-  if (FRAME) {
-    st32(row, (uint32_t)(8 + L.fixed_size));
-    st32(row + 4, (uint32_t)(uint64_t)L.schema_hash);
-    st32(row + 8, (uint32_t)((uint64_t)L.schema_hash >> 32));
-  }
-  constexpr int HDR = FRAME ? 12 : 0;
-  for (int b = 0; b < L.bitmap_bytes; b += 4) st32(row + HDR + b, 0u);
-}
-
-// LDS tile image -> HBM: `bytes` contiguous bytes, 16-B stores, 4 in flight.
-__device__ __forceinline__ void store_tile(const uint8_t* lds, uint8_t* __restrict__ dst, int bytes, int tid) {
-  const int n16 = bytes >> 4;
-  int c = tid;
-  for (; c + 3 * kWG < n16; c += 4 * kWG) {
-    const u32x4 x0 = *reinterpret_cast<const u32x4*>(lds + c * 16);
-    const u32x4 x1 = *reinterpret_cast<const u32x4*>(lds + (c + kWG) * 16);
-    const u32x4 x2 = *reinterpret_cast<const u32x4*>(lds + (c + 2 * kWG) * 16);
-    const u32x4 x3 = *reinterpret_cast<const u32x4*>(lds + (c + 3 * kWG) * 16);
-    *reinterpret_cast<u32x4*>(dst + c * 16) = x0;
-    *reinterpret_cast<u32x4*>(dst + (c + kWG) * 16) = x1;
-    *reinterpret_cast<u32x4*>(dst + (c + 2 * kWG) * 16) = x2;
-    *reinterpret_cast<u32x4*>(dst + (c + 3 * kWG) * 16) = x3;
-  }
-  for (; c < n16; c += kWG) *reinterpret_cast<u32x4*>(dst + c * 16) = *reinterpret_cast<const u32x4*>(lds + c * 16);
-  const int tail4 = (bytes & 15) >> 2;
-  if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
-}
-
-// One width group [g0, g1) of the encode: U loads in flight, then U slots.
-template <int W, int TR, bool FRAME>
-__device__ __forceinline__ void enc_group(const FixedFieldDev* __restrict__ fields, int g0, int g1, int wave, int fsub,
-                                          int64_t idx, uint8_t* row, int hdr_bm) {
-  constexpr int FPW = 64 / TR;
-  constexpr int FSTEP = kWaves * FPW;
-  constexpr int U = 16;
-  for (int pb = g0 + wave * FPW; pb < g1; pb += FSTEP * U) {
-    uint64_t v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int p = field_of<TR>(pb, u, FSTEP, fsub);
-      v[u] = p < g1 ? ldw<W>(fields[p].values, idx) : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int p = field_of<TR>(pb, u, FSTEP, fsub);
-      if (p < g1) {
-        const FixedFieldDev& fd = fields[p];
-        put_slot<FRAME>(row, hdr_bm, fd.slot, v[u], input_null(fd, idx), fd.flags);
-      }
-    }
-  }
-}
-
-template <int TR, bool FRAME>
-__global__ __launch_bounds__(kWG) void encode_fixed_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
-                                                           uint8_t* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int HDR = FRAME ? 12 : 0;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane % TR;
-  const int fsub = lane / TR;
-  const int64_t r0 = (L.tile0 + (int64_t)blockIdx.x) * TR;
-  const int64_t left = L.num_rows - r0;
-  const int rows = left < TR ? (int)left : TR;
-  const int hdr_bm = HDR + L.bitmap_bytes;
-  uint8_t* row = lds + r * L.stride;
-  const int64_t idx = r < rows ? r0 + r : r0;
-
-  if (wave == 0 && fsub == 0) put_header<FRAME>(row, L);
-  if (L.any_nullable) __syncthreads();  // null bits are OR-ed into the zeroed bitmap
-
-  enc_group<8, TR, FRAME>(fields, L.group[0], L.group[1], wave, fsub, idx, row, hdr_bm);
-  enc_group<4, TR, FRAME>(fields, L.group[1], L.group[2], wave, fsub, idx, row, hdr_bm);
-  enc_group<2, TR, FRAME>(fields, L.group[2], L.group[3], wave, fsub, idx, row, hdr_bm);
-  enc_group<1, TR, FRAME>(fields, L.group[3], L.group[4], wave, fsub, idx, row, hdr_bm);
-  __syncthreads();
-  store_tile(lds, out + r0 * L.stride, rows * L.stride, tid);
-}
-
-// Persistent, software-pipelined encode (TR = 64). Each wave keeps its share
-// of the next tile's column values in VGPRs (per width group at most
-// 4*M8 / 4*M4 / 4*M2 / 4*M1 fields per schema) while this tile's rows are
-// stored.
-template <int W, typename T, int M>
-__device__ __forceinline__ void pipe_load(T (&v)[M], const FixedFieldDev* __restrict__ fields, int g0, int g1,
-                                          int wave, int64_t idx) {
-#pragma unroll
-  for (int u = 0; u < M; ++u) {
-    const int p = __builtin_amdgcn_readfirstlane(g0 + wave + u * kWaves);
-    if (p < g1) v[u] = (T)ldw<W>(fields[p].values, idx);
-  }
-}
-
-template <bool FRAME, typename T, int M>
-__device__ __forceinline__ void pipe_put(const T (&v)[M], const FixedFieldDev* __restrict__ fields, int g0, int g1,
-                                         int wave, int64_t idx, uint8_t* row, int hdr_bm) {
-#pragma unroll
-  for (int u = 0; u < M; ++u) {
-    const int p = __builtin_amdgcn_readfirstlane(g0 + wave + u * kWaves);
-    if (p < g1) {
-      const FixedFieldDev& fd = fields[p];
-      put_slot<FRAME>(row, hdr_bm, fd.slot, (uint64_t)v[u], input_null(fd, idx), fd.flags);
-    }
-  }
-}
-
-constexpr int kM8 = 16, kM4 = 16, kM2 = 8, kM1 = 8;
-
-template <bool FRAME>
-__global__ __launch_bounds__(kWG, 2) void encode_fixed_pipe_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
-                                                                uint8_t* __restrict__ out, int64_t tiles) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int HDR = FRAME ? 12 : 0;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int stride = L.stride;
-  const int hdr_bm = HDR + L.bitmap_bytes;
-  uint8_t* row = lds + lane * stride;
-  int64_t t = blockIdx.x;
-  if (t >= tiles) return;
-
-  uint64_t v8[kM8];
-  uint32_t v4[kM4], v2[kM2], v1[kM1];
-  int64_t idx = t * 64 + lane < L.num_rows ? t * 64 + lane : t * 64;
-  pipe_load<8>(v8, fields, L.group[0], L.group[1], wave, idx);
-  pipe_load<4>(v4, fields, L.group[1], L.group[2], wave, idx);
-  pipe_load<2>(v2, fields, L.group[2], L.group[3], wave, idx);
-  pipe_load<1>(v1, fields, L.group[3], L.group[4], wave, idx);
-  if (wave == 0) put_header<FRAME>(row, L);  // constant across tiles
-  for (;;) {
-    if (L.any_nullable) {
-      if (wave == 0) put_header<FRAME>(row, L);  // re-zero the bitmap
-      __syncthreads();
-    }
-    pipe_put<FRAME>(v8, fields, L.group[0], L.group[1], wave, idx, row, hdr_bm);
-    pipe_put<FRAME>(v4, fields, L.group[1], L.group[2], wave, idx, row, hdr_bm);
-    pipe_put<FRAME>(v2, fields, L.group[2], L.group[3], wave, idx, row, hdr_bm);
-    pipe_put<FRAME>(v1, fields, L.group[3], L.group[4], wave, idx, row, hdr_bm);
-    __syncthreads();
-    const int64_t r0 = t * 64;
-    const int64_t left = L.num_rows - r0;
-    const int rows = left < 64 ? (int)left : 64;
-    const int64_t tn = t + gridDim.x;
-    if (tn < tiles) {  // next tile's loads go out before this tile's stores
-      idx = tn * 64 + lane < L.num_rows ? tn * 64 + lane : tn * 64;
-      pipe_load<8>(v8, fields, L.group[0], L.group[1], wave, idx);
-      pipe_load<4>(v4, fields, L.group[1], L.group[2], wave, idx);
-      pipe_load<2>(v2, fields, L.group[2], L.group[3], wave, idx);
-      pipe_load<1>(v1, fields, L.group[3], L.group[4], wave, idx);
-    }
-    store_tile(lds, out + r0 * stride, rows * stride, tid);
-    __syncthreads();
-    if (tn >= tiles) break;
-    t = tn;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Encode v3: 16-byte column chunks per lane (R records per tile, 4R threads)
-// ---------------------------------------------------------------------------
-// Column reads are the encode's limiter: 4/8-byte loads of 256-byte column
-// segments reach ~1.6 TB/s at two workgroups per CU, while 16-byte loads of
-// >= 512-byte segments reach ~5.9 TB/s (scripts/microbench/colread.hip).
-// So each lane loads one 16-byte chunk of ONE field's column segment
-// (E = 16/w consecutive records) and scatters its E values into the LDS row
-// image. A field of width w spans CPF = R*w/16 chunks per tile; one wave
-// instruction (64 x 16 B) covers FPI = 64/CPF fields. Instructions are
-// numbered per width group (8, 4, 2, 1 bytes); wave v issues v, v+NW, ....
-// Persistent + software-pipelined: tile t+1's chunks are in flight while
-// tile t's rows are stored. Only full tiles; the tail goes to encode_fixed_kernel.
-template <int R>
-__device__ __forceinline__ bool v3_insn_g(int i, const int32_t* group, int* w, int* p0, int* pend) {
-  const int fpi8 = 1024 / (R * 8), fpi4 = 1024 / (R * 4), fpi2 = 1024 / (R * 2), fpi1 = 1024 / R;
-  const int n8 = group[1] - group[0], n4 = group[2] - group[1];
-  const int n2 = group[3] - group[2], n1 = group[4] - group[3];
-  const int i8 = (n8 + fpi8 - 1) / fpi8, i4 = (n4 + fpi4 - 1) / fpi4;
-  const int i2 = (n2 + fpi2 - 1) / fpi2, i1 = (n1 + fpi1 - 1) / fpi1;
-  if (i < i8) { *w = 8; *p0 = group[0] + i * fpi8; *pend = group[1]; return true; }
-  i -= i8;
-  if (i < i4) { *w = 4; *p0 = group[1] + i * fpi4; *pend = group[2]; return true; }
-  i -= i4;
-  if (i < i2) { *w = 2; *p0 = group[2] + i * fpi2; *pend = group[3]; return true; }
-  i -= i2;
-  if (i < i1) { *w = 1; *p0 = group[3] + i * fpi1; *pend = group[4]; return true; }
-  return false;
-}
-
-template <int R>
-__device__ __forceinline__ bool v3_insn(int i, const FixedLaunch& L, int* w, int* p0, int* pend) {
-  return v3_insn_g<R>(i, L.group, w, p0, pend);
-}
-
-template <int R>
-__host__ __device__ inline int v3_insn_count(const int* group) {
-  const int fpi8 = 1024 / (R * 8), fpi4 = 1024 / (R * 4), fpi2 = 1024 / (R * 2), fpi1 = 1024 / R;
-  const int n8 = group[1] - group[0], n4 = group[2] - group[1];
-  const int n2 = group[3] - group[2], n1 = group[4] - group[3];
-  return (n8 + fpi8 - 1) / fpi8 + (n4 + fpi4 - 1) / fpi4 + (n2 + fpi2 - 1) / fpi2 + (n1 + fpi1 - 1) / fpi1;
-}
-
-constexpr int kV3K = 12;  // instructions per wave per tile
-
-template <int R, bool FRAME, bool NULLS, bool PAD>
-__global__ __launch_bounds__(4 * R, 1) void encode_fixed_v3_kernel(FixedLaunch L,
-                                                                    const FixedFieldDev* __restrict__ fields,
-                                                                    uint8_t* __restrict__ out, int64_t tiles) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int WG = 4 * R;
-  constexpr int NW = WG / 64;
-  constexpr int HDR = FRAME ? 12 : 0;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int stride = L.stride;
-  // LDS row pitch: PAD (raw rows) spaces rows by pitch = 4 mod 32 bytes so the
-  // 16 lanes of a ds_write_b64 group (records 2c / 4c of one field) spread
-  // over the banks; the store phase then re-packs rows with 4-byte reads.
-  const int pitch = PAD ? L.pitch : stride;
-  const int hdr_bm = HDR + L.bitmap_bytes;
-  int64_t t = blockIdx.x;
-  if (t >= tiles) return;
-
-  // per-lane descriptors, loop-invariant across tiles
-  const uint8_t* ptr[kV3K];
-  const uint8_t* vptr[kV3K];
-  uint32_t sf[kV3K];  // slot | flags << 16 | active << 20 | rb << 21 (rb = first record of the chunk)
-#pragma unroll
-  for (int k = 0; k < kV3K; ++k) {
-    int w = 8, p0 = 0, pend = 0;
-    const bool ok = v3_insn<R>(wave + k * NW, L, &w, &p0, &pend);
-    const int cpf = R * w / 16;
-    const int p = p0 + lane / cpf, c = lane % cpf;
-    ptr[k] = nullptr;
-    vptr[k] = nullptr;
-    sf[k] = 0;
-    if (ok && p < pend) {
-      const FixedFieldDev& fd = fields[p];
-      ptr[k] = fd.values + c * 16;
-      if (NULLS) vptr[k] = (fd.flags & 1) ? fd.validity : nullptr;
-      sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (1u << 20) | ((uint32_t)(c * (16 / w)) << 21);
-    }
-  }
-  u32x4 d[kV3K];
-  uint32_t vb[kV3K];
-  auto issue = [&](int64_t tile) {
-    const int64_t r0 = tile * R;
-#pragma unroll
-    for (int k = 0; k < kV3K; ++k) {
-      int w = 8, p0, pend;
-      if (!v3_insn<R>(wave + k * NW, L, &w, &p0, &pend)) continue;  // uniform
-      if (sf[k] & (1u << 20)) {
-        d[k] = *gp(reinterpret_cast<const u32x4*>(ptr[k] + r0 * w));
-        if (NULLS) {
-          vb[k] = 0xffffffffu;
-          if (vptr[k]) {
-            const int64_t rec = r0 + (sf[k] >> 21);
-            vb[k] = w == 1 ? *gp(reinterpret_cast<const uint16_t*>(vptr[k] + (rec >> 3)))
-                           : (uint32_t)load_byte(vptr[k] + (rec >> 3)) >> (rec & 7);
-          }
-        }
-      }
-    }
-  };
-
-  issue(t);
-  if (tid < R) put_header<FRAME>(lds + tid * pitch, L);  // constant across tiles
-  for (;;) {
-    if (NULLS) {
-      if (tid < R) put_header<FRAME>(lds + tid * pitch, L);  // re-zero the bitmaps
-      __syncthreads();
-    }
-#pragma unroll
-    for (int k = 0; k < kV3K; ++k) {
-      int w = 8, p0, pend;
-      if (!v3_insn<R>(wave + k * NW, L, &w, &p0, &pend)) continue;
-      if (!(sf[k] & (1u << 20))) continue;
-      const int slot = sf[k] & 0xffff, flags = (sf[k] >> 16) & 0xf, rb = sf[k] >> 21;
-      uint8_t* row = lds + rb * pitch;
-      const uint32_t nb = NULLS ? ~vb[k] : 0u;  // 1 = null
-      const u32x4 x = d[k];
-      if (w == 8) {
-        put_slot<FRAME>(row, hdr_bm, slot, (uint64_t)x.x | ((uint64_t)x.y << 32), nb & 1, flags);
-        put_slot<FRAME>(row + pitch, hdr_bm, slot, (uint64_t)x.z | ((uint64_t)x.w << 32), (nb >> 1) & 1, flags);
-      } else if (w == 4) {
-        put_slot<FRAME>(row, hdr_bm, slot, x.x, nb & 1, flags);
-        put_slot<FRAME>(row + pitch, hdr_bm, slot, x.y, (nb >> 1) & 1, flags);
-        put_slot<FRAME>(row + 2 * pitch, hdr_bm, slot, x.z, (nb >> 2) & 1, flags);
-        put_slot<FRAME>(row + 3 * pitch, hdr_bm, slot, x.w, (nb >> 3) & 1, flags);
-      } else if (w == 2) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          put_slot<FRAME>(row + e * pitch, hdr_bm, slot, (x[e >> 1] >> (16 * (e & 1))) & 0xffff, (nb >> e) & 1, flags);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 16; ++e)
-          put_slot<FRAME>(row + e * pitch, hdr_bm, slot, (x[e >> 2] >> (8 * (e & 3))) & 0xff, (nb >> e) & 1, flags);
-      }
-    }
-    __syncthreads();
-    const int64_t tn = t + gridDim.x;
-    if (tn < tiles) issue(tn);  // next tile's column chunks go out before this tile's rows
-    {
-      uint8_t* dst = out + t * R * stride;
-      const int bytes = R * stride;
-      const int n16 = bytes >> 4;
-      int c = tid;
-      if constexpr (PAD) {
-        // tile byte o -> LDS (o / stride) * pitch + o % stride, 4 bytes at a time
-        for (; c < n16; c += WG) {
-          u32x4 y;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t o = (uint32_t)(c * 16 + 4 * i);
-            uint32_t j = __umulhi(o, L.stride_magic);
-            uint32_t r = o - j * (uint32_t)stride;
-            if (r >= (uint32_t)stride) { ++j; r -= stride; }
-            y[i] = ld32(lds + j * pitch + r);
-          }
-          *reinterpret_cast<u32x4*>(dst + c * 16) = y;
-        }
-      }
-      for (; c + 3 * WG < n16; c += 4 * WG) {
-        const u32x4 y0 = *reinterpret_cast<const u32x4*>(lds + c * 16);
-        const u32x4 y1 = *reinterpret_cast<const u32x4*>(lds + (c + WG) * 16);
-        const u32x4 y2 = *reinterpret_cast<const u32x4*>(lds + (c + 2 * WG) * 16);
-        const u32x4 y3 = *reinterpret_cast<const u32x4*>(lds + (c + 3 * WG) * 16);
-        *reinterpret_cast<u32x4*>(dst + c * 16) = y0;
-        *reinterpret_cast<u32x4*>(dst + (c + WG) * 16) = y1;
-        *reinterpret_cast<u32x4*>(dst + (c + 2 * WG) * 16) = y2;
-        *reinterpret_cast<u32x4*>(dst + (c + 3 * WG) * 16) = y3;
-      }
-      for (; c < n16; c += WG) *reinterpret_cast<u32x4*>(dst + c * 16) = *reinterpret_cast<const u32x4*>(lds + c * 16);
-      const int tail4 = (bytes & 15) >> 2;
-      if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
-    }
-    __syncthreads();
-    if (tn >= tiles) break;
-    t = tn;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Encode v5: v3 with a depth-2 load pipeline
-// ---------------------------------------------------------------------------
-// Two tiles of column chunks are in flight per workgroup (register sets A/B,
-// the loop unrolled by 2 so both stay static). Every lane issues exactly K
-// loads per tile (inactive lanes / absent instructions re-read a valid dummy
-// address), so hipcc can wait with a counted vmcnt for the older set while
-// the younger set stays in flight. Order per stage: write X -> barrier ->
-// store this tile's rows -> issue X for tile + 2*grid -> barrier.
-template <int R, int K, int NT = 0>
-__device__ __forceinline__ void v5_issue(const uint8_t* const (&ptr)[K], const int (&wk)[K], int64_t r0,
-                                         u32x4 (&d)[K]) {
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const GAS u32x4* a = gp(reinterpret_cast<const u32x4*>(ptr[k] + r0 * wk[k]));
-    if constexpr (NT & 1) d[k] = __builtin_nontemporal_load(a);  // once-read column stream
-    else d[k] = *a;
-  }
-}
-
-template <int R, int K, bool FRAME, bool PAD>
-__device__ __forceinline__ void v5_write(uint8_t* lds, int pitch, int hdr_bm, const int (&wk)[K],
-                                         const uint32_t (&sf)[K], const u32x4 (&d)[K]) {
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int w = wk[k];
-    if (!(sf[k] & (1u << 20))) continue;
-    const int slot = sf[k] & 0xffff, flags = (sf[k] >> 16) & 0xf, rb = sf[k] >> 21;
-    uint8_t* row = lds + rb * pitch;
-    const u32x4 x = d[k];
-    if (w == 8) {
-      put_slot<FRAME>(row, hdr_bm, slot, (uint64_t)x.x | ((uint64_t)x.y << 32), false, flags);
-      put_slot<FRAME>(row + pitch, hdr_bm, slot, (uint64_t)x.z | ((uint64_t)x.w << 32), false, flags);
-    } else if (w == 4) {
-      put_slot<FRAME>(row, hdr_bm, slot, x.x, false, flags);
-      put_slot<FRAME>(row + pitch, hdr_bm, slot, x.y, false, flags);
-      put_slot<FRAME>(row + 2 * pitch, hdr_bm, slot, x.z, false, flags);
-      put_slot<FRAME>(row + 3 * pitch, hdr_bm, slot, x.w, false, flags);
-    } else if (w == 2) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        put_slot<FRAME>(row + e * pitch, hdr_bm, slot, (x[e >> 1] >> (16 * (e & 1))) & 0xffff, false, flags);
-    } else if (w == 1) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e)
-        put_slot<FRAME>(row + e * pitch, hdr_bm, slot, (x[e >> 2] >> (8 * (e & 3))) & 0xff, false, flags);
-    }
-  }
-}
-
-template <int R, int WG, bool PAD, int NT = 0>
-__device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* lds, int pitch, uint8_t* dst, int tid) {
-  const int stride = L.stride;
-  const int bytes = R * stride;
-  const int n16 = bytes >> 4;
-  int c = tid;
-  if constexpr (PAD) {
-    for (; c < n16; c += WG) {
-      u32x4 y;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t o = (uint32_t)(c * 16 + 4 * i);
-        uint32_t j = __umulhi(o, L.stride_magic);
-        uint32_t r = o - j * (uint32_t)stride;
-        if (r >= (uint32_t)stride) { ++j; r -= stride; }
-        y[i] = ld32(lds + j * pitch + r);
-      }
-      *gp(reinterpret_cast<u32x4*>(dst + c * 16)) = y;
-    }
-  } else {
-    for (; c < n16; c += WG) {
-      const u32x4 y = *reinterpret_cast<const u32x4*>(lds + c * 16);
-      if constexpr (NT & 2) __builtin_nontemporal_store(y, gp(reinterpret_cast<u32x4*>(dst + c * 16)));
-      else *gp(reinterpret_cast<u32x4*>(dst + c * 16)) = y;
-    }
-    const int tail4 = (bytes & 15) >> 2;
-    if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
-  }
-}
-
-// ONESHOT: one tile per workgroup, grid = tiles (no pipeline). Workgroups are
-// dispatched in tile order, so the addresses in flight chip-wide stay a
-// compact window; persistent grids drift apart (scripts/microbench/copybw.hip:
-// one-shot 16-B copy 6.25 TB/s vs 5.2-5.6 TB/s for grid-stride loops).
-template <int R, int WG, int K, bool FRAME, bool PAD, bool ONESHOT = false, int NT = 0>
-__global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
-                                                                 const FixedFieldDev* __restrict__ fields,
-                                                                 uint8_t* __restrict__ out, int64_t tiles) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int NW = WG / 64;
-  constexpr int HDR = FRAME ? 12 : 0;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int stride = L.stride;
-  const int pitch = PAD ? L.pitch : stride;
-  const int hdr_bm = HDR + L.bitmap_bytes;
-  int64_t t = blockIdx.x;
-  if (t >= tiles) return;
-
-  const uint8_t* dummy = fields[L.group[0]].values;  // any valid column (never null: num_rows > 0)
-  const uint8_t* ptr[K];
-  int wk[K];
-  uint32_t sf[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    int w = 0, p0 = 0, pend = 0;
-    const bool ok = v3_insn<R>(wave + k * NW, L, &w, &p0, &pend);
-    wk[k] = ok ? w : 0;  // absent instruction: width 0 -> re-reads the dummy address
-    const int cpf = R * (ok ? w : 8) / 16;
-    const int p = p0 + lane / cpf, c = lane % cpf;
-    ptr[k] = dummy;
-    sf[k] = 0;
-    if (ok && p < pend) {
-      const FixedFieldDev& fd = fields[p];
-      ptr[k] = fd.values + c * 16;
-      sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (1u << 20) | ((uint32_t)(c * (16 / w)) << 21);
-    }
-  }
-  if (tid < R) put_header<FRAME>(lds + tid * pitch, L);  // constant across tiles (no nullable fields)
-  u32x4 dA[K], dB[K];
-  if constexpr (ONESHOT) {
-    v5_issue<R, K, NT>(ptr, wk, t * R, dA);
-    v5_write<R, K, FRAME, PAD>(lds, pitch, hdr_bm, wk, sf, dA);
-    __syncthreads();
-    v5_store<R, WG, PAD, NT>(L, lds, pitch, out + t * R * stride, tid);
-    return;
-  }
-  const int64_t last = tiles - 1;
-  v5_issue<R, K, NT>(ptr, wk, t * R, dA);
-  v5_issue<R, K, NT>(ptr, wk, min(t + (int64_t)gridDim.x, last) * R, dB);
-  for (;;) {
-    v5_write<R, K, FRAME, PAD>(lds, pitch, hdr_bm, wk, sf, dA);
-    __syncthreads();
-    v5_store<R, WG, PAD, NT>(L, lds, pitch, out + t * R * stride, tid);
-    v5_issue<R, K, NT>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dA);
-    __syncthreads();
-    t += gridDim.x;
-    if (t >= tiles) break;
-    v5_write<R, K, FRAME, PAD>(lds, pitch, hdr_bm, wk, sf, dB);
-    __syncthreads();
-    v5_store<R, WG, PAD, NT>(L, lds, pitch, out + t * R * stride, tid);
-    v5_issue<R, K, NT>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dB);
-    __syncthreads();
-    t += gridDim.x;
-    if (t >= tiles) break;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Encode v4: v3's 16-byte column chunks, tiles split into column slabs
-// ---------------------------------------------------------------------------
-// v3's full-row LDS image (R * stride bytes) caps residency at 2 workgroups
-// per CU, and each workgroup alternates LDS-write / barrier / store phases, so
-// the CU idles on HBM between them. v4 cuts every row into S 16-byte-aligned
-// byte slabs (e.g. [0, 432) and [432, 848) of an 848-byte row) and runs one
-// (tile, slab) stage at a time through an R x slab_pitch image: LDS per
-// workgroup drops S-fold, 4-5 workgroups share a CU and hide each other's
-// phases. Stages are software-pipelined: stage k+1's column chunks are in
-// flight while stage k's slab is stored. A slab's rows leave as R runs of
-// nbytes (16-B stores); row lines split across slabs are completed in L2 by
-// the next stage of the same workgroup. Raw rows only (8-byte slots, rows a
-// multiple of 16 bytes), no nullable fields.
-constexpr int kV4K = 8;  // instructions per wave per slab
-
-template <int R, int S>
-__device__ __forceinline__ void v4_desc(const FixedLaunch& L, const FixedFieldDev* __restrict__ fields, int wave,
-                                        int lane, int s, const uint8_t* (&ptr)[kV4K], uint32_t (&sf)[kV4K]) {
-  constexpr int NW = 4 * R / 64;
-#pragma unroll
-  for (int k = 0; k < kV4K; ++k) {
-    int w = 8, p0 = 0, pend = 0;
-    const bool ok = v3_insn_g<R>(wave + k * NW, L.slab[s].group, &w, &p0, &pend);
-    const int cpf = R * w / 16;
-    const int p = p0 + lane / cpf, c = lane % cpf;
-    ptr[k] = nullptr;
-    sf[k] = 0;
-    if (ok && p < pend) {
-      const FixedFieldDev& fd = fields[p];
-      // byte of the slot inside the slab image row
-      const int sb = L.bitmap_bytes + 8 * fd.slot - L.slab[s].byte0;
-      ptr[k] = fd.values + c * 16;
-      sf[k] = (uint32_t)sb | ((uint32_t)fd.flags << 12) | (1u << 16) | ((uint32_t)(c * (16 / w)) << 17);
-    }
-  }
-}
-
-template <int R>
-__device__ __forceinline__ void v4_issue(const FixedLaunch& L, int s, int wave, int64_t r0,
-                                         const uint8_t* const (&ptr)[kV4K], const uint32_t (&sf)[kV4K],
-                                         u32x4 (&d)[kV4K]) {
-  constexpr int NW = 4 * R / 64;
-#pragma unroll
-  for (int k = 0; k < kV4K; ++k) {
-    int w = 8, p0, pend;
-    if (!v3_insn_g<R>(wave + k * NW, L.slab[s].group, &w, &p0, &pend)) continue;  // uniform
-    if (sf[k] & (1u << 16)) d[k] = *gp(reinterpret_cast<const u32x4*>(ptr[k] + r0 * w));
-  }
-}
-
-__device__ __forceinline__ void v4_put(uint8_t* p, uint64_t x, int flags) {
-  if (flags & 2) x = x ? 1 : 0;  // MemoryBuffer.putBoolean
-  *reinterpret_cast<uint64_t*>(p) = x;
-}
-
-template <int R>
-__device__ __forceinline__ void v4_write(const FixedLaunch& L, int s, int wave, uint8_t* lds, int sp,
-                                         const uint32_t (&sf)[kV4K], const u32x4 (&d)[kV4K]) {
-  constexpr int NW = 4 * R / 64;
-#pragma unroll
-  for (int k = 0; k < kV4K; ++k) {
-    int w = 8, p0, pend;
-    if (!v3_insn_g<R>(wave + k * NW, L.slab[s].group, &w, &p0, &pend)) continue;
-    if (!(sf[k] & (1u << 16))) continue;
-    const int sb = sf[k] & 0xfff, flags = (sf[k] >> 12) & 0xf, rb = sf[k] >> 17;
-    uint8_t* p = lds + rb * sp + sb;
-    const u32x4 x = d[k];
-    if (w == 8) {
-      v4_put(p, (uint64_t)x.x | ((uint64_t)x.y << 32), flags);
-      v4_put(p + sp, (uint64_t)x.z | ((uint64_t)x.w << 32), flags);
-    } else if (w == 4) {
-      v4_put(p, x.x, flags);
-      v4_put(p + sp, x.y, flags);
-      v4_put(p + 2 * sp, x.z, flags);
-      v4_put(p + 3 * sp, x.w, flags);
-    } else if (w == 2) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v4_put(p + e * sp, (x[e >> 1] >> (16 * (e & 1))) & 0xffff, flags);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) v4_put(p + e * sp, (x[e >> 2] >> (8 * (e & 3))) & 0xff, flags);
-    }
-  }
-}
-
-// Slab s of tile rows [r0, r0+R): R runs of nbytes from the LDS image.
-template <int R>
-__device__ __forceinline__ void v4_store(const FixedLaunch& L, int s, const uint8_t* lds, int sp, uint8_t* out,
-                                         int64_t r0, int tid) {
-  constexpr int WG = 4 * R;
-  const uint32_t cpr = (uint32_t)L.slab[s].nbytes >> 4;
-  const int n16 = R * (int)cpr;
-  uint8_t* base = out + r0 * L.stride + L.slab[s].byte0;
-  for (int q = tid; q < n16; q += WG) {
-    uint32_t j = __umulhi((uint32_t)q, L.slab[s].cpr_magic);
-    uint32_t c = (uint32_t)q - j * cpr;
-    if (c >= cpr) { ++j; c -= cpr; }
-    const u32x4 y = *reinterpret_cast<const u32x4*>(lds + j * sp + c * 16);
-    *gp(reinterpret_cast<u32x4*>(base + (int64_t)j * L.stride + c * 16)) = y;
-  }
-}
-
-template <int R, int S>
-__global__ __launch_bounds__(4 * R, 4) void encode_fixed_v4_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
-                                                                  uint8_t* __restrict__ out, int64_t tiles) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int sp = L.slab_pitch;
-  int64_t t = blockIdx.x;
-  if (t >= tiles) return;
-
-  const uint8_t* ptr[S][kV4K];
-  uint32_t sf[S][kV4K];
-#pragma unroll
-  for (int s = 0; s < S; ++s) v4_desc<R, S>(L, fields, wave, lane, s, ptr[s], sf[s]);
-  u32x4 d[kV4K];
-  v4_issue<R>(L, 0, wave, t * R, ptr[0], sf[0], d);
-  for (;;) {
-    const int64_t tn = t + gridDim.x;
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      if (s == 0 && tid < R) {  // slab 0 holds the null bitmap: zero it (no nullable fields here)
-        for (int b = 0; b < L.bitmap_bytes; b += 8) *reinterpret_cast<uint64_t*>(lds + tid * sp + b) = 0;
-      }
-      v4_write<R>(L, s, wave, lds, sp, sf[s], d);
-      __syncthreads();
-      if (s + 1 < S) v4_issue<R>(L, s + 1, wave, t * R, ptr[s + 1], sf[s + 1], d);
-      else if (tn < tiles) v4_issue<R>(L, 0, wave, tn * R, ptr[0], sf[0], d);
-      v4_store<R>(L, s, lds, sp, out, t * R, tid);
-      __syncthreads();
-    }
-    if (tn >= tiles) break;
-    t = tn;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Fixed-width decode: rows -> columns
-// ---------------------------------------------------------------------------
-// LDS-DMA of `bytes` contiguous bytes into the LDS image (1 KiB per wave
-// instruction; lanes past the end masked off).
-// NT & 4: non-temporal policy (aux = 2) on the once-read row stream.
-template <int NT = 0>
-__device__ __forceinline__ void dma_tile(uint8_t* lds, const uint8_t* __restrict__ src, int bytes, int tid, int wave) {
-  const int n16 = bytes >> 4;
-  for (int c0 = 0; c0 < n16; c0 += kWG) {
-    const int c = c0 + tid;
-    if (c < n16)
-      __builtin_amdgcn_global_load_lds((const GAS void*)(src + (int64_t)c * 16),
-                                       (__attribute__((address_space(3))) void*)(lds + (c0 + wave * 64) * 16), 16,
-                                       0, (NT & 4) ? 2 : 0);
-  }
-  const int tail4 = (bytes & 15) >> 2;
-  if (tid < tail4) st32(lds + n16 * 16 + tid * 4, ld32(src + n16 * 16 + tid * 4));
-}
-
-template <bool FRAME>
-__device__ __forceinline__ void check_frame(const uint8_t* row, const FixedLaunch& L, int32_t* status) {
-  // Encoders.decode (Encoders.java:177-190): size, then the schema hash.
-  const uint32_t len = ld32(row);
-  const uint64_t h = (uint64_t)ld32(row + 4) | ((uint64_t)ld32(row + 8) << 32);
-  if (h != (uint64_t)L.schema_hash) set_status(status, FORY_ERR_SCHEMA_MISMATCH);
-  else if (len != (uint32_t)(8 + L.fixed_size)) set_status(status, FORY_ERR_CORRUPT);
-}
-
-// Slot of an LDS row (UnsafeTrait.getX: the low W bytes).
-template <int W, bool FRAME>
-__device__ __forceinline__ uint64_t get_slot(const uint8_t* row, int hdr_bm, int slot) {
-  const uint8_t* p = row + hdr_bm + 8 * slot;
-  if constexpr (W == 8) {
-    if (FRAME) return (uint64_t)ld32(p) | ((uint64_t)ld32(p + 4) << 32);
-    return *reinterpret_cast<const uint64_t*>(p);
-  }
-  return ld32(p);
-}
-
-// Arrow validity of field fd for the TR records of this lane group.
-template <int TR>
-__device__ __forceinline__ void put_validity(const FixedFieldDev& fd, bool isnull, bool live, int r, int fsub,
-                                             int64_t r0, int rows) {
-  const uint64_t m = __ballot(!isnull && live);
-  if (r == 0) {
-    const uint64_t mine = (m >> (fsub * TR)) & (TR == 64 ? ~0ull : ((1ull << TR) - 1));
-    uint8_t* vb = fd.out_validity + (r0 >> 3);
-    const int nb = (rows + 7) >> 3;
-    for (int b = 0; b < nb; ++b) store_byte(vb + b, (uint8_t)(mine >> (8 * b)));
-  }
-}
-
-// Decodes slot values of one width group: null -> 0 (RowEncoderBuilder.java:239-246),
-// bool -> 0/1 (MemoryBuffer.getBoolean), coalesced column stores.
-template <int W, int TR, bool FRAME, int NT = 0>
-__device__ __forceinline__ void dec_group(const FixedFieldDev* __restrict__ fields, int g0, int g1, int wave, int fsub,
-                                          int r, const uint8_t* row, int hdr_bm, int hdr, bool live, int64_t grow,
-                                          int64_t r0, int rows) {
-  constexpr int FPW = 64 / TR;
-  constexpr int FSTEP = kWaves * FPW;
-  constexpr int U = 8;
-  for (int pb = g0 + wave * FPW; pb < g1; pb += FSTEP * U) {
-    uint64_t x[U];
-    bool nul[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int p = field_of<TR>(pb, u, FSTEP, fsub);
-      x[u] = 0;
-      nul[u] = true;
-      if (p < g1) {
-        const int slot = fields[p].slot;
-        nul[u] = (ld32(row + hdr + ((slot >> 5) << 2)) >> (slot & 31)) & 1;  // BinaryRow.isNullAt
-        x[u] = get_slot<W, FRAME>(row, hdr_bm, slot);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int p = field_of<TR>(pb, u, FSTEP, fsub);
-      if (p < g1) {
-        const FixedFieldDev& fd = fields[p];
-        uint64_t v = nul[u] ? 0 : x[u];
-        if (fd.flags & 2) v = (v & 0xff) ? 1 : 0;
-        if (live) {
-          if constexpr ((NT & 8) && W >= 4) {  // non-temporal column stores
-            if constexpr (W == 8) __builtin_nontemporal_store(v, gp(reinterpret_cast<uint64_t*>(fd.out_values)) + grow);
-            else __builtin_nontemporal_store((uint32_t)v, gp(reinterpret_cast<uint32_t*>(fd.out_values)) + grow);
-          } else {
-            stw<W>(fd.out_values, grow, v);
-          }
-        }
-        if ((fd.flags & 1) && fd.out_validity) put_validity<TR>(fd, nul[u], live, r, fsub, r0, rows);
-      }
-    }
-  }
-}
-
-template <int TR, bool FRAME, int NT = 0>
-__global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
-                                                           const uint8_t* __restrict__ in, int32_t* status) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int HDR = FRAME ? 12 : 0;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane % TR;
-  const int fsub = lane / TR;
-  const int64_t r0 = (L.tile0 + (int64_t)blockIdx.x) * TR;
-  const int64_t left = L.num_rows - r0;
-  const int rows = left < TR ? (int)left : TR;
-  const int stride = L.stride;
-  const int hdr_bm = HDR + L.bitmap_bytes;
-
-  dma_tile<NT>(lds, in + r0 * stride, rows * stride, tid, wave);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  const uint8_t* row = lds + r * stride;
-  const int64_t grow = r0 + r;
-  const bool live = r < rows;
-  if (FRAME && wave == 0 && fsub == 0 && live) check_frame<FRAME>(row, L, status);
-  dec_group<8, TR, FRAME, NT>(fields, L.group[0], L.group[1], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
-  dec_group<4, TR, FRAME, NT>(fields, L.group[1], L.group[2], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
-  dec_group<2, TR, FRAME, NT>(fields, L.group[2], L.group[3], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
-  dec_group<1, TR, FRAME, NT>(fields, L.group[3], L.group[4], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
-}
-
-// Decode v3: the mirror of encode v3/v5 — each lane assembles one 16-byte chunk
-// of ONE field's column segment (16/w consecutive records of the tile) from the
-// LDS row image and stores it with one 16-B store: 39 store instructions per
-// 64-record Struct104 tile instead of 104 per-lane 4/8-byte ones. One full
-// 64-record tile per workgroup (tail: decode_fixed_kernel), not-null schemas
-// only (nullable fields need per-record validity bits: decode_fixed_kernel).
-// Null bits are still honoured (RowEncoderBuilder.java:239-246 reads isNullAt
-// for every field): a set bit decodes to 0. Descriptors are loaded per lane
-// before the tile's LDS-DMA wait, so their latency hides under it.
-template <bool FRAME, int K, int NT>
-__global__ __launch_bounds__(kWG) void decode_fixed_v3_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
-                                                              const uint8_t* __restrict__ in, int32_t* status) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int HDR = FRAME ? 12 : 0;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t r0 = (L.tile0 + (int64_t)blockIdx.x) * 64;
-  const int stride = L.stride;
-  const int hdr_bm = HDR + L.bitmap_bytes;
-  uint8_t* optr[K];
-  int wk[K], rb[K], slot[K], flg[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    int w = 0, p0 = 0, pend = 0;
-    const bool ok = v3_insn<64>(wave + k * kWaves, L, &w, &p0, &pend);
-    const int cpf = ok ? 4 * w : 32;
-    const int p = p0 + lane / cpf, c = lane % cpf;
-    wk[k] = 0;
-    optr[k] = nullptr;
-    rb[k] = slot[k] = flg[k] = 0;
-    if (ok && p < pend) {
-      const FixedFieldDev& fd = fields[p];
-      wk[k] = w;
-      optr[k] = fd.out_values + (r0 * w + c * 16);
-      rb[k] = c * (16 / w);
-      slot[k] = fd.slot;
-      flg[k] = fd.flags;
-    }
-  }
-  dma_tile<NT>(lds, in + r0 * stride, 64 * stride, tid, wave);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (FRAME && wave == 0) check_frame<FRAME>(lds + lane * stride, L, status);
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int w = wk[k];
-    if (!w) continue;
-    const uint8_t* row = lds + rb[k] * stride;
-    const int s = slot[k];
-    const int bmo = HDR + ((s >> 5) << 2), bit = s & 31;
-    const uint8_t* sp = row + hdr_bm + 8 * s;
-    u32x4 y;
-    if (w == 8) {
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const bool nul = (ld32(row + e * stride + bmo) >> bit) & 1;
-        y[2 * e] = nul ? 0u : ld32(sp + e * stride);
-        y[2 * e + 1] = nul ? 0u : ld32(sp + e * stride + 4);
-      }
-    } else if (w == 4) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool nul = (ld32(row + e * stride + bmo) >> bit) & 1;
-        y[e] = nul ? 0u : ld32(sp + e * stride);
-      }
-    } else if (w == 2) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int e = 2 * q + h;
-          const bool nul = (ld32(row + e * stride + bmo) >> bit) & 1;
-          v |= (nul ? 0u : (ld32(sp + e * stride) & 0xffffu)) << (16 * h);
-        }
-        y[q] = v;
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const int e = 4 * q + h;
-          const bool nul = (ld32(row + e * stride + bmo) >> bit) & 1;
-          uint32_t b = nul ? 0u : (ld32(sp + e * stride) & 0xffu);
-          if (flg[k] & 2) b = b ? 1u : 0u;  // MemoryBuffer.getBoolean
-          v |= b << (8 * h);
-        }
-        y[q] = v;
-      }
-    }
-    if constexpr (NT & 8) __builtin_nontemporal_store(y, gp(reinterpret_cast<u32x4*>(optr[k])));
-    else *gp(reinterpret_cast<u32x4*>(optr[k])) = y;
-  }
-}
-
-// Decode v2: one tile of TR records (TR a multiple of 64) per workgroup of WG
-// threads; lane = record within a 64-record half; wave instruction i covers
-// field i / (TR/64), records (i % (TR/64)) * 64 + lane. Same LDS-DMA image and
-// per-field batching as decode_fixed_kernel, more waves / larger column runs.
-template <int TR, int WG, bool FRAME>
-__global__ __launch_bounds__(WG) void decode_fixed_v2_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
-                                                             const uint8_t* __restrict__ in, int32_t* status) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int NW = WG / 64;
-  constexpr int H = TR / 64;  // 64-record halves per tile
-  constexpr int HDR = FRAME ? 12 : 0;
-  constexpr int U = 8;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t r0 = (L.tile0 + (int64_t)blockIdx.x) * TR;
-  const int64_t left = L.num_rows - r0;
-  const int rows = left < TR ? (int)left : TR;
-  const int stride = L.stride;
-  const int hdr_bm = HDR + L.bitmap_bytes;
-  {  // tile image HBM -> LDS (LDS-DMA, 1 KiB per wave instruction)
-    const uint8_t* src = in + r0 * stride;
-    const int bytes = rows * stride;
-    const int n16 = bytes >> 4;
-    for (int c0 = 0; c0 < n16; c0 += WG) {
-      const int c = c0 + tid;
-      if (c < n16)
-        __builtin_amdgcn_global_load_lds((const GAS void*)(src + (int64_t)c * 16),
-                                         (__attribute__((address_space(3))) void*)(lds + (c0 + wave * 64) * 16), 16,
-                                         0, 0);
-    }
-    const int tail4 = (bytes & 15) >> 2;
-    if (tid < tail4) st32(lds + n16 * 16 + tid * 4, ld32(src + n16 * 16 + tid * 4));
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (FRAME) {
-    for (int r = tid; r < rows; r += WG) check_frame<FRAME>(lds + r * stride, L, status);
-  }
-  const int nins = L.num_fields * H;
-  for (int ib = wave; ib < nins; ib += NW * U) {
-    uint64_t x[U];
-    bool nul[U];
-    int rr[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = __builtin_amdgcn_readfirstlane(ib + u * NW);
-      const int p = i / H, h = i % H;
-      rr[u] = h * 64 + lane;
-      x[u] = 0;
-      nul[u] = true;
-      if (i < nins) {
-        const uint8_t* row = lds + rr[u] * stride;
-        const int slot = fields[p].slot;
-        const int w = fields[p].width;
-        nul[u] = (ld32(row + HDR + ((slot >> 5) << 2)) >> (slot & 31)) & 1;
-        const uint8_t* sp = row + hdr_bm + 8 * slot;
-        if (w == 8) x[u] = (FRAME ? ((uint64_t)ld32(sp) | ((uint64_t)ld32(sp + 4) << 32))
-                                  : *reinterpret_cast<const uint64_t*>(sp));
-        else x[u] = ld32(sp);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = __builtin_amdgcn_readfirstlane(ib + u * NW);
-      if (i < nins) {
-        const int p = i / H;
-        const FixedFieldDev& fd = fields[p];
-        const bool live = rr[u] < rows;
-        uint64_t v = nul[u] ? 0 : x[u];
-        if (fd.flags & 2) v = (v & 0xff) ? 1 : 0;
-        if (live) {
-          switch (fd.width) {
-            case 8: stw<8>(fd.out_values, r0 + rr[u], v); break;
-            case 4: stw<4>(fd.out_values, r0 + rr[u], v); break;
-            case 2: stw<2>(fd.out_values, r0 + rr[u], v); break;
-            default: stw<1>(fd.out_values, r0 + rr[u], v); break;
-          }
-        }
-        if ((fd.flags & 1) && fd.out_validity) {
-          const int h = i % H;
-          const int hrows = rows - h * 64 < 64 ? rows - h * 64 : 64;
-          if (hrows > 0) put_validity<64>(fd, nul[u], live, lane, 0, r0 + h * 64, hrows);
-        }
-      }
-    }
-  }
-}
-
-// Persistent, software-pipelined decode (TR = 64, tile image <= MAXC*4 KiB):
-// the next tile streams HBM -> VGPRs while this tile's columns are stored,
-// then VGPRs -> LDS (async-stage split).
-template <int MAXC>
-__device__ __forceinline__ void stage_issue(u32x4 (&buf)[MAXC], uint32_t& tail, const uint8_t* __restrict__ src,
-                                            int bytes, int tid) {
-  const int n16 = bytes >> 4;
-  const int last = n16 > 0 ? n16 - 1 : 0;  // lanes past the end re-read the last chunk (no divergence)
-#pragma unroll
-  for (int k = 0; k < MAXC; ++k) {
-    const int c = min(k * kWG + tid, last);
-    buf[k] = *reinterpret_cast<const u32x4*>(src + (int64_t)c * 16);
-  }
-  if (tid < ((bytes & 15) >> 2)) tail = ld32(src + n16 * 16 + tid * 4);
-}
-
-template <int MAXC>
-__device__ __forceinline__ void stage_commit(const u32x4 (&buf)[MAXC], uint32_t tail, uint8_t* lds, int bytes,
-                                             int tid) {
-  const int n16 = bytes >> 4;
-#pragma unroll
-  for (int k = 0; k < MAXC; ++k) {
-    const int c = k * kWG + tid;
-    if (c < n16) *reinterpret_cast<u32x4*>(lds + c * 16) = buf[k];
-  }
-  if (tid < ((bytes & 15) >> 2)) st32(lds + n16 * 16 + tid * 4, tail);
-}
-
-template <bool FRAME, int MAXC>
-__global__ __launch_bounds__(kWG, 2) void decode_fixed_pipe_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
-                                                                const uint8_t* __restrict__ in, int32_t* status,
-                                                                int64_t tiles) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int HDR = FRAME ? 12 : 0;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int stride = L.stride;
-  const int hdr_bm = HDR + L.bitmap_bytes;
-  int64_t t = blockIdx.x;
-  if (t >= tiles) return;
-
-  u32x4 buf[MAXC];
-  uint32_t tail = 0;
-  auto rows_of = [&](int64_t tile) {
-    const int64_t left = L.num_rows - tile * 64;
-    return left < 64 ? (int)left : 64;
-  };
-  stage_issue<MAXC>(buf, tail, in + t * 64 * stride, rows_of(t) * stride, tid);
-  stage_commit<MAXC>(buf, tail, lds, rows_of(t) * stride, tid);
-  __syncthreads();
-  const uint8_t* row = lds + lane * stride;
-  for (;;) {
-    const int64_t tn = t + gridDim.x;
-    if (tn < tiles) stage_issue<MAXC>(buf, tail, in + tn * 64 * stride, rows_of(tn) * stride, tid);
-    const int64_t r0 = t * 64;
-    const int rows = rows_of(t);
-    const bool live = lane < rows;
-    const int64_t grow = r0 + lane;
-    if (FRAME && wave == 0 && live) check_frame<FRAME>(row, L, status);
-    dec_group<8, 64, FRAME>(fields, L.group[0], L.group[1], wave, 0, lane, row, hdr_bm, HDR, live, grow, r0, rows);
-    dec_group<4, 64, FRAME>(fields, L.group[1], L.group[2], wave, 0, lane, row, hdr_bm, HDR, live, grow, r0, rows);
-    dec_group<2, 64, FRAME>(fields, L.group[2], L.group[3], wave, 0, lane, row, hdr_bm, HDR, live, grow, r0, rows);
-    dec_group<1, 64, FRAME>(fields, L.group[3], L.group[4], wave, 0, lane, row, hdr_bm, HDR, live, grow, r0, rows);
-    __syncthreads();
-    if (tn >= tiles) break;
-    stage_commit<MAXC>(buf, tail, lds, rows_of(tn) * stride, tid);
-    __syncthreads();
-    t = tn;
-  }
-}
-
-__global__ void fill_offsets_kernel(int64_t* offs, int64_t n, int64_t stride) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i <= n) offs[i] = i * stride;
-}
-
-// ---------------------------------------------------------------------------
-// Device-wide scan (3 kernels): block reduce, scan of partials, downsweep.
-// ---------------------------------------------------------------------------
-constexpr int kScanItems = 16;
-constexpr int kScanTile = kWG * kScanItems;  // 4096 items per block
-
-__device__ __forceinline__ int64_t wave_incl_scan(int64_t x, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int64_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  return x;
-}
-
-// Returns the exclusive prefix of `x` over the workgroup; *total = sum.
-__device__ __forceinline__ int64_t block_excl_scan(int64_t x, int64_t* smem, int64_t* total) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t inc = wave_incl_scan(x, lane);
-  if (lane == 63) smem[w] = inc;
-  __syncthreads();
-  int64_t wpre = 0, tot = 0;
-#pragma unroll
-  for (int k = 0; k < kWaves; ++k) {
-    const int64_t s = smem[k];
-    if (k < w) wpre += s;
-    tot += s;
-  }
-  __syncthreads();
-  *total = tot;
-  return wpre + inc - x;
-}
-
-// MODE 0: int64 data, exclusive, data[n] = total.
-// MODE 1: int32 Arrow offsets: lengths at offs[1..n], inclusive into offs[1..n].
-template <int MODE>
-__device__ __forceinline__ int64_t scan_load(void* data, int64_t i) {
-  if (MODE == 0) return reinterpret_cast<const int64_t*>(data)[i];
-  return reinterpret_cast<const int32_t*>(data)[i + 1];
-}
-
-template <int MODE>
-__global__ __launch_bounds__(kWG) void scan_reduce_kernel(void* data, int64_t n, int64_t* partials) {
-  __shared__ int64_t smem[kWaves];
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-  int64_t s = 0;
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k)
-    if (base + k < n) s += scan_load<MODE>(data, base + k);
-  int64_t tot;
-  block_excl_scan(s, smem, &tot);
-  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
-}
-
-// Single workgroup: exclusive scan of the partials in place (any count).
-__global__ __launch_bounds__(kWG) void scan_partials_kernel(int64_t* partials, int64_t nb) {
-  __shared__ int64_t smem[kWaves];
-  int64_t carry = 0;
-  for (int64_t b0 = 0; b0 < nb; b0 += kScanTile) {
-    const int64_t base = b0 + (int64_t)threadIdx.x * kScanItems;
-    int64_t v[kScanItems];
-    int64_t s = 0;
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-      v[k] = base + k < nb ? partials[base + k] : 0;
-      s += v[k];
-    }
-    int64_t tot;
-    int64_t pre = block_excl_scan(s, smem, &tot) + carry;
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-      if (base + k < nb) partials[base + k] = pre;
-      pre += v[k];
-    }
-    carry += tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) partials[nb] = carry;
-}
-
-// SEG (MODE 1): a segment of a longer offsets array: data[0] already holds the
-// previous segment's last offset (the carry; 0 for the first) and is left as is.
-template <int MODE, bool SEG = false>
-__global__ __launch_bounds__(kWG) void scan_down_kernel(void* data, int64_t n, const int64_t* partials,
-                                                        int32_t* status) {
-  __shared__ int64_t smem[kWaves];
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-  int64_t v[kScanItems];
-  int64_t s = 0;
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    v[k] = base + k < n ? scan_load<MODE>(data, base + k) : 0;
-    s += v[k];
-  }
-  int64_t tot;
-  int64_t pre = block_excl_scan(s, smem, &tot) + partials[blockIdx.x];
-  if (SEG) pre += reinterpret_cast<const int32_t*>(data)[0];
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    if (base + k < n) {
-      if (MODE == 0) {
-        reinterpret_cast<int64_t*>(data)[base + k] = pre;
-        pre += v[k];
-      } else {
-        pre += v[k];
-        if (pre > 0x7fffffffLL) set_status(status, FORY_ERR_CAPACITY);
-        reinterpret_cast<int32_t*>(data)[base + k + 1] = (int32_t)pre;
-      }
-    }
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    if (MODE == 0) reinterpret_cast<int64_t*>(data)[n] = partials[gridDim.x];
-    else if (!SEG) reinterpret_cast<int32_t*>(data)[0] = 0;
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Varlen / nested: per-record op program, one lane per record.
@@ -2279,11 +1024,10 @@ __global__ __launch_bounds__(64) void var_decode_tile_kernel(VarLaunch L, const 
 // bigger than the LDS image take per-lane paths with the same results.
 // ---------------------------------------------------------------------------
 
-// Waves that place var fields in the encode tile kernel: waves 1..NW-1 (wave 0
-// lays the rows out) when every field gets a wave of its own, else all NW.
 // Waves that place var payloads in the encode tile kernel: all NW when num_var >= NW
-// (wave 0 takes its fields after the layout); FORY_ROWFMT_VARPL=0 keeps wave 0 to
-// the layout (waves 1..NW-1 place everything: Mixed encode 6.42 -> 6.77 ms, so off).
+// (wave 0 takes its fields after the layout), else waves 1..NW-1 (wave 0 lays the
+// rows out). Keeping wave 0 to the layout always was slower (Mixed encode 6.42 ->
+// 6.77 ms); pl_all = 0 selects it.
 __host__ __device__ __forceinline__ int var_placers(int num_var, int nw, int pl_all) {
   return pl_all && num_var >= nw ? nw : nw - 1;
 }
@@ -3281,432 +2025,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
 #undef DEC_STAMP
 }
 
-
-template <typename K>
-void raise_lds_cap(K* kernel) {
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
-}
-
-int num_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
-    if (cus <= 0) cus = 256;
-  }
-  return cus;
-}
-
-// Persistent grid: resident workgroups per CU (occupancy query) x CUs.
-template <typename K>
-int64_t persistent_grid(K* kernel, size_t lds, int64_t tiles, int wg = kWG) {
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, wg, lds) != hipSuccess || per_cu <= 0)
-    per_cu = 1;
-  const int64_t g = (int64_t)per_cu * num_cus();
-  return tiles < g ? tiles : g;
-}
-
-// Kernel variant for A/B runs (FORY_ROWFMT_PIPE): 0 one tile per workgroup,
-// 1 persistent pipelined (lane = record), 2 / 3 encode v3 with R = 64 / 128,
-// 4 encode v4 column slabs, 5..8 encode v5 depth-2 pipeline (8 = default:
-// R = 64, 512 threads; see try_encode_v5), fallbacks: v3, one-tile kernel.
-int variant() {
-  const char* e = getenv("FORY_ROWFMT_PIPE");
-  return e ? atoi(e) : 8;
-}
-
-template <int R, bool FRAME, bool NULLS, bool PAD>
-hipError_t launch_encode_v3(const FixedLaunch& L, uint8_t* out, hipStream_t s, bool* done) {
-  *done = false;
-  if (v3_insn_count<R>(L.group) > kV3K * (4 * R / 64)) return hipSuccess;  // too many fields: fall back
-  const int64_t full = L.num_rows / R;
-  if (full > 0) {
-    auto* k = &encode_fixed_v3_kernel<R, FRAME, NULLS, PAD>;
-    static bool init = false;
-    if (!init) { raise_lds_cap(k); init = true; }
-    const size_t lds = (size_t)R * (PAD ? L.pitch : L.stride);
-    const int64_t grid = persistent_grid(k, lds, full, 4 * R);
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(4 * R), lds, s, L, L.fields, out, full);
-  }
-  if (L.num_rows > full * R) {  // tail (< R records): one-tile kernel from tile full*R/64
-    FixedLaunch T = L;
-    T.tile0 = full * R / 64;
-    auto* k = &encode_fixed_kernel<64, FRAME>;
-    static bool init2 = false;
-    if (!init2) { raise_lds_cap(k); init2 = true; }
-    const int64_t tail_tiles = (L.num_rows - full * R + 63) / 64;
-    hipLaunchKernelGGL(k, dim3((unsigned)tail_tiles), dim3(kWG), (size_t)64 * L.stride, s, T, L.fields, out);
-  }
-  *done = true;
-  return hipGetLastError();
-}
-
-template <int R, int S>
-hipError_t launch_encode_v4(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
-  const int64_t full = L.num_rows / R;
-  if (full > 0) {
-    auto* k = &encode_fixed_v4_kernel<R, S>;
-    static bool init = false;
-    if (!init) { raise_lds_cap(k); init = true; }
-    const size_t lds = (size_t)R * L.slab_pitch;
-    const int64_t grid = persistent_grid(k, lds, full, 4 * R);
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(4 * R), lds, s, L, L.slab_fields, out, full);
-  }
-  if (L.num_rows > full * R) {  // tail (< R records): one-tile kernel
-    FixedLaunch T = L;
-    T.tile0 = full * R / 64;
-    auto* k = &encode_fixed_kernel<64, false>;
-    static bool init2 = false;
-    if (!init2) { raise_lds_cap(k); init2 = true; }
-    const int64_t tail_tiles = (L.num_rows - full * R + 63) / 64;
-    hipLaunchKernelGGL(k, dim3((unsigned)tail_tiles), dim3(kWG), (size_t)64 * L.stride, s, T, L.fields, out);
-  }
-  return hipGetLastError();
-}
-
-// Cache-policy bits (FORY_ROWFMT_NT, for A/B): 1 nt column loads / 2 nt row
-// stores (encode v5), 4 nt LDS-DMA row loads / 8 nt column stores (decode).
-// Default 2|4|8: at 64M Struct104 rows nt row stores take encode 18.43 ->
-// 18.03 ms, nt loads + stores take decode 17.72 -> 17.52 ms; nt column loads
-// in encode are slower (18.60 ms) (scripts/ab_nt.py, profiles/r01/ab_nt.json).
-int nt_mode() {
-  const char* e = getenv("FORY_ROWFMT_NT");
-  return e ? atoi(e) : 14;
-}
-
-template <int R, int WG, int K, bool FRAME, bool PAD, bool ONESHOT = false, int NT = 0>
-hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
-  const int64_t full = L.num_rows / R;
-  if (full > 0) {
-    auto* k = &encode_fixed_v5_kernel<R, WG, K, FRAME, PAD, ONESHOT, NT>;
-    static bool init = false;
-    if (!init) { raise_lds_cap(k); init = true; }
-    const size_t lds = (size_t)R * (PAD ? L.pitch : L.stride);
-    const int64_t grid = ONESHOT ? full : persistent_grid(k, lds, full, WG);
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(WG), lds, s, L, L.fields, out, full);
-  }
-  if (L.num_rows > full * R) {
-    FixedLaunch T = L;
-    T.tile0 = full * R / 64;
-    auto* k = &encode_fixed_kernel<64, FRAME>;
-    static bool init2 = false;
-    if (!init2) { raise_lds_cap(k); init2 = true; }
-    const int64_t tail_tiles = (L.num_rows - full * R + 63) / 64;
-    hipLaunchKernelGGL(k, dim3((unsigned)tail_tiles), dim3(kWG), (size_t)64 * L.stride, s, T, L.fields, out);
-  }
-  return hipGetLastError();
-}
-
-// v5 (depth-2 pipeline): not-null schemas, <= K load instructions per wave.
-// v5 shapes: 5 = R64/WG256, 6 = R128/WG512 (default), 7 = R128/WG1024, 8 = R64/WG512.
-template <bool FRAME>
-hipError_t try_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s, int var, bool* done) {
-  *done = false;
-  if (L.any_nullable) return hipSuccess;
-  FixedLaunch P = L;
-  P.pitch = L.stride + ((4 - L.stride % 32) + 32) % 32;
-  P.stride_magic = 0xffffffffu / (uint32_t)L.stride;
-  // LDS pitch padding (raw rows): measured neutral-to-negative for the
-  // 512-thread shapes, so off unless FORY_ROWFMT_PAD=1.
-  const bool pad = !FRAME && getenv("FORY_ROWFMT_PAD") && !getenv("FORY_ROWFMT_NOPAD");
-  const int i64 = v3_insn_count<64>(L.group), i128 = v3_insn_count<128>(L.group);
-  hipError_t e = hipSuccess;
-#define V5(R, WG, K)                                                                             \
-  do {                                                                                           \
-    e = pad ? launch_encode_v5<R, WG, K, FRAME, true>(P, out, s) : launch_encode_v5<R, WG, K, FRAME, false>(P, out, s); \
-    *done = true;                                                                                \
-  } while (0)
-  if (var == 5 && (i64 + 3) / 4 <= 12) V5(64, 256, 12);
-  else if (var == 6 && (i128 + 7) / 8 <= 12) V5(128, 512, 12);
-  else if (var == 7 && (i128 + 15) / 16 <= 6) V5(128, 1024, 6);
-  else if (var == 8 && (i64 + 7) / 8 <= 6 && !pad) {
-    switch (nt_mode() & 3) {
-      case 1: e = launch_encode_v5<64, 512, 6, FRAME, false, false, 1>(P, out, s); break;
-      case 2: e = launch_encode_v5<64, 512, 6, FRAME, false, false, 2>(P, out, s); break;
-      case 3: e = launch_encode_v5<64, 512, 6, FRAME, false, false, 3>(P, out, s); break;
-      default: e = launch_encode_v5<64, 512, 6, FRAME, false, false, 0>(P, out, s); break;
-    }
-    *done = true;
-  } else if (var == 8 && (i64 + 7) / 8 <= 6) V5(64, 512, 6);
-  else if (var == 9 && (i64 + 7) / 8 <= 6) {  // one-shot shapes
-    e = launch_encode_v5<64, 512, 6, FRAME, false, true>(P, out, s);
-    *done = true;
-  } else if (var == 10 && (i64 + 3) / 4 <= 12) {
-    e = launch_encode_v5<64, 256, 12, FRAME, false, true>(P, out, s);
-    *done = true;
-  } else if (var == 11 && (i128 + 7) / 8 <= 12) {
-    e = launch_encode_v5<128, 512, 12, FRAME, false, true>(P, out, s);
-    *done = true;
-  }
-#undef V5
-  return e;
-}
-
-// v4 applies to raw rows of not-null schemas whose row size is a multiple of
-// 16 and whose slabs fit kV4K instructions per wave.
-bool v4_ok(const FixedLaunch& L) {
-  if (L.frame || L.any_nullable || L.num_slabs < 2 || L.num_slabs > 4 || (L.fixed_size & 15)) return false;
-  for (int s = 0; s < L.num_slabs; ++s)
-    if (v3_insn_count<64>(L.slab[s].group) > kV4K * 4) return false;
-  return L.slab_fields != nullptr;
-}
-
-template <int TR, bool FRAME>
-hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
-  const int64_t tiles = (L.num_rows + TR - 1) / TR;
-  const size_t lds = (size_t)TR * L.stride;
-  if constexpr (TR == 64) {
-    const int var = variant();
-    if (var >= 5 && var <= 11) {  // v5: depth-2 pipeline / one-shot (shapes: try_encode_v5)
-      bool done = false;
-      hipError_t e = try_encode_v5<FRAME>(L, out, s, var, &done);
-      if (done || e != hipSuccess) return e;
-      if (!L.any_nullable) {  // too many fields per wave for v5: v3
-        e = launch_encode_v3<64, FRAME, false, false>(L, out, s, &done);
-        if (done || e != hipSuccess) return e;
-      }
-    }
-    if (var == 4 && !FRAME && v4_ok(L)) {
-      switch (L.num_slabs) {
-        case 2: return launch_encode_v4<64, 2>(L, out, s);
-        case 3: return launch_encode_v4<64, 3>(L, out, s);
-        default: return launch_encode_v4<64, 4>(L, out, s);
-      }
-    }
-    if (var == 4) {  // frames / nullable / odd rows: v3 (R = 64 for frames, 128 otherwise)
-      bool done = false;
-      hipError_t e = hipSuccess;
-      if (!L.any_nullable) {
-        FixedLaunch P = L;
-        P.pitch = L.stride + ((4 - L.stride % 32) + 32) % 32;
-        P.stride_magic = 0xffffffffu / (uint32_t)L.stride;
-        e = FRAME ? launch_encode_v3<64, FRAME, false, false>(L, out, s, &done)
-                  : launch_encode_v3<128, FRAME, false, false>(L, out, s, &done);
-        if (done || e != hipSuccess) return e;
-      }
-    }
-    if (var == 2 || var == 3) {
-      bool done = false;
-      hipError_t e = hipSuccess;
-      // v3 covers not-null schemas (the nullable form spills: falls back below)
-      if (!L.any_nullable) {
-        // raw rows (8-byte aligned slots): padded LDS pitch; frames: pitch = stride
-        FixedLaunch P = L;
-        P.pitch = L.stride + ((4 - L.stride % 32) + 32) % 32;  // pitch = 4 (mod 32) bytes
-        P.stride_magic = 0xffffffffu / (uint32_t)L.stride;
-        if (FRAME || getenv("FORY_ROWFMT_NOPAD"))
-          e = var == 3 ? launch_encode_v3<128, FRAME, false, false>(L, out, s, &done)
-                       : launch_encode_v3<64, FRAME, false, false>(L, out, s, &done);
-        else
-          e = var == 3 ? launch_encode_v3<128, FRAME, false, true>(P, out, s, &done)
-                       : launch_encode_v3<64, FRAME, false, true>(P, out, s, &done);
-        if (done || e != hipSuccess) return e;
-      }
-    }
-    const int n8 = L.group[1] - L.group[0], n4 = L.group[2] - L.group[1];
-    const int n2 = L.group[3] - L.group[2], n1 = L.group[4] - L.group[3];
-    if (n8 <= 4 * kM8 && n4 <= 4 * kM4 && n2 <= 4 * kM2 && n1 <= 4 * kM1 && var == 1) {
-      auto* k = &encode_fixed_pipe_kernel<FRAME>;
-      static bool init = false;
-      if (!init) { raise_lds_cap(k); init = true; }
-      const int64_t grid = persistent_grid(k, lds, tiles, kWG);
-      hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kWG), lds, s, L, L.fields, out, tiles);
-      return hipGetLastError();
-    }
-  }
-  auto* k = &encode_fixed_kernel<TR, FRAME>;
-  static bool init = false;
-  if (!init) { raise_lds_cap(k); init = true; }
-  hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(kWG), lds, s, L, L.fields, out);
-  return hipGetLastError();
-}
-
-template <int TR, int WG, bool FRAME>
-hipError_t launch_decode_v2(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
-  const int64_t tiles = (L.num_rows + TR - 1) / TR;
-  auto* k = &decode_fixed_v2_kernel<TR, WG, FRAME>;
-  static bool init = false;
-  if (!init) { raise_lds_cap(k); init = true; }
-  hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(WG), (size_t)TR * L.stride, s, L, L.fields, in, status);
-  return hipGetLastError();
-}
-
-template <bool FRAME>
-hipError_t launch_decode_v3(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s, bool* done) {
-  constexpr int K = 12;
-  *done = false;
-  if (L.any_nullable || v3_insn_count<64>(L.group) > K * kWaves) return hipSuccess;
-  const int64_t full = L.num_rows / 64;
-  const size_t lds = (size_t)64 * L.stride;
-  if (full > 0) {
-    auto* k = (nt_mode() & 12) == 12 ? &decode_fixed_v3_kernel<FRAME, K, 12> : &decode_fixed_v3_kernel<FRAME, K, 0>;
-    static bool init[2] = {false, false};
-    const int ix = (nt_mode() & 12) == 12;
-    if (!init[ix]) { raise_lds_cap(k); init[ix] = true; }
-    hipLaunchKernelGGL(k, dim3((unsigned)full), dim3(kWG), lds, s, L, L.fields, in, status);
-  }
-  if (L.num_rows > full * 64) {  // tail tile
-    FixedLaunch T = L;
-    T.tile0 = full;
-    auto* k = &decode_fixed_kernel<64, FRAME>;
-    static bool init2 = false;
-    if (!init2) { raise_lds_cap(k); init2 = true; }
-    hipLaunchKernelGGL(k, dim3(1), dim3(kWG), lds, s, T, L.fields, in, status);
-  }
-  *done = true;
-  return hipGetLastError();
-}
-
-int dec_variant() {  // FORY_ROWFMT_DEC: 0 decode_fixed_kernel (default), 1..3 decode v2 shapes, 4 TR=32, 5 decode v3
-  const char* e = getenv("FORY_ROWFMT_DEC");
-  return e ? atoi(e) : 0;
-}
-
-template <int TR, bool FRAME>
-hipError_t launch_decode_tr(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
-  const int64_t tiles = (L.num_rows + TR - 1) / TR;
-  const size_t lds = (size_t)TR * L.stride;
-  if constexpr (TR == 64) {
-    const int dv = dec_variant();
-    if (dv == 5) {
-      bool done = false;
-      hipError_t e = launch_decode_v3<FRAME>(L, in, status, s, &done);
-      if (done || e != hipSuccess) return e;
-    }
-    if (dv == 1 && 64 * L.stride <= 80 * 1024) return launch_decode_v2<64, 512, FRAME>(L, in, status, s);
-    if (dv == 2 && 128 * L.stride <= 160 * 1024) return launch_decode_v2<128, 512, FRAME>(L, in, status, s);
-    if (dv == 3 && 128 * L.stride <= 160 * 1024) return launch_decode_v2<128, 1024, FRAME>(L, in, status, s);
-    if (dv == 4) {  // 32-record tiles: more workgroups per CU
-      auto* k = &decode_fixed_kernel<32, FRAME>;
-      static bool init32 = false;
-      if (!init32) { raise_lds_cap(k); init32 = true; }
-      hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 31) / 32)), dim3(kWG), (size_t)32 * L.stride, s, L,
-                         L.fields, in, status);
-      return hipGetLastError();
-    }
-    constexpr int MAXC = 14;
-    if (lds <= (size_t)MAXC * kWG * 16 && variant() == 1) {
-      auto* k = &decode_fixed_pipe_kernel<FRAME, MAXC>;
-      static bool init = false;
-      if (!init) { raise_lds_cap(k); init = true; }
-      const int64_t grid = persistent_grid(k, lds, tiles);
-      hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kWG), lds, s, L, L.fields, in, status, tiles);
-      return hipGetLastError();
-    }
-  }
-  auto* k = &decode_fixed_kernel<TR, FRAME>;
-  int nt = 0;
-  if constexpr (TR == 64) {
-    nt = (nt_mode() & 12) >> 2;
-    if (nt == 1) k = &decode_fixed_kernel<TR, FRAME, 4>;
-    else if (nt == 2) k = &decode_fixed_kernel<TR, FRAME, 8>;
-    else if (nt == 3) k = &decode_fixed_kernel<TR, FRAME, 12>;
-  }
-  static bool init[4] = {false, false, false, false};
-  if (!init[nt]) { raise_lds_cap(k); init[nt] = true; }
-  hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(kWG), lds, s, L, L.fields, in, status);
-  return hipGetLastError();
-}
-
 }  // namespace
-
-// Records per tile: 64 (one field per wave-instruction) while a tile fits
-// 80 KiB of LDS (two workgroups per CU), else fewer records, more fields.
-static int pick_tr(int stride) {
-  if (64 * stride <= 80 * 1024) return 64;
-  if (32 * stride <= 80 * 1024) return 32;
-  if (16 * stride <= 80 * 1024) return 16;
-  if (8 * stride <= 160 * 1024) return 8;
-  return 0;
-}
-
-hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
-  if (L.num_rows <= 0) return hipSuccess;
-  switch (pick_tr(L.stride) * 2 + (L.frame ? 1 : 0)) {
-    case 128: return launch_encode_tr<64, false>(L, out, s);
-    case 129: return launch_encode_tr<64, true>(L, out, s);
-    case 64: return launch_encode_tr<32, false>(L, out, s);
-    case 65: return launch_encode_tr<32, true>(L, out, s);
-    case 32: return launch_encode_tr<16, false>(L, out, s);
-    case 33: return launch_encode_tr<16, true>(L, out, s);
-    case 16: return launch_encode_tr<8, false>(L, out, s);
-    case 17: return launch_encode_tr<8, true>(L, out, s);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-hipError_t launch_decode_fixed(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
-  if (L.num_rows <= 0) return hipSuccess;
-  switch (pick_tr(L.stride) * 2 + (L.frame ? 1 : 0)) {
-    case 128: return launch_decode_tr<64, false>(L, in, status, s);
-    case 129: return launch_decode_tr<64, true>(L, in, status, s);
-    case 64: return launch_decode_tr<32, false>(L, in, status, s);
-    case 65: return launch_decode_tr<32, true>(L, in, status, s);
-    case 32: return launch_decode_tr<16, false>(L, in, status, s);
-    case 33: return launch_decode_tr<16, true>(L, in, status, s);
-    case 16: return launch_decode_tr<8, false>(L, in, status, s);
-    case 17: return launch_decode_tr<8, true>(L, in, status, s);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-bool fixed_tiled_supported(int stride) { return pick_tr(stride) != 0; }
-
-hipError_t launch_fill_offsets(int64_t* offs, int64_t n, int64_t stride, hipStream_t s) {
-  const int64_t blocks = (n + 1 + kWG - 1) / kWG;
-  hipLaunchKernelGGL(fill_offsets_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, offs, n, stride);
-  return hipGetLastError();
-}
-
-int64_t scan_partials(int64_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
-
-hipError_t launch_scan_i64(int64_t* data, int64_t n, int64_t* partials, hipStream_t s) {
-  const int64_t nb = (n + kScanTile - 1) / kScanTile;
-  if (n <= 0) {
-    (void)hipMemsetAsync(data, 0, sizeof(int64_t), s);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL(scan_reduce_kernel<0>, dim3((unsigned)nb), dim3(kWG), 0, s, (void*)data, n, partials);
-  hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kWG), 0, s, partials, nb);
-  hipLaunchKernelGGL(scan_down_kernel<0>, dim3((unsigned)nb), dim3(kWG), 0, s, (void*)data, n,
-                     (const int64_t*)partials, (int32_t*)nullptr);
-  return hipGetLastError();
-}
-
-hipError_t launch_scan_offsets_i32(int32_t* offs, int64_t n, int64_t* partials, int32_t* status,
-                                   hipStream_t s) {
-  const int64_t nb = (n + kScanTile - 1) / kScanTile;
-  if (n <= 0) {
-    (void)hipMemsetAsync(offs, 0, sizeof(int32_t), s);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL(scan_reduce_kernel<1>, dim3((unsigned)nb), dim3(kWG), 0, s, (void*)offs, n, partials);
-  hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kWG), 0, s, partials, nb);
-  hipLaunchKernelGGL(scan_down_kernel<1>, dim3((unsigned)nb), dim3(kWG), 0, s, (void*)offs, n,
-                     (const int64_t*)partials, status);
-  return hipGetLastError();
-}
-
-hipError_t launch_scan_offsets_i32_segmented(int32_t* offs, int64_t n, int64_t* partials, int64_t partial_words,
-                                             int32_t* status, hipStream_t s) {
-  (void)hipMemsetAsync(offs, 0, sizeof(int32_t), s);
-  const int64_t seg = kScanTile * (partial_words - 1);
-  if (n <= 0) return hipGetLastError();
-  if (seg <= 0) return hipErrorInvalidValue;
-  for (int64_t a = 0; a < n; a += seg) {
-    const int64_t m = n - a < seg ? n - a : seg;
-    const int64_t nb = (m + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(scan_reduce_kernel<1>, dim3((unsigned)nb), dim3(kWG), 0, s, (void*)(offs + a), m, partials);
-    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(kWG), 0, s, partials, nb);
-    hipLaunchKernelGGL((scan_down_kernel<1, true>), dim3((unsigned)nb), dim3(kWG), 0, s, (void*)(offs + a), m,
-                       (const int64_t*)partials, status);
-  }
-  return hipGetLastError();
-}
 
 hipError_t launch_var_sizes(const VarLaunch& L, int64_t* d_row_offsets, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
@@ -3715,7 +2034,16 @@ hipError_t launch_var_sizes(const VarLaunch& L, int64_t* d_row_offsets, hipStrea
   return hipGetLastError();
 }
 
-// FORY_ROWFMT_VARTILE=0: per-record global interpreters only (A/B baseline).
+namespace {
+
+// Test knobs (environment, read per call): they force the fallback engines and
+// LDS budgets so the parity suite exercises every path; none selects a rejected
+// variant.
+//   FORY_ROWFMT_VARTILE=0   per-record global interpreter for every tile
+//   FORY_ROWFMT_VARFLAT=0   generic tile interpreter for cooperative plans too
+//   FORY_ROWFMT_VARCAP / FORY_ROWFMT_SPILLCAP / FORY_ROWFMT_VARFIT   LDS image budgets
+//   FORY_ROWFMT_VARSTG      staging slot bytes
+//   FORY_ROWFMT_VARPROF=1   phase timeline (debug), FORY_ROWFMT_VARDIAG=1 LDS sizing to stderr
 bool var_tiles() {
   const char* e = getenv("FORY_ROWFMT_VARTILE");
   return !e || atoi(e) != 0;
@@ -3740,23 +2068,18 @@ int fit_cap(const VarLaunch& L, int64_t mean_row) {
   return (int)need;
 }
 
-template <typename K>
-void var_tile_launch(K* k, const VarLaunch&, int) {
-  // once per kernel (kernels of one signature share this instantiation)
-  static const void* done[16] = {};
-  static int nd = 0;
-  for (int i = 0; i < nd; ++i)
-    if (done[i] == reinterpret_cast<const void*>(k)) return;
-  raise_lds_cap(k);
-  if (nd < 16) done[nd++] = reinterpret_cast<const void*>(k);
-}
-
+// Debug timeline of the cooperative kernels (FORY_ROWFMT_VARPROF=1): one
+// process-wide buffer, 8 stamps per tile.
+std::mutex g_prof_mu;
 uint64_t* g_prof = nullptr;
 int64_t g_prof_words = 0;
+
+}  // namespace
 
 uint64_t* var_prof_buffer(int64_t tiles) {
   const char* e = getenv("FORY_ROWFMT_VARPROF");
   if (!e || atoi(e) == 0) return nullptr;
+  std::lock_guard<std::mutex> lock(g_prof_mu);
   if (tiles * 8 > g_prof_words) {
     if (g_prof) (void)hipFree(g_prof);
     g_prof = nullptr;
@@ -3768,6 +2091,7 @@ uint64_t* var_prof_buffer(int64_t tiles) {
 }
 
 int64_t var_prof_copy(uint64_t* host, int64_t max_words) {
+  std::lock_guard<std::mutex> lock(g_prof_mu);
   if (!g_prof) return 0;
   const int64_t n = max_words < g_prof_words ? max_words : g_prof_words;
   if (hipDeviceSynchronize() != hipSuccess) return -1;
@@ -3775,39 +2099,48 @@ int64_t var_prof_copy(uint64_t* host, int64_t max_words) {
   return n;
 }
 
-// FORY_ROWFMT_VARFLAT=0: generic tile interpreter for flat plans too (A/B).
+namespace {
+
 bool var_flat(const VarLaunch& L) {
   const char* e = getenv("FORY_ROWFMT_VARFLAT");
   return L.flat && (!e || atoi(e) != 0);
 }
 
-int flat_nw() {  // FORY_ROWFMT_VARNW: waves per 64-record tile (4 or 8)
-  const char* e = getenv("FORY_ROWFMT_VARNW");
-  return e && atoi(e) == 8 ? 8 : 4;
-}
+constexpr int kNW = 4;  // waves per 64-record tile of the cooperative kernels (8 was slower at every occupancy)
 
 size_t sbase_lds(const VarLaunch& L) {
   return L.num_struct ? (size_t)(1 + L.num_struct) * 64 * sizeof(int32_t) : 0;
 }
 
-// LDS of the flat tile kernels: row image, per-wave staging, payload offsets
-// (encode) and child-row offsets (nested plans).
-size_t flat_lds(const VarLaunch& L, int cap, int nw) {
-  return (size_t)cap + (size_t)nw * L.stg_bytes + (size_t)L.num_var * 64 * sizeof(int32_t) + sbase_lds(L);
-}
-
-// Encode: staging only for the min(NW, num_var) waves that place var fields.
+// Encode LDS: row image, staging for the min(NW, num_var) waves that place var
+// fields, payload offsets and child-row offsets (nested plans).
 size_t flat_lds_enc(const VarLaunch& L, int cap, int nw) {
-  const int np = var_placers(L.num_var, nw, L.pl_all);
+  const int np = var_placers(L.num_var, nw, 1);
   const int nslot = L.num_var < np ? L.num_var : np;
   return (size_t)cap + (size_t)nslot * L.stg_bytes + (size_t)L.num_var * 64 * sizeof(int32_t) + sbase_lds(L);
+}
+
+// The largest slot (up to b) that keeps the most resident workgroups any slot in
+// [1, 2] KiB reaches (occupancy with the kernel's registers and LDS).
+template <typename K, typename F>
+int fit_slot(K* k, int threads, int b, F lds_of) {
+  int want = -1;
+  for (int t = 2048; t >= 1024; t -= 256) {
+    const int o = occupancy_of(k, threads, lds_of(t));
+    want = o > want ? o : want;
+  }
+  int r = 1024;
+  if (want > 0) {
+    r = b;
+    while (r > 1024 && occupancy_of(k, threads, lds_of(r)) < want) r -= 256;
+  }
+  return r;
 }
 
 // Encode staging per slot sized from the caller's capacity (normally the exact
 // encoded size): 1.5x the mean per-field span of a 64-record tile, in [2, 16] KiB,
 // so most tiles stage each field in one record group -- but never at the cost of
-// resident workgroups (hipOccupancy with the kernel's registers and LDS):
-// FORY_ROWFMT_VARSTG overrides.
+// resident workgroups. FORY_ROWFMT_VARSTG overrides.
 template <typename K>
 int enc_stg_bytes(K* k, const VarLaunch& L, int64_t capacity, int cap, int nw) {
   if (getenv("FORY_ROWFMT_VARSTG") || L.num_rows < 64 || L.num_var == 0) return L.stg_bytes;
@@ -3815,35 +2148,11 @@ int enc_stg_bytes(K* k, const VarLaunch& L, int64_t capacity, int cap, int nw) {
   const int64_t per = var_row > 0 ? 64 * var_row / L.num_var : 0;
   int b = (int)((per * 3 / 2 + 512 + 255) & ~int64_t(255));
   b = b < 2048 ? 2048 : (b > 16384 ? 16384 : b);
-  auto occ = [&](int stg) {
+  return fit_slot(k, 64 * nw, b, [&](int stg) {
     VarLaunch T = L;
     T.stg_bytes = stg;
-    int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(k), 64 * nw,
-                                                     flat_lds_enc(T, cap, nw)) != hipSuccess)
-      return -1;
-    return blocks;
-  };
-  // memo of the last answer per instantiation (same plan shape -> same answer)
-  static const void* m_k = nullptr;
-  static int m_cap = -1, m_b = -1, m_nv = -1, m_ns = -1, m_pl = -1, m_res = 2048;
-  if (m_k == (const void*)k && m_cap == cap && m_b == b && m_nv == L.num_var && m_ns == L.num_struct &&
-      m_pl == L.pl_all)
-    return m_res;
-  // the most resident workgroups any slot size in [1, 2] KiB reaches, then the
-  // largest slot (up to b) that keeps them
-  int want = -1;
-  for (int t = 2048; t >= 1024; t -= 256) {
-    const int o = occ(t);
-    want = o > want ? o : want;
-  }
-  int r = 1024;
-  if (want > 0) {
-    r = b;
-    while (r > 1024 && occ(r) < want) r -= 256;
-  }
-  m_k = (const void*)k, m_cap = cap, m_b = b, m_nv = L.num_var, m_ns = L.num_struct, m_pl = L.pl_all, m_res = r;
-  return r;
+    return flat_lds_enc(T, cap, nw);
+  });
 }
 
 // LDS image of the spill launches: 3x the main image, in [32, 96] KiB
@@ -3879,109 +2188,65 @@ int dec_stg_bytes(K* k, const VarLaunch& L, int cap, int nw) {
   if (getenv("FORY_ROWFMT_VARSTG") || L.num_var == 0) return L.stg_bytes;
   int b = (int)(((int64_t)64 * L.var_est_row * 5 / 4 + 512 + 255) & ~int64_t(255));
   b = b < 2048 ? 2048 : (b > 16384 ? 16384 : b);
-  auto occ = [&](int stg) {
+  return fit_slot(k, 64 * nw, b, [&](int stg) {
     VarLaunch T = L;
     T.stg_bytes = stg;
-    int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(k), 64 * nw,
-                                                     flat_lds_dec(T, cap, nw)) != hipSuccess)
-      return -1;
-    return blocks;
-  };
-  static int m_cap = -1, m_b = -1, m_nv = -1, m_ns = -1, m_res = 2048;
-  if (m_cap == cap && m_b == b && m_nv == L.num_var && m_ns == L.num_struct) return m_res;
-  // the most resident workgroups any slot size in [1, 2] KiB reaches, then the
-  // largest slot (up to b) that keeps them
-  int want = -1;
-  for (int t = 2048; t >= 1024; t -= 256) {
-    const int o = occ(t);
-    want = o > want ? o : want;
-  }
-  int r = 1024;
-  if (want > 0) {
-    r = b;
-    while (r > 1024 && occ(r) < want) r -= 256;
-  }
-  m_cap = cap, m_b = b, m_nv = L.num_var, m_ns = L.num_struct, m_res = r;
-  return r;
+    return flat_lds_dec(T, cap, nw);
+  });
 }
 
 // Grows a data-fitted tile image (fit_cap) in 256-B steps, up to +20 %, while the
 // resident workgroups per CU stay the same: spill margin that costs no occupancy.
-// Memoised per kernel instantiation (same inputs -> same answer).
 template <typename K, typename F>
-int grow_cap(K* k, int threads, int cap, int key, F lds_of) {
+int grow_cap(K* k, int threads, int cap, F lds_of) {
   if (getenv("FORY_ROWFMT_VARCAP") || getenv("FORY_ROWFMT_VARFIT")) return cap;
-  static const void* m_k = nullptr;
-  static int m_cap = -1, m_key = -1, m_res = 0;
-  if (m_k == (const void*)k && m_cap == cap && m_key == key) return m_res;
-  auto occ = [&](int c) {
-    int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(k), threads, lds_of(c)) !=
-        hipSuccess)
-      return -1;
-    return b;
-  };
-  const int b0 = occ(cap);
+  const int b0 = occupancy_of(k, threads, lds_of(cap));
   int c = cap;
   const int limit = cap * 6 / 5 < 64 * 1024 ? cap * 6 / 5 : 64 * 1024;
   if (b0 > 0)
-    while (c + 256 <= limit && occ(c + 256) >= b0) c += 256;
-  m_k = (const void*)k, m_cap = cap, m_key = key, m_res = c;
+    while (c + 256 <= limit && occupancy_of(k, threads, lds_of(c + 256)) >= b0) c += 256;
   return c;
 }
 
 // FORY_ROWFMT_VARDIAG=1: the tile kernels' LDS sizing and resulting residency, to stderr.
 template <typename K>
 void var_diag(const char* what, K* k, int threads, int cap, int stg, size_t lds) {
-  static const bool on = getenv("FORY_ROWFMT_VARDIAG") != nullptr;
-  if (!on) return;
-  int b = 0;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(k), threads, lds);
+  if (!getenv("FORY_ROWFMT_VARDIAG")) return;
   fprintf(stderr, "[fory_rowfmt] %s tile kernel: image %d B, staging %d B/slot, LDS %zu B, %d workgroups/CU\n", what,
-          cap, stg, lds, b);
+          cap, stg, lds, occupancy_of(k, threads, lds));
 }
 
+// Encode: default or lean kernel (5 waves per SIMD register budget), whichever keeps
+// more workgroups per CU resident with its own staging / image sizing (ties: default).
 template <bool FRAME, int NW, bool PROF>
 void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                        int cap, hipStream_t s) {
   VarLaunch L = L0;
-  const char* pl = getenv("FORY_ROWFMT_VARPL");
-  L.pl_all = pl ? atoi(pl) : 1;
-  // default or lean kernel: whichever keeps more workgroups per CU resident with its
-  // own staging / image sizing (ties: default; FORY_ROWFMT_VARLEAN=0/1 forces)
+  L.pl_all = 1;
   auto* kd = &var_encode_flat_kernel<FRAME, NW, PROF, false>;
   auto* kl = &var_encode_flat_lean_kernel<FRAME, NW, PROF, false>;
-  var_tile_launch(kd, L0, cap);
-  var_tile_launch(kl, L0, cap);
   auto size_for = [&](decltype(kd) kk, int* stg, int* c) {
     VarLaunch T = L;
     *stg = enc_stg_bytes(kk, T, capacity, cap, NW);
     T.stg_bytes = *stg;
-    *c = grow_cap(kk, 64 * NW, cap, *stg * 4096 + L.num_var * 64 + L.num_struct,
-                  [&](int x) { return flat_lds_enc(T, x, NW); });
-    T.stg_bytes = *stg;
-    int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(kk), 64 * NW,
-                                                     flat_lds_enc(T, *c, NW)) != hipSuccess)
-      b = 0;
-    return b;
+    *c = grow_cap(kk, 64 * NW, cap, [&](int x) { return flat_lds_enc(T, x, NW); });
+    return occupancy_of(kk, 64 * NW, flat_lds_enc(T, *c, NW));
   };
   int stg_d = 0, cap_d = cap, stg_l = 0, cap_l = cap;
   const int occ_d = size_for(kd, &stg_d, &cap_d);
   const int occ_l = size_for(kl, &stg_l, &cap_l);
-  const char* lean_env = getenv("FORY_ROWFMT_VARLEAN");
-  const bool lean = lean_env ? atoi(lean_env) != 0 : occ_l > occ_d;
+  const bool lean = occ_l > occ_d;
   auto* k = lean ? kl : kd;
   L.stg_bytes = lean ? stg_l : stg_d;
   cap = lean ? cap_l : cap_d;
+  raise_lds_cap(k);
   const SpillArgs sp = spill_args(L, cap);
   (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
   var_diag(lean ? "encode (lean)" : "encode", k, 64 * NW, cap, L.stg_bytes, flat_lds_enc(L, cap, NW));
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds_enc(L, cap, NW), s, L, L.prog,
                      L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, cap, sp);
   auto* k2 = lean ? &var_encode_flat_lean_kernel<FRAME, NW, PROF, true> : &var_encode_flat_kernel<FRAME, NW, PROF, true>;
-  var_tile_launch(k2, L, sp.cap);
+  raise_lds_cap(k2);
   hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds_enc(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
                      flat_lds_enc(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, sp.cap,
                      sp);
@@ -3998,12 +2263,10 @@ template <bool FRAME, bool WRITE, int NW>
 void launch_flat_dec(const VarLaunch& L0, const uint8_t* rows, const int64_t* offs, int64_t* tile_tot,
                      int32_t* status, int cap, hipStream_t s) {
   auto* k = &var_decode_flat_kernel<FRAME, WRITE, NW, false>;
-  var_tile_launch(k, L0, cap);
+  raise_lds_cap(k);
   VarLaunch L = L0;
   if (WRITE) L.stg_bytes = dec_stg_bytes(k, L0, cap, NW);
-  if (WRITE && L.mean_row > 0)
-    cap = grow_cap(k, 64 * NW, cap, L.stg_bytes * 4096 + L.num_var * 64 + L.num_struct,
-                   [&](int c) { return flat_lds_dec(L, c, NW); });
+  if (WRITE && L.mean_row > 0) cap = grow_cap(k, 64 * NW, cap, [&](int c) { return flat_lds_dec(L, c, NW); });
   const SpillArgs sp = spill_args(L, cap);
   (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
   const size_t lds = WRITE ? flat_lds_dec(L, cap, NW) : (size_t)cap + sbase_lds(L);  // pass 1: row image (+ struct offsets)
@@ -4011,7 +2274,7 @@ void launch_flat_dec(const VarLaunch& L0, const uint8_t* rows, const int64_t* of
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
                      L.vf, L.st, rows, offs, tile_tot, status, cap, sp);
   auto* k2 = &var_decode_flat_kernel<FRAME, WRITE, NW, true>;
-  var_tile_launch(k2, L, sp.cap);
+  raise_lds_cap(k2);
   const size_t lds2 = WRITE ? flat_lds_dec(L, sp.cap, NW) : (size_t)sp.cap + sbase_lds(L);
   hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, lds2, 64 * NW)), dim3(64 * NW), lds2, s, L, L.prog, L.cols, L.fix,
                      L.vf, L.st, rows, offs, tile_tot, status, sp.cap, sp);
@@ -4024,64 +2287,24 @@ int enc_cap(const VarLaunch& L, int64_t capacity) {
   return fit_cap(L, capacity / L.num_rows);
 }
 
-hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity,
-                             int32_t* status, hipStream_t s) {
-  if (L.num_rows <= 0) return hipSuccess;
-  if (var_tiles() && var_flat(L)) {
-    const int cap = enc_cap(L, capacity);
-    const int nw = flat_nw();
-    if (L.frame) {
-      if (nw == 8) launch_flat_enc<true, 8>(L, offs, out, capacity, status, cap, s);
-      else launch_flat_enc<true, 4>(L, offs, out, capacity, status, cap, s);
-    } else {
-      if (nw == 8) launch_flat_enc<false, 8>(L, offs, out, capacity, status, cap, s);
-      else launch_flat_enc<false, 4>(L, offs, out, capacity, status, cap, s);
-    }
-    return hipGetLastError();
-  }
-  if (var_tiles()) {
-    const int cap = enc_cap(L, capacity);
-    const SpillArgs sp = spill_args(L, cap);
-    (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
-    var_tile_launch(&var_encode_tile_kernel<false>, L, cap);
-    hipLaunchKernelGGL(var_encode_tile_kernel<false>, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64),
-                       (size_t)cap, s, L, L.prog, L.cols, offs, out, capacity, status, cap, sp);
-    var_tile_launch(&var_encode_tile_kernel<true>, L, sp.cap);
-    hipLaunchKernelGGL(var_encode_tile_kernel<true>,
-                       dim3(spill_grid(&var_encode_tile_kernel<true>, L, (size_t)sp.cap, 64)), dim3(64),
-                       (size_t)sp.cap, s, L, L.prog, L.cols, offs, out, capacity, status, sp.cap, sp);
-    return hipGetLastError();
-  }
-  const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
-  hipLaunchKernelGGL(var_encode_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.prog, L.cols, offs, out,
-                     capacity, status);
-  return hipGetLastError();
-}
-
 template <bool WRITE>
 hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int64_t* tile_tot,
                                   int32_t* status, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
   if (var_tiles() && var_flat(L)) {
     const int cap = fit_cap(L, L.mean_row);
-    const int nw = flat_nw();
-    if (L.frame) {
-      if (nw == 8) launch_flat_dec<true, WRITE, 8>(L, rows, offs, tile_tot, status, cap, s);
-      else launch_flat_dec<true, WRITE, 4>(L, rows, offs, tile_tot, status, cap, s);
-    } else {
-      if (nw == 8) launch_flat_dec<false, WRITE, 8>(L, rows, offs, tile_tot, status, cap, s);
-      else launch_flat_dec<false, WRITE, 4>(L, rows, offs, tile_tot, status, cap, s);
-    }
+    if (L.frame) launch_flat_dec<true, WRITE, kNW>(L, rows, offs, tile_tot, status, cap, s);
+    else launch_flat_dec<false, WRITE, kNW>(L, rows, offs, tile_tot, status, cap, s);
     return hipGetLastError();
   }
   if (var_tiles()) {
     const int cap = var_cap(L);
     const SpillArgs sp = spill_args(L, cap);
     (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
-    var_tile_launch(&var_decode_tile_kernel<WRITE, false>, L, cap);
+    raise_lds_cap(&var_decode_tile_kernel<WRITE, false>);
     hipLaunchKernelGGL((var_decode_tile_kernel<WRITE, false>), dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64),
                        (size_t)cap, s, L, L.prog, L.cols, rows, offs, status, cap, sp);
-    var_tile_launch(&var_decode_tile_kernel<WRITE, true>, L, sp.cap);
+    raise_lds_cap(&var_decode_tile_kernel<WRITE, true>);
     hipLaunchKernelGGL((var_decode_tile_kernel<WRITE, true>),
                        dim3(spill_grid(&var_decode_tile_kernel<WRITE, true>, L, (size_t)sp.cap, 64)), dim3(64),
                        (size_t)sp.cap, s, L, L.prog, L.cols, rows, offs, status, sp.cap, sp);
@@ -4090,6 +2313,36 @@ hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const
   const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
   hipLaunchKernelGGL(var_decode_kernel<WRITE>, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.prog, L.cols, rows, offs,
                      status);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity,
+                             int32_t* status, hipStream_t s) {
+  if (L.num_rows <= 0) return hipSuccess;
+  if (var_tiles() && var_flat(L)) {
+    const int cap = enc_cap(L, capacity);
+    if (L.frame) launch_flat_enc<true, kNW>(L, offs, out, capacity, status, cap, s);
+    else launch_flat_enc<false, kNW>(L, offs, out, capacity, status, cap, s);
+    return hipGetLastError();
+  }
+  if (var_tiles()) {
+    const int cap = enc_cap(L, capacity);
+    const SpillArgs sp = spill_args(L, cap);
+    (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
+    raise_lds_cap(&var_encode_tile_kernel<false>);
+    hipLaunchKernelGGL(var_encode_tile_kernel<false>, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64),
+                       (size_t)cap, s, L, L.prog, L.cols, offs, out, capacity, status, cap, sp);
+    raise_lds_cap(&var_encode_tile_kernel<true>);
+    hipLaunchKernelGGL(var_encode_tile_kernel<true>,
+                       dim3(spill_grid(&var_encode_tile_kernel<true>, L, (size_t)sp.cap, 64)), dim3(64),
+                       (size_t)sp.cap, s, L, L.prog, L.cols, offs, out, capacity, status, sp.cap, sp);
+    return hipGetLastError();
+  }
+  const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
+  hipLaunchKernelGGL(var_encode_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.prog, L.cols, offs, out,
+                     capacity, status);
   return hipGetLastError();
 }
 

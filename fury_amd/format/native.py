@@ -199,16 +199,28 @@ class HostPipeline:
 
     def decode_var(self, rows, offsets, n: int, frame: int):
         """Host rows -> host columns (HostColumn list, pre-order)."""
+        counts, nbytes = self.decode_var_sizes(rows, offsets, n, frame)
+        return self.decode_var_finish(counts, nbytes)
+
+    def decode_var_sizes(self, rows, offsets, n: int, frame: int):
+        """fory_rowfmt_host_decode_var_sizes: stages the rows, returns per-column
+        (element counts, value bytes)."""
         import numpy as np
-        from .columns import HostColumn, NP_DTYPE, validity_bytes
-        from .types import ArrowType, preorder
-        lib = _lib.load()
+        from .types import preorder
         fields = preorder(self.plan.schema)
         counts = np.zeros(max(1, len(fields)), np.int64)
         nbytes = np.zeros(max(1, len(fields)), np.int64)
         offs = np.ascontiguousarray(offsets, dtype=np.int64)
-        _check(lib.fory_rowfmt_host_decode_var_sizes(self.handle, _np_ptr(rows), _np_ptr(offs), n, frame,
-                                                     _np_ptr(counts), _np_ptr(nbytes)))
+        _check(_lib.load().fory_rowfmt_host_decode_var_sizes(self.handle, _np_ptr(rows), _np_ptr(offs), n, frame,
+                                                             _np_ptr(counts), _np_ptr(nbytes)))
+        return counts, nbytes
+
+    def decode_var_finish(self, counts, nbytes):
+        """fory_rowfmt_host_decode_var: the staged batch into freshly sized host columns."""
+        import numpy as np
+        from .columns import HostColumn, NP_DTYPE, validity_bytes
+        from .types import ArrowType, preorder
+        fields = preorder(self.plan.schema)
         cols = []
         for i, f in enumerate(fields):
             k, t = int(counts[i]), f.type.id
@@ -222,7 +234,7 @@ class HostPipeline:
             if f.nullable:
                 c.validity = np.zeros(validity_bytes(k), np.uint8)
             cols.append(c)
-        _check(lib.fory_rowfmt_host_decode_var(self.handle, self._host_array(cols)))
+        _check(_lib.load().fory_rowfmt_host_decode_var(self.handle, self._host_array(cols)))
         return cols
 
 

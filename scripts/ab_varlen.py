@@ -26,15 +26,15 @@ arr = native.column_array(cols)
 status = torch.zeros(1, dtype=torch.int32, device=dev)
 variants = {"global": {"FORY_ROWFMT_VARTILE": "0"}, "tile": {"FORY_ROWFMT_VARFLAT": "0"}, "flat": {},
             "cap12k": {"FORY_ROWFMT_VARCAP": "12288"}, "cap24k": {"FORY_ROWFMT_VARCAP": "24576"},
-            "flat_nw8": {"FORY_ROWFMT_VARNW": "8"}, "flat_cap48k": {"FORY_ROWFMT_VARCAP": "49152"}}
+            "flat_cap48k": {"FORY_ROWFMT_VARCAP": "49152"}}
 if len(sys.argv) > 4:  # variants as JSON: {"name": {"ENV": "value", ...}, ...}
     variants = json.loads(sys.argv[4])
 res = {}
 
 
 def set_env(envs):
-    for k in ("FORY_ROWFMT_VARTILE", "FORY_ROWFMT_VARCAP", "FORY_ROWFMT_VARFLAT", "FORY_ROWFMT_VARNW",
-              "FORY_ROWFMT_VARSTG", "FORY_ROWFMT_SPILLCAP", "FORY_ROWFMT_VARPL"):
+    for k in ("FORY_ROWFMT_VARTILE", "FORY_ROWFMT_VARCAP", "FORY_ROWFMT_VARFLAT",
+              "FORY_ROWFMT_VARSTG", "FORY_ROWFMT_SPILLCAP"):
         os.environ.pop(k, None)
     os.environ.update(envs)
 

@@ -124,3 +124,41 @@ def test_host_varlen_errors():
         _check(_lib.load().fory_rowfmt_host_encode_var(hp.handle, hp._host_array(cols), n, 1, small.ctypes.data,
                                                         small.nbytes, None, ctypes.byref(total)))
     assert total.value == expect.nbytes
+
+
+def test_host_varlen_staged_decode_is_dropped_by_an_encode():
+    """A context serves one call at a time: an encode between decode_var_sizes and
+    decode_var reuses the staged device buffers, so decode_var must refuse (not
+    decode the encode's bytes or read freed memory)."""
+    from fury_amd.format import IllegalArgumentException
+    schema, make = catalog()["mixed40_nulls"]
+    n = 2000
+    cols = make(n, 9)
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    hp = HostPipeline(NativePlan(schema))
+    counts, nbytes = hp.decode_var_sizes(expect, eoffs, n, 1)
+    big = make(4 * n, 10)  # grows the context's buffers
+    hp.encode_var(big, 4 * n, 1)
+    with pytest.raises(IllegalArgumentException):
+        hp.decode_var_finish(counts, nbytes)
+    # a fresh sizes call makes it decodable again
+    counts, nbytes = hp.decode_var_sizes(expect, eoffs, n, 1)
+    assert columns_equal(schema, cols, hp.decode_var_finish(counts, nbytes)) == []
+    hp.close()
+
+
+@pytest.mark.parametrize("name", ["mixed40_nulls", "nested_nulls", "maps"])
+def test_host_varlen_decode_of_a_sub_range(name):
+    """Rows k.. of a stream whose first row starts at a non-16-byte-aligned offset: the
+    device sees the host buffer's phase, offsets rebased to the staged run."""
+    schema, make = catalog()[name]
+    n = 1500
+    cols = make(n, 4)
+    for frame in (0, 1):
+        expect, eoffs = oracle.encode(schema, cols, n, frame)
+        k = next(j for j in range(1, n) if eoffs[j] % 16 != 0)
+        hp = HostPipeline(NativePlan(schema))
+        dec = hp.decode_var(expect, eoffs[k:], n - k, frame)
+        ref = oracle.decode(schema, expect[int(eoffs[k]):], eoffs[k:] - eoffs[k], n - k, frame)
+        assert columns_equal(schema, ref, dec) == []
+        hp.close()

@@ -36,41 +36,21 @@ def encoder_for(name):
     return _ENC[name]
 
 
-@pytest.fixture(params=["8", "8p", "6", "7", "5", "9", "10", "11", "4", "3", "2", "1", "0", "d1", "d2", "d3", "d4", "d5"],
-                ids=["v5r64w512", "v5r64w512pad", "v5r128", "v5r128w1024", "v5r64", "once_r64w512", "once_r64w256",
-                     "once_r128w512", "v4", "v3r128", "v3r64", "pipe", "tile", "dec_v2r64w512", "dec_v2r128",
-                     "dec_v2r128w1024", "dec_tr32", "dec_v3"])
-def kernel_variant(request, monkeypatch):
-    """Fixed-width kernel variants. FORY_ROWFMT_PIPE: 8 (default) / 6 / 7 / 5 encode v5
-    (depth-2 pipeline; R64-WG512 / R128-WG512 / R128-WG1024 / R64-WG256), 9 / 10 / 11
-    one-shot v5 (R64-WG512 / R64-WG256 / R128-WG512), "p" suffix =
-    padded LDS pitch, 4 encode v4 (column slabs), 3/2 encode v3 (128/64 records per
-    tile), 1 persistent pipelined, 0 one tile per workgroup. "dK" = FORY_ROWFMT_DEC=K,
-    decode v2 shapes (R64-WG512, R128-WG512, R128-WG1024)."""
-    if request.param.startswith("d"):  # decode variants (encode default)
-        monkeypatch.setenv("FORY_ROWFMT_DEC", request.param[1])
-        return request.param
-    monkeypatch.setenv("FORY_ROWFMT_PIPE", request.param.rstrip("p"))
-    if request.param.endswith("p"):
-        monkeypatch.setenv("FORY_ROWFMT_PAD", "1")
-    return request.param
-
-
 VARLEN = [k for k, (sch, _) in catalog().items()
           if any(f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.STRUCT, ArrowType.MAP)
                  for f in sch.fields)]
 FIXED = [k for k in catalog() if k not in VARLEN]
 
 
-@pytest.fixture(params=["flat", "flat_nw8", "flat_stg256", "tile", "global", "spill", "nocap", "tile_nocap"])
+@pytest.fixture(params=["flat", "flat_stg256", "tile", "global", "spill", "nocap", "tile_nocap"])
 def varlen_engine(request, monkeypatch):
     """Varlen engines: flat cooperative tile kernels (default for flat plans), the
     generic one-wave tile interpreter (FORY_ROWFMT_VARFLAT=0), the per-record global
     interpreter (FORY_ROWFMT_VARTILE=0); a 2 KiB LDS image so tiles spill to the second
     (big-image) launch; 2 KiB for both launches so tiles take the per-record global path
-    inside the tile kernels (flat and generic); flat with 8 waves per tile, and with a
-    256-byte staging buffer (most spans take the per-lane copy)."""
-    env = {"flat": {}, "flat_nw8": {"FORY_ROWFMT_VARNW": "8"}, "flat_stg256": {"FORY_ROWFMT_VARSTG": "256"},
+    inside the tile kernels (flat and generic); flat with a 256-byte staging buffer
+    (most spans take the per-lane copy)."""
+    env = {"flat": {}, "flat_stg256": {"FORY_ROWFMT_VARSTG": "256"},
            "tile": {"FORY_ROWFMT_VARFLAT": "0"}, "global": {"FORY_ROWFMT_VARTILE": "0"},
            "spill": {"FORY_ROWFMT_VARCAP": "2048"},
            "nocap": {"FORY_ROWFMT_VARCAP": "2048", "FORY_ROWFMT_SPILLCAP": "2048"},
@@ -107,7 +87,7 @@ def check_parity(name, n, frame):
 @pytest.mark.parametrize("frame", [0, 1])
 @pytest.mark.parametrize("n", SIZES)
 @pytest.mark.parametrize("name", FIXED)
-def test_encode_decode_parity(name, n, frame, kernel_variant):
+def test_encode_decode_parity(name, n, frame):
     check_parity(name, n, frame)
 
 
@@ -223,7 +203,7 @@ def test_capacity_errors():
         native.read_status(status)
 
 
-def test_struct_large_round_trip_and_sampled_parity(kernel_variant):
+def test_struct_large_round_trip_and_sampled_parity():
     """S at 2M rows: device-generated java.util.Random values, round trip exact,
     and 4 sampled tiles compared byte-for-byte with the oracle."""
     n = 2 * 1024 * 1024 + 3
