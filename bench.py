@@ -424,8 +424,16 @@ def main():
         dcols = enc.decode(out[:total], n, frame, offs)
         darr = native.column_array(dcols)
 
+        # frame streams decode from the stream alone (a receiver has no row offsets):
+        # the device frame index (fory_rowfmt_index_frames) runs inside the decode
+        ioffs, iws = offs, None
+        if frame:
+            ioffs = torch.empty(n + 1, dtype=torch.int64, device=device)
+            iws = torch.empty(max(256, native.index_workspace_bytes(plan, n, total)), dtype=torch.uint8,
+                              device=device)
+
         def step(ev=None):
-            # events: 0 | encoded_size | 3 | encode | 1 | decode_sizes | 4 | decode | 2
+            # events: 0 | encoded_size | 3 | encode | 1 | index_frames | 5 | decode_sizes | 4 | decode | 2
             if ev:
                 ev[0].record()
             native.encoded_size(plan, arr, n, frame, offs, ws, stream)
@@ -434,10 +442,14 @@ def main():
             native.encode(plan, arr, n, frame, offs, out, status, ws, stream)
             if ev:
                 ev[1].record()
-            native.decode_sizes(plan, out, offs, n, frame, darr, status, ws, stream)
+            if frame:
+                native.index_frames(plan, out, total, n, frame, ioffs, status, iws, stream)
+            if ev:
+                ev[5].record()
+            native.decode_sizes(plan, out, ioffs, n, frame, darr, status, ws, stream)
             if ev:
                 ev[4].record()
-            native.decode(plan, out, offs, n, frame, darr, status, ws, stream)
+            native.decode(plan, out, ioffs, n, frame, darr, status, ws, stream)
             if ev:
                 ev[2].record()
 
@@ -447,7 +459,7 @@ def main():
         bad = check_round_trip(plan, cols, dcols, n)
         if bad:
             raise SystemExit(f"round-trip mismatch on the benchmark batch: {bad}")
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
         barrier(dist)
         t0 = time.perf_counter()
         for k in range(args.steps):
@@ -456,7 +468,8 @@ def main():
         el = max_over_ranks(dist, time.perf_counter() - t0, args.backend)
         native.read_status(status, stream)
         enc_avg = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)  # sizes + scan + encode
-        dec_avg = sum(e[1].elapsed_time(e[2]) for e in evs) / len(evs)  # decode_sizes + decode
+        dec_avg = sum(e[1].elapsed_time(e[2]) for e in evs) / len(evs)  # [index] + decode_sizes + decode
+        idx_avg = sum(e[1].elapsed_time(e[5]) for e in evs) / len(evs)  # frame index (stream mode)
         enc_k = sum(e[3].elapsed_time(e[1]) for e in evs) / len(evs)    # encode call alone
         dec_k = sum(e[4].elapsed_time(e[2]) for e in evs) / len(evs)    # decode call alone
         algo = col_bytes + total
@@ -482,14 +495,15 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (numpy seeded)",
-            "config": {"workload": f"{config} {'frame-stream' if frame else 'raw rows'}, {total_rows} records "
-                                   f"split over {world} rank(s)",
+            "config": {"workload": f"{config} {'frame-stream (decoded from the stream alone)' if frame else 'raw rows'}, "
+                                   f"{total_rows} records split over {world} rank(s)",
                        "total_rows": total_rows, "rows_per_gpu": n, "row_bytes_total_per_gpu": total,
                        "column_bytes_per_gpu": col_bytes, "frame_mode": "stream" if frame else "raw",
                        "schema_hash": plan.schema_hash,
                        "parallelism": f"record-sharded x{world} (contiguous ranges), no collective"},
             "kernels_ms": {"encode_avg": round(enc_avg, 4), "decode_avg": round(dec_avg, 4),
-                           "encode_call_avg": round(enc_k, 4), "decode_call_avg": round(dec_k, 4)},
+                           "encode_call_avg": round(enc_k, 4), "decode_call_avg": round(dec_k, 4),
+                           "frame_index_avg": round(idx_avg, 4) if frame else None},
             "roofline": {"bound": "hbm", "kernel": dom + " (sizing passes included)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),

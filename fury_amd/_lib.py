@@ -94,6 +94,11 @@ PROTOTYPES = {
          ctypes.c_void_p],
     ),
     "fory_rowfmt_read_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "fory_rowfmt_index_workspace_bytes": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64]),
+    "fory_rowfmt_index_frames": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     "fory_rowfmt_host_ctx_create": (
         ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),
     "fory_rowfmt_host_ctx_destroy": (None, [ctypes.c_void_p]),
@@ -113,6 +118,10 @@ PROTOTYPES = {
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
          ctypes.c_void_p]),
+    "fory_rowfmt_host_decode_stream_sizes": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.POINTER(ctypes.c_int64)]),
     "fory_rowfmt_host_decode_var": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Column)]),
     "fory_rowfmt_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "fory_rowfmt_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),

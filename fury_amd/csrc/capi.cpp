@@ -686,6 +686,50 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows, const int64_t*
   return e == hipSuccess ? FORY_OK : hip_fail(e, "var_decode");
 }
 
+int64_t fory_rowfmt_index_workspace_bytes(const fory_plan* plan, int64_t num_rows, int64_t rows_bytes) {
+  if (!plan || num_rows < 0 || rows_bytes < 0) return -1;
+  return align_up(fory_amd::frame_index_words(num_rows, rows_bytes) * 8);
+}
+
+int fory_rowfmt_index_frames(const fory_plan* plan, const void* d_rows, int64_t rows_bytes, int64_t num_rows,
+                             int32_t frame_mode, int64_t* d_row_offsets, int32_t* d_status, void* d_workspace,
+                             int64_t workspace_bytes, void* stream) {
+  if (!plan) return fail(FORY_ERR_INVALID_ARGUMENT, "plan is null");
+  if (num_rows < 0 || rows_bytes < 0) return fail(FORY_ERR_INVALID_ARGUMENT, "num_rows or rows_bytes < 0");
+  if (frame_mode == FORY_FRAME_RAW)
+    return fail(FORY_ERR_INVALID_ARGUMENT, "raw rows are not self-delimiting: pass their row offsets to decode");
+  if (frame_mode != FORY_FRAME_STREAM)
+    return fail(FORY_ERR_UNSUPPORTED, "frame index: stream frames only (collection frames carry no schema hash)");
+  if (!d_row_offsets) return fail(FORY_ERR_INVALID_ARGUMENT, "d_row_offsets is null");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const Plan& p = plan->p;
+  hipError_t e;
+  if (p.fixed_width) {  // every frame is fixed_size + 12 bytes; decode checks each size and hash
+    const int64_t stride = p.fixed_size + 12;
+    if (num_rows * stride > rows_bytes)
+      return fail(FORY_ERR_CORRUPT, "stream holds " + std::to_string(rows_bytes) + " bytes < " +
+                                        std::to_string(num_rows) + " frames x " + std::to_string(stride));
+    e = fory_amd::launch_fill_offsets(d_row_offsets, num_rows, stride, s);
+    return e == hipSuccess ? FORY_OK : hip_fail(e, "fill_offsets");
+  }
+  if (num_rows > 0 && !d_rows) return fail(FORY_ERR_INVALID_ARGUMENT, "d_rows is null");
+  if (reinterpret_cast<uintptr_t>(d_rows) & 3)
+    return fail(FORY_ERR_INVALID_ARGUMENT, "d_rows must be 4-byte aligned (frame starts are 4-byte aligned)");
+  const int64_t need = fory_rowfmt_index_workspace_bytes(plan, num_rows, rows_bytes);
+  if (num_rows > 0 && (!d_workspace || workspace_bytes < need))
+    return fail(FORY_ERR_INVALID_ARGUMENT, "index workspace too small: need " + std::to_string(need) + " bytes");
+  if (num_rows > 0 && rows_bytes < 12 + 8 + p.fixed_size)
+    return fail(FORY_ERR_CORRUPT, "stream shorter than one frame");
+  fory_amd::FrameIndexLaunch L{};
+  L.rows_bytes = rows_bytes;
+  L.num_rows = num_rows;
+  L.schema_hash = p.schema_hash;
+  L.fixed_size = p.fixed_size;
+  e = fory_amd::launch_frame_index(L, static_cast<const uint8_t*>(d_rows), d_row_offsets,
+                                   static_cast<int64_t*>(d_workspace), d_status, s);
+  return e == hipSuccess ? FORY_OK : hip_fail(e, "index_frames");
+}
+
 int fory_rowfmt_read_status(const int32_t* d_status, void* stream) {
   if (!d_status) return FORY_OK;
   int32_t h = 0;

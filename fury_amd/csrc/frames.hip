@@ -1,0 +1,227 @@
+// frames.hip — frame index of a self-delimiting STREAM batch on the device.
+//
+// A receiver on an RPC socket has only the frame stream that N calls of
+// Encoder.encode(MemoryBuffer, T) wrote: [i32 size][i64 schemaHash][row] back
+// to back, size = 8 + rowSize (Encoders.java:213-225). Encoder.decode(MemoryBuffer)
+// walks it frame by frame — readInt32, readInt64 (hash check), row.pointTo,
+// increaseReaderIndex(size - 8) (Encoders.java:176-193). That walk is serial;
+// here it is split over chunks of the stream and stitched:
+//
+//  1. spec  (one lane per chunk): the first plausible frame start in the chunk
+//     (4-byte aligned position whose next 8 bytes equal the schema hash and whose
+//     size is sane) — chunk 0 starts at 0 — then the walk of sizes from it to the
+//     first frame start at or past the chunk's end: (start, exit, frames).
+//  2. check (one lane per chunk): chunk k is consistent when its start equals the
+//     exit of chunk k-1 (then, by induction from chunk 0, its walk IS the true
+//     chain); any inconsistency, or a chunk with no candidate, sets a flag.
+//  3. fixup (one workgroup, only when flagged): Gauss-Seidel over contiguous
+//     blocks of chunks — each chunk re-walks from its predecessor's exit — until
+//     no exit changes. Payload bytes that mimic a frame header (hash + plausible
+//     size) can mislead step 1 but not this step.
+//  4. scan of the per-chunk frame counts -> frame index of each chunk's first frame.
+//  5. write (one lane per chunk): re-walk, row_offsets[f] = frame start,
+//     row_offsets[N] = end of frame N-1; a size out of range or fewer than N
+//     frames in rows_bytes -> FORY_ERR_CORRUPT (frames past N are never read).
+// Schema hashes are checked by the decode kernels that follow (per frame), as in
+// Encoders.decode; the walk itself follows sizes only.
+#include "kcommon.h"
+
+namespace fory_amd {
+
+namespace {
+
+constexpr int64_t kNone = -1;    // chunk holds no candidate frame start
+constexpr int64_t kBroken = -2;  // the chain hit a size out of range
+
+// Frame header at p (4-byte aligned offset into the stream): size field and hash.
+__device__ __forceinline__ uint32_t frame_size(const uint8_t* rows, int64_t p) {
+  return *gp(reinterpret_cast<const uint32_t*>(rows + p));
+}
+
+// A size field that can start a frame of this plan: >= 8 + fixed_size, a multiple
+// of 8 (rows are 8-byte padded) and the frame inside the stream.
+__device__ __forceinline__ bool sane_size(uint32_t size, int64_t p, const FrameIndexLaunch& L) {
+  return size >= (uint32_t)(8 + L.fixed_size) && (size & 7) == 0 && p + 4 + (int64_t)size <= L.rows_bytes;
+}
+
+// Walks sizes from p while p < end; returns the first position >= end (or
+// kBroken) and the number of frames started before end.
+__device__ __forceinline__ int64_t walk(const uint8_t* rows, int64_t p, int64_t end, const FrameIndexLaunch& L,
+                                        int64_t* frames) {
+  int64_t f = 0;
+  while (p < end) {
+    const uint32_t size = frame_size(rows, p);
+    if (!sane_size(size, p, L)) {
+      *frames = f;
+      return kBroken;
+    }
+    ++f;
+    p += 4 + (int64_t)size;
+  }
+  *frames = f;
+  return p;
+}
+
+__global__ __launch_bounds__(kWG) void frame_spec_kernel(FrameIndexLaunch L, const uint8_t* __restrict__ rows,
+                                                         int64_t* __restrict__ start, int64_t* __restrict__ exit_,
+                                                         int64_t* __restrict__ count) {
+  const int64_t k = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (k >= L.chunks) return;
+  const int64_t base = k * L.chunk, end = min(base + L.chunk, L.rows_bytes);
+  const uint32_t hlo = (uint32_t)(uint64_t)L.schema_hash, hhi = (uint32_t)((uint64_t)L.schema_hash >> 32);
+  int64_t s = kNone;
+  if (k == 0) {
+    s = 0;
+  } else {
+    // 8 positions per step from 10 dwords (the last two carried into the next step)
+    uint32_t d[10];
+    const int64_t lim = L.rows_bytes - 12;  // a candidate needs its 12 header bytes
+    auto ld = [&](int64_t q) -> uint32_t { return q + 4 <= L.rows_bytes ? frame_size(rows, q) : 0u; };
+    d[0] = ld(base);
+    d[1] = ld(base + 4);
+    for (int64_t p = base; p < end && p <= lim && s == kNone; p += 32) {
+#pragma unroll
+      for (int j = 2; j < 10; ++j) d[j] = ld(p + 4 * j);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t q = p + 4 * j;
+        if (s == kNone && q < end && q <= lim && d[j + 1] == hlo && d[j + 2] == hhi && sane_size(d[j], q, L)) s = q;
+      }
+      d[0] = d[8];
+      d[1] = d[9];
+    }
+  }
+  int64_t frames = 0, ex = kNone;
+  if (s != kNone) ex = walk(rows, s, end, L, &frames);
+  start[k] = s;
+  exit_[k] = ex;
+  count[k] = frames;
+}
+
+// Chunk k's walk is the true chain iff its start is its predecessor's exit.
+__global__ __launch_bounds__(kWG) void frame_check_kernel(FrameIndexLaunch L, const int64_t* __restrict__ start,
+                                                          const int64_t* __restrict__ exit_, int64_t* flag) {
+  const int64_t k = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (k >= L.chunks) return;
+  bool ok;
+  if (k == 0) ok = true;
+  else if (exit_[k - 1] == kBroken) ok = true;  // the chain ended before this chunk: nothing here counts
+  else ok = start[k] != kNone && start[k] == exit_[k - 1];
+  if (k > 0 && start[k - 1] == kNone) ok = false;  // a chunk without a candidate passes its entry through
+  if (!ok) atomicOr(reinterpret_cast<unsigned long long*>(flag), 1ull);
+}
+
+// One workgroup: chunk k's entry is chunk k-1's exit; a chunk whose start differs
+// re-walks from its entry. Thread t owns chunks [t*B, (t+1)*B) and sweeps them in
+// order (its own updates propagate at once); sweeps repeat until no exit changes,
+// so after sweep i at least the blocks 0..i-1 hold the true chain.
+__global__ __launch_bounds__(1024) void frame_fixup_kernel(FrameIndexLaunch L, const uint8_t* __restrict__ rows,
+                                                           int64_t* start, int64_t* exit_, int64_t* count,
+                                                           const int64_t* flag) {
+  if (*flag == 0) return;
+  __shared__ int changed;
+  const int64_t B = (L.chunks + 1023) / 1024;
+  const int64_t k0 = (int64_t)threadIdx.x * B, k1 = min(k0 + B, L.chunks);
+  for (int64_t sweep = 0; sweep <= 1025; ++sweep) {
+    if (threadIdx.x == 0) changed = 0;
+    __syncthreads();
+    bool mine = false;
+    for (int64_t k = k0; k < k1; ++k) {
+      const int64_t entry = k == 0 ? 0 : __hip_atomic_load(&exit_[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int64_t base = k * L.chunk, end = min(base + L.chunk, L.rows_bytes);
+      int64_t s, ex, frames = 0;
+      if (entry == kBroken || entry == kNone) {
+        s = kNone;
+        ex = kBroken;
+      } else if (entry >= end) {  // a frame spans the whole chunk
+        s = kNone;
+        ex = entry;
+      } else {
+        s = entry;
+        if (s == start[k] && __hip_atomic_load(&exit_[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kNone)
+          continue;  // already walked from here
+        ex = walk(rows, s, end, L, &frames);
+      }
+      if (s != start[k] || ex != __hip_atomic_load(&exit_[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+          frames != count[k]) {
+        start[k] = s;
+        count[k] = frames;
+        __hip_atomic_store(&exit_[k], ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mine = true;
+      }
+    }
+    __threadfence();
+    if (mine) changed = 1;
+    __syncthreads();
+    if (!changed) break;
+    __syncthreads();
+  }
+}
+
+// Chunk k's frames get indices base[k] .. base[k] + count[k] - 1 (count scanned in place).
+__global__ __launch_bounds__(kWG) void frame_write_kernel(FrameIndexLaunch L, const uint8_t* __restrict__ rows,
+                                                          const int64_t* __restrict__ start,
+                                                          const int64_t* __restrict__ base,
+                                                          int64_t* __restrict__ offs, int32_t* status) {
+  const int64_t k = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (k == 0 && base[L.chunks] < L.num_rows) set_status(status, FORY_ERR_CORRUPT);  // fewer than N frames
+  if (k >= L.chunks) return;
+  int64_t p = start[k], f = base[k];
+  if (p < 0 || f >= L.num_rows) return;
+  const int64_t end = min((k + 1) * L.chunk, L.rows_bytes);
+  while (p < end && f < L.num_rows) {
+    const uint32_t size = frame_size(rows, p);
+    if (!sane_size(size, p, L)) {  // Encoders.decode would read past the frame: corrupt stream
+      set_status(status, FORY_ERR_CORRUPT);
+      return;
+    }
+    offs[f] = p;
+    p += 4 + (int64_t)size;
+    if (f == L.num_rows - 1) offs[L.num_rows] = p;
+    ++f;
+  }
+}
+
+}  // namespace
+
+void frame_index_plan(int64_t num_rows, int64_t rows_bytes, int64_t* chunk, int64_t* chunks) {
+  // ~16 frames per chunk at the batch's mean frame size, in [1, 64] KiB
+  const int64_t n = num_rows > 0 ? num_rows : 1;
+  int64_t c = (16 * (rows_bytes / n) + 255) / 256 * 256;
+  c = c < 1024 ? 1024 : (c > 65536 ? 65536 : c);
+  *chunk = c;
+  *chunks = rows_bytes > 0 ? (rows_bytes + c - 1) / c : 0;
+}
+
+int64_t frame_index_words(int64_t num_rows, int64_t rows_bytes) {
+  int64_t c, k;
+  frame_index_plan(num_rows, rows_bytes, &c, &k);
+  return 3 * k + 2 + 2 + scan_partials(k);  // start, exit, count (+ total), flag, scan partials
+}
+
+hipError_t launch_frame_index(const FrameIndexLaunch& L0, const uint8_t* rows, int64_t* offs, int64_t* ws,
+                              int32_t* status, hipStream_t s) {
+  FrameIndexLaunch L = L0;
+  frame_index_plan(L.num_rows, L.rows_bytes, &L.chunk, &L.chunks);
+  if (L.num_rows <= 0) {
+    (void)hipMemsetAsync(offs, 0, sizeof(int64_t), s);
+    return hipGetLastError();
+  }
+  const int64_t K = L.chunks;
+  int64_t* start = ws;
+  int64_t* exit_ = start + K;
+  int64_t* count = exit_ + K;  // K + 1 (scan total)
+  int64_t* flag = count + K + 1;
+  int64_t* partials = flag + 2;
+  (void)hipMemsetAsync(flag, 0, sizeof(int64_t), s);
+  const unsigned blocks = (unsigned)((K + kWG - 1) / kWG);
+  hipLaunchKernelGGL(frame_spec_kernel, dim3(blocks), dim3(kWG), 0, s, L, rows, start, exit_, count);
+  hipLaunchKernelGGL(frame_check_kernel, dim3(blocks), dim3(kWG), 0, s, L, start, exit_, flag);
+  hipLaunchKernelGGL(frame_fixup_kernel, dim3(1), dim3(1024), 0, s, L, rows, start, exit_, count, flag);
+  hipError_t e = launch_scan_i64(count, K, partials, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(frame_write_kernel, dim3(blocks), dim3(kWG), 0, s, L, rows, start, count, offs, status);
+  return hipGetLastError();
+}
+
+}  // namespace fory_amd

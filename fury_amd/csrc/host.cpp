@@ -60,7 +60,6 @@ struct fory_host_ctx {
   // decode state between host_decode_var_sizes and host_decode_var
   int64_t dec_n = -1;
   int32_t dec_frame = 0;
-  int64_t dec_r0 = 0;
   std::vector<int64_t> dec_count, dec_bytes;
   std::vector<fory_column> dec_cols;
   int64_t* dec_offs = nullptr;
@@ -496,29 +495,58 @@ int fory_rowfmt_host_encode_var(fory_host_ctx* c, const fory_column* host_cols, 
   return rc;
 }
 
-int fory_rowfmt_host_decode_var_sizes(fory_host_ctx* c, const void* host_rows, const int64_t* host_row_offsets,
-                                      int64_t n, int32_t frame, int64_t* host_counts, int64_t* host_bytes) {
-  if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
-  if (!c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "fixed-width plan: use fory_rowfmt_host_decode");
-  if (n < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
-  if (!host_row_offsets || !host_counts || !host_bytes || (n > 0 && !host_rows))
-    return fail_host(FORY_ERR_INVALID_ARGUMENT, "host rows, row offsets or size outputs null");
+}  // extern "C"
+
+namespace {
+
+// Stages a decode batch on the device: rows (host_row_offsets given: the run
+// [offs[0], offs[n]) with offsets rebased to it; else the first rows_bytes bytes of
+// a frame stream, indexed on the device by fory_rowfmt_index_frames) and sizes
+// every output column (fory_rowfmt_decode_sizes, repeated while list/map element
+// counts become known). The staged state serves the next host_decode_var.
+int decode_var_stage(fory_host_ctx* c, const void* host_rows, const int64_t* host_row_offsets, int64_t rows_bytes,
+                     int64_t n, int32_t frame, int64_t* host_counts, int64_t* host_bytes, int64_t* consumed) {
   const int N = c->info.num_columns;
   c->dec_n = -1;
-  const int64_t r0 = host_row_offsets[0], r1 = host_row_offsets[n];
-  if (r1 < r0 || r0 < 0) return fail_host(FORY_ERR_CORRUPT, "row offsets decrease");
+  int64_t r0 = 0, r1 = rows_bytes;
+  if (host_row_offsets) {
+    r0 = host_row_offsets[0];
+    r1 = host_row_offsets[n];
+    if (r1 < r0 || r0 < 0) return fail_host(FORY_ERR_CORRUPT, "row offsets decrease");
+  }
   int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
-  // rows at their 16-byte phase, so the device sees the host buffer's alignment
-  rc = ensure(c, &c->drows, &c->drows_bytes, (r1 - r0) + 32);
+  // device run: [rows (16-byte aligned start)][row offsets n+1][index status][index workspace]
+  const int64_t rows_sz = align_up((r1 - r0) + 16), offs_sz = align_up((n + 1) * 8);
+  const int64_t iws = host_row_offsets ? 0 : fory_rowfmt_index_workspace_bytes(c->plan, n, r1 - r0);
+  rc = ensure(c, &c->drows, &c->drows_bytes, rows_sz + offs_sz + kAlign + iws);
   if (rc) return rc;
-  uint8_t* drow0 = c->drows + (r0 & 15);
+  uint8_t* drow0 = c->drows;
+  int64_t* d_offs = reinterpret_cast<int64_t*>(c->drows + rows_sz);
+  int32_t* istatus = reinterpret_cast<int32_t*>(c->drows + rows_sz + offs_sz);
   if (r1 > r0)
     rc = hip_check(hipMemcpyAsync(drow0, static_cast<const uint8_t*>(host_rows) + r0, (size_t)(r1 - r0),
                                   hipMemcpyHostToDevice, c->s_k), "H2D rows");
-  // row offsets relative to the staged run (its first byte at drow0)
-  std::vector<int64_t> rel_offs((size_t)n + 1);
-  for (int64_t k = 0; k <= n; ++k) rel_offs[(size_t)k] = host_row_offsets[k] - r0;
+  if (host_row_offsets) {  // row offsets relative to the staged run
+    std::vector<int64_t> rel_offs((size_t)n + 1);
+    for (int64_t k = 0; k <= n; ++k) rel_offs[(size_t)k] = host_row_offsets[k] - r0;
+    if (!rc)
+      rc = hip_check(hipMemcpyAsync(d_offs, rel_offs.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->s_k),
+                     "H2D row offsets");
+    if (!rc) rc = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize");  // rel_offs is pageable
+    if (consumed) *consumed = r1;
+  } else {  // Encoder.decode(MemoryBuffer) x n over the stream alone
+    if (!rc) rc = hip_check(hipMemsetAsync(istatus, 0, 4, c->s_k), "hipMemsetAsync");
+    if (!rc)
+      rc = fory_rowfmt_index_frames(c->plan, drow0, r1 - r0, n, frame, d_offs, istatus,
+                                    c->drows + rows_sz + offs_sz + kAlign, iws, c->s_k);
+    int64_t end = 0;
+    if (!rc) rc = hip_check(hipMemcpyAsync(&end, d_offs + n, 8, hipMemcpyDeviceToHost, c->s_k), "D2H frame end");
+    if (!rc) rc = fory_rowfmt_read_status(istatus, c->s_k);  // synchronises the stream
+    if (rc) return rc;
+    if (consumed) *consumed = end;
+  }
+  if (rc) return rc;
   // element counts: top level n; struct fields as their struct; list/map elements
   // from the container totals (pass 1), string/binary elements' bytes (pass 2)
   std::vector<int64_t> cnt(N, -1), vbytes(N, 0);
@@ -535,7 +563,6 @@ int fory_rowfmt_host_decode_var_sizes(fory_host_ctx* c, const void* host_rows, c
   resolve();
   const int64_t ws_bytes = fory_rowfmt_workspace_bytes(c->plan, n);
   std::vector<fory_column> d;
-  int64_t* d_offs = nullptr;
   void* ws = nullptr;
   int32_t* status = nullptr;
   for (int pass = 0; pass < 3 && !rc; ++pass) {
@@ -547,16 +574,13 @@ int fory_rowfmt_host_decode_var_sizes(fory_host_ctx* c, const void* host_rows, c
     rc = ensure(c, &c->dbuf, &c->dbuf_bytes, carve(c, nullptr, kc, vb0, wv, n, nullptr, nullptr, nullptr, ws_bytes,
                                                    nullptr));
     if (rc) break;
-    carve(c, c->dbuf, kc, vb0, wv, n, &d, &d_offs, &ws, ws_bytes, &status);
+    carve(c, c->dbuf, kc, vb0, wv, n, &d, nullptr, &ws, ws_bytes, &status);
     for (int i = 0; i < N; ++i) {
       d[i].values = nullptr;
       d[i].capacity = 0;
       if (kc[i] < 0) d[i] = fory_column{};
     }
-    // the row offsets' place moves with the layout: copy them for every pass
-    rc = hip_check(hipMemcpyAsync(d_offs, rel_offs.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->s_k),
-                   "H2D row offsets");
-    if (!rc) rc = hip_check(hipMemsetAsync(status, 0, 4, c->s_k), "hipMemsetAsync");
+    rc = hip_check(hipMemsetAsync(status, 0, 4, c->s_k), "hipMemsetAsync");
     if (!rc)
       rc = fory_rowfmt_decode_sizes(c->plan, drow0, d_offs, n, frame, d.data(), status, ws, ws_bytes, c->s_k);
     std::vector<int32_t> tot(N, 0);
@@ -585,14 +609,38 @@ int fory_rowfmt_host_decode_var_sizes(fory_host_ctx* c, const void* host_rows, c
   }
   c->dec_n = n;
   c->dec_frame = frame;
-  c->dec_r0 = r0;
   c->dec_count = cnt;
   c->dec_bytes = vbytes;
   c->dec_cols = d;  // the last pass's device offsets (tile bases / totals for decode)
-  c->dec_offs = d_offs;
+  c->dec_offs = d_offs;  // in the drows run
   c->dec_ws = ws;
   c->dec_status = status;
   return FORY_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fory_rowfmt_host_decode_var_sizes(fory_host_ctx* c, const void* host_rows, const int64_t* host_row_offsets,
+                                      int64_t n, int32_t frame, int64_t* host_counts, int64_t* host_bytes) {
+  if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+  if (!c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "fixed-width plan: use fory_rowfmt_host_decode");
+  if (n < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
+  if (!host_row_offsets || !host_counts || !host_bytes || (n > 0 && !host_rows))
+    return fail_host(FORY_ERR_INVALID_ARGUMENT, "host rows, row offsets or size outputs null");
+  return decode_var_stage(c, host_rows, host_row_offsets, 0, n, frame, host_counts, host_bytes, nullptr);
+}
+
+int fory_rowfmt_host_decode_stream_sizes(fory_host_ctx* c, const void* host_rows, int64_t rows_bytes, int64_t n,
+                                         int64_t* host_counts, int64_t* host_bytes, int64_t* consumed_bytes) {
+  if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+  if (!c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "fixed-width plan: use fory_rowfmt_host_decode");
+  if (n < 0 || rows_bytes < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "num_rows or rows_bytes < 0");
+  if (!host_counts || !host_bytes || (n > 0 && !host_rows))
+    return fail_host(FORY_ERR_INVALID_ARGUMENT, "host rows or size outputs null");
+  return decode_var_stage(c, host_rows, nullptr, rows_bytes, n, FORY_FRAME_STREAM, host_counts, host_bytes,
+                          consumed_bytes);
 }
 
 int fory_rowfmt_host_decode_var(fory_host_ctx* c, const fory_column* host_out_cols) {
@@ -640,9 +688,8 @@ int fory_rowfmt_host_decode_var(fory_host_ctx* c, const fory_column* host_out_co
                      "hipMemsetAsync");
   }
   if (!rc) rc = hip_check(hipMemsetAsync(status, 0, 4, c->s_k), "hipMemsetAsync");
-  uint8_t* drow0 = c->drows + (c->dec_r0 & 15);
   if (!rc)
-    rc = fory_rowfmt_decode(c->plan, drow0, d_offs, n, c->dec_frame, d.data(), status, ws, ws_bytes, c->s_k);
+    rc = fory_rowfmt_decode(c->plan, c->drows, d_offs, n, c->dec_frame, d.data(), status, ws, ws_bytes, c->s_k);
   for (int i = 0; i < N && !rc; ++i) {  // D2H of every column
     const fory_column& h = host_out_cols[i];
     if (d[i].values && c->dec_bytes[i] > 0)

@@ -109,4 +109,20 @@ hipError_t launch_scan_offsets_i32(int32_t* offs, int64_t n, int64_t* partials,
 hipError_t launch_scan_offsets_i32_segmented(int32_t* offs, int64_t n, int64_t* partials, int64_t partial_words,
                                              int32_t* status, hipStream_t s);
 
+// Frame index of a STREAM batch (frames.hip): the starts of the first num_rows
+// frames of rows_bytes bytes, found on the device from the stream alone.
+struct FrameIndexLaunch {
+  int64_t rows_bytes;
+  int64_t num_rows;
+  int64_t schema_hash;
+  int32_t fixed_size;
+  int32_t pad;
+  int64_t chunk;   // bytes per chunk (frame_index_plan)
+  int64_t chunks;
+};
+void frame_index_plan(int64_t num_rows, int64_t rows_bytes, int64_t* chunk, int64_t* chunks);
+int64_t frame_index_words(int64_t num_rows, int64_t rows_bytes);  // int64 workspace words
+hipError_t launch_frame_index(const FrameIndexLaunch& L, const uint8_t* rows, int64_t* d_row_offsets, int64_t* ws,
+                              int32_t* status, hipStream_t s);
+
 }  // namespace fory_amd

@@ -156,7 +156,9 @@ class RowEncoder:
             if f.nullable:
                 cols[i].validity = torch.zeros(_validity_bytes(n), dtype=torch.uint8, device=self.device)
         if offsets is None:
-            raise ValueError("varlen schema: row offsets are required to decode")
+            if frame_mode != FRAME_STREAM:
+                raise ValueError("raw rows / collection frames are not self-delimiting: row offsets are required")
+            offsets = self.index_frames(buf, n)
         native.decode_sizes(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
         var_idx = [i for i, f in enumerate(fields) if i not in item_of and
                    f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP)]
@@ -193,6 +195,20 @@ class RowEncoder:
         native.decode(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
         native.read_status(status)
         return cols
+
+    def index_frames(self, buf, num_rows: int):
+        """Frame starts of the first num_rows frames of a STREAM buffer, found on the device
+        (Encoder.decode(MemoryBuffer) x N walks [i32 size][i64 hash] frames, Encoders.java:176-193).
+        Returns the int64 offsets tensor [n+1]; offsets[n] = bytes consumed."""
+        import torch
+        p = self.plan
+        offs = torch.empty(num_rows + 1, dtype=torch.int64, device=self.device)
+        need = max(256, native.index_workspace_bytes(p, num_rows, buf.numel()))
+        iws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        native.index_frames(p, buf, buf.numel(), num_rows, FRAME_STREAM, offs, status, iws)
+        native.read_status(status)
+        return offs
 
     def from_rows(self, rows: EncodedRows) -> List[DeviceColumn]:
         return self.decode(rows)

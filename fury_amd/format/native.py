@@ -120,6 +120,18 @@ def decode(plan: NativePlan, rows, d_offsets, n: int, frame: int, cols_arr, stat
                                   _ptr(status), _ptr(ws), ws.numel(), s))
 
 
+def index_workspace_bytes(plan: NativePlan, n: int, rows_bytes: int) -> int:
+    return int(_lib.load().fory_rowfmt_index_workspace_bytes(plan.handle, n, rows_bytes))
+
+
+def index_frames(plan: NativePlan, rows, rows_bytes: int, n: int, frame: int, d_offsets, status, ws, stream=None):
+    """fory_rowfmt_index_frames: frame starts of a STREAM batch from the stream alone."""
+    lib = _lib.load()
+    s = stream if stream is not None else _stream_handle()
+    _check(lib.fory_rowfmt_index_frames(plan.handle, _ptr(rows), rows_bytes, n, frame, _ptr(d_offsets),
+                                        _ptr(status), _ptr(ws), 0 if ws is None else ws.numel(), s))
+
+
 def read_status(status, stream=None):
     lib = _lib.load()
     s = stream if stream is not None else _stream_handle()
@@ -214,6 +226,20 @@ class HostPipeline:
         _check(_lib.load().fory_rowfmt_host_decode_var_sizes(self.handle, _np_ptr(rows), _np_ptr(offs), n, frame,
                                                              _np_ptr(counts), _np_ptr(nbytes)))
         return counts, nbytes
+
+    def decode_stream(self, rows, n: int):
+        """N x Encoder.decode(MemoryBuffer) over host frames alone (no row offsets):
+        returns (columns, bytes consumed)."""
+        import numpy as np
+        from .types import preorder
+        fields = preorder(self.plan.schema)
+        counts = np.zeros(max(1, len(fields)), np.int64)
+        nbytes = np.zeros(max(1, len(fields)), np.int64)
+        used = ctypes.c_int64(0)
+        _check(_lib.load().fory_rowfmt_host_decode_stream_sizes(self.handle, _np_ptr(rows), rows.nbytes, n,
+                                                                _np_ptr(counts), _np_ptr(nbytes),
+                                                                ctypes.byref(used)))
+        return self.decode_var_finish(counts, nbytes), used.value
 
     def decode_var_finish(self, counts, nbytes):
         """fory_rowfmt_host_decode_var: the staged batch into freshly sized host columns."""

@@ -227,6 +227,24 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows,
                        int32_t* d_status, void* d_workspace,
                        int64_t workspace_bytes, void* stream);
 
+/* --- frame index: the stream alone -> row offsets, on the device.
+ * Encoder.decode(MemoryBuffer) reads [i32 size][i64 hash], checks the hash and
+ * advances by the frame (Encoders.java:176-193): the frames delimit themselves.
+ * A receiver that has only the stream (e.g. from an RPC socket) calls this
+ * before fory_rowfmt_decode_sizes / fory_rowfmt_decode: it writes the starts of
+ * the first num_rows frames of d_rows (rows_bytes bytes, 4-byte aligned) to
+ * d_row_offsets[0..num_rows-1] and the end of frame num_rows-1 (= the bytes the
+ * N decodes consume) to d_row_offsets[num_rows]. FORY_FRAME_STREAM only (RAW
+ * rows are not self-delimiting; collection frames carry no schema hash to
+ * resynchronise on: FORY_ERR_UNSUPPORTED). A size field out of range, or fewer
+ * than num_rows frames in rows_bytes, sets *d_status = FORY_ERR_CORRUPT; schema
+ * hashes are checked by the decode that follows. Bytes past the last frame are
+ * never required to be frames. Workspace: fory_rowfmt_index_workspace_bytes. */
+int64_t fory_rowfmt_index_workspace_bytes(const fory_plan* plan, int64_t num_rows, int64_t rows_bytes);
+int fory_rowfmt_index_frames(const fory_plan* plan, const void* d_rows, int64_t rows_bytes, int64_t num_rows,
+                             int32_t frame_mode, int64_t* d_row_offsets, int32_t* d_status, void* d_workspace,
+                             int64_t workspace_bytes, void* stream);
+
 /* Synchronises `stream` and returns the status word written by decode
  * (FORY_OK if none). Sets last_error with the reference's message shape. */
 int fory_rowfmt_read_status(const int32_t* d_status, void* stream);
@@ -284,6 +302,16 @@ int fory_rowfmt_host_encode_var(fory_host_ctx* ctx, const fory_column* host_cols
 int fory_rowfmt_host_decode_var_sizes(fory_host_ctx* ctx, const void* host_rows,
                                       const int64_t* host_row_offsets, int64_t num_rows,
                                       int32_t frame_mode, int64_t* host_counts, int64_t* host_bytes);
+/* The same staging for a receiver that has only the frame stream (STREAM mode):
+ * the first num_rows frames of host_rows (rows_bytes bytes) are found on the
+ * device (fory_rowfmt_index_frames), *consumed_bytes receives the bytes those
+ * frames span (Encoder.decode's reader index after num_rows calls), then
+ * host_decode_var decodes them. */
+int fory_rowfmt_host_decode_stream_sizes(fory_host_ctx* ctx, const void* host_rows, int64_t rows_bytes,
+                                         int64_t num_rows, int64_t* host_counts, int64_t* host_bytes,
+                                         int64_t* consumed_bytes);
+/* Any host_encode_var on the context between the sizes call and this one drops
+ * the staged batch (FORY_ERR_INVALID_ARGUMENT: stage it again). */
 int fory_rowfmt_host_decode_var(fory_host_ctx* ctx, const fory_column* host_out_cols);
 int fory_rowfmt_host_register(void* host_ptr, int64_t bytes);
 int fory_rowfmt_host_unregister(void* host_ptr);

@@ -129,3 +129,25 @@ def test_host_path_validation_without_gpu():
         _lib.FORY_ERR_INVALID_ARGUMENT
     assert lib.fory_rowfmt_host_decode_var_sizes(None, None, None, 1, 0, None, None) == _lib.FORY_ERR_INVALID_ARGUMENT
     assert lib.fory_rowfmt_host_decode_var(None, cols) == _lib.FORY_ERR_INVALID_ARGUMENT
+    used = ctypes.c_int64(0)
+    assert lib.fory_rowfmt_host_decode_stream_sizes(None, None, 0, 1, None, None, ctypes.byref(used)) == \
+        _lib.FORY_ERR_INVALID_ARGUMENT
+
+
+def test_frame_index_validation_without_gpu():
+    """fory_rowfmt_index_frames: RAW rows are not self-delimiting, collection frames carry
+    no schema hash; a fixed-width stream too short for N frames is corrupt — all
+    decided before any device work."""
+    lib = _lib.load()
+    p = NativePlan(W.struct_schema())
+    assert lib.fory_rowfmt_index_frames(p.handle, None, 0, 1, 0, None, None, None, 0, None) == \
+        _lib.FORY_ERR_INVALID_ARGUMENT
+    assert lib.fory_rowfmt_index_frames(p.handle, None, 0, 1, 2, None, None, None, 0, None) == \
+        _lib.FORY_ERR_UNSUPPORTED
+    assert lib.fory_rowfmt_index_frames(p.handle, None, 860 * 3 - 1, 3, 1, ctypes.c_void_p(64), None, None, 0,
+                                        None) == _lib.FORY_ERR_CORRUPT
+    m = NativePlan(W.mixed_schema())
+    assert lib.fory_rowfmt_index_frames(m.handle, ctypes.c_void_p(18), 10000, 3, 1, ctypes.c_void_p(64), None,
+                                        None, 0, None) == _lib.FORY_ERR_INVALID_ARGUMENT  # misaligned rows
+    need = lib.fory_rowfmt_index_workspace_bytes(m.handle, 1 << 24, 8 << 30)
+    assert 0 < need < (1 << 24) * 8  # a few bytes per record

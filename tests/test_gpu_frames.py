@@ -1,0 +1,181 @@
+"""GPU: self-delimiting STREAM decode — the frame stream alone, no row offsets.
+
+Encoder.decode(MemoryBuffer) reads [i32 size][i64 schemaHash] and advances past
+the frame (Encoders.java:176-193); a receiver on an RPC socket has only those
+bytes. fory_rowfmt_index_frames finds the frame starts on the device; decode then
+runs as usual. Parity: the offsets equal the oracle encoder's, the columns equal
+the oracle's decode, for every varlen schema and sizes across chunk boundaries;
+adversarial payloads (string bytes that repeat the frame header: the schema hash
+and plausible sizes) must not derail it; bytes after the N-th frame are ignored;
+errors follow the reference (corrupt size / too few frames, hash mismatch)."""
+import struct
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import oracle  # noqa: E402
+from fury_amd import workloads as W  # noqa: E402
+from fury_amd.format import ClassNotCompatibleException, CorruptRowException  # noqa: E402
+from fury_amd.format.columns import HostColumn, to_host  # noqa: E402
+from fury_amd.format.encoder import RowEncoder  # noqa: E402
+from fury_amd.format.native import HostPipeline, NativePlan  # noqa: E402
+from fury_amd.format.types import ArrowType, DataType, Field, Schema  # noqa: E402
+
+from helpers import catalog, columns_equal  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+VARLEN = [k for k, (sch, _) in catalog().items()
+          if any(f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.STRUCT, ArrowType.MAP)
+                 for f in sch.fields)]
+_ENC = {}
+
+
+def encoder_for(name, schema=None):
+    if name not in _ENC:
+        _ENC[name] = RowEncoder(schema if schema is not None else catalog()[name][0])
+    return _ENC[name]
+
+
+def device_bytes(a, pad=0):
+    return torch.from_numpy(np.concatenate([a, np.zeros(pad, np.uint8)]) if pad else a.copy()).cuda()
+
+
+def check_stream(name, schema, cols, n, trailing=b""):
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    enc = encoder_for(name, schema)
+    stream = np.concatenate([expect, np.frombuffer(trailing, np.uint8)]) if trailing else expect
+    buf = device_bytes(stream)
+    offs = enc.index_frames(buf, n)
+    assert np.array_equal(offs.cpu().numpy(), eoffs)
+    dec = to_host(enc.decode(buf, n, 1))  # no offsets: indexed on the device
+    assert columns_equal(schema, cols, dec) == []
+    return expect, eoffs
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 1000, 4097, 20000])
+@pytest.mark.parametrize("name", VARLEN)
+def test_stream_decode_without_offsets(name, n):
+    schema, make = catalog()[name]
+    check_stream(name, schema, make(n, n + 1), n)
+
+
+def test_stream_decode_ignores_bytes_after_the_last_frame():
+    schema, make = catalog()["mixed40_nulls"]
+    n = 3000
+    cols = make(n, 2)
+    rng = np.random.default_rng(0)
+    check_stream("mixed40_nulls", schema, cols, n, trailing=bytes(rng.integers(0, 256, 5000, dtype=np.uint8)))
+    # a stream holding more than n frames: the first n are decoded
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    enc = encoder_for("mixed40_nulls")
+    offs = enc.index_frames(device_bytes(expect), n - 100)
+    assert np.array_equal(offs.cpu().numpy(), eoffs[:n - 99])
+
+
+def _adversarial_schema():
+    return Schema([Field("a", DataType(ArrowType.INT64), False), Field("s", DataType(ArrowType.STRING), True),
+                   Field("t", DataType(ArrowType.STRING), True)])
+
+
+def _adversarial_columns(n, schema_hash, fixed_size, seed, long_every=0):
+    """String payloads built of fake frame headers: [i32 plausible size][i64 the schema
+    hash], repeated — every one passes the candidate test of the frame index. Some
+    strings are 4-byte misaligned fakes; long_every > 0 adds >64 KiB strings (frames
+    spanning whole chunks)."""
+    rng = np.random.default_rng(seed)
+    a = rng.integers(-2**62, 2**62, size=n, dtype=np.int64)
+    cols = [HostColumn(a, None, None, n)]
+    for f in range(2):
+        parts, offs, valid = [], [0], []
+        for i in range(n):
+            k = int(rng.integers(0, 12))
+            fake = b"".join(struct.pack("<iq", 8 + fixed_size + 8 * int(rng.integers(0, 40)), schema_hash)
+                            for _ in range(k))
+            if rng.random() < 0.3:
+                fake = b"\x00" * int(rng.integers(1, 4)) + fake  # misaligned copy
+            if long_every and i % long_every == 7:
+                fake = fake * 1 + struct.pack("<iq", 8 + fixed_size, schema_hash) * 7000  # ~84 KiB
+            ok = rng.random() > 0.1
+            valid.append(ok)
+            if ok:
+                parts.append(fake)
+            offs.append(offs[-1] + (len(fake) if ok else 0))
+        from fury_amd.format.columns import pack_validity
+        data = np.frombuffer(b"".join(parts) + b"\0" * 8, np.uint8).copy()
+        cols.append(HostColumn(data, np.array(offs, np.int32), pack_validity(np.array(valid)), n))
+    return cols
+
+
+@pytest.mark.parametrize("n,long_every", [(50, 0), (3000, 0), (20000, 0), (400, 37)])
+def test_stream_decode_adversarial_payloads(n, long_every):
+    schema = _adversarial_schema()
+    enc = encoder_for("adversarial", schema)
+    h = enc.plan.schema_hash
+    cols = _adversarial_columns(n, h if h < 2**63 else h - 2**64, enc.plan.fixed_size, n, long_every)
+    check_stream("adversarial", schema, cols, n)
+
+
+def test_stream_decode_errors():
+    schema, make = catalog()["mixed40"]
+    n = 500
+    cols = make(n, 4)
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    enc = encoder_for("mixed40")
+    # fewer than n frames in the stream
+    with pytest.raises(CorruptRowException):
+        enc.decode(device_bytes(expect[:int(eoffs[n - 1])]), n, 1)
+    # a size field out of range (frame 200)
+    bad = expect.copy()
+    bad[int(eoffs[200]):int(eoffs[200]) + 4] = np.frombuffer(struct.pack("<i", 3), np.uint8)
+    with pytest.raises(CorruptRowException):
+        enc.decode(device_bytes(bad), n, 1)
+    # a schema hash that differs (frame 321): ClassNotCompatibleException from the decode
+    bad = expect.copy()
+    bad[int(eoffs[321]) + 7] ^= 0x10
+    with pytest.raises(ClassNotCompatibleException):
+        enc.decode(device_bytes(bad), n, 1)
+
+
+def test_stream_decode_fixed_width_plan():
+    schema, make = catalog()["struct104"]
+    n = 1000
+    cols = make(n, 3)
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    enc = encoder_for("struct104")
+    assert np.array_equal(enc.index_frames(device_bytes(expect), n).cpu().numpy(), eoffs)
+    with pytest.raises(CorruptRowException):
+        enc.index_frames(device_bytes(expect[:-1]), n)
+
+
+@pytest.mark.parametrize("name", ["mixed40_nulls", "nested_nulls", "maps", "deep_nested"])
+def test_host_stream_decode(name):
+    """fory_rowfmt_host_decode_stream_sizes + host_decode_var: host frames alone -> columns,
+    and the bytes the N decodes consume (the reader index)."""
+    schema, make = catalog()[name]
+    n = 2500
+    cols = make(n, 6)
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    hp = HostPipeline(NativePlan(schema))
+    tail = np.full(333, 0xAB, np.uint8)
+    dec, used = hp.decode_stream(np.concatenate([expect, tail]), n)
+    assert used == expect.nbytes
+    assert columns_equal(schema, cols, dec) == []
+    dec, used = hp.decode_stream(expect, n // 2)  # the first n/2 frames of the stream
+    assert used == int(eoffs[n // 2])
+    hp.close()
+
+
+def test_mixed_stream_decode_large():
+    """16M-row-scale property check at 1M rows: stream-only decode round trips and the
+    index equals the encoder's offsets."""
+    schema = W.mixed_schema()
+    n = 1 << 20
+    host = W.mixed_host_columns(n, seed=99)
+    enc = encoder_for("mixed40_big", schema)
+    from fury_amd.format.columns import to_device
+    rows = enc.encode(to_device(host), n, 1)
+    offs = enc.index_frames(rows.buffer, n)
+    assert torch.equal(offs, rows.offsets)
