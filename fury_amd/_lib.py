@@ -26,6 +26,7 @@ FORY_ERR_ENCODER = 7
 FRAME_RAW = 0
 FRAME_STREAM = 1
 FRAME_COLLECTION = 2
+FRAME_HASHED = 3  # Encoder.encode(T) -> [i64 schemaHash][row] (Encoders.java:203-210)
 
 
 class FieldDesc(ctypes.Structure):
@@ -99,6 +100,14 @@ PROTOTYPES = {
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "fory_rowfmt_split_windows": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+         ctypes.POINTER(ctypes.c_int32)]),
+    "fory_rowfmt_host_encode_windows": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.POINTER(Column), ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
     "fory_rowfmt_host_ctx_create": (
         ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),
     "fory_rowfmt_host_ctx_destroy": (None, [ctypes.c_void_p]),

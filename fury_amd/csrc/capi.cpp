@@ -46,8 +46,8 @@ constexpr int64_t kAlign = 256;
 int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
 int64_t table_bytes(const Plan& p) {
-  // fixed-width: width-ordered table + slab-ordered copy (encode v4)
-  if (p.fixed_width) return align_up(2 * (int64_t)p.top.size() * (int64_t)sizeof(FixedFieldDev));
+  // fixed-width: the width-ordered field table
+  if (p.fixed_width) return align_up((int64_t)p.top.size() * (int64_t)sizeof(FixedFieldDev));
   return align_up((int64_t)p.nodes.size() * (int64_t)sizeof(ColumnDev)) +
          align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::Op)) +
          align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::VarFieldDev)) +
@@ -64,15 +64,17 @@ int64_t num_var_ops(const Plan& p) {
 }
 
 bool use_tiled(const Plan& p, int frame) {
-  return p.fixed_width && fory_amd::fixed_tiled_supported(p.fixed_size + (frame ? 12 : 0));
+  return p.fixed_width && fory_amd::fixed_tiled_supported(p.fixed_size + fory_amd::frame_header_bytes(frame));
 }
 
 int check_common(const fory_plan* plan, const fory_column* cols, int64_t n, int frame,
                  void* ws, int64_t ws_bytes) {
   if (!plan) return fail(FORY_ERR_INVALID_ARGUMENT, "plan is null");
   if (n < 0) return fail(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
-  if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM && frame != FORY_FRAME_COLLECTION)
-    return fail(FORY_ERR_INVALID_ARGUMENT, "frame_mode must be 0 (raw), 1 (stream) or 2 (collection)");
+  if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM && frame != FORY_FRAME_COLLECTION &&
+      frame != FORY_FRAME_HASHED)
+    return fail(FORY_ERR_INVALID_ARGUMENT,
+                "frame_mode must be 0 (raw), 1 (stream), 2 (collection) or 3 (hashed)");
   if (frame == FORY_FRAME_COLLECTION) {
     const Plan& p = plan->p;
     const int k = p.top.size() == 1 ? p.nodes[p.top[0]].kind : -1;
@@ -174,7 +176,7 @@ fory_amd::FixedLaunch fixed_launch(const Plan& p, const void* table, int64_t n, 
   L.num_fields = (int32_t)p.top.size();
   L.bitmap_bytes = p.bitmap_bytes;
   L.fixed_size = p.fixed_size;
-  L.stride = p.fixed_size + (frame ? 12 : 0);
+  L.stride = p.fixed_size + fory_amd::frame_header_bytes(frame);
   L.schema_hash = p.schema_hash;
   L.num_rows = n;
   L.any_nullable = p.any_nullable ? 1 : 0;
@@ -191,44 +193,6 @@ fory_amd::FixedLaunch fixed_launch(const Plan& p, const void* table, int64_t n, 
   return L;
 }
 
-// Column slabs of encode v4 (kernels.hip): rows cut into S 16-byte-aligned
-// byte ranges of <= ~448 bytes; the field table reordered by (slab, width).
-void build_slabs(const Plan& p, const std::vector<FixedFieldDev>& tab, int frame, fory_amd::FixedLaunch* L,
-                 std::vector<FixedFieldDev>* stab) {
-  L->num_slabs = 0;
-  L->slab_fields = nullptr;
-  if (frame || p.any_nullable || (p.fixed_size & 15) || p.top.empty()) return;
-  const int chunks = p.fixed_size / 16;
-  int S = (p.fixed_size + 447) / 448;
-  if (S < 2 || S > 4) return;
-  const int cps = (chunks + S - 1) / S;
-  S = (chunks + cps - 1) / cps;
-  auto slab_of = [&](const FixedFieldDev& f) { return ((p.bitmap_bytes + 8 * f.slot) / 16) / cps; };
-  *stab = tab;
-  std::stable_sort(stab->begin(), stab->end(), [&](const FixedFieldDev& a, const FixedFieldDev& b) {
-    return slab_of(a) < slab_of(b);
-  });
-  const int widths[4] = {8, 4, 2, 1};
-  int at = 0;
-  int pitch = 0;
-  for (int sl = 0; sl < S; ++sl) {
-    fory_amd::FixedLaunch::Slab& d = L->slab[sl];
-    for (int g = 0; g < 4; ++g) {
-      d.group[g] = at;
-      for (const FixedFieldDev& f : *stab)
-        if (slab_of(f) == sl && f.width == widths[g]) ++at;
-    }
-    d.group[4] = at;
-    d.byte0 = sl * cps * 16;
-    const int c1 = std::min(chunks, (sl + 1) * cps);
-    d.nbytes = (c1 - sl * cps) * 16;
-    d.cpr_magic = 0xffffffffu / (uint32_t)(d.nbytes / 16);
-    pitch = std::max(pitch, d.nbytes);
-  }
-  L->num_slabs = S;
-  L->slab_pitch = pitch;
-}
-
 int32_t* spill_ptr(const Plan& p, void* ws, int64_t n);
 
 // LDS budget of one 64-record tile image for the varlen tile engine: 64 x an
@@ -237,7 +201,7 @@ int32_t* spill_ptr(const Plan& p, void* ws, int64_t n);
 // workgroups per CU. Bigger tiles spill to a second launch with a 96 KiB
 // image (kSpillCap); FORY_ROWFMT_VARCAP overrides.
 int var_tile_cap(const Plan& p, int frame) {
-  int64_t est = p.fixed_size + (frame ? 12 : 0);
+  int64_t est = p.fixed_size + fory_amd::frame_header_bytes(frame);
   for (size_t k = 0; k < p.nodes.size(); ++k) {
     const fory_amd::Node& nd = p.nodes[k];
     if (nd.kind == fory_amd::KIND_BYTES) est += 32;
@@ -394,7 +358,7 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
 // is missing or the batch is small.
 int64_t decode_mean_row(const Plan& p, const fory_amd::VarLaunch& L, const fory_column* cols, int64_t n, int frame) {
   if (!L.flat || n < 4096 || !cols) return 0;
-  double row = p.fixed_size + (frame ? 12 : 0);
+  double row = p.fixed_size + fory_amd::frame_header_bytes(frame);
   for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
     const fory_amd::Node& nd = p.nodes[idx];
     if (nd.kind == fory_amd::KIND_STRUCT) {
@@ -531,7 +495,7 @@ int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols, int
   const Plan& p = plan->p;
   hipError_t e;
   if (p.fixed_width) {
-    e = fory_amd::launch_fill_offsets(d_row_offsets, num_rows, p.fixed_size + (frame_mode ? 12 : 0), s);
+    e = fory_amd::launch_fill_offsets(d_row_offsets, num_rows, p.fixed_size + fory_amd::frame_header_bytes(frame_mode), s);
     return e == hipSuccess ? FORY_OK : hip_fail(e, "fill_offsets");
   }
   if (num_rows == 0) {
@@ -559,22 +523,18 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
   const Plan& p = plan->p;
   hipError_t e;
   if (use_tiled(p, frame_mode)) {
-    const int64_t stride = p.fixed_size + (frame_mode ? 12 : 0);
+    const int64_t stride = p.fixed_size + fory_amd::frame_header_bytes(frame_mode);
     if (num_rows * stride > out_capacity)
       return fail(FORY_ERR_CAPACITY, "output capacity " + std::to_string(out_capacity) + " < " +
                                          std::to_string(num_rows * stride) + " bytes");
     if (reinterpret_cast<uintptr_t>(d_out) & 15)
       return fail(FORY_ERR_INVALID_ARGUMENT, "d_out must be 16-byte aligned");
-    std::vector<FixedFieldDev> tab, stab;
+    std::vector<FixedFieldDev> tab;
     rc = bind_fixed(p, cols, num_rows, false, &tab);
     if (rc) return rc;
     fory_amd::FixedLaunch L = fixed_launch(p, d_workspace, num_rows, frame_mode);
-    build_slabs(p, tab, frame_mode, &L, &stab);
-    std::vector<FixedFieldDev> both(tab);
-    both.insert(both.end(), stab.begin(), stab.end());
-    rc = upload(d_workspace, both.data(), (int64_t)(both.size() * sizeof(FixedFieldDev)), s);
+    rc = upload(d_workspace, tab.data(), (int64_t)(tab.size() * sizeof(FixedFieldDev)), s);
     if (rc) return rc;
-    if (L.num_slabs) L.slab_fields = static_cast<const FixedFieldDev*>(d_workspace) + tab.size();
     e = fory_amd::launch_encode_fixed(L, static_cast<uint8_t*>(d_out), s);
     return e == hipSuccess ? FORY_OK : hip_fail(e, "encode_fixed");
   }
@@ -728,6 +688,35 @@ int fory_rowfmt_index_frames(const fory_plan* plan, const void* d_rows, int64_t 
   e = fory_amd::launch_frame_index(L, static_cast<const uint8_t*>(d_rows), d_row_offsets,
                                    static_cast<int64_t*>(d_workspace), d_status, s);
   return e == hipSuccess ? FORY_OK : hip_fail(e, "index_frames");
+}
+
+int fory_rowfmt_split_windows(const int64_t* row_offsets, int64_t stride, int64_t num_rows, int64_t max_window_bytes,
+                              int32_t max_windows, int64_t* first, int32_t* num_windows) {
+  if (num_rows < 0 || max_window_bytes <= 0 || max_windows <= 0 || !first || !num_windows ||
+      (!row_offsets && stride <= 0))
+    return fail(FORY_ERR_INVALID_ARGUMENT, "split_windows: bad arguments");
+  auto at = [&](int64_t i) { return row_offsets ? row_offsets[i] : i * stride; };
+  int64_t start = 0;
+  int32_t w = 0;
+  first[0] = 0;
+  while (start < num_rows) {
+    if (w == max_windows)
+      return fail(FORY_ERR_CAPACITY, "more than " + std::to_string(max_windows) + " windows needed");
+    const int64_t limit = at(start) + max_window_bytes;
+    int64_t lo = start, hi = num_rows;  // largest e with at(e) <= limit
+    while (lo < hi) {
+      const int64_t mid = hi - (hi - lo) / 2;
+      if (at(mid) <= limit) lo = mid;
+      else hi = mid - 1;
+    }
+    if (lo == start)
+      return fail(FORY_ERR_CAPACITY, "row " + std::to_string(start) + " (" + std::to_string(at(start + 1) - at(start)) +
+                                         " bytes) exceeds a window of " + std::to_string(max_window_bytes) + " bytes");
+    first[++w] = lo;
+    start = lo;
+  }
+  *num_windows = w;
+  return FORY_OK;
 }
 
 int fory_rowfmt_read_status(const int32_t* d_status, void* stream) {

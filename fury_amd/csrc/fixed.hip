@@ -52,16 +52,17 @@ __device__ __forceinline__ bool input_null(const FixedFieldDev& fd, int64_t idx)
 
 // Stores a slot into the LDS row image (BinaryRowWriter.write: slot zeroed,
 // value in the low bytes; null -> bit set, slot left zero; bool -> 0/1).
-template <bool FRAME>
+// HDR: frame header bytes before the row — 0 (raw rows), 12 (STREAM frames:
+// [i32 size][i64 hash]), 8 (HASHED frames of Encoder.encode(T): [i64 hash]).
+template <int HDR>
 __device__ __forceinline__ void put_slot(uint8_t* row, int hdr_bm, int slot, uint64_t x, bool isnull, int flags) {
-  constexpr int HDR = FRAME ? 12 : 0;
   if (flags & 2) x = x ? 1 : 0;  // MemoryBuffer.putBoolean
   if (isnull) {
     x = 0;
     atomicOr(reinterpret_cast<uint32_t*>(row + HDR + ((slot >> 5) << 2)), 1u << (slot & 31));
   }
   uint8_t* p = row + hdr_bm + 8 * slot;
-  if (FRAME) {  // frame rows start 12 bytes into the frame: slots are only 4-byte aligned
+  if (HDR == 12) {  // stream rows start 12 bytes into the frame: slots are only 4-byte aligned
     st32(p, (uint32_t)x);
     st32(p + 4, (uint32_t)(x >> 32));
   } else {
@@ -70,14 +71,16 @@ __device__ __forceinline__ void put_slot(uint8_t* row, int hdr_bm, int slot, uin
 }
 
 // Frame header [i32 8+rowSize][i64 hash] + zeroed null bitmap of this lane's row.
-template <bool FRAME>
+template <int HDR>
 __device__ __forceinline__ void put_header(uint8_t* row, const FixedLaunch& L) {
-  if (FRAME) {
+  if (HDR == 8) {  // Encoder.encode(T): [i64 hash][row] (Encoders.java:203-210)
+    st32(row, (uint32_t)(uint64_t)L.schema_hash);
+    st32(row + 4, (uint32_t)((uint64_t)L.schema_hash >> 32));
+  } else if (HDR == 12) {
     st32(row, (uint32_t)(8 + L.fixed_size));
     st32(row + 4, (uint32_t)(uint64_t)L.schema_hash);
     st32(row + 8, (uint32_t)((uint64_t)L.schema_hash >> 32));
   }
-  constexpr int HDR = FRAME ? 12 : 0;
   for (int b = 0; b < L.bitmap_bytes; b += 4) st32(row + HDR + b, 0u);
 }
 
@@ -101,7 +104,7 @@ __device__ __forceinline__ void store_tile(const uint8_t* lds, uint8_t* __restri
 }
 
 // One width group [g0, g1) of the encode: U loads in flight, then U slots.
-template <int W, int TR, bool FRAME>
+template <int W, int TR, int HDR>
 __device__ __forceinline__ void enc_group(const FixedFieldDev* __restrict__ fields, int g0, int g1, int wave, int fsub,
                                           int64_t idx, uint8_t* row, int hdr_bm) {
   constexpr int FPW = 64 / TR;
@@ -119,17 +122,16 @@ __device__ __forceinline__ void enc_group(const FixedFieldDev* __restrict__ fiel
       const int p = field_of<TR>(pb, u, FSTEP, fsub);
       if (p < g1) {
         const FixedFieldDev& fd = fields[p];
-        put_slot<FRAME>(row, hdr_bm, fd.slot, v[u], input_null(fd, idx), fd.flags);
+        put_slot<HDR>(row, hdr_bm, fd.slot, v[u], input_null(fd, idx), fd.flags);
       }
     }
   }
 }
 
-template <int TR, bool FRAME>
+template <int TR, int HDR>
 __global__ __launch_bounds__(kWG) void encode_fixed_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
                                                            uint8_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int HDR = FRAME ? 12 : 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -142,13 +144,13 @@ __global__ __launch_bounds__(kWG) void encode_fixed_kernel(FixedLaunch L, const 
   uint8_t* row = lds + r * L.stride;
   const int64_t idx = r < rows ? r0 + r : r0;
 
-  if (wave == 0 && fsub == 0) put_header<FRAME>(row, L);
+  if (wave == 0 && fsub == 0) put_header<HDR>(row, L);
   if (L.any_nullable) __syncthreads();  // null bits are OR-ed into the zeroed bitmap
 
-  enc_group<8, TR, FRAME>(fields, L.group[0], L.group[1], wave, fsub, idx, row, hdr_bm);
-  enc_group<4, TR, FRAME>(fields, L.group[1], L.group[2], wave, fsub, idx, row, hdr_bm);
-  enc_group<2, TR, FRAME>(fields, L.group[2], L.group[3], wave, fsub, idx, row, hdr_bm);
-  enc_group<1, TR, FRAME>(fields, L.group[3], L.group[4], wave, fsub, idx, row, hdr_bm);
+  enc_group<8, TR, HDR>(fields, L.group[0], L.group[1], wave, fsub, idx, row, hdr_bm);
+  enc_group<4, TR, HDR>(fields, L.group[1], L.group[2], wave, fsub, idx, row, hdr_bm);
+  enc_group<2, TR, HDR>(fields, L.group[2], L.group[3], wave, fsub, idx, row, hdr_bm);
+  enc_group<1, TR, HDR>(fields, L.group[3], L.group[4], wave, fsub, idx, row, hdr_bm);
   __syncthreads();
   store_tile(lds, out + r0 * L.stride, rows * L.stride, tid);
 }
@@ -210,7 +212,7 @@ __device__ __forceinline__ void v5_issue(const uint8_t* const (&ptr)[K], const i
   for (int k = 0; k < K; ++k) d[k] = *gp(reinterpret_cast<const u32x4*>(ptr[k] + r0 * wk[k]));
 }
 
-template <int R, int K, bool FRAME>
+template <int R, int K, int HDR>
 __device__ __forceinline__ void v5_write(uint8_t* lds, int stride, int hdr_bm, const int (&wk)[K],
                                          const uint32_t (&sf)[K], const u32x4 (&d)[K]) {
 #pragma unroll
@@ -221,21 +223,21 @@ __device__ __forceinline__ void v5_write(uint8_t* lds, int stride, int hdr_bm, c
     uint8_t* row = lds + rb * stride;
     const u32x4 x = d[k];
     if (w == 8) {
-      put_slot<FRAME>(row, hdr_bm, slot, (uint64_t)x.x | ((uint64_t)x.y << 32), false, flags);
-      put_slot<FRAME>(row + stride, hdr_bm, slot, (uint64_t)x.z | ((uint64_t)x.w << 32), false, flags);
+      put_slot<HDR>(row, hdr_bm, slot, (uint64_t)x.x | ((uint64_t)x.y << 32), false, flags);
+      put_slot<HDR>(row + stride, hdr_bm, slot, (uint64_t)x.z | ((uint64_t)x.w << 32), false, flags);
     } else if (w == 4) {
-      put_slot<FRAME>(row, hdr_bm, slot, x.x, false, flags);
-      put_slot<FRAME>(row + stride, hdr_bm, slot, x.y, false, flags);
-      put_slot<FRAME>(row + 2 * stride, hdr_bm, slot, x.z, false, flags);
-      put_slot<FRAME>(row + 3 * stride, hdr_bm, slot, x.w, false, flags);
+      put_slot<HDR>(row, hdr_bm, slot, x.x, false, flags);
+      put_slot<HDR>(row + stride, hdr_bm, slot, x.y, false, flags);
+      put_slot<HDR>(row + 2 * stride, hdr_bm, slot, x.z, false, flags);
+      put_slot<HDR>(row + 3 * stride, hdr_bm, slot, x.w, false, flags);
     } else if (w == 2) {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        put_slot<FRAME>(row + e * stride, hdr_bm, slot, (x[e >> 1] >> (16 * (e & 1))) & 0xffff, false, flags);
+        put_slot<HDR>(row + e * stride, hdr_bm, slot, (x[e >> 1] >> (16 * (e & 1))) & 0xffff, false, flags);
     } else if (w == 1) {
 #pragma unroll
       for (int e = 0; e < 16; ++e)
-        put_slot<FRAME>(row + e * stride, hdr_bm, slot, (x[e >> 2] >> (8 * (e & 3))) & 0xff, false, flags);
+        put_slot<HDR>(row + e * stride, hdr_bm, slot, (x[e >> 2] >> (8 * (e & 3))) & 0xff, false, flags);
     }
   }
 }
@@ -253,13 +255,12 @@ __device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* ld
   if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
 }
 
-template <int R, int WG, int K, bool FRAME>
+template <int R, int WG, int K, int HDR>
 __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
                                                                  const FixedFieldDev* __restrict__ fields,
                                                                  uint8_t* __restrict__ out, int64_t tiles) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int NW = WG / 64;
-  constexpr int HDR = FRAME ? 12 : 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -287,20 +288,20 @@ __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
       sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (1u << 20) | ((uint32_t)(c * (16 / w)) << 21);
     }
   }
-  if (tid < R) put_header<FRAME>(lds + tid * stride, L);  // constant across tiles (no nullable fields)
+  if (tid < R) put_header<HDR>(lds + tid * stride, L);  // constant across tiles (no nullable fields)
   u32x4 dA[K], dB[K];
   const int64_t last = tiles - 1;
   v5_issue<R, K>(ptr, wk, t * R, dA);
   v5_issue<R, K>(ptr, wk, min(t + (int64_t)gridDim.x, last) * R, dB);
   for (;;) {
-    v5_write<R, K, FRAME>(lds, stride, hdr_bm, wk, sf, dA);
+    v5_write<R, K, HDR>(lds, stride, hdr_bm, wk, sf, dA);
     __syncthreads();
     v5_store<R, WG>(L, lds, out + t * R * stride, tid);
     v5_issue<R, K>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dA);
     __syncthreads();
     t += gridDim.x;
     if (t >= tiles) break;
-    v5_write<R, K, FRAME>(lds, stride, hdr_bm, wk, sf, dB);
+    v5_write<R, K, HDR>(lds, stride, hdr_bm, wk, sf, dB);
     __syncthreads();
     v5_store<R, WG>(L, lds, out + t * R * stride, tid);
     v5_issue<R, K>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dB);
@@ -330,8 +331,13 @@ __device__ __forceinline__ void dma_tile(uint8_t* lds, const uint8_t* __restrict
   if (tid < tail4) st32(lds + n16 * 16 + tid * 4, ld32(src + n16 * 16 + tid * 4));
 }
 
-template <bool FRAME>
+template <int HDR>
 __device__ __forceinline__ void check_frame(const uint8_t* row, const FixedLaunch& L, int32_t* status) {
+  if (HDR == 8) {  // Encoder.decode(byte[]): the schema hash only (Encoders.java:181-190, 195-197)
+    const uint64_t h = (uint64_t)ld32(row) | ((uint64_t)ld32(row + 4) << 32);
+    if (h != (uint64_t)L.schema_hash) set_status(status, FORY_ERR_SCHEMA_MISMATCH);
+    return;
+  }
   // Encoders.decode (Encoders.java:177-190): size, then the schema hash.
   const uint32_t len = ld32(row);
   const uint64_t h = (uint64_t)ld32(row + 4) | ((uint64_t)ld32(row + 8) << 32);
@@ -340,11 +346,11 @@ __device__ __forceinline__ void check_frame(const uint8_t* row, const FixedLaunc
 }
 
 // Slot of an LDS row (UnsafeTrait.getX: the low W bytes).
-template <int W, bool FRAME>
+template <int W, int HDR>
 __device__ __forceinline__ uint64_t get_slot(const uint8_t* row, int hdr_bm, int slot) {
   const uint8_t* p = row + hdr_bm + 8 * slot;
   if constexpr (W == 8) {
-    if (FRAME) return (uint64_t)ld32(p) | ((uint64_t)ld32(p + 4) << 32);
+    if (HDR == 12) return (uint64_t)ld32(p) | ((uint64_t)ld32(p + 4) << 32);
     return *reinterpret_cast<const uint64_t*>(p);
   }
   return ld32(p);
@@ -365,7 +371,7 @@ __device__ __forceinline__ void put_validity(const FixedFieldDev& fd, bool isnul
 
 // Decodes slot values of one width group: null -> 0 (RowEncoderBuilder.java:239-246),
 // bool -> 0/1 (MemoryBuffer.getBoolean), coalesced column stores.
-template <int W, int TR, bool FRAME, int NT = 0>
+template <int W, int TR, int HDR, int NT = 0>
 __device__ __forceinline__ void dec_group(const FixedFieldDev* __restrict__ fields, int g0, int g1, int wave, int fsub,
                                           int r, const uint8_t* row, int hdr_bm, int hdr, bool live, int64_t grow,
                                           int64_t r0, int rows) {
@@ -383,7 +389,7 @@ __device__ __forceinline__ void dec_group(const FixedFieldDev* __restrict__ fiel
       if (p < g1) {
         const int slot = fields[p].slot;
         nul[u] = (ld32(row + hdr + ((slot >> 5) << 2)) >> (slot & 31)) & 1;  // BinaryRow.isNullAt
-        x[u] = get_slot<W, FRAME>(row, hdr_bm, slot);
+        x[u] = get_slot<W, HDR>(row, hdr_bm, slot);
       }
     }
 #pragma unroll
@@ -407,11 +413,10 @@ __device__ __forceinline__ void dec_group(const FixedFieldDev* __restrict__ fiel
   }
 }
 
-template <int TR, bool FRAME, int NT = 0>
+template <int TR, int HDR, int NT = 0>
 __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
                                                            const uint8_t* __restrict__ in, int32_t* status) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int HDR = FRAME ? 12 : 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -430,11 +435,11 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
   const uint8_t* row = lds + r * stride;
   const int64_t grow = r0 + r;
   const bool live = r < rows;
-  if (FRAME && wave == 0 && fsub == 0 && live) check_frame<FRAME>(row, L, status);
-  dec_group<8, TR, FRAME, NT>(fields, L.group[0], L.group[1], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
-  dec_group<4, TR, FRAME, NT>(fields, L.group[1], L.group[2], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
-  dec_group<2, TR, FRAME, NT>(fields, L.group[2], L.group[3], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
-  dec_group<1, TR, FRAME, NT>(fields, L.group[3], L.group[4], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  if (HDR && wave == 0 && fsub == 0 && live) check_frame<HDR>(row, L, status);
+  dec_group<8, TR, HDR, NT>(fields, L.group[0], L.group[1], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<4, TR, HDR, NT>(fields, L.group[1], L.group[2], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<2, TR, HDR, NT>(fields, L.group[2], L.group[3], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
+  dec_group<1, TR, HDR, NT>(fields, L.group[3], L.group[4], wave, fsub, r, row, hdr_bm, HDR, live, grow, r0, rows);
 }
 
 // ---------------------------------------------------------------------------
@@ -444,11 +449,11 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
 // tile (Struct104: 39 load instructions over 8 waves), nt row stores.
 constexpr int kV5R = 64, kV5WG = 512, kV5K = 6;
 
-template <bool FRAME>
+template <int HDR>
 hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const int64_t full = L.num_rows / kV5R;
   if (full > 0) {
-    auto* k = &encode_fixed_v5_kernel<kV5R, kV5WG, kV5K, FRAME>;
+    auto* k = &encode_fixed_v5_kernel<kV5R, kV5WG, kV5K, HDR>;
     raise_lds_cap(k);
     const size_t lds = (size_t)kV5R * L.stride;
     const int64_t grid = persistent_grid(k, lds, full, kV5WG);
@@ -457,7 +462,7 @@ hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   if (L.num_rows > full * kV5R) {  // tail (< R records): one-tile kernel
     FixedLaunch T = L;
     T.tile0 = full * kV5R / 64;
-    auto* k = &encode_fixed_kernel<64, FRAME>;
+    auto* k = &encode_fixed_kernel<64, HDR>;
     raise_lds_cap(k);
     const int64_t tail_tiles = (L.num_rows - full * kV5R + 63) / 64;
     hipLaunchKernelGGL(k, dim3((unsigned)tail_tiles), dim3(kWG), (size_t)64 * L.stride, s, T, L.fields, out);
@@ -465,27 +470,27 @@ hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int TR, bool FRAME>
+template <int TR, int HDR>
 hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const int64_t tiles = (L.num_rows + TR - 1) / TR;
   const size_t lds = (size_t)TR * L.stride;
   if constexpr (TR == 64) {
     // v5: not-null schemas whose chunk instructions fit K per wave
     if (!L.any_nullable && (v3_insn_count<kV5R>(L.group) + kV5WG / 64 - 1) / (kV5WG / 64) <= kV5K)
-      return launch_encode_v5<FRAME>(L, out, s);
+      return launch_encode_v5<HDR>(L, out, s);
   }
-  auto* k = &encode_fixed_kernel<TR, FRAME>;
+  auto* k = &encode_fixed_kernel<TR, HDR>;
   raise_lds_cap(k);
   hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(kWG), lds, s, L, L.fields, out);
   return hipGetLastError();
 }
 
-template <int TR, bool FRAME>
+template <int TR, int HDR>
 hipError_t launch_decode_tr(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
   const int64_t tiles = (L.num_rows + TR - 1) / TR;
   const size_t lds = (size_t)TR * L.stride;
   // TR = 64: non-temporal LDS-DMA row loads + column stores (17.72 -> 17.52 ms at 64M Struct104)
-  auto* k = TR == 64 ? &decode_fixed_kernel<TR, FRAME, 12> : &decode_fixed_kernel<TR, FRAME, 0>;
+  auto* k = TR == 64 ? &decode_fixed_kernel<TR, HDR, 12> : &decode_fixed_kernel<TR, HDR, 0>;
   raise_lds_cap(k);
   hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(kWG), lds, s, L, L.fields, in, status);
   return hipGetLastError();
@@ -503,32 +508,48 @@ static int pick_tr(int stride) {
   return 0;
 }
 
+namespace {
+
+template <int HDR>
+hipError_t encode_hdr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
+  switch (pick_tr(L.stride)) {
+    case 64: return launch_encode_tr<64, HDR>(L, out, s);
+    case 32: return launch_encode_tr<32, HDR>(L, out, s);
+    case 16: return launch_encode_tr<16, HDR>(L, out, s);
+    case 8: return launch_encode_tr<8, HDR>(L, out, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int HDR>
+hipError_t decode_hdr(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
+  switch (pick_tr(L.stride)) {
+    case 64: return launch_decode_tr<64, HDR>(L, in, status, s);
+    case 32: return launch_decode_tr<32, HDR>(L, in, status, s);
+    case 16: return launch_decode_tr<16, HDR>(L, in, status, s);
+    case 8: return launch_decode_tr<8, HDR>(L, in, status, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
 hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
-  switch (pick_tr(L.stride) * 2 + (L.frame ? 1 : 0)) {
-    case 128: return launch_encode_tr<64, false>(L, out, s);
-    case 129: return launch_encode_tr<64, true>(L, out, s);
-    case 64: return launch_encode_tr<32, false>(L, out, s);
-    case 65: return launch_encode_tr<32, true>(L, out, s);
-    case 32: return launch_encode_tr<16, false>(L, out, s);
-    case 33: return launch_encode_tr<16, true>(L, out, s);
-    case 16: return launch_encode_tr<8, false>(L, out, s);
-    case 17: return launch_encode_tr<8, true>(L, out, s);
+  switch (frame_header_bytes(L.frame)) {
+    case 0: return encode_hdr<0>(L, out, s);
+    case 8: return encode_hdr<8>(L, out, s);
+    case 12: return encode_hdr<12>(L, out, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 hipError_t launch_decode_fixed(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
-  switch (pick_tr(L.stride) * 2 + (L.frame ? 1 : 0)) {
-    case 128: return launch_decode_tr<64, false>(L, in, status, s);
-    case 129: return launch_decode_tr<64, true>(L, in, status, s);
-    case 64: return launch_decode_tr<32, false>(L, in, status, s);
-    case 65: return launch_decode_tr<32, true>(L, in, status, s);
-    case 32: return launch_decode_tr<16, false>(L, in, status, s);
-    case 33: return launch_decode_tr<16, true>(L, in, status, s);
-    case 16: return launch_decode_tr<8, false>(L, in, status, s);
-    case 17: return launch_decode_tr<8, true>(L, in, status, s);
+  switch (frame_header_bytes(L.frame)) {
+    case 0: return decode_hdr<0>(L, in, status, s);
+    case 8: return decode_hdr<8>(L, in, status, s);
+    case 12: return decode_hdr<12>(L, in, status, s);
     default: return hipErrorInvalidValue;
   }
 }

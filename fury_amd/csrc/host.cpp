@@ -11,6 +11,7 @@
 // capi.cpp (plan_info / workspace_bytes / encode / decode / read_status).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -213,29 +214,80 @@ int fory_rowfmt_host_unregister(void* host_ptr) {
   return hip_check(hipHostUnregister(host_ptr), "hipHostUnregister");
 }
 
-int fory_rowfmt_host_encode(fory_host_ctx* c, const fory_column* host_cols, int64_t n, int32_t frame,
-                            void* host_out, int64_t out_capacity) {
-  if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+}  // extern "C"
+
+namespace {
+
+// Host output windows: window w receives rows [first[w], first[w+1]) of the batch
+// (whole rows/frames only), at most cap[w] bytes. One window of the caller's
+// capacity is the contiguous MemoryBuffer of host_encode / host_encode_var.
+struct OutWindows {
+  std::vector<uint8_t*> ptr;
+  std::vector<int64_t> cap;
+  std::vector<int64_t> first;  // size() + 1 entries once split
+};
+
+// Greedy split (a MemoryBuffer is int-sized, MemoryBuffer.java:87: the JNI side
+// fills one buffer with whole frames, then the next): window w takes rows while
+// they fit its capacity. Offsets from `offs` (n+1, host) or i * stride. A window too
+// small for the next row stays empty; running out of windows is FORY_ERR_CAPACITY.
+int split_rows(const int64_t* offs, int64_t stride, int64_t n, OutWindows* W) {
+  const int64_t nw = (int64_t)W->cap.size();
+  W->first.assign((size_t)nw + 1, n);
+  auto at = [&](int64_t i) { return offs ? offs[i] : i * stride; };
+  int64_t start = 0;
+  for (int64_t w = 0; w < nw; ++w) {
+    W->first[(size_t)w] = start;
+    if (start >= n) continue;
+    const int64_t limit = at(start) + W->cap[(size_t)w];
+    int64_t lo = start, hi = n;  // largest e in [start, n] with at(e) <= limit
+    while (lo < hi) {
+      const int64_t mid = hi - (hi - lo) / 2;
+      if (at(mid) <= limit) lo = mid;
+      else hi = mid - 1;
+    }
+    start = lo;
+  }
+  W->first[(size_t)nw] = start;
+  if (start < n)
+    return fail_host(FORY_ERR_CAPACITY, "output windows hold " + std::to_string(start) + " of " + std::to_string(n) +
+                                            " rows (" + std::to_string(at(n) - at(start)) + " more bytes needed)");
+  return FORY_OK;
+}
+
+// Queues the D2H of rows [a, a + rows) (contiguous at `src`, row i at (i - a) * stride)
+// into the windows they belong to.
+int d2h_rows_windows(const OutWindows& W, const uint8_t* src, int64_t a, int64_t rows, int64_t stride, hipStream_t s) {
+  int rc = FORY_OK;
+  for (size_t w = 0; w + 1 < W.first.size() && !rc; ++w) {
+    const int64_t lo = std::max(a, W.first[w]), hi = std::min(a + rows, W.first[w + 1]);
+    if (lo >= hi) continue;
+    rc = hip_check(hipMemcpyAsync(W.ptr[w] + (lo - W.first[w]) * stride, src + (lo - a) * stride,
+                                  (size_t)((hi - lo) * stride), hipMemcpyDeviceToHost, s), "D2H");
+  }
+  return rc;
+}
+
+int host_encode_fixed(fory_host_ctx* c, const fory_column* host_cols, int64_t n, int32_t frame, OutWindows* W) {
   if (c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "varlen plan: use fory_rowfmt_host_encode_var");
-  if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM)
-    return fail_host(FORY_ERR_INVALID_ARGUMENT, "frame_mode must be 0 (raw) or 1 (stream)");
+  if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM && frame != FORY_FRAME_HASHED)
+    return fail_host(FORY_ERR_INVALID_ARGUMENT, "frame_mode must be 0 (raw), 1 (stream) or 3 (hashed)");
   if (n < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
-  if (n == 0) return FORY_OK;
-  if (!host_cols || !host_out) return fail_host(FORY_ERR_INVALID_ARGUMENT, "host columns or output is null");
-  const int64_t stride = c->info.fixed_size + (frame ? 12 : 0);
-  if (n * stride > out_capacity)  // MemoryBuffer bounds check (MemoryBuffer.java:303-309)
-    return fail_host(FORY_ERR_CAPACITY, "output capacity " + std::to_string(out_capacity) + " < " +
-                                            std::to_string(n * stride) + " bytes");
+  const int64_t stride = c->info.fixed_size + (frame == FORY_FRAME_STREAM ? 12 : frame == FORY_FRAME_HASHED ? 8 : 0);
+  int rc = split_rows(nullptr, stride, n, W);  // MemoryBuffer bounds check (MemoryBuffer.java:303-309)
+  if (rc || n == 0) return rc;
+  if (!host_cols) return fail_host(FORY_ERR_INVALID_ARGUMENT, "host columns are null");
+  for (size_t w = 0; w + 1 < W->first.size(); ++w)
+    if (W->first[w + 1] > W->first[w] && !W->ptr[w]) return fail_host(FORY_ERR_INVALID_ARGUMENT, "output is null");
   for (int i = 0; i < c->info.num_columns; ++i)
     if (!host_cols[i].values || host_cols[i].length < n)
       return fail_host(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(i) + " missing or shorter than num_rows");
-  int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
+  rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
   for (int b = 0; b < 2 && !rc; ++b)
     rc = hip_check(hipMemsetAsync(c->buf[b].status, 0, 4, c->s_k), "hipMemsetAsync");
   const int64_t chunks = (n + c->chunk - 1) / c->chunk;
   std::vector<fory_column> dcols(c->info.num_columns);
-  uint8_t* out = static_cast<uint8_t*>(host_out);
   for (int64_t k = 0; k < chunks && !rc; ++k) {
     const int b = (int)(k & 1);
     int64_t a, rows;
@@ -261,11 +313,9 @@ int fory_rowfmt_host_encode(fory_host_ctx* c, const fory_column* host_cols, int6
       rc = fory_rowfmt_encode(c->plan, dcols.data(), rows, frame, nullptr, B.rows, rows * stride, B.status, B.ws,
                               c->ws_bytes, c->s_k);
     if (!rc) rc = hip_check(hipEventRecord(c->ev_k[b], c->s_k), "hipEventRecord");
-    // D2H: the chunk's rows, contiguous in the output (row/frame i at i * stride)
+    // D2H: the chunk's rows into the window(s) holding them
     if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_out, c->ev_k[b], 0), "hipStreamWaitEvent");
-    if (!rc)
-      rc = hip_check(hipMemcpyAsync(out + a * stride, B.rows, (size_t)(rows * stride), hipMemcpyDeviceToHost,
-                                    c->s_out), "D2H");
+    if (!rc) rc = d2h_rows_windows(*W, B.rows, a, rows, stride, c->s_out);
     if (!rc) rc = hip_check(hipEventRecord(c->ev_out[b], c->s_out), "hipEventRecord");
   }
   const int rc_sync = hip_check(hipStreamSynchronize(c->s_out), "hipStreamSynchronize");
@@ -280,16 +330,30 @@ int fory_rowfmt_host_encode(fory_host_ctx* c, const fory_column* host_cols, int6
   return FORY_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int fory_rowfmt_host_encode(fory_host_ctx* c, const fory_column* host_cols, int64_t n, int32_t frame,
+                            void* host_out, int64_t out_capacity) {
+  if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+  if (n > 0 && !host_out) return fail_host(FORY_ERR_INVALID_ARGUMENT, "output is null");
+  OutWindows W;
+  W.ptr = {static_cast<uint8_t*>(host_out)};
+  W.cap = {out_capacity};
+  return host_encode_fixed(c, host_cols, n, frame, &W);
+}
+
 int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t rows_bytes, int64_t n, int32_t frame,
                             const fory_column* host_out_cols) {
   if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
   if (c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "varlen plan: use fory_rowfmt_host_decode_var");
-  if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM)
-    return fail_host(FORY_ERR_INVALID_ARGUMENT, "frame_mode must be 0 (raw) or 1 (stream)");
+  if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM && frame != FORY_FRAME_HASHED)
+    return fail_host(FORY_ERR_INVALID_ARGUMENT, "frame_mode must be 0 (raw), 1 (stream) or 3 (hashed)");
   if (n < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
   if (n == 0) return FORY_OK;
   if (!host_rows || !host_out_cols) return fail_host(FORY_ERR_INVALID_ARGUMENT, "host rows or output columns null");
-  const int64_t stride = c->info.fixed_size + (frame ? 12 : 0);
+  const int64_t stride = c->info.fixed_size + (frame == FORY_FRAME_STREAM ? 12 : frame == FORY_FRAME_HASHED ? 8 : 0);
   if (n * stride > rows_bytes)
     return fail_host(FORY_ERR_CORRUPT, "row buffer holds " + std::to_string(rows_bytes) + " bytes < " +
                                            std::to_string(n) + " rows x " + std::to_string(stride));
@@ -417,12 +481,10 @@ int64_t carve(fory_host_ctx* c, uint8_t* base, const std::vector<int64_t>& cnt, 
 
 }  // namespace
 
-extern "C" {
+namespace {
 
-int fory_rowfmt_host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, int32_t frame,
-                                void* host_out, int64_t out_capacity, int64_t* host_row_offsets,
-                                int64_t* out_bytes) {
-  if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+int host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, int32_t frame, OutWindows* W,
+                    int64_t* host_row_offsets, int64_t* out_bytes) {
   if (!c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "fixed-width plan: use fory_rowfmt_host_encode");
   if (n < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
   if (out_bytes) *out_bytes = 0;
@@ -430,7 +492,7 @@ int fory_rowfmt_host_encode_var(fory_host_ctx* c, const fory_column* host_cols, 
     if (host_row_offsets) host_row_offsets[0] = 0;
     return FORY_OK;
   }
-  if (!host_cols || !host_out) return fail_host(FORY_ERR_INVALID_ARGUMENT, "host columns or output is null");
+  if (!host_cols) return fail_host(FORY_ERR_INVALID_ARGUMENT, "host columns are null");
   // the encode reuses the device buffers a staged decode lives in: a later
   // host_decode_var must be preceded by a fresh host_decode_var_sizes
   c->dec_n = -1;
@@ -476,23 +538,78 @@ int fory_rowfmt_host_encode_var(fory_host_ctx* c, const fory_column* host_cols, 
   }
   if (!rc) rc = hip_check(hipMemsetAsync(status, 0, 4, c->s_k), "hipMemsetAsync");
   if (!rc) rc = fory_rowfmt_encoded_size(c->plan, d.data(), n, frame, d_offs, ws, ws_bytes, c->s_k);
-  int64_t total = 0;
-  if (!rc) rc = hip_check(hipMemcpyAsync(&total, d_offs + n, 8, hipMemcpyDeviceToHost, c->s_k), "D2H total");
+  // row/frame offsets to the host: the split into the caller's windows needs them
+  std::vector<int64_t> tmp;
+  int64_t* ho = host_row_offsets;
+  if (!ho) {
+    tmp.resize((size_t)n + 1);
+    ho = tmp.data();
+  }
+  if (!rc) rc = hip_check(hipMemcpyAsync(ho, d_offs, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, c->s_k), "D2H offsets");
   if (!rc) rc = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize");
   if (rc) return rc;
+  const int64_t total = ho[n];
   if (out_bytes) *out_bytes = total;
-  if (total > out_capacity)  // MemoryBuffer bounds check (MemoryBuffer.java:303-309)
-    return fail_host(FORY_ERR_CAPACITY, "output capacity " + std::to_string(out_capacity) + " < " +
-                                            std::to_string(total) + " bytes");
+  rc = split_rows(ho, 0, n, W);  // MemoryBuffer bounds check (MemoryBuffer.java:303-309)
+  if (rc) return rc;
+  for (size_t w = 0; w + 1 < W->first.size(); ++w)
+    if (W->first[w + 1] > W->first[w] && !W->ptr[w]) return fail_host(FORY_ERR_INVALID_ARGUMENT, "output is null");
   rc = ensure(c, &c->drows, &c->drows_bytes, total + 16);
   if (!rc) rc = fory_rowfmt_encode(c->plan, d.data(), n, frame, d_offs, c->drows, total, status, ws, ws_bytes, c->s_k);
-  if (!rc && total > 0)
-    rc = hip_check(hipMemcpyAsync(host_out, c->drows, (size_t)total, hipMemcpyDeviceToHost, c->s_k), "D2H rows");
-  if (!rc && host_row_offsets)
-    rc = hip_check(hipMemcpyAsync(host_row_offsets, d_offs, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, c->s_k),
-                   "D2H row offsets");
+  for (size_t w = 0; w + 1 < W->first.size() && !rc; ++w) {  // each window: its rows' contiguous bytes
+    const int64_t lo = ho[W->first[w]], hi = ho[W->first[w + 1]];
+    if (hi > lo)
+      rc = hip_check(hipMemcpyAsync(W->ptr[w], c->drows + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, c->s_k),
+                     "D2H rows");
+  }
   if (!rc) rc = fory_rowfmt_read_status(status, c->s_k);  // synchronises the stream
   return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fory_rowfmt_host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, int32_t frame,
+                                void* host_out, int64_t out_capacity, int64_t* host_row_offsets,
+                                int64_t* out_bytes) {
+  if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+  OutWindows W;
+  W.ptr = {static_cast<uint8_t*>(host_out)};
+  W.cap = {out_capacity};
+  return host_encode_var(c, host_cols, n, frame, &W, host_row_offsets, out_bytes);
+}
+
+int fory_rowfmt_host_encode_windows(fory_host_ctx* c, const fory_column* host_cols, int64_t n, int32_t frame,
+                                    void* const* windows, const int64_t* window_caps, int32_t num_windows,
+                                    int64_t* window_rows, int64_t* window_bytes) {
+  if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+  if (num_windows <= 0 || !windows || !window_caps)
+    return fail_host(FORY_ERR_INVALID_ARGUMENT, "windows / window_caps null or num_windows <= 0");
+  OutWindows W;
+  for (int32_t w = 0; w < num_windows; ++w) {
+    if (window_caps[w] < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "window capacity < 0");
+    W.ptr.push_back(static_cast<uint8_t*>(windows[w]));
+    W.cap.push_back(window_caps[w]);
+  }
+  int rc;
+  int64_t stride = 0;
+  std::vector<int64_t> offs;
+  if (c->varlen) {
+    offs.resize((size_t)(n > 0 ? n : 0) + 1, 0);
+    rc = host_encode_var(c, host_cols, n, frame, &W, offs.data(), nullptr);
+  } else {
+    stride = c->info.fixed_size + (frame == FORY_FRAME_STREAM ? 12 : frame == FORY_FRAME_HASHED ? 8 : 0);
+    rc = host_encode_fixed(c, host_cols, n, frame, &W);
+  }
+  if (rc) return rc;
+  if (W.first.size() != (size_t)num_windows + 1) W.first.assign((size_t)num_windows + 1, 0);
+  for (int32_t w = 0; w < num_windows; ++w) {
+    const int64_t f0 = W.first[(size_t)w], f1 = W.first[(size_t)w + 1];
+    if (window_rows) window_rows[w] = f1 - f0;
+    if (window_bytes) window_bytes[w] = c->varlen ? offs[(size_t)f1] - offs[(size_t)f0] : (f1 - f0) * stride;
+  }
+  return FORY_OK;
 }
 
 }  // extern "C"

@@ -10,6 +10,13 @@
 
 namespace fory_amd {
 
+// Bytes before the row in each framing (include/fory_rowfmt.h): RAW none, STREAM
+// [i32 size][i64 hash], COLLECTION [i32 size] (the payload replaces the row),
+// HASHED [i64 hash].
+__host__ __device__ inline int frame_header_bytes(int mode) {
+  return mode == FORY_FRAME_STREAM ? 12 : mode == FORY_FRAME_HASHED ? 8 : mode == FORY_FRAME_COLLECTION ? 4 : 0;
+}
+
 struct FixedLaunch {
   const FixedFieldDev* fields;  // device table
   int32_t num_fields;
@@ -22,19 +29,6 @@ struct FixedLaunch {
   int32_t frame;
   int32_t group[5];             // table index where the 8/4/2/1-byte groups start; group[4] = num_fields
   int64_t tile0;                // first tile of this launch (tail launches after a persistent kernel)
-  int32_t pitch;                // LDS row pitch of the v3 encode image (>= stride)
-  uint32_t stride_magic;        // floor((2^32-1) / stride): division by stride in the store phase
-  // Column slabs (encode v4, raw rows): slab s = row bytes [byte0, byte0 + nbytes),
-  // 16-B aligned; its fields are slab_fields[group[0] .. group[4]) by width group.
-  const FixedFieldDev* slab_fields;
-  int32_t num_slabs;
-  int32_t slab_pitch;           // LDS row pitch of one slab image
-  struct Slab {
-    int32_t group[5];
-    int32_t byte0;
-    int32_t nbytes;
-    uint32_t cpr_magic;         // floor((2^32-1) / (nbytes/16))
-  } slab[8];
 };
 
 hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s);

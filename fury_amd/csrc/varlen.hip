@@ -110,7 +110,7 @@ __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* _
   // FORY_FRAME_COLLECTION (ArrayEncoder/MapEncoder.encode(MemoryBuffer, T), Encoders.java:418-431,
   // 559-572): [i32 size][the single field's BinaryArray / BinaryMap], no row around it
   const bool coll = L.frame == FORY_FRAME_COLLECTION;
-  int64_t size = coll ? 4 : L.fixed_size + (L.frame ? 12 : 0);
+  int64_t size = coll ? 4 : L.fixed_size + frame_header_bytes(L.frame);
   int absent_depth = 0;  // >0: inside a null struct
   for (int pc = 0; pc < L.num_ops; ++pc) {
     const Op op = prog[pc];
@@ -247,10 +247,13 @@ __device__ __forceinline__ void enc_record(const VarLaunch& L, const Op* __restr
   if (coll) {
     st32(base, (uint32_t)(size - 4));
     row = base + 4 - L.fixed_size;
-  } else if (L.frame) {  // Encoders.encode(MemoryBuffer,T): [i32 8+rowSize][i64 hash]
+  } else if (L.frame == FORY_FRAME_STREAM) {  // Encoders.encode(MemoryBuffer,T): [i32 8+rowSize][i64 hash]
     st32(base, (uint32_t)(size - 4));
     gst64(base + 4, (uint64_t)L.schema_hash);
     row = base + 12;
+  } else if (L.frame == FORY_FRAME_HASHED) {  // Encoders.encode(T): [i64 hash][row]
+    gst64(base, (uint64_t)L.schema_hash);
+    row = base + 8;
   }
   // writer stack: start (relative to row), header bytes, ordinal in parent
   int32_t st_start[kMaxDepth], st_hdr[kMaxDepth], st_ord[kMaxDepth];
@@ -517,13 +520,19 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
     }
     row = base + 4 - L.fixed_size;  // the payload sits where the field's var data would
     row_len += L.fixed_size - 4;
-  } else if (live && L.frame) {
+  } else if (live && L.frame == FORY_FRAME_STREAM) {
     const uint32_t len = ld32(base);
     const uint64_t h = gld64(base + 4);
     if (h != (uint64_t)L.schema_hash) { if (WRITE) set_status(status, FORY_ERR_SCHEMA_MISMATCH); bad = true; }
     else if ((int64_t)len + 4 != row_len || len < (uint32_t)(8 + L.fixed_size)) { if (WRITE) set_status(status, FORY_ERR_CORRUPT); bad = true; }
     row = base + 12;
     row_len -= 12;
+  } else if (live && L.frame == FORY_FRAME_HASHED) {  // Encoder.decode(byte[]) (Encoders.java:195-197)
+    const uint64_t h = gld64(base);
+    if (h != (uint64_t)L.schema_hash) { if (WRITE) set_status(status, FORY_ERR_SCHEMA_MISMATCH); bad = true; }
+    else if (row_len < 8 + L.fixed_size) { if (WRITE) set_status(status, FORY_ERR_CORRUPT); bad = true; }
+    row = base + 8;
+    row_len -= 8;
   }
   int32_t st_start[kMaxDepth], st_hdr[kMaxDepth];
   int depth = 0;
@@ -1372,7 +1381,7 @@ __device__ __forceinline__ void flat_dec_struct_bases(const VarLaunch& L, const 
 // (Mixed-like plans are LDS-limited at 4 workgroups per CU anyway) and a lean one for
 // 5 waves per SIMD (small-row plans such as Nested are register-limited: encode
 // 1.49 -> 1.26 ms; its spills would cost Mixed 27 %). launch_flat_enc_t picks by occupancy.
-template <bool FRAME, int NW, bool PROF, bool SPILL>
+template <int HDR, int NW, bool PROF, bool SPILL>
 __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
                                                                   const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
                                                                   const StructDev* __restrict__ st,
@@ -1380,7 +1389,6 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
                                                                   uint8_t* __restrict__ out, int64_t capacity,
                                                                   int32_t* status, int cap, SpillArgs sp) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int HDR = FRAME ? 12 : 0;
   const int stg_bytes = L.stg_bytes;
   uint8_t* img = lds;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1469,9 +1477,11 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
   if (wave == 0) {
     // Encoders.encode frame header; BinaryRowWriter.reset zeroes the bitmap (BinaryRowWriter.java:76-84)
     if (live) {
-      if (FRAME) {
+      if (HDR == 12) {
         st32(fp, (uint32_t)(end - beg - 4));
         st64_lds(fp + 4, (uint64_t)L.schema_hash);
+      } else if (HDR == 8) {
+        st64_lds(fp, (uint64_t)L.schema_hash);
       }
       for (int b = 0; b < L.bitmap_bytes; b += 4) st32(row + b, 0);
     }
@@ -1633,14 +1643,14 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
       const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,                         \
       const StructDev* __restrict__ st, const int64_t* __restrict__ offs, uint8_t* __restrict__ out,    \
       int64_t capacity, int32_t* status, int cap, SpillArgs sp
-template <bool FRAME, int NW, bool PROF, bool SPILL>
+template <int HDR, int NW, bool PROF, bool SPILL>
 __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(FORY_VAR_ENC_PARAMS) {
-  var_encode_flat_body<FRAME, NW, PROF, SPILL>(L, prog, cols, fix, vf, st, offs, out, capacity, status, cap, sp);
+  var_encode_flat_body<HDR, NW, PROF, SPILL>(L, prog, cols, fix, vf, st, offs, out, capacity, status, cap, sp);
 }
-template <bool FRAME, int NW, bool PROF, bool SPILL>
+template <int HDR, int NW, bool PROF, bool SPILL>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(5, 8))) void var_encode_flat_lean_kernel(
     FORY_VAR_ENC_PARAMS) {
-  var_encode_flat_body<FRAME, NW, PROF, SPILL>(L, prog, cols, fix, vf, st, offs, out, capacity, status, cap, sp);
+  var_encode_flat_body<HDR, NW, PROF, SPILL>(L, prog, cols, fix, vf, st, offs, out, capacity, status, cap, sp);
 }
 #undef FORY_VAR_ENC_PARAMS
 
@@ -1759,7 +1769,25 @@ __device__ __forceinline__ void flat_dec_fixed(const VarLaunch& L, const FixedFi
   }
 }
 
-template <bool FRAME, bool WRITE, int NW, bool SPILL>
+// Frame header of a staged record (HDR 12: Encoders.decode(MemoryBuffer) reads the
+// size then the hash, Encoders.java:177-193; HDR 8: decode(byte[]), the hash only,
+// :195-197). False (and the status word set when `report`) on a mismatch.
+template <int HDR>
+__device__ __forceinline__ bool frame_ok(const VarLaunch& L, const uint8_t* fp, int64_t frame_len, bool report,
+                                         int32_t* status) {
+  const int ho = HDR == 12 ? 4 : 0;
+  const uint64_t h = (uint64_t)ld32(fp + ho) | ((uint64_t)ld32(fp + ho + 4) << 32);
+  if (h != (uint64_t)L.schema_hash) {
+    if (report) set_status(status, FORY_ERR_SCHEMA_MISMATCH);
+    return false;
+  }
+  const bool size_ok = HDR == 12 ? ((int64_t)ld32(fp) + 4 == frame_len && ld32(fp) >= (uint32_t)(8 + L.fixed_size))
+                                 : frame_len >= 8 + L.fixed_size;
+  if (!size_ok && report) set_status(status, FORY_ERR_CORRUPT);
+  return size_ok;
+}
+
+template <int HDR, bool WRITE, int NW, bool SPILL>
 __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
                                                                   const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
                                                                   const StructDev* __restrict__ st,
@@ -1768,7 +1796,6 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
                                                                   int64_t* __restrict__ tile_tot, int32_t* status,
                                                                   int cap, SpillArgs sp) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int HDR = FRAME ? 12 : 0;
   const int stg_bytes = L.stg_bytes;
   uint8_t* img = lds;
   const int nslot = L.num_var < NW ? L.num_var : NW;  // staging slots: waves with var fields (v = wave + k NW)
@@ -1800,12 +1827,8 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
       const uint8_t* row = fp + HDR;
       int64_t row_len = end - beg;
       bool bad = !live;
-      if (live && FRAME) {
-        const uint32_t len = ld32(fp);
-        const uint64_t h = (uint64_t)ld32(fp + 4) | ((uint64_t)ld32(fp + 8) << 32);
-        bad = h != (uint64_t)L.schema_hash || (int64_t)len + 4 != row_len || len < (uint32_t)(8 + L.fixed_size);
-        row_len -= 12;
-      }
+      if (live && HDR) bad = !frame_ok<HDR>(L, fp, row_len, false, status);
+      row_len -= HDR;
       if (L.num_struct) {
         const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
         flat_dec_struct_bases<false>(L, st, bad, live, lane, r0, rows, row, row_len, sbase, status);
@@ -1853,19 +1876,8 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   const uint8_t* row = fp + HDR;
   int64_t row_len = end - beg;
   bool bad = !live;
-  if (live && FRAME) {  // Encoders.decode: length + schema hash (Encoders.java:177-200)
-    const uint32_t len = ld32(fp);
-    const uint64_t h = (uint64_t)ld32(fp + 4) | ((uint64_t)ld32(fp + 8) << 32);
-    const bool report = WRITE && wave == 0;
-    if (h != (uint64_t)L.schema_hash) {
-      if (report) set_status(status, FORY_ERR_SCHEMA_MISMATCH);
-      bad = true;
-    } else if ((int64_t)len + 4 != row_len || len < (uint32_t)(8 + L.fixed_size)) {
-      if (report) set_status(status, FORY_ERR_CORRUPT);
-      bad = true;
-    }
-    row_len -= 12;
-  }
+  if (live && HDR) bad = !frame_ok<HDR>(L, fp, row_len, WRITE && wave == 0, status);  // Encoders.decode
+  row_len -= HDR;
   if (L.num_struct) {  // child-row offsets (+ struct validity) for every wave
     if (wave == 0) flat_dec_struct_bases<WRITE>(L, st, bad, live, lane, r0, rows, row, row_len, sbase, status);
     __syncthreads();
@@ -2144,7 +2156,7 @@ int fit_slot(K* k, int threads, int b, F lds_of) {
 template <typename K>
 int enc_stg_bytes(K* k, const VarLaunch& L, int64_t capacity, int cap, int nw) {
   if (getenv("FORY_ROWFMT_VARSTG") || L.num_rows < 64 || L.num_var == 0) return L.stg_bytes;
-  const int64_t var_row = capacity / L.num_rows - L.fixed_size - (L.frame ? 12 : 0) - L.nested_fixed;
+  const int64_t var_row = capacity / L.num_rows - L.fixed_size - frame_header_bytes(L.frame) - L.nested_fixed;
   const int64_t per = var_row > 0 ? 64 * var_row / L.num_var : 0;
   int b = (int)((per * 3 / 2 + 512 + 255) & ~int64_t(255));
   b = b < 2048 ? 2048 : (b > 16384 ? 16384 : b);
@@ -2218,13 +2230,13 @@ void var_diag(const char* what, K* k, int threads, int cap, int stg, size_t lds)
 
 // Encode: default or lean kernel (5 waves per SIMD register budget), whichever keeps
 // more workgroups per CU resident with its own staging / image sizing (ties: default).
-template <bool FRAME, int NW, bool PROF>
+template <int HDR, int NW, bool PROF>
 void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                        int cap, hipStream_t s) {
   VarLaunch L = L0;
   L.pl_all = 1;
-  auto* kd = &var_encode_flat_kernel<FRAME, NW, PROF, false>;
-  auto* kl = &var_encode_flat_lean_kernel<FRAME, NW, PROF, false>;
+  auto* kd = &var_encode_flat_kernel<HDR, NW, PROF, false>;
+  auto* kl = &var_encode_flat_lean_kernel<HDR, NW, PROF, false>;
   auto size_for = [&](decltype(kd) kk, int* stg, int* c) {
     VarLaunch T = L;
     *stg = enc_stg_bytes(kk, T, capacity, cap, NW);
@@ -2245,24 +2257,24 @@ void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, i
   var_diag(lean ? "encode (lean)" : "encode", k, 64 * NW, cap, L.stg_bytes, flat_lds_enc(L, cap, NW));
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds_enc(L, cap, NW), s, L, L.prog,
                      L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, cap, sp);
-  auto* k2 = lean ? &var_encode_flat_lean_kernel<FRAME, NW, PROF, true> : &var_encode_flat_kernel<FRAME, NW, PROF, true>;
+  auto* k2 = lean ? &var_encode_flat_lean_kernel<HDR, NW, PROF, true> : &var_encode_flat_kernel<HDR, NW, PROF, true>;
   raise_lds_cap(k2);
   hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds_enc(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
                      flat_lds_enc(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, sp.cap,
                      sp);
 }
 
-template <bool FRAME, int NW>
+template <int HDR, int NW>
 void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                      int cap, hipStream_t s) {
-  if (L.prof) launch_flat_enc_t<FRAME, NW, true>(L, offs, out, capacity, status, cap, s);
-  else launch_flat_enc_t<FRAME, NW, false>(L, offs, out, capacity, status, cap, s);
+  if (L.prof) launch_flat_enc_t<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
+  else launch_flat_enc_t<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
 }
 
-template <bool FRAME, bool WRITE, int NW>
+template <int HDR, bool WRITE, int NW>
 void launch_flat_dec(const VarLaunch& L0, const uint8_t* rows, const int64_t* offs, int64_t* tile_tot,
                      int32_t* status, int cap, hipStream_t s) {
-  auto* k = &var_decode_flat_kernel<FRAME, WRITE, NW, false>;
+  auto* k = &var_decode_flat_kernel<HDR, WRITE, NW, false>;
   raise_lds_cap(k);
   VarLaunch L = L0;
   if (WRITE) L.stg_bytes = dec_stg_bytes(k, L0, cap, NW);
@@ -2273,7 +2285,7 @@ void launch_flat_dec(const VarLaunch& L0, const uint8_t* rows, const int64_t* of
   var_diag(WRITE ? "decode" : "decode lengths", k, 64 * NW, cap, L.stg_bytes, lds);
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
                      L.vf, L.st, rows, offs, tile_tot, status, cap, sp);
-  auto* k2 = &var_decode_flat_kernel<FRAME, WRITE, NW, true>;
+  auto* k2 = &var_decode_flat_kernel<HDR, WRITE, NW, true>;
   raise_lds_cap(k2);
   const size_t lds2 = WRITE ? flat_lds_dec(L, sp.cap, NW) : (size_t)sp.cap + sbase_lds(L);
   hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, lds2, 64 * NW)), dim3(64 * NW), lds2, s, L, L.prog, L.cols, L.fix,
@@ -2293,8 +2305,11 @@ hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const
   if (L.num_rows <= 0) return hipSuccess;
   if (var_tiles() && var_flat(L)) {
     const int cap = fit_cap(L, L.mean_row);
-    if (L.frame) launch_flat_dec<true, WRITE, kNW>(L, rows, offs, tile_tot, status, cap, s);
-    else launch_flat_dec<false, WRITE, kNW>(L, rows, offs, tile_tot, status, cap, s);
+    switch (frame_header_bytes(L.frame)) {
+      case 12: launch_flat_dec<12, WRITE, kNW>(L, rows, offs, tile_tot, status, cap, s); break;
+      case 8: launch_flat_dec<8, WRITE, kNW>(L, rows, offs, tile_tot, status, cap, s); break;
+      default: launch_flat_dec<0, WRITE, kNW>(L, rows, offs, tile_tot, status, cap, s); break;
+    }
     return hipGetLastError();
   }
   if (var_tiles()) {
@@ -2323,8 +2338,11 @@ hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* o
   if (L.num_rows <= 0) return hipSuccess;
   if (var_tiles() && var_flat(L)) {
     const int cap = enc_cap(L, capacity);
-    if (L.frame) launch_flat_enc<true, kNW>(L, offs, out, capacity, status, cap, s);
-    else launch_flat_enc<false, kNW>(L, offs, out, capacity, status, cap, s);
+    switch (frame_header_bytes(L.frame)) {
+      case 12: launch_flat_enc<12, kNW>(L, offs, out, capacity, status, cap, s); break;
+      case 8: launch_flat_enc<8, kNW>(L, offs, out, capacity, status, cap, s); break;
+      default: launch_flat_enc<0, kNW>(L, offs, out, capacity, status, cap, s); break;
+    }
     return hipGetLastError();
   }
   if (var_tiles()) {

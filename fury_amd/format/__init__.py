@@ -10,7 +10,7 @@ from .columns import HostColumn, build_columns, pack_validity, unpack_validity  
 def __getattr__(name):
     # The device path (Encoders/RowEncoder) imports torch lazily.
     if name in ("Encoders", "RowEncoder", "CollectionEncoder", "EncodedRows", "FRAME_RAW", "FRAME_STREAM",
-                "FRAME_COLLECTION"):
+                "FRAME_COLLECTION", "FRAME_HASHED"):
         from . import encoder
         return getattr(encoder, name)
     raise AttributeError(name)

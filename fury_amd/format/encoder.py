@@ -10,6 +10,8 @@ Here the unit of work is a batch of N objects held as device columns:
                                                   into one fresh buffer
   encode(columns, n, frame_mode=FRAME_RAW)     == N x toRow(obj).toBytes()
   decode(rows, frame_mode=...)                 == N x decode(buffer) / fromRow(row)
+  encode(columns, n, frame_mode=FRAME_HASHED)  == N x encode(obj) -> byte[] ([i64 hash][row]),
+                                                  back to back with row offsets
   Encoders.array_encoder / map_encoder         == N x ArrayEncoder / MapEncoder
                                                   .encode(MemoryBuffer, collection)
 Same bytes, same schema hash, same exceptions (errors.py).
@@ -28,6 +30,7 @@ from .types import ArrowType, Schema
 FRAME_RAW = _lib.FRAME_RAW
 FRAME_STREAM = _lib.FRAME_STREAM
 FRAME_COLLECTION = _lib.FRAME_COLLECTION
+FRAME_HASHED = _lib.FRAME_HASHED
 
 
 def _torch_dtype(type_id):

@@ -14,6 +14,12 @@ from .errors import raise_for
 from .types import ArrowType, Schema, flatten, preorder
 
 
+def frame_header_bytes(frame_mode: int) -> int:
+    """Bytes before each row: STREAM [i32 size][i64 hash], HASHED [i64 hash],
+    COLLECTION [i32 size] (the payload replaces the row), RAW none."""
+    return {_lib.FRAME_STREAM: 12, _lib.FRAME_HASHED: 8, _lib.FRAME_COLLECTION: 4}.get(frame_mode, 0)
+
+
 def _ptr(t) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
@@ -58,7 +64,7 @@ class NativePlan:
 
     def stride(self, frame_mode: int) -> int:
         assert self.fixed_width
-        return self.fixed_size + (12 if frame_mode else 0)
+        return self.fixed_size + frame_header_bytes(frame_mode)
 
     def workspace_bytes(self, num_rows: int) -> int:
         return int(_lib.load().fory_rowfmt_workspace_bytes(self.handle, num_rows))
@@ -186,6 +192,20 @@ class HostPipeline:
         _check(_lib.load().fory_rowfmt_host_encode(self.handle, self._host_array(host_cols), n, frame,
                                                    _np_ptr(out), out.nbytes))
 
+    def encode_windows(self, host_cols, n: int, frame: int, windows):
+        """fory_rowfmt_host_encode_windows: whole rows/frames into a list of uint8 numpy
+        windows (greedy); returns (rows per window, bytes per window)."""
+        import numpy as np
+        nw = len(windows)
+        ptrs = (ctypes.c_void_p * nw)(*[w.ctypes.data for w in windows])
+        caps = np.array([w.nbytes for w in windows], np.int64)
+        rows = np.zeros(nw, np.int64)
+        nbytes = np.zeros(nw, np.int64)
+        _check(_lib.load().fory_rowfmt_host_encode_windows(self.handle, self._host_array(host_cols), n, frame,
+                                                           ctypes.cast(ptrs, ctypes.c_void_p), _np_ptr(caps), nw,
+                                                           _np_ptr(rows), _np_ptr(nbytes)))
+        return rows, nbytes
+
     def decode(self, rows, n: int, frame: int, host_out_cols) -> None:
         _check(_lib.load().fory_rowfmt_host_decode(self.handle, _np_ptr(rows), rows.nbytes, n, frame,
                                                    self._host_array(host_out_cols)))
@@ -262,6 +282,21 @@ class HostPipeline:
             cols.append(c)
         _check(_lib.load().fory_rowfmt_host_decode_var(self.handle, self._host_array(cols)))
         return cols
+
+
+def split_windows(row_offsets, n: int, max_window_bytes: int = (1 << 31) - 1, stride: int = 0):
+    """fory_rowfmt_split_windows: rows [first[w], first[w+1]) per <= max_window_bytes window
+    (host numpy offsets, or row i at i * stride)."""
+    import numpy as np
+    offs = None if row_offsets is None else np.ascontiguousarray(row_offsets, dtype=np.int64)
+    total = int(offs[n]) if offs is not None else n * stride
+    # each window holds >= 1 row, and two consecutive windows hold > max_window_bytes
+    cap = max(1, min(n, 2 * total // max(1, max_window_bytes) + 2))
+    first = np.zeros(cap + 1, np.int64)
+    nw = ctypes.c_int32(0)
+    _check(_lib.load().fory_rowfmt_split_windows(_np_ptr(offs), stride, n, max_window_bytes, cap, _np_ptr(first),
+                                                 ctypes.byref(nw)))
+    return first[:nw.value + 1]
 
 
 def host_register(a) -> None:

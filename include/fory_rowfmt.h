@@ -132,7 +132,16 @@ typedef struct fory_plan_info {
  *                     Encoder.encode(MemoryBuffer, T) write into one buffer
  *                     (Encoders.java:213-225):
  *                     [int32 LE 8+rowSize][int64 LE schemaHash][row].     */
-enum fory_frame_mode { FORY_FRAME_RAW = 0, FORY_FRAME_STREAM = 1, FORY_FRAME_COLLECTION = 2 };
+enum fory_frame_mode { FORY_FRAME_RAW = 0, FORY_FRAME_STREAM = 1, FORY_FRAME_COLLECTION = 2, FORY_FRAME_HASHED = 3 };
+/*  FORY_FRAME_HASHED: N calls of Encoder.encode(T) -> byte[] (Encoders.java:203-210):
+ *                     [int64 LE schemaHash][row] per record, back to back; like
+ *                     RAW rows they do not delimit themselves, so row offsets
+ *                     (encoded_size) locate each byte[]. Decode = N x
+ *                     Encoder.decode(byte[]) (Encoders.java:195-197): the hash is
+ *                     checked (FORY_ERR_SCHEMA_MISMATCH). The reference points the
+ *                     BinaryRow at [8, 8 + bytes.length) — a size 8 bytes too large
+ *                     (Encoders.java:191-193); the decoded values do not depend on
+ *                     it, and the row's own bytes here are [8, bytes.length). */
 /*  FORY_FRAME_COLLECTION: the standalone collection encoders — N calls of
  *                     ArrayEncoder / MapEncoder .encode(MemoryBuffer, T)
  *                     (Encoders.arrayEncoder / mapEncoder, Encoders.java:418-431,
@@ -249,6 +258,19 @@ int fory_rowfmt_index_frames(const fory_plan* plan, const void* d_rows, int64_t 
  * (FORY_OK if none). Sets last_error with the reference's message shape. */
 int fory_rowfmt_read_status(const int32_t* d_status, void* stream);
 
+/* --- <= 2 GiB MemoryBuffer windows. A MemoryBuffer is int-sized
+ * (java/fory-core/.../memory/MemoryBuffer.java:87), so a JVM receives a big batch
+ * as several buffers, each holding whole rows/frames. fory_rowfmt_split_windows
+ * splits a batch's output (HOST row_offsets[0..num_rows], or row i at i * stride
+ * when row_offsets is NULL) greedily into windows of at most max_window_bytes
+ * (2^31 - 1 for a MemoryBuffer): window w = rows [first[w], first[w+1]) = bytes
+ * [offsets[first[w]], offsets[first[w+1]]) of the device output, never a row or
+ * frame across a boundary. first has room for max_windows + 1 entries;
+ * *num_windows receives the count. A row larger than a window, or more than
+ * max_windows windows: FORY_ERR_CAPACITY. Host-only (no device work). */
+int fory_rowfmt_split_windows(const int64_t* row_offsets, int64_t stride, int64_t num_rows, int64_t max_window_bytes,
+                              int32_t max_windows, int64_t* first, int32_t* num_windows);
+
 /* --- host path: replaces N x Encoder.encode(MemoryBuffer, T) /
  *     Encoder.decode(MemoryBuffer) over OFF-HEAP host buffers
  *     (Encoders.java:177-225; MemoryBuffer.getUnsafeAddress,
@@ -280,6 +302,15 @@ int fory_rowfmt_host_encode(fory_host_ctx* ctx, const fory_column* host_cols, in
  * hash (FORY_ERR_SCHEMA_MISMATCH: ClassNotCompatibleException). */
 int fory_rowfmt_host_decode(fory_host_ctx* ctx, const void* host_rows, int64_t rows_bytes,
                             int64_t num_rows, int32_t frame_mode, const fory_column* host_out_cols);
+/* Encode into several host windows (e.g. the off-heap addresses of int-sized
+ * MemoryBuffers): window w receives whole rows/frames while they fit
+ * window_caps[w] bytes (greedy, in order; a window too small for the next row stays
+ * empty), then the next window; window_rows / window_bytes (num_windows each,
+ * nullable) receive what each holds. Fixed-width and varlen plans. Not enough room
+ * in all windows: FORY_ERR_CAPACITY before any row is copied. */
+int fory_rowfmt_host_encode_windows(fory_host_ctx* ctx, const fory_column* host_cols, int64_t num_rows,
+                                    int32_t frame_mode, void* const* windows, const int64_t* window_caps,
+                                    int32_t num_windows, int64_t* window_rows, int64_t* window_bytes);
 /* Varlen plans (strings, lists, maps, nested structs; also FORY_FRAME_COLLECTION):
  * the whole batch per call (row sizes are data-dependent, so there are no fixed
  * chunk strides); the context keeps its device buffers and grows them as needed.

@@ -392,7 +392,10 @@ static void write_value(owriter* w, int64_t ordinal, const otree* t, int idx,
 /* ---------------------------------------------------------------------- */
 
 /* Encode N rows. frame_mode 0: rows back to back (BinaryRow.toBytes of each
- * toRow); 1: N calls of Encoder.encode(MemoryBuffer, T) (Encoders.java:213-225).
+ * toRow); 1: N calls of Encoder.encode(MemoryBuffer, T) (Encoders.java:213-225);
+ * 2: N calls of ArrayEncoder / MapEncoder.encode(MemoryBuffer, T); 3: N calls of
+ * Encoder.encode(T) -> byte[] = [i64 schemaHash][row] (Encoders.java:203-210),
+ * concatenated.
  * out is zeroed first. row_offsets (N+1, nullable) receives row/frame starts.
  * Returns total bytes, -1 on capacity overflow, -2 on bad schema. */
 int64_t oracle_encode(const fory_field_desc* d, int n_desc, const fory_column* cols,
@@ -421,14 +424,16 @@ int64_t oracle_encode(const fory_field_desc* d, int n_desc, const fory_column* c
       if (b.overflow == 2) { free_tree(&t); return -2; }
       continue;
     }
-    if (frame_mode) {
+    if (frame_mode == 3) {                            /* encode(T): buffer.writeInt64(schemaHash) */
+      put64(&b, b.wi, (uint64_t)hash); b.wi += 8;
+    } else if (frame_mode) {
       put32(&b, b.wi, 0xFFFFFFFFu); b.wi += 4;        /* writeInt32(-1) */
       put64(&b, b.wi, (uint64_t)hash); b.wi += 8;     /* writeInt64(schemaHash) */
     }
     owriter w;
     row_reset(&w, &b, t.ntop);
     for (int k = 0; k < t.ntop; k++) write_value(&w, k, &t, t.top[k], cols, i);
-    if (frame_mode) put32(&b, frame, (uint32_t)(b.wi - frame - 4)); /* back-patch */
+    if (frame_mode == 1) put32(&b, frame, (uint32_t)(b.wi - frame - 4)); /* back-patch */
     if (b.overflow == 2) { free_tree(&t); return -2; }
   }
   if (row_offsets) row_offsets[nrows] = b.wi;
@@ -621,7 +626,15 @@ int oracle_decode(const fory_field_desc* d, int n_desc, const uint8_t* buf, int6
       else if (D.bad) rc = 5;
       continue;
     }
-    if (frame_mode) {
+    if (frame_mode == 3) {  /* decode(byte[] bytes) = decode(wrap(bytes), bytes.length) (Encoders.java:195-197) */
+      int64_t peer = (int64_t)rd(&D, start, 8);       /* buffer.readInt64() */
+      int64_t end = row_offsets ? row_offsets[i + 1] : start + 8 + fixed;
+      if (D.bad) { rc = 5; break; }
+      if (peer != hash) { rc = 4; break; }            /* ClassNotCompatibleException */
+      if (end - start < 8 + fixed || end > len) { rc = 5; break; }
+      row_at = start + 8;
+      pos = end;
+    } else if (frame_mode) {
       int64_t size = (int32_t)rd(&D, start, 4);       /* buffer.readInt32() */
       int64_t peer = (int64_t)rd(&D, start + 4, 8);   /* buffer.readInt64() */
       if (D.bad) { rc = 5; break; }

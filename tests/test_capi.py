@@ -151,3 +151,27 @@ def test_frame_index_validation_without_gpu():
                                         None, 0, None) == _lib.FORY_ERR_INVALID_ARGUMENT  # misaligned rows
     need = lib.fory_rowfmt_index_workspace_bytes(m.handle, 1 << 24, 8 << 30)
     assert 0 < need < (1 << 24) * 8  # a few bytes per record
+
+
+def test_split_windows_greedy():
+    """fory_rowfmt_split_windows (host-only): whole rows per <= max-byte window, greedy,
+    the way a JNI caller fills int-sized MemoryBuffers (MemoryBuffer.java:87)."""
+    import numpy as np
+    from fury_amd.format.native import split_windows
+    from fury_amd.format.errors import IndexOutOfBoundsException
+    rng = np.random.default_rng(1)
+    sizes = rng.integers(20, 900, size=5000)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    for cap in (900, 1000, 4096, 100000, int(offs[-1]), 1 << 40):
+        first = split_windows(offs, 5000, cap)
+        assert first[0] == 0 and first[-1] == 5000
+        for a, b in zip(first[:-1], first[1:]):
+            assert b > a and offs[b] - offs[a] <= cap
+            if b < 5000:  # greedy: the next row would not fit
+                assert offs[b + 1] - offs[a] > cap
+    # fixed stride
+    first = split_windows(None, 10, 2000, stride=860)
+    assert list(first) == [0, 2, 4, 6, 8, 10]
+    with pytest.raises(IndexOutOfBoundsException):  # a row larger than a window
+        split_windows(offs, 5000, 500)
+    assert list(split_windows(offs, 0, 100)) == [0]

@@ -84,14 +84,14 @@ def check_parity(name, n, frame):
     assert columns_equal(schema, ref, dec2) == []
 
 
-@pytest.mark.parametrize("frame", [0, 1])
+@pytest.mark.parametrize("frame", [0, 1, 3])
 @pytest.mark.parametrize("n", SIZES)
 @pytest.mark.parametrize("name", FIXED)
 def test_encode_decode_parity(name, n, frame):
     check_parity(name, n, frame)
 
 
-@pytest.mark.parametrize("frame", [0, 1])
+@pytest.mark.parametrize("frame", [0, 1, 3])
 @pytest.mark.parametrize("n", SIZES + [5000])
 @pytest.mark.parametrize("name", VARLEN)
 def test_varlen_parity(name, n, frame, varlen_engine):
@@ -134,7 +134,7 @@ def test_varlen_unaligned_buffers(name, shift, varlen_engine):
     dcols = to_device(cols)
     arr = native.column_array(dcols)
     ws = enc.workspace(n)
-    for frame in (0, 1):
+    for frame in (0, 1, 3):
         expect, offs = oracle.encode(schema, cols, n, frame)
         d_offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
         native.encoded_size(enc.plan, arr, n, frame, d_offs, ws)
@@ -211,9 +211,9 @@ def test_struct_large_round_trip_and_sampled_parity():
     enc = encoder_for("struct104")
     vals = W.gen_struct_device(n)
     dcols = [native.DeviceColumn(v, None, None, n) for v in vals]
-    for frame in (0, 1):
+    for frame in (0, 1, 3):
         rows = enc.encode(dcols, n, frame)
-        stride = 848 + 12 * frame
+        stride = 848 + {0: 0, 1: 12, 3: 8}[frame]
         for r0 in (0, 12345, n // 2, n - 70):
             cnt = min(64, n - r0)
             host = W.struct_host_columns(cnt, row0=r0)
@@ -235,3 +235,19 @@ def test_mixed_and_nested_large_round_trip(varlen_engine):
         assert columns_equal(schema, cols, dec) == []
         expect, offs = oracle.encode(schema, cols, n, 1)
         assert np.array_equal(rows.buffer.cpu().numpy(), expect)
+
+
+def test_hashed_frames_schema_mismatch_raises():
+    """Encoder.decode(byte[]) checks the [i64 hash] prefix (Encoders.java:181-190, 195-197)."""
+    for name in ("struct104", "mixed40", "nested"):
+        enc = encoder_for(name)
+        schema, make = catalog()[name]
+        cols = make(200, 1)
+        rows = enc.encode(to_device(cols), 200, 3)
+        bad = rows.buffer.clone()
+        o = 0 if rows.offsets is None else int(rows.offsets[77].item())
+        if rows.offsets is None:
+            o = 77 * rows.stride
+        bad[o + 3] ^= 0x04
+        with pytest.raises(ClassNotCompatibleException):
+            enc.decode(EncodedRows(bad, rows.offsets, 200, 3, rows.stride))
