@@ -255,10 +255,30 @@ __device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* ld
   if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
 }
 
+// XCD-grouped tile order: workgroups are dispatched round-robin over the 8 XCDs
+// (workgroup b on XCD b % 8), so in dispatch order every XCD takes every 8th tile.
+// Within each block of 8*C consecutive logical tiles the C tiles one XCD's
+// workgroups take are made contiguous: each XCD's L2 and write stream see one run
+// of C tiles. In-process A/B at 64Mi Struct104 rows on four boxes
+// (scripts/microbench/fixed_ab.hip, profiles/r02/ab_fixed_*.jsonl), dispatch order
+// vs grouped: encode R64/WG512 19.16 -> 17.85, 18.08 -> 17.29, 18.13 -> 18.95,
+// 17.89 -> 17.80 ms; R64/WG1024 grouped 17.20, 18.12, 17.82 / 17.61 ms (never
+// slower than dispatch order on a box): the product encode. Decode: within
+// +-0.5 %, so it keeps the dispatch order. C = 0: dispatch order. The last partial
+// block keeps the dispatch order.
+__device__ __forceinline__ int64_t map_tile(int64_t t, int64_t tiles, int64_t C) {
+  if (C <= 0) return t;
+  const int64_t blk = t / (8 * C);
+  if ((blk + 1) * 8 * C > tiles) return t;
+  const int64_t b = t - blk * 8 * C;
+  return blk * 8 * C + (b % 8) * C + b / 8;
+}
+
 template <int R, int WG, int K, int HDR>
 __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
                                                                  const FixedFieldDev* __restrict__ fields,
-                                                                 uint8_t* __restrict__ out, int64_t tiles) {
+                                                                 uint8_t* __restrict__ out, int64_t tiles,
+                                                                 int64_t xcd_run) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int NW = WG / 64;
   const int tid = threadIdx.x;
@@ -291,20 +311,23 @@ __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
   if (tid < R) put_header<HDR>(lds + tid * stride, L);  // constant across tiles (no nullable fields)
   u32x4 dA[K], dB[K];
   const int64_t last = tiles - 1;
-  v5_issue<R, K>(ptr, wk, t * R, dA);
-  v5_issue<R, K>(ptr, wk, min(t + (int64_t)gridDim.x, last) * R, dB);
+  // logical tile t -> tile map_tile(t): xcd_run = grid / 8 (each step's grid tiles,
+  // one contiguous run per XCD) or 0
+  auto mt = [&](int64_t x) { return map_tile(x, tiles, xcd_run); };
+  v5_issue<R, K>(ptr, wk, mt(t) * R, dA);
+  v5_issue<R, K>(ptr, wk, mt(min(t + (int64_t)gridDim.x, last)) * R, dB);
   for (;;) {
     v5_write<R, K, HDR>(lds, stride, hdr_bm, wk, sf, dA);
     __syncthreads();
-    v5_store<R, WG>(L, lds, out + t * R * stride, tid);
-    v5_issue<R, K>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dA);
+    v5_store<R, WG>(L, lds, out + mt(t) * R * stride, tid);
+    v5_issue<R, K>(ptr, wk, mt(min(t + 2 * (int64_t)gridDim.x, last)) * R, dA);
     __syncthreads();
     t += gridDim.x;
     if (t >= tiles) break;
     v5_write<R, K, HDR>(lds, stride, hdr_bm, wk, sf, dB);
     __syncthreads();
-    v5_store<R, WG>(L, lds, out + t * R * stride, tid);
-    v5_issue<R, K>(ptr, wk, min(t + 2 * (int64_t)gridDim.x, last) * R, dB);
+    v5_store<R, WG>(L, lds, out + mt(t) * R * stride, tid);
+    v5_issue<R, K>(ptr, wk, mt(min(t + 2 * (int64_t)gridDim.x, last)) * R, dB);
     __syncthreads();
     t += gridDim.x;
     if (t >= tiles) break;
@@ -422,7 +445,7 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane % TR;
   const int fsub = lane / TR;
-  const int64_t r0 = (L.tile0 + (int64_t)blockIdx.x) * TR;
+  const int64_t r0 = (L.tile0 + map_tile((int64_t)blockIdx.x, gridDim.x, L.xcd_run)) * TR;
   const int64_t left = L.num_rows - r0;
   const int rows = left < TR ? (int)left : TR;
   const int stride = L.stride;
@@ -445,9 +468,10 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-// Encode v5: R = 64 records per tile, 512 threads, <= 6 chunk loads per wave per
-// tile (Struct104: 39 load instructions over 8 waves), nt row stores.
-constexpr int kV5R = 64, kV5WG = 512, kV5K = 6;
+// Encode v5: R = 64 records per tile, 1024 threads (two workgroups per CU: LDS),
+// <= 3 chunk loads per wave per tile (Struct104: 39 load instructions over 16
+// waves), nt row stores, XCD-grouped tile order.
+constexpr int kV5R = 64, kV5WG = 1024, kV5K = 3;
 
 template <int HDR>
 hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
@@ -457,7 +481,8 @@ hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
     raise_lds_cap(k);
     const size_t lds = (size_t)kV5R * L.stride;
     const int64_t grid = persistent_grid(k, lds, full, kV5WG);
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kV5WG), lds, s, L, L.fields, out, full);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kV5WG), lds, s, L, L.fields, out, full,
+                       (int64_t)(grid % 8 == 0 ? grid / 8 : 0));
   }
   if (L.num_rows > full * kV5R) {  // tail (< R records): one-tile kernel
     FixedLaunch T = L;

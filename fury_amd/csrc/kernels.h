@@ -29,6 +29,7 @@ struct FixedLaunch {
   int32_t frame;
   int32_t group[5];             // table index where the 8/4/2/1-byte groups start; group[4] = num_fields
   int64_t tile0;                // first tile of this launch (tail launches after a persistent kernel)
+  int64_t xcd_run;              // XCD-grouped tile order: tiles per XCD run (0 = dispatch order)
 };
 
 hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s);
