@@ -19,9 +19,11 @@
 //     no exit changes. Payload bytes that mimic a frame header (hash + plausible
 //     size) can mislead step 1 but not this step.
 //  4. scan of the per-chunk frame counts -> frame index of each chunk's first frame.
-//  5. write (one lane per chunk): re-walk, row_offsets[f] = frame start,
-//     row_offsets[N] = end of frame N-1; a size out of range or fewer than N
-//     frames in rows_bytes -> FORY_ERR_CORRUPT (frames past N are never read).
+//  5. write (one lane per chunk): row_offsets[f] = frame start (the positions
+//     step 1 saved, or a re-walk for chunks the fix-up changed or with more than
+//     kSaved frames), row_offsets[N] = end of frame N-1; a size out of range or
+//     fewer than N frames in rows_bytes -> FORY_ERR_CORRUPT (frames past N are
+//     never read).
 // Schema hashes are checked by the decode kernels that follow (per frame), as in
 // Encoders.decode; the walk itself follows sizes only.
 #include "kcommon.h"
@@ -32,6 +34,10 @@ namespace {
 
 constexpr int64_t kNone = -1;    // chunk holds no candidate frame start
 constexpr int64_t kBroken = -2;  // the chain hit a size out of range
+// Frame starts the spec walk saves per chunk (uint16 offsets from the chunk base,
+// chunk <= 64 KiB), stored position-major (pos[j * chunks + k]) so the write pass
+// reads them coalesced; chunks target ~16 frames.
+constexpr int kSaved = 32;
 
 // Frame header at p (4-byte aligned offset into the stream): size field and hash.
 __device__ __forceinline__ uint32_t frame_size(const uint8_t* rows, int64_t p) {
@@ -46,8 +52,10 @@ __device__ __forceinline__ bool sane_size(uint32_t size, int64_t p, const FrameI
 
 // Walks sizes from p while p < end; returns the first position >= end (or
 // kBroken) and the number of frames started before end.
+// pos (nullable): the first kSaved frame starts, relative to `base`, at pos[j * stride].
 __device__ __forceinline__ int64_t walk(const uint8_t* rows, int64_t p, int64_t end, const FrameIndexLaunch& L,
-                                        int64_t* frames) {
+                                        int64_t* frames, uint16_t* pos = nullptr, int64_t base = 0,
+                                        int64_t stride = 0) {
   int64_t f = 0;
   while (p < end) {
     const uint32_t size = frame_size(rows, p);
@@ -55,6 +63,7 @@ __device__ __forceinline__ int64_t walk(const uint8_t* rows, int64_t p, int64_t 
       *frames = f;
       return kBroken;
     }
+    if (pos && f < kSaved) pos[f * stride] = (uint16_t)(p - base);
     ++f;
     p += 4 + (int64_t)size;
   }
@@ -64,7 +73,8 @@ __device__ __forceinline__ int64_t walk(const uint8_t* rows, int64_t p, int64_t 
 
 __global__ __launch_bounds__(kWG) void frame_spec_kernel(FrameIndexLaunch L, const uint8_t* __restrict__ rows,
                                                          int64_t* __restrict__ start, int64_t* __restrict__ exit_,
-                                                         int64_t* __restrict__ count) {
+                                                         int64_t* __restrict__ count, uint16_t* __restrict__ pos,
+                                                         int32_t* __restrict__ saved) {
   const int64_t k = (int64_t)blockIdx.x * kWG + threadIdx.x;
   if (k >= L.chunks) return;
   const int64_t base = k * L.chunk, end = min(base + L.chunk, L.rows_bytes);
@@ -73,29 +83,29 @@ __global__ __launch_bounds__(kWG) void frame_spec_kernel(FrameIndexLaunch L, con
   if (k == 0) {
     s = 0;
   } else {
-    // 8 positions per step from 10 dwords (the last two carried into the next step)
-    uint32_t d[10];
+    // S positions per step from S + 2 dwords, all loads of a step in flight at once
+    // (the first frame start is on average half a frame into the chunk; S = 32 and
+    // 8-frame chunks were not faster: Mixed index 0.94 / 1.05 ms vs 0.92 ms)
+    constexpr int S = 8;
     const int64_t lim = L.rows_bytes - 12;  // a candidate needs its 12 header bytes
     auto ld = [&](int64_t q) -> uint32_t { return q + 4 <= L.rows_bytes ? frame_size(rows, q) : 0u; };
-    d[0] = ld(base);
-    d[1] = ld(base + 4);
-    for (int64_t p = base; p < end && p <= lim && s == kNone; p += 32) {
+    for (int64_t p = base; p < end && p <= lim && s == kNone; p += 4 * S) {
+      uint32_t d[S + 2];
 #pragma unroll
-      for (int j = 2; j < 10; ++j) d[j] = ld(p + 4 * j);
+      for (int j = 0; j < S + 2; ++j) d[j] = ld(p + 4 * j);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < S; ++j) {
         const int64_t q = p + 4 * j;
         if (s == kNone && q < end && q <= lim && d[j + 1] == hlo && d[j + 2] == hhi && sane_size(d[j], q, L)) s = q;
       }
-      d[0] = d[8];
-      d[1] = d[9];
     }
   }
   int64_t frames = 0, ex = kNone;
-  if (s != kNone) ex = walk(rows, s, end, L, &frames);
+  if (s != kNone) ex = walk(rows, s, end, L, &frames, pos + k, base, L.chunks);
   start[k] = s;
   exit_[k] = ex;
   count[k] = frames;
+  saved[k] = frames <= kSaved ? (int32_t)frames : -1;
 }
 
 // Chunk k's walk is the true chain iff its start is its predecessor's exit.
@@ -117,7 +127,7 @@ __global__ __launch_bounds__(kWG) void frame_check_kernel(FrameIndexLaunch L, co
 // so after sweep i at least the blocks 0..i-1 hold the true chain.
 __global__ __launch_bounds__(1024) void frame_fixup_kernel(FrameIndexLaunch L, const uint8_t* __restrict__ rows,
                                                            int64_t* start, int64_t* exit_, int64_t* count,
-                                                           const int64_t* flag) {
+                                                           int32_t* saved, const int64_t* flag) {
   if (*flag == 0) return;
   __shared__ int changed;
   const int64_t B = (L.chunks + 1023) / 1024;
@@ -146,6 +156,7 @@ __global__ __launch_bounds__(1024) void frame_fixup_kernel(FrameIndexLaunch L, c
           frames != count[k]) {
         start[k] = s;
         count[k] = frames;
+        saved[k] = -1;  // the positions step 1 saved are not this chain's: the write pass re-walks
         __hip_atomic_store(&exit_[k], ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         mine = true;
       }
@@ -161,14 +172,28 @@ __global__ __launch_bounds__(1024) void frame_fixup_kernel(FrameIndexLaunch L, c
 // Chunk k's frames get indices base[k] .. base[k] + count[k] - 1 (count scanned in place).
 __global__ __launch_bounds__(kWG) void frame_write_kernel(FrameIndexLaunch L, const uint8_t* __restrict__ rows,
                                                           const int64_t* __restrict__ start,
+                                                          const int64_t* __restrict__ exit_,
                                                           const int64_t* __restrict__ base,
+                                                          const uint16_t* __restrict__ pos,
+                                                          const int32_t* __restrict__ saved,
                                                           int64_t* __restrict__ offs, int32_t* status) {
   const int64_t k = (int64_t)blockIdx.x * kWG + threadIdx.x;
   if (k == 0 && base[L.chunks] < L.num_rows) set_status(status, FORY_ERR_CORRUPT);  // fewer than N frames
   if (k >= L.chunks) return;
   int64_t p = start[k], f = base[k];
   if (p < 0 || f >= L.num_rows) return;
-  const int64_t end = min((k + 1) * L.chunk, L.rows_bytes);
+  const int64_t cbase = k * L.chunk, end = min(cbase + L.chunk, L.rows_bytes);
+  const int64_t cnt = base[k + 1] - f;
+  if (saved[k] == cnt) {  // the spec walk is the true chain and saved every start
+    for (int64_t j = 0; j < cnt && f < L.num_rows; ++j, ++f) {
+      const int64_t q = cbase + pos[j * L.chunks + k];
+      offs[f] = q;
+      if (f == L.num_rows - 1) offs[L.num_rows] = q + 4 + (int64_t)frame_size(rows, q);
+    }
+    // the chain broke inside this chunk before frame N: Encoders.decode would read past it
+    if (exit_[k] == kBroken && f < L.num_rows) set_status(status, FORY_ERR_CORRUPT);
+    return;
+  }
   while (p < end && f < L.num_rows) {
     const uint32_t size = frame_size(rows, p);
     if (!sane_size(size, p, L)) {  // Encoders.decode would read past the frame: corrupt stream
@@ -186,8 +211,11 @@ __global__ __launch_bounds__(kWG) void frame_write_kernel(FrameIndexLaunch L, co
 
 void frame_index_plan(int64_t num_rows, int64_t rows_bytes, int64_t* chunk, int64_t* chunks) {
   // ~16 frames per chunk at the batch's mean frame size, in [1, 64] KiB
+  // (FORY_ROWFMT_IDXFRAMES overrides the 16, for A/B)
   const int64_t n = num_rows > 0 ? num_rows : 1;
-  int64_t c = (16 * (rows_bytes / n) + 255) / 256 * 256;
+  const char* e = getenv("FORY_ROWFMT_IDXFRAMES");
+  const int64_t per = e ? atoi(e) : 16;
+  int64_t c = (per * (rows_bytes / n) + 255) / 256 * 256;
   c = c < 1024 ? 1024 : (c > 65536 ? 65536 : c);
   *chunk = c;
   *chunks = rows_bytes > 0 ? (rows_bytes + c - 1) / c : 0;
@@ -196,7 +224,8 @@ void frame_index_plan(int64_t num_rows, int64_t rows_bytes, int64_t* chunk, int6
 int64_t frame_index_words(int64_t num_rows, int64_t rows_bytes) {
   int64_t c, k;
   frame_index_plan(num_rows, rows_bytes, &c, &k);
-  return 3 * k + 2 + 2 + scan_partials(k);  // start, exit, count (+ total), flag, scan partials
+  // start, exit, count (+ total), flag, scan partials, saved counts (int32), positions (uint16)
+  return 3 * k + 2 + 2 + scan_partials(k) + (k + 1) / 2 + (kSaved * k + 3) / 4 + 1;
 }
 
 hipError_t launch_frame_index(const FrameIndexLaunch& L0, const uint8_t* rows, int64_t* offs, int64_t* ws,
@@ -213,14 +242,17 @@ hipError_t launch_frame_index(const FrameIndexLaunch& L0, const uint8_t* rows, i
   int64_t* count = exit_ + K;  // K + 1 (scan total)
   int64_t* flag = count + K + 1;
   int64_t* partials = flag + 2;
+  int32_t* saved = reinterpret_cast<int32_t*>(partials + scan_partials(K));
+  uint16_t* pos = reinterpret_cast<uint16_t*>(saved + 2 * ((K + 1) / 2));
   (void)hipMemsetAsync(flag, 0, sizeof(int64_t), s);
   const unsigned blocks = (unsigned)((K + kWG - 1) / kWG);
-  hipLaunchKernelGGL(frame_spec_kernel, dim3(blocks), dim3(kWG), 0, s, L, rows, start, exit_, count);
+  hipLaunchKernelGGL(frame_spec_kernel, dim3(blocks), dim3(kWG), 0, s, L, rows, start, exit_, count, pos, saved);
   hipLaunchKernelGGL(frame_check_kernel, dim3(blocks), dim3(kWG), 0, s, L, start, exit_, flag);
-  hipLaunchKernelGGL(frame_fixup_kernel, dim3(1), dim3(1024), 0, s, L, rows, start, exit_, count, flag);
+  hipLaunchKernelGGL(frame_fixup_kernel, dim3(1), dim3(1024), 0, s, L, rows, start, exit_, count, saved, flag);
   hipError_t e = launch_scan_i64(count, K, partials, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(frame_write_kernel, dim3(blocks), dim3(kWG), 0, s, L, rows, start, count, offs, status);
+  hipLaunchKernelGGL(frame_write_kernel, dim3(blocks), dim3(kWG), 0, s, L, rows, start, exit_, count, pos, saved,
+                     offs, status);
   return hipGetLastError();
 }
 
