@@ -48,6 +48,9 @@ int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 int64_t table_bytes(const Plan& p) {
   // fixed-width: the width-ordered field table
   if (p.fixed_width) return align_up((int64_t)p.top.size() * (int64_t)sizeof(FixedFieldDev));
+  if (p.generic)  // columns, then the node table
+    return align_up((int64_t)p.nodes.size() * (int64_t)sizeof(ColumnDev)) +
+           align_up((int64_t)p.gnodes.size() * (int64_t)sizeof(fory_amd::GNode));
   return align_up((int64_t)p.nodes.size() * (int64_t)sizeof(ColumnDev)) +
          align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::Op)) +
          align_up((int64_t)p.program.size() * (int64_t)sizeof(fory_amd::VarFieldDev)) +
@@ -396,7 +399,55 @@ int32_t* spill_ptr(const Plan& p, void* ws, int64_t n) {
 // Scan partials of the element string/binary columns (after the spill list): the
 // element count is unknown when the workspace is sized, so their offsets are
 // scanned in segments of kScanTile x (words - 1) elements (one segment in practice).
-int64_t elem_partials_words(const Plan& p, int64_t n) { return elem_bytes_cols(p).empty() ? 0 : n / 8 + 8; }
+int64_t elem_partials_words(const Plan& p, int64_t n) {
+  return p.generic || !elem_bytes_cols(p).empty() ? n / 8 + 8 : 0;
+}
+
+bool is_var_kind(int k) {
+  return k == fory_amd::KIND_BYTES || k == fory_amd::KIND_LIST || k == fory_amd::KIND_MAP;
+}
+
+// Tree-engine launch: columns then the node table in the workspace. need_level:
+// var columns of container depth <= need_level must carry offsets (encode: all of
+// them; the decode values pass: all; decode_sizes checks levels itself).
+int prepare_gen(const Plan& p, const fory_column* cols, int64_t n, int frame, void* ws, hipStream_t s,
+                fory_amd::GenLaunch* L, int32_t need_level) {
+  std::vector<ColumnDev> cd(p.nodes.size());
+  for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
+    const fory_amd::Node& nd = p.nodes[idx];
+    const fory_column& c = cols[idx];
+    if (n > 0 && is_var_kind(nd.kind) && p.gnodes[idx].cdepth <= need_level && !c.offsets)
+      return fail(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(idx) + " needs offsets");
+    if (n > 0 && p.gnodes[idx].cdepth == 0 && nd.kind != fory_amd::KIND_STRUCT && !is_var_kind(nd.kind) &&
+        !c.values)
+      return fail(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(idx) + " has no values");
+    ColumnDev d{};
+    d.values = static_cast<const uint8_t*>(c.values);
+    d.offsets = c.offsets;
+    d.validity = nd.nullable ? c.validity : nullptr;
+    d.out_values = static_cast<uint8_t*>(c.values);
+    d.out_offsets = c.offsets;
+    d.out_validity = nd.nullable ? c.validity : nullptr;
+    cd[idx] = d;
+  }
+  const int64_t col_bytes = align_up((int64_t)cd.size() * (int64_t)sizeof(ColumnDev));
+  std::vector<uint8_t> host((size_t)table_bytes(p), 0);
+  std::memcpy(host.data(), cd.data(), cd.size() * sizeof(ColumnDev));
+  std::memcpy(host.data() + col_bytes, p.gnodes.data(), p.gnodes.size() * sizeof(fory_amd::GNode));
+  int rc = upload(ws, host.data(), (int64_t)host.size(), s);
+  if (rc) return rc;
+  L->cols = static_cast<const ColumnDev*>(ws);
+  L->nodes = reinterpret_cast<const fory_amd::GNode*>(static_cast<uint8_t*>(ws) + col_bytes);
+  L->num_nodes = (int32_t)p.gnodes.size();
+  L->bitmap_bytes = p.bitmap_bytes;
+  L->fixed_size = p.fixed_size;
+  L->frame = frame;
+  L->schema_hash = p.schema_hash;
+  L->num_rows = n;
+  L->fill_level = -1;
+  L->max_depth = p.max_depth;
+  return FORY_OK;
+}
 
 int64_t* elem_partials_ptr(const Plan& p, void* ws, int64_t n) {
   return reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(spill_ptr(p, ws, n)) +
@@ -454,7 +505,7 @@ int fory_rowfmt_plan_create(const fory_field_desc* fields, int32_t num_desc, for
     delete plan;
     return fail(rc, "Create encoder failed: " + err);
   }
-  if (!plan->p.fixed_width && plan->p.max_depth > 8) {
+  if (!plan->p.fixed_width && !plan->p.generic && plan->p.max_depth > 8) {
     delete plan;
     return fail(FORY_ERR_UNSUPPORTED, "device path supports struct nesting depth <= 8");
   }
@@ -502,6 +553,15 @@ int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols, int
     e = hipMemsetAsync(d_row_offsets, 0, sizeof(int64_t), s);
     return e == hipSuccess ? FORY_OK : hip_fail(e, "hipMemsetAsync");
   }
+  if (p.generic) {
+    fory_amd::GenLaunch G{};
+    rc = prepare_gen(p, cols, num_rows, frame_mode, d_workspace, s, &G, 1 << 20);
+    if (rc) return rc;
+    e = fory_amd::launch_gen_sizes(G, d_row_offsets, s);
+    if (e != hipSuccess) return hip_fail(e, "gen_sizes");
+    e = fory_amd::launch_scan_i64(d_row_offsets, num_rows, partials_ptr(p, d_workspace), s);
+    return e == hipSuccess ? FORY_OK : hip_fail(e, "scan");
+  }
   fory_amd::VarLaunch L{};
   rc = prepare_var(p, cols, num_rows, frame_mode, d_workspace, s, &L);
   if (rc) return rc;
@@ -542,6 +602,13 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
     return fail(FORY_ERR_UNSUPPORTED, "row too wide for the device path");
   if (!d_row_offsets)
     return fail(FORY_ERR_INVALID_ARGUMENT, "varlen schema: d_row_offsets (from encoded_size) required");
+  if (p.generic) {
+    fory_amd::GenLaunch G{};
+    rc = prepare_gen(p, cols, num_rows, frame_mode, d_workspace, s, &G, 1 << 20);
+    if (rc) return rc;
+    e = fory_amd::launch_gen_encode(G, d_row_offsets, static_cast<uint8_t*>(d_out), out_capacity, d_status, s);
+    return e == hipSuccess ? FORY_OK : hip_fail(e, "gen_encode");
+  }
   fory_amd::VarLaunch L{};
   rc = prepare_var(p, cols, num_rows, frame_mode, d_workspace, s, &L);
   if (rc) return rc;
@@ -571,6 +638,35 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
   if (!d_rows || !d_row_offsets)
     return fail(FORY_ERR_INVALID_ARGUMENT, "varlen schema: d_rows and d_row_offsets required");
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p.generic) {
+    // Container depth 0 (the rows' own strings / lists / maps), then each deeper depth
+    // whose columns the caller has allocated (positions = the totals of the level above).
+    fory_amd::GenLaunch G{};
+    rc = prepare_gen(p, out_cols, num_rows, frame_mode, d_workspace, s, &G, 0);
+    if (rc) return rc;
+    for (int32_t level = 0; level <= p.max_cdepth; ++level) {
+      bool any = false, ready = true;
+      for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
+        if (!is_var_kind(p.nodes[idx].kind) || p.gnodes[idx].cdepth != level) continue;
+        any = true;
+        if (!out_cols[idx].offsets || out_cols[idx].length < 0) ready = false;
+      }
+      if (!any || !ready) break;
+      G.fill_level = level;
+      hipError_t e = fory_amd::launch_gen_decode(G, static_cast<const uint8_t*>(d_rows), d_row_offsets, d_status, s);
+      if (e != hipSuccess) return hip_fail(e, "gen_decode (lengths)");
+      for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
+        if (!is_var_kind(p.nodes[idx].kind) || p.gnodes[idx].cdepth != level) continue;
+        e = level == 0 ? fory_amd::launch_scan_offsets_i32(out_cols[idx].offsets, num_rows,
+                                                           partials_ptr(p, d_workspace), d_status, s)
+                       : fory_amd::launch_scan_offsets_i32_segmented(
+                             out_cols[idx].offsets, out_cols[idx].length, elem_partials_ptr(p, d_workspace, num_rows),
+                             elem_partials_words(p, num_rows), d_status, s);
+        if (e != hipSuccess) return hip_fail(e, "scan offsets");
+      }
+    }
+    return FORY_OK;
+  }
   fory_amd::VarLaunch L{};
   rc = prepare_var(p, out_cols, num_rows, frame_mode, d_workspace, s, &L, true);
   if (rc) return rc;
@@ -638,6 +734,13 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows, const int64_t*
   if (p.fixed_width) return fail(FORY_ERR_UNSUPPORTED, "row too wide for the device path");
   if (!d_row_offsets)
     return fail(FORY_ERR_INVALID_ARGUMENT, "varlen schema: d_row_offsets required");
+  if (p.generic) {
+    fory_amd::GenLaunch G{};
+    rc = prepare_gen(p, out_cols, num_rows, frame_mode, d_workspace, s, &G, 1 << 20);
+    if (rc) return rc;
+    e = fory_amd::launch_gen_decode(G, static_cast<const uint8_t*>(d_rows), d_row_offsets, d_status, s);
+    return e == hipSuccess ? FORY_OK : hip_fail(e, "gen_decode");
+  }
   fory_amd::VarLaunch L{};
   rc = prepare_var(p, out_cols, num_rows, frame_mode, d_workspace, s, &L);
   if (rc) return rc;

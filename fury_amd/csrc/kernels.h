@@ -104,6 +104,25 @@ hipError_t launch_scan_offsets_i32(int32_t* offs, int64_t n, int64_t* partials,
 hipError_t launch_scan_offsets_i32_segmented(int32_t* offs, int64_t n, int64_t* partials, int64_t partial_words,
                                              int32_t* status, hipStream_t s);
 
+// Tree engine (generic.hip): any nesting, one lane per record.
+struct GenLaunch {
+  const GNode* nodes;      // device, pre-order (index = column index)
+  const ColumnDev* cols;   // device
+  int32_t num_nodes;
+  int32_t bitmap_bytes;
+  int32_t fixed_size;
+  int32_t frame;
+  int64_t schema_hash;
+  int64_t num_rows;
+  int32_t fill_level;      // decode: lengths pass of container depth L (>= 0), or -1 = values
+  int32_t max_depth;       // schema depth (Plan::max_depth): frames per lane
+};
+hipError_t launch_gen_sizes(const GenLaunch& L, int64_t* sizes, hipStream_t s);
+hipError_t launch_gen_encode(const GenLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity,
+                             int32_t* status, hipStream_t s);
+hipError_t launch_gen_decode(const GenLaunch& L, const uint8_t* rows, const int64_t* offs, int32_t* status,
+                             hipStream_t s);
+
 // Frame index of a STREAM batch (frames.hip): the starts of the first num_rows
 // frames of rows_bytes bytes, found on the device from the stream alone.
 struct FrameIndexLaunch {

@@ -210,6 +210,29 @@ static int compile_field(const Plan& p, int32_t idx, int32_t ordinal, std::vecto
   return FORY_ERR_ENCODER;
 }
 
+// Pre-order node table of the tree engine: subtree ends and container depths.
+static int32_t fill_gnode(Plan* p, int32_t idx, int32_t cdepth) {
+  const Node& nd = p->nodes[idx];
+  GNode& g = p->gnodes[idx];
+  g.kind = nd.kind;
+  g.width = nd.width;
+  g.flags = nd.nullable ? 1 : 0;
+  g.nchild = (int32_t)nd.children.size();
+  g.cdepth = cdepth;
+  if (cdepth > p->max_cdepth) p->max_cdepth = cdepth;
+  const int32_t inner = cdepth + (nd.kind == KIND_LIST || nd.kind == KIND_MAP ? 1 : 0);
+  int32_t end = idx + 1;
+  for (int32_t ch : nd.children) end = fill_gnode(p, ch, inner);
+  p->gnodes[idx].end = end;
+  return end;
+}
+
+static void build_gnodes(Plan* p) {
+  p->gnodes.assign(p->nodes.size(), GNode{});
+  p->max_cdepth = 0;
+  for (int32_t t : p->top) fill_gnode(p, t, 0);
+}
+
 int build_plan(const fory_field_desc* fields, int32_t num_desc, Plan* p, std::string* err) {
   if (num_desc < 0 || (num_desc > 0 && fields == nullptr)) {
     *err = "fields is null or num_desc < 0";
@@ -237,11 +260,26 @@ int build_plan(const fory_field_desc* fields, int32_t num_desc, Plan* p, std::st
     if (k != KIND_FIXED && k != KIND_BOOL) p->fixed_width = false;
   }
   p->program.clear();
+  build_gnodes(p);
+  p->generic = false;
   if (!p->fixed_width) {
     for (size_t k = 0; k < p->top.size(); ++k) {
       int rc = compile_field(*p, p->top[k], (int32_t)k, &p->program, err);
+      if (rc == FORY_ERR_UNSUPPORTED) {  // a nesting the op programs do not cover: tree engine
+        p->generic = true;
+        p->program.clear();
+        err->clear();
+        break;
+      }
       if (rc) return rc;
     }
+  }
+  if (p->generic) {  // the checks compile_field made on the way (map keys) for every map
+    for (const Node& nd : p->nodes)
+      if (nd.kind == KIND_MAP && p->nodes[nd.children[0]].nullable) {
+        *err = "Map's keys must be non-nullable";  // DataTypes.mapField (DataTypes.java:419)
+        return FORY_ERR_ENCODER;
+      }
   }
   return FORY_OK;
 }

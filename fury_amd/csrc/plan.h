@@ -108,6 +108,17 @@ struct ColumnDev {  // per-column device view (bound per call)
   uint8_t* out_validity;
 };
 
+// Schema tree node of the tree engine (generic.hip), one per pre-order
+// descriptor: a node's children follow it, its subtree ends at `end`.
+struct GNode {
+  int32_t kind;    // FieldKind
+  int32_t width;   // 1/2/4/8 for fixed width, else -1
+  int32_t flags;   // bit0 nullable
+  int32_t end;     // index after the subtree
+  int32_t nchild;
+  int32_t cdepth;  // list / map ancestors: the decode lengths pass that sizes this column
+};
+
 struct Node {
   int32_t type_id = 0;
   int32_t nullable = 0;
@@ -127,6 +138,11 @@ struct Plan {
   bool any_nullable = false;
   std::vector<Op> program;        // varlen plans
   int32_t max_depth = 0;
+  // Nestings the op programs do not cover (list<list<...>>, List<Bean> with var
+  // fields, maps of structs / lists) run on the tree engine over `gnodes`.
+  bool generic = false;
+  std::vector<GNode> gnodes;
+  int32_t max_cdepth = 0;
 };
 
 // Returns FORY_OK or an error code, with a message in `err`.

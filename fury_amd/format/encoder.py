@@ -134,67 +134,49 @@ class RowEncoder:
             native.decode(p, buf, None, num_rows, frame_mode, native.column_array(cols), status, ws)
             native.read_status(status)
             return cols
-        # varlen: offsets/validity/row-level values first, then sizes, then items/bytes
+        # varlen: columns are sized level by level. Level L = the columns under L
+        # lists / maps; their positions are the element totals of the level above.
+        # decode_sizes fills the Arrow offsets of every level whose columns are
+        # allocated; each round allocates the next level from the totals.
         n = num_rows
         fields = p.fields
-        cols = [DeviceColumn(length=n) for _ in fields]
-        # element columns sized after decode_sizes: list item subtrees (a list of structs:
-        # the struct and its fields), map keys + values
-        item_of = {}
-        sub = {}  # list/map column -> its element columns (pre-order)
-        for i, f in enumerate(fields):
-            if f.type.id in (ArrowType.LIST, ArrowType.MAP):
-                size = sum(_subtree_size(c) for c in f.children)
-                sub[i] = list(range(i + 1, i + 1 + size))
-                for k in sub[i]:
-                    item_of[k] = i
-        for i, f in enumerate(fields):
-            if i in item_of:
-                continue  # sized after decode_sizes
-            t = f.type.id
-            if t in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP):
-                cols[i].offsets = torch.zeros(n + 1, dtype=torch.int32, device=self.device)
-            elif t != ArrowType.STRUCT:
-                cols[i].values = torch.empty(max(1, n), dtype=_torch_dtype(t), device=self.device)
-            if f.nullable:
-                cols[i].validity = torch.zeros(_validity_bytes(n), dtype=torch.uint8, device=self.device)
+        container, cdepth = _containers(p.schema)
+        cols = [DeviceColumn(length=0) for _ in fields]
+        var_kinds = (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP)
+        totals = {}
+
+        def alloc(level):
+            for i, f in enumerate(fields):
+                if cdepth[i] != level:
+                    continue
+                npos = n if container[i] < 0 else int(totals[container[i]])
+                c = DeviceColumn(length=npos)
+                t = f.type.id
+                if t in var_kinds:
+                    c.offsets = torch.zeros(npos + 1, dtype=torch.int32, device=self.device)
+                elif t != ArrowType.STRUCT:
+                    c.values = torch.empty(max(1, npos), dtype=_torch_dtype(t), device=self.device)
+                if f.nullable:
+                    c.validity = torch.zeros(_validity_bytes(npos), dtype=torch.uint8, device=self.device)
+                cols[i] = c
+
         if offsets is None:
             if frame_mode != FRAME_STREAM:
                 raise ValueError("raw rows / collection frames are not self-delimiting: row offsets are required")
             offsets = self.index_frames(buf, n)
-        native.decode_sizes(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
-        var_idx = [i for i, f in enumerate(fields) if i not in item_of and
-                   f.type.id in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP)]
-        totals = {}
-        if var_idx and n > 0:
-            last = torch.stack([cols[i].offsets[n] for i in var_idx]).cpu().tolist()
-            totals = dict(zip(var_idx, last))
-        native.read_status(status)
-        elem_bytes = []  # string/binary list elements / map keys+values: sized by a second pass
-        for i in var_idx:
-            tot = int(totals.get(i, 0))
-            f = fields[i]
-            if f.type.id in (ArrowType.LIST, ArrowType.MAP):
-                for k in sub[i]:
-                    it = fields[k]
-                    vals, offs = None, None
-                    if it.type.id in (ArrowType.STRING, ArrowType.BINARY):
-                        offs = torch.zeros(tot + 1, dtype=torch.int32, device=self.device)
-                        elem_bytes.append(k)
-                    elif it.type.id != ArrowType.STRUCT:
-                        vals = torch.empty(max(1, tot), dtype=_torch_dtype(it.type.id), device=self.device)
-                    cols[k] = DeviceColumn(
-                        vals, offs,
-                        torch.zeros(_validity_bytes(tot), dtype=torch.uint8, device=self.device)
-                        if it.nullable else None, tot)
-            else:
-                cols[i].values = torch.empty(max(1, tot), dtype=torch.uint8, device=self.device)
-        if elem_bytes:
+        alloc(0)
+        for level in range(max(cdepth) + 1):
+            var_idx = [i for i, f in enumerate(fields) if cdepth[i] == level and f.type.id in var_kinds]
+            if not var_idx:
+                break
             native.decode_sizes(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
-            last = torch.stack([cols[k].offsets[cols[k].length] for k in elem_bytes]).cpu().tolist()
+            last = torch.stack([cols[i].offsets[cols[i].length] for i in var_idx]).cpu().tolist()
             native.read_status(status)
-            for k, tot in zip(elem_bytes, last):
-                cols[k].values = torch.empty(max(1, int(tot)), dtype=torch.uint8, device=self.device)
+            totals.update(zip(var_idx, last))
+            for i in var_idx:  # string / binary bytes of this level
+                if fields[i].type.id in (ArrowType.STRING, ArrowType.BINARY):
+                    cols[i].values = torch.empty(max(1, int(totals[i])), dtype=torch.uint8, device=self.device)
+            alloc(level + 1)
         native.decode(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
         native.read_status(status)
         return cols
@@ -219,6 +201,24 @@ class RowEncoder:
 
 def _subtree_size(f) -> int:
     return 1 + sum(_subtree_size(c) for c in f.children)
+
+
+def _containers(schema):
+    """Per pre-order column: the nearest list / map ancestor (-1: none) and the
+    number of list / map ancestors (the decode_sizes level that positions it)."""
+    container, cdepth = [], []
+
+    def walk(f, anc, depth):
+        container.append(anc)
+        cdepth.append(depth)
+        me = len(container) - 1
+        inner = f.type.id in (ArrowType.LIST, ArrowType.MAP)
+        for c in f.children:
+            walk(c, me if inner else anc, depth + (1 if inner else 0))
+
+    for f in schema.fields:
+        walk(f, -1, 0)
+    return container, cdepth
 
 
 def _validity_bytes(n: int) -> int:

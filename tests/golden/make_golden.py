@@ -7,7 +7,10 @@ which needs the unbuilt Cython extension) and records:
   - compute_schema_hash (infer.py:160-190) of the S / M / N schemas and of a
     few edge schemas, built as pyarrow schemas mirroring the Java inferred
     schemas (pyarrow type ids == Java ArrowType ordinals, ArrowType.java:25-160);
-  - the field order infer_schema produces for the benchmark Struct (infer.py:94-106).
+  - the field order infer_schema produces for the benchmark Struct (infer.py:94-106);
+  - infer_schema's type trees (names, type ids, nullability, children) of Python
+    classes mirroring the Mixed / Nested / RowEncoderTest.Foo, Bar / collection
+    beans (infer.py:94-145).
 No reference source is copied; only the resulting numbers are committed.
 
 Usage: python tests/golden/make_golden.py [/root/reference]
@@ -111,6 +114,43 @@ def main():
     inferred = infer.infer_schema(cls)
     out["struct104_field_order"] = [f.name for f in inferred]
     out["struct104_inferred_hash"] = int(infer.compute_schema_hash(inferred))
+
+    # infer_schema type trees of Python classes mirroring the configs' Java beans:
+    # field names (sorted), type ids and children, recursively (infer.py:94-106,
+    # ArrowTypeVisitor :109-145). The reference's Python marks every field
+    # nullable (pa.field default); Java's TypeInference makes primitives not-null
+    # (TypeInference.java:164-181) — nullability is recorded as produced.
+    import typing
+
+    def tree(field):
+        t = field.type
+        kids = []
+        if isinstance(t, pa.ListType):
+            kids = [tree(t.value_field)]
+        elif isinstance(t, pa.StructType):
+            kids = [tree(t.field(i)) for i in range(t.num_fields)]
+        elif isinstance(t, pa.MapType):
+            kids = [tree(t.key_field), tree(t.item_field)]
+        return {"name": field.name, "type_id": int(t.id), "nullable": bool(field.nullable), "children": kids}
+
+    def cls(name, ann):
+        return type(name, (), {"__annotations__": ann, "__module__": "golden"})
+
+    pa_of = {ArrowType.INT32: pa.int32, ArrowType.INT64: pa.int64, ArrowType.DOUBLE: pa.float64,
+             ArrowType.STRING: str}
+    mixed = cls("Mixed", {n: pa_of[k] for n, k in W.mixed_decl()})
+    inner = cls("Inner", {"x": pa.int32, "y": pa.int64, "z": typing.List[pa.int64]})
+    nested = cls("Nested", {"a": pa.int64, "b": pa.float64, "c": inner})
+    bar = cls("Bar", {"f1": pa.int32, "f2": str})
+    foo = cls("Foo", {"f1": pa.int32, "f2": str, "f3": typing.List[str], "f4": typing.Dict[str, pa.int32],
+                      "f5": bar})
+    colls = cls("Colls", {"double2d": typing.List[typing.List[pa.float64]], "bars": typing.List[bar],
+                          "bar_map": typing.Dict[str, bar], "nest": typing.List[typing.List[typing.List[bar]]],
+                          "counts": typing.Dict[pa.int32, pa.int64], "blobs": typing.List[bytes]})
+    out["inferred"] = {}
+    for name, c in (("mixed40", mixed), ("nested", nested), ("bar", bar), ("foo", foo), ("collections", colls)):
+        sch = infer.infer_schema(c)
+        out["inferred"][name] = {"fields": [tree(f) for f in sch], "hash": int(infer.compute_schema_hash(sch))}
 
     path = os.path.join(HERE, "schema_hashes.json")
     with open(path, "w") as fh:

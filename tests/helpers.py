@@ -404,3 +404,98 @@ def collection_cases(n=300, seed=5):
         rows = [{key: empty if r[key] is None else r[key]} for r in string_elems_rows(n, seed)]
         out.append((schema, build_columns(schema, rows)))
     return out
+
+
+# --- nested collections (the tree engine's shapes) -----------------------------------
+# Mirrors of the reference's test beans, inferred like Encoders.bean does
+# (TypeInference.java:141-254): RowEncoderTest.Foo / Bar (RowEncoderTest.java:66-95),
+# BeanA / BeanB (fory-test-core .../bean/BeanA.java:34-53, BeanB.java:29-36) without
+# BeanA.f16 (BigDecimal: no device decimal) and the transient f13. Java arrays are
+# lists of not-null elements (int[] -> list<int32>, byte[] -> list<int8>,
+# Iterable<BeanB> -> list<struct>).
+def reference_beans():
+    from typing import Dict, List as L
+    from fury_amd.format import infer as I
+    bar = type("Bar", (), {"__annotations__": {"f1": I.jint, "f2": I.String}})
+    foo = type("Foo", (), {"__annotations__": {"f1": I.jint, "f2": I.String, "f3": L[I.String],
+                                               "f4": Dict[I.String, I.Integer], "f5": bar}})
+    bean_b = type("BeanB", (), {"__annotations__": {
+        "f1": I.jshort, "f2": I.Integer, "f3": I.jlong, "f4": I.Float, "f5": I.jdouble,
+        "intArr": L[I.jint], "intList": L[I.Integer]}})
+    bean_a = type("BeanA", (), {"__annotations__": {
+        "f1": I.jshort, "f2": I.Integer, "f3": I.jlong, "f4": I.Float, "f5": I.jdouble, "beanB": bean_b,
+        "intArray": L[I.jint], "bytes": L[I.jbyte], "f12": I.jboolean, "f15": I.Integer, "f17": I.String,
+        "longStringField": I.String, "doubleList": L[I.Double], "beanBIterable": L[bean_b],
+        "beanBList": L[bean_b], "stringBeanBMap": Dict[I.String, bean_b], "int2DArray": L[L[I.jint]],
+        "double2DList": L[L[I.Double]]}})
+    return {"Bar": bar, "Foo": foo, "BeanA": bean_a, "BeanB": bean_b}
+
+
+def nested_schemas():
+    """name -> schema of nestings the op programs do not cover (plus Foo, which they do)."""
+    from typing import Dict, List as L
+    from fury_amd.format import infer as I
+    B = reference_beans()
+    bar, foo = B["Bar"], B["Foo"]
+    holder = type("Holder", (), {"__annotations__": {
+        "id": I.jlong, "bars": L[bar], "barMap": Dict[I.String, bar], "tag": I.String}})
+    lists = type("Lists", (), {"__annotations__": {
+        "longs2d": L[L[I.Long]], "names2d": L[L[I.String]], "shorts3d": L[L[L[I.jshort]]], "x": I.jint}})
+    maps = type("Maps", (), {"__annotations__": {
+        "fooBars": Dict[foo, L[bar]], "nest": Dict[I.String, L[L[bar]]], "ints": Dict[I.String, L[I.Integer]],
+        "k": I.Byte}})
+    deep = DataTypes.array_field("deep", DataTypes.map_field(
+        "item", Field("key", DataType(ArrowType.STRING), False),
+        DataTypes.array_field("value", DataTypes.struct_field("item", True, [
+            Field("s", DataType(ArrowType.STRING), True),
+            DataTypes.array_field("l", DataTypes.array_field("item", Field("item", DataType(ArrowType.INT16), True))),
+            Field("b", DataType(ArrowType.BOOL), False)]))))
+    chain = Field("item", DataType(ArrowType.INT32), True)
+    for k in range(9):  # list^9<int32>: 10 schema levels (the 18-frame instantiation)
+        chain = DataTypes.array_field("item" if k < 8 else "chain", chain)
+    return {
+        "holder": I.infer_schema(holder),
+        "lists": I.infer_schema(lists),
+        "maps_nested": I.infer_schema(maps),
+        "foo": I.infer_schema(foo),
+        "bean_a": I.infer_schema(B["BeanA"]),
+        "deep": Schema([Field("id", DataType(ArrowType.INT32), False), deep]),
+        "chain": Schema([chain, Field("z", DataType(ArrowType.INT64), True)]),
+    }
+
+
+def random_value(f: Field, rng, depth: int = 0, null_p: float = 0.12):
+    """A random Python value of field f (None for nulls): containers hold 0-4 elements,
+    one in twelve near the top holds up to 70 (element bitmaps beyond one word)."""
+    if f.nullable and rng.random() < null_p:
+        return None
+    t = f.type.id
+    if t == ArrowType.STRUCT:
+        return {c.name: random_value(c, rng, depth + 1, null_p) for c in f.children}
+    if t in (ArrowType.LIST, ArrowType.MAP):
+        k = int(rng.integers(0, 70)) if depth < 2 and rng.random() < 1 / 12 else int(rng.integers(0, 5))
+        if t == ArrowType.LIST:
+            return [random_value(f.children[0], rng, depth + 1, null_p) for _ in range(k)]
+        return [(random_value(f.children[0], rng, depth + 1, null_p), random_value(f.children[1], rng, depth + 1, null_p))
+                for _ in range(k)]
+    if t == ArrowType.STRING:
+        alphabet = "abcdefghij0123456789 éü中文😀"
+        return "".join(alphabet[int(x)] for x in rng.integers(0, len(alphabet), size=rng.integers(0, 24)))
+    if t == ArrowType.BINARY:
+        return bytes(rng.integers(0, 256, size=rng.integers(0, 24), dtype=np.uint8))
+    if t == ArrowType.BOOL:
+        return bool(rng.random() < 0.5)
+    if t in (ArrowType.FLOAT, ArrowType.DOUBLE):
+        return float(np.float32(rng.standard_normal())) if t == ArrowType.FLOAT else float(rng.standard_normal())
+    bits = {ArrowType.INT8: 8, ArrowType.INT16: 16, ArrowType.INT32: 32, ArrowType.DATE32: 32}.get(t, 64)
+    return int(rng.integers(-2 ** (bits - 1), 2 ** (bits - 1) - 1, dtype=np.int64))
+
+
+def random_rows(schema: Schema, n: int, seed: int, null_p: float = 0.12):
+    rng = np.random.default_rng(seed)
+    return [{f.name: random_value(f, rng, 0, null_p) for f in schema.fields} for _ in range(n)]
+
+
+def nested_columns(name: str, n: int, seed: int):
+    schema = nested_schemas()[name]
+    return schema, build_columns(schema, random_rows(schema, n, seed))

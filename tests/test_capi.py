@@ -69,23 +69,25 @@ def test_plan_errors():
         NativePlan(bad_nested)
     with pytest.raises(errors.EncoderException):  # a map needs [key, value] children
         NativePlan(Schema([Field("m", DataType(ArrowType.MAP), True)]))
-    # device path: map keys/values of fixed width, string or binary
+    # every nesting has a device path (op programs, or the tree engine for
+    # Map<K, Bean>, list<list<...>>, List<Bean with var fields>)
     NativePlan(Schema([DataTypes.map_field("m", Field("key", DataType(ArrowType.STRING), False),
                                            Field("value", DataType(ArrowType.INT32), True))]))
-    with pytest.raises(errors.UnsupportedOperationException):
-        NativePlan(Schema([DataTypes.map_field("m", Field("key", DataType(ArrowType.STRING), False),
-                                               DataTypes.struct_field("value", True, [
-                                                   Field("a", DataType(ArrowType.INT32))]))]))
+    NativePlan(Schema([DataTypes.map_field("m", Field("key", DataType(ArrowType.STRING), False),
+                                           DataTypes.struct_field("value", True, [
+                                               Field("a", DataType(ArrowType.INT32))]))]))
     with pytest.raises(errors.EncoderException):  # Map's keys must be non-nullable (DataTypes.java:419)
         NativePlan(Schema([Field("m", DataType(ArrowType.MAP), True, [Field("key", DataType(ArrowType.INT32), True),
                                                                        Field("value", DataType(ArrowType.INT32))])]))
+    with pytest.raises(errors.EncoderException):  # ... also behind a nesting the tree engine takes
+        NativePlan(Schema([DataTypes.array_field("l", DataTypes.array_field("item", Field("item", DataType(ArrowType.INT32)))),
+                           Field("m", DataType(ArrowType.MAP), True, [Field("key", DataType(ArrowType.INT32), True),
+                                                                       Field("value", DataType(ArrowType.INT32))])]))
     NativePlan(Schema([DataTypes.array_field("l", Field("item", DataType(ArrowType.STRING)))]))
-    with pytest.raises(errors.UnsupportedOperationException):  # device path: no list<list<...>> yet
-        NativePlan(Schema([DataTypes.array_field("l", DataTypes.array_field(
-            "item", Field("item", DataType(ArrowType.INT32))))]))
-    with pytest.raises(errors.UnsupportedOperationException):  # List<Bean> of fixed-width fields only
-        NativePlan(Schema([DataTypes.array_field("l", DataTypes.struct_field(
-            "item", True, [Field("s", DataType(ArrowType.STRING))]))]))
+    NativePlan(Schema([DataTypes.array_field("l", DataTypes.array_field(
+        "item", Field("item", DataType(ArrowType.INT32))))]))
+    NativePlan(Schema([DataTypes.array_field("l", DataTypes.struct_field(
+        "item", True, [Field("s", DataType(ArrowType.STRING))]))]))
     # truncated descriptor: a struct promising 2 children with only 1 present
     desc, n = flatten(Schema([DataTypes.struct_field("s", True, [Field("a", DataType(ArrowType.INT32))])]))
     desc[0].num_children = 2

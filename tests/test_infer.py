@@ -134,3 +134,60 @@ def test_infer_list_of_beans(golden):
     lst = schema.fields[1]
     assert lst.type.id == ArrowType.LIST and lst.children[0].type.id == ArrowType.STRUCT
     assert NativePlan(schema).schema_hash == golden["schema_hash"]["list_struct"]
+
+
+# --- type trees against the reference's Python infer_schema (tests/golden) ----------
+def _java_classes():
+    """Java-typed mirrors of the golden classes (primitives where the Java beans have them:
+    Mixed / Nested fields, RowEncoderTest.Bar.f1 / Foo.f1 are int/long/double)."""
+    from typing import Dict
+    kinds = {ArrowType.INT32: I.jint, ArrowType.INT64: I.jlong, ArrowType.DOUBLE: I.jdouble,
+             ArrowType.STRING: I.String}
+    mixed = type("Mixed", (), {"__annotations__": {n: kinds[k] for n, k in W.mixed_decl()}})
+    inner = type("Inner", (), {"__annotations__": {"x": I.jint, "y": I.jlong, "z": List[I.Long]}})
+    nested = type("Nested", (), {"__annotations__": {"a": I.jlong, "b": I.jdouble, "c": inner}})
+    bar = type("Bar", (), {"__annotations__": {"f1": I.jint, "f2": I.String}})
+    foo = type("Foo", (), {"__annotations__": {"f1": I.jint, "f2": I.String, "f3": List[I.String],
+                                               "f4": Dict[I.String, I.Integer], "f5": bar}})
+    colls = type("Colls", (), {"__annotations__": {
+        "double2d": List[List[I.Double]], "bars": List[bar], "bar_map": Dict[I.String, bar],
+        "nest": List[List[List[bar]]], "counts": Dict[I.Integer, I.Long], "blobs": List[I.Binary]}})
+    return {"mixed40": mixed, "nested": nested, "bar": bar, "foo": foo, "collections": colls}
+
+
+def _tree(f):
+    return {"name": f.name, "type_id": int(f.type.id), "nullable": bool(f.nullable),
+            "children": [_tree(c) for c in f.children]}
+
+
+def _strip_nullable(t, primitive_ids):
+    """The reference Python marks every field nullable; Java primitives are not-null
+    (TypeInference.java:164-181): compare nullability only for non-primitive fields."""
+    out = dict(t)
+    if t["type_id"] in primitive_ids and not t["nullable"]:
+        out["nullable"] = None
+    out["children"] = [_strip_nullable(c, primitive_ids) for c in t["children"]]
+    return out
+
+
+@pytest.mark.parametrize("name", ["mixed40", "nested", "bar", "foo", "collections"])
+def test_type_trees_match_reference_infer_schema(golden, name):
+    from fury_amd.format.native import NativePlan
+    want = golden["inferred"][name]
+    s = I.infer_schema(_java_classes()[name])
+    got = [_tree(f) for f in s]
+    prim = {ArrowType.BOOL, ArrowType.INT8, ArrowType.INT16, ArrowType.INT32, ArrowType.INT64,
+            ArrowType.FLOAT, ArrowType.DOUBLE}
+    g = [_strip_nullable(t, prim) for t in got]
+
+    def relax(w, gg):  # where ours is a not-null primitive, accept the reference's nullable=True
+        return {**w, "nullable": gg["nullable"] if gg["nullable"] is None else w["nullable"],
+                "children": [relax(a, b) for a, b in zip(w["children"], gg["children"])]}
+
+    assert [relax(w, x) for w, x in zip(want["fields"], g)] == g
+    from oracle import oracle
+    assert oracle.schema_hash(s) == want["hash"]
+    assert NativePlan(s).schema_hash == want["hash"]
+    if name in ("mixed40", "nested"):  # the bench's hand-built schemas are the inferred ones
+        ref = W.mixed_schema() if name == "mixed40" else W.nested_schema()
+        assert [_tree(f) for f in ref] == got
