@@ -33,7 +33,19 @@ $(ORACLE): oracle/rowfmt_oracle.c include/fory_rowfmt.h
 	@mkdir -p oracle/_build
 	gcc -O2 -std=c11 -Wall -Wextra -fPIC -shared -o $@ $<
 
+# The oracle under AddressSanitizer + UBSan (host code only), driven by the CPU tests
+# that exercise it: `make asan`.
+ORACLE_ASAN := oracle/_build/liboracle_asan.so
+$(ORACLE_ASAN): oracle/rowfmt_oracle.c include/fory_rowfmt.h
+	@mkdir -p oracle/_build
+	gcc -O1 -g -std=c11 -Wall -fsanitize=address,undefined -fno-sanitize-recover=undefined \
+	  -fno-omit-frame-pointer -fPIC -shared -o $@ $<
+
+asan: $(ORACLE_ASAN)
+	ORACLE_LIB=$(abspath $(ORACLE_ASAN)) LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $$(gcc -print-file-name=libubsan.so)" \
+	  ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 python -m pytest tests/test_oracle_golden.py tests/test_infer.py -q -p no:cacheprovider
+
 clean:
 	rm -rf fury_amd/lib oracle/_build $(CAPI_TEST)
 
-.PHONY: all clean
+.PHONY: all clean asan

@@ -23,7 +23,8 @@ def short(name):
     m = re.search(r"(encode_fixed_\w*?kernel|decode_fixed_\w*?kernel|var_encode_kernel|var_decode_kernelILb[01]|"
                   r"var_encode_tile_kernel|var_decode_tile_kernelILb[01]|var_encode_flat_lean_kernel|var_encode_flat_kernel|"
                   r"var_decode_flat_kernel|"
-                  r"var_sizes_kernel|scan_\w+?_kernel|fill_offsets_kernel)", name)
+                  r"var_sizes_kernel|scan_\w+?_kernel|fill_offsets_kernel|frame_\w+?_kernel|flat_tile_bases_kernel|"
+                  r"gen_\w+?_kernel)", name)
     if m:
         k = m.group(1)
         t = re.search(r"var_(?:en|de)code_flat_(?:lean_)?kernel<([^>]*)>", name)
@@ -34,8 +35,8 @@ def short(name):
             return k
         if k.startswith("var_decode") and not k.endswith(("0", "1")):
             if k == "var_decode_flat_kernel":
-                k += "<pass2>" if re.search(r"<(true|false), true", name) or "ILb1ELb1E" in name or "ILb0ELb1E" in name \
-                    else "<pass1>"
+                m2 = re.search(r"var_decode_flat_kernel<(\d+|true|false), (true|false)", name)
+                k += "<pass2>" if (m2 and m2.group(2) == "true") else "<pass1>"
             else:
                 k += "ILb1" if "<true>" in name else ("ILb0" if "<false>" in name else "")
         return k
@@ -43,7 +44,8 @@ def short(name):
 
 
 out = {"kernels": {}, "pmc": {}}
-stats = list(rows("trace/**/*kernel_stats.csv"))
+stats = [r for f in glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True)
+         if "pmc_" not in os.path.relpath(f, root) for r in csv.DictReader(open(f))]
 for r in stats:
     out["kernels"][short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                         "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
