@@ -52,7 +52,9 @@ void ensure_lds_cap(const void* kernel) {
   const int dev = current_device();
   std::lock_guard<std::mutex> lock(g_mu);
   if (!lds_done().insert({kernel, dev}).second) return;
-  (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncAttributes attr{};
+  const size_t stat = hipFuncGetAttributes(&attr, kernel) == hipSuccess ? attr.sharedSizeBytes : 0;
+  (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024 - stat));
 }
 
 int num_cus() {

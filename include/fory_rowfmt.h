@@ -209,16 +209,18 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols,
  * between): pass the same rows, row offsets and column arrays to both calls
  * and do not modify `offsets` in between.
  *
- * String/binary list elements and map keys/values (columns indexed by element):
- * their offsets array has (element total + 1) entries, known only after a first
- * decode_sizes. Pass such a column with offsets = NULL to the first call (it
- * is skipped), then allocate offsets (length = the container's element total,
- * offsets[length] of the container column) and call decode_sizes again: the
- * second call also writes the element sizes and scans them (element
- * offsets[length] = total bytes). The device path supports list elements of
- * fixed width, string, binary or struct-of-fixed-width, and map keys/values of
- * fixed width, string or binary (FORY_ERR_UNSUPPORTED at plan creation
- * otherwise).
+ * Columns under lists / maps (indexed by element) are sized level by level.
+ * Level L = the columns with L list/map ancestors; level 0 are the rows' own
+ * columns (num_rows positions). A level-(L+1) column has as many positions as
+ * its nearest list/map ancestor's total (offsets[length] of that column). Pass
+ * the deeper columns with offsets = NULL (skipped) to the first call; after
+ * each call allocate the next level's columns (offsets of length+1 int32 for
+ * STRING/BINARY/LIST/MAP, `length` = positions) and call decode_sizes again:
+ * every call re-sizes each level whose STRING/BINARY/LIST/MAP columns all have
+ * offsets, in order, and stops at the first level that does not. Any nesting of
+ * struct / list / map fields has a device path (op programs for the common
+ * shapes, a tree engine for list<list<...>>, List<Bean> with var fields,
+ * Map<K, Bean> and the like).
  *
  * fory_rowfmt_decode: writes values/offsets/validity of out_cols. Null
  * values decode to 0 (RowEncoderBuilder.java:239-246 leaves the Java default).
@@ -235,6 +237,26 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows,
                        int32_t frame_mode, const fory_column* out_cols,
                        int32_t* d_status, void* d_workspace,
                        int64_t workspace_bytes, void* stream);
+
+/* Single-pass decode (no decode_sizes): for plans whose fields are fixed width,
+ * STRING / BINARY, LIST of fixed width, or structs of those (the cooperative
+ * tile kernels), one pass stages every 64-row tile once, publishes its var
+ * fields' totals and takes its Arrow offset base from a decoupled look-back
+ * over the earlier tiles, then writes offsets, values and validity. The caller
+ * sizes the var `values` buffers from an estimate (typically the previous
+ * batch's totals) and gives their byte size in `capacity`; list item columns
+ * likewise (validity sized for capacity / item width items). A field whose
+ * total exceeds its capacity gets its offsets written but not its values, and
+ * *d_status = FORY_ERR_CAPACITY: read every STRING/BINARY/LIST column's
+ * offsets[num_rows] (its total, always written), regrow and call again.
+ * Level-0 offsets arrays (num_rows+1 int32) are required. Returns
+ * FORY_ERR_UNSUPPORTED (nothing enqueued) for other plans: use decode_sizes +
+ * decode. */
+int fory_rowfmt_decode_fused(const fory_plan* plan, const void* d_rows,
+                             const int64_t* d_row_offsets, int64_t num_rows,
+                             int32_t frame_mode, const fory_column* out_cols,
+                             int32_t* d_status, void* d_workspace,
+                             int64_t workspace_bytes, void* stream);
 
 /* --- frame index: the stream alone -> row offsets, on the device.
  * Encoder.decode(MemoryBuffer) reads [i32 size][i64 hash], checks the hash and
