@@ -94,12 +94,6 @@ PROTOTYPES = {
          ctypes.POINTER(Column), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
          ctypes.c_void_p],
     ),
-    "fory_rowfmt_decode_fused": (
-        ctypes.c_int,
-        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
-         ctypes.POINTER(Column), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
-         ctypes.c_void_p],
-    ),
     "fory_rowfmt_read_status": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "fory_rowfmt_index_workspace_bytes": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64]),
     "fory_rowfmt_index_frames": (

@@ -197,7 +197,6 @@ fory_amd::FixedLaunch fixed_launch(const Plan& p, const void* table, int64_t n, 
 }
 
 int32_t* spill_ptr(const Plan& p, void* ws, int64_t n);
-int64_t* tile_totals_ptr(const Plan& p, void* ws, int64_t n);
 
 // LDS budget of one 64-record tile image for the varlen tile engine: 64 x an
 // estimated row (fixed part, nested struct rows, ~32 bytes per string,
@@ -217,23 +216,6 @@ int var_tile_cap(const Plan& p, int frame) {
   }
   int64_t cap = (64 * est + 1023) / 1024 * 1024;
   return (int)std::min<int64_t>(std::max<int64_t>(cap, 8 * 1024), 64 * 1024);
-}
-
-// Plans of the cooperative tile kernels: fixed / string / binary / list<fixed> fields
-// at any struct level, up to 32 var fields and kMaxTileStructs structs; maps, lists
-// of structs and lists of strings run on the generic tile interpreter
-// (enc_record / dec_record).
-bool plan_flat(const Plan& p, int frame) {
-  if (frame == FORY_FRAME_COLLECTION || p.generic || p.fixed_width) return false;
-  int nvar = 0, nst = 0;
-  for (const fory_amd::Op& op : p.program) {
-    if (op.code == fory_amd::OP_MAP || op.code == fory_amd::OP_LIST_STRUCT ||
-        (op.code == fory_amd::OP_LIST && ((op.e >> 8) & 4)))
-      return false;
-    nvar += op.code == fory_amd::OP_BYTES || op.code == fory_amd::OP_LIST;
-    nst += op.code == fory_amd::OP_STRUCT_BEGIN;
-  }
-  return nvar <= 32 && nst <= fory_amd::kMaxTileStructs;
 }
 
 // Var launch: columns table then program in the workspace.
@@ -297,14 +279,12 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
         v.is_list = 1;
         v.w = op.e & 0xff;
         v.iflags = op.e >> 8;
-        v.out_cap = it.capacity > 0 ? it.capacity / v.w : 0;
         v.values = static_cast<const uint8_t*>(it.values);
         v.out_values = static_cast<uint8_t*>(it.values);
         v.item_validity = (v.iflags & 1) ? it.validity : nullptr;
         v.out_item_validity = (v.iflags & 1) ? it.validity : nullptr;
       } else {
         v.w = 1;
-        v.out_cap = c.capacity > 0 ? c.capacity : 0;
         v.values = static_cast<const uint8_t*>(c.values);
         v.out_values = static_cast<uint8_t*>(c.values);
       }
@@ -323,7 +303,16 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   rc = upload(ws, host.data(), (int64_t)host.size(), s);
   if (rc) return rc;
   uint8_t* wsb = static_cast<uint8_t*>(ws);
-  L->flat = plan_flat(p, frame) ? 1 : 0;
+  bool has_map = false;  // (and lists of structs)
+  for (const fory_amd::Op& op : p.program)
+    has_map |= op.code == fory_amd::OP_MAP || op.code == fory_amd::OP_LIST_STRUCT ||
+               (op.code == fory_amd::OP_LIST && ((op.e >> 8) & 4));
+  // maps, lists of structs and lists of strings run on the generic tile interpreter
+  // (enc_record / dec_record)
+  L->flat = !has_map && frame != FORY_FRAME_COLLECTION && var.size() <= 32 &&
+                    st.size() <= (size_t)fory_amd::kMaxTileStructs
+                ? 1
+                : 0;
   L->num_var = (int32_t)var.size();
   L->num_struct = (int32_t)st.size();
   L->vf = reinterpret_cast<const fory_amd::VarFieldDev*>(wsb + o_var);
@@ -362,9 +351,6 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   L->frame = frame;
   L->tile_cap = var_tile_cap(p, frame);
   L->level2 = 0;
-  L->fused = 0;
-  L->lb = reinterpret_cast<uint64_t*>(tile_totals_ptr(p, ws, n));
-  L->ticket = L->spill_count + 1;
   return FORY_OK;
 }
 
@@ -761,36 +747,6 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows, const int64_t*
   L.mean_row = decode_mean_row(p, L, out_cols, num_rows, frame_mode);
   e = fory_amd::launch_var_decode(L, static_cast<const uint8_t*>(d_rows), d_row_offsets, d_status, s);
   return e == hipSuccess ? FORY_OK : hip_fail(e, "var_decode");
-}
-
-int fory_rowfmt_decode_fused(const fory_plan* plan, const void* d_rows, const int64_t* d_row_offsets,
-                             int64_t num_rows, int32_t frame_mode, const fory_column* out_cols, int32_t* d_status,
-                             void* d_workspace, int64_t workspace_bytes, void* stream) {
-  int rc = check_common(plan, out_cols, num_rows, frame_mode, d_workspace, workspace_bytes);
-  if (rc) return rc;
-  const Plan& p = plan->p;
-  if (p.fixed_width || p.generic) return fail(FORY_ERR_UNSUPPORTED, "single-pass decode: varlen op-program plans only");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  fory_amd::VarLaunch L{};
-  L.flat = plan_flat(p, frame_mode) ? 1 : 0;
-  if (!fory_amd::var_decode_fused_supported(L))
-    return fail(FORY_ERR_UNSUPPORTED, "single-pass decode: this plan needs decode_sizes + decode");
-  if (num_rows > 0) {
-    if (!d_rows || !d_row_offsets)
-      return fail(FORY_ERR_INVALID_ARGUMENT, "varlen schema: d_rows and d_row_offsets required");
-    rc = prepare_var(p, out_cols, num_rows, frame_mode, d_workspace, s, &L, true);
-    if (rc) return rc;
-  }
-  if (num_rows == 0) {
-    for (size_t idx = 0; idx < p.nodes.size(); ++idx)
-      if (is_var_kind(p.nodes[idx].kind) && out_cols && out_cols[idx].offsets)
-        (void)hipMemsetAsync(out_cols[idx].offsets, 0, sizeof(int32_t), s);
-    return FORY_OK;
-  }
-  L.fused = 1;
-  L.mean_row = decode_mean_row(p, L, out_cols, num_rows, frame_mode);
-  hipError_t e = fory_amd::launch_var_decode_fused(L, static_cast<const uint8_t*>(d_rows), d_row_offsets, d_status, s);
-  return e == hipSuccess ? FORY_OK : hip_fail(e, "var_decode_fused");
 }
 
 int64_t fory_rowfmt_index_workspace_bytes(const fory_plan* plan, int64_t num_rows, int64_t rows_bytes) {

@@ -68,9 +68,6 @@ struct VarLaunch {
   int32_t pl_all;               // encode tile kernel: wave 0 places var payloads too (A/B)
   int32_t level2;               // decode lengths pass 2: sizes of string/binary list/map
                                 // elements (container offsets already scanned)
-  int32_t fused;                // single-pass decode (launch_var_decode_fused)
-  uint64_t* lb;                 // fused: look-back state [num_var][tiles + 1] (zeroed per call)
-  int32_t* ticket;              // fused: tile ticket counter (in-order tile claim)
 };
 
 // sizes -> d_row_offsets[0..n-1] (row/frame byte sizes), then exclusive scan.
@@ -89,16 +86,6 @@ int64_t var_tile_totals_words(int64_t num_var, int64_t n);
 int64_t var_spill_words(int64_t n);
 hipError_t launch_var_decode(const VarLaunch& L, const uint8_t* rows,
                              const int64_t* d_row_offsets, int32_t* status, hipStream_t s);
-// Single-pass decode of a cooperative (flat) plan: every tile stages its rows once,
-// publishes its var fields' payload totals and finds its Arrow offset base by a
-// decoupled look-back over earlier tiles (claimed in order by a ticket), then
-// writes offsets, values and validity. Values buffers come with capacities
-// (VarFieldDev::out_cap); a field whose total exceeds its capacity sets
-// FORY_ERR_CAPACITY and leaves its values unwritten; out_offsets[n] holds every
-// field's total either way. False when the plan has no single-pass path.
-bool var_decode_fused_supported(const VarLaunch& L);
-hipError_t launch_var_decode_fused(const VarLaunch& L, const uint8_t* rows, const int64_t* d_row_offsets,
-                                   int32_t* status, hipStream_t s);
 
 // Exclusive scan of n int64 values in place; data[n] receives the total.
 // partials: >= scan_partials(n) int64 of workspace.

@@ -52,7 +52,7 @@ void ensure_lds_cap(const void* kernel) {
   const int dev = current_device();
   std::lock_guard<std::mutex> lock(g_mu);
   if (!lds_done().insert({kernel, dev}).second) return;
-  hipFuncAttributes attr{};
+  hipFuncAttributes attr{};  // dynamic LDS up to 160 KiB less the kernel's static LDS
   const size_t stat = hipFuncGetAttributes(&attr, kernel) == hipSuccess ? attr.sharedSizeBytes : 0;
   (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024 - stat));
 }

@@ -81,7 +81,7 @@ struct VarFieldDev {
   int32_t iflags;                // item flags: bit0 nullable, bit1 bool
   int32_t flags;                 // field flags: bit0 nullable
   int32_t parent;                // enclosing struct id (0 = the row itself)
-  int64_t out_cap;               // single-pass decode: out_values capacity in elements (bytes / items)
+  int32_t pad[2];
 };
 
 // Nested struct fields of a tile-engine plan, in pre-order (id = index + 1; id

@@ -1787,63 +1787,7 @@ __device__ __forceinline__ bool frame_ok(const VarLaunch& L, const uint8_t* fp, 
   return size_ok;
 }
 
-// Decoupled look-back of the single-pass decode: per (var field, tile) one word,
-// flag << 62 | value: kLbAgg = the tile's payload total, kLbPre = the inclusive
-// prefix through the tile. Vector atomics at agent scope (L2-coherent).
-constexpr uint64_t kLbAgg = 1ull << 62, kLbPre = 2ull << 62, kLbVal = (1ull << 62) - 1;
-
-__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
-  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Exclusive prefix of tile t over row[0 .. t-1] (one wave, all lanes): 64
-// predecessors per poll, nearest first; sums aggregates back to the nearest
-// published prefix. Predecessors claimed their tiles earlier (ticket order) and
-// publish without waiting on later tiles, so the wait always ends; a bounded poll
-// count turns a broken invariant into a status error instead of a hang.
-__device__ __noinline__ int64_t lb_exclusive(const uint64_t* row, int64_t t, int lane, int32_t* status) {
-  int64_t acc = 0;
-  int64_t hi = t - 1;
-  int polls = 0;
-  while (hi >= 0) {
-    const int64_t j = hi - lane;
-    const uint64_t s = j >= 0 ? lb_load(row + j) : kLbPre;  // before tile 0: prefix 0
-    const uint64_t pre = __ballot((s >> 62) == 2);
-    const int np = pre ? __builtin_ctzll(pre) : 64;
-    const uint64_t upto = np >= 63 ? ~0ull : ((2ull << np) - 1);  // lanes 0..np
-    if (__ballot((s >> 62) == 0) & upto) {
-      if (++polls > (1 << 22)) {
-        set_status(status, FORY_ERR_DEVICE);
-        return acc;
-      }
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    acc += wave_sum64(lane <= np ? (int64_t)(s & kLbVal) : 0);
-    if (np < 64) return acc;
-    hi -= 64;
-  }
-  return acc;
-}
-
-// Publishes tile t's total of field v and returns its exclusive prefix (main
-// launch: look-back; spill launch: the predecessor's final prefix).
-template <bool SPILL>
-__device__ __forceinline__ int64_t lb_base(const VarLaunch& L, int v, int64_t t, int64_t sum, int lane,
-                                           int32_t* status) {
-  const int64_t tiles = (L.num_rows + 63) / 64;
-  const uint64_t* row = L.lb + v * (tiles + 1);
-  if (SPILL) return t ? (int64_t)(lb_load(row + t - 1) & kLbVal) : 0;
-  const int64_t base = t ? lb_exclusive(row, t, lane, status) : 0;
-  if (lane == 0) lb_store(L.lb + v * (tiles + 1) + t, kLbPre | (uint64_t)(base + sum));
-  return base;
-}
-
-template <int HDR, bool WRITE, int NW, bool SPILL, bool FUSED = false>
+template <int HDR, bool WRITE, int NW, bool SPILL>
 __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
                                                                   const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
                                                                   const StructDev* __restrict__ st,
@@ -1874,12 +1818,11 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   const int64_t total = mis + (B1 - B0);
   const int64_t tiles = (L.num_rows + 63) / 64;
   if (!sane || (mis & 3) || total > cap) {  // per-lane path on global rows (one wave)
-    const bool to_spill = !SPILL && sane && !(mis & 3) && total <= sp.cap;  // the big-image launch takes it
-    if (to_spill && !FUSED) {
+    if (!SPILL && sane && !(mis & 3) && total <= sp.cap) {  // spill: the big-image launch takes it
       if (threadIdx.x == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
       return;
     }
-    if (wave == 0) {  // (fused: a spilled tile still publishes its totals and prefixes here)
+    if (wave == 0) {
       const uint8_t* fp = in + beg;
       const uint8_t* row = fp + HDR;
       int64_t row_len = end - beg;
@@ -1891,7 +1834,6 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
         flat_dec_struct_bases<false>(L, st, bad, live, lane, r0, rows, row, row_len, sbase, status);
         wave_lds_sync();
       }
-      bool room = true;
       for (int v = 0; v < L.num_var; ++v) {
         int64_t rel = 0, n = 0;
         if (!bad) flat_var_slot(L, vf[v], st, sbase, lane, row, row_len, &rel, &n, !WRITE, status);
@@ -1899,32 +1841,19 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
           const int64_t sum = wave_sum64(n);
           if (lane == 0) tile_tot[v * (tiles + 1) + tile] = sum;
         } else {
-          const int64_t incl = wave_incl_scan64(n, lane);
-          int64_t base;
-          if (FUSED) {
-            const int64_t sum = __shfl(incl, 63);
-            base = lb_base<SPILL>(L, v, tile, sum, lane, status);
-            if (base + sum > vf[v].out_cap || base + sum > 0x7fffffffLL) room = false;
-            if (!SPILL && tile == tiles - 1 && lane == 0) vf[v].out_offsets[L.num_rows] = (int32_t)(base + sum);
-          } else {
-            base = vf[v].out_offsets[r0];
-          }
-          if (live && !to_spill) vf[v].out_offsets[r0 + lane] = (int32_t)(base + incl - n);
+          const int64_t base = vf[v].out_offsets[r0];
+          const int64_t excl = wave_incl_scan64(n, lane) - n;
+          if (live) vf[v].out_offsets[r0 + lane] = (int32_t)(base + excl);
         }
       }
-      if (FUSED && !room) set_status(status, FORY_ERR_CAPACITY);
-      if (to_spill) {
-        if (lane == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
-        return;
-      }
-      if (WRITE && room) dec_record<true>(L, prog, cols, r0 + lane, live, in + beg, end - beg, status);
+      if (WRITE) dec_record<true>(L, prog, cols, r0 + lane, live, in + beg, end - beg, status);
     }
     return;
   }
   // tile-start Arrow offsets of every var field (written by decode_sizes): loaded
   // now so their latency hides under the staging loads (lane v holds field v's)
   int64_t obase = 0;
-  if (WRITE && !FUSED && lane < L.num_var) obase = vf[lane].out_offsets[r0];
+  if (WRITE && lane < L.num_var) obase = vf[lane].out_offsets[r0];
   {  // stage the tile's rows: LDS-DMA of whole 16-B chunks (1 KiB per wave
      // instruction, all in flight at once, nt policy for the once-read rows); the
      // edge chunks' bytes outside the tile (same 16-B blocks) are never read
@@ -1952,14 +1881,6 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   if (L.num_struct) {  // child-row offsets (+ struct validity) for every wave
     if (wave == 0) flat_dec_struct_bases<WRITE>(L, st, bad, live, lane, r0, rows, row, row_len, sbase, status);
     __syncthreads();
-  }
-  if (FUSED && !SPILL) {  // publish this tile's totals first: later tiles' look-backs need only these
-    for (int v = wave; v < L.num_var; v += NW) {
-      int64_t rel = 0, n = 0;
-      if (!bad) flat_var_slot(L, vf[v], st, sbase, lane, row, row_len, &rel, &n, false, status);
-      const int64_t sum = wave_sum64(n);
-      if (lane == 0) lb_store(L.lb + v * (tiles + 1) + tile, (tile ? kLbAgg : kLbPre) | (uint64_t)sum);
-    }
   }
   if (!WRITE) {  // pass 1: per-tile payload totals (scanned over tiles by the host launcher)
     for (int v = wave; v < L.num_var; v += NW) {
@@ -1992,20 +1913,12 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
       const uint64_t m = __ballot(live && !nul);
       if (lane == 0) write_validity64(f.out_validity, r0, rows, m);
     }
-    // Arrow offsets of this tile: base (tile prefix: written by decode_sizes, or the
-    // look-back of the single-pass decode) + in-wave prefix
+    // Arrow offsets of this tile: base (tile prefix written by decode_sizes) + in-wave prefix
+    const int64_t O0 = __shfl(obase, v);
     const int64_t incl = wave_incl_scan64(n, lane);
-    const int64_t O0 = FUSED ? lb_base<SPILL>(L, v, tile, __shfl(incl, 63), lane, status) : __shfl(obase, v);
     const int64_t O1 = O0 + __shfl(incl, 63);
     const int64_t e0 = O0 + incl - n;
     if (live) f.out_offsets[i] = (int32_t)e0;
-    if (FUSED) {
-      if (!SPILL && tile == tiles - 1 && lane == 0) f.out_offsets[L.num_rows] = (int32_t)O1;
-      if (O1 > f.out_cap || O1 > 0x7fffffffLL) {  // values do not fit: offsets only (the caller regrows)
-        set_status(status, FORY_ERR_CAPACITY);
-        continue;
-      }
-    }
     const int64_t S = (O1 - O0) * w;
     uint8_t* gdst = f.out_values + O0 * w;
     const int phase = (int)(reinterpret_cast<uintptr_t>(gdst) & 15);
@@ -2113,16 +2026,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   }
   };
   if (!SPILL) {
-    if (FUSED) {  // tiles claimed in order: every earlier tile is resident or done
-      volatile int32_t* claim = reinterpret_cast<volatile int32_t*>(lds);  // (the image's first word, before staging)
-      if (threadIdx.x == 0) *claim = atomicAdd(L.ticket, 1);
-      __syncthreads();
-      const int64_t t = *claim;
-      __syncthreads();
-      body(t);
-    } else {
-      body(blockIdx.x);
-    }
+    body(blockIdx.x);
     return;
   }
   const int64_t count = *sp.count;  // tiles the main launch spilled
@@ -2367,26 +2271,21 @@ void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int6
   else launch_flat_enc_t<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
 }
 
-template <int HDR, bool WRITE, int NW, bool FUSED = false>
+template <int HDR, bool WRITE, int NW>
 void launch_flat_dec(const VarLaunch& L0, const uint8_t* rows, const int64_t* offs, int64_t* tile_tot,
                      int32_t* status, int cap, hipStream_t s) {
-  auto* k = &var_decode_flat_kernel<HDR, WRITE, NW, false, FUSED>;
+  auto* k = &var_decode_flat_kernel<HDR, WRITE, NW, false>;
   raise_lds_cap(k);
   VarLaunch L = L0;
   if (WRITE) L.stg_bytes = dec_stg_bytes(k, L0, cap, NW);
   if (WRITE && L.mean_row > 0) cap = grow_cap(k, 64 * NW, cap, [&](int c) { return flat_lds_dec(L, c, NW); });
   const SpillArgs sp = spill_args(L, cap);
   (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
-  if (FUSED) {  // look-back words and the ticket start from zero
-    const int64_t tiles = (L.num_rows + 63) / 64;
-    (void)hipMemsetAsync(L.lb, 0, (size_t)L.num_var * (tiles + 1) * sizeof(uint64_t), s);
-    (void)hipMemsetAsync(L.ticket, 0, sizeof(int32_t), s);
-  }
   const size_t lds = WRITE ? flat_lds_dec(L, cap, NW) : (size_t)cap + sbase_lds(L);  // pass 1: row image (+ struct offsets)
   var_diag(WRITE ? "decode" : "decode lengths", k, 64 * NW, cap, L.stg_bytes, lds);
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
                      L.vf, L.st, rows, offs, tile_tot, status, cap, sp);
-  auto* k2 = &var_decode_flat_kernel<HDR, WRITE, NW, true, FUSED>;
+  auto* k2 = &var_decode_flat_kernel<HDR, WRITE, NW, true>;
   raise_lds_cap(k2);
   const size_t lds2 = WRITE ? flat_lds_dec(L, sp.cap, NW) : (size_t)sp.cap + sbase_lds(L);
   hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, lds2, 64 * NW)), dim3(64 * NW), lds2, s, L, L.prog, L.cols, L.fix,
@@ -2489,20 +2388,6 @@ hipError_t launch_var_decode_lengths(const VarLaunch& L, const uint8_t* rows, co
 hipError_t launch_var_decode(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int32_t* status,
                              hipStream_t s) {
   return launch_var_decode_pass<true>(L, rows, offs, nullptr, status, s);
-}
-
-bool var_decode_fused_supported(const VarLaunch& L) { return var_tiles() && var_flat(L); }
-
-hipError_t launch_var_decode_fused(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int32_t* status,
-                                   hipStream_t s) {
-  if (L.num_rows <= 0) return hipSuccess;
-  const int cap = fit_cap(L, L.mean_row);
-  switch (frame_header_bytes(L.frame)) {
-    case 12: launch_flat_dec<12, true, kNW, true>(L, rows, offs, nullptr, status, cap, s); break;
-    case 8: launch_flat_dec<8, true, kNW, true>(L, rows, offs, nullptr, status, cap, s); break;
-    default: launch_flat_dec<0, true, kNW, true>(L, rows, offs, nullptr, status, cap, s); break;
-  }
-  return hipGetLastError();
 }
 
 }  // namespace fory_amd

@@ -60,9 +60,6 @@ class RowEncoder:
         self.device = device
         self.plan = NativePlan(schema)
         self._ws = None
-        # single-pass decode: None = not tried yet, False = the plan has none,
-        # else {column: elements per record} learned from the last batch (sizing)
-        self._fused = None
 
     # -- RowEncoder.schema() ------------------------------------------------
     def schema(self) -> Schema:
@@ -167,10 +164,6 @@ class RowEncoder:
             if frame_mode != FRAME_STREAM:
                 raise ValueError("raw rows / collection frames are not self-delimiting: row offsets are required")
             offsets = self.index_frames(buf, n)
-        if isinstance(self._fused, dict) and n > 0:
-            out = self._decode_fused(buf, offsets, n, frame_mode, container, cdepth, status, ws)
-            if out is not None:
-                return out
         alloc(0)
         for level in range(max(cdepth) + 1):
             var_idx = [i for i, f in enumerate(fields) if cdepth[i] == level and f.type.id in var_kinds]
@@ -186,64 +179,6 @@ class RowEncoder:
             alloc(level + 1)
         native.decode(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
         native.read_status(status)
-        if self._fused is not False and n > 0 and frame_mode != FRAME_COLLECTION and max(cdepth) <= 1:
-            self._fused = {i: totals[i] / n for i in totals}  # next batch: single pass
-        return cols
-
-    def _decode_fused(self, buf, offsets, n, frame_mode, container, cdepth, status, ws, retry=True):
-        """Single-pass decode (fory_rowfmt_decode_fused) with var buffers sized from the
-        last batch's totals per record (+6 %); a short buffer -> exact sizes, one retry.
-        None when the plan has no single-pass path (then decode_sizes + decode)."""
-        import torch
-        from .errors import IndexOutOfBoundsException, UnsupportedOperationException
-        fields = self.plan.fields
-        var_kinds = (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP)
-        per = self._fused
-        caps = {i: int(per.get(i, 0) * n * 1.0625) + 64 for i in per}
-        cols = []
-        for i, f in enumerate(fields):
-            t = f.type.id
-            npos = n if container[i] < 0 else caps.get(container[i], 0)
-            c = DeviceColumn(length=npos)
-            if t in var_kinds:
-                c.offsets = torch.zeros(npos + 1, dtype=torch.int32, device=self.device)
-                if t in (ArrowType.STRING, ArrowType.BINARY):
-                    c.values = torch.empty(max(1, caps.get(i, 0)), dtype=torch.uint8, device=self.device)
-            elif t != ArrowType.STRUCT:
-                c.values = torch.empty(max(1, npos), dtype=_torch_dtype(t), device=self.device)
-            if f.nullable:
-                c.validity = torch.zeros(_validity_bytes(npos), dtype=torch.uint8, device=self.device)
-            cols.append(c)
-        try:
-            native.decode_fused(self.plan, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
-        except UnsupportedOperationException:
-            self._fused = False
-            return None
-        var_idx = [i for i, f in enumerate(fields) if cdepth[i] == 0 and f.type.id in var_kinds]
-        totals = dict(zip(var_idx, torch.stack([cols[i].offsets[n] for i in var_idx]).cpu().tolist())) \
-            if var_idx else {}
-        try:
-            native.read_status(status)
-        except IndexOutOfBoundsException:
-            short = {i: t for i, t in totals.items() if t > caps.get(i, 0) or t < 0}
-            if not short or not retry:
-                raise
-            status.zero_()
-            self._fused = {i: max(per.get(i, 0), (totals[i] + 1) / n) for i in totals}
-            return self._decode_fused(buf, offsets, n, frame_mode, container, cdepth, status, ws, retry=False)
-        for i in var_idx:  # trim to the totals
-            tot = int(totals[i])
-            if fields[i].type.id in (ArrowType.STRING, ArrowType.BINARY):
-                cols[i].values = cols[i].values[:max(1, tot)]
-            else:
-                for k, f in enumerate(fields):
-                    if container[k] == i:
-                        cols[k].length = tot
-                        if cols[k].values is not None:
-                            cols[k].values = cols[k].values[:max(1, tot)]
-                        if cols[k].validity is not None:
-                            cols[k].validity = cols[k].validity[:_validity_bytes(tot)]
-        self._fused = {i: max(per.get(i, 0) * 0.75, totals[i] / n) for i in totals}
         return cols
 
     def index_frames(self, buf, num_rows: int):

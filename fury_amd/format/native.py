@@ -126,15 +126,6 @@ def decode(plan: NativePlan, rows, d_offsets, n: int, frame: int, cols_arr, stat
                                   _ptr(status), _ptr(ws), ws.numel(), s))
 
 
-def decode_fused(plan: NativePlan, rows, d_offsets, n: int, frame: int, cols_arr, status, ws, stream=None):
-    """Single-pass decode (fory_rowfmt_decode_fused); raises UnsupportedOperationException
-    for plans without one."""
-    lib = _lib.load()
-    s = stream if stream is not None else _stream_handle()
-    _check(lib.fory_rowfmt_decode_fused(plan.handle, _ptr(rows), _ptr(d_offsets), n, frame, cols_arr,
-                                        _ptr(status), _ptr(ws), ws.numel(), s))
-
-
 def index_workspace_bytes(plan: NativePlan, n: int, rows_bytes: int) -> int:
     return int(_lib.load().fory_rowfmt_index_workspace_bytes(plan.handle, n, rows_bytes))
 

@@ -238,26 +238,6 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows,
                        int32_t* d_status, void* d_workspace,
                        int64_t workspace_bytes, void* stream);
 
-/* Single-pass decode (no decode_sizes): for plans whose fields are fixed width,
- * STRING / BINARY, LIST of fixed width, or structs of those (the cooperative
- * tile kernels), one pass stages every 64-row tile once, publishes its var
- * fields' totals and takes its Arrow offset base from a decoupled look-back
- * over the earlier tiles, then writes offsets, values and validity. The caller
- * sizes the var `values` buffers from an estimate (typically the previous
- * batch's totals) and gives their byte size in `capacity`; list item columns
- * likewise (validity sized for capacity / item width items). A field whose
- * total exceeds its capacity gets its offsets written but not its values, and
- * *d_status = FORY_ERR_CAPACITY: read every STRING/BINARY/LIST column's
- * offsets[num_rows] (its total, always written), regrow and call again.
- * Level-0 offsets arrays (num_rows+1 int32) are required. Returns
- * FORY_ERR_UNSUPPORTED (nothing enqueued) for other plans: use decode_sizes +
- * decode. */
-int fory_rowfmt_decode_fused(const fory_plan* plan, const void* d_rows,
-                             const int64_t* d_row_offsets, int64_t num_rows,
-                             int32_t frame_mode, const fory_column* out_cols,
-                             int32_t* d_status, void* d_workspace,
-                             int64_t workspace_bytes, void* stream);
-
 /* --- frame index: the stream alone -> row offsets, on the device.
  * Encoder.decode(MemoryBuffer) reads [i32 size][i64 hash], checks the hash and
  * advances by the frame (Encoders.java:176-193): the frames delimit themselves.
