@@ -10,6 +10,8 @@
 #include <cstdlib>
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -166,10 +168,50 @@ int bind_var(const Plan& p, const fory_column* cols, int64_t n, std::vector<Colu
   return FORY_OK;
 }
 
+// Plan tables reach the workspace by an async copy from pinned host memory that
+// outlives the call: per device a ring of pinned slots (process lifetime, shared by
+// all threads under a mutex), each reused only after the copy that last read it
+// has completed (its event). A copy straight from a local vector could be read by
+// the DMA engine after the call returned (a flaky plan table in the host pipeline).
+struct UploadRing {
+  static constexpr int kSlots = 32;
+  void* buf[kSlots] = {};
+  size_t cap[kSlots] = {};
+  hipEvent_t ev[kSlots] = {};
+  bool used[kSlots] = {};
+  int next = 0;
+};
+
+std::mutex g_upload_mu;
+
 int upload(void* ws, const void* host, int64_t bytes, hipStream_t s) {
   if (bytes == 0) return FORY_OK;
-  hipError_t e = hipMemcpyAsync(ws, host, (size_t)bytes, hipMemcpyHostToDevice, s);
+  static std::map<int, UploadRing*>* rings = new std::map<int, UploadRing*>();  // never freed
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lock(g_upload_mu);
+  UploadRing*& rp = (*rings)[dev];
+  if (!rp) rp = new UploadRing();
+  UploadRing& r = *rp;
+  const int k = r.next;
+  r.next = (r.next + 1) % UploadRing::kSlots;
+  hipError_t e = hipSuccess;
+  if (r.used[k]) e = hipEventSynchronize(r.ev[k]);  // the slot's previous copy has been read
+  if (e == hipSuccess && !r.ev[k]) e = hipEventCreateWithFlags(&r.ev[k], hipEventDisableTiming);
+  if (e == hipSuccess && r.cap[k] < (size_t)bytes) {
+    if (r.buf[k]) (void)hipHostFree(r.buf[k]);
+    r.buf[k] = nullptr;
+    r.cap[k] = 0;
+    const size_t want = std::max<size_t>((size_t)bytes, 64 * 1024);
+    e = hipHostMalloc(&r.buf[k], want, hipHostMallocDefault);
+    if (e == hipSuccess) r.cap[k] = want;
+  }
+  if (e != hipSuccess) return hip_fail(e, "plan table staging");
+  std::memcpy(r.buf[k], host, (size_t)bytes);
+  e = hipMemcpyAsync(ws, r.buf[k], (size_t)bytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipEventRecord(r.ev[k], s);
   if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(plan table)");
+  r.used[k] = true;
   return FORY_OK;
 }
 
@@ -727,8 +769,11 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows, const int64_t*
     if (rc) return rc;
     rc = upload(d_workspace, tab.data(), (int64_t)(tab.size() * sizeof(FixedFieldDev)), s);
     if (rc) return rc;
-    e = fory_amd::launch_decode_fixed(fixed_launch(p, d_workspace, num_rows, frame_mode),
-                                      static_cast<const uint8_t*>(d_rows), d_status, s);
+    fory_amd::FixedLaunch L = fixed_launch(p, d_workspace, num_rows, frame_mode);
+    L.cols_aligned16 = 1;
+    for (const FixedFieldDev& f : tab)
+      if (reinterpret_cast<uintptr_t>(f.out_values) & 15) L.cols_aligned16 = 0;
+    e = fory_amd::launch_decode_fixed(L, static_cast<const uint8_t*>(d_rows), d_status, s);
     return e == hipSuccess ? FORY_OK : hip_fail(e, "decode_fixed");
   }
   if (p.fixed_width) return fail(FORY_ERR_UNSUPPORTED, "row too wide for the device path");

@@ -205,11 +205,15 @@ __host__ __device__ inline int v3_insn_count(const int* group) {
 // vmcnt for the older set while the younger set stays in flight. Order per
 // stage: write X -> barrier -> store this tile's rows -> issue X for tile +
 // 2*grid -> barrier. Not-null schemas only (the nullable form spills).
-template <int R, int K>
+template <int R, int K, int OPT = 0>
 __device__ __forceinline__ void v5_issue(const uint8_t* const (&ptr)[K], const int (&wk)[K], int64_t r0,
                                          u32x4 (&d)[K]) {
 #pragma unroll
-  for (int k = 0; k < K; ++k) d[k] = *gp(reinterpret_cast<const u32x4*>(ptr[k] + r0 * wk[k]));
+  for (int k = 0; k < K; ++k) {
+    const u32x4* a = reinterpret_cast<const u32x4*>(ptr[k] + r0 * wk[k]);
+    if constexpr (OPT & 1) d[k] = __builtin_nontemporal_load(gp(a));  // once-read column streams
+    else d[k] = *gp(a);
+  }
 }
 
 template <int R, int K, int HDR>
@@ -274,7 +278,7 @@ __device__ __forceinline__ int64_t map_tile(int64_t t, int64_t tiles, int64_t C)
   return blk * 8 * C + (b % 8) * C + b / 8;
 }
 
-template <int R, int WG, int K, int HDR>
+template <int R, int WG, int K, int HDR, int OPT = 0>
 __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
                                                                  const FixedFieldDev* __restrict__ fields,
                                                                  uint8_t* __restrict__ out, int64_t tiles,
@@ -313,24 +317,35 @@ __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
   const int64_t last = tiles - 1;
   // logical tile t -> tile map_tile(t): xcd_run = grid / 8 (each step's grid tiles,
   // one contiguous run per XCD) or 0
-  auto mt = [&](int64_t x) { return map_tile(x, tiles, xcd_run); };
-  v5_issue<R, K>(ptr, wk, mt(t) * R, dA);
-  v5_issue<R, K>(ptr, wk, mt(min(t + (int64_t)gridDim.x, last)) * R, dB);
+  // OPT & 2: blocked order (A/B) -- workgroup b walks tiles [b*per, (b+1)*per) in order
+  const int64_t per = (tiles + gridDim.x - 1) / gridDim.x;
+  auto mt = [&](int64_t x) -> int64_t {
+    if constexpr (OPT & 2) return min((x % (int64_t)gridDim.x) * per + x / (int64_t)gridDim.x, last);
+    return map_tile(x, tiles, xcd_run);
+  };
+  int64_t tend = tiles;
+  if constexpr (OPT & 2) {  // this workgroup's logical steps: x = b + j * grid while its tile < tiles
+    const int64_t mine = min(per, tiles - (int64_t)blockIdx.x * per);
+    if (mine <= 0) return;
+    tend = (int64_t)blockIdx.x + mine * gridDim.x;
+  }
+  v5_issue<R, K, OPT>(ptr, wk, mt(t) * R, dA);
+  v5_issue<R, K, OPT>(ptr, wk, mt(min(t + (int64_t)gridDim.x, tend - 1)) * R, dB);
   for (;;) {
     v5_write<R, K, HDR>(lds, stride, hdr_bm, wk, sf, dA);
     __syncthreads();
     v5_store<R, WG>(L, lds, out + mt(t) * R * stride, tid);
-    v5_issue<R, K>(ptr, wk, mt(min(t + 2 * (int64_t)gridDim.x, last)) * R, dA);
+    v5_issue<R, K, OPT>(ptr, wk, mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)) * R, dA);
     __syncthreads();
     t += gridDim.x;
-    if (t >= tiles) break;
+    if (t >= tend) break;
     v5_write<R, K, HDR>(lds, stride, hdr_bm, wk, sf, dB);
     __syncthreads();
     v5_store<R, WG>(L, lds, out + mt(t) * R * stride, tid);
-    v5_issue<R, K>(ptr, wk, mt(min(t + 2 * (int64_t)gridDim.x, last)) * R, dB);
+    v5_issue<R, K, OPT>(ptr, wk, mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)) * R, dB);
     __syncthreads();
     t += gridDim.x;
-    if (t >= tiles) break;
+    if (t >= tend) break;
   }
 }
 
@@ -466,6 +481,156 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
 }
 
 // ---------------------------------------------------------------------------
+// Decode v5: the encode v5 mirrored. Persistent workgroups; the row stream of a
+// tile (R * stride contiguous bytes) comes in as K 16-B chunks per thread, two
+// tiles in flight in registers (sets A/B, the loop unrolled by 2; every thread
+// issues exactly K loads per tile, inactive ones re-read chunk 0, so the compiler
+// waits with a counted vmcnt for the older set while the younger set and the
+// column stores stay in flight: no vmcnt(0) drain per tile). Per stage: rows ->
+// LDS -> barrier -> each lane gathers ONE field's 16-B column chunk (E = 16/w
+// consecutive records, null -> 0, bool -> 0/1) and stores it non-temporally
+// (one 1-KiB wave instruction per FPI fields, numbered like the encode's,
+// v3_insn_g) -> issue the rows of tile + 2*grid -> barrier. Not-null schemas
+// whose column chunks fit K2 instructions per wave (the null bits are still read:
+// a set bit decodes to 0, as in decode_fixed_kernel).
+template <int R, int K>
+__device__ __forceinline__ void d5_issue(const uint8_t* in, int64_t base, int stride, int tid, int n16, int WGT,
+                                         u32x4 (&d)[K]) {
+  const uint8_t* tile = in + base * stride;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int c = tid + k * WGT;
+    d[k] = __builtin_nontemporal_load(gp(reinterpret_cast<const u32x4*>(tile + (int64_t)(c < n16 ? c : 0) * 16)));
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void d5_write(uint8_t* lds, int tid, int n16, int WGT, const u32x4 (&d)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int c = tid + k * WGT;
+    if (c < n16) *reinterpret_cast<u32x4*>(lds + c * 16) = d[k];
+  }
+}
+
+// Lane k-th column chunk: E records from rb of field slot `sf` (slot | flags << 16 |
+// valid << 20 | rb << 21) gathered from the LDS rows, stored to optr (column + rb * w).
+template <int R, int K2, int HDR>
+__device__ __forceinline__ void d5_columns(const uint8_t* lds, int stride, int hdr_bm, const int (&wk)[K2],
+                                           const uint32_t (&sf)[K2], uint8_t* const (&optr)[K2], int64_t r0) {
+#pragma unroll
+  for (int k = 0; k < K2; ++k) {
+    if (!(sf[k] & (1u << 20))) continue;
+    const int w = wk[k];
+    const int slot = sf[k] & 0xffff, flags = (sf[k] >> 16) & 0xf, rb = sf[k] >> 21;
+    const uint8_t* row = lds + rb * stride;
+    const int bmo = HDR + ((slot >> 5) << 2);
+    const uint32_t bit = 1u << (slot & 31);
+    auto val = [&](int e) -> uint64_t {  // UnsafeTrait.getX of record rb + e; null -> 0
+      const uint8_t* r = row + e * stride;
+      if (ld32(r + bmo) & bit) return 0;
+      const uint8_t* p = r + hdr_bm + 8 * slot;
+      return w == 8 ? ((uint64_t)ld32(p) | ((uint64_t)ld32(p + 4) << 32)) : (uint64_t)ld32(p);
+    };
+    u32x4 x;
+    if (w == 8) {
+      const uint64_t a = val(0), b = val(1);
+      x = u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+    } else if (w == 4) {
+      x = u32x4{(uint32_t)val(0), (uint32_t)val(1), (uint32_t)val(2), (uint32_t)val(3)};
+    } else if (w == 2) {
+      uint32_t h[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) h[q] = (uint32_t)(val(2 * q) & 0xffff) | ((uint32_t)(val(2 * q + 1) & 0xffff) << 16);
+      x = u32x4{h[0], h[1], h[2], h[3]};
+    } else {
+      uint32_t h[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          uint32_t b = (uint32_t)(val(4 * q + e) & 0xff);
+          if (flags & 2) b = b ? 1 : 0;  // MemoryBuffer.getBoolean
+          acc |= b << (8 * e);
+        }
+        h[q] = acc;
+      }
+      x = u32x4{h[0], h[1], h[2], h[3]};
+    }
+    __builtin_nontemporal_store(x, gp(reinterpret_cast<u32x4*>(optr[k] + r0 * w)));
+  }
+}
+
+template <int R, int WG, int K, int K2, int HDR, int OPT = 0>
+__global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
+                                                                 const FixedFieldDev* __restrict__ fields,
+                                                                 const uint8_t* __restrict__ in, int64_t tiles,
+                                                                 int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int NW = WG / 64;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int stride = L.stride;
+  const int hdr_bm = HDR + L.bitmap_bytes;
+  const int n16 = R * stride / 16;
+  int64_t t = blockIdx.x;
+  if (t >= tiles) return;
+
+  int wk[K2];
+  uint32_t sf[K2];
+  uint8_t* optr[K2];
+#pragma unroll
+  for (int k = 0; k < K2; ++k) {
+    int w = 0, p0 = 0, pend = 0;
+    const bool ok = v3_insn<R>(wave + k * NW, L, &w, &p0, &pend);
+    wk[k] = ok ? w : 8;
+    const int cpf = R * wk[k] / 16;
+    const int p = p0 + lane / cpf, c = lane % cpf;
+    sf[k] = 0;
+    optr[k] = nullptr;
+    if (ok && p < pend) {
+      const FixedFieldDev& fd = fields[p];
+      const int rb = c * (16 / w);
+      sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (1u << 20) | ((uint32_t)rb << 21);
+      optr[k] = fd.out_values + (int64_t)rb * w;
+    }
+  }
+  u32x4 dA[K], dB[K];
+  const int64_t last = tiles - 1;
+  // OPT & 2: blocked order -- workgroup b walks tiles [b*per, (b+1)*per) in order
+  const int64_t per = (tiles + gridDim.x - 1) / gridDim.x;
+  auto mt = [&](int64_t x) -> int64_t {
+    if constexpr (OPT & 2) return min((x % (int64_t)gridDim.x) * per + x / (int64_t)gridDim.x, last);
+    return x;
+  };
+  int64_t tend = tiles;
+  if constexpr (OPT & 2) {
+    const int64_t mine = min(per, tiles - (int64_t)blockIdx.x * per);
+    if (mine <= 0) return;
+    tend = (int64_t)blockIdx.x + mine * gridDim.x;
+  }
+  d5_issue<R, K>(in, mt(t) * R, stride, tid, n16, WG, dA);
+  d5_issue<R, K>(in, mt(min(t + (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, dB);
+  auto stage = [&](u32x4 (&d)[K]) {
+    d5_write<K>(lds, tid, n16, WG, d);
+    __syncthreads();
+    if (HDR && tid < R) check_frame<HDR>(lds + tid * stride, L, status);
+    d5_columns<R, K2, HDR>(lds, stride, hdr_bm, wk, sf, optr, mt(t) * R);
+    d5_issue<R, K>(in, mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, d);
+    __syncthreads();
+    t += gridDim.x;
+  };
+  for (;;) {
+    stage(dA);
+    if (t >= tend) break;
+    stage(dB);
+    if (t >= tend) break;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
 // Encode v5: R = 64 records per tile, 1024 threads (two workgroups per CU: LDS),
@@ -510,8 +675,43 @@ hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Decode v5: 64 records per tile, 1024 threads (LDS: two workgroups per CU), <= 4
+// row-chunk loads per thread (stride <= 1024 B), <= 3 column-chunk instructions
+// per wave. In-process A/B at 64Mi Struct104 rows (scripts/microbench/fixed_ab.hip,
+// profiles/r02/ab_dec5.jsonl): 17.51 -> 15.31 ms; WG 512 15.65, WG 256 18.00.
+constexpr int kD5R = 64, kD5WG = 1024, kD5K = 4, kD5K2 = 3;
+
+template <int HDR>
+bool decode_v5_fits(const FixedLaunch& L) {
+  return !L.any_nullable && L.cols_aligned16 && kD5R * L.stride <= kD5K * kD5WG * 16 &&
+         (kD5R * L.stride) % 16 == 0 && v3_insn_count<kD5R>(L.group) <= kD5K2 * (kD5WG / 64);
+}
+
+template <int HDR>
+hipError_t launch_decode_v5(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
+  const int64_t full = L.num_rows / kD5R;
+  if (full > 0) {
+    auto* k = &decode_fixed_v5_kernel<kD5R, kD5WG, kD5K, kD5K2, HDR>;
+    raise_lds_cap(k);
+    const size_t lds = (size_t)kD5R * L.stride;
+    const int64_t grid = persistent_grid(k, lds, full, kD5WG);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kD5WG), lds, s, L, L.fields, in, full, status);
+  }
+  if (L.num_rows > full * kD5R) {  // tail (< 64 records): the one-tile kernel
+    FixedLaunch T = L;
+    T.tile0 = full;
+    auto* k = &decode_fixed_kernel<64, HDR, 12>;
+    raise_lds_cap(k);
+    hipLaunchKernelGGL(k, dim3(1), dim3(kWG), (size_t)64 * L.stride, s, T, L.fields, in, status);
+  }
+  return hipGetLastError();
+}
+
 template <int TR, int HDR>
 hipError_t launch_decode_tr(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
+  if constexpr (TR == 64) {
+    if (decode_v5_fits<HDR>(L)) return launch_decode_v5<HDR>(L, in, status, s);
+  }
   const int64_t tiles = (L.num_rows + TR - 1) / TR;
   const size_t lds = (size_t)TR * L.stride;
   // TR = 64: non-temporal LDS-DMA row loads + column stores (17.72 -> 17.52 ms at 64M Struct104)

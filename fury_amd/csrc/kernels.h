@@ -30,6 +30,8 @@ struct FixedLaunch {
   int32_t group[5];             // table index where the 8/4/2/1-byte groups start; group[4] = num_fields
   int64_t tile0;                // first tile of this launch (tail launches after a persistent kernel)
   int64_t xcd_run;              // XCD-grouped tile order: tiles per XCD run (0 = dispatch order)
+  int32_t cols_aligned16;       // decode: every output column 16-byte aligned (decode v5's chunk stores)
+  int32_t pad;
 };
 
 hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s);

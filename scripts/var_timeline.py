@@ -18,7 +18,7 @@ from fury_amd.format import native  # noqa: E402
 from fury_amd.format.encoder import RowEncoder  # noqa: E402
 
 config = sys.argv[1] if len(sys.argv) > 1 else "mixed40"
-n = int(sys.argv[2]) if len(sys.argv) > 2 else bench.DEFAULT_ROWS[config]
+n = int(sys.argv[2]) if len(sys.argv) > 2 else bench.DEFAULT_TOTAL[config]
 dev = torch.device("cuda", 0)
 schema, cols, col_bytes = bench.make_batch(config, n, 0, dev)
 enc = RowEncoder(schema, device=dev)
