@@ -266,10 +266,11 @@ __device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* ld
 // of C tiles. In-process A/B at 64Mi Struct104 rows on four boxes
 // (scripts/microbench/fixed_ab.hip, profiles/r02/ab_fixed_*.jsonl), dispatch order
 // vs grouped: encode R64/WG512 19.16 -> 17.85, 18.08 -> 17.29, 18.13 -> 18.95,
-// 17.89 -> 17.80 ms; R64/WG1024 grouped 17.20, 18.12, 17.82 / 17.61 ms (never
-// slower than dispatch order on a box): the product encode. Decode: within
-// +-0.5 %, so it keeps the dispatch order. C = 0: dispatch order. The last partial
-// block keeps the dispatch order.
+// 17.89 -> 17.80 ms; R64/WG1024 grouped 17.20, 18.12, 17.82 / 17.61 ms. One run
+// per XCD over the whole batch (C = tiles / 8) did better still for the encode
+// (launch_encode_v5); decode v5 is fastest in dispatch order (15.15 vs 15.68 ms
+// grouped, 15.89 XCD-blocked). C = 0: dispatch order. The last partial block
+// keeps the dispatch order.
 __device__ __forceinline__ int64_t map_tile(int64_t t, int64_t tiles, int64_t C) {
   if (C <= 0) return t;
   const int64_t blk = t / (8 * C);
@@ -603,7 +604,7 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
   const int64_t per = (tiles + gridDim.x - 1) / gridDim.x;
   auto mt = [&](int64_t x) -> int64_t {
     if constexpr (OPT & 2) return min((x % (int64_t)gridDim.x) * per + x / (int64_t)gridDim.x, last);
-    return x;
+    return map_tile(x, tiles, L.xcd_run);
   };
   int64_t tend = tiles;
   if constexpr (OPT & 2) {
@@ -635,19 +636,22 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
 // ---------------------------------------------------------------------------
 // Encode v5: R = 64 records per tile, 1024 threads (two workgroups per CU: LDS),
 // <= 3 chunk loads per wave per tile (Struct104: 39 load instructions over 16
-// waves), nt row stores, XCD-grouped tile order.
+// waves), nt column loads and row stores, XCD-blocked tile order (map_tile with
+// runs of tiles/8: every XCD walks one contiguous eighth of the batch, its
+// workgroups on adjacent tiles). In-process A/B at 64Mi Struct104 rows on two
+// boxes (profiles/r02/ab_order_box*.jsonl): runs of grid/8 17.98 / 17.53 ms,
+// XCD-blocked 16.45 / 16.35, + nt column loads 16.38 / 16.12.
 constexpr int kV5R = 64, kV5WG = 1024, kV5K = 3;
 
 template <int HDR>
 hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const int64_t full = L.num_rows / kV5R;
   if (full > 0) {
-    auto* k = &encode_fixed_v5_kernel<kV5R, kV5WG, kV5K, HDR>;
+    auto* k = &encode_fixed_v5_kernel<kV5R, kV5WG, kV5K, HDR, 1>;
     raise_lds_cap(k);
     const size_t lds = (size_t)kV5R * L.stride;
     const int64_t grid = persistent_grid(k, lds, full, kV5WG);
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kV5WG), lds, s, L, L.fields, out, full,
-                       (int64_t)(grid % 8 == 0 ? grid / 8 : 0));
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kV5WG), lds, s, L, L.fields, out, full, (int64_t)(full / 8));
   }
   if (L.num_rows > full * kV5R) {  // tail (< R records): one-tile kernel
     FixedLaunch T = L;

@@ -141,16 +141,14 @@ int main(int argc, char** argv) {
     const unsigned long long bad = diff(rows, rows2, row_bytes);
     report(name, time_ms(f), bad);
   };
-  run("enc_r64_wg512_xcd (product)", &encode_fixed_v5_kernel<64, 512, 6, 0>, 64, 512, -1);
-  run("enc_r64_wg1024_k3_xcd", &encode_fixed_v5_kernel<64, 1024, 3, 0>, 64, 1024, -1);
-  run("enc_r128_wg1024_xcd", &encode_fixed_v5_kernel<128, 1024, 6, 0>, 128, 1024, -1);
+  const int64_t T8 = n / 64 / 8;  // XCD-blocked: each XCD one contiguous eighth of the tiles
+  run("enc_r64_wg1024_k3_xcd (product)", &encode_fixed_v5_kernel<64, 1024, 3, 0>, 64, 1024, -1);
+  run("enc_r64_wg1024_k3_xcdblk", &encode_fixed_v5_kernel<64, 1024, 3, 0>, 64, 1024, T8);
+  run("enc_r64_wg1024_k3_xcdblk_ntload", &encode_fixed_v5_kernel<64, 1024, 3, 0, 1>, 64, 1024, T8);
   run("enc_r64_wg1024_k3_xcd_ntload", &encode_fixed_v5_kernel<64, 1024, 3, 0, 1>, 64, 1024, -1);
-  run("enc_r64_wg1024_k3_blocked", &encode_fixed_v5_kernel<64, 1024, 3, 0, 2>, 64, 1024, 0);
   run("enc_r64_wg1024_k3_blocked_ntload", &encode_fixed_v5_kernel<64, 1024, 3, 0, 3>, 64, 1024, 0);
-  run("enc_r64_wg1024_k3_dispatch", &encode_fixed_v5_kernel<64, 1024, 3, 0>, 64, 1024, 0);
-  run("enc_r64_wg512_k6_blocked_ntload", &encode_fixed_v5_kernel<64, 512, 6, 0, 3>, 64, 512, 0);
   run("enc_r128_wg1024_k6_blocked_ntload", &encode_fixed_v5_kernel<128, 1024, 6, 0, 3>, 128, 1024, 0);
-  run("enc_r64_wg1024_k3_blocked_ntload (again)", &encode_fixed_v5_kernel<64, 1024, 3, 0, 3>, 64, 1024, 0);
+  run("enc_r128_wg1024_k6_xcdblk", &encode_fixed_v5_kernel<128, 1024, 6, 0>, 128, 1024, n / 128 / 8);
   // ---- decode (inputs: the baseline's rows)
   auto dec = [&](int64_t xcd) {
     auto* k = &decode_fixed_kernel<64, 0, 12>;
@@ -172,15 +170,17 @@ int main(int argc, char** argv) {
     report(name, time_ms(f), bad);
   }
   // ---- decode v5 (register-pipelined rows, 16-B column chunks): every column checked
-  auto dec5 = [&](auto* k, int WG) {
+  auto dec5 = [&](auto* k, int WG, int64_t xcd) {
     raise_lds_cap(k);
     const size_t lds = (size_t)64 * 848;
     const int64_t g = persistent_grid(k, lds, tiles, WG);
-    return [=]() { hipLaunchKernelGGL(k, dim3((unsigned)g), dim3(WG), lds, 0, L, L.fields, rows, tiles, status); };
+    FixedLaunch D = L;
+    D.xcd_run = xcd < 0 ? (g % 8 == 0 ? g / 8 : 0) : xcd;
+    return [=]() { hipLaunchKernelGGL(k, dim3((unsigned)g), dim3(WG), lds, 0, D, D.fields, rows, tiles, status); };
   };
-  auto run_dec5 = [&](const char* name, auto* k, int WG) {
+  auto run_dec5 = [&](const char* name, auto* k, int WG, int64_t xcd = 0) {
     for (int c = 0; c < 104; ++c) CHECK(hipMemset(dcols[c], 0, n * width[c]));
-    auto f = dec5(k, WG);
+    auto f = dec5(k, WG, xcd);
     f();
     CHECK(hipDeviceSynchronize());
     unsigned long long bad = 0;
@@ -188,14 +188,13 @@ int main(int argc, char** argv) {
     report(name, time_ms(f), bad);
   };
   run_dec5("dec_v5_wg1024_k4_k3", &decode_fixed_v5_kernel<64, 1024, 4, 3, 0>, 1024);
-  run_dec5("dec_v5_wg512_k7_k5", &decode_fixed_v5_kernel<64, 512, 7, 5, 0>, 512);
-  run_dec5("dec_v5_wg1024_k4_k3_blocked", &decode_fixed_v5_kernel<64, 1024, 4, 3, 0, 2>, 1024);
-  run_dec5("dec_v5_wg512_k7_k5_blocked", &decode_fixed_v5_kernel<64, 512, 7, 5, 0, 2>, 512);
+  run_dec5("dec_v5_wg1024_k4_k3_xcd", &decode_fixed_v5_kernel<64, 1024, 4, 3, 0>, 1024, -1);
+  run_dec5("dec_v5_wg1024_k4_k3_xcdblk", &decode_fixed_v5_kernel<64, 1024, 4, 3, 0>, 1024, T8);
 
   report("dec_tile64 dispatch order (again 2)", time_ms(base_dec), 0);
   run_dec5("dec_v5_wg1024_k4_k3 (again)", &decode_fixed_v5_kernel<64, 1024, 4, 3, 0>, 1024);
-  report("enc_r64_wg512 dispatch order (again)", time_ms(base_enc), 0);
-  run("enc_r64_wg512_xcd (product, again)", &encode_fixed_v5_kernel<64, 512, 6, 0>, 64, 512, -1);
+  run("enc_r64_wg1024_k3_xcd (product, again)", &encode_fixed_v5_kernel<64, 1024, 3, 0>, 64, 1024, -1);
+  run("enc_r64_wg1024_k3_xcdblk (again)", &encode_fixed_v5_kernel<64, 1024, 3, 0>, 64, 1024, T8);
   report("dec_tile64 dispatch order (again)", time_ms(base_dec), 0);
   return 0;
 }

@@ -38,7 +38,12 @@ def test_host_pipeline_parity(name, n, frame):
     out = np.zeros(expect.nbytes, np.uint8)
     hp.encode(cols, n, frame, out)
     bad = np.nonzero(out != expect)[0]
-    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+    if len(bad):
+        stride = expect.nbytes // n
+        rows = np.unique(bad // stride)
+        detail = (f"rows {rows[:6]}..{rows[-3:]} ({len(rows)}), zeros in out: {int((out[bad] == 0).sum())}, "
+                  f"got {out[bad[:8]]}, expected {expect[bad[:8]]}")
+    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}: {detail}"
     dec = empty_like(schema, n)
     hp.decode(expect, n, frame, dec)
     assert columns_equal(schema, cols, dec) == []
