@@ -460,8 +460,8 @@ int prepare_gen(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
     const fory_column& c = cols[idx];
     if (n > 0 && is_var_kind(nd.kind) && p.gnodes[idx].cdepth <= need_level && !c.offsets)
       return fail(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(idx) + " needs offsets");
-    if (n > 0 && p.gnodes[idx].cdepth == 0 && nd.kind != fory_amd::KIND_STRUCT && !is_var_kind(nd.kind) &&
-        !c.values)
+    if (n > 0 && need_level > 0 && p.gnodes[idx].cdepth == 0 && nd.kind != fory_amd::KIND_STRUCT &&
+        !is_var_kind(nd.kind) && !c.values)  // (the sizes passes read no fixed values)
       return fail(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(idx) + " has no values");
     ColumnDev d{};
     d.values = static_cast<const uint8_t*>(c.values);

@@ -682,7 +682,7 @@ int decode_var_stage(fory_host_ctx* c, const void* host_rows, const int64_t* hos
   std::vector<fory_column> d;
   void* ws = nullptr;
   int32_t* status = nullptr;
-  for (int pass = 0; pass < 3 && !rc; ++pass) {
+  for (int pass = 0; pass < 20 && !rc; ++pass) {  // one level of list/map nesting per pass (<= 17)
     // layout for the counts known so far (unknown: no buffers, length 0)
     std::vector<int64_t> kc(N);
     for (int i = 0; i < N; ++i) kc[i] = cnt[i] < 0 ? -1 : cnt[i];

@@ -167,3 +167,25 @@ def test_host_varlen_decode_of_a_sub_range(name):
         ref = oracle.decode(schema, expect[int(eoffs[k]):], eoffs[k:] - eoffs[k], n - k, frame)
         assert columns_equal(schema, ref, dec) == []
         hp.close()
+
+
+@pytest.mark.parametrize("frame", [0, 1])
+@pytest.mark.parametrize("name", ["holder", "lists", "maps_nested", "bean_a", "deep", "chain"])
+def test_host_varlen_nested_collections(name, frame):
+    """The tree engine's shapes (list<list<...>>, List<Bean with strings>, Map<K, Bean>,
+    BeanA, list^9) through the host path: bytes and offsets == the oracle, decode
+    sizes every nesting level (one decode_sizes pass per level) and round-trips; the
+    stream-only decode indexes the frames on the device."""
+    from helpers import nested_columns
+    n = 60 if name == "chain" else 900
+    schema, cols = nested_columns(name, n, 31 + frame)
+    expect, eoffs = oracle.encode(schema, cols, n, frame)
+    hp = HostPipeline(NativePlan(schema))
+    rows, offs = hp.encode_var(cols, n, frame)
+    assert np.array_equal(rows, expect) and np.array_equal(offs, eoffs)
+    assert columns_equal(schema, cols, hp.decode_var(expect, eoffs, n, frame)) == []
+    if frame == 1:
+        dec, consumed = hp.decode_stream(np.concatenate([expect, np.zeros(40, np.uint8)]), n)
+        assert consumed == expect.nbytes
+        assert columns_equal(schema, cols, dec) == []
+    hp.close()
