@@ -92,6 +92,30 @@ int fail_host(int code, const std::string& msg) { return fory_rowfmt_internal_se
 
 int64_t validity_bytes(int64_t rows) { return ((rows + 7) / 8 + 3) / 4 * 4; }
 
+// Caller host memory is copied asynchronously only when it is pinned (registered
+// with fory_rowfmt_host_register / hipHostRegister, or hipHostMalloc): the chunk
+// pipeline orders those copies with events. Pageable memory is copied with a
+// blocking hipMemcpy once the stream's earlier work (and the events it waits on) is
+// done: the async pageable path was seen to leave a chunk kernel reading columns
+// whose H2D had not landed (tests/test_gpu_host.py, intermittent, first rows zero).
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t a{};
+  if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type != hipMemoryTypeUnregistered;
+}
+
+int hcopy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s, const char* what) {
+  if (bytes == 0) return FORY_OK;
+  if (host_pinned(kind == hipMemcpyHostToDevice ? src : dst))
+    return hip_check(hipMemcpyAsync(dst, src, bytes, kind, s), what);
+  int rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (!rc) rc = hip_check(hipMemcpy(dst, src, bytes, kind), what);
+  return rc;
+}
+
 // Chunk k's row range.
 void chunk_range(const fory_host_ctx* c, int64_t n, int64_t k, int64_t* a, int64_t* rows) {
   *a = k * c->chunk;
@@ -262,8 +286,7 @@ int d2h_rows_windows(const OutWindows& W, const uint8_t* src, int64_t a, int64_t
   for (size_t w = 0; w + 1 < W.first.size() && !rc; ++w) {
     const int64_t lo = std::max(a, W.first[w]), hi = std::min(a + rows, W.first[w + 1]);
     if (lo >= hi) continue;
-    rc = hip_check(hipMemcpyAsync(W.ptr[w] + (lo - W.first[w]) * stride, src + (lo - a) * stride,
-                                  (size_t)((hi - lo) * stride), hipMemcpyDeviceToHost, s), "D2H");
+    rc = hcopy(W.ptr[w] + (lo - W.first[w]) * stride, src + (lo - a) * stride, (size_t)((hi - lo) * stride), hipMemcpyDeviceToHost, s, "D2H");
   }
   return rc;
 }
@@ -297,11 +320,9 @@ int host_encode_fixed(fory_host_ctx* c, const fory_column* host_cols, int64_t n,
     if (k >= 2) rc = hip_check(hipStreamWaitEvent(c->s_in, c->ev_k[b], 0), "hipStreamWaitEvent");
     for (int i = 0; i < c->info.num_columns && !rc; ++i) {
       const fory_column& h = host_cols[i];
-      rc = hip_check(hipMemcpyAsync(B.cols[i].values, static_cast<const uint8_t*>(h.values) + a * c->width[i],
-                                    (size_t)(rows * c->width[i]), hipMemcpyHostToDevice, c->s_in), "H2D");
+      rc = hcopy(B.cols[i].values, static_cast<const uint8_t*>(h.values) + a * c->width[i], (size_t)(rows * c->width[i]), hipMemcpyHostToDevice, c->s_in, "H2D");
       if (!rc && c->nullable[i] && h.validity)
-        rc = hip_check(hipMemcpyAsync(B.cols[i].validity, h.validity + a / 8, (size_t)((rows + 7) / 8),
-                                      hipMemcpyHostToDevice, c->s_in), "H2D validity");
+        rc = hcopy(B.cols[i].validity, h.validity + a / 8, (size_t)((rows + 7) / 8), hipMemcpyHostToDevice, c->s_in, "H2D validity");
       dcols[i] = fory_column{B.cols[i].values, nullptr, (c->nullable[i] && h.validity) ? B.cols[i].validity : nullptr,
                              rows, rows * c->width[i]};
     }
@@ -376,8 +397,7 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
     fory_host_ctx::Buf& B = c->buf[b];
     if (k >= 2) rc = hip_check(hipStreamWaitEvent(c->s_in, c->ev_k[b], 0), "hipStreamWaitEvent");
     if (!rc)
-      rc = hip_check(hipMemcpyAsync(B.rows, in + a * stride, (size_t)(rows * stride), hipMemcpyHostToDevice, c->s_in),
-                     "H2D");
+      rc = hcopy(B.rows, in + a * stride, (size_t)(rows * stride), hipMemcpyHostToDevice, c->s_in, "H2D");
     if (!rc) rc = hip_check(hipEventRecord(c->ev_in[b], c->s_in), "hipEventRecord");
     if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_k, c->ev_in[b], 0), "hipStreamWaitEvent");
     if (!rc && k >= 2) rc = hip_check(hipStreamWaitEvent(c->s_k, c->ev_out[b], 0), "hipStreamWaitEvent");
@@ -391,11 +411,9 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
     if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_out, c->ev_k[b], 0), "hipStreamWaitEvent");
     for (int i = 0; i < c->info.num_columns && !rc; ++i) {
       const fory_column& h = host_out_cols[i];
-      rc = hip_check(hipMemcpyAsync(static_cast<uint8_t*>(h.values) + a * c->width[i], B.cols[i].values,
-                                    (size_t)(rows * c->width[i]), hipMemcpyDeviceToHost, c->s_out), "D2H");
+      rc = hcopy(static_cast<uint8_t*>(h.values) + a * c->width[i], B.cols[i].values, (size_t)(rows * c->width[i]), hipMemcpyDeviceToHost, c->s_out, "D2H");
       if (!rc && dcols[i].validity)
-        rc = hip_check(hipMemcpyAsync(h.validity + a / 8, B.cols[i].validity, (size_t)((rows + 7) / 8),
-                                      hipMemcpyDeviceToHost, c->s_out), "D2H validity");
+        rc = hcopy(h.validity + a / 8, B.cols[i].validity, (size_t)((rows + 7) / 8), hipMemcpyDeviceToHost, c->s_out, "D2H validity");
     }
     if (!rc) rc = hip_check(hipEventRecord(c->ev_out[b], c->s_out), "hipEventRecord");
   }
@@ -528,13 +546,11 @@ int host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, i
   for (int i = 0; i < N && !rc; ++i) {  // H2D of every column
     const fory_column& h = host_cols[i];
     if (d[i].values && vbytes[i] > 0)
-      rc = hip_check(hipMemcpyAsync(d[i].values, h.values, (size_t)vbytes[i], hipMemcpyHostToDevice, c->s_k), "H2D");
+      rc = hcopy(d[i].values, h.values, (size_t)vbytes[i], hipMemcpyHostToDevice, c->s_k, "H2D");
     if (!rc && d[i].offsets)
-      rc = hip_check(hipMemcpyAsync(d[i].offsets, h.offsets, (size_t)(cnt[i] + 1) * 4, hipMemcpyHostToDevice, c->s_k),
-                     "H2D offsets");
+      rc = hcopy(d[i].offsets, h.offsets, (size_t)(cnt[i] + 1) * 4, hipMemcpyHostToDevice, c->s_k, "H2D offsets");
     if (!rc && d[i].validity)
-      rc = hip_check(hipMemcpyAsync(d[i].validity, h.validity, (size_t)((cnt[i] + 7) / 8), hipMemcpyHostToDevice,
-                                    c->s_k), "H2D validity");
+      rc = hcopy(d[i].validity, h.validity, (size_t)((cnt[i] + 7) / 8), hipMemcpyHostToDevice, c->s_k, "H2D validity");
   }
   if (!rc) rc = hip_check(hipMemsetAsync(status, 0, 4, c->s_k), "hipMemsetAsync");
   if (!rc) rc = fory_rowfmt_encoded_size(c->plan, d.data(), n, frame, d_offs, ws, ws_bytes, c->s_k);
@@ -545,7 +561,7 @@ int host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, i
     tmp.resize((size_t)n + 1);
     ho = tmp.data();
   }
-  if (!rc) rc = hip_check(hipMemcpyAsync(ho, d_offs, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, c->s_k), "D2H offsets");
+  if (!rc) rc = hcopy(ho, d_offs, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, c->s_k, "D2H offsets");
   if (!rc) rc = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize");
   if (rc) return rc;
   const int64_t total = ho[n];
@@ -559,8 +575,7 @@ int host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, i
   for (size_t w = 0; w + 1 < W->first.size() && !rc; ++w) {  // each window: its rows' contiguous bytes
     const int64_t lo = ho[W->first[w]], hi = ho[W->first[w + 1]];
     if (hi > lo)
-      rc = hip_check(hipMemcpyAsync(W->ptr[w], c->drows + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, c->s_k),
-                     "D2H rows");
+      rc = hcopy(W->ptr[w], c->drows + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, c->s_k, "D2H rows");
   }
   if (!rc) rc = fory_rowfmt_read_status(status, c->s_k);  // synchronises the stream
   return rc;
@@ -642,14 +657,12 @@ int decode_var_stage(fory_host_ctx* c, const void* host_rows, const int64_t* hos
   int64_t* d_offs = reinterpret_cast<int64_t*>(c->drows + rows_sz);
   int32_t* istatus = reinterpret_cast<int32_t*>(c->drows + rows_sz + offs_sz);
   if (r1 > r0)
-    rc = hip_check(hipMemcpyAsync(drow0, static_cast<const uint8_t*>(host_rows) + r0, (size_t)(r1 - r0),
-                                  hipMemcpyHostToDevice, c->s_k), "H2D rows");
+    rc = hcopy(drow0, static_cast<const uint8_t*>(host_rows) + r0, (size_t)(r1 - r0), hipMemcpyHostToDevice, c->s_k, "H2D rows");
   if (host_row_offsets) {  // row offsets relative to the staged run
     std::vector<int64_t> rel_offs((size_t)n + 1);
     for (int64_t k = 0; k <= n; ++k) rel_offs[(size_t)k] = host_row_offsets[k] - r0;
     if (!rc)
-      rc = hip_check(hipMemcpyAsync(d_offs, rel_offs.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->s_k),
-                     "H2D row offsets");
+      rc = hcopy(d_offs, rel_offs.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->s_k, "H2D row offsets");
     if (!rc) rc = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize");  // rel_offs is pageable
     if (consumed) *consumed = r1;
   } else {  // Encoder.decode(MemoryBuffer) x n over the stream alone
@@ -658,7 +671,7 @@ int decode_var_stage(fory_host_ctx* c, const void* host_rows, const int64_t* hos
       rc = fory_rowfmt_index_frames(c->plan, drow0, r1 - r0, n, frame, d_offs, istatus,
                                     c->drows + rows_sz + offs_sz + kAlign, iws, c->s_k);
     int64_t end = 0;
-    if (!rc) rc = hip_check(hipMemcpyAsync(&end, d_offs + n, 8, hipMemcpyDeviceToHost, c->s_k), "D2H frame end");
+    if (!rc) rc = hcopy(&end, d_offs + n, 8, hipMemcpyDeviceToHost, c->s_k, "D2H frame end");
     if (!rc) rc = fory_rowfmt_read_status(istatus, c->s_k);  // synchronises the stream
     if (rc) return rc;
     if (consumed) *consumed = end;
@@ -703,7 +716,7 @@ int decode_var_stage(fory_host_ctx* c, const void* host_rows, const int64_t* hos
     std::vector<int32_t> tot(N, 0);
     for (int i = 0; i < N && !rc; ++i)
       if (d[i].offsets && kc[i] >= 0)
-        rc = hip_check(hipMemcpyAsync(&tot[i], d[i].offsets + kc[i], 4, hipMemcpyDeviceToHost, c->s_k), "D2H totals");
+        rc = hcopy(&tot[i], d[i].offsets + kc[i], 4, hipMemcpyDeviceToHost, c->s_k, "D2H totals");
     if (!rc) rc = fory_rowfmt_read_status(status, c->s_k);
     if (rc) break;
     bool changed = false;
@@ -810,14 +823,11 @@ int fory_rowfmt_host_decode_var(fory_host_ctx* c, const fory_column* host_out_co
   for (int i = 0; i < N && !rc; ++i) {  // D2H of every column
     const fory_column& h = host_out_cols[i];
     if (d[i].values && c->dec_bytes[i] > 0)
-      rc = hip_check(hipMemcpyAsync(h.values, d[i].values, (size_t)c->dec_bytes[i], hipMemcpyDeviceToHost, c->s_k),
-                     "D2H values");
+      rc = hcopy(h.values, d[i].values, (size_t)c->dec_bytes[i], hipMemcpyDeviceToHost, c->s_k, "D2H values");
     if (!rc && d[i].offsets)
-      rc = hip_check(hipMemcpyAsync(h.offsets, d[i].offsets, (size_t)(kc[i] + 1) * 4, hipMemcpyDeviceToHost, c->s_k),
-                     "D2H offsets");
+      rc = hcopy(h.offsets, d[i].offsets, (size_t)(kc[i] + 1) * 4, hipMemcpyDeviceToHost, c->s_k, "D2H offsets");
     if (!rc && d[i].validity)
-      rc = hip_check(hipMemcpyAsync(h.validity, d[i].validity, (size_t)((kc[i] + 7) / 8), hipMemcpyDeviceToHost,
-                                    c->s_k), "D2H validity");
+      rc = hcopy(h.validity, d[i].validity, (size_t)((kc[i] + 7) / 8), hipMemcpyDeviceToHost, c->s_k, "D2H validity");
   }
   if (!rc) rc = fory_rowfmt_read_status(status, c->s_k);
   return rc;

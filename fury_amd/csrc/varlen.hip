@@ -1370,11 +1370,12 @@ __device__ __forceinline__ void flat_dec_struct_bases(const VarLaunch& L, const 
   }
 }
 
-// PROF: thread 0 stamps s_memrealtime (100 MHz) at phase boundaries into
-// L.prof[tile * 8 + k] (debug timeline, FORY_ROWFMT_VARPROF=1).
+// Debug timeline (FORY_ROWFMT_VARPROF=1, L.prof set): thread 0 stamps
+// s_memrealtime (100 MHz) at phase boundaries into L.prof[tile * 8 + k] (a uniform
+// branch when off; the PROF template parameter is always false now).
 #define FLAT_STAMP(k)                                                                            \
   do {                                                                                          \
-    if (PROF && tid == 0) L.prof[tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime();            \
+    if (L.prof && tid == 0) L.prof[tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime();          \
   } while (0)
 
 // Encode tile kernel body, compiled as two kernels: the default register budget
@@ -1563,7 +1564,7 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
     flat_enc_fixed<2, NW>(L, fix, L.fix_group[2], L.fix_group[3], jb[2], jb[4], wave, lane, live, i, row, st, sbase);
     flat_enc_fixed<1, NW>(L, fix, L.fix_group[3], L.fix_group[4], jb[3], jb[4], wave, lane, live, i, row, st, sbase);
   }
-  if (PROF) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (L.prof) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   FLAT_STAMP(3);
   __syncthreads();
   FLAT_STAMP(4);
@@ -1605,7 +1606,7 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
       lo = hi;
     }
   }
-  if (PROF) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (L.prof) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   FLAT_STAMP(5);
   __syncthreads();
   FLAT_STAMP(6);
@@ -1624,7 +1625,7 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
       }
     }
   }
-  if (PROF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (L.prof) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   FLAT_STAMP(7);
   };
   if (!SPILL) {
@@ -2120,6 +2121,18 @@ bool var_flat(const VarLaunch& L) {
 
 constexpr int kNW = 4;  // waves per 64-record tile of the cooperative kernels (8 was slower at every occupancy)
 
+// Waves per tile: 4, or 2 for plans with at most two var fields, whose small tiles
+// leave waves idle (the layout is wave 0's; two waves per tile double the tiles in
+// flight per CU). bench A/B on one box (profiles/r02/nw/): Nested encode 1.215 ->
+// 0.896 ms, decode 1.043 -> 0.766 ms (1 wave: 1.47 ms); Mixed (8 strings) is best at
+// 4 (2 waves: encode 4.60 -> 6.64 ms, decode 4.08 -> 5.90 ms).
+// FORY_ROWFMT_VARNW=2|4 forces one (tests).
+int flat_waves(const VarLaunch& L) {
+  const char* e = getenv("FORY_ROWFMT_VARNW");
+  if (e && (atoi(e) == 2 || atoi(e) == 4)) return atoi(e);
+  return L.num_var <= 2 ? 2 : 4;
+}
+
 size_t sbase_lds(const VarLaunch& L) {
   return L.num_struct ? (size_t)(1 + L.num_struct) * 64 * sizeof(int32_t) : 0;
 }
@@ -2267,8 +2280,7 @@ void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, i
 template <int HDR, int NW>
 void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                      int cap, hipStream_t s) {
-  if (L.prof) launch_flat_enc_t<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
-  else launch_flat_enc_t<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
+  launch_flat_enc_t<HDR, NW, false>(L, offs, out, capacity, status, cap, s);  // (timeline stamps: runtime L.prof)
 }
 
 template <int HDR, bool WRITE, int NW>
@@ -2305,6 +2317,14 @@ hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const
   if (L.num_rows <= 0) return hipSuccess;
   if (var_tiles() && var_flat(L)) {
     const int cap = fit_cap(L, L.mean_row);
+    if (flat_waves(L) == 2) {
+      switch (frame_header_bytes(L.frame)) {
+        case 12: launch_flat_dec<12, WRITE, 2>(L, rows, offs, tile_tot, status, cap, s); break;
+        case 8: launch_flat_dec<8, WRITE, 2>(L, rows, offs, tile_tot, status, cap, s); break;
+        default: launch_flat_dec<0, WRITE, 2>(L, rows, offs, tile_tot, status, cap, s); break;
+      }
+      return hipGetLastError();
+    }
     switch (frame_header_bytes(L.frame)) {
       case 12: launch_flat_dec<12, WRITE, kNW>(L, rows, offs, tile_tot, status, cap, s); break;
       case 8: launch_flat_dec<8, WRITE, kNW>(L, rows, offs, tile_tot, status, cap, s); break;
@@ -2338,6 +2358,14 @@ hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* o
   if (L.num_rows <= 0) return hipSuccess;
   if (var_tiles() && var_flat(L)) {
     const int cap = enc_cap(L, capacity);
+    if (flat_waves(L) == 2) {
+      switch (frame_header_bytes(L.frame)) {
+        case 12: launch_flat_enc<12, 2>(L, offs, out, capacity, status, cap, s); break;
+        case 8: launch_flat_enc<8, 2>(L, offs, out, capacity, status, cap, s); break;
+        default: launch_flat_enc<0, 2>(L, offs, out, capacity, status, cap, s); break;
+      }
+      return hipGetLastError();
+    }
     switch (frame_header_bytes(L.frame)) {
       case 12: launch_flat_enc<12, kNW>(L, offs, out, capacity, status, cap, s); break;
       case 8: launch_flat_enc<8, kNW>(L, offs, out, capacity, status, cap, s); break;

@@ -41,8 +41,10 @@ def test_host_pipeline_parity(name, n, frame):
     if len(bad):
         stride = expect.nbytes // n
         rows = np.unique(bad // stride)
+        r0 = rows[0]
+        rb = bad[bad // stride == r0] - r0 * stride
         detail = (f"rows {rows[:6]}..{rows[-3:]} ({len(rows)}), zeros in out: {int((out[bad] == 0).sum())}, "
-                  f"got {out[bad[:8]]}, expected {expect[bad[:8]]}")
+                  f"row {r0} bad byte offsets {rb[:64].tolist()}, got {out[bad[:8]]}, expected {expect[bad[:8]]}")
     assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}: {detail}"
     dec = empty_like(schema, n)
     hp.decode(expect, n, frame, dec)

@@ -42,20 +42,21 @@ VARLEN = [k for k, (sch, _) in catalog().items()
 FIXED = [k for k in catalog() if k not in VARLEN]
 
 
-@pytest.fixture(params=["flat", "flat_stg256", "tile", "global", "spill", "nocap", "tile_nocap"])
+@pytest.fixture(params=["flat", "flat_stg256", "tile", "global", "spill", "nocap", "tile_nocap", "waves2", "waves4"])
 def varlen_engine(request, monkeypatch):
     """Varlen engines: flat cooperative tile kernels (default for flat plans), the
     generic one-wave tile interpreter (FORY_ROWFMT_VARFLAT=0), the per-record global
     interpreter (FORY_ROWFMT_VARTILE=0); a 2 KiB LDS image so tiles spill to the second
     (big-image) launch; 2 KiB for both launches so tiles take the per-record global path
     inside the tile kernels (flat and generic); flat with a 256-byte staging buffer
-    (most spans take the per-lane copy)."""
+    (most spans take the per-lane copy); cooperative tiles of 2 / 4 waves forced."""
     env = {"flat": {}, "flat_stg256": {"FORY_ROWFMT_VARSTG": "256"},
            "tile": {"FORY_ROWFMT_VARFLAT": "0"}, "global": {"FORY_ROWFMT_VARTILE": "0"},
            "spill": {"FORY_ROWFMT_VARCAP": "2048"},
            "nocap": {"FORY_ROWFMT_VARCAP": "2048", "FORY_ROWFMT_SPILLCAP": "2048"},
            "tile_nocap": {"FORY_ROWFMT_VARFLAT": "0", "FORY_ROWFMT_VARCAP": "2048",
-                          "FORY_ROWFMT_SPILLCAP": "2048"}}[request.param]
+                          "FORY_ROWFMT_SPILLCAP": "2048"},
+           "waves2": {"FORY_ROWFMT_VARNW": "2"}, "waves4": {"FORY_ROWFMT_VARNW": "4"}}[request.param]
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     return request.param
@@ -251,3 +252,25 @@ def test_hashed_frames_schema_mismatch_raises():
         bad[o + 3] ^= 0x04
         with pytest.raises(ClassNotCompatibleException):
             enc.decode(EncodedRows(bad, rows.offsets, 200, 3, rows.stride))
+
+
+@pytest.mark.parametrize("shift", [0, 8, 24])
+def test_fixed_decode_into_unaligned_columns(shift):
+    """Decode v5 stores 16-B column chunks: output columns that are not 16-byte aligned
+    take the one-tile kernel; both give the input columns back (tail tile included)."""
+    schema, make = catalog()["struct104"]
+    n = 64 * 37 + 5
+    cols = make(n, 3)
+    enc = encoder_for("struct104")
+    rows = enc.encode(to_device(cols), n, 0)
+    outs, backing = [], []
+    for c in enc.alloc_fixed_outputs(n):
+        k = c.values.element_size()
+        big = torch.empty(n * k + 64, dtype=torch.uint8, device="cuda")
+        backing.append(big)
+        c.values = big[shift:shift + n * k].view(c.values.dtype)
+        outs.append(c)
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    native.decode(enc.plan, rows.buffer, None, n, 0, native.column_array(outs), status, enc.workspace(n))
+    native.read_status(status)
+    assert columns_equal(schema, cols, to_host(outs)) == []
