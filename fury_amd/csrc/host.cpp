@@ -49,9 +49,21 @@ struct fory_host_ctx {
   int64_t ws_bytes = 0;
   hipStream_t s_in = nullptr, s_k = nullptr, s_out = nullptr;
   hipEvent_t ev_in[2] = {}, ev_k[2] = {}, ev_out[2] = {};
-  // varlen plans (whole batch per call; device buffers kept and grown)
+  // varlen plans: encode pipelined over two chunk slots (grown on demand), decode
+  // whole batch per call (device buffers kept and grown)
   bool varlen = false;
   std::vector<int32_t> kind, parent;
+  struct VarSlot {
+    uint8_t* dev = nullptr;  // column slices, row offsets, workspace
+    int64_t dev_bytes = 0;
+    uint8_t* rows = nullptr;  // the chunk's rows / frames
+    int64_t rows_bytes = 0;
+    int64_t* pin = nullptr;  // pinned host copy of the chunk's row offsets
+    int64_t pin_words = 0;
+    bool used = false;  // events of this slot have been recorded
+  } vs[2];
+  hipEvent_t ev_sz[2] = {};
+  int32_t* vstatus = nullptr;  // one status word per slot (sticky over a call)
   uint8_t* dbuf = nullptr;   // columns, row offsets, workspace, status
   int64_t dbuf_bytes = 0;
   uint8_t* drows = nullptr;  // rows / frames
@@ -134,11 +146,14 @@ int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t c
   fory_plan_info info{};
   int rc = fory_rowfmt_plan_info(plan, &info);
   if (rc) return rc;
+  if (chunk_rows <= 0) chunk_rows = 1 << 20;
+  chunk_rows = (chunk_rows + 63) / 64 * 64;  // whole 64-record tiles: validity slices are byte aligned
   if (!info.fixed_width) {  // varlen: fory_rowfmt_host_encode_var / host_decode_var_sizes / host_decode_var
     fory_host_ctx* c = new fory_host_ctx();
     c->plan = plan;
     c->info = info;
     c->device = device;
+    c->chunk = chunk_rows;
     c->varlen = true;
     c->kind.resize(info.num_columns);
     c->parent.resize(info.num_columns);
@@ -146,7 +161,12 @@ int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t c
     c->nullable.resize(info.num_columns);
     fory_rowfmt_internal_node_layout(plan, c->kind.data(), c->width.data(), c->nullable.data(), c->parent.data());
     rc = hip_check(hipSetDevice(device), "hipSetDevice");
-    if (!rc) rc = hip_check(hipStreamCreateWithFlags(&c->s_k, hipStreamNonBlocking), "hipStreamCreate");
+    for (hipStream_t* s : {&c->s_in, &c->s_k, &c->s_out})
+      if (!rc) rc = hip_check(hipStreamCreateWithFlags(s, hipStreamNonBlocking), "hipStreamCreate");
+    for (int b = 0; b < 2 && !rc; ++b)
+      for (hipEvent_t* e : {&c->ev_in[b], &c->ev_k[b], &c->ev_out[b], &c->ev_sz[b]})
+        if (!rc) rc = hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
+    if (!rc) rc = hip_check(hipMalloc(&c->vstatus, kAlign), "hipMalloc(status)");
     if (rc) {
       fory_rowfmt_host_ctx_destroy(c);
       return rc;
@@ -154,8 +174,6 @@ int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t c
     *out = c;
     return FORY_OK;
   }
-  if (chunk_rows <= 0) chunk_rows = 1 << 20;
-  chunk_rows = (chunk_rows + 63) / 64 * 64;  // whole 64-record tiles: validity slices are byte aligned
   fory_host_ctx* c = new fory_host_ctx();
   c->plan = plan;
   c->info = info;
@@ -217,12 +235,17 @@ void fory_rowfmt_host_ctx_destroy(fory_host_ctx* c) {
   if (c->s_in) (void)hipStreamSynchronize(c->s_in);
   if (c->s_k) (void)hipStreamSynchronize(c->s_k);
   if (c->s_out) (void)hipStreamSynchronize(c->s_out);
-  for (int b = 0; b < 2; ++b)
-    for (hipEvent_t e : {c->ev_in[b], c->ev_k[b], c->ev_out[b]})
+  for (int b = 0; b < 2; ++b) {
+    for (hipEvent_t e : {c->ev_in[b], c->ev_k[b], c->ev_out[b], c->ev_sz[b]})
       if (e) (void)hipEventDestroy(e);
+    for (uint8_t* p : {c->vs[b].dev, c->vs[b].rows})
+      if (p) (void)hipFree(p);
+    if (c->vs[b].pin) (void)hipHostFree(c->vs[b].pin);
+  }
   for (hipStream_t s : {c->s_in, c->s_k, c->s_out})
     if (s) (void)hipStreamDestroy(s);
   if (c->arena) (void)hipFree(c->arena);
+  if (c->vstatus) (void)hipFree(c->vstatus);
   for (uint8_t* b : {c->dbuf, c->drows, c->dout})
     if (b) (void)hipFree(b);
   delete c;
@@ -501,83 +524,274 @@ int64_t carve(fory_host_ctx* c, uint8_t* base, const std::vector<int64_t>& cnt, 
 
 namespace {
 
+// Chunk k's slice of a varlen batch (rows [a, a + rows)) per pre-order column:
+// elements [lo, hi) are the chunk's own — the rows themselves at the top level and in
+// struct fields, below a list/map the children its offsets name. The H2D copies
+// start at aligned host positions and the device column pointers are biased back
+// ("virtual bases"): the kernels index a slice with the host's absolute element
+// indices and offsets (top level: chunk-row indices), so nothing is rebased.
+struct VarSlice {
+  int64_t lo = 0, hi = 0;  // absolute element range
+  int64_t s = 0;           // absolute element the kernels' index 0 denotes (a at the top, 0 below a list/map)
+  int64_t v0 = 0, v1 = 0;  // host value bytes copied (v0 16-byte aligned)
+  int64_t o0 = 0;          // first offsets entry copied (a multiple of 4), through entry hi
+  int64_t h0 = 0, h1 = 0;  // host validity bytes copied (h0 a multiple of 8)
+  bool validity = false;
+};
+
+constexpr int64_t kSlack = 64;  // the kernels' aligned loads may read past a span's end
+
+int var_slices(const fory_host_ctx* c, const fory_column* h, int64_t a, int64_t rows, std::vector<VarSlice>* out) {
+  const int N = c->info.num_columns;
+  out->assign((size_t)N, VarSlice{});
+  for (int i = 0; i < N; ++i) {
+    VarSlice& v = (*out)[(size_t)i];
+    const int p = c->parent[i];
+    if (p < 0) {
+      v.lo = a, v.hi = a + rows, v.s = a;
+    } else if (c->kind[p] == kKindStruct) {
+      v.lo = (*out)[(size_t)p].lo, v.hi = (*out)[(size_t)p].hi, v.s = (*out)[(size_t)p].s;
+    } else {  // list items / map entries of the chunk
+      v.lo = h[p].offsets[(*out)[(size_t)p].lo];
+      v.hi = h[p].offsets[(*out)[(size_t)p].hi];
+      v.s = 0;
+      if (v.lo < 0 || v.hi < v.lo) return fail_host(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(p) + " offsets decrease");
+    }
+    if (c->kind[i] == kKindFixed || c->kind[i] == kKindBool) {
+      v.v0 = (v.lo * c->width[i]) & ~int64_t(15);
+      v.v1 = v.hi * c->width[i];
+    } else if (c->kind[i] == kKindBytes) {
+      const int64_t b0 = h[i].offsets[v.lo], b1 = h[i].offsets[v.hi];
+      if (b0 < 0 || b1 < b0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(i) + " offsets decrease");
+      v.v0 = b0 & ~int64_t(15);
+      v.v1 = b1;
+    }
+    if (v.v1 > v.v0 && !h[i].values)
+      return fail_host(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(i) + " has no values");
+    v.o0 = v.lo & ~int64_t(3);
+    v.validity = c->nullable[i] && h[i].validity;
+    if (v.validity) {
+      v.h0 = (v.lo >> 3) & ~int64_t(7);
+      v.h1 = (v.hi + 7) >> 3;
+    }
+  }
+  return FORY_OK;
+}
+
+// Bytes of a slot's device region for these slices (base null), or carves it: the
+// biased device columns, the chunk's row offsets and the workspace.
+int64_t carve_slices(const fory_host_ctx* c, const std::vector<VarSlice>& sl, int64_t rows, int64_t ws_bytes,
+                     uint8_t* base, std::vector<fory_column>* cols, int64_t** d_offs, void** ws) {
+  int64_t at = 0;
+  const int N = (int)sl.size();
+  if (cols) cols->assign((size_t)N, fory_column{});
+  for (int i = 0; i < N; ++i) {
+    const VarSlice& v = sl[(size_t)i];
+    fory_column d{};
+    d.length = v.hi - v.lo;
+    if (c->kind[i] == kKindFixed || c->kind[i] == kKindBool || c->kind[i] == kKindBytes) {
+      const int64_t bias = c->kind[i] == kKindBytes ? -v.v0 : v.s * c->width[i] - v.v0;
+      if (base) d.values = base + at + bias;
+      d.capacity = v.v1 - v.v0;
+      at += align_up(v.v1 - v.v0 + kSlack);
+    }
+    if (has_offsets(c->kind[i])) {
+      if (base) d.offsets = reinterpret_cast<int32_t*>(base + at) + (v.s - v.o0);
+      at += align_up((v.hi - v.o0 + 1) * 4 + kSlack);
+    }
+    if (v.validity) {
+      if (base) d.validity = base + at + ((v.s >> 3) - v.h0);
+      at += align_up(v.h1 - v.h0 + kSlack);
+    }
+    if (cols) (*cols)[(size_t)i] = d;
+  }
+  if (d_offs) *d_offs = base ? reinterpret_cast<int64_t*>(base + at) : nullptr;
+  at += align_up((rows + 1) * 8);
+  if (ws) *ws = base ? base + at : nullptr;
+  at += align_up(ws_bytes);
+  return at;
+}
+
+// H2D of the slices into a slot's carved region (the unbiased region starts).
+int h2d_slices(const fory_host_ctx* c, const fory_column* h, const std::vector<VarSlice>& sl,
+               const std::vector<fory_column>& d, hipStream_t s) {
+  int rc = FORY_OK;
+  for (size_t i = 0; i < sl.size() && !rc; ++i) {
+    const VarSlice& v = sl[i];
+    if (d[i].values && v.v1 > v.v0) {
+      const int64_t bias = c->kind[i] == kKindBytes ? -v.v0 : v.s * c->width[i] - v.v0;
+      rc = hcopy(static_cast<uint8_t*>(d[i].values) - bias, static_cast<const uint8_t*>(h[i].values) + v.v0,
+                 (size_t)(v.v1 - v.v0), hipMemcpyHostToDevice, s, "H2D values");
+    }
+    if (!rc && d[i].offsets)
+      rc = hcopy(d[i].offsets - (v.s - v.o0), h[i].offsets + v.o0, (size_t)(v.hi - v.o0 + 1) * 4,
+                 hipMemcpyHostToDevice, s, "H2D offsets");
+    if (!rc && v.validity && v.h1 > v.h0)
+      rc = hcopy(d[i].validity - ((v.s >> 3) - v.h0), h[i].validity + v.h0, (size_t)(v.h1 - v.h0),
+                 hipMemcpyHostToDevice, s, "H2D validity");
+  }
+  return rc;
+}
+
+// Varlen encode, chunk pipeline over two slots. Per chunk k (slot b = k & 1):
+//   s_in : H2D of its column slices -> encoded_size (row sizes + scan) -> D2H of its
+//          row offsets to pinned memory (ev_sz)
+//   host : waits for ev_sz, places the chunk after the rows so far (windows, output
+//          row offsets), grows the slot's row buffer if needed
+//   s_k  : encode into the slot's row buffer (ev_k)
+//   s_out: D2H of the rows into their window(s) (ev_out)
+// Chunk k+1 is staged before chunk k's encode is queued, so H2D (k+1) || encode (k)
+// || D2H (k-1). A window overflow stops the copies; the remaining chunks are only
+// sized, so *out_bytes reports the total (then FORY_ERR_CAPACITY).
 int host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, int32_t frame, OutWindows* W,
                     int64_t* host_row_offsets, int64_t* out_bytes) {
   if (!c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "fixed-width plan: use fory_rowfmt_host_encode");
   if (n < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
   if (out_bytes) *out_bytes = 0;
+  const int64_t nw = (int64_t)W->cap.size();
   if (n == 0) {
     if (host_row_offsets) host_row_offsets[0] = 0;
+    W->first.assign((size_t)nw + 1, 0);
     return FORY_OK;
   }
   if (!host_cols) return fail_host(FORY_ERR_INVALID_ARGUMENT, "host columns are null");
-  // the encode reuses the device buffers a staged decode lives in: a later
-  // host_decode_var must be preceded by a fresh host_decode_var_sizes
+  // a context serves one call at a time: a staged decode does not survive an encode
   c->dec_n = -1;
   const int N = c->info.num_columns;
-  // element count and value bytes of every column, from the host offsets
-  std::vector<int64_t> cnt(N, 0), vbytes(N, 0);
-  std::vector<char> want_validity(N, 0);
-  for (int i = 0; i < N; ++i) {
-    const int p = c->parent[i];
-    if (p < 0) cnt[i] = n;
-    else if (c->kind[p] == kKindStruct) cnt[i] = cnt[p];
-    else cnt[i] = cnt[p] > 0 ? host_cols[p].offsets[cnt[p]] : 0;  // list items / map entries
-    const fory_column& h = host_cols[i];
-    if (has_offsets(c->kind[i]) && !h.offsets)
+  for (int i = 0; i < N; ++i)
+    if (has_offsets(c->kind[i]) && !host_cols[i].offsets)
       return fail_host(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(i) + " needs offsets");
-    if (c->kind[i] == kKindFixed || c->kind[i] == kKindBool) vbytes[i] = cnt[i] * c->width[i];
-    else if (c->kind[i] == kKindBytes) vbytes[i] = cnt[i] > 0 ? h.offsets[cnt[i]] : 0;
-    if (vbytes[i] > 0 && !h.values)
-      return fail_host(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(i) + " has no values");
-    want_validity[i] = c->nullable[i] && h.validity;
-  }
   int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
-  const int64_t ws_bytes = fory_rowfmt_workspace_bytes(c->plan, n);
-  rc = ensure(c, &c->dbuf, &c->dbuf_bytes, carve(c, nullptr, cnt, vbytes, want_validity, n, nullptr, nullptr,
-                                                 nullptr, ws_bytes, nullptr));
-  if (rc) return rc;
-  std::vector<fory_column> d;
-  int64_t* d_offs = nullptr;
-  void* ws = nullptr;
-  int32_t* status = nullptr;
-  carve(c, c->dbuf, cnt, vbytes, want_validity, n, &d, &d_offs, &ws, ws_bytes, &status);
-  for (int i = 0; i < N && !rc; ++i) {  // H2D of every column
-    const fory_column& h = host_cols[i];
-    if (d[i].values && vbytes[i] > 0)
-      rc = hcopy(d[i].values, h.values, (size_t)vbytes[i], hipMemcpyHostToDevice, c->s_k, "H2D");
-    if (!rc && d[i].offsets)
-      rc = hcopy(d[i].offsets, h.offsets, (size_t)(cnt[i] + 1) * 4, hipMemcpyHostToDevice, c->s_k, "H2D offsets");
-    if (!rc && d[i].validity)
-      rc = hcopy(d[i].validity, h.validity, (size_t)((cnt[i] + 7) / 8), hipMemcpyHostToDevice, c->s_k, "H2D validity");
-  }
-  if (!rc) rc = hip_check(hipMemsetAsync(status, 0, 4, c->s_k), "hipMemsetAsync");
-  if (!rc) rc = fory_rowfmt_encoded_size(c->plan, d.data(), n, frame, d_offs, ws, ws_bytes, c->s_k);
-  // row/frame offsets to the host: the split into the caller's windows needs them
-  std::vector<int64_t> tmp;
-  int64_t* ho = host_row_offsets;
-  if (!ho) {
-    tmp.resize((size_t)n + 1);
-    ho = tmp.data();
-  }
-  if (!rc) rc = hcopy(ho, d_offs, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, c->s_k, "D2H offsets");
+  const int64_t chunks = (n + c->chunk - 1) / c->chunk;
+  const int64_t ws_bytes = fory_rowfmt_workspace_bytes(c->plan, std::min(n, c->chunk));
+  rc = hip_check(hipMemsetAsync(c->vstatus, 0, 8, c->s_k), "hipMemsetAsync");
   if (!rc) rc = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize");
   if (rc) return rc;
-  const int64_t total = ho[n];
-  if (out_bytes) *out_bytes = total;
-  rc = split_rows(ho, 0, n, W);  // MemoryBuffer bounds check (MemoryBuffer.java:303-309)
-  if (rc) return rc;
-  for (size_t w = 0; w + 1 < W->first.size(); ++w)
-    if (W->first[w + 1] > W->first[w] && !W->ptr[w]) return fail_host(FORY_ERR_INVALID_ARGUMENT, "output is null");
-  rc = ensure(c, &c->drows, &c->drows_bytes, total + 16);
-  if (!rc) rc = fory_rowfmt_encode(c->plan, d.data(), n, frame, d_offs, c->drows, total, status, ws, ws_bytes, c->s_k);
-  for (size_t w = 0; w + 1 < W->first.size() && !rc; ++w) {  // each window: its rows' contiguous bytes
-    const int64_t lo = ho[W->first[w]], hi = ho[W->first[w + 1]];
-    if (hi > lo)
-      rc = hcopy(W->ptr[w], c->drows + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, c->s_k, "D2H rows");
+  std::vector<fory_column> dcols[2];
+  int64_t* d_offs[2] = {};
+  void* ws[2] = {};
+  int64_t crow[2] = {}, c0[2] = {};  // rows and first row of the chunk in each slot
+
+  // H2D + sizes of chunk k into slot k & 1 (queued on s_in)
+  auto stage = [&](int64_t k) -> int {
+    const int b = (int)(k & 1);
+    fory_host_ctx::VarSlot& S = c->vs[b];
+    const int64_t a = k * c->chunk, rows = std::min(c->chunk, n - a);
+    std::vector<VarSlice> sl;
+    int r = var_slices(c, host_cols, a, rows, &sl);
+    if (r) return r;
+    const int64_t need = carve_slices(c, sl, rows, ws_bytes, nullptr, nullptr, nullptr, nullptr);
+    if (S.used) r = hip_check(hipStreamWaitEvent(c->s_in, c->ev_k[b], 0), "hipStreamWaitEvent");  // chunk k-2 read it
+    if (!r && need > S.dev_bytes) {
+      if (S.used) r = hip_check(hipEventSynchronize(c->ev_k[b]), "hipEventSynchronize");
+      if (S.dev) (void)hipFree(S.dev);
+      S.dev = nullptr, S.dev_bytes = 0;
+      const int64_t sz = align_up(need + need / 4);
+      if (!r) r = hip_check(hipMalloc(&S.dev, (size_t)sz), "hipMalloc(host ctx chunk slot)");
+      if (!r) S.dev_bytes = sz;
+    }
+    if (!r && S.pin_words < rows + 1) {
+      if (S.used) r = hip_check(hipEventSynchronize(c->ev_sz[b]), "hipEventSynchronize");
+      if (S.pin) (void)hipHostFree(S.pin);
+      S.pin = nullptr, S.pin_words = 0;
+      if (!r) r = hip_check(hipHostMalloc(reinterpret_cast<void**>(&S.pin), (size_t)(c->chunk + 1) * 8, hipHostMallocDefault),
+                            "hipHostMalloc(row offsets)");
+      if (!r) S.pin_words = c->chunk + 1;
+    }
+    if (r) return r;
+    carve_slices(c, sl, rows, ws_bytes, S.dev, &dcols[b], &d_offs[b], &ws[b]);
+    r = h2d_slices(c, host_cols, sl, dcols[b], c->s_in);
+    if (!r) r = fory_rowfmt_encoded_size(c->plan, dcols[b].data(), rows, frame, d_offs[b], ws[b], ws_bytes, c->s_in);
+    if (!r) r = hcopy(S.pin, d_offs[b], (size_t)(rows + 1) * 8, hipMemcpyDeviceToHost, c->s_in, "D2H row offsets");
+    if (!r) r = hip_check(hipEventRecord(c->ev_sz[b], c->s_in), "hipEventRecord");
+    crow[b] = rows, c0[b] = a;
+    return r;
+  };
+
+  // greedy window placement (split_rows, incrementally): window w started at row
+  // first[w]; its byte limit is that row's offset + cap[w]
+  W->first.assign((size_t)nw + 1, n);
+  std::vector<int64_t> wbyte((size_t)nw + 1, 0);  // batch byte offset where window w starts
+  int64_t w = 0, wlimit = W->cap.empty() ? -1 : W->cap[0];
+  W->first[0] = 0;
+  bool overflow = nw == 0;
+  int64_t base = 0;  // bytes of the chunks before
+  rc = stage(0);
+  for (int64_t k = 0; k < chunks && !rc; ++k) {
+    const int b = (int)(k & 1);
+    fory_host_ctx::VarSlot& S = c->vs[b];
+    if (k + 1 < chunks) rc = stage(k + 1);
+    if (!rc) rc = hip_check(hipEventSynchronize(c->ev_sz[b]), "hipEventSynchronize");
+    if (rc) break;
+    const int64_t a = c0[b], rows = crow[b];
+    const int64_t* po = S.pin;
+    const int64_t total = po[rows];
+    if (host_row_offsets)
+      for (int64_t i = 0; i <= rows; ++i) host_row_offsets[a + i] = base + po[i];
+    // rows of this chunk per window: [lo, hi) of the batch
+    auto at = [&](int64_t e) { return base + po[e - a]; };
+    std::vector<int64_t> piece_w, piece_lo, piece_hi;
+    int64_t cur = a;
+    while (!overflow && cur < a + rows) {
+      int64_t lo = cur, hi = a + rows;  // largest e in [cur, a + rows] with at(e) <= wlimit
+      while (lo < hi) {
+        const int64_t mid = hi - (hi - lo) / 2;
+        if (at(mid) <= wlimit) lo = mid;
+        else hi = mid - 1;
+      }
+      if (lo > cur) piece_w.push_back(w), piece_lo.push_back(cur), piece_hi.push_back(lo);
+      cur = lo;
+      if (cur < a + rows) {  // row cur does not fit window w: the next window starts there
+        W->first[(size_t)++w] = cur;
+        wbyte[(size_t)w] = at(cur);
+        if (w == nw) overflow = true;
+        else wlimit = at(cur) + W->cap[(size_t)w];
+      }
+    }
+    for (int64_t pw : piece_w)
+      if (!W->ptr[(size_t)pw]) rc = fail_host(FORY_ERR_INVALID_ARGUMENT, "output is null");
+    if (!overflow && !rc) {
+      if (S.used) rc = hip_check(hipStreamWaitEvent(c->s_k, c->ev_out[b], 0), "hipStreamWaitEvent");  // k-2's D2H
+      if (!rc && total + 16 > S.rows_bytes) {
+        if (S.used) rc = hip_check(hipEventSynchronize(c->ev_out[b]), "hipEventSynchronize");
+        if (S.rows) (void)hipFree(S.rows);
+        S.rows = nullptr, S.rows_bytes = 0;
+        const int64_t sz = align_up(total + total / 4 + 16);
+        if (!rc) rc = hip_check(hipMalloc(&S.rows, (size_t)sz), "hipMalloc(host ctx chunk rows)");
+        if (!rc) S.rows_bytes = sz;
+      }
+      if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_k, c->ev_sz[b], 0), "hipStreamWaitEvent");
+      if (!rc)
+        rc = fory_rowfmt_encode(c->plan, dcols[b].data(), rows, frame, d_offs[b], S.rows, total, c->vstatus + b,
+                                ws[b], ws_bytes, c->s_k);
+      if (!rc) rc = hip_check(hipEventRecord(c->ev_k[b], c->s_k), "hipEventRecord");
+      if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_out, c->ev_k[b], 0), "hipStreamWaitEvent");
+      for (size_t q = 0; q < piece_w.size() && !rc; ++q) {
+        const int64_t pw = piece_w[q];
+        rc = hcopy(W->ptr[(size_t)pw] + (at(piece_lo[q]) - wbyte[(size_t)pw]), S.rows + po[piece_lo[q] - a], (size_t)(at(piece_hi[q]) - at(piece_lo[q])), hipMemcpyDeviceToHost,
+                   c->s_out, "D2H rows");
+      }
+      if (!rc) rc = hip_check(hipEventRecord(c->ev_out[b], c->s_out), "hipEventRecord");
+    } else if (!rc) {  // sizes only from here: the slot's columns are free again once sized
+      rc = hip_check(hipEventRecord(c->ev_k[b], c->s_in), "hipEventRecord");
+      if (!rc) rc = hip_check(hipEventRecord(c->ev_out[b], c->s_in), "hipEventRecord");
+    }
+    S.used = true;
+    base += total;
   }
-  if (!rc) rc = fory_rowfmt_read_status(status, c->s_k);  // synchronises the stream
+  const int rc_sync = hip_check(hipStreamSynchronize(c->s_out), "hipStreamSynchronize");
+  (void)hipStreamSynchronize(c->s_k);
+  (void)hipStreamSynchronize(c->s_in);
+  if (rc) return rc;
+  if (rc_sync) return rc_sync;
+  if (out_bytes) *out_bytes = base;
+  if (overflow) {
+    int64_t placed = nw > 0 ? W->first[(size_t)nw] : 0;
+    return fail_host(FORY_ERR_CAPACITY, "output windows hold " + std::to_string(placed) + " of " + std::to_string(n) +
+                                            " rows (" + std::to_string(base) + " bytes in all)");
+  }
+  for (int b = 0; b < 2 && !rc; ++b) rc = fory_rowfmt_read_status(c->vstatus + b, c->s_k);
   return rc;
 }
 

@@ -105,6 +105,10 @@ hipError_t launch_scan_offsets_i32(int32_t* offs, int64_t n, int64_t* partials,
 // partial_words int64 (segments of 4096 x (partial_words - 1) items, carried).
 hipError_t launch_scan_offsets_i32_segmented(int32_t* offs, int64_t n, int64_t* partials, int64_t partial_words,
                                              int32_t* status, hipStream_t s);
+// Host decode pipeline: offs[0..n] += base; bits [0, nbits) of src to bits
+// [shift, shift + nbits) of dst ((shift + nbits + 7) / 8 bytes, zero elsewhere).
+hipError_t launch_offsets_add(int32_t* offs, int64_t n, int32_t base, hipStream_t s);
+hipError_t launch_bits_shift(const uint8_t* src, int64_t nbits, uint8_t* dst, int shift, hipStream_t s);
 
 // Tree engine (generic.hip): any nesting, one lane per record.
 struct GenLaunch {

@@ -127,7 +127,43 @@ __global__ __launch_bounds__(kWG) void scan_down_kernel(void* data, int64_t n, c
   }
 }
 
+// Host decode pipeline (host.cpp): a chunk's Arrow offsets (0-based) moved to their
+// place in the batch, and its validity bits (from bit 0) moved to bit `shift` of
+// their first byte (the chunk's first element is not on a byte boundary there).
+__global__ void offsets_add_kernel(int32_t* offs, int64_t n, int32_t base) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= n) offs[i] += base;
+}
+
+__global__ void bits_shift_kernel(const uint8_t* __restrict__ src, int64_t nbits, uint8_t* __restrict__ dst,
+                                  int shift) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= (shift + nbits + 7) >> 3) return;
+  uint32_t out = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int64_t t = 8 * j + q - shift;
+    if (t >= 0 && t < nbits) out |= ((uint32_t)(src[t >> 3] >> (t & 7)) & 1u) << q;
+  }
+  dst[j] = (uint8_t)out;
+}
+
 }  // namespace
+
+hipError_t launch_offsets_add(int32_t* offs, int64_t n, int32_t base, hipStream_t s) {
+  if (base == 0) return hipSuccess;
+  const int64_t blocks = (n + 1 + kWG - 1) / kWG;
+  hipLaunchKernelGGL(offsets_add_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, offs, n, base);
+  return hipGetLastError();
+}
+
+hipError_t launch_bits_shift(const uint8_t* src, int64_t nbits, uint8_t* dst, int shift, hipStream_t s) {
+  const int64_t bytes = (shift + nbits + 7) >> 3;
+  if (bytes <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bits_shift_kernel, dim3((unsigned)((bytes + kWG - 1) / kWG)), dim3(kWG), 0, s, src, nbits, dst,
+                     shift);
+  return hipGetLastError();
+}
 
 hipError_t launch_fill_offsets(int64_t* offs, int64_t n, int64_t stride, hipStream_t s) {
   const int64_t blocks = (n + 1 + kWG - 1) / kWG;

@@ -1,0 +1,47 @@
+"""Throughput of the tree engine (fury_amd/csrc/generic.hip) on the nested test shapes:
+device-resident encode (sizes + scan + encode) and decode (level-by-level sizes +
+values), bytes = row bytes + column bytes per direction. Diagnostic, not the bench.
+Usage: python scripts/bench_nested_shapes.py [rows]"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from helpers import nested_columns  # noqa: E402
+from fury_amd.format.columns import to_device  # noqa: E402
+from fury_amd.format.encoder import RowEncoder  # noqa: E402
+
+n0 = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
+out = {}
+for name, div in (("holder", 1), ("lists", 1), ("maps_nested", 8), ("bean_a", 8)):
+    n = n0 // div  # (the Python row generator is slow on the map shapes)
+    print("generating", name, n, flush=True)
+    schema, cols = nested_columns(name, n, 5)
+    col_bytes = sum(a.nbytes for c in cols for a in (c.values, c.offsets, c.validity) if a is not None)
+    enc = RowEncoder(schema)
+    dcols = to_device(cols)
+    rows = enc.encode(dcols, n, 1)
+    enc.decode(rows)
+    torch.cuda.synchronize()
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    te, td = [], []
+    for _ in range(5):
+        e0.record()
+        rows = enc.encode(dcols, n, 1)
+        e1.record()
+        enc.decode(rows)
+        e2.record()
+        torch.cuda.synchronize()
+        te.append(e0.elapsed_time(e1))
+        td.append(e1.elapsed_time(e2))
+    rb = rows.buffer.numel()
+    t_e, t_d = min(te), min(td)
+    out[name] = {"rows": n, "row_bytes": rb, "column_bytes": col_bytes,
+                 "encode_ms": round(t_e, 3), "decode_ms": round(t_d, 3),
+                 "encode_GBps": round((rb + col_bytes) / t_e / 1e6, 1), "decode_GBps": round((rb + col_bytes) / t_d / 1e6, 1)}
+    print(name, out[name], flush=True)
+print(json.dumps(out))

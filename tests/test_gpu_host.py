@@ -79,16 +79,18 @@ VARLEN_HOST = ["mixed40_nulls", "nested_nulls", "strings_lists", "flat_mix", "de
                "string_elems"]
 
 
+@pytest.mark.parametrize("chunk", [1 << 20, 1024])
 @pytest.mark.parametrize("frame", [0, 1])
 @pytest.mark.parametrize("n", [0, 1, 777, 5000])
 @pytest.mark.parametrize("name", VARLEN_HOST)
-def test_host_varlen_parity(name, n, frame):
+def test_host_varlen_parity(name, n, frame, chunk):
     """fory_rowfmt_host_encode_var / decode_var: host columns -> the oracle's rows and row
-    offsets; host rows -> the input columns (whole batch, device buffers kept in the ctx)."""
+    offsets (one chunk, or 1024-row chunks: slices of every nested column at their
+    parents' offsets); host rows -> the input columns (device buffers kept in the ctx)."""
     schema, make = catalog()[name]
     cols = make(n, n + 3)
     expect, eoffs = oracle.encode(schema, cols, n, frame)
-    hp = HostPipeline(NativePlan(schema))
+    hp = HostPipeline(NativePlan(schema), chunk_rows=chunk)
     rows, offs = hp.encode_var(cols, n, frame)  # starts from a 1-byte buffer: capacity error, grow, retry
     assert rows.nbytes == expect.nbytes
     bad = np.nonzero(rows != expect)[0]
@@ -182,7 +184,7 @@ def test_host_varlen_nested_collections(name, frame):
     n = 60 if name == "chain" else 900
     schema, cols = nested_columns(name, n, 31 + frame)
     expect, eoffs = oracle.encode(schema, cols, n, frame)
-    hp = HostPipeline(NativePlan(schema))
+    hp = HostPipeline(NativePlan(schema), chunk_rows=256 if name != "chain" else 64)
     rows, offs = hp.encode_var(cols, n, frame)
     assert np.array_equal(rows, expect) and np.array_equal(offs, eoffs)
     assert columns_equal(schema, cols, hp.decode_var(expect, eoffs, n, frame)) == []
@@ -191,3 +193,51 @@ def test_host_varlen_nested_collections(name, frame):
         assert consumed == expect.nbytes
         assert columns_equal(schema, cols, dec) == []
     hp.close()
+
+
+@pytest.mark.parametrize("name", ["mixed40_nulls", "nested_nulls", "maps", "list_struct", "holder", "maps_nested"])
+def test_host_varlen_pipeline_registered(name):
+    """Registered (pinned) host columns and output: the chunk pipeline's copies are
+    asynchronous (H2D of chunk k+1 || encode of chunk k || D2H of chunk k-1), ordered
+    by events only; bytes and offsets == the oracle over many chunks, twice on one
+    context (slots reused)."""
+    from helpers import nested_columns
+    n = 6000
+    if name in ("holder", "maps_nested"):
+        schema, cols = nested_columns(name, n, 77)
+    else:
+        schema, make = catalog()[name]
+        cols = make(n, 77)
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    hp = HostPipeline(NativePlan(schema), chunk_rows=512)
+
+    def paged(a):  # a copy on whole pages of its own (registrations must not share a page)
+        raw = np.zeros(((a.nbytes + 4095) // 4096 + 1) * 4096, np.uint8)
+        k = (-raw.ctypes.data) % 4096
+        b = raw[k:k + (a.nbytes + 4095) // 4096 * 4096]
+        b[:a.nbytes] = a.view(np.uint8).reshape(-1)
+        return b, b[:a.nbytes].view(a.dtype)
+
+    regs = []
+    for c in cols:
+        for attr in ("values", "offsets", "validity"):
+            a = getattr(c, attr)
+            if a is not None and a.nbytes > 0:
+                whole, view = paged(a)
+                regs.append(whole)
+                setattr(c, attr, view)
+    whole_out, out = paged(np.zeros(expect.nbytes + 64, np.uint8))
+    arrays = regs + [whole_out]
+    for a in arrays:
+        host_register(a)
+    try:
+        for _ in range(2):
+            out[:] = 0
+            rows, offs = hp.encode_var(cols, n, 1, out)
+            assert np.array_equal(offs, eoffs)
+            bad = np.nonzero(out[:expect.nbytes] != expect)[0]
+            assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+    finally:
+        for a in arrays:
+            host_unregister(a)
+        hp.close()

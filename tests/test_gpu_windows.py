@@ -83,7 +83,7 @@ def test_windows_many_small(name, frame):
     assert int(nrows.sum()) == n
     for w, exp in enumerate(want):
         assert nbytes[w] == exp.nbytes and np.array_equal(wins[w][:nbytes[w]], exp), w
-    # too few windows: IndexOutOfBoundsException before anything is written
+    # too few windows: IndexOutOfBoundsException
     with pytest.raises(IndexOutOfBoundsException):
         hp.encode_windows(cols, n, frame, wins[:-1])
     # device path: the encoder's own offsets split the same way
