@@ -132,6 +132,10 @@ PROTOTYPES = {
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
          ctypes.POINTER(ctypes.c_int64)]),
     "fory_rowfmt_host_decode_var": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Column)]),
+    "fory_rowfmt_host_decode_var_into": (
+        ctypes.c_int,
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(Column),
+         ctypes.c_void_p, ctypes.c_void_p]),
     "fory_rowfmt_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "fory_rowfmt_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
 }

@@ -178,19 +178,20 @@ struct UploadRing {
   void* buf[kSlots] = {};
   size_t cap[kSlots] = {};
   hipEvent_t ev[kSlots] = {};
+  hipStream_t st[kSlots] = {};  // the stream the slot's copy was queued on
   bool used[kSlots] = {};
   int next = 0;
 };
 
 std::mutex g_upload_mu;
+std::map<int, UploadRing*>* g_rings = new std::map<int, UploadRing*>();  // never freed
 
 int upload(void* ws, const void* host, int64_t bytes, hipStream_t s) {
   if (bytes == 0) return FORY_OK;
-  static std::map<int, UploadRing*>* rings = new std::map<int, UploadRing*>();  // never freed
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lock(g_upload_mu);
-  UploadRing*& rp = (*rings)[dev];
+  UploadRing*& rp = (*g_rings)[dev];
   if (!rp) rp = new UploadRing();
   UploadRing& r = *rp;
   const int k = r.next;
@@ -212,6 +213,7 @@ int upload(void* ws, const void* host, int64_t bytes, hipStream_t s) {
   if (e == hipSuccess) e = hipEventRecord(r.ev[k], s);
   if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(plan table)");
   r.used[k] = true;
+  r.st[k] = s;
   return FORY_OK;
 }
 
@@ -509,6 +511,16 @@ int64_t fory_rowfmt_debug_timeline(uint64_t* host, int64_t max_words) {
 }
 
 const char* fory_rowfmt_last_error(void) { return g_err.c_str(); }
+
+// Library-internal (host.cpp): a stream about to be destroyed (its work complete) —
+// ring slots whose copy was queued on it are free, and their events are never
+// waited on again (an event of a destroyed stream is not safe to synchronise).
+void fory_rowfmt_internal_retire_stream(void* stream) {
+  std::lock_guard<std::mutex> lock(g_upload_mu);
+  for (auto& kv : *g_rings)
+    for (int k = 0; k < UploadRing::kSlots; ++k)
+      if (kv.second->used[k] && kv.second->st[k] == static_cast<hipStream_t>(stream)) kv.second->used[k] = false;
+}
 
 // Library-internal (host.cpp): shares last_error and the planner's column layout.
 int fory_rowfmt_internal_set_error(int code, const char* msg) { return fail(code, msg); }

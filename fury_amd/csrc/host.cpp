@@ -19,6 +19,11 @@
 
 #include "../../include/fory_rowfmt.h"
 
+namespace fory_amd {  // scan.hip (kernels.h)
+hipError_t launch_offsets_add(int32_t* offs, int64_t n, int32_t base, hipStream_t s);
+hipError_t launch_bits_shift(const uint8_t* src, int64_t nbits, uint8_t* dst, int shift, hipStream_t s);
+}  // namespace fory_amd
+
 namespace {
 
 
@@ -94,6 +99,7 @@ int hip_check(hipError_t e, const char* what) {
 // Library-internal helpers of capi.cpp (not in the public header): last_error
 // is thread-local there; column widths/nullability of a fixed-width plan.
 extern "C" int fory_rowfmt_internal_set_error(int code, const char* msg);
+extern "C" void fory_rowfmt_internal_retire_stream(void* stream);
 extern "C" int fory_rowfmt_internal_column_layout(const fory_plan* plan, int32_t* width, int32_t* nullable);
 extern "C" int fory_rowfmt_internal_node_layout(const fory_plan* plan, int32_t* kind, int32_t* width,
                                                 int32_t* nullable, int32_t* parent);
@@ -243,7 +249,10 @@ void fory_rowfmt_host_ctx_destroy(fory_host_ctx* c) {
     if (c->vs[b].pin) (void)hipHostFree(c->vs[b].pin);
   }
   for (hipStream_t s : {c->s_in, c->s_k, c->s_out})
-    if (s) (void)hipStreamDestroy(s);
+    if (s) {
+      fory_rowfmt_internal_retire_stream(s);
+      (void)hipStreamDestroy(s);
+    }
   if (c->arena) (void)hipFree(c->arena);
   if (c->vstatus) (void)hipFree(c->vstatus);
   for (uint8_t* b : {c->dbuf, c->drows, c->dout})
@@ -1048,3 +1057,275 @@ int fory_rowfmt_host_decode_var(fory_host_ctx* c, const fory_column* host_out_co
 }
 
 }  // extern "C"
+
+namespace {
+
+// One-call varlen decode, chunk pipeline over the two slots. Per chunk k (slot b):
+//   s_in : H2D of its row run and chunk-relative row offsets (queued one chunk ahead)
+//   s_k  : decode_sizes, once per list/map level (the host reads each level's totals),
+//          then the values pass into the slot's output region; offsets moved by the
+//          elements of the chunks before, validity bits shifted to their batch bit
+//   s_out: D2H of every column slice to its place in the caller's columns
+// so H2D (k+1) || sizes + decode (k) || D2H (k-1). A validity byte shared by two
+// chunks is written whole by the chunk holding its bit 0 and OR-ed by the other
+// (from a pinned stash, after the last copy). Columns that would overflow the
+// caller's capacities stop the copies; the rest of the batch is only sized.
+int host_decode_var_into(fory_host_ctx* c, const uint8_t* host_rows, const int64_t* host_row_offsets, int64_t n,
+                         int32_t frame, const fory_column* out, int64_t* host_counts, int64_t* host_bytes) {
+  const int N = c->info.num_columns;
+  c->dec_n = -1;  // a staged two-call decode does not survive this call
+  for (int i = 0; i < N; ++i) host_counts[i] = 0, host_bytes[i] = 0;
+  if (n == 0) {
+    for (int i = 0; i < N; ++i)
+      if (out[i].offsets && out[i].length >= 0) out[i].offsets[0] = 0;
+    return FORY_OK;
+  }
+  for (int64_t k = 0; k < n; ++k)
+    if (host_row_offsets[k + 1] < host_row_offsets[k]) return fail_host(FORY_ERR_CORRUPT, "row offsets decrease");
+  if (host_row_offsets[0] < 0) return fail_host(FORY_ERR_CORRUPT, "row offsets decrease");
+  for (int i = 0; i < N; ++i)
+    if (has_offsets(c->kind[i]) && !out[i].offsets)
+      return fail_host(FORY_ERR_INVALID_ARGUMENT, "output column " + std::to_string(i) + " needs offsets");
+  int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
+  if (rc) return rc;
+  const int64_t chunks = (n + c->chunk - 1) / c->chunk;
+  const int64_t ws_bytes = fory_rowfmt_workspace_bytes(c->plan, std::min(n, c->chunk));
+  rc = hip_check(hipMemsetAsync(c->vstatus, 0, 8, c->s_k), "hipMemsetAsync");
+  if (!rc) rc = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize");
+  if (rc) return rc;
+  std::vector<char> wv(N, 0);
+  for (int i = 0; i < N; ++i) wv[i] = c->nullable[i] && out[i].validity;
+  std::vector<int64_t> E(N, 0), VB(N, 0);  // elements / value bytes of the chunks before
+  struct Stash { int col; int64_t byte; int64_t slot; };
+  std::vector<Stash> stash;
+  uint8_t* pin = nullptr;  // pinned: [N int32 level totals][chunks x N validity stash bytes]
+  rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin), (size_t)(4 * N + chunks * N + 16), hipHostMallocDefault),
+                 "hipHostMalloc");
+  if (rc) return rc;
+  int32_t* tpin = reinterpret_cast<int32_t*>(pin);
+  uint8_t* spin = pin + 4 * N;
+  bool overflow = false;
+  int64_t crow[2] = {};
+  int64_t* d_offs[2] = {};
+
+  auto prefetch = [&](int64_t k) -> int {  // rows + relative offsets of chunk k (s_in)
+    const int b = (int)(k & 1);
+    fory_host_ctx::VarSlot& S = c->vs[b];
+    const int64_t a = k * c->chunk, rows = std::min(c->chunk, n - a);
+    const int64_t lo = host_row_offsets[a], hi = host_row_offsets[a + rows];
+    const int64_t run = align_up(hi - lo + 16), need = run + align_up((rows + 1) * 8);
+    int r = FORY_OK;
+    if (S.used) r = hip_check(hipStreamWaitEvent(c->s_in, c->ev_k[b], 0), "hipStreamWaitEvent");  // k-2 decoded
+    if (!r && S.used) r = hip_check(hipEventSynchronize(c->ev_in[b]), "hipEventSynchronize");  // its pin copy left
+    if (!r && need > S.rows_bytes) {
+      if (S.used) r = hip_check(hipEventSynchronize(c->ev_k[b]), "hipEventSynchronize");
+      if (S.rows) (void)hipFree(S.rows);
+      S.rows = nullptr, S.rows_bytes = 0;
+      const int64_t sz = align_up(need + need / 4);
+      if (!r) r = hip_check(hipMalloc(&S.rows, (size_t)sz), "hipMalloc(host ctx chunk rows)");
+      if (!r) S.rows_bytes = sz;
+    }
+    if (!r && S.pin_words < rows + 1) {
+      if (S.pin) (void)hipHostFree(S.pin);
+      S.pin = nullptr, S.pin_words = 0;
+      r = hip_check(hipHostMalloc(reinterpret_cast<void**>(&S.pin), (size_t)(c->chunk + 1) * 8, hipHostMallocDefault),
+                    "hipHostMalloc(row offsets)");
+      if (!r) S.pin_words = c->chunk + 1;
+    }
+    if (r) return r;
+    for (int64_t i = 0; i <= rows; ++i) S.pin[i] = host_row_offsets[a + i] - lo;
+    d_offs[b] = reinterpret_cast<int64_t*>(S.rows + run);
+    if (hi > lo) r = hcopy(S.rows, host_rows + lo, (size_t)(hi - lo), hipMemcpyHostToDevice, c->s_in, "H2D rows");
+    if (!r) r = hcopy(d_offs[b], S.pin, (size_t)(rows + 1) * 8, hipMemcpyHostToDevice, c->s_in, "H2D row offsets");
+    if (!r) r = hip_check(hipEventRecord(c->ev_in[b], c->s_in), "hipEventRecord");
+    crow[b] = rows;
+    return r;
+  };
+
+  rc = prefetch(0);
+  for (int64_t k = 0; k < chunks && !rc; ++k) {
+    const int b = (int)(k & 1);
+    fory_host_ctx::VarSlot& S = c->vs[b];
+    if (k + 1 < chunks) rc = prefetch(k + 1);
+    const int64_t rows = crow[b];
+    int32_t* status = c->vstatus + b;
+    // sizes, level by level (decode_var_stage): counts of the columns known so far
+    if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_k, c->ev_in[b], 0), "hipStreamWaitEvent");
+    if (!rc && S.used) rc = hip_check(hipStreamWaitEvent(c->s_k, c->ev_out[b], 0), "hipStreamWaitEvent");
+    std::vector<int64_t> cnt(N, -1), vbytes(N, 0);
+    auto resolve = [&]() {
+      for (int i = 0; i < N; ++i) {
+        const int p = c->parent[i];
+        if (cnt[i] >= 0) continue;
+        if (p < 0) cnt[i] = rows;
+        else if (cnt[p] >= 0 && c->kind[p] == kKindStruct) cnt[i] = cnt[p];
+      }
+    };
+    resolve();
+    std::vector<fory_column> d;
+    void* ws = nullptr;
+    std::vector<char> nov(N, 0);
+    std::vector<int64_t> vb0(N, 0), kc(N);
+    for (int pass = 0; pass < 20 && !rc; ++pass) {
+      for (int i = 0; i < N; ++i) kc[i] = cnt[i];
+      const int64_t need = carve(c, nullptr, kc, vb0, nov, rows, nullptr, nullptr, nullptr, ws_bytes, nullptr);
+      if (need > S.dev_bytes) {
+        rc = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize");
+        if (!rc && S.used) rc = hip_check(hipEventSynchronize(c->ev_out[b]), "hipEventSynchronize");
+        if (S.dev) (void)hipFree(S.dev);
+        S.dev = nullptr, S.dev_bytes = 0;
+        const int64_t sz = align_up(need + need / 4);
+        if (!rc) rc = hip_check(hipMalloc(&S.dev, (size_t)sz), "hipMalloc(host ctx chunk slot)");
+        if (!rc) S.dev_bytes = sz;
+        if (rc) break;
+      }
+      carve(c, S.dev, kc, vb0, nov, rows, &d, nullptr, &ws, ws_bytes, nullptr);
+      for (int i = 0; i < N; ++i) {
+        d[i].values = nullptr;
+        d[i].capacity = 0;
+        if (kc[i] < 0) d[i] = fory_column{};
+      }
+      rc = fory_rowfmt_decode_sizes(c->plan, S.rows, d_offs[b], rows, frame, d.data(), status, ws, ws_bytes, c->s_k);
+      for (int i = 0; i < N && !rc; ++i)
+        if (d[i].offsets && kc[i] >= 0)
+          rc = hip_check(hipMemcpyAsync(tpin + i, d[i].offsets + kc[i], 4, hipMemcpyDeviceToHost, c->s_k), "D2H totals");
+      if (!rc) rc = fory_rowfmt_read_status(status, c->s_k);  // synchronises s_k
+      const int32_t* tot = tpin;
+      if (rc) break;
+      bool changed = false;
+      for (int i = 0; i < N; ++i) {
+        if (!has_offsets(c->kind[i]) || kc[i] < 0) continue;
+        if (c->kind[i] == kKindBytes) vbytes[i] = tot[i];
+        else
+          for (int j = 0; j < N; ++j)
+            if (c->parent[j] == i && cnt[j] < 0) cnt[j] = tot[i], changed = true;
+      }
+      resolve();
+      if (!changed) break;
+    }
+    if (rc) break;
+    for (int i = 0; i < N; ++i) {
+      if (cnt[i] < 0) cnt[i] = 0, kc[i] = -1;  // (no buffers in the sizes layout)
+      if (c->kind[i] == kKindFixed || c->kind[i] == kKindBool) vbytes[i] = cnt[i] * c->width[i];
+      host_counts[i] += cnt[i];
+      host_bytes[i] += vbytes[i];
+      const int64_t vcap = c->kind[i] == kKindBytes ? out[i].capacity : (out[i].length) * c->width[i];
+      if (E[i] + cnt[i] > out[i].length || (vbytes[i] > 0 && VB[i] + vbytes[i] > vcap) ||
+          (vbytes[i] > 0 && !out[i].values))
+        overflow = true;
+    }
+    if (!overflow) {
+      // output region after the sizes layout: values, validity, shifted validity
+      const int64_t at0 = carve(c, nullptr, kc, vb0, nov, rows, nullptr, nullptr, nullptr, ws_bytes, nullptr);
+      int64_t at = at0;
+      std::vector<int64_t> o_val(N, -1), o_vld(N, -1), o_sh(N, -1);
+      for (int i = 0; i < N; ++i) {
+        if (vbytes[i] > 0) o_val[i] = at, at += align_up(vbytes[i] + kSlack);
+        if (wv[i]) {
+          o_vld[i] = at, at += align_up(validity_bytes(cnt[i] > 0 ? cnt[i] : 1) + kSlack);
+          if (E[i] & 7) o_sh[i] = at, at += align_up(cnt[i] / 8 + 2 + kSlack);
+        }
+      }
+      if (at > S.dev_bytes) {  // grow, keeping the sizes layout's offsets
+        uint8_t* nd = nullptr;
+        const int64_t sz = align_up(at + at / 4);
+        rc = hip_check(hipMalloc(&nd, (size_t)sz), "hipMalloc(host ctx chunk slot)");
+        if (!rc) rc = hip_check(hipMemcpyAsync(nd, S.dev, (size_t)at0, hipMemcpyDeviceToDevice, c->s_k), "D2D");
+        if (!rc) rc = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize");
+        if (rc) {
+          if (nd) (void)hipFree(nd);
+          break;
+        }
+        (void)hipFree(S.dev);
+        S.dev = nd, S.dev_bytes = sz;
+        carve(c, S.dev, kc, vb0, nov, rows, &d, nullptr, &ws, ws_bytes, nullptr);
+      }
+      for (int i = 0; i < N && !rc; ++i) {
+        d[i].values = o_val[i] >= 0 ? S.dev + o_val[i] : nullptr;
+        d[i].capacity = vbytes[i];
+        d[i].length = cnt[i];
+        d[i].validity = o_vld[i] >= 0 ? S.dev + o_vld[i] : nullptr;
+        if (d[i].validity)
+          rc = hip_check(hipMemsetAsync(d[i].validity, 0, (size_t)validity_bytes(cnt[i] > 0 ? cnt[i] : 1), c->s_k),
+                         "hipMemsetAsync");
+      }
+      if (!rc)
+        rc = fory_rowfmt_decode(c->plan, S.rows, d_offs[b], rows, frame, d.data(), status, ws, ws_bytes, c->s_k);
+      for (int i = 0; i < N && !rc; ++i) {  // batch positions
+        if (d[i].offsets) {
+          const int64_t base = c->kind[i] == kKindBytes ? VB[i] : [&]() {
+            for (int j = 0; j < N; ++j)
+              if (c->parent[j] == i) return E[j];
+            return int64_t(0);
+          }();
+          if (base > INT32_MAX) {
+            rc = fail_host(FORY_ERR_CAPACITY, "column " + std::to_string(i) + " exceeds int32 offsets");
+            break;
+          }
+          rc = hip_check(fory_amd::launch_offsets_add(d[i].offsets, cnt[i], (int32_t)base, c->s_k), "offsets_add");
+        }
+        if (!rc && o_sh[i] >= 0)
+          rc = hip_check(fory_amd::launch_bits_shift(d[i].validity, cnt[i], S.dev + o_sh[i], (int)(E[i] & 7), c->s_k),
+                         "bits_shift");
+      }
+      if (!rc) rc = hip_check(hipEventRecord(c->ev_k[b], c->s_k), "hipEventRecord");
+      if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_out, c->ev_k[b], 0), "hipStreamWaitEvent");
+      for (int i = 0; i < N && !rc; ++i) {
+        const fory_column& h = out[i];
+        if (d[i].values && vbytes[i] > 0) {
+          const int64_t dst = c->kind[i] == kKindBytes ? VB[i] : E[i] * c->width[i];
+          rc = hcopy(static_cast<uint8_t*>(h.values) + dst, d[i].values, (size_t)vbytes[i], hipMemcpyDeviceToHost,
+                     c->s_out, "D2H values");
+        }
+        if (!rc && d[i].offsets)
+          rc = hcopy(h.offsets + E[i], d[i].offsets, (size_t)(cnt[i] + 1) * 4, hipMemcpyDeviceToHost, c->s_out,
+                     "D2H offsets");
+        if (!rc && d[i].validity && cnt[i] > 0) {
+          const int sh = (int)(E[i] & 7);
+          const int64_t nbytes = (sh + cnt[i] + 7) >> 3;
+          const uint8_t* src = sh ? S.dev + o_sh[i] : d[i].validity;
+          if (sh) {  // byte 0 is shared with the chunk before: OR-ed at the end
+            const int64_t slot = k * N + i;
+            stash.push_back(Stash{i, E[i] >> 3, slot});
+            rc = hip_check(hipMemcpyAsync(spin + slot, src, 1, hipMemcpyDeviceToHost, c->s_out), "D2H validity");
+          }
+          if (!rc && nbytes > (sh ? 1 : 0))
+            rc = hcopy(h.validity + (E[i] >> 3) + (sh ? 1 : 0), src + (sh ? 1 : 0), (size_t)(nbytes - (sh ? 1 : 0)),
+                       hipMemcpyDeviceToHost, c->s_out, "D2H validity");
+        }
+      }
+      if (!rc) rc = hip_check(hipEventRecord(c->ev_out[b], c->s_out), "hipEventRecord");
+    } else {  // sized only
+      rc = hip_check(hipEventRecord(c->ev_k[b], c->s_k), "hipEventRecord");
+      if (!rc) rc = hip_check(hipEventRecord(c->ev_out[b], c->s_k), "hipEventRecord");
+    }
+    S.used = true;
+    for (int i = 0; i < N; ++i) E[i] += cnt[i], VB[i] += vbytes[i];
+  }
+  const int rc_sync = hip_check(hipStreamSynchronize(c->s_out), "hipStreamSynchronize");
+  (void)hipStreamSynchronize(c->s_k);
+  (void)hipStreamSynchronize(c->s_in);
+  if (!rc && !rc_sync && !overflow)
+    for (const Stash& st : stash) out[st.col].validity[st.byte] |= spin[st.slot];
+  (void)hipHostFree(pin);
+  if (rc) return rc;
+  if (rc_sync) return rc_sync;
+  for (int b = 0; b < 2 && !rc; ++b) rc = fory_rowfmt_read_status(c->vstatus + b, c->s_k);
+  if (rc) return rc;
+  if (overflow) return fail_host(FORY_ERR_CAPACITY, "output columns too small (host_counts / host_bytes: the sizes)");
+  return FORY_OK;
+}
+
+}  // namespace
+
+extern "C" int fory_rowfmt_host_decode_var_into(fory_host_ctx* c, const void* host_rows, const int64_t* host_row_offsets,
+                                                int64_t n, int32_t frame, const fory_column* host_out_cols,
+                                                int64_t* host_counts, int64_t* host_bytes) {
+  if (!c) return fail_host(FORY_ERR_INVALID_ARGUMENT, "ctx is null");
+  if (!c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "fixed-width plan: use fory_rowfmt_host_decode");
+  if (n < 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
+  if (!host_row_offsets || !host_counts || !host_bytes || !host_out_cols || (n > 0 && !host_rows))
+    return fail_host(FORY_ERR_INVALID_ARGUMENT, "host rows, row offsets, output columns or size outputs null");
+  return host_decode_var_into(c, static_cast<const uint8_t*>(host_rows), host_row_offsets, n, frame, host_out_cols,
+                              host_counts, host_bytes);
+}

@@ -261,6 +261,67 @@ class HostPipeline:
                                                                 ctypes.byref(used)))
         return self.decode_var_finish(counts, nbytes), used.value
 
+    def decode_var_into(self, rows, offsets, n: int, frame: int, cols=None):
+        """fory_rowfmt_host_decode_var_into: one pipelined call into caller-sized host
+        columns (HostColumn list, `length` = element capacity, as a receiver keeps its
+        buffers across batches); on FORY_ERR_CAPACITY the columns are sized from the
+        reported totals and the call repeats. Returns the columns, trimmed to the batch."""
+        import numpy as np
+        from .types import preorder
+        lib = _lib.load()
+        fields = preorder(self.plan.schema)
+        counts = np.zeros(max(1, len(fields)), np.int64)
+        nbytes = np.zeros(max(1, len(fields)), np.int64)
+        offs = np.ascontiguousarray(offsets, dtype=np.int64)
+        if cols is None:
+            cols = self.alloc_columns(np.zeros_like(counts), np.zeros_like(nbytes))
+        rc = lib.fory_rowfmt_host_decode_var_into(self.handle, _np_ptr(rows), _np_ptr(offs), n, frame,
+                                                  self._host_array(cols), _np_ptr(counts), _np_ptr(nbytes))
+        if rc == _lib.FORY_ERR_CAPACITY:
+            cols = self.alloc_columns(counts, nbytes)
+            rc = lib.fory_rowfmt_host_decode_var_into(self.handle, _np_ptr(rows), _np_ptr(offs), n, frame,
+                                                      self._host_array(cols), _np_ptr(counts), _np_ptr(nbytes))
+        _check(rc)
+        return self.trim_columns(cols, counts, nbytes)
+
+    def trim_columns(self, cols, counts, nbytes):
+        """Views of the first counts[i] elements (nbytes[i] string bytes) of each column."""
+        from .columns import HostColumn, validity_bytes
+        out = []
+        for i, c in enumerate(cols):
+            k = int(counts[i])
+            t = HostColumn(length=k)
+            if c.values is not None:
+                t.values = c.values[:max(1, int(nbytes[i]))] if c.values.dtype.itemsize == 1 and c.offsets is not None \
+                    else c.values[:max(1, k)]
+            if c.offsets is not None:
+                t.offsets = c.offsets[:k + 1]
+            if c.validity is not None:
+                t.validity = c.validity[:validity_bytes(k)]
+            out.append(t)
+        return out
+
+    def alloc_columns(self, counts, nbytes):
+        """Zeroed host columns for per-column element counts / string bytes (length = count)."""
+        import numpy as np
+        from .columns import HostColumn, NP_DTYPE, validity_bytes
+        from .types import ArrowType, preorder
+        fields = preorder(self.plan.schema)
+        cols = []
+        for i, f in enumerate(fields):
+            k, t = int(counts[i]), f.type.id
+            c = HostColumn(length=k)
+            if t in (ArrowType.STRING, ArrowType.BINARY):
+                c.values = np.zeros(max(1, int(nbytes[i])), np.uint8)
+            elif t in NP_DTYPE:
+                c.values = np.zeros(max(1, k), NP_DTYPE[t])
+            if t in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP):
+                c.offsets = np.zeros(k + 1, np.int32)
+            if f.nullable:
+                c.validity = np.zeros(validity_bytes(k), np.uint8)
+            cols.append(c)
+        return cols
+
     def decode_var_finish(self, counts, nbytes):
         """fory_rowfmt_host_decode_var: the staged batch into freshly sized host columns."""
         import numpy as np

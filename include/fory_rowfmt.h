@@ -309,17 +309,20 @@ int fory_rowfmt_host_decode(fory_host_ctx* ctx, const void* host_rows, int64_t r
  * window_caps[w] bytes (greedy, in order; a window too small for the next row stays
  * empty), then the next window; window_rows / window_bytes (num_windows each,
  * nullable) receive what each holds. Fixed-width and varlen plans. Not enough room
- * in all windows: FORY_ERR_CAPACITY before any row is copied. */
+ * in all windows: FORY_ERR_CAPACITY (fixed-width plans: before any row is copied;
+ * varlen plans: the chunks before the overflow may already be written). */
 int fory_rowfmt_host_encode_windows(fory_host_ctx* ctx, const fory_column* host_cols, int64_t num_rows,
                                     int32_t frame_mode, void* const* windows, const int64_t* window_caps,
                                     int32_t num_windows, int64_t* window_rows, int64_t* window_bytes);
 /* Varlen plans (strings, lists, maps, nested structs; also FORY_FRAME_COLLECTION):
- * the whole batch per call (row sizes are data-dependent, so there are no fixed
- * chunk strides); the context keeps its device buffers and grows them as needed.
+ * the context keeps its device buffers and grows them as needed.
  * host_encode_var: host columns (Arrow layout, as fory_rowfmt_encode) -> rows /
- * frames back to back in host_out; *out_bytes receives the total (also on
- * FORY_ERR_CAPACITY, so the caller can grow its buffer), host_row_offsets (n+1,
- * may be NULL) the row/frame starts. */
+ * frames back to back in host_out, pipelined by chunks of chunk_rows records (each
+ * chunk's column slices follow its rows' offsets; its rows are sized on the device,
+ * then placed after the chunks before); *out_bytes receives the total (also on
+ * FORY_ERR_CAPACITY, so the caller can grow its buffer; rows of the chunks before
+ * the overflow may already be written), host_row_offsets (n+1, may be NULL) the
+ * row/frame starts. */
 int fory_rowfmt_host_encode_var(fory_host_ctx* ctx, const fory_column* host_cols, int64_t num_rows,
                                 int32_t frame_mode, void* host_out, int64_t out_capacity,
                                 int64_t* host_row_offsets, int64_t* out_bytes);
@@ -346,6 +349,18 @@ int fory_rowfmt_host_decode_stream_sizes(fory_host_ctx* ctx, const void* host_ro
 /* Any host_encode_var on the context between the sizes call and this one drops
  * the staged batch (FORY_ERR_INVALID_ARGUMENT: stage it again). */
 int fory_rowfmt_host_decode_var(fory_host_ctx* ctx, const fory_column* host_out_cols);
+/* One-call decode into caller-sized host columns, pipelined by chunks of chunk_rows
+ * records (H2D of chunk k+1 || sizes + decode of chunk k || D2H of chunk k-1): the
+ * receiver that keeps (and grows) its Arrow buffers across batches, as host_encode_var
+ * does its output. host_out_cols[i].length: element capacity of every column (offsets
+ * need length + 1 entries, validity (length + 7) / 8 bytes, fixed values length x
+ * width); .capacity: value-byte capacity of string/binary columns. host_counts /
+ * host_bytes (num_columns each) receive the batch's element counts and value bytes —
+ * also on FORY_ERR_CAPACITY (a column too small; the columns hold a partial decode),
+ * so the caller can grow and call again. host_row_offsets (n+1) required. */
+int fory_rowfmt_host_decode_var_into(fory_host_ctx* ctx, const void* host_rows, const int64_t* host_row_offsets,
+                                     int64_t num_rows, int32_t frame_mode, const fory_column* host_out_cols,
+                                     int64_t* host_counts, int64_t* host_bytes);
 int fory_rowfmt_host_register(void* host_ptr, int64_t bytes);
 int fory_rowfmt_host_unregister(void* host_ptr);
 

@@ -1,6 +1,6 @@
 """Host-inclusive rate of the varlen configs through the C-ABI host path
-(fory_rowfmt_host_encode_var / host_decode_var_sizes / host_decode_var: whole batch per
-call, H2D + kernels + D2H in series). Host columns and rows in registered (pinned)
+(fory_rowfmt_host_encode_var: chunk pipeline; host_decode_var_sizes + host_decode_var:
+whole batch, H2D + kernels + D2H in series; host_decode_var_into: chunk pipeline). Host columns and rows in registered (pinned)
 memory. Recorded in DESIGN.md, never bench `value`.
 Usage: python scripts/host_native_var.py [rows]"""
 import ctypes
@@ -53,7 +53,10 @@ for config in ("mixed40", "nested"):
         host_register(a)
     hin, hback = hp._host_array(host), hp._host_array(back)
     total = ctypes.c_int64(0)
-    te, td = [], []
+    te, td, ti = [], [], []
+    hc, hb = np.zeros(len(fields), np.int64), np.zeros(len(fields), np.int64)
+    for c, k in zip(back, counts):
+        c.length = int(k)
     for _ in range(4):
         t0 = time.perf_counter()
         _check(lib.fory_rowfmt_host_encode_var(hp.handle, hin, n, 1, out.ctypes.data, out.nbytes, ro.ctypes.data,
@@ -64,15 +67,23 @@ for config in ("mixed40", "nested"):
                                                      counts.ctypes.data, nbytes.ctypes.data))
         _check(lib.fory_rowfmt_host_decode_var(hp.handle, hback))
         td.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        _check(lib.fory_rowfmt_host_decode_var_into(hp.handle, out.ctypes.data, ro.ctypes.data, n, 1, hback,
+                                                    hc.ctypes.data, hb.ctypes.data))
+        ti.append(time.perf_counter() - t0)
     ok = bool(np.array_equal(out, rows))
     for a in arrays:
         host_unregister(a)
     hp.close()
-    t_enc, t_dec = min(te[1:]), min(td[1:])
+    t_enc, t_dec, t_into = min(te[1:]), min(td[1:]), min(ti[1:])
     col_bytes = sum(a.nbytes for c in host for a in (c.values, c.offsets, c.validity) if a is not None)
     res[config] = {"frames_equal_first_call": ok, "encode_s": round(t_enc, 4), "decode_s": round(t_dec, 4),
                    "value_GiBs": round(2 * rows.nbytes / (t_enc + t_dec) / 2**30, 2),
                    "row_bytes": int(rows.nbytes), "column_bytes": int(col_bytes),
                    "pcie_GBs_encode": round((col_bytes + rows.nbytes) / t_enc / 1e9, 1),
-                   "pcie_GBs_decode": round((col_bytes + rows.nbytes) / t_dec / 1e9, 1)}
+                   "pcie_GBs_decode": round((col_bytes + rows.nbytes) / t_dec / 1e9, 1),
+                   "decode_into_s": round(t_into, 4),
+                   "value_GiBs_decode_into": round(2 * rows.nbytes / (t_enc + t_into) / 2**30, 2),
+                   "pcie_GBs_decode_into": round((col_bytes + rows.nbytes) / t_into / 1e9, 1),
+                   "sizes_match": bool(np.array_equal(hc, counts) and np.array_equal(hb, nbytes))}
 print(json.dumps(res))

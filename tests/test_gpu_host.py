@@ -237,7 +237,108 @@ def test_host_varlen_pipeline_registered(name):
             assert np.array_equal(offs, eoffs)
             bad = np.nonzero(out[:expect.nbytes] != expect)[0]
             assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+        dec = hp.decode_var_into(out[:expect.nbytes], eoffs, n, 1)  # (sized by a first call)
+        counts = [c.length for c in dec]
+        nb = [c.values.nbytes if c.values is not None and c.offsets is not None else 0 for c in dec]
+        outs = hp.alloc_columns(np.array(counts), np.array(nb))
+        for c in outs:
+            for attr in ("values", "offsets", "validity"):
+                a = getattr(c, attr)
+                if a is not None and a.nbytes > 0:
+                    whole, view = paged(a)
+                    arrays.append(whole)
+                    host_register(whole)
+                    setattr(c, attr, view)
+        for _ in range(2):
+            for c in outs:
+                for a in (c.values, c.offsets, c.validity):
+                    if a is not None:
+                        a.view(np.uint8)[:] = 0x5A
+            assert columns_equal(schema, cols, hp.decode_var_into(out[:expect.nbytes], eoffs, n, 1, outs)) == []
     finally:
         for a in arrays:
             host_unregister(a)
         hp.close()
+
+
+def same_arrays(x, y):
+    """Byte identity of two decodes (offsets, validity bits of the batch, values)."""
+    errs = []
+    for i, (a, b) in enumerate(zip(x, y)):
+        k = a.length
+        if k != b.length:
+            errs.append(f"{i}: length {k} != {b.length}")
+            continue
+        if a.offsets is not None and not np.array_equal(a.offsets[:k + 1], b.offsets[:k + 1]):
+            errs.append(f"{i}: offsets differ at {np.nonzero(a.offsets[:k + 1] != b.offsets[:k + 1])[0][:5]}")
+        if a.validity is not None:
+            ua = np.unpackbits(a.validity, bitorder="little")[:k]
+            ub = np.unpackbits(b.validity, bitorder="little")[:k]
+            if not np.array_equal(ua, ub):
+                errs.append(f"{i}: validity differs at {np.nonzero(ua != ub)[0][:5]}")
+        if a.values is not None:
+            m = int(a.offsets[k]) if a.offsets is not None else k  # string bytes / elements
+            va, vb = a.values[:m].view(np.uint8), b.values[:m].view(np.uint8)
+            if not np.array_equal(va, vb):
+                errs.append(f"{i}: values differ")
+    return errs
+
+
+@pytest.mark.parametrize("chunk", [1024, 1 << 20])
+@pytest.mark.parametrize("frame", [0, 1, 3])
+@pytest.mark.parametrize("name", VARLEN_HOST)
+def test_host_varlen_decode_into(name, frame, chunk):
+    """fory_rowfmt_host_decode_var_into: one pipelined call into caller-sized columns.
+    Empty columns first (FORY_ERR_CAPACITY with the batch's sizes), then sized ones;
+    then oversized buffers reused across calls. Chunked: each chunk's offsets moved to
+    its place in the batch, list-item validity bits shifted across byte boundaries."""
+    n = 5000
+    schema, make = catalog()[name]
+    cols = make(n, n + 5)
+    expect, eoffs = oracle.encode(schema, cols, n, frame)
+    hp = HostPipeline(NativePlan(schema), chunk_rows=chunk)
+    dec = hp.decode_var_into(expect, eoffs, n, frame)
+    assert columns_equal(schema, cols, dec) == []
+    assert same_arrays(dec, hp.decode_var(expect, eoffs, n, frame)) == []  # == the whole-batch decode
+    counts = np.array([c.length for c in dec], np.int64)
+    nbytes = np.array([c.values.nbytes if c.values is not None and c.offsets is not None else 0 for c in dec], np.int64)
+    big = hp.alloc_columns(counts + counts // 3 + 5, nbytes + 100)
+    for c in big:  # garbage in the reused buffers: every byte of the batch's range is rewritten
+        for a in (c.values, c.offsets, c.validity):
+            if a is not None:
+                a.view(np.uint8)[:] = 0xA5
+    for _ in range(2):
+        dec2 = hp.decode_var_into(expect, eoffs, n, frame, big)
+        assert columns_equal(schema, cols, dec2) == []
+    hp.close()
+
+
+@pytest.mark.parametrize("name", ["holder", "lists", "maps_nested", "bean_a", "deep"])
+def test_host_varlen_decode_into_nested(name):
+    """The tree engine's shapes through the one-call decode, 256-row chunks: every
+    nesting level sized per chunk, offsets of every level rebased."""
+    from helpers import nested_columns
+    n = 1100
+    schema, cols = nested_columns(name, n, 41)
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    hp = HostPipeline(NativePlan(schema), chunk_rows=256)
+    dec = hp.decode_var_into(expect, eoffs, n, 1)
+    assert columns_equal(schema, cols, dec) == []
+    assert same_arrays(dec, hp.decode_var(expect, eoffs, n, 1)) == []
+    hp.close()
+
+
+def test_host_varlen_decode_into_errors_and_empty():
+    schema, make = catalog()["mixed40_nulls"]
+    n = 3000
+    cols = make(n, 2)
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    hp = HostPipeline(NativePlan(schema), chunk_rows=1024)
+    bad = expect.copy()
+    bad[int(eoffs[2500]) + 5] ^= 1  # a frame's schema hash, in the third chunk
+    with pytest.raises(ClassNotCompatibleException):
+        hp.decode_var_into(bad, eoffs, n, 1)
+    empty = hp.decode_var_into(expect, eoffs[:1], 0, 1)
+    assert all(c.length == 0 for c in empty)
+    assert columns_equal(schema, cols, hp.decode_var_into(expect, eoffs, n, 1)) == []  # usable after an error
+    hp.close()
