@@ -63,6 +63,45 @@ __device__ __forceinline__ void gzero(uint8_t* p, int64_t n) {  // p 4-byte alig
   for (int64_t k = 0; k < n; k += 4) st32(p + k, 0u);
 }
 
+// writeUnaligned's bytes (+ zero padding to 8) at a 4-byte aligned row position from a
+// source of any alignment: aligned source dwords, each holding at least one byte of
+// the string (never outside the mapped buffer), funnel-shifted into dword stores.
+__device__ __forceinline__ void g_put_bytes(uint8_t* dst, const uint8_t* src, int64_t n) {
+  const int sh = (int)(reinterpret_cast<uintptr_t>(src) & 3);
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(src - sh);
+  const int64_t nw = (n + 3) >> 2;
+  uint32_t lo = nw > 0 ? s[0] : 0u;
+  for (int64_t k = 0; k < nw; ++k) {
+    uint32_t w = lo;
+    if (sh) {
+      const uint32_t hi = 4 * (k + 1) - sh < n ? s[k + 1] : 0u;
+      w = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh));
+      lo = hi;
+    } else if (k + 1 < nw) {
+      lo = s[k + 1];
+    }
+    const int64_t left = n - 4 * k;
+    if (left < 4) w &= (1u << (8 * left)) - 1u;
+    st32(dst + 4 * k, w);
+  }
+  if (gr8(n) > 4 * nw) st32(dst + 4 * nw, 0u);  // zeroOutPaddingBytes
+}
+
+// Row bytes (4-byte aligned source) to an Arrow values buffer of any alignment:
+// byte head to a 4-byte boundary, dword body (funnel-shifted source), byte tail.
+__device__ __forceinline__ void g_get_bytes(uint8_t* dst, const uint8_t* src, int64_t n) {
+  int64_t b = 0;
+  for (; b < n && (reinterpret_cast<uintptr_t>(dst + b) & 3); ++b) dst[b] = src[b];
+  const int ph = (int)(b & 3);  // src + b phase (src aligned)
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(src + b - ph);
+  for (int64_t k = 0; b + 4 <= n; b += 4, ++k) {
+    uint32_t w = s[k];
+    if (ph) w = (uint32_t)((((uint64_t)s[k + 1] << 32) | w) >> (8 * ph));
+    st32(dst + b, w);
+  }
+  for (; b < n; ++b) dst[b] = src[b];
+}
+
 __device__ __forceinline__ bool is_scalar(int kind) { return kind == KIND_FIXED || kind == KIND_BOOL; }
 __device__ __forceinline__ int elem_size(const GNode& it) { return is_scalar(it.kind) ? it.width : 8; }
 
@@ -167,8 +206,33 @@ __device__ int64_t g_sizes(const GenLaunch& L, int64_t i, bool* overflow) {
   return total;
 }
 
-template <int D>
-__global__ __launch_bounds__(kWG) void gen_sizes_kernel(GenLaunch L, int64_t* sizes) {
+// The node table and column views in LDS (every visit reads them; from global they
+// add two dependent loads per visit). Plans with more nodes read them from global.
+constexpr int kGenLdsNodes = 128;
+
+struct GenTables {
+  GNode nodes[kGenLdsNodes];
+  ColumnDev cols[kGenLdsNodes];
+};
+
+template <bool TAB>
+__device__ __forceinline__ GenLaunch gen_tables(const GenLaunch& L, GenTables* t) {
+  if (!TAB) return L;
+  for (int k = threadIdx.x; k < L.num_nodes; k += kWG) {
+    t->nodes[k] = L.nodes[k];
+    t->cols[k] = L.cols[k];
+  }
+  __syncthreads();
+  GenLaunch LL = L;
+  LL.nodes = t->nodes;
+  LL.cols = t->cols;
+  return LL;
+}
+
+template <int D, bool TAB>
+__global__ __launch_bounds__(kWG) void gen_sizes_kernel(GenLaunch L0, int64_t* sizes) {
+  __shared__ GenTables tabs;
+  const GenLaunch L = gen_tables<TAB>(L0, &tabs);
   const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
   if (i >= L.num_rows) return;
   bool overflow = false;
@@ -230,9 +294,7 @@ __device__ bool g_encode(const GenLaunch& L, uint8_t* row, int64_t i) {
       }
       case KIND_BYTES: {
         const int64_t s0 = c.offsets[pos], n = (int64_t)c.offsets[pos + 1] - s0;
-        uint8_t* dst = row + wi;
-        gzero(dst + (n & ~int64_t(3)), gr8(n) - (n & ~int64_t(3)));  // zeroOutPaddingBytes
-        for (int64_t b = 0; b < n; ++b) dst[b] = c.values[s0 + b];
+        g_put_bytes(row + wi, c.values + s0, n);
         gput(row + slot, ((uint64_t)rel << 32) | (uint32_t)n, 8);
         wi += (int32_t)gr8(n);
         return;
@@ -327,10 +389,12 @@ __device__ bool g_encode(const GenLaunch& L, uint8_t* row, int64_t i) {
   return ok;
 }
 
-template <int D>
-__global__ __launch_bounds__(kWG) void gen_encode_kernel(GenLaunch L, const int64_t* __restrict__ offs,
+template <int D, bool TAB>
+__global__ __launch_bounds__(kWG) void gen_encode_kernel(GenLaunch L0, const int64_t* __restrict__ offs,
                                                          uint8_t* __restrict__ out, int64_t capacity,
                                                          int32_t* status) {
+  __shared__ GenTables tabs;
+  const GenLaunch L = gen_tables<TAB>(L0, &tabs);
   const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
   if (i >= L.num_rows) return;
   const int64_t beg = offs[i], end = offs[i + 1];
@@ -502,8 +566,7 @@ __device__ void g_decode(const GenLaunch& L, const uint8_t* row, int64_t row_len
         corrupt();
         return;
       }
-      uint8_t* dst = c.out_values + o0;
-      for (int64_t b = 0; b < size; ++b) dst[b] = row[at + b];
+      g_get_bytes(c.out_values + o0, row + at, size);
       return;
     }
     open_container(node, at, size, pos);
@@ -563,9 +626,11 @@ __device__ void g_decode(const GenLaunch& L, const uint8_t* row, int64_t row_len
   }
 }
 
-template <int D>
-__global__ __launch_bounds__(kWG) void gen_decode_kernel(GenLaunch L, const uint8_t* __restrict__ in,
+template <int D, bool TAB>
+__global__ __launch_bounds__(kWG) void gen_decode_kernel(GenLaunch L0, const uint8_t* __restrict__ in,
                                                          const int64_t* __restrict__ offs, int32_t* status) {
+  __shared__ GenTables tabs;
+  const GenLaunch L = gen_tables<TAB>(L0, &tabs);
   const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
   if (i >= L.num_rows) return;
   const int64_t beg = offs[i], end = offs[i + 1];
@@ -596,14 +661,22 @@ __global__ __launch_bounds__(kWG) void gen_decode_kernel(GenLaunch L, const uint
   g_decode<D>(L, frame + hdr, bad ? 0 : len - hdr, i, !bad, status);
 }
 
+template <int D, bool TAB>
+hipError_t launch_gen_t(const GenLaunch& L, int what, int64_t* sizes, const int64_t* offs, uint8_t* out,
+                        int64_t capacity, const uint8_t* rows, int32_t* status, hipStream_t s) {
+  const dim3 grid((unsigned)((L.num_rows + kWG - 1) / kWG));
+  if (what == 0) hipLaunchKernelGGL((gen_sizes_kernel<D, TAB>), grid, dim3(kWG), 0, s, L, sizes);
+  else if (what == 1)
+    hipLaunchKernelGGL((gen_encode_kernel<D, TAB>), grid, dim3(kWG), 0, s, L, offs, out, capacity, status);
+  else hipLaunchKernelGGL((gen_decode_kernel<D, TAB>), grid, dim3(kWG), 0, s, L, rows, offs, status);
+  return hipGetLastError();
+}
+
 template <int D>
 hipError_t launch_gen_d(const GenLaunch& L, int what, int64_t* sizes, const int64_t* offs, uint8_t* out,
                         int64_t capacity, const uint8_t* rows, int32_t* status, hipStream_t s) {
-  const dim3 grid((unsigned)((L.num_rows + kWG - 1) / kWG));
-  if (what == 0) hipLaunchKernelGGL(gen_sizes_kernel<D>, grid, dim3(kWG), 0, s, L, sizes);
-  else if (what == 1) hipLaunchKernelGGL(gen_encode_kernel<D>, grid, dim3(kWG), 0, s, L, offs, out, capacity, status);
-  else hipLaunchKernelGGL(gen_decode_kernel<D>, grid, dim3(kWG), 0, s, L, rows, offs, status);
-  return hipGetLastError();
+  if (L.num_nodes <= kGenLdsNodes) return launch_gen_t<D, true>(L, what, sizes, offs, out, capacity, rows, status, s);
+  return launch_gen_t<D, false>(L, what, sizes, offs, out, capacity, rows, status, s);
 }
 
 // Frames = open containers + the row: schema depth + 1 (plan depth <= 17).

@@ -12,15 +12,38 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from helpers import nested_columns  # noqa: E402
-from fury_amd.format.columns import to_device  # noqa: E402
+from fury_amd.format.columns import HostColumn, pack_validity, to_device, unpack_validity  # noqa: E402
+from fury_amd.format.types import ArrowType, preorder  # noqa: E402
+
+
+def tile_columns(schema, cols, reps):
+    """The batch repeated reps times (Arrow columns: offsets shifted per copy)."""
+    out = []
+    for f, c in zip(preorder(schema), cols):
+        k = c.length
+        t = HostColumn(length=k * reps)
+        if c.offsets is not None:
+            o = c.offsets.astype(np.int64)
+            t.offsets = np.concatenate([o[:k] + r * o[k] for r in range(reps)] + [o[k:k + 1] * reps]).astype(np.int32)
+        if c.values is not None:
+            if f.type.id in (ArrowType.STRING, ArrowType.BINARY):
+                t.values = np.tile(c.values[:int(c.offsets[k])], reps)
+            else:
+                t.values = np.tile(c.values[:k], reps)
+        if c.validity is not None:
+            t.validity = pack_validity(np.tile(unpack_validity(c.validity, k), reps))
+        out.append(t)
+    return out
 from fury_amd.format.encoder import RowEncoder  # noqa: E402
 
 n0 = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
 out = {}
-for name, div in (("holder", 1), ("lists", 1), ("maps_nested", 8), ("bean_a", 8)):
-    n = n0 // div  # (the Python row generator is slow on the map shapes)
-    print("generating", name, n, flush=True)
-    schema, cols = nested_columns(name, n, 5)
+for name in ("holder", "lists", "maps_nested", "bean_a"):
+    base = 16384  # generated once (the Python row generator is slow), then tiled
+    print("generating", name, n0, flush=True)
+    schema, cols = nested_columns(name, base, 5)
+    n = n0 // base * base
+    cols = tile_columns(schema, cols, n // base)
     col_bytes = sum(a.nbytes for c in cols for a in (c.values, c.offsets, c.validity) if a is not None)
     enc = RowEncoder(schema)
     dcols = to_device(cols)
