@@ -162,6 +162,61 @@ __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* _
   sizes[i] = size;
 }
 
+// The same sizes for flat plans (L.flat: top-level and nested-struct strings and
+// list<fixed>, no maps / string elements / collection frames), from the var-field
+// and struct tables instead of the op program: every validity byte and offsets pair
+// is loaded before any is used (unrolled batches), so a row costs one memory latency
+// per batch rather than one per op.
+constexpr int kSizeBatch = 8;
+
+__global__ __launch_bounds__(kWG) void var_sizes_flat_kernel(VarLaunch L, const VarFieldDev* __restrict__ vf,
+                                                             const StructDev* __restrict__ st, int64_t* sizes) {
+  const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  if (i >= L.num_rows) return;
+  int64_t size = L.fixed_size + frame_header_bytes(L.frame);
+  uint32_t present = 1;  // bit id: struct id present (id 0 = the row)
+  if (L.num_struct) {
+    bool valid[kMaxTileStructs];
+#pragma unroll
+    for (int s = 0; s < kMaxTileStructs; ++s) {
+      valid[s] = true;
+      if (s < L.num_struct && (st[s].flags & 1) && st[s].validity) valid[s] = (st[s].validity[i >> 3] >> (i & 7)) & 1;
+    }
+#pragma unroll
+    for (int s = 0; s < kMaxTileStructs; ++s) {
+      if (s >= L.num_struct) break;
+      if (valid[s] && ((present >> st[s].parent) & 1)) {
+        present |= 1u << (s + 1);
+        size += st[s].hdr + 8LL * st[s].nfields;
+      }
+    }
+  }
+  for (int v0 = 0; v0 < L.num_var; v0 += kSizeBatch) {
+    int32_t a[kSizeBatch], b[kSizeBatch];
+    bool on[kSizeBatch];
+#pragma unroll
+    for (int k = 0; k < kSizeBatch; ++k) {
+      const int v = v0 + k;
+      a[k] = b[k] = 0;
+      on[k] = false;
+      if (v < L.num_var) {
+        const VarFieldDev& f = vf[v];
+        on[k] = ((present >> f.parent) & 1) && (!(f.flags & 1) || !f.validity || ((f.validity[i >> 3] >> (i & 7)) & 1));
+        a[k] = f.offsets[i];
+        b[k] = f.offsets[i + 1];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kSizeBatch; ++k) {
+      const int v = v0 + k;
+      if (v >= L.num_var || !on[k]) continue;
+      const int64_t n = (int64_t)b[k] - a[k];
+      size += vf[v].is_list ? 8 + bitmap_bytes(n) + round8(n * vf[v].w) : round8(n);
+    }
+  }
+  sizes[i] = size;
+}
+
 constexpr int kFixBatch = 8;  // consecutive OP_FIXED ops whose loads are issued together
 
 // A var/struct/list/map slot store; slot == null for the top-level field of a
@@ -2043,7 +2098,11 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
 hipError_t launch_var_sizes(const VarLaunch& L, int64_t* d_row_offsets, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
   const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
-  hipLaunchKernelGGL(var_sizes_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.prog, L.cols, d_row_offsets);
+  const bool program_walk = getenv("FORY_ROWFMT_SIZES_PROGRAM") != nullptr;  // A/B knob (per call)
+  if (L.flat && !program_walk)
+    hipLaunchKernelGGL(var_sizes_flat_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.vf, L.st, d_row_offsets);
+  else
+    hipLaunchKernelGGL(var_sizes_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.prog, L.cols, d_row_offsets);
   return hipGetLastError();
 }
 
