@@ -109,8 +109,11 @@ __global__ __launch_bounds__(kWG) void frame_spec_kernel(FrameIndexLaunch L, con
 }
 
 // Chunk k's walk is the true chain iff its start is its predecessor's exit.
+// Inconsistent chunks are marked dirty for the fix-up, which visits only those and
+// the chunks whose entry it moves.
 __global__ __launch_bounds__(kWG) void frame_check_kernel(FrameIndexLaunch L, const int64_t* __restrict__ start,
-                                                          const int64_t* __restrict__ exit_, int64_t* flag) {
+                                                          const int64_t* __restrict__ exit_, int64_t* flag,
+                                                          uint8_t* __restrict__ dirty, int32_t* __restrict__ moved) {
   const int64_t k = (int64_t)blockIdx.x * kWG + threadIdx.x;
   if (k >= L.chunks) return;
   bool ok;
@@ -118,6 +121,8 @@ __global__ __launch_bounds__(kWG) void frame_check_kernel(FrameIndexLaunch L, co
   else if (exit_[k - 1] == kBroken) ok = true;  // the chain ended before this chunk: nothing here counts
   else ok = start[k] != kNone && start[k] == exit_[k - 1];
   if (k > 0 && start[k - 1] == kNone) ok = false;  // a chunk without a candidate passes its entry through
+  dirty[k] = ok ? 0 : 1;
+  moved[k] = 0;
   if (!ok) atomicOr(reinterpret_cast<unsigned long long*>(flag), 1ull);
 }
 
@@ -125,9 +130,13 @@ __global__ __launch_bounds__(kWG) void frame_check_kernel(FrameIndexLaunch L, co
 // re-walks from its entry. Thread t owns chunks [t*B, (t+1)*B) and sweeps them in
 // order (its own updates propagate at once); sweeps repeat until no exit changes,
 // so after sweep i at least the blocks 0..i-1 hold the true chain.
+// Only dirty chunks (check kernel) and chunks whose predecessor's exit moved are
+// visited: a few inconsistent chunks (a frame longer than a chunk, a payload that
+// mimics a header) cost a few walks, not a sweep over every chunk.
 __global__ __launch_bounds__(1024) void frame_fixup_kernel(FrameIndexLaunch L, const uint8_t* __restrict__ rows,
                                                            int64_t* start, int64_t* exit_, int64_t* count,
-                                                           int32_t* saved, const int64_t* flag) {
+                                                           int32_t* saved, const int64_t* flag, uint8_t* dirty,
+                                                           int32_t* moved) {
   if (*flag == 0) return;
   __shared__ int changed;
   const int64_t B = (L.chunks + 1023) / 1024;
@@ -136,7 +145,16 @@ __global__ __launch_bounds__(1024) void frame_fixup_kernel(FrameIndexLaunch L, c
     if (threadIdx.x == 0) changed = 0;
     __syncthreads();
     bool mine = false;
+    bool carry = false;  // this thread moved chunk k-1's exit
     for (int64_t k = k0; k < k1; ++k) {
+      bool need = carry;
+      carry = false;
+      if (k == k0 && k > 0) need = atomicExch(&moved[k - 1], 0) != 0;  // the previous block's last chunk
+      if (dirty[k]) {
+        need = true;
+        dirty[k] = 0;
+      }
+      if (!need) continue;
       const int64_t entry = k == 0 ? 0 : __hip_atomic_load(&exit_[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int64_t base = k * L.chunk, end = min(base + L.chunk, L.rows_bytes);
       int64_t s, ex, frames = 0;
@@ -159,6 +177,8 @@ __global__ __launch_bounds__(1024) void frame_fixup_kernel(FrameIndexLaunch L, c
         saved[k] = -1;  // the positions step 1 saved are not this chain's: the write pass re-walks
         __hip_atomic_store(&exit_[k], ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         mine = true;
+        if (k + 1 == k1) atomicExch(&moved[k], 1);  // the next block's first chunk re-checks
+        else carry = true;
       }
     }
     __threadfence();
@@ -224,8 +244,9 @@ void frame_index_plan(int64_t num_rows, int64_t rows_bytes, int64_t* chunk, int6
 int64_t frame_index_words(int64_t num_rows, int64_t rows_bytes) {
   int64_t c, k;
   frame_index_plan(num_rows, rows_bytes, &c, &k);
-  // start, exit, count (+ total), flag, scan partials, saved counts (int32), positions (uint16)
-  return 3 * k + 2 + 2 + scan_partials(k) + (k + 1) / 2 + (kSaved * k + 3) / 4 + 1;
+  // start, exit, count (+ total), flag, scan partials, saved counts (int32), positions
+  // (uint16), moved flags (int32), dirty flags (uint8)
+  return 3 * k + 2 + 2 + scan_partials(k) + (k + 1) / 2 + (kSaved * k + 3) / 4 + 1 + (k + 1) / 2 + (k + 7) / 8 + 1;
 }
 
 hipError_t launch_frame_index(const FrameIndexLaunch& L0, const uint8_t* rows, int64_t* offs, int64_t* ws,
@@ -244,11 +265,14 @@ hipError_t launch_frame_index(const FrameIndexLaunch& L0, const uint8_t* rows, i
   int64_t* partials = flag + 2;
   int32_t* saved = reinterpret_cast<int32_t*>(partials + scan_partials(K));
   uint16_t* pos = reinterpret_cast<uint16_t*>(saved + 2 * ((K + 1) / 2));
+  int32_t* moved = reinterpret_cast<int32_t*>(pos + 4 * ((kSaved * K + 3) / 4) + 4);
+  uint8_t* dirty = reinterpret_cast<uint8_t*>(moved + 2 * ((K + 1) / 2));
   (void)hipMemsetAsync(flag, 0, sizeof(int64_t), s);
   const unsigned blocks = (unsigned)((K + kWG - 1) / kWG);
   hipLaunchKernelGGL(frame_spec_kernel, dim3(blocks), dim3(kWG), 0, s, L, rows, start, exit_, count, pos, saved);
-  hipLaunchKernelGGL(frame_check_kernel, dim3(blocks), dim3(kWG), 0, s, L, start, exit_, flag);
-  hipLaunchKernelGGL(frame_fixup_kernel, dim3(1), dim3(1024), 0, s, L, rows, start, exit_, count, saved, flag);
+  hipLaunchKernelGGL(frame_check_kernel, dim3(blocks), dim3(kWG), 0, s, L, start, exit_, flag, dirty, moved);
+  hipLaunchKernelGGL(frame_fixup_kernel, dim3(1), dim3(1024), 0, s, L, rows, start, exit_, count, saved, flag, dirty,
+                     moved);
   hipError_t e = launch_scan_i64(count, K, partials, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(frame_write_kernel, dim3(blocks), dim3(kWG), 0, s, L, rows, start, exit_, count, pos, saved,

@@ -179,3 +179,18 @@ def test_mixed_stream_decode_large():
     rows = enc.encode(to_device(host), n, 1)
     offs = enc.index_frames(rows.buffer, n)
     assert torch.equal(offs, rows.offsets)
+
+
+@pytest.mark.parametrize("per", ["1", "2", "4"])
+def test_stream_decode_small_chunks_many_fixups(per, monkeypatch):
+    """Chunks of 1-4 frames' bytes (FORY_ROWFMT_IDXFRAMES): many chunks hold no frame
+    start or a misleading one, so most of the chain goes through the fix-up, which
+    visits only dirty chunks and the chunks whose entry it moved."""
+    monkeypatch.setenv("FORY_ROWFMT_IDXFRAMES", per)
+    schema, make = catalog()["mixed40_nulls"]
+    check_stream("mixed40_nulls", schema, make(6000, 17), 6000)
+    schema = _adversarial_schema()
+    enc = encoder_for("adversarial", schema)
+    h = enc.plan.schema_hash
+    cols = _adversarial_columns(800, h if h < 2**63 else h - 2**64, enc.plan.fixed_size, 5, 41)
+    check_stream("adversarial", schema, cols, 800)

@@ -108,10 +108,11 @@ def test_host_varlen_collection_frames():
     for schema, cols in collection_cases(900, 21):
         n = cols[0].length
         expect, eoffs = oracle.encode(schema, cols, n, 2)
-        hp = HostPipeline(NativePlan(schema))
+        hp = HostPipeline(NativePlan(schema), chunk_rows=256)
         rows, offs = hp.encode_var(cols, n, 2)
         assert np.array_equal(rows, expect) and np.array_equal(offs, eoffs)
         assert columns_equal(schema, cols, hp.decode_var(expect, eoffs, n, 2)) == []
+        assert columns_equal(schema, cols, hp.decode_var_into(expect, eoffs, n, 2)) == []
 
 
 def test_host_varlen_errors():
