@@ -17,8 +17,8 @@
 // bound by HBM.
 //
 // Kernels: encode_fixed_v5_kernel (persistent, depth-2 pipelined, 16-byte
-// column chunks; not-null schemas) with encode_fixed_kernel for the tail,
-// nullable schemas and wide rows; decode_fixed_kernel. Rejected variants of
+// column chunks; not-null and nullable schemas) with encode_fixed_kernel for the
+// tail and wide rows; decode_fixed_v5_kernel likewise with decode_fixed_kernel. Rejected variants of
 // round 1 (pipe, v3, v4, one-shot, decode v2/v3/pipe) are gone from the
 // product library; their measurements are in DESIGN.md §6.1.
 #include "kcommon.h"
@@ -204,7 +204,9 @@ __host__ __device__ inline int v3_insn_count(const int* group) {
 // instructions re-read a valid dummy address), so hipcc waits with a counted
 // vmcnt for the older set while the younger set stays in flight. Order per
 // stage: write X -> barrier -> store this tile's rows -> issue X for tile +
-// 2*grid -> barrier. Not-null schemas only (the nullable form spills).
+// 2*grid -> barrier. Nullable schemas take the NUL form (validity bits loaded
+// with the chunks, null bits OR-ed into the LDS bitmaps, bitmaps re-zeroed as the
+// rows leave).
 template <int R, int K, int OPT = 0>
 __device__ __forceinline__ void v5_issue(const uint8_t* const (&ptr)[K], const int (&wk)[K], int64_t r0,
                                          u32x4 (&d)[K]) {
@@ -216,24 +218,52 @@ __device__ __forceinline__ void v5_issue(const uint8_t* const (&ptr)[K], const i
   }
 }
 
-template <int R, int K, int HDR>
+// Nullable schemas (NUL): the E validity bits of a lane's chunk (records r0 + rb ..
+// + E - 1; one byte, two for E = 16) are loaded with the chunk. Fields without
+// validity re-read a dummy address, so every lane still issues 2K loads per tile.
+template <int K>
+__device__ __forceinline__ void v5_issue_bits(const uint8_t* const (&vptr)[K], const int (&wk)[K], int64_t r0,
+                                              uint32_t (&b)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint8_t* p = vptr[k] + (r0 >> 3);
+    b[k] = wk[k] == 1 ? (uint32_t)load_byte(p) | ((uint32_t)load_byte(p + 1) << 8) : (uint32_t)load_byte(p);
+  }
+}
+
+// sf[k]: slot | flags << 16 | nullable-with-validity << 19 | live << 20 | rb << 21.
+// A null record (BinaryWriter.setNullAt) gets its bit OR-ed into the row bitmap
+// and a zero slot.
+template <int R, int K, int HDR, bool NUL = false>
 __device__ __forceinline__ void v5_write(uint8_t* lds, int stride, int hdr_bm, const int (&wk)[K],
-                                         const uint32_t (&sf)[K], const u32x4 (&d)[K]) {
+                                         const uint32_t (&sf)[K], const u32x4 (&d)[K], const uint32_t (&vb)[K]) {
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int w = wk[k];
     if (!(sf[k] & (1u << 20))) continue;
-    const int slot = sf[k] & 0xffff, flags = (sf[k] >> 16) & 0xf, rb = sf[k] >> 21;
+    const int slot = sf[k] & 0xffff, flags = (sf[k] >> 16) & 0x7, rb = sf[k] >> 21;
+    const uint32_t ok = NUL && (sf[k] & (1u << 19)) ? vb[k] >> (rb & 7) : 0xffffffffu;  // bit e: record rb+e valid
+    auto nul = [&](int e) { return NUL && !((ok >> e) & 1); };
     uint8_t* row = lds + rb * stride;
     const u32x4 x = d[k];
     if (w == 8) {
-      put_slot<HDR>(row, hdr_bm, slot, (uint64_t)x.x | ((uint64_t)x.y << 32), false, flags);
-      put_slot<HDR>(row + stride, hdr_bm, slot, (uint64_t)x.z | ((uint64_t)x.w << 32), false, flags);
+      put_slot<HDR>(row, hdr_bm, slot, (uint64_t)x.x | ((uint64_t)x.y << 32), nul(0), flags);
+      put_slot<HDR>(row + stride, hdr_bm, slot, (uint64_t)x.z | ((uint64_t)x.w << 32), nul(1), flags);
     } else if (w == 4) {
-      put_slot<HDR>(row, hdr_bm, slot, x.x, false, flags);
-      put_slot<HDR>(row + stride, hdr_bm, slot, x.y, false, flags);
-      put_slot<HDR>(row + 2 * stride, hdr_bm, slot, x.z, false, flags);
-      put_slot<HDR>(row + 3 * stride, hdr_bm, slot, x.w, false, flags);
+      put_slot<HDR>(row, hdr_bm, slot, x.x, nul(0), flags);
+      put_slot<HDR>(row + stride, hdr_bm, slot, x.y, nul(1), flags);
+      put_slot<HDR>(row + 2 * stride, hdr_bm, slot, x.z, nul(2), flags);
+      put_slot<HDR>(row + 3 * stride, hdr_bm, slot, x.w, nul(3), flags);
+    } else if constexpr (NUL) {  // 2- and 1-byte fields, rolled: unrolled with the null
+      // bits, the NUL form spilled (the dword of record e picked by selects)
+      const int E = 16 / w;
+#pragma unroll 1
+      for (int e = 0; e < E; ++e) {
+        const int q = e / (E / 4);
+        const uint32_t wd = q == 0 ? x.x : q == 1 ? x.y : q == 2 ? x.z : x.w;
+        const uint32_t v = (wd >> (8 * w * (e % (E / 4)))) & (w == 2 ? 0xffffu : 0xffu);
+        put_slot<HDR>(row + e * stride, hdr_bm, slot, v, nul(e), flags);
+      }
     } else if (w == 2) {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
@@ -246,17 +276,35 @@ __device__ __forceinline__ void v5_write(uint8_t* lds, int stride, int hdr_bm, c
   }
 }
 
+// Nullable schemas: the thread that stores 16-B chunk [lo, lo + 16) of the tile
+// image zeroes the null-bitmap dwords inside it once read (BinaryRowWriter.reset
+// for the next tile; same-thread order, so no extra barrier).
+template <int HDR>
+__device__ __forceinline__ void v5_zero_bitmaps(uint8_t* lds, int lo, int hi, int stride, int bm) {
+  int rr = lo / stride;
+#pragma unroll
+  for (int q = 0; q < 2; ++q, ++rr) {
+    const int b0 = rr * stride + HDR, b1 = b0 + bm;
+    for (int o = lo > b0 ? lo : b0; o < (hi < b1 ? hi : b1); o += 4) st32(lds + o, 0u);
+  }
+}
+
 // The tile's rows (R * stride contiguous bytes) leave with non-temporal 16-B
 // stores: the once-written row stream does not displace L2 lines
 // (18.43 -> 18.03 ms at 64M Struct104 rows).
-template <int R, int WG>
-__device__ __forceinline__ void v5_store(const FixedLaunch& L, const uint8_t* lds, uint8_t* dst, int tid) {
+template <int R, int WG, int HDR = 0, bool NUL = false>
+__device__ __forceinline__ void v5_store(const FixedLaunch& L, uint8_t* lds, uint8_t* dst, int tid) {
   const int bytes = R * L.stride;
   const int n16 = bytes >> 4;
-  for (int c = tid; c < n16; c += WG)
+  for (int c = tid; c < n16; c += WG) {
     __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(lds + c * 16), gp(reinterpret_cast<u32x4*>(dst + c * 16)));
+    if constexpr (NUL) v5_zero_bitmaps<HDR>(lds, c * 16, c * 16 + 16, L.stride, L.bitmap_bytes);
+  }
   const int tail4 = (bytes & 15) >> 2;
-  if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
+  if (tid < tail4) {
+    st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
+    if constexpr (NUL) v5_zero_bitmaps<HDR>(lds, n16 * 16 + tid * 4, n16 * 16 + tid * 4 + 4, L.stride, L.bitmap_bytes);
+  }
 }
 
 // XCD-grouped tile order: workgroups are dispatched round-robin over the 8 XCDs
@@ -279,11 +327,9 @@ __device__ __forceinline__ int64_t map_tile(int64_t t, int64_t tiles, int64_t C)
   return blk * 8 * C + (b % 8) * C + b / 8;
 }
 
-template <int R, int WG, int K, int HDR, int OPT = 0>
-__global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
-                                                                 const FixedFieldDev* __restrict__ fields,
-                                                                 uint8_t* __restrict__ out, int64_t tiles,
-                                                                 int64_t xcd_run) {
+template <int R, int WG, int K, int HDR, int OPT, bool NUL>
+__device__ __forceinline__ void encode_v5_body(const FixedLaunch& L, const FixedFieldDev* __restrict__ fields,
+                                               uint8_t* __restrict__ out, int64_t tiles, int64_t xcd_run) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int NW = WG / 64;
   const int tid = threadIdx.x;
@@ -296,6 +342,7 @@ __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
 
   const uint8_t* dummy = fields[L.group[0]].values;  // any valid column (never null: num_rows > 0)
   const uint8_t* ptr[K];
+  const uint8_t* vptr[K];
   int wk[K];
   uint32_t sf[K];
 #pragma unroll
@@ -306,15 +353,23 @@ __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
     const int cpf = R * (ok ? w : 8) / 16;
     const int p = p0 + lane / cpf, c = lane % cpf;
     ptr[k] = dummy;
+    vptr[k] = dummy;
     sf[k] = 0;
     if (ok && p < pend) {
       const FixedFieldDev& fd = fields[p];
+      const int rb = c * (16 / w);
       ptr[k] = fd.values + c * 16;
-      sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (1u << 20) | ((uint32_t)(c * (16 / w)) << 21);
+      const bool nv = (fd.flags & 1) && fd.validity;
+      if (nv) vptr[k] = fd.validity + (rb >> 3);
+      sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (nv ? 1u << 19 : 0u) | (1u << 20) | ((uint32_t)rb << 21);
     }
   }
-  if (tid < R) put_header<HDR>(lds + tid * stride, L);  // constant across tiles (no nullable fields)
+  // frame header + zeroed bitmaps; the header is constant across tiles, the bitmaps
+  // of nullable schemas are re-zeroed chunk by chunk as the rows leave (v5_store)
+  if (tid < R) put_header<HDR>(lds + tid * stride, L);
+  if constexpr (NUL) __syncthreads();  // null bits are OR-ed into the zeroed bitmaps
   u32x4 dA[K], dB[K];
+  uint32_t bA[K], bB[K];
   const int64_t last = tiles - 1;
   // logical tile t -> tile map_tile(t): xcd_run = grid / 8 (each step's grid tiles,
   // one contiguous run per XCD) or 0
@@ -330,24 +385,37 @@ __global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L,
     if (mine <= 0) return;
     tend = (int64_t)blockIdx.x + mine * gridDim.x;
   }
-  v5_issue<R, K, OPT>(ptr, wk, mt(t) * R, dA);
-  v5_issue<R, K, OPT>(ptr, wk, mt(min(t + (int64_t)gridDim.x, tend - 1)) * R, dB);
+  auto issue = [&](int64_t tile, u32x4 (&d)[K], uint32_t (&b)[K]) {
+    v5_issue<R, K, OPT>(ptr, wk, tile * R, d);
+    if constexpr (NUL) v5_issue_bits<K>(vptr, wk, tile * R, b);
+  };
+  issue(mt(t), dA, bA);
+  issue(mt(min(t + (int64_t)gridDim.x, tend - 1)), dB, bB);
   for (;;) {
-    v5_write<R, K, HDR>(lds, stride, hdr_bm, wk, sf, dA);
+    v5_write<R, K, HDR, NUL>(lds, stride, hdr_bm, wk, sf, dA, bA);
     __syncthreads();
-    v5_store<R, WG>(L, lds, out + mt(t) * R * stride, tid);
-    v5_issue<R, K, OPT>(ptr, wk, mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)) * R, dA);
+    v5_store<R, WG, HDR, NUL>(L, lds, out + mt(t) * R * stride, tid);
+    issue(mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)), dA, bA);
     __syncthreads();
     t += gridDim.x;
     if (t >= tend) break;
-    v5_write<R, K, HDR>(lds, stride, hdr_bm, wk, sf, dB);
+    v5_write<R, K, HDR, NUL>(lds, stride, hdr_bm, wk, sf, dB, bB);
     __syncthreads();
-    v5_store<R, WG>(L, lds, out + mt(t) * R * stride, tid);
-    v5_issue<R, K, OPT>(ptr, wk, mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)) * R, dB);
+    v5_store<R, WG, HDR, NUL>(L, lds, out + mt(t) * R * stride, tid);
+    issue(mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)), dB, bB);
     __syncthreads();
     t += gridDim.x;
     if (t >= tend) break;
   }
+}
+
+// NUL (nullable schemas) takes ~90 VGPRs: one 1024-thread workgroup per CU instead
+// of two (forcing 64 spills 27); measured 5.56 vs 4.69 ms for not-null at 16Mi rows.
+template <int R, int WG, int K, int HDR, int OPT = 0, bool NUL = false>
+__global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
+                                                                 uint8_t* __restrict__ out, int64_t tiles,
+                                                                 int64_t xcd_run) {
+  encode_v5_body<R, WG, K, HDR, OPT, NUL>(L, fields, out, tiles, xcd_run);
 }
 
 // ---------------------------------------------------------------------------
@@ -491,9 +559,10 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
 // LDS -> barrier -> each lane gathers ONE field's 16-B column chunk (E = 16/w
 // consecutive records, null -> 0, bool -> 0/1) and stores it non-temporally
 // (one 1-KiB wave instruction per FPI fields, numbered like the encode's,
-// v3_insn_g) -> issue the rows of tile + 2*grid -> barrier. Not-null schemas
-// whose column chunks fit K2 instructions per wave (the null bits are still read:
-// a set bit decodes to 0, as in decode_fixed_kernel).
+// v3_insn_g) -> issue the rows of tile + 2*grid -> barrier. Schemas whose column
+// chunks fit K2 instructions per wave; nullable ones also write the Arrow validity
+// (NUL form, d5_validity). Null bits are always read: a set bit decodes to 0, as
+// in decode_fixed_kernel.
 template <int R, int K>
 __device__ __forceinline__ void d5_issue(const uint8_t* in, int64_t base, int stride, int tid, int n16, int WGT,
                                          u32x4 (&d)[K]) {
@@ -516,6 +585,37 @@ __device__ __forceinline__ void d5_write(uint8_t* lds, int tid, int n16, int WGT
 
 // Lane k-th column chunk: E records from rb of field slot `sf` (slot | flags << 16 |
 // valid << 20 | rb << 21) gathered from the LDS rows, stored to optr (column + rb * w).
+// Nullable schemas (NUL): the lane's E validity bits (1 = valid, Arrow) are OR-ed
+// across the 32/E lanes that share a 32-bit word of the field's validity (xor
+// shuffles: those lanes are adjacent and the groups aligned), and the group's first
+// lane stores the word's 4 bytes (tiles are 64 records: no byte is shared between
+// tiles).
+template <int R, int K2, int HDR, bool NUL>
+__device__ __forceinline__ void d5_validity(const uint8_t* lds, int stride, const int (&wk)[K2],
+                                            const uint32_t (&sf)[K2], uint8_t* const (&vout)[K2], int64_t r0,
+                                            int lane) {
+#pragma unroll
+  for (int k = 0; k < K2; ++k) {
+    const int w = wk[k];  // wave-uniform
+    const int E = 16 / w;
+    const int rb = sf[k] >> 21;
+    uint32_t m = 0;
+    if (vout[k]) {
+      const int slot = sf[k] & 0xffff;
+      const uint8_t* b = lds + rb * stride + HDR + ((slot >> 5) << 2);
+      const uint32_t bit = 1u << (slot & 31);
+      for (int e = 0; e < E; ++e) m |= (ld32(b + e * stride) & bit) ? 0u : 1u << e;  // BinaryRow.isNullAt
+    }
+    uint32_t word = m << (rb & 31);
+    for (int sh = 1; sh < 32 / E; sh <<= 1) word |= __shfl_xor(word, sh);
+    if (vout[k] && (rb & 31) == 0) {
+      uint8_t* v = vout[k] + ((r0 + rb) >> 3);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) store_byte(v + q, (uint8_t)(word >> (8 * q)));
+    }
+  }
+}
+
 template <int R, int K2, int HDR>
 __device__ __forceinline__ void d5_columns(const uint8_t* lds, int stride, int hdr_bm, const int (&wk)[K2],
                                            const uint32_t (&sf)[K2], uint8_t* const (&optr)[K2], int64_t r0) {
@@ -539,31 +639,33 @@ __device__ __forceinline__ void d5_columns(const uint8_t* lds, int stride, int h
       x = u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
     } else if (w == 4) {
       x = u32x4{(uint32_t)val(0), (uint32_t)val(1), (uint32_t)val(2), (uint32_t)val(3)};
-    } else if (w == 2) {
-      uint32_t h[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) h[q] = (uint32_t)(val(2 * q) & 0xffff) | ((uint32_t)(val(2 * q + 1) & 0xffff) << 16);
-      x = u32x4{h[0], h[1], h[2], h[3]};
     } else {
-      uint32_t h[4];
-#pragma unroll
+      // 2- and 1-byte fields: one dword (2 or 4 records) per iteration of a rolled
+      // loop, placed by selects; unrolled, the 16 records' LDS reads were all hoisted
+      // and the kernel spilled ~30 VGPRs on every schema (this branch is cold for
+      // Struct104, the spill code was not)
+      const int per = 4 / w;  // records per dword
+      uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+#pragma unroll 1
       for (int q = 0; q < 4; ++q) {
         uint32_t acc = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          uint32_t b = (uint32_t)(val(4 * q + e) & 0xff);
+        for (int e = 0; e < per; ++e) {
+          uint32_t b = (uint32_t)val(per * q + e) & (w == 2 ? 0xffffu : 0xffu);
           if (flags & 2) b = b ? 1 : 0;  // MemoryBuffer.getBoolean
-          acc |= b << (8 * e);
+          acc |= b << (8 * w * e);
         }
-        h[q] = acc;
+        h0 = q == 0 ? acc : h0;
+        h1 = q == 1 ? acc : h1;
+        h2 = q == 2 ? acc : h2;
+        h3 = q == 3 ? acc : h3;
       }
-      x = u32x4{h[0], h[1], h[2], h[3]};
+      x = u32x4{h0, h1, h2, h3};
     }
     __builtin_nontemporal_store(x, gp(reinterpret_cast<u32x4*>(optr[k] + r0 * w)));
   }
 }
 
-template <int R, int WG, int K, int K2, int HDR, int OPT = 0>
+template <int R, int WG, int K, int K2, int HDR, int OPT = 0, bool NUL = false>
 __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
                                                                  const FixedFieldDev* __restrict__ fields,
                                                                  const uint8_t* __restrict__ in, int64_t tiles,
@@ -582,6 +684,7 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
   int wk[K2];
   uint32_t sf[K2];
   uint8_t* optr[K2];
+  uint8_t* vout[K2];
 #pragma unroll
   for (int k = 0; k < K2; ++k) {
     int w = 0, p0 = 0, pend = 0;
@@ -591,11 +694,13 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
     const int p = p0 + lane / cpf, c = lane % cpf;
     sf[k] = 0;
     optr[k] = nullptr;
+    vout[k] = nullptr;
     if (ok && p < pend) {
       const FixedFieldDev& fd = fields[p];
       const int rb = c * (16 / w);
       sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (1u << 20) | ((uint32_t)rb << 21);
       optr[k] = fd.out_values + (int64_t)rb * w;
+      if ((fd.flags & 1) && fd.out_validity) vout[k] = fd.out_validity;
     }
   }
   u32x4 dA[K], dB[K];
@@ -619,6 +724,7 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
     __syncthreads();
     if (HDR && tid < R) check_frame<HDR>(lds + tid * stride, L, status);
     d5_columns<R, K2, HDR>(lds, stride, hdr_bm, wk, sf, optr, mt(t) * R);
+    if constexpr (NUL) d5_validity<R, K2, HDR, NUL>(lds, stride, wk, sf, vout, mt(t) * R, lane);
     d5_issue<R, K>(in, mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, d);
     __syncthreads();
     t += gridDim.x;
@@ -643,11 +749,11 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
 // XCD-blocked 16.45 / 16.35, + nt column loads 16.38 / 16.12.
 constexpr int kV5R = 64, kV5WG = 1024, kV5K = 3;
 
-template <int HDR>
+template <int HDR, bool NUL>
 hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const int64_t full = L.num_rows / kV5R;
   if (full > 0) {
-    auto* k = &encode_fixed_v5_kernel<kV5R, kV5WG, kV5K, HDR, 1>;
+    auto* k = &encode_fixed_v5_kernel<kV5R, kV5WG, kV5K, HDR, 1, NUL>;
     raise_lds_cap(k);
     const size_t lds = (size_t)kV5R * L.stride;
     const int64_t grid = persistent_grid(k, lds, full, kV5WG);
@@ -669,9 +775,9 @@ hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const int64_t tiles = (L.num_rows + TR - 1) / TR;
   const size_t lds = (size_t)TR * L.stride;
   if constexpr (TR == 64) {
-    // v5: not-null schemas whose chunk instructions fit K per wave
-    if (!L.any_nullable && (v3_insn_count<kV5R>(L.group) + kV5WG / 64 - 1) / (kV5WG / 64) <= kV5K)
-      return launch_encode_v5<HDR>(L, out, s);
+    // v5: schemas whose chunk instructions fit K per wave (nullable ones: the NUL form)
+    if ((v3_insn_count<kV5R>(L.group) + kV5WG / 64 - 1) / (kV5WG / 64) <= kV5K)
+      return L.any_nullable ? launch_encode_v5<HDR, true>(L, out, s) : launch_encode_v5<HDR, false>(L, out, s);
   }
   auto* k = &encode_fixed_kernel<TR, HDR>;
   raise_lds_cap(k);
@@ -687,7 +793,7 @@ constexpr int kD5R = 64, kD5WG = 1024, kD5K = 4, kD5K2 = 3;
 
 template <int HDR>
 bool decode_v5_fits(const FixedLaunch& L) {
-  return !L.any_nullable && L.cols_aligned16 && kD5R * L.stride <= kD5K * kD5WG * 16 &&
+  return L.cols_aligned16 && kD5R * L.stride <= kD5K * kD5WG * 16 &&
          (kD5R * L.stride) % 16 == 0 && v3_insn_count<kD5R>(L.group) <= kD5K2 * (kD5WG / 64);
 }
 
@@ -695,7 +801,8 @@ template <int HDR>
 hipError_t launch_decode_v5(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
   const int64_t full = L.num_rows / kD5R;
   if (full > 0) {
-    auto* k = &decode_fixed_v5_kernel<kD5R, kD5WG, kD5K, kD5K2, HDR>;
+    auto* k = L.any_nullable ? &decode_fixed_v5_kernel<kD5R, kD5WG, kD5K, kD5K2, HDR, 0, true>
+                             : &decode_fixed_v5_kernel<kD5R, kD5WG, kD5K, kD5K2, HDR, 0, false>;
     raise_lds_cap(k);
     const size_t lds = (size_t)kD5R * L.stride;
     const int64_t grid = persistent_grid(k, lds, full, kD5WG);
