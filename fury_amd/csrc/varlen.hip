@@ -1105,14 +1105,30 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // LDS -> LDS copy of n bytes (src any alignment, dst 4-byte aligned), zero
 // padded to round8(n). Reads up to 4 bytes past the source span (staging slack).
+// Bytes [8 sb, 8 sb + 32) of the 64-bit pair (hi:lo) -- v_alignbyte_b32.
+__device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, int sb) {
+  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sb);
+}
+
+// 16 bytes per step with all five source dwords read before the four stores (the
+// per-dword loop waited out one LDS round trip per dword: src and dst may alias as
+// far as the compiler knows).
 __device__ __forceinline__ void lds_copy_padded(uint8_t* dst, const uint8_t* src, int64_t n) {
   const int sb = (int)(reinterpret_cast<uintptr_t>(src) & 3);
   const uint8_t* s0 = src - sb;
   const int64_t n4 = (n + 3) & ~int64_t(3);
-  for (int64_t k = 0; k < n4; k += 4) {
+  int64_t k = 0;
+  for (; k + 16 <= n; k += 16) {
+    const uint32_t a0 = ld32(s0 + k), a1 = ld32(s0 + k + 4), a2 = ld32(s0 + k + 8), a3 = ld32(s0 + k + 12);
+    const uint32_t a4 = sb ? ld32(s0 + k + 16) : 0u;
+    st32(dst + k, funnel(a0, a1, sb));
+    st32(dst + k + 4, funnel(a1, a2, sb));
+    st32(dst + k + 8, funnel(a2, a3, sb));
+    st32(dst + k + 12, funnel(a3, a4, sb));
+  }
+  for (; k < n4; k += 4) {
     const uint32_t a = ld32(s0 + k);
-    uint32_t w = a;
-    if (sb) w = (a >> (8 * sb)) | (ld32(s0 + k + 4) << (32 - 8 * sb));
+    uint32_t w = sb ? funnel(a, ld32(s0 + k + 4), sb) : a;
     if (n - k < 4) w &= (1u << (8 * (n - k))) - 1u;
     st32(dst + k, w);
   }
@@ -1129,11 +1145,20 @@ __device__ __forceinline__ void lds_copy_any(uint8_t* dst, const uint8_t* src, i
   const int sb = (int)(reinterpret_cast<uintptr_t>(s) & 3);
   const uint8_t* s0 = s - sb;
   const int m = (n - k) & ~3;
-  for (int j = 0; j < m; j += 4) {
-    const uint32_t a = ld32(s0 + j);
-    st32(dst + k + j, sb ? (a >> (8 * sb)) | (ld32(s0 + j + 4) << (32 - 8 * sb)) : a);
+  int j = 0;
+  for (; j + 16 <= m; j += 16) {  // loads before stores, as lds_copy_padded
+    const uint32_t a0 = ld32(s0 + j), a1 = ld32(s0 + j + 4), a2 = ld32(s0 + j + 8), a3 = ld32(s0 + j + 12);
+    const uint32_t a4 = sb ? ld32(s0 + j + 16) : 0u;
+    st32(dst + k + j, funnel(a0, a1, sb));
+    st32(dst + k + j + 4, funnel(a1, a2, sb));
+    st32(dst + k + j + 8, funnel(a2, a3, sb));
+    st32(dst + k + j + 12, funnel(a3, a4, sb));
   }
-  for (int j = k + m; j < n; ++j) dst[j] = src[j];
+  for (; j < m; j += 4) {
+    const uint32_t a = ld32(s0 + j);
+    st32(dst + k + j, sb ? funnel(a, ld32(s0 + j + 4), sb) : a);
+  }
+  for (int q = k + m; q < n; ++q) dst[q] = src[q];
 }
 
 __device__ __forceinline__ void st64_lds(uint8_t* p, uint64_t v) {  // 4-byte aligned LDS
@@ -1248,11 +1273,21 @@ __device__ __forceinline__ void flat_place(const VarFieldDev& f, bool staged, co
       const uint8_t* sv = stg + vofs;
       const int64_t A = (base >> 3) & ~int64_t(3);  // first staged bitmap byte
       uint8_t* abm = row + p + 8;
-      for (int64_t j = 0; j < n; ++j) {
+      for (int64_t j = 0; j < n;) {  // a staged validity byte at a time: all-valid runs skip
         const int64_t q = e0 + j;
-        if ((sv[(q >> 3) - A] >> (q & 7)) & 1) continue;
-        abm[j >> 3] |= (uint8_t)(1u << (j & 7));
-        for (int b = 0; b < w; ++b) dst[j * w + b] = 0;
+        const int bi = (int)(q & 7);
+        const int take = (int)(n - j < 8 - bi ? n - j : 8 - bi);
+        const uint32_t m = ((1u << take) - 1u) << bi;
+        const uint32_t byte = sv[(q >> 3) - A];
+        if ((byte & m) != m) {
+          for (int t = 0; t < take; ++t) {
+            if ((byte >> (bi + t)) & 1) continue;
+            const int64_t jj = j + t;
+            abm[jj >> 3] |= (uint8_t)(1u << (jj & 7));
+            for (int b = 0; b < w; ++b) dst[jj * w + b] = 0;
+          }
+        }
+        j += take;
       }
     }
   } else if (!f.is_list) {
@@ -1987,10 +2022,30 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
         } else {  // BinaryArray.toXArray; null items (BinaryArray.isNullAt) read as 0
           const uint8_t* abm = row + rel + 8;
           if (w == 8 || w == 4) {  // src 4-byte aligned (8-padded row offsets), d w-aligned
-            for (int64_t j = 0; j < n; ++j) {
-              const bool en = (abm[j >> 3] >> (j & 7)) & 1;
-              st32(d + j * w, en ? 0u : ld32(src + j * w));
-              if (w == 8) st32(d + j * w + 4, en ? 0u : ld32(src + j * w + 4));
+            // a bitmap byte (8 items) at a time: items of a null-free byte move as up to
+            // 16 dwords, all loads before the stores; bytes with nulls item by item
+            for (int64_t j = 0; j < n; j += 8) {
+              const int take = n - j < 8 ? (int)(n - j) : 8;
+              const uint32_t nb = abm[j >> 3] & ((1u << take) - 1u);
+              const uint8_t* sp = src + j * w;
+              uint8_t* dp = d + j * w;
+              if (!nb) {
+                const int nd = take * w / 4;
+                for (int h = 0; h < nd; h += 8) {
+                  uint32_t t[8];
+#pragma unroll
+                  for (int u = 0; u < 8; ++u) t[u] = h + u < nd ? ld32(sp + 4 * (h + u)) : 0u;
+#pragma unroll
+                  for (int u = 0; u < 8; ++u)
+                    if (h + u < nd) st32(dp + 4 * (h + u), t[u]);
+                }
+              } else {
+                for (int t = 0; t < take; ++t) {
+                  const bool en = (nb >> t) & 1;
+                  st32(dp + t * w, en ? 0u : ld32(sp + t * w));
+                  if (w == 8) st32(dp + t * w + 4, en ? 0u : ld32(sp + t * w + 4));
+                }
+              }
             }
           } else {
             for (int64_t j = 0; j < n; ++j) {
@@ -2022,10 +2077,17 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
         const int nwd = O1 > O0 ? (int)(((O1 - 1) >> 5) - W0 + 1) : 0;
         for (int k = lane; k < nwd; k += 64) bw[k] = 0;
         wave_lds_sync();
-        if (live && n > 0) {
+        if (live && n > 0) {  // a bitmap byte (8 items) per step, at most two words each
           const uint8_t* abm = row + rel + 8;
-          for (int64_t j = 0; j < n; ++j)
-            if (!((abm[j >> 3] >> (j & 7)) & 1)) atomicOr(&bw[((e0 + j) >> 5) - W0], 1u << ((e0 + j) & 31));
+          for (int64_t j = 0; j < n; j += 8) {
+            const int take = n - j < 8 ? (int)(n - j) : 8;
+            const uint32_t vbits = ~(uint32_t)abm[j >> 3] & ((1u << take) - 1u);  // 1 = valid item
+            if (!vbits) continue;
+            const int64_t q = e0 + j;
+            const int sh = (int)(q & 31);
+            atomicOr(&bw[(q >> 5) - W0], vbits << sh);
+            if (sh + take > 32 && (vbits >> (32 - sh))) atomicOr(&bw[(q >> 5) - W0 + 1], vbits >> (32 - sh));
+          }
         }
         wave_lds_sync();
         uint32_t* gv = reinterpret_cast<uint32_t*>(f.out_item_validity) + W0;
