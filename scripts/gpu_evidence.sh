@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest exit $rc" >> gpurun_out/pytest_gpu.log; tail -2 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 OUT=gpurun_out/prof_final bash scripts/profile.sh > gpurun_out/profile.log 2>&1
@@ -19,3 +19,5 @@ for cfg in mixed40 nested; do
   timeout -k 10 400 python bench.py --config $cfg --steps 10 --warmup 3 --cpu-seconds 8 > gpurun_out/bench_$cfg.json 2> gpurun_out/bench_$cfg.err
   rc=$?; echo "bench $cfg exit $rc"; cat gpurun_out/bench_$cfg.json; [ $rc -eq 0 ] || exit $rc
 done
+timeout -k 10 120 python scripts/bench_nullable_fixed.py 16777216 0 > gpurun_out/bench_nullable.json
+rc=$?; echo "bench nullable exit $rc"; cat gpurun_out/bench_nullable.json; [ $rc -eq 0 ] || exit $rc
