@@ -248,6 +248,28 @@ def test_nullable_fixed_many_tiles_parity(name):
         assert columns_equal(schema, ref, to_host(enc.decode(buf, n, frame, None))) == []
 
 
+@pytest.mark.parametrize("shift", [1, 4])
+def test_nullable_fixed_unaligned_validity(shift):
+    """Validity buffers at odd / 4-byte offsets (the NUL v5 encode reads each chunk's
+    validity byte(s) at any alignment): bytes still equal the oracle's."""
+    schema, make = catalog()["struct104_boxed"]
+    n = 64 * 40 + 9
+    cols = make(n, 13)
+    enc = encoder_for("struct104_boxed")
+    dcols, keep = [], []
+    for c in to_device(cols):
+        if c.validity is not None:
+            big = torch.zeros(c.validity.numel() + 16, dtype=torch.uint8, device="cuda")
+            big[shift:shift + c.validity.numel()] = c.validity
+            keep.append(big)
+            c.validity = big[shift:shift + c.validity.numel()]
+        dcols.append(c)
+    for frame in (0, 1):
+        expect, _ = oracle.encode(schema, cols, n, frame)
+        got = enc.encode(dcols, n, frame).buffer.cpu().numpy()
+        assert np.array_equal(got, expect), frame
+
+
 def test_mixed_and_nested_large_round_trip(varlen_engine):
     for name, n in (("mixed40_nulls", 300_000), ("nested_nulls", 300_000), ("flat_mix", 100_000)):
         schema, make = catalog()[name]
