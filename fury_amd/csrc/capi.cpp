@@ -384,6 +384,7 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   int32_t est = 0;  // ~32 B per string, 16 items (+ their validity bits) per list
   for (const fory_amd::VarFieldDev& v : var) est = std::max(est, v.is_list ? 16 * v.w + 2 : 32);
   L->var_est_row = est;
+  L->iv_split = var.size() == 1 && var[0].is_list && var[0].out_item_validity ? 1 : 0;
   L->cols = static_cast<const ColumnDev*>(ws);
   L->prog = reinterpret_cast<const fory_amd::Op*>(static_cast<uint8_t*>(ws) + col_bytes);
   L->num_ops = (int32_t)p.program.size();

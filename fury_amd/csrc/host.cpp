@@ -134,6 +134,16 @@ int hcopy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStrea
   return rc;
 }
 
+// End of a pipelined call: every stream of the context drained, the first error
+// reported (an asynchronous kernel fault surfaces in the call that caused it, not in
+// the context's next call).
+int sync_all(fory_host_ctx* c) {
+  int rc = hip_check(hipStreamSynchronize(c->s_out), "hipStreamSynchronize(out)");
+  const int rk = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize(kernels)");
+  const int ri = hip_check(hipStreamSynchronize(c->s_in), "hipStreamSynchronize(in)");
+  return rc ? rc : (rk ? rk : ri);
+}
+
 // Chunk k's row range.
 void chunk_range(const fory_host_ctx* c, int64_t n, int64_t k, int64_t* a, int64_t* rows) {
   *a = k * c->chunk;
@@ -371,9 +381,7 @@ int host_encode_fixed(fory_host_ctx* c, const fory_column* host_cols, int64_t n,
     if (!rc) rc = d2h_rows_windows(*W, B.rows, a, rows, stride, c->s_out);
     if (!rc) rc = hip_check(hipEventRecord(c->ev_out[b], c->s_out), "hipEventRecord");
   }
-  const int rc_sync = hip_check(hipStreamSynchronize(c->s_out), "hipStreamSynchronize");
-  (void)hipStreamSynchronize(c->s_k);
-  (void)hipStreamSynchronize(c->s_in);
+  const int rc_sync = sync_all(c);
   if (rc) return rc;
   if (rc_sync) return rc_sync;
   for (int b = 0; b < 2; ++b) {
@@ -449,9 +457,7 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
     }
     if (!rc) rc = hip_check(hipEventRecord(c->ev_out[b], c->s_out), "hipEventRecord");
   }
-  const int rc_sync = hip_check(hipStreamSynchronize(c->s_out), "hipStreamSynchronize");
-  (void)hipStreamSynchronize(c->s_k);
-  (void)hipStreamSynchronize(c->s_in);
+  const int rc_sync = sync_all(c);
   if (rc) return rc;
   if (rc_sync) return rc_sync;
   for (int b = 0; b < 2; ++b) {
@@ -789,9 +795,7 @@ int host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, i
     S.used = true;
     base += total;
   }
-  const int rc_sync = hip_check(hipStreamSynchronize(c->s_out), "hipStreamSynchronize");
-  (void)hipStreamSynchronize(c->s_k);
-  (void)hipStreamSynchronize(c->s_in);
+  const int rc_sync = sync_all(c);
   if (rc) return rc;
   if (rc_sync) return rc_sync;
   if (out_bytes) *out_bytes = base;
@@ -1302,9 +1306,7 @@ int host_decode_var_into(fory_host_ctx* c, const uint8_t* host_rows, const int64
     S.used = true;
     for (int i = 0; i < N; ++i) E[i] += cnt[i], VB[i] += vbytes[i];
   }
-  const int rc_sync = hip_check(hipStreamSynchronize(c->s_out), "hipStreamSynchronize");
-  (void)hipStreamSynchronize(c->s_k);
-  (void)hipStreamSynchronize(c->s_in);
+  const int rc_sync = sync_all(c);
   if (!rc && !rc_sync && !overflow)
     for (const Stash& st : stash) out[st.col].validity[st.byte] |= spin[st.slot];
   (void)hipHostFree(pin);

@@ -68,6 +68,7 @@ struct VarLaunch {
   int32_t* spill_count;         // workspace: number of spilled tiles
   int64_t mean_row;             // decode: mean row/frame bytes of the batch (tile image sizing), 0 = unknown
   int32_t pl_all;               // encode tile kernel: wave 0 places var payloads too (A/B)
+  int32_t iv_split;             // decode tile kernel: the one var field is a list with item validity (wave 1 assembles it)
   int32_t level2;               // decode lengths pass 2: sizes of string/binary list/map
                                 // elements (container offsets already scanned)
 };

@@ -1878,6 +1878,42 @@ __device__ __forceinline__ bool frame_ok(const VarLaunch& L, const uint8_t* fp, 
   return size_ok;
 }
 
+// Arrow item validity of a list field's staged span [O0, O1) (1 = valid item),
+// assembled in LDS words bw (BinaryArray.isNullAt of each item, a bitmap byte at a
+// time) and stored; words shared with a neighbouring tile touch only this span's bits.
+__device__ __forceinline__ void dec_item_validity(const VarFieldDev& f, int64_t O0, int64_t O1, int64_t e0, int64_t n,
+                                                  const uint8_t* abm, bool live, int lane, uint32_t* bw) {
+  const int64_t W0 = O0 >> 5;
+  const int nwd = O1 > O0 ? (int)(((O1 - 1) >> 5) - W0 + 1) : 0;
+  for (int k = lane; k < nwd; k += 64) bw[k] = 0;
+  wave_lds_sync();
+  if (live && n > 0) {  // a bitmap byte (8 items) per step, at most two words each
+    for (int64_t j = 0; j < n; j += 8) {
+      const int take = n - j < 8 ? (int)(n - j) : 8;
+      const uint32_t vbits = ~(uint32_t)abm[j >> 3] & ((1u << take) - 1u);  // 1 = valid item
+      if (!vbits) continue;
+      const int64_t q = e0 + j;
+      const int sh = (int)(q & 31);
+      atomicOr(&bw[(q >> 5) - W0], vbits << sh);
+      if (sh + take > 32 && (vbits >> (32 - sh))) atomicOr(&bw[(q >> 5) - W0 + 1], vbits >> (32 - sh));
+    }
+  }
+  wave_lds_sync();
+  uint32_t* gv = reinterpret_cast<uint32_t*>(f.out_item_validity) + W0;
+  for (int k = lane; k < nwd; k += 64) {
+    const int64_t lo = (W0 + k) * 32, hi = lo + 32;
+    const int b0 = O0 > lo ? (int)(O0 - lo) : 0, b1 = O1 < hi ? (int)(O1 - lo) : 32;
+    const uint32_t span = (b1 - b0 == 32) ? ~0u : (((1u << (b1 - b0)) - 1u) << b0);
+    if (span == ~0u) {
+      *gp(gv + k) = bw[k];
+    } else {  // word shared with a neighbouring tile: touch only this span's bits
+      atomicAnd(gv + k, ~span);
+      atomicOr(gv + k, bw[k]);
+    }
+  }
+  wave_lds_sync();
+}
+
 template <int HDR, bool WRITE, int NW, bool SPILL>
 __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
                                                                   const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
@@ -1992,6 +2028,8 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   DEC_STAMP(3);
   // var fields: one per wave at a time, output span staged in LDS
   uint8_t* stg = lds + cap + wave * stg_bytes;
+  const bool ivs = NW >= 2 && L.iv_split;  // wave 1 assembles field 0's item validity
+  uint32_t* ivw = reinterpret_cast<uint32_t*>(sbase + (L.num_struct ? (1 + L.num_struct) * 64 : 0));
   for (int v = wave; v < L.num_var; v += NW) {
     const VarFieldDev& f = vf[v];
     const bool islist = f.is_list;
@@ -2071,39 +2109,10 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
         }
       }
       wave_lds_sync();
-      if (islist && f.out_item_validity) {  // the span's item validity, assembled in LDS (staging reused)
-        uint32_t* bw = reinterpret_cast<uint32_t*>(stg);
-        const int64_t W0 = O0 >> 5;
-        const int nwd = O1 > O0 ? (int)(((O1 - 1) >> 5) - W0 + 1) : 0;
-        for (int k = lane; k < nwd; k += 64) bw[k] = 0;
-        wave_lds_sync();
-        if (live && n > 0) {  // a bitmap byte (8 items) per step, at most two words each
-          const uint8_t* abm = row + rel + 8;
-          for (int64_t j = 0; j < n; j += 8) {
-            const int take = n - j < 8 ? (int)(n - j) : 8;
-            const uint32_t vbits = ~(uint32_t)abm[j >> 3] & ((1u << take) - 1u);  // 1 = valid item
-            if (!vbits) continue;
-            const int64_t q = e0 + j;
-            const int sh = (int)(q & 31);
-            atomicOr(&bw[(q >> 5) - W0], vbits << sh);
-            if (sh + take > 32 && (vbits >> (32 - sh))) atomicOr(&bw[(q >> 5) - W0 + 1], vbits >> (32 - sh));
-          }
-        }
-        wave_lds_sync();
-        uint32_t* gv = reinterpret_cast<uint32_t*>(f.out_item_validity) + W0;
-        for (int k = lane; k < nwd; k += 64) {
-          const int64_t lo = (W0 + k) * 32, hi = lo + 32;
-          const int b0 = O0 > lo ? (int)(O0 - lo) : 0, b1 = O1 < hi ? (int)(O1 - lo) : 32;
-          const uint32_t span = (b1 - b0 == 32) ? ~0u : (((1u << (b1 - b0)) - 1u) << b0);
-          if (span == ~0u) {
-            *gp(gv + k) = bw[k];
-          } else {  // word shared with a neighbouring tile: touch only this span's bits
-            atomicAnd(gv + k, ~span);
-            atomicOr(gv + k, bw[k]);
-          }
-        }
-        wave_lds_sync();
-      }
+      // the span's item validity, assembled in LDS (staging reused); with one var field
+      // and an idle second wave, that wave does it (below) while this one copies
+      if (islist && f.out_item_validity && !ivs)
+        dec_item_validity(f, O0, O1, e0, n, row + rel + 8, live, lane, reinterpret_cast<uint32_t*>(stg));
     } else if (live && n > 0) {
       if (!islist) {
         copy_out(f.out_values + e0, src, n);
@@ -2133,6 +2142,17 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
         }
       }
     }
+  }
+  if (ivs && wave == 1) {  // field 0's item validity (the staged span of wave 0's pass)
+    const VarFieldDev& f = vf[0];
+    int64_t rel = 0, n = 0;
+    if (!bad) flat_var_slot(L, f, st, sbase, lane, row, row_len, &rel, &n, false, status);
+    const int64_t O0 = __shfl(obase, 0);
+    const int64_t incl = wave_incl_scan64(n, lane);
+    const int64_t O1 = O0 + __shfl(incl, 63);
+    const int64_t S = (O1 - O0) * f.w;
+    if ((f.iflags & 2) == 0 && S >= 0 && S + 32 <= stg_bytes)
+      dec_item_validity(f, O0, O1, O0 + incl - n, n, row + rel + 8, live, lane, ivw);
   }
   if (WRITE && L.prof) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -2321,7 +2341,9 @@ unsigned spill_grid(K* k, const VarLaunch& L, size_t lds, int wg) {
 // Decode values pass: staging only for the waves that own var fields.
 size_t flat_lds_dec(const VarLaunch& L, int cap, int nw) {
   const int nslot = L.num_var < nw ? L.num_var : nw;
-  return (size_t)cap + (size_t)nslot * L.stg_bytes + sbase_lds(L);
+  // wave 1's item-validity words: a staged span holds <= stg_bytes items
+  const size_t ivw = nw >= 2 && L.iv_split ? (size_t)((L.stg_bytes / 8 + 16 + 15) & ~15) : 0;
+  return (size_t)cap + (size_t)nslot * L.stg_bytes + sbase_lds(L) + ivw;
 }
 
 // Decode staging per slot: the output span of a 64-record tile of the widest
