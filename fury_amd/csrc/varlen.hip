@@ -1180,7 +1180,7 @@ __device__ __forceinline__ int fix_owner(int j, int nbatch, int nw) {
   return nbatch <= 2 * (nw - 1) ? 1 + j % (nw - 1) : j % nw;
 }
 
-template <int W, int NW>
+template <int W, int NW, bool NEST = true>
 __device__ __forceinline__ void flat_enc_fixed(const VarLaunch& L, const FixedFieldDev* __restrict__ fix, int g0, int g1,
                                                int j0, int nbatch, int wave, int lane, bool live, int64_t i,
                                                uint8_t* row, const StructDev* __restrict__ st,
@@ -1202,7 +1202,7 @@ __device__ __forceinline__ void flat_enc_fixed(const VarLaunch& L, const FixedFi
         const FixedFieldDev& f = fix[k0 + k];
         uint64_t x = ((vb[k] >> (ii & 7)) & 1) ? v[k] : 0;
         if (f.flags & 2) x = x ? 1 : 0;
-        if (!f.parent) {
+        if (!NEST || !f.parent) {
           st64_lds(row + L.bitmap_bytes + 8 * f.slot, x);
         } else {
           const int32_t b = sbase[f.parent * 64 + lane];
@@ -1462,7 +1462,7 @@ __device__ __forceinline__ void flat_dec_struct_bases(const VarLaunch& L, const 
 
 // Debug timeline (FORY_ROWFMT_VARPROF=1, L.prof set): thread 0 stamps
 // s_memrealtime (100 MHz) at phase boundaries into L.prof[tile * 8 + k] (a uniform
-// branch when off; the PROF template parameter is always false now).
+// branch when off).
 #define FLAT_STAMP(k)                                                                            \
   do {                                                                                          \
     if (L.prof && tid == 0) L.prof[tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime();          \
@@ -1472,7 +1472,7 @@ __device__ __forceinline__ void flat_dec_struct_bases(const VarLaunch& L, const 
 // (Mixed-like plans are LDS-limited at 4 workgroups per CU anyway) and a lean one for
 // 5 waves per SIMD (small-row plans such as Nested are register-limited: encode
 // 1.49 -> 1.26 ms; its spills would cost Mixed 27 %). launch_flat_enc_t picks by occupancy.
-template <int HDR, int NW, bool PROF, bool SPILL>
+template <int HDR, int NW, bool NEST, bool SPILL>
 __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
                                                                   const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
                                                                   const StructDev* __restrict__ st,
@@ -1520,7 +1520,7 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
       pe1[k] = lv ? f.offsets[i + 1] : ee;
     }
   }
-  const bool pre_layout = wave == 0 && !L.num_struct && L.num_var > 0;
+  const bool pre_layout = !NEST && wave == 0 && L.num_var > 0;
   int64_t le0[kFixBatch], le1[kFixBatch];
   uint32_t lvb[kFixBatch];
   if (pre_layout) {
@@ -1576,7 +1576,7 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
       }
       for (int b = 0; b < L.bitmap_bytes; b += 4) st32(row + b, 0);
     }
-    if (L.num_struct) {  // nested struct fields: program walk
+    if constexpr (NEST) {  // nested struct fields: program walk
       flat_enc_layout_nested(L, prog, cols, live, i, st, lane, row, pos, sbase);
     } else {
     // null bits of nullable fixed fields (this wave only: no bitmap races)
@@ -1643,16 +1643,16 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
     }
   }
   FLAT_STAMP(2);
-  if (L.num_struct) __syncthreads();  // nested fixed slots need the child-row offsets
+  if constexpr (NEST) __syncthreads();  // nested fixed slots need the child-row offsets
   // fixed slots (all waves): BinaryRowWriter.write(ordinal, v), null -> 0
   {
     int jb[5];
     jb[0] = 0;
     for (int g = 0; g < 4; ++g) jb[g + 1] = jb[g] + (L.fix_group[g + 1] - L.fix_group[g] + kFixBatch - 1) / kFixBatch;
-    flat_enc_fixed<8, NW>(L, fix, L.fix_group[0], L.fix_group[1], jb[0], jb[4], wave, lane, live, i, row, st, sbase);
-    flat_enc_fixed<4, NW>(L, fix, L.fix_group[1], L.fix_group[2], jb[1], jb[4], wave, lane, live, i, row, st, sbase);
-    flat_enc_fixed<2, NW>(L, fix, L.fix_group[2], L.fix_group[3], jb[2], jb[4], wave, lane, live, i, row, st, sbase);
-    flat_enc_fixed<1, NW>(L, fix, L.fix_group[3], L.fix_group[4], jb[3], jb[4], wave, lane, live, i, row, st, sbase);
+    flat_enc_fixed<8, NW, NEST>(L, fix, L.fix_group[0], L.fix_group[1], jb[0], jb[4], wave, lane, live, i, row, st, sbase);
+    flat_enc_fixed<4, NW, NEST>(L, fix, L.fix_group[1], L.fix_group[2], jb[1], jb[4], wave, lane, live, i, row, st, sbase);
+    flat_enc_fixed<2, NW, NEST>(L, fix, L.fix_group[2], L.fix_group[3], jb[2], jb[4], wave, lane, live, i, row, st, sbase);
+    flat_enc_fixed<1, NW, NEST>(L, fix, L.fix_group[3], L.fix_group[4], jb[3], jb[4], wave, lane, live, i, row, st, sbase);
   }
   if (L.prof) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   FLAT_STAMP(3);
@@ -1734,14 +1734,14 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
       const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,                         \
       const StructDev* __restrict__ st, const int64_t* __restrict__ offs, uint8_t* __restrict__ out,    \
       int64_t capacity, int32_t* status, int cap, SpillArgs sp
-template <int HDR, int NW, bool PROF, bool SPILL>
+template <int HDR, int NW, bool NEST, bool SPILL>
 __global__ __launch_bounds__(64 * NW) void var_encode_flat_kernel(FORY_VAR_ENC_PARAMS) {
-  var_encode_flat_body<HDR, NW, PROF, SPILL>(L, prog, cols, fix, vf, st, offs, out, capacity, status, cap, sp);
+  var_encode_flat_body<HDR, NW, NEST, SPILL>(L, prog, cols, fix, vf, st, offs, out, capacity, status, cap, sp);
 }
-template <int HDR, int NW, bool PROF, bool SPILL>
+template <int HDR, int NW, bool NEST, bool SPILL>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(5, 8))) void var_encode_flat_lean_kernel(
     FORY_VAR_ENC_PARAMS) {
-  var_encode_flat_body<HDR, NW, PROF, SPILL>(L, prog, cols, fix, vf, st, offs, out, capacity, status, cap, sp);
+  var_encode_flat_body<HDR, NW, NEST, SPILL>(L, prog, cols, fix, vf, st, offs, out, capacity, status, cap, sp);
 }
 #undef FORY_VAR_ENC_PARAMS
 
@@ -2386,13 +2386,13 @@ void var_diag(const char* what, K* k, int threads, int cap, int stg, size_t lds)
 
 // Encode: default or lean kernel (5 waves per SIMD register budget), whichever keeps
 // more workgroups per CU resident with its own staging / image sizing (ties: default).
-template <int HDR, int NW, bool PROF>
+template <int HDR, int NW, bool NEST>
 void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                        int cap, hipStream_t s) {
   VarLaunch L = L0;
   L.pl_all = 1;
-  auto* kd = &var_encode_flat_kernel<HDR, NW, PROF, false>;
-  auto* kl = &var_encode_flat_lean_kernel<HDR, NW, PROF, false>;
+  auto* kd = &var_encode_flat_kernel<HDR, NW, NEST, false>;
+  auto* kl = &var_encode_flat_lean_kernel<HDR, NW, NEST, false>;
   auto size_for = [&](decltype(kd) kk, int* stg, int* c) {
     VarLaunch T = L;
     *stg = enc_stg_bytes(kk, T, capacity, cap, NW);
@@ -2413,7 +2413,7 @@ void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, i
   var_diag(lean ? "encode (lean)" : "encode", k, 64 * NW, cap, L.stg_bytes, flat_lds_enc(L, cap, NW));
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds_enc(L, cap, NW), s, L, L.prog,
                      L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, cap, sp);
-  auto* k2 = lean ? &var_encode_flat_lean_kernel<HDR, NW, PROF, true> : &var_encode_flat_kernel<HDR, NW, PROF, true>;
+  auto* k2 = lean ? &var_encode_flat_lean_kernel<HDR, NW, NEST, true> : &var_encode_flat_kernel<HDR, NW, NEST, true>;
   raise_lds_cap(k2);
   hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds_enc(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
                      flat_lds_enc(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, sp.cap,
@@ -2423,7 +2423,10 @@ void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, i
 template <int HDR, int NW>
 void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                      int cap, hipStream_t s) {
-  launch_flat_enc_t<HDR, NW, false>(L, offs, out, capacity, status, cap, s);  // (timeline stamps: runtime L.prof)
+  // plans with nested struct fields and flat ones get their own instantiations: each
+  // carries only its layout path (the other one's registers would count against it)
+  if (L.num_struct) launch_flat_enc_t<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
+  else launch_flat_enc_t<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
 }
 
 template <int HDR, bool WRITE, int NW>
