@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "../../include/fory_rowfmt.h"
@@ -125,12 +126,39 @@ bool host_pinned(const void* p) {
   return a.type != hipMemoryTypeUnregistered;
 }
 
+// Pageable memory goes through one process-wide pinned bounce buffer (8 MiB pieces,
+// host memcpy + async copy + stream sync), never through the runtime's pageable
+// hipMemcpy: a full-batch pageable H2D was seen to fault ("illegal memory access")
+// intermittently after other host ranges had been registered and unregistered in
+// the process (tests/test_gpu_host.py). The pageable path was synchronous already.
+std::mutex g_bounce_mu;
+uint8_t* g_bounce = nullptr;
+constexpr size_t kBounce = size_t(8) << 20;
+
 int hcopy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s, const char* what) {
   if (bytes == 0) return FORY_OK;
-  if (host_pinned(kind == hipMemcpyHostToDevice ? src : dst))
-    return hip_check(hipMemcpyAsync(dst, src, bytes, kind, s), what);
+  const bool h2d = kind == hipMemcpyHostToDevice;
+  if (host_pinned(h2d ? src : dst)) return hip_check(hipMemcpyAsync(dst, src, bytes, kind, s), what);
   int rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-  if (!rc) rc = hip_check(hipMemcpy(dst, src, bytes, kind), what);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lock(g_bounce_mu);
+  if (!g_bounce) {
+    rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&g_bounce), kBounce, hipHostMallocPortable),
+                   "hipHostMalloc(bounce)");
+    if (rc) return rc;
+  }
+  for (size_t off = 0; off < bytes && !rc; off += kBounce) {
+    const size_t len = bytes - off < kBounce ? bytes - off : kBounce;
+    if (h2d) {
+      std::memcpy(g_bounce, static_cast<const uint8_t*>(src) + off, len);
+      rc = hip_check(hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, g_bounce, len, kind, s), what);
+      if (!rc) rc = hip_check(hipStreamSynchronize(s), what);
+    } else {
+      rc = hip_check(hipMemcpyAsync(g_bounce, static_cast<const uint8_t*>(src) + off, len, kind, s), what);
+      if (!rc) rc = hip_check(hipStreamSynchronize(s), what);
+      if (!rc) std::memcpy(static_cast<uint8_t*>(dst) + off, g_bounce, len);
+    }
+  }
   return rc;
 }
 
