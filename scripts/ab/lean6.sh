@@ -1,3 +1,5 @@
+# Experiment script of a rejected variant (6 waves/SIMD nested encode); its
+# FORY_AB_LEAN6 knob left the library with it. Kept as the record of how it was measured.
 set -o pipefail
 mkdir -p gpurun_out
 FORY_AB_LEAN6=1 FORY_ROWFMT_VARDIAG=1 timeout 100 python bench.py --config nested --steps 2 --warmup 1 --no-cpu-baseline 2>&1 >/dev/null | grep "encode" | sort | uniq
