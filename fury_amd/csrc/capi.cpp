@@ -169,51 +169,103 @@ int bind_var(const Plan& p, const fory_column* cols, int64_t n, std::vector<Colu
 }
 
 // Plan tables reach the workspace by an async copy from pinned host memory that
-// outlives the call: per device a ring of pinned slots (process lifetime, shared by
-// all threads under a mutex), each reused only after the copy that last read it
-// has completed (its event). A copy straight from a local vector could be read by
-// the DMA engine after the call returned (a flaky plan table in the host pipeline).
-struct UploadRing {
-  static constexpr int kSlots = 32;
-  void* buf[kSlots] = {};
-  size_t cap[kSlots] = {};
-  hipEvent_t ev[kSlots] = {};
-  hipStream_t st[kSlots] = {};  // the stream the slot's copy was queued on
-  bool used[kSlots] = {};
-  int next = 0;
+// outlives the call: per device a pool of pinned slots (process lifetime). A slot is
+// taken only when the copy that last read it has completed (hipEventQuery: nobody
+// waits under a lock); when every slot is still in flight the pool grows, up to
+// kMaxSlots, and only then the oldest slot is waited for — outside the lock. A copy
+// straight from a local vector could be read by the DMA engine after the call
+// returned (a flaky plan table in the host pipeline, round 1).
+struct UploadSlot {
+  void* buf = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  hipStream_t st = nullptr;  // the stream the slot's last copy was queued on
+  uint64_t stamp = 0;        // queue order of that copy
+  bool pending = false;      // a copy was queued and not yet seen complete
+  bool busy = false;         // taken by a call right now
 };
 
-std::mutex g_upload_mu;
+struct UploadRing {
+  static constexpr size_t kMaxSlots = 256;
+  std::mutex mu;
+  std::vector<UploadSlot*> slots;  // never freed (process lifetime)
+  uint64_t clock = 0;
+};
+
+std::mutex g_rings_mu;
 std::map<int, UploadRing*>* g_rings = new std::map<int, UploadRing*>();  // never freed
+
+// hipEventQuery: true when the slot's copy is done (clears the "not ready" status it
+// leaves as the thread's last error, so a caller's hipGetLastError is not disturbed).
+bool slot_done(UploadSlot* sl) {
+  if (!sl->pending) return true;
+  const hipError_t e = hipEventQuery(sl->ev);
+  if (e == hipErrorNotReady) {
+    (void)hipGetLastError();
+    return false;
+  }
+  sl->pending = false;  // complete (or an error the next synchronising call reports)
+  return true;
+}
 
 int upload(void* ws, const void* host, int64_t bytes, hipStream_t s) {
   if (bytes == 0) return FORY_OK;
   int dev = 0;
   (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> lock(g_upload_mu);
-  UploadRing*& rp = (*g_rings)[dev];
-  if (!rp) rp = new UploadRing();
-  UploadRing& r = *rp;
-  const int k = r.next;
-  r.next = (r.next + 1) % UploadRing::kSlots;
-  hipError_t e = hipSuccess;
-  if (r.used[k]) e = hipEventSynchronize(r.ev[k]);  // the slot's previous copy has been read
-  if (e == hipSuccess && !r.ev[k]) e = hipEventCreateWithFlags(&r.ev[k], hipEventDisableTiming);
-  if (e == hipSuccess && r.cap[k] < (size_t)bytes) {
-    if (r.buf[k]) (void)hipHostFree(r.buf[k]);
-    r.buf[k] = nullptr;
-    r.cap[k] = 0;
-    const size_t want = std::max<size_t>((size_t)bytes, 64 * 1024);
-    e = hipHostMalloc(&r.buf[k], want, hipHostMallocDefault);
-    if (e == hipSuccess) r.cap[k] = want;
+  UploadRing* r = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(g_rings_mu);
+    UploadRing*& rp = (*g_rings)[dev];
+    if (!rp) rp = new UploadRing();
+    r = rp;
   }
-  if (e != hipSuccess) return hip_fail(e, "plan table staging");
-  std::memcpy(r.buf[k], host, (size_t)bytes);
-  e = hipMemcpyAsync(ws, r.buf[k], (size_t)bytes, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipEventRecord(r.ev[k], s);
-  if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(plan table)");
-  r.used[k] = true;
-  r.st[k] = s;
+  UploadSlot* sl = nullptr;
+  bool wait_first = false;
+  {
+    std::lock_guard<std::mutex> lock(r->mu);
+    UploadSlot* oldest = nullptr;
+    for (UploadSlot* c : r->slots) {
+      if (c->busy) continue;
+      if (slot_done(c)) {
+        if (!sl || (sl->cap < (size_t)bytes && c->cap >= (size_t)bytes)) sl = c;
+        if (sl->cap >= (size_t)bytes) break;
+      } else if (!oldest || c->stamp < oldest->stamp) {
+        oldest = c;
+      }
+    }
+    if (!sl && r->slots.size() < UploadRing::kMaxSlots) {
+      sl = new UploadSlot();
+      r->slots.push_back(sl);
+    }
+    if (!sl) sl = oldest, wait_first = true;
+    if (!sl) return fail(FORY_ERR_DEVICE, "plan table staging: every slot is taken");
+    sl->busy = true;
+  }
+  hipError_t e = hipSuccess;
+  if (wait_first) e = hipEventSynchronize(sl->ev);  // the oldest copy, outside the lock
+  if (e == hipSuccess && !sl->ev) e = hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming);
+  if (e == hipSuccess && sl->cap < (size_t)bytes) {
+    if (sl->buf) (void)hipHostFree(sl->buf);
+    sl->buf = nullptr;
+    sl->cap = 0;
+    const size_t want = std::max<size_t>((size_t)bytes, 64 * 1024);
+    e = hipHostMalloc(&sl->buf, want, hipHostMallocPortable);
+    if (e == hipSuccess) sl->cap = want;
+  }
+  bool queued = false;
+  if (e == hipSuccess) {
+    std::memcpy(sl->buf, host, (size_t)bytes);
+    e = hipMemcpyAsync(ws, sl->buf, (size_t)bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipEventRecord(sl->ev, s), queued = true;
+  }
+  {
+    std::lock_guard<std::mutex> lock(r->mu);
+    if (queued || wait_first) sl->pending = queued;
+    sl->st = s;
+    sl->stamp = ++r->clock;
+    sl->busy = false;
+  }
+  if (e != hipSuccess) return hip_fail(e, "plan table upload");
   return FORY_OK;
 }
 
@@ -372,11 +424,11 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
     }
     L->fix_group[4] = at;
   }
-  L->prof = fory_amd::var_prof_buffer((n + 63) / 64);
+  L->kn = p.kn;
+  L->prof = fory_amd::var_prof_buffer((n + 63) / 64, p.kn.prof != 0);
   L->spill_count = spill_ptr(p, ws, n);
   L->spill = L->spill_count + 4;
-  const char* stg = getenv("FORY_ROWFMT_VARSTG");
-  L->stg_bytes = stg ? std::max(256, std::min(16384, atoi(stg))) & ~15 : 2048;
+  L->stg_bytes = p.kn.var_stg > 0 ? std::max(256, std::min(16384, p.kn.var_stg)) & ~15 : 2048;
   int64_t nested_fixed = 0;
   for (const fory_amd::StructDev& sd : st) nested_fixed += sd.hdr + 8LL * sd.nfields;
   for (const fory_amd::VarFieldDev& v : var) nested_fixed += v.is_list ? 8 : 0;
@@ -514,13 +566,22 @@ int64_t fory_rowfmt_debug_timeline(uint64_t* host, int64_t max_words) {
 const char* fory_rowfmt_last_error(void) { return g_err.c_str(); }
 
 // Library-internal (host.cpp): a stream about to be destroyed (its work complete) —
-// ring slots whose copy was queued on it are free, and their events are never
-// waited on again (an event of a destroyed stream is not safe to synchronise).
+// slots whose last copy was queued on it are waited for now, while the stream is
+// alive, and never queried again through an event of a destroyed stream.
 void fory_rowfmt_internal_retire_stream(void* stream) {
-  std::lock_guard<std::mutex> lock(g_upload_mu);
-  for (auto& kv : *g_rings)
-    for (int k = 0; k < UploadRing::kSlots; ++k)
-      if (kv.second->used[k] && kv.second->st[k] == static_cast<hipStream_t>(stream)) kv.second->used[k] = false;
+  std::vector<UploadRing*> rings;
+  {
+    std::lock_guard<std::mutex> lock(g_rings_mu);
+    for (auto& kv : *g_rings) rings.push_back(kv.second);
+  }
+  for (UploadRing* r : rings) {
+    std::lock_guard<std::mutex> lock(r->mu);
+    for (UploadSlot* sl : r->slots)
+      if (sl->pending && !sl->busy && sl->st == static_cast<hipStream_t>(stream)) {
+        (void)hipEventSynchronize(sl->ev);
+        sl->pending = false;
+      }
+  }
 }
 
 // Library-internal (host.cpp): shares last_error and the planner's column layout.
@@ -564,6 +625,7 @@ int fory_rowfmt_plan_create(const fory_field_desc* fields, int32_t num_desc, for
     delete plan;
     return fail(FORY_ERR_UNSUPPORTED, "device path supports struct nesting depth <= 8");
   }
+  plan->p.kn = fory_amd::knobs_from_env();  // launch knobs fixed for the plan's life
   *out_plan = plan;
   return FORY_OK;
 }
@@ -809,7 +871,7 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows, const int64_t*
 
 int64_t fory_rowfmt_index_workspace_bytes(const fory_plan* plan, int64_t num_rows, int64_t rows_bytes) {
   if (!plan || num_rows < 0 || rows_bytes < 0) return -1;
-  return align_up(fory_amd::frame_index_words(num_rows, rows_bytes) * 8);
+  return align_up(fory_amd::frame_index_words(num_rows, rows_bytes, plan->p.kn.idx_frames) * 8);
 }
 
 int fory_rowfmt_index_frames(const fory_plan* plan, const void* d_rows, int64_t rows_bytes, int64_t num_rows,
@@ -846,6 +908,7 @@ int fory_rowfmt_index_frames(const fory_plan* plan, const void* d_rows, int64_t 
   L.num_rows = num_rows;
   L.schema_hash = p.schema_hash;
   L.fixed_size = p.fixed_size;
+  L.idx_frames = p.kn.idx_frames;
   e = fory_amd::launch_frame_index(L, static_cast<const uint8_t*>(d_rows), d_row_offsets,
                                    static_cast<int64_t*>(d_workspace), d_status, s);
   return e == hipSuccess ? FORY_OK : hip_fail(e, "index_frames");
@@ -882,11 +945,21 @@ int fory_rowfmt_split_windows(const int64_t* row_offsets, int64_t stride, int64_
 
 int fory_rowfmt_read_status(const int32_t* d_status, void* stream) {
   if (!d_status) return FORY_OK;
-  int32_t h = 0;
+  // the status word lands in pinned memory of this thread (an async DMA; never the
+  // runtime's pageable path), allocated once per thread and kept for its life
+  thread_local int32_t* pinned_word = nullptr;
+  hipError_t e = hipSuccess;
+  if (!pinned_word) e = hipHostMalloc(reinterpret_cast<void**>(&pinned_word), 64, hipHostMallocPortable);
+  if (e != hipSuccess) {
+    pinned_word = nullptr;
+    return hip_fail(e, "read_status (pinned word)");
+  }
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipError_t e = hipMemcpyAsync(&h, d_status, sizeof(h), hipMemcpyDeviceToHost, s);
+  *pinned_word = 0;
+  e = hipMemcpyAsync(pinned_word, d_status, sizeof(int32_t), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(e, "read_status");
+  const int32_t h = *pinned_word;
   switch (h) {
     case FORY_OK: return FORY_OK;
     case FORY_ERR_SCHEMA_MISMATCH:

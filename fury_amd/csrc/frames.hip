@@ -149,7 +149,10 @@ __global__ __launch_bounds__(1024) void frame_fixup_kernel(FrameIndexLaunch L, c
     for (int64_t k = k0; k < k1; ++k) {
       bool need = carry;
       carry = false;
-      if (k == k0 && k > 0) need = atomicExch(&moved[k - 1], 0) != 0;  // the previous block's last chunk
+      // the previous block's last chunk: acquire pairs with the release below, so a
+      // seen flag comes with the exit_[k-1] stored before it
+      if (k == k0 && k > 0)
+        need = __hip_atomic_exchange(&moved[k - 1], 0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0;
       if (dirty[k]) {
         need = true;
         dirty[k] = 0;
@@ -177,7 +180,8 @@ __global__ __launch_bounds__(1024) void frame_fixup_kernel(FrameIndexLaunch L, c
         saved[k] = -1;  // the positions step 1 saved are not this chain's: the write pass re-walks
         __hip_atomic_store(&exit_[k], ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         mine = true;
-        if (k + 1 == k1) atomicExch(&moved[k], 1);  // the next block's first chunk re-checks
+        // the next block's first chunk re-checks: release orders the exit_ store first
+        if (k + 1 == k1) __hip_atomic_exchange(&moved[k], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         else carry = true;
       }
     }
@@ -229,21 +233,20 @@ __global__ __launch_bounds__(kWG) void frame_write_kernel(FrameIndexLaunch L, co
 
 }  // namespace
 
-void frame_index_plan(int64_t num_rows, int64_t rows_bytes, int64_t* chunk, int64_t* chunks) {
+void frame_index_plan(int64_t num_rows, int64_t rows_bytes, int32_t idx_frames, int64_t* chunk, int64_t* chunks) {
   // ~16 frames per chunk at the batch's mean frame size, in [1, 64] KiB
-  // (FORY_ROWFMT_IDXFRAMES overrides the 16, for A/B)
+  // (the plan's FORY_ROWFMT_IDXFRAMES knob overrides the 16, for A/B)
   const int64_t n = num_rows > 0 ? num_rows : 1;
-  const char* e = getenv("FORY_ROWFMT_IDXFRAMES");
-  const int64_t per = e ? atoi(e) : 16;
+  const int64_t per = idx_frames > 0 ? idx_frames : 16;
   int64_t c = (per * (rows_bytes / n) + 255) / 256 * 256;
   c = c < 1024 ? 1024 : (c > 65536 ? 65536 : c);
   *chunk = c;
   *chunks = rows_bytes > 0 ? (rows_bytes + c - 1) / c : 0;
 }
 
-int64_t frame_index_words(int64_t num_rows, int64_t rows_bytes) {
+int64_t frame_index_words(int64_t num_rows, int64_t rows_bytes, int32_t idx_frames) {
   int64_t c, k;
-  frame_index_plan(num_rows, rows_bytes, &c, &k);
+  frame_index_plan(num_rows, rows_bytes, idx_frames, &c, &k);
   // start, exit, count (+ total), flag, scan partials, saved counts (int32), positions
   // (uint16), moved flags (int32), dirty flags (uint8)
   return 3 * k + 2 + 2 + scan_partials(k) + (k + 1) / 2 + (kSaved * k + 3) / 4 + 1 + (k + 1) / 2 + (k + 7) / 8 + 1;
@@ -252,7 +255,7 @@ int64_t frame_index_words(int64_t num_rows, int64_t rows_bytes) {
 hipError_t launch_frame_index(const FrameIndexLaunch& L0, const uint8_t* rows, int64_t* offs, int64_t* ws,
                               int32_t* status, hipStream_t s) {
   FrameIndexLaunch L = L0;
-  frame_index_plan(L.num_rows, L.rows_bytes, &L.chunk, &L.chunks);
+  frame_index_plan(L.num_rows, L.rows_bytes, L.idx_frames, &L.chunk, &L.chunks);
   if (L.num_rows <= 0) {
     (void)hipMemsetAsync(offs, 0, sizeof(int64_t), s);
     return hipGetLastError();

@@ -36,6 +36,25 @@ struct Slice {  // one column's device chunk buffers
   uint8_t* validity = nullptr;
 };
 
+// Pinned staging of a context for caller memory that is not pinned over the whole
+// copy (pageable, or a range only partly inside a registration). A ring of blocks:
+// an H2D piece is memcpy'd into a block and DMA'd from it; a D2H piece is DMA'd into
+// a block and memcpy'd out when the block is next needed or at the end of the call
+// (drain). A block is reused only after the event of its last DMA completed, so the
+// host memcpy of one piece overlaps the DMA of the others and nothing is ever copied
+// by the runtime's own pageable path. Owned by one context (one call at a time): no
+// lock, nothing shared across contexts or devices.
+struct Staging {
+  static constexpr size_t kBlock = size_t(4) << 20;
+  static constexpr int kBlocks = 8;
+  uint8_t* mem = nullptr;  // kBlocks x kBlock, hipHostMalloc'd on first use
+  hipEvent_t ev[kBlocks] = {};
+  bool inflight[kBlocks] = {};  // ev recorded, completion not yet observed
+  struct Owed { uint8_t* dst = nullptr; size_t len = 0; } owed[kBlocks];  // D2H host copies pending
+  int next = 0;
+  int64_t pieces = 0;  // statistics: pieces staged over the context's life
+};
+
 }  // namespace
 
 struct fory_host_ctx {
@@ -84,6 +103,9 @@ struct fory_host_ctx {
   int64_t* dec_offs = nullptr;
   void* dec_ws = nullptr;
   int32_t* dec_status = nullptr;
+  Staging stage;               // pageable caller memory
+  uint8_t* hpin = nullptr;     // pinned scratch: level totals, frame end, validity stash
+  int64_t hpin_bytes = 0;
 };
 
 namespace {
@@ -111,65 +133,134 @@ int fail_host(int code, const std::string& msg) { return fory_rowfmt_internal_se
 
 int64_t validity_bytes(int64_t rows) { return ((rows + 7) / 8 + 3) / 4 * 4; }
 
-// Caller host memory is copied asynchronously only when it is pinned (registered
-// with fory_rowfmt_host_register / hipHostRegister, or hipHostMalloc): the chunk
-// pipeline orders those copies with events. Pageable memory is copied with a
-// blocking hipMemcpy once the stream's earlier work (and the events it waits on) is
-// done: the async pageable path was seen to leave a chunk kernel reading columns
-// whose H2D had not landed (tests/test_gpu_host.py, intermittent, first rows zero).
-bool host_pinned(const void* p) {
-  hipPointerAttribute_t a{};
-  if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+// Is [p, p + bytes) pinned as ONE mapping, so that an async DMA may read or write it
+// directly? Round 2 judged a copy by its first byte only: a range that begins inside
+// a registration (hipHostRegister / fory_rowfmt_host_register, or hipHostMalloc) and
+// runs past its end was handed to hipMemcpyAsync as if pinned, and the DMA then
+// reaches host pages the device has no mapping for. Now the first and the last byte
+// must both be pinned, map to device addresses exactly bytes - 1 apart, and lie in
+// the allocation range the runtime reports. Anything else is staged (Staging).
+bool pinned_range(const void* p, size_t bytes) {
+  if (!p || bytes == 0) return false;
+  const uint8_t* first = static_cast<const uint8_t*>(p);
+  const uint8_t* last = first + (bytes - 1);
+  hipPointerAttribute_t a{}, b{};
+  if (hipPointerGetAttributes(&a, first) != hipSuccess || hipPointerGetAttributes(&b, last) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
-  return a.type != hipMemoryTypeUnregistered;
+  if (a.type == hipMemoryTypeUnregistered || b.type == hipMemoryTypeUnregistered) return false;
+  if (!a.devicePointer || !b.devicePointer ||
+      static_cast<const uint8_t*>(b.devicePointer) - static_cast<const uint8_t*>(a.devicePointer) !=
+          static_cast<std::ptrdiff_t>(bytes - 1))
+    return false;
+  void* start = nullptr;
+  size_t size = 0;
+  if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, const_cast<uint8_t*>(first)) ==
+          hipSuccess &&
+      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, const_cast<uint8_t*>(first)) == hipSuccess &&
+      start && size) {
+    // the runtime may report the range in host or in device addresses: either must hold the copy
+    const uint8_t* s0 = static_cast<const uint8_t*>(start);
+    const uint8_t* d0 = static_cast<const uint8_t*>(a.devicePointer);
+    const bool host_in = first >= s0 && last < s0 + size;
+    const bool dev_in = d0 >= s0 && d0 + (bytes - 1) < s0 + size;
+    if (!host_in && !dev_in) return false;
+  } else {
+    (void)hipGetLastError();
+  }
+  return true;
 }
 
-// Pageable memory goes through one process-wide pinned bounce buffer (8 MiB pieces,
-// host memcpy + async copy + stream sync), never through the runtime's pageable
-// hipMemcpy: a full-batch pageable H2D was seen to fault ("illegal memory access")
-// intermittently after other host ranges had been registered and unregistered in
-// the process (tests/test_gpu_host.py). The pageable path was synchronous already.
-std::mutex g_bounce_mu;
-uint8_t* g_bounce = nullptr;
-constexpr size_t kBounce = size_t(8) << 20;
+int stage_alloc(Staging& st) {
+  if (st.mem) return FORY_OK;
+  int rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&st.mem), Staging::kBlock * Staging::kBlocks,
+                                   hipHostMallocPortable),
+                     "hipHostMalloc(staging)");
+  for (int j = 0; j < Staging::kBlocks && !rc; ++j)
+    if (!st.ev[j]) rc = hip_check(hipEventCreateWithFlags(&st.ev[j], hipEventDisableTiming), "hipEventCreate");
+  return rc;
+}
 
-int hcopy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s, const char* what) {
+// Block j free for a new piece: its last DMA done, an owed D2H host copy made.
+int stage_retire(Staging& st, int j) {
+  if (st.inflight[j]) {
+    int rc = hip_check(hipEventSynchronize(st.ev[j]), "hipEventSynchronize(staging)");
+    if (rc) return rc;
+    st.inflight[j] = false;
+  }
+  if (st.owed[j].dst) {
+    std::memcpy(st.owed[j].dst, st.mem + (size_t)j * Staging::kBlock, st.owed[j].len);
+    st.owed[j] = Staging::Owed{};
+  }
+  return FORY_OK;
+}
+
+// Every staged piece complete, every owed D2H copy in caller memory (oldest first).
+int stage_drain(Staging& st) {
+  if (!st.mem) return FORY_OK;
+  int rc = FORY_OK;
+  for (int i = 0; i < Staging::kBlocks; ++i) {
+    const int r = stage_retire(st, (st.next + i) % Staging::kBlocks);
+    if (!rc) rc = r;
+  }
+  return rc;
+}
+
+// One copy between caller host memory and the device, queued on stream s. Pinned
+// over its whole range: one async DMA. Otherwise through the context's staging: H2D
+// pieces are in pinned memory before this returns (the caller may reuse its buffer);
+// D2H pieces land in caller memory at the next stage_drain (finish()).
+int hcopy(fory_host_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s,
+          const char* what) {
   if (bytes == 0) return FORY_OK;
   const bool h2d = kind == hipMemcpyHostToDevice;
-  if (host_pinned(h2d ? src : dst)) return hip_check(hipMemcpyAsync(dst, src, bytes, kind, s), what);
-  int rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-  if (rc) return rc;
-  std::lock_guard<std::mutex> lock(g_bounce_mu);
-  if (!g_bounce) {
-    rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&g_bounce), kBounce, hipHostMallocPortable),
-                   "hipHostMalloc(bounce)");
-    if (rc) return rc;
-  }
-  for (size_t off = 0; off < bytes && !rc; off += kBounce) {
-    const size_t len = bytes - off < kBounce ? bytes - off : kBounce;
+  if (pinned_range(h2d ? src : dst, bytes)) return hip_check(hipMemcpyAsync(dst, src, bytes, kind, s), what);
+  Staging& st = c->stage;
+  int rc = stage_alloc(st);
+  for (size_t off = 0; off < bytes && !rc; off += Staging::kBlock) {
+    const size_t len = std::min(bytes - off, Staging::kBlock);
+    const int j = st.next;
+    st.next = (st.next + 1) % Staging::kBlocks;
+    rc = stage_retire(st, j);
+    if (rc) break;
+    uint8_t* blk = st.mem + (size_t)j * Staging::kBlock;
     if (h2d) {
-      std::memcpy(g_bounce, static_cast<const uint8_t*>(src) + off, len);
-      rc = hip_check(hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, g_bounce, len, kind, s), what);
-      if (!rc) rc = hip_check(hipStreamSynchronize(s), what);
+      std::memcpy(blk, static_cast<const uint8_t*>(src) + off, len);
+      rc = hip_check(hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, blk, len, kind, s), what);
     } else {
-      rc = hip_check(hipMemcpyAsync(g_bounce, static_cast<const uint8_t*>(src) + off, len, kind, s), what);
-      if (!rc) rc = hip_check(hipStreamSynchronize(s), what);
-      if (!rc) std::memcpy(static_cast<uint8_t*>(dst) + off, g_bounce, len);
+      rc = hip_check(hipMemcpyAsync(blk, static_cast<const uint8_t*>(src) + off, len, kind, s), what);
+      if (!rc) st.owed[j] = Staging::Owed{static_cast<uint8_t*>(dst) + off, len};
     }
+    if (!rc) rc = hip_check(hipEventRecord(st.ev[j], s), "hipEventRecord(staging)");
+    if (!rc) st.inflight[j] = true;
+    ++st.pieces;
   }
+  return rc;
+}
+
+// Context-owned pinned scratch of at least `bytes` (grown, never per call).
+int ensure_hpin(fory_host_ctx* c, int64_t bytes) {
+  if (bytes <= c->hpin_bytes) return FORY_OK;
+  if (c->hpin) (void)hipHostFree(c->hpin);
+  c->hpin = nullptr;
+  c->hpin_bytes = 0;
+  const int64_t sz = align_up(bytes + bytes / 2);
+  int rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)sz, hipHostMallocDefault),
+                     "hipHostMalloc(ctx scratch)");
+  if (!rc) c->hpin_bytes = sz;
   return rc;
 }
 
 // End of a pipelined call: every stream of the context drained, the first error
 // reported (an asynchronous kernel fault surfaces in the call that caused it, not in
-// the context's next call).
+// the context's next call), and every staged D2H piece in caller memory.
 int sync_all(fory_host_ctx* c) {
   int rc = hip_check(hipStreamSynchronize(c->s_out), "hipStreamSynchronize(out)");
   const int rk = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize(kernels)");
   const int ri = hip_check(hipStreamSynchronize(c->s_in), "hipStreamSynchronize(in)");
-  return rc ? rc : (rk ? rk : ri);
+  const int rs = stage_drain(c->stage);
+  return rc ? rc : (rk ? rk : (ri ? ri : rs));
 }
 
 // Chunk k's row range.
@@ -295,6 +386,10 @@ void fory_rowfmt_host_ctx_destroy(fory_host_ctx* c) {
   if (c->vstatus) (void)hipFree(c->vstatus);
   for (uint8_t* b : {c->dbuf, c->drows, c->dout})
     if (b) (void)hipFree(b);
+  for (hipEvent_t e : c->stage.ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stage.mem) (void)hipHostFree(c->stage.mem);
+  if (c->hpin) (void)hipHostFree(c->hpin);
   delete c;
 }
 
@@ -351,12 +446,12 @@ int split_rows(const int64_t* offs, int64_t stride, int64_t n, OutWindows* W) {
 
 // Queues the D2H of rows [a, a + rows) (contiguous at `src`, row i at (i - a) * stride)
 // into the windows they belong to.
-int d2h_rows_windows(const OutWindows& W, const uint8_t* src, int64_t a, int64_t rows, int64_t stride, hipStream_t s) {
+int d2h_rows_windows(fory_host_ctx* c, const OutWindows& W, const uint8_t* src, int64_t a, int64_t rows, int64_t stride, hipStream_t s) {
   int rc = FORY_OK;
   for (size_t w = 0; w + 1 < W.first.size() && !rc; ++w) {
     const int64_t lo = std::max(a, W.first[w]), hi = std::min(a + rows, W.first[w + 1]);
     if (lo >= hi) continue;
-    rc = hcopy(W.ptr[w] + (lo - W.first[w]) * stride, src + (lo - a) * stride, (size_t)((hi - lo) * stride), hipMemcpyDeviceToHost, s, "D2H");
+    rc = hcopy(c, W.ptr[w] + (lo - W.first[w]) * stride, src + (lo - a) * stride, (size_t)((hi - lo) * stride), hipMemcpyDeviceToHost, s, "D2H");
   }
   return rc;
 }
@@ -390,9 +485,9 @@ int host_encode_fixed(fory_host_ctx* c, const fory_column* host_cols, int64_t n,
     if (k >= 2) rc = hip_check(hipStreamWaitEvent(c->s_in, c->ev_k[b], 0), "hipStreamWaitEvent");
     for (int i = 0; i < c->info.num_columns && !rc; ++i) {
       const fory_column& h = host_cols[i];
-      rc = hcopy(B.cols[i].values, static_cast<const uint8_t*>(h.values) + a * c->width[i], (size_t)(rows * c->width[i]), hipMemcpyHostToDevice, c->s_in, "H2D");
+      rc = hcopy(c, B.cols[i].values, static_cast<const uint8_t*>(h.values) + a * c->width[i], (size_t)(rows * c->width[i]), hipMemcpyHostToDevice, c->s_in, "H2D");
       if (!rc && c->nullable[i] && h.validity)
-        rc = hcopy(B.cols[i].validity, h.validity + a / 8, (size_t)((rows + 7) / 8), hipMemcpyHostToDevice, c->s_in, "H2D validity");
+        rc = hcopy(c, B.cols[i].validity, h.validity + a / 8, (size_t)((rows + 7) / 8), hipMemcpyHostToDevice, c->s_in, "H2D validity");
       dcols[i] = fory_column{B.cols[i].values, nullptr, (c->nullable[i] && h.validity) ? B.cols[i].validity : nullptr,
                              rows, rows * c->width[i]};
     }
@@ -406,7 +501,7 @@ int host_encode_fixed(fory_host_ctx* c, const fory_column* host_cols, int64_t n,
     if (!rc) rc = hip_check(hipEventRecord(c->ev_k[b], c->s_k), "hipEventRecord");
     // D2H: the chunk's rows into the window(s) holding them
     if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_out, c->ev_k[b], 0), "hipStreamWaitEvent");
-    if (!rc) rc = d2h_rows_windows(*W, B.rows, a, rows, stride, c->s_out);
+    if (!rc) rc = d2h_rows_windows(c, *W, B.rows, a, rows, stride, c->s_out);
     if (!rc) rc = hip_check(hipEventRecord(c->ev_out[b], c->s_out), "hipEventRecord");
   }
   const int rc_sync = sync_all(c);
@@ -465,7 +560,7 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
     fory_host_ctx::Buf& B = c->buf[b];
     if (k >= 2) rc = hip_check(hipStreamWaitEvent(c->s_in, c->ev_k[b], 0), "hipStreamWaitEvent");
     if (!rc)
-      rc = hcopy(B.rows, in + a * stride, (size_t)(rows * stride), hipMemcpyHostToDevice, c->s_in, "H2D");
+      rc = hcopy(c, B.rows, in + a * stride, (size_t)(rows * stride), hipMemcpyHostToDevice, c->s_in, "H2D");
     if (!rc) rc = hip_check(hipEventRecord(c->ev_in[b], c->s_in), "hipEventRecord");
     if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_k, c->ev_in[b], 0), "hipStreamWaitEvent");
     if (!rc && k >= 2) rc = hip_check(hipStreamWaitEvent(c->s_k, c->ev_out[b], 0), "hipStreamWaitEvent");
@@ -479,9 +574,9 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
     if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_out, c->ev_k[b], 0), "hipStreamWaitEvent");
     for (int i = 0; i < c->info.num_columns && !rc; ++i) {
       const fory_column& h = host_out_cols[i];
-      rc = hcopy(static_cast<uint8_t*>(h.values) + a * c->width[i], B.cols[i].values, (size_t)(rows * c->width[i]), hipMemcpyDeviceToHost, c->s_out, "D2H");
+      rc = hcopy(c, static_cast<uint8_t*>(h.values) + a * c->width[i], B.cols[i].values, (size_t)(rows * c->width[i]), hipMemcpyDeviceToHost, c->s_out, "D2H");
       if (!rc && dcols[i].validity)
-        rc = hcopy(h.validity + a / 8, B.cols[i].validity, (size_t)((rows + 7) / 8), hipMemcpyDeviceToHost, c->s_out, "D2H validity");
+        rc = hcopy(c, h.validity + a / 8, B.cols[i].validity, (size_t)((rows + 7) / 8), hipMemcpyDeviceToHost, c->s_out, "D2H validity");
     }
     if (!rc) rc = hip_check(hipEventRecord(c->ev_out[b], c->s_out), "hipEventRecord");
   }
@@ -656,21 +751,21 @@ int64_t carve_slices(const fory_host_ctx* c, const std::vector<VarSlice>& sl, in
 }
 
 // H2D of the slices into a slot's carved region (the unbiased region starts).
-int h2d_slices(const fory_host_ctx* c, const fory_column* h, const std::vector<VarSlice>& sl,
+int h2d_slices(fory_host_ctx* c, const fory_column* h, const std::vector<VarSlice>& sl,
                const std::vector<fory_column>& d, hipStream_t s) {
   int rc = FORY_OK;
   for (size_t i = 0; i < sl.size() && !rc; ++i) {
     const VarSlice& v = sl[i];
     if (d[i].values && v.v1 > v.v0) {
       const int64_t bias = c->kind[i] == kKindBytes ? -v.v0 : v.s * c->width[i] - v.v0;
-      rc = hcopy(static_cast<uint8_t*>(d[i].values) - bias, static_cast<const uint8_t*>(h[i].values) + v.v0,
+      rc = hcopy(c, static_cast<uint8_t*>(d[i].values) - bias, static_cast<const uint8_t*>(h[i].values) + v.v0,
                  (size_t)(v.v1 - v.v0), hipMemcpyHostToDevice, s, "H2D values");
     }
     if (!rc && d[i].offsets)
-      rc = hcopy(d[i].offsets - (v.s - v.o0), h[i].offsets + v.o0, (size_t)(v.hi - v.o0 + 1) * 4,
+      rc = hcopy(c, d[i].offsets - (v.s - v.o0), h[i].offsets + v.o0, (size_t)(v.hi - v.o0 + 1) * 4,
                  hipMemcpyHostToDevice, s, "H2D offsets");
     if (!rc && v.validity && v.h1 > v.h0)
-      rc = hcopy(d[i].validity - ((v.s >> 3) - v.h0), h[i].validity + v.h0, (size_t)(v.h1 - v.h0),
+      rc = hcopy(c, d[i].validity - ((v.s >> 3) - v.h0), h[i].validity + v.h0, (size_t)(v.h1 - v.h0),
                  hipMemcpyHostToDevice, s, "H2D validity");
   }
   return rc;
@@ -746,7 +841,7 @@ int host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, i
     carve_slices(c, sl, rows, ws_bytes, S.dev, &dcols[b], &d_offs[b], &ws[b]);
     r = h2d_slices(c, host_cols, sl, dcols[b], c->s_in);
     if (!r) r = fory_rowfmt_encoded_size(c->plan, dcols[b].data(), rows, frame, d_offs[b], ws[b], ws_bytes, c->s_in);
-    if (!r) r = hcopy(S.pin, d_offs[b], (size_t)(rows + 1) * 8, hipMemcpyDeviceToHost, c->s_in, "D2H row offsets");
+    if (!r) r = hcopy(c, S.pin, d_offs[b], (size_t)(rows + 1) * 8, hipMemcpyDeviceToHost, c->s_in, "D2H row offsets");
     if (!r) r = hip_check(hipEventRecord(c->ev_sz[b], c->s_in), "hipEventRecord");
     crow[b] = rows, c0[b] = a;
     return r;
@@ -812,7 +907,7 @@ int host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, i
       if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_out, c->ev_k[b], 0), "hipStreamWaitEvent");
       for (size_t q = 0; q < piece_w.size() && !rc; ++q) {
         const int64_t pw = piece_w[q];
-        rc = hcopy(W->ptr[(size_t)pw] + (at(piece_lo[q]) - wbyte[(size_t)pw]), S.rows + po[piece_lo[q] - a], (size_t)(at(piece_hi[q]) - at(piece_lo[q])), hipMemcpyDeviceToHost,
+        rc = hcopy(c, W->ptr[(size_t)pw] + (at(piece_lo[q]) - wbyte[(size_t)pw]), S.rows + po[piece_lo[q] - a], (size_t)(at(piece_hi[q]) - at(piece_lo[q])), hipMemcpyDeviceToHost,
                    c->s_out, "D2H rows");
       }
       if (!rc) rc = hip_check(hipEventRecord(c->ev_out[b], c->s_out), "hipEventRecord");
@@ -907,29 +1002,29 @@ int decode_var_stage(fory_host_ctx* c, const void* host_rows, const int64_t* hos
   const int64_t rows_sz = align_up((r1 - r0) + 16), offs_sz = align_up((n + 1) * 8);
   const int64_t iws = host_row_offsets ? 0 : fory_rowfmt_index_workspace_bytes(c->plan, n, r1 - r0);
   rc = ensure(c, &c->drows, &c->drows_bytes, rows_sz + offs_sz + kAlign + iws);
+  if (!rc) rc = ensure_hpin(c, 16 + 4 * (int64_t)N);
   if (rc) return rc;
   uint8_t* drow0 = c->drows;
   int64_t* d_offs = reinterpret_cast<int64_t*>(c->drows + rows_sz);
   int32_t* istatus = reinterpret_cast<int32_t*>(c->drows + rows_sz + offs_sz);
   if (r1 > r0)
-    rc = hcopy(drow0, static_cast<const uint8_t*>(host_rows) + r0, (size_t)(r1 - r0), hipMemcpyHostToDevice, c->s_k, "H2D rows");
+    rc = hcopy(c, drow0, static_cast<const uint8_t*>(host_rows) + r0, (size_t)(r1 - r0), hipMemcpyHostToDevice, c->s_k, "H2D rows");
   if (host_row_offsets) {  // row offsets relative to the staged run
     std::vector<int64_t> rel_offs((size_t)n + 1);
     for (int64_t k = 0; k <= n; ++k) rel_offs[(size_t)k] = host_row_offsets[k] - r0;
     if (!rc)
-      rc = hcopy(d_offs, rel_offs.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->s_k, "H2D row offsets");
-    if (!rc) rc = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize");  // rel_offs is pageable
-    if (consumed) *consumed = r1;
+      rc = hcopy(c, d_offs, rel_offs.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->s_k, "H2D row offsets");
+    if (consumed) *consumed = r1;  // (rel_offs is staged: pinned before hcopy returns)
   } else {  // Encoder.decode(MemoryBuffer) x n over the stream alone
     if (!rc) rc = hip_check(hipMemsetAsync(istatus, 0, 4, c->s_k), "hipMemsetAsync");
     if (!rc)
       rc = fory_rowfmt_index_frames(c->plan, drow0, r1 - r0, n, frame, d_offs, istatus,
                                     c->drows + rows_sz + offs_sz + kAlign, iws, c->s_k);
-    int64_t end = 0;
-    if (!rc) rc = hcopy(&end, d_offs + n, 8, hipMemcpyDeviceToHost, c->s_k, "D2H frame end");
+    int64_t* end = reinterpret_cast<int64_t*>(c->hpin);  // pinned: an async D2H, read after the sync
+    if (!rc) rc = hip_check(hipMemcpyAsync(end, d_offs + n, 8, hipMemcpyDeviceToHost, c->s_k), "D2H frame end");
     if (!rc) rc = fory_rowfmt_read_status(istatus, c->s_k);  // synchronises the stream
     if (rc) return rc;
-    if (consumed) *consumed = end;
+    if (consumed) *consumed = *end;
   }
   if (rc) return rc;
   // element counts: top level n; struct fields as their struct; list/map elements
@@ -968,11 +1063,12 @@ int decode_var_stage(fory_host_ctx* c, const void* host_rows, const int64_t* hos
     rc = hip_check(hipMemsetAsync(status, 0, 4, c->s_k), "hipMemsetAsync");
     if (!rc)
       rc = fory_rowfmt_decode_sizes(c->plan, drow0, d_offs, n, frame, d.data(), status, ws, ws_bytes, c->s_k);
-    std::vector<int32_t> tot(N, 0);
+    int32_t* tot = reinterpret_cast<int32_t*>(c->hpin + 16);  // pinned level totals
+    for (int i = 0; i < N; ++i) tot[i] = 0;
     for (int i = 0; i < N && !rc; ++i)
       if (d[i].offsets && kc[i] >= 0)
-        rc = hcopy(&tot[i], d[i].offsets + kc[i], 4, hipMemcpyDeviceToHost, c->s_k, "D2H totals");
-    if (!rc) rc = fory_rowfmt_read_status(status, c->s_k);
+        rc = hip_check(hipMemcpyAsync(&tot[i], d[i].offsets + kc[i], 4, hipMemcpyDeviceToHost, c->s_k), "D2H totals");
+    if (!rc) rc = fory_rowfmt_read_status(status, c->s_k);  // synchronises the stream
     if (rc) break;
     bool changed = false;
     for (int i = 0; i < N; ++i) {
@@ -1078,14 +1174,15 @@ int fory_rowfmt_host_decode_var(fory_host_ctx* c, const fory_column* host_out_co
   for (int i = 0; i < N && !rc; ++i) {  // D2H of every column
     const fory_column& h = host_out_cols[i];
     if (d[i].values && c->dec_bytes[i] > 0)
-      rc = hcopy(h.values, d[i].values, (size_t)c->dec_bytes[i], hipMemcpyDeviceToHost, c->s_k, "D2H values");
+      rc = hcopy(c, h.values, d[i].values, (size_t)c->dec_bytes[i], hipMemcpyDeviceToHost, c->s_k, "D2H values");
     if (!rc && d[i].offsets)
-      rc = hcopy(h.offsets, d[i].offsets, (size_t)(kc[i] + 1) * 4, hipMemcpyDeviceToHost, c->s_k, "D2H offsets");
+      rc = hcopy(c, h.offsets, d[i].offsets, (size_t)(kc[i] + 1) * 4, hipMemcpyDeviceToHost, c->s_k, "D2H offsets");
     if (!rc && d[i].validity)
-      rc = hcopy(h.validity, d[i].validity, (size_t)((kc[i] + 7) / 8), hipMemcpyDeviceToHost, c->s_k, "D2H validity");
+      rc = hcopy(c, h.validity, d[i].validity, (size_t)((kc[i] + 7) / 8), hipMemcpyDeviceToHost, c->s_k, "D2H validity");
   }
   if (!rc) rc = fory_rowfmt_read_status(status, c->s_k);
-  return rc;
+  const int rd = stage_drain(c->stage);  // staged D2H pieces into the caller's columns
+  return rc ? rc : rd;
 }
 
 }  // extern "C"
@@ -1130,10 +1227,11 @@ int host_decode_var_into(fory_host_ctx* c, const uint8_t* host_rows, const int64
   std::vector<int64_t> E(N, 0), VB(N, 0);  // elements / value bytes of the chunks before
   struct Stash { int col; int64_t byte; int64_t slot; };
   std::vector<Stash> stash;
-  uint8_t* pin = nullptr;  // pinned: [N int32 level totals][chunks x N validity stash bytes]
-  rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&pin), (size_t)(4 * N + chunks * N + 16), hipHostMallocDefault),
-                 "hipHostMalloc");
+  // context-owned pinned scratch (grown, not allocated per call):
+  // [N int32 level totals][chunks x N validity stash bytes]
+  rc = ensure_hpin(c, 4 * (int64_t)N + chunks * N + 16);
   if (rc) return rc;
+  uint8_t* pin = c->hpin;
   int32_t* tpin = reinterpret_cast<int32_t*>(pin);
   uint8_t* spin = pin + 4 * N;
   bool overflow = false;
@@ -1167,8 +1265,8 @@ int host_decode_var_into(fory_host_ctx* c, const uint8_t* host_rows, const int64
     if (r) return r;
     for (int64_t i = 0; i <= rows; ++i) S.pin[i] = host_row_offsets[a + i] - lo;
     d_offs[b] = reinterpret_cast<int64_t*>(S.rows + run);
-    if (hi > lo) r = hcopy(S.rows, host_rows + lo, (size_t)(hi - lo), hipMemcpyHostToDevice, c->s_in, "H2D rows");
-    if (!r) r = hcopy(d_offs[b], S.pin, (size_t)(rows + 1) * 8, hipMemcpyHostToDevice, c->s_in, "H2D row offsets");
+    if (hi > lo) r = hcopy(c, S.rows, host_rows + lo, (size_t)(hi - lo), hipMemcpyHostToDevice, c->s_in, "H2D rows");
+    if (!r) r = hcopy(c, d_offs[b], S.pin, (size_t)(rows + 1) * 8, hipMemcpyHostToDevice, c->s_in, "H2D row offsets");
     if (!r) r = hip_check(hipEventRecord(c->ev_in[b], c->s_in), "hipEventRecord");
     crow[b] = rows;
     return r;
@@ -1285,12 +1383,17 @@ int host_decode_var_into(fory_host_ctx* c, const uint8_t* host_rows, const int64
         rc = fory_rowfmt_decode(c->plan, S.rows, d_offs[b], rows, frame, d.data(), status, ws, ws_bytes, c->s_k);
       for (int i = 0; i < N && !rc; ++i) {  // batch positions
         if (d[i].offsets) {
-          const int64_t base = c->kind[i] == kKindBytes ? VB[i] : [&]() {
+          int64_t base = 0, span = 0;  // batch position of the chunk's first element / value byte, chunk total
+          if (c->kind[i] == kKindBytes) {
+            base = VB[i], span = vbytes[i];
+          } else {
             for (int j = 0; j < N; ++j)
-              if (c->parent[j] == i) return E[j];
-            return int64_t(0);
-          }();
-          if (base > INT32_MAX) {
+              if (c->parent[j] == i) {
+                base = E[j], span = cnt[j];
+                break;
+              }
+          }
+          if (base + span > INT32_MAX) {  // the moved offsets end at base + span
             rc = fail_host(FORY_ERR_CAPACITY, "column " + std::to_string(i) + " exceeds int32 offsets");
             break;
           }
@@ -1306,11 +1409,11 @@ int host_decode_var_into(fory_host_ctx* c, const uint8_t* host_rows, const int64
         const fory_column& h = out[i];
         if (d[i].values && vbytes[i] > 0) {
           const int64_t dst = c->kind[i] == kKindBytes ? VB[i] : E[i] * c->width[i];
-          rc = hcopy(static_cast<uint8_t*>(h.values) + dst, d[i].values, (size_t)vbytes[i], hipMemcpyDeviceToHost,
+          rc = hcopy(c, static_cast<uint8_t*>(h.values) + dst, d[i].values, (size_t)vbytes[i], hipMemcpyDeviceToHost,
                      c->s_out, "D2H values");
         }
         if (!rc && d[i].offsets)
-          rc = hcopy(h.offsets + E[i], d[i].offsets, (size_t)(cnt[i] + 1) * 4, hipMemcpyDeviceToHost, c->s_out,
+          rc = hcopy(c, h.offsets + E[i], d[i].offsets, (size_t)(cnt[i] + 1) * 4, hipMemcpyDeviceToHost, c->s_out,
                      "D2H offsets");
         if (!rc && d[i].validity && cnt[i] > 0) {
           const int sh = (int)(E[i] & 7);
@@ -1322,7 +1425,7 @@ int host_decode_var_into(fory_host_ctx* c, const uint8_t* host_rows, const int64
             rc = hip_check(hipMemcpyAsync(spin + slot, src, 1, hipMemcpyDeviceToHost, c->s_out), "D2H validity");
           }
           if (!rc && nbytes > (sh ? 1 : 0))
-            rc = hcopy(h.validity + (E[i] >> 3) + (sh ? 1 : 0), src + (sh ? 1 : 0), (size_t)(nbytes - (sh ? 1 : 0)),
+            rc = hcopy(c, h.validity + (E[i] >> 3) + (sh ? 1 : 0), src + (sh ? 1 : 0), (size_t)(nbytes - (sh ? 1 : 0)),
                        hipMemcpyDeviceToHost, c->s_out, "D2H validity");
         }
       }
@@ -1334,10 +1437,9 @@ int host_decode_var_into(fory_host_ctx* c, const uint8_t* host_rows, const int64
     S.used = true;
     for (int i = 0; i < N; ++i) E[i] += cnt[i], VB[i] += vbytes[i];
   }
-  const int rc_sync = sync_all(c);
+  const int rc_sync = sync_all(c);  // (drains the staged D2H pieces before the OR below)
   if (!rc && !rc_sync && !overflow)
     for (const Stash& st : stash) out[st.col].validity[st.byte] |= spin[st.slot];
-  (void)hipHostFree(pin);
   if (rc) return rc;
   if (rc_sync) return rc_sync;
   for (int b = 0; b < 2 && !rc; ++b) rc = fory_rowfmt_read_status(c->vstatus + b, c->s_k);
@@ -1359,3 +1461,12 @@ extern "C" int fory_rowfmt_host_decode_var_into(fory_host_ctx* c, const void* ho
   return host_decode_var_into(c, static_cast<const uint8_t*>(host_rows), host_row_offsets, n, frame, host_out_cols,
                               host_counts, host_bytes);
 }
+
+// Library-internal, for tests (not in the public header): how hcopy would move
+// [p, p + bytes) — 1 = one async DMA (pinned over the whole range), 0 = staged — and
+// how many pieces a context has staged so far.
+extern "C" int fory_rowfmt_internal_host_copy_path(const void* p, int64_t bytes) {
+  return bytes > 0 && pinned_range(p, (size_t)bytes) ? 1 : 0;
+}
+
+extern "C" int64_t fory_rowfmt_internal_host_staged_pieces(const fory_host_ctx* c) { return c ? c->stage.pieces : -1; }

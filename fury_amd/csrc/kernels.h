@@ -71,6 +71,7 @@ struct VarLaunch {
   int32_t iv_split;             // decode tile kernel: the one var field is a list with item validity (wave 1 assembles it)
   int32_t level2;               // decode lengths pass 2: sizes of string/binary list/map
                                 // elements (container offsets already scanned)
+  LaunchKnobs kn;               // the plan's knobs (host-side launch decisions only)
 };
 
 // sizes -> d_row_offsets[0..n-1] (row/frame byte sizes), then exclusive scan.
@@ -95,7 +96,7 @@ hipError_t launch_var_decode(const VarLaunch& L, const uint8_t* rows,
 int64_t scan_partials(int64_t n);
 
 // Debug timeline buffer for the flat tile kernels (FORY_ROWFMT_VARPROF=1).
-uint64_t* var_prof_buffer(int64_t tiles);
+uint64_t* var_prof_buffer(int64_t tiles, bool on);
 int64_t var_prof_copy(uint64_t* host, int64_t max_words);
 hipError_t launch_scan_i64(int64_t* data, int64_t n, int64_t* partials, hipStream_t s);
 // Arrow offsets: offs[1..n] hold lengths; writes offs[0]=0 and inclusive
@@ -137,12 +138,12 @@ struct FrameIndexLaunch {
   int64_t num_rows;
   int64_t schema_hash;
   int32_t fixed_size;
-  int32_t pad;
+  int32_t idx_frames;  // frames per chunk (0 = 16; LaunchKnobs::idx_frames)
   int64_t chunk;   // bytes per chunk (frame_index_plan)
   int64_t chunks;
 };
-void frame_index_plan(int64_t num_rows, int64_t rows_bytes, int64_t* chunk, int64_t* chunks);
-int64_t frame_index_words(int64_t num_rows, int64_t rows_bytes);  // int64 workspace words
+void frame_index_plan(int64_t num_rows, int64_t rows_bytes, int32_t idx_frames, int64_t* chunk, int64_t* chunks);
+int64_t frame_index_words(int64_t num_rows, int64_t rows_bytes, int32_t idx_frames);  // int64 workspace words
 hipError_t launch_frame_index(const FrameIndexLaunch& L, const uint8_t* rows, int64_t* d_row_offsets, int64_t* ws,
                               int32_t* status, hipStream_t s);
 

@@ -13,6 +13,10 @@
 //     images and staging slots by querying many candidate sizes.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
+#include "kernels.h"
+
 #include <map>
 #include <mutex>
 #include <set>
@@ -85,6 +89,31 @@ int occupancy(const void* kernel, int threads, size_t lds) {
   std::lock_guard<std::mutex> lock(g_mu);
   occ_cache()[key] = blocks;
   return blocks;
+}
+
+// The plan's launch knobs (kernels.h / plan.h: LaunchKnobs), from the environment
+// at plan creation; never read on a launch path.
+LaunchKnobs knobs_from_env() {
+  auto num = [](const char* name, int32_t unset) -> int32_t {
+    const char* e = std::getenv(name);
+    return e ? (int32_t)std::atoi(e) : unset;
+  };
+  auto set = [](const char* name) -> int32_t { return std::getenv(name) ? 1 : 0; };
+  LaunchKnobs k{};
+  const char* t = std::getenv("FORY_ROWFMT_VARTILE");
+  k.no_tiles = t && std::atoi(t) == 0;
+  const char* f = std::getenv("FORY_ROWFMT_VARFLAT");
+  k.no_flat = f && std::atoi(f) == 0;
+  k.var_cap = num("FORY_ROWFMT_VARCAP", 0);
+  k.var_fit = set("FORY_ROWFMT_VARFIT");
+  k.var_stg = num("FORY_ROWFMT_VARSTG", 0);
+  k.spill_cap = num("FORY_ROWFMT_SPILLCAP", 0);
+  k.var_nw = num("FORY_ROWFMT_VARNW", 0);
+  k.sizes_program = set("FORY_ROWFMT_SIZES_PROGRAM");
+  k.idx_frames = num("FORY_ROWFMT_IDXFRAMES", 0);
+  k.prof = num("FORY_ROWFMT_VARPROF", 0) != 0;
+  k.diag = set("FORY_ROWFMT_VARDIAG");
+  return k;
 }
 
 }  // namespace fory_amd

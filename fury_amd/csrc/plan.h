@@ -127,6 +127,34 @@ struct Node {
   std::vector<int32_t> children;  // desc indices
 };
 
+// Test / A-B knobs of the launchers, read from the environment ONCE, when a plan is
+// created (fory_rowfmt_plan_create), and carried by value in the launch structs: no
+// getenv on a launch path (a setenv on another thread cannot race a launch). They
+// force the fallback engines and LDS budgets so the parity suite reaches every path;
+// none selects a rejected variant. 0 = unset.
+//   FORY_ROWFMT_VARTILE=0   per-record global interpreter for every tile
+//   FORY_ROWFMT_VARFLAT=0   generic tile interpreter for cooperative plans too
+//   FORY_ROWFMT_VARCAP / SPILLCAP / VARFIT   LDS image budgets, VARSTG staging slot bytes
+//   FORY_ROWFMT_VARNW=2|4   waves per cooperative tile
+//   FORY_ROWFMT_SIZES_PROGRAM  sizes by the op-program walk for flat plans too
+//   FORY_ROWFMT_IDXFRAMES   frames per frame-index chunk
+//   FORY_ROWFMT_VARPROF=1   phase timeline (debug), FORY_ROWFMT_VARDIAG=1 LDS sizing to stderr
+struct LaunchKnobs {
+  int32_t no_tiles;
+  int32_t no_flat;
+  int32_t var_cap;
+  int32_t var_fit;
+  int32_t var_stg;
+  int32_t spill_cap;
+  int32_t var_nw;
+  int32_t sizes_program;
+  int32_t idx_frames;
+  int32_t prof;
+  int32_t diag;
+  int32_t pad;
+};
+LaunchKnobs knobs_from_env();
+
 struct Plan {
   std::vector<fory_field_desc> desc;
   std::vector<Node> nodes;
@@ -143,6 +171,7 @@ struct Plan {
   bool generic = false;
   std::vector<GNode> gnodes;
   int32_t max_cdepth = 0;
+  LaunchKnobs kn{};  // read from the environment once, at plan creation
 };
 
 // Returns FORY_OK or an error code, with a message in `err`.

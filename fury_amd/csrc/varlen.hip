@@ -2180,8 +2180,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
 hipError_t launch_var_sizes(const VarLaunch& L, int64_t* d_row_offsets, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
   const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
-  const bool program_walk = getenv("FORY_ROWFMT_SIZES_PROGRAM") != nullptr;  // A/B knob (per call)
-  if (L.flat && !program_walk)
+  if (L.flat && !L.kn.sizes_program)  // (A/B knob of the plan)
     hipLaunchKernelGGL(var_sizes_flat_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.vf, L.st, d_row_offsets);
   else
     hipLaunchKernelGGL(var_sizes_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.prog, L.cols, d_row_offsets);
@@ -2190,22 +2189,13 @@ hipError_t launch_var_sizes(const VarLaunch& L, int64_t* d_row_offsets, hipStrea
 
 namespace {
 
-// Test knobs (environment, read per call): they force the fallback engines and
-// LDS budgets so the parity suite exercises every path; none selects a rejected
-// variant.
-//   FORY_ROWFMT_VARTILE=0   per-record global interpreter for every tile
-//   FORY_ROWFMT_VARFLAT=0   generic tile interpreter for cooperative plans too
-//   FORY_ROWFMT_VARCAP / FORY_ROWFMT_SPILLCAP / FORY_ROWFMT_VARFIT   LDS image budgets
-//   FORY_ROWFMT_VARSTG      staging slot bytes
-//   FORY_ROWFMT_VARPROF=1   phase timeline (debug), FORY_ROWFMT_VARDIAG=1 LDS sizing to stderr
-bool var_tiles() {
-  const char* e = getenv("FORY_ROWFMT_VARTILE");
-  return !e || atoi(e) != 0;
-}
+// Test knobs: the plan's LaunchKnobs (plan.h), read from the environment once at
+// plan creation. They force the fallback engines and LDS budgets so the parity
+// suite exercises every path; none selects a rejected variant.
+bool var_tiles(const VarLaunch& L) { return !L.kn.no_tiles; }
 
 int var_cap(const VarLaunch& L) {
-  const char* e = getenv("FORY_ROWFMT_VARCAP");
-  const int cap = e ? atoi(e) : L.tile_cap;
+  const int cap = L.kn.var_cap ? L.kn.var_cap : L.tile_cap;
   return cap < 1024 ? 1024 : (cap > 160 * 1024 ? 160 * 1024 : cap);
 }
 
@@ -2215,14 +2205,14 @@ int var_cap(const VarLaunch& L) {
 // to the data instead of the plan's static estimate is what sets the resident
 // workgroups per CU (Mixed: 37 KiB static -> 32 KiB, 3 -> 4 workgroups per CU).
 int fit_cap(const VarLaunch& L, int64_t mean_row) {
-  if (getenv("FORY_ROWFMT_VARCAP") || getenv("FORY_ROWFMT_VARFIT") || mean_row <= 0 || L.num_rows < 64)
+  if (L.kn.var_cap || L.kn.var_fit || mean_row <= 0 || L.num_rows < 64)
     return var_cap(L);
   int64_t need = (64 * mean_row * 104 / 100 + 16 + 255) & ~int64_t(255);
   need = need < 4096 ? 4096 : (need > 64 * 1024 ? 64 * 1024 : need);
   return (int)need;
 }
 
-// Debug timeline of the cooperative kernels (FORY_ROWFMT_VARPROF=1): one
+// Debug timeline of the cooperative kernels (the plan's FORY_ROWFMT_VARPROF=1): one
 // process-wide buffer, 8 stamps per tile.
 std::mutex g_prof_mu;
 uint64_t* g_prof = nullptr;
@@ -2230,9 +2220,8 @@ int64_t g_prof_words = 0;
 
 }  // namespace
 
-uint64_t* var_prof_buffer(int64_t tiles) {
-  const char* e = getenv("FORY_ROWFMT_VARPROF");
-  if (!e || atoi(e) == 0) return nullptr;
+uint64_t* var_prof_buffer(int64_t tiles, bool on) {
+  if (!on) return nullptr;
   std::lock_guard<std::mutex> lock(g_prof_mu);
   if (tiles * 8 > g_prof_words) {
     if (g_prof) (void)hipFree(g_prof);
@@ -2255,10 +2244,7 @@ int64_t var_prof_copy(uint64_t* host, int64_t max_words) {
 
 namespace {
 
-bool var_flat(const VarLaunch& L) {
-  const char* e = getenv("FORY_ROWFMT_VARFLAT");
-  return L.flat && (!e || atoi(e) != 0);
-}
+bool var_flat(const VarLaunch& L) { return L.flat && !L.kn.no_flat; }
 
 constexpr int kNW = 4;  // waves per 64-record tile of the cooperative kernels (8 was slower at every occupancy)
 
@@ -2269,8 +2255,7 @@ constexpr int kNW = 4;  // waves per 64-record tile of the cooperative kernels (
 // 4 (2 waves: encode 4.60 -> 6.64 ms, decode 4.08 -> 5.90 ms).
 // FORY_ROWFMT_VARNW=2|4 forces one (tests).
 int flat_waves(const VarLaunch& L) {
-  const char* e = getenv("FORY_ROWFMT_VARNW");
-  if (e && (atoi(e) == 2 || atoi(e) == 4)) return atoi(e);
+  if (L.kn.var_nw == 2 || L.kn.var_nw == 4) return L.kn.var_nw;
   return L.num_var <= 2 ? 2 : 4;
 }
 
@@ -2309,7 +2294,7 @@ int fit_slot(K* k, int threads, int b, F lds_of) {
 // resident workgroups. FORY_ROWFMT_VARSTG overrides.
 template <typename K>
 int enc_stg_bytes(K* k, const VarLaunch& L, int64_t capacity, int cap, int nw) {
-  if (getenv("FORY_ROWFMT_VARSTG") || L.num_rows < 64 || L.num_var == 0) return L.stg_bytes;
+  if (L.kn.var_stg || L.num_rows < 64 || L.num_var == 0) return L.stg_bytes;
   const int64_t var_row = capacity / L.num_rows - L.fixed_size - frame_header_bytes(L.frame) - L.nested_fixed;
   const int64_t per = var_row > 0 ? 64 * var_row / L.num_var : 0;
   int b = (int)((per * 3 / 2 + 512 + 255) & ~int64_t(255));
@@ -2323,14 +2308,13 @@ int enc_stg_bytes(K* k, const VarLaunch& L, int64_t capacity, int cap, int nw) {
 
 // LDS image of the spill launches: 3x the main image, in [32, 96] KiB
 // (FORY_ROWFMT_SPILLCAP overrides, for tests).
-int spill_cap(int cap) {
-  const char* e = getenv("FORY_ROWFMT_SPILLCAP");
-  int c = e ? atoi(e) : 3 * cap;
-  if (!e) c = c < 32 * 1024 ? 32 * 1024 : (c > 96 * 1024 ? 96 * 1024 : c);
+int spill_cap(const VarLaunch& L, int cap) {
+  int c = L.kn.spill_cap ? L.kn.spill_cap : 3 * cap;
+  if (!L.kn.spill_cap) c = c < 32 * 1024 ? 32 * 1024 : (c > 96 * 1024 ? 96 * 1024 : c);
   return c < 1024 ? 1024 : (c > 128 * 1024 ? 128 * 1024 : c);
 }
 
-SpillArgs spill_args(const VarLaunch& L, int cap) { return SpillArgs{L.spill, L.spill_count, spill_cap(cap), 0}; }
+SpillArgs spill_args(const VarLaunch& L, int cap) { return SpillArgs{L.spill, L.spill_count, spill_cap(L, cap), 0}; }
 
 // Persistent spill grid: resident workgroups at the spill image size.
 template <typename K>
@@ -2353,7 +2337,7 @@ size_t flat_lds_dec(const VarLaunch& L, int cap, int nw) {
 // take the per-lane path.
 template <typename K>
 int dec_stg_bytes(K* k, const VarLaunch& L, int cap, int nw) {
-  if (getenv("FORY_ROWFMT_VARSTG") || L.num_var == 0) return L.stg_bytes;
+  if (L.kn.var_stg || L.num_var == 0) return L.stg_bytes;
   int b = (int)(((int64_t)64 * L.var_est_row * 5 / 4 + 512 + 255) & ~int64_t(255));
   b = b < 2048 ? 2048 : (b > 16384 ? 16384 : b);
   return fit_slot(k, 64 * nw, b, [&](int stg) {
@@ -2366,8 +2350,8 @@ int dec_stg_bytes(K* k, const VarLaunch& L, int cap, int nw) {
 // Grows a data-fitted tile image (fit_cap) in 256-B steps, up to +20 %, while the
 // resident workgroups per CU stay the same: spill margin that costs no occupancy.
 template <typename K, typename F>
-int grow_cap(K* k, int threads, int cap, F lds_of) {
-  if (getenv("FORY_ROWFMT_VARCAP") || getenv("FORY_ROWFMT_VARFIT")) return cap;
+int grow_cap(const VarLaunch& L, K* k, int threads, int cap, F lds_of) {
+  if (L.kn.var_cap || L.kn.var_fit) return cap;
   const int b0 = occupancy_of(k, threads, lds_of(cap));
   int c = cap;
   const int limit = cap * 6 / 5 < 64 * 1024 ? cap * 6 / 5 : 64 * 1024;
@@ -2378,8 +2362,8 @@ int grow_cap(K* k, int threads, int cap, F lds_of) {
 
 // FORY_ROWFMT_VARDIAG=1: the tile kernels' LDS sizing and resulting residency, to stderr.
 template <typename K>
-void var_diag(const char* what, K* k, int threads, int cap, int stg, size_t lds) {
-  if (!getenv("FORY_ROWFMT_VARDIAG")) return;
+void var_diag(const VarLaunch& L, const char* what, K* k, int threads, int cap, int stg, size_t lds) {
+  if (!L.kn.diag) return;
   fprintf(stderr, "[fory_rowfmt] %s tile kernel: image %d B, staging %d B/slot, LDS %zu B, %d workgroups/CU\n", what,
           cap, stg, lds, occupancy_of(k, threads, lds));
 }
@@ -2397,7 +2381,7 @@ void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, i
     VarLaunch T = L;
     *stg = enc_stg_bytes(kk, T, capacity, cap, NW);
     T.stg_bytes = *stg;
-    *c = grow_cap(kk, 64 * NW, cap, [&](int x) { return flat_lds_enc(T, x, NW); });
+    *c = grow_cap(T, kk, 64 * NW, cap, [&](int x) { return flat_lds_enc(T, x, NW); });
     return occupancy_of(kk, 64 * NW, flat_lds_enc(T, *c, NW));
   };
   int stg_d = 0, cap_d = cap, stg_l = 0, cap_l = cap;
@@ -2410,7 +2394,7 @@ void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, i
   raise_lds_cap(k);
   const SpillArgs sp = spill_args(L, cap);
   (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
-  var_diag(lean ? "encode (lean)" : "encode", k, 64 * NW, cap, L.stg_bytes, flat_lds_enc(L, cap, NW));
+  var_diag(L, lean ? "encode (lean)" : "encode", k, 64 * NW, cap, L.stg_bytes, flat_lds_enc(L, cap, NW));
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), flat_lds_enc(L, cap, NW), s, L, L.prog,
                      L.cols, L.fix, L.vf, L.st, offs, out, capacity, status, cap, sp);
   auto* k2 = lean ? &var_encode_flat_lean_kernel<HDR, NW, NEST, true> : &var_encode_flat_kernel<HDR, NW, NEST, true>;
@@ -2436,11 +2420,11 @@ void launch_flat_dec(const VarLaunch& L0, const uint8_t* rows, const int64_t* of
   raise_lds_cap(k);
   VarLaunch L = L0;
   if (WRITE) L.stg_bytes = dec_stg_bytes(k, L0, cap, NW);
-  if (WRITE && L.mean_row > 0) cap = grow_cap(k, 64 * NW, cap, [&](int c) { return flat_lds_dec(L, c, NW); });
+  if (WRITE && L.mean_row > 0) cap = grow_cap(L, k, 64 * NW, cap, [&](int c) { return flat_lds_dec(L, c, NW); });
   const SpillArgs sp = spill_args(L, cap);
   (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
   const size_t lds = WRITE ? flat_lds_dec(L, cap, NW) : (size_t)cap + sbase_lds(L);  // pass 1: row image (+ struct offsets)
-  var_diag(WRITE ? "decode" : "decode lengths", k, 64 * NW, cap, L.stg_bytes, lds);
+  var_diag(L, WRITE ? "decode" : "decode lengths", k, 64 * NW, cap, L.stg_bytes, lds);
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
                      L.vf, L.st, rows, offs, tile_tot, status, cap, sp);
   auto* k2 = &var_decode_flat_kernel<HDR, WRITE, NW, true>;
@@ -2461,7 +2445,7 @@ template <bool WRITE>
 hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const int64_t* offs, int64_t* tile_tot,
                                   int32_t* status, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
-  if (var_tiles() && var_flat(L)) {
+  if (var_tiles(L) && var_flat(L)) {
     const int cap = fit_cap(L, L.mean_row);
     if (flat_waves(L) == 2) {
       switch (frame_header_bytes(L.frame)) {
@@ -2478,7 +2462,7 @@ hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const
     }
     return hipGetLastError();
   }
-  if (var_tiles()) {
+  if (var_tiles(L)) {
     const int cap = var_cap(L);
     const SpillArgs sp = spill_args(L, cap);
     (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
@@ -2502,7 +2486,7 @@ hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const
 hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity,
                              int32_t* status, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
-  if (var_tiles() && var_flat(L)) {
+  if (var_tiles(L) && var_flat(L)) {
     const int cap = enc_cap(L, capacity);
     if (flat_waves(L) == 2) {
       switch (frame_header_bytes(L.frame)) {
@@ -2519,7 +2503,7 @@ hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* o
     }
     return hipGetLastError();
   }
-  if (var_tiles()) {
+  if (var_tiles(L)) {
     const int cap = enc_cap(L, capacity);
     const SpillArgs sp = spill_args(L, cap);
     (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
@@ -2538,7 +2522,7 @@ hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* o
   return hipGetLastError();
 }
 
-bool var_decode_tiled_offsets(const VarLaunch& L) { return L.num_rows > 0 && var_tiles() && var_flat(L); }
+bool var_decode_tiled_offsets(const VarLaunch& L) { return L.num_rows > 0 && var_tiles(L) && var_flat(L); }
 
 int64_t var_tile_totals_words(int64_t num_var, int64_t n) { return num_var * ((n + 63) / 64 + 1); }
 

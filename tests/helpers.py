@@ -499,3 +499,10 @@ def random_rows(schema: Schema, n: int, seed: int, null_p: float = 0.12):
 def nested_columns(name: str, n: int, seed: int):
     schema = nested_schemas()[name]
     return schema, build_columns(schema, random_rows(schema, n, seed))
+
+
+def knob_key():
+    """The FORY_ROWFMT_* launch knobs in the environment: a plan reads them once, when it
+    is created, so encoder caches in the tests are keyed by them too."""
+    import os
+    return tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("FORY_ROWFMT_") and k != "FORY_ROWFMT_LIB"))

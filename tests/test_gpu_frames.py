@@ -23,7 +23,7 @@ from fury_amd.format.encoder import RowEncoder  # noqa: E402
 from fury_amd.format.native import HostPipeline, NativePlan  # noqa: E402
 from fury_amd.format.types import ArrowType, DataType, Field, Schema  # noqa: E402
 
-from helpers import catalog, columns_equal  # noqa: E402
+from helpers import catalog, columns_equal, knob_key  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -34,9 +34,10 @@ _ENC = {}
 
 
 def encoder_for(name, schema=None):
-    if name not in _ENC:
-        _ENC[name] = RowEncoder(schema if schema is not None else catalog()[name][0])
-    return _ENC[name]
+    key = (name, knob_key())  # a plan reads the launch knobs when it is created
+    if key not in _ENC:
+        _ENC[key] = RowEncoder(schema if schema is not None else catalog()[name][0])
+    return _ENC[key]
 
 
 def device_bytes(a, pad=0):

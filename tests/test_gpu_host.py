@@ -58,8 +58,9 @@ def test_host_pipeline_registered_buffers_and_errors():
     cols = make(n, 3)
     plan = NativePlan(schema)
     hp = HostPipeline(plan, chunk_rows=512)
-    out = np.zeros(n * plan.stride(1), np.uint8)
-    host_register(out)
+    out_pages, _ = page_buffer(n * plan.stride(1))  # a registration on pages of its own
+    out = out_pages[:n * plan.stride(1)]
+    host_register(out_pages)
     try:
         hp.encode(cols, n, 1, out)
         expect, _ = oracle.encode(schema, cols, n, 1)
@@ -71,7 +72,162 @@ def test_host_pipeline_registered_buffers_and_errors():
         with pytest.raises(ClassNotCompatibleException):
             hp.decode(bad, n, 1, empty_like(schema, n))
     finally:
-        host_unregister(out)
+        host_unregister(out_pages)
+        hp.close()
+
+
+def unregister_all(arrays):
+    """Unregisters every array, each on its own: one failure must not leave the rest
+    registered when numpy frees and re-issues their pages (round-2 cleanup stopped at
+    the first failure)."""
+    errors = []
+    for a in arrays:
+        try:
+            host_unregister(a)
+        except Exception as e:  # noqa: BLE001 - reported after the loop
+            errors.append(e)
+    if errors:
+        raise errors[0]
+
+
+def page_buffer(nbytes, pages_before=0):
+    """A uint8 view on whole pages of its own (a registration never shares a page with
+    other data), plus the owning array."""
+    npages = (nbytes + 4095) // 4096
+    raw = np.zeros((npages + pages_before + 2) * 4096, np.uint8)
+    k = (-raw.ctypes.data) % 4096 + pages_before * 4096
+    return raw[k:k + npages * 4096], raw
+
+
+def _internal(name, restype, argtypes):
+    import ctypes
+    from fury_amd import _lib
+    f = getattr(_lib.load(), name)
+    f.restype, f.argtypes = restype, argtypes
+    return f
+
+
+def copy_path(a, nbytes=None):
+    import ctypes
+    f = _internal("fory_rowfmt_internal_host_copy_path", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64])
+    return f(a.ctypes.data, a.nbytes if nbytes is None else nbytes)
+
+
+def staged_pieces(hp):
+    import ctypes
+    f = _internal("fory_rowfmt_internal_host_staged_pieces", ctypes.c_int64, [ctypes.c_void_p])
+    return f(hp.handle)
+
+
+def test_host_copy_classification_is_by_whole_range():
+    """The round-2 host-path fault mechanism, deterministically: a copy was judged
+    pinned by its FIRST byte, so a range that begins inside a registration and runs
+    past it (or a range whose pages were registered before and have been unregistered
+    and re-used) could be handed to an async DMA as pinned. Now a copy is a direct DMA
+    only when the whole range is one pinned mapping; everything else is staged."""
+    buf, raw = page_buffer(64 << 10)
+    assert copy_path(buf) == 0  # pageable
+    head = buf[:32 << 10]  # register the first half only
+    host_register(head)
+    try:
+        assert copy_path(head) == 1
+        assert copy_path(head[4096:]) == 1  # inside the registration
+        assert copy_path(buf) == 0  # starts inside, runs past the end: staged, never a direct DMA
+        assert copy_path(buf[(32 << 10) - 8:]) == 0  # the last 8 registered bytes + pageable ones
+        assert copy_path(buf[32 << 10:]) == 0  # wholly past it
+    finally:
+        host_unregister(head)
+    assert copy_path(head) == 0  # unregistered pages are pageable again
+    # registered -> unregistered -> freed -> the same pages re-used by a fresh batch
+    host_register(buf)
+    host_unregister(buf)
+    addr = buf.ctypes.data
+    del buf, head, raw
+    again, raw2 = page_buffer(64 << 10)
+    assert copy_path(again) == 0, (hex(addr), hex(again.ctypes.data))
+
+
+@pytest.mark.parametrize("name", ["struct104", "mixed40_nulls", "maps"])
+def test_host_copies_straddling_a_registration(name):
+    """Columns and output whose first pages are registered and whose rest is not (and
+    pages registered, unregistered and re-used): every copy straddling a registration
+    is staged (the context counts its staged pieces), the bytes equal the oracle's,
+    and fully registered buffers are never staged."""
+    n = 4000
+    schema, make = catalog()[name]
+    cols = make(n, 91)
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    hp = HostPipeline(NativePlan(schema), chunk_rows=1024)
+    regs, keep = [], []
+    for c in cols:  # every host array on pages of its own, its first half registered
+        for attr in ("values", "offsets", "validity"):
+            a = getattr(c, attr)
+            if a is None or a.nbytes < 8192:
+                continue
+            pb, raw = page_buffer(a.nbytes)
+            pb[:a.nbytes] = a.view(np.uint8).reshape(-1)
+            keep.append(raw)
+            setattr(c, attr, pb[:a.nbytes].view(a.dtype))
+            head = pb[:(a.nbytes // 2) // 4096 * 4096]
+            if head.nbytes:
+                host_register(head)
+                regs.append(head)
+    out, raw_out = page_buffer(expect.nbytes + 64)
+    out_head = out[:(expect.nbytes // 2) // 4096 * 4096]
+    host_register(out_head)
+    regs.append(out_head)
+    try:
+        before = staged_pieces(hp)
+        if NativePlan(schema).fixed_width:
+            hp.encode(cols, n, 1, out[:expect.nbytes])
+            got = out[:expect.nbytes]
+        else:
+            got, offs = hp.encode_var(cols, n, 1, out)
+            assert np.array_equal(offs, eoffs)
+        assert staged_pieces(hp) > before  # the straddling copies went through the staging
+        bad = np.nonzero(got != expect)[0]
+        assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+    finally:
+        unregister_all(regs)
+    # the same pages, now pageable again: decode through them
+    rows_pb, raw_rows = page_buffer(expect.nbytes)
+    rows_pb[:expect.nbytes] = expect
+    host_register(rows_pb)
+    host_unregister(rows_pb)
+    rows = rows_pb[:expect.nbytes]
+    if NativePlan(schema).fixed_width:
+        dec = empty_like(schema, n)
+        hp.decode(rows, n, 1, dec)
+    else:
+        dec = hp.decode_var_into(rows, eoffs, n, 1)
+        assert same_arrays(dec, hp.decode_var(rows, eoffs, n, 1)) == []
+    assert columns_equal(schema, cols, dec) == []
+    hp.close()
+
+
+def test_host_registered_buffers_are_never_staged():
+    """Whole-range registered columns and output: every copy is a direct async DMA."""
+    schema, make = catalog()["struct104"]
+    n = 3000
+    cols = make(n, 5)
+    expect, _ = oracle.encode(schema, cols, n, 1)
+    regs = []
+    for c in cols:
+        pb, raw = page_buffer(c.values.nbytes)
+        pb[:c.values.nbytes] = c.values.view(np.uint8)
+        c.values = pb[:c.values.nbytes].view(c.values.dtype)
+        regs.append(pb)
+    out, raw_out = page_buffer(expect.nbytes)
+    regs.append(out)
+    for a in regs:
+        host_register(a)
+    hp = HostPipeline(NativePlan(schema), chunk_rows=1024)
+    try:
+        hp.encode(cols, n, 1, out[:expect.nbytes])
+        assert np.array_equal(out[:expect.nbytes], expect)
+        assert staged_pieces(hp) == 0
+    finally:
+        unregister_all(regs)
         hp.close()
 
 
@@ -257,8 +413,7 @@ def test_host_varlen_pipeline_registered(name):
                         a.view(np.uint8)[:] = 0x5A
             assert columns_equal(schema, cols, hp.decode_var_into(out[:expect.nbytes], eoffs, n, 1, outs)) == []
     finally:
-        for a in arrays:
-            host_unregister(a)
+        unregister_all(arrays)
         hp.close()
 
 

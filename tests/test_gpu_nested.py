@@ -19,7 +19,7 @@ from fury_amd.format.encoder import CollectionEncoder, EncodedRows, RowEncoder  
 from fury_amd.format.types import DataTypes, Schema  # noqa: E402
 from fury_amd.format import infer as I  # noqa: E402
 
-from helpers import columns_equal, nested_columns, nested_schemas, random_rows, reference_beans  # noqa: E402
+from helpers import columns_equal, nested_columns, nested_schemas, random_rows, reference_beans, knob_key  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -27,9 +27,10 @@ _ENC = {}
 
 
 def encoder_for(name):
-    if name not in _ENC:
-        _ENC[name] = RowEncoder(nested_schemas()[name])
-    return _ENC[name]
+    key = (name, knob_key())  # a plan reads the launch knobs when it is created
+    if key not in _ENC:
+        _ENC[key] = RowEncoder(nested_schemas()[name])
+    return _ENC[key]
 
 
 def check(schema, enc, cols, n, frame):

@@ -22,7 +22,7 @@ from fury_amd.format.encoder import CollectionEncoder, EncodedRows, Encoders, Ro
 from fury_amd.format import native  # noqa: E402
 from fury_amd.format.types import ArrowType  # noqa: E402
 
-from helpers import catalog, collection_cases, columns_equal  # noqa: E402
+from helpers import catalog, collection_cases, columns_equal, knob_key  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -31,9 +31,10 @@ _ENC = {}
 
 
 def encoder_for(name):
-    if name not in _ENC:
-        _ENC[name] = RowEncoder(catalog()[name][0])
-    return _ENC[name]
+    key = (name, knob_key())  # a plan reads the launch knobs when it is created
+    if key not in _ENC:
+        _ENC[key] = RowEncoder(catalog()[name][0])
+    return _ENC[key]
 
 
 VARLEN = [k for k, (sch, _) in catalog().items()
