@@ -122,6 +122,45 @@ def setup_dist(args):
     return dist, world, rank, dev
 
 
+def device_identity(dev: int) -> dict:
+    """This rank's device: ordinal and PCI bus id (hipDeviceGetPCIBusId), so that a
+    multi-GPU line proves its ranks ran on distinct GPUs."""
+    import ctypes
+    import torch
+    ident = {"ordinal": dev, "pci_bus_id": None}
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, dev) == 0:
+            ident["pci_bus_id"] = buf.value.decode()
+    except OSError:
+        pass
+    props = torch.cuda.get_device_properties(dev)
+    ident["name"] = props.name
+    uuid = getattr(props, "uuid", None)
+    if uuid is not None:
+        ident["uuid"] = str(uuid)
+    return ident
+
+
+def check_devices(devices, oversubscribe: bool):
+    """A multi-rank line must come from distinct GPUs: two ranks on one device (same
+    PCI bus id, or the same ordinal when no id is known) is an error unless the run is
+    an explicit --oversubscribe rehearsal. Returns an error string or None."""
+    keys = [d.get("pci_bus_id") or f"ordinal:{d.get('ordinal')}" for d in devices]
+    if len(set(keys)) < len(keys) and not oversubscribe:
+        return f"{len(keys)} ranks ran on {len(set(keys))} distinct device(s): {keys}"
+    return None
+
+
+def gather_devices(dist, ident, world):
+    if dist is None:
+        return [ident]
+    out = [None] * world
+    dist.all_gather_object(out, ident)
+    return out
+
+
 def barrier(dist):
     import torch
     torch.cuda.synchronize()
@@ -277,6 +316,10 @@ def main():
     import torch
     dist, world, rank, dev = setup_dist(args)
     device = torch.device("cuda", dev)
+    devices = gather_devices(dist, device_identity(dev), world)
+    bad_devices = check_devices(devices, args.oversubscribe)
+    if bad_devices:
+        raise SystemExit(f"bench.py: {bad_devices}; refusing to report a multi-GPU line")
     from fury_amd.format.encoder import RowEncoder
     from fury_amd.format import native
     from fury_amd.shard import shard_range
@@ -403,8 +446,10 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(args.pmc, config, wmax, frame, dom),
-                         "traffic_source": "profiles/pmc_latest.json (rocprofv3 --pmc pass of this command)",
+                         "traffic_source": "profiles/pmc_latest.json (rocprofv3 --pmc pass of this command, "
+                                           "same lib_sha16; null when the build differs)",
                          "algorithmic_bytes_per_launch": algo},
+            "lib_sha16": lib_sha16(),
             "step_hbm_frac": round(2 * algo / ((enc_avg + dec_avg) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             if enc_avg + dec_avg > 0 else None,
         }
@@ -510,10 +555,15 @@ def main():
                          "call_frac": {"encode": round(algo / (enc_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                        "decode": round(algo / (dec_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
                          "traffic": pmc_traffic(args.pmc, config, n, frame, dom),
-                         "traffic_source": "profiles/pmc_latest.json (rocprofv3 --pmc pass of this command)",
+                         "traffic_source": "profiles/pmc_latest.json (rocprofv3 --pmc pass of this command, "
+                                           "same lib_sha16; null when the build differs)",
                          "algorithmic_bytes_per_launch": algo},
+            "lib_sha16": lib_sha16(),
             "step_hbm_frac": round(2 * algo / ((enc_avg + dec_avg) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         }
+    res["devices"] = devices
+    if args.oversubscribe:
+        res["oversubscribed"] = True
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # all host cores of this GPU's share (the box allots 16 per GPU), then one core
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
@@ -529,13 +579,27 @@ def main():
         dist.destroy_process_group()
 
 
+def lib_sha16() -> str:
+    """Identity of the product library build that runs (sha256 of libfory_rowfmt.so)."""
+    import hashlib
+    from fury_amd import _lib
+    try:
+        with open(_lib.LIB_PATH, "rb") as fh:
+            return hashlib.sha256(fh.read()).hexdigest()[:16]
+    except OSError:
+        return ""
+
+
 def pmc_traffic(path, config, n, frame, dom):
+    """Per-launch HBM bytes of the dominant kernel from a stored rocprofv3 PMC pass —
+    only when that pass measured THIS library build (entry's lib_sha16); else null."""
     try:
         with open(path) as fh:
             pmc = json.load(fh)
         key = f"{config}:{n}:{frame}"
-        if key in pmc:
-            return pmc[key].get(dom)
+        ent = pmc.get(key)
+        if ent and ent.get("lib_sha16") and ent.get("lib_sha16") == lib_sha16():
+            return ent.get(dom)
     except (OSError, ValueError):
         pass
     return None

@@ -1,8 +1,12 @@
 """profiles/pmc_latest.json from a scripts/profile.sh summary: per-launch HBM bytes of the
 bench's encode and decode kernels = FETCH_SIZE*1024*2 (gfx950 half-count correction,
 MI355X_MICROARCH.md §HBM; calibrated here: it equals the algorithmic read bytes exactly)
-+ WRITE_SIZE*1024. Usage: python scripts/pmc_to_traffic.py SUMMARY KEY [OUT]"""
++ WRITE_SIZE*1024. Usage: python scripts/pmc_to_traffic.py SUMMARY KEY [OUT]
+Each entry is stamped with lib_sha16 (the profiled libfory_rowfmt.so): bench.py reports
+the traffic only when the running build has the same hash."""
+import hashlib
 import json
+import os
 import sys
 
 summ = json.load(open(sys.argv[1]))
@@ -24,6 +28,8 @@ for name, e in summ["pmc"].items():
         ent[role + "_kernel"] = name
         ent[role + "_fetch_bytes_x2"] = int(e["fetch_bytes_x2"])
         ent[role + "_write_bytes"] = int(e["write_bytes"])
+lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "fury_amd", "lib", "libfory_rowfmt.so")
+ent["lib_sha16"] = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
 cur[key] = ent
 json.dump(cur, open(out, "w"), indent=1, sort_keys=True)
 print(json.dumps(ent))

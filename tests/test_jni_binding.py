@@ -1,0 +1,95 @@
+"""CPU: the Java/JNI binding (jni/) is kept honest against include/fory_rowfmt.h.
+
+No JDK exists on either image, so the Java side is checked structurally and the C shim
+is compiled against the C-ABI header with a minimal declaration of the JNI types it uses
+(tests/jni_stub/jni.h, the JNI specification's signatures; it checks this repo's shim,
+not any reference code):
+- gcc -fsyntax-only -Werror of jni/fory_rowfmt_jni.c: every fory_rowfmt_* call matches a
+  header prototype (implicit declarations are errors);
+- the shim links against libfory_rowfmt.so with no undefined symbol;
+- every `native` method of BatchRowEncoder.java has its JNIEXPORT entry (and vice versa)
+  with the JNI arity (env, class + the Java parameters);
+- the upcalls the shim makes (ColumnBatch.addresses / allocate) exist with the JNI
+  descriptors it uses, and the per-column field count and ArrowType ids agree."""
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JNI = os.path.join(REPO, "jni")
+JAVA = os.path.join(JNI, "java", "org", "apache", "fory", "format", "encoder")
+SHIM = os.path.join(JNI, "fory_rowfmt_jni.c")
+
+
+def read(p):
+    with open(p) as fh:
+        return fh.read()
+
+
+def test_shim_compiles_against_the_header():
+    r = subprocess.run(["gcc", "-fsyntax-only", "-std=c11", "-Wall", "-Wextra", "-Werror",
+                        "-Werror=implicit-function-declaration", "-I", os.path.join(REPO, "tests", "jni_stub"),
+                        "-I", os.path.join(REPO, "include"), SHIM], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_shim_links_against_the_library(tmp_path):
+    lib = os.path.join(REPO, "fury_amd", "lib", "libfory_rowfmt.so")
+    if not os.path.exists(lib):
+        pytest.skip("libfory_rowfmt.so not built")
+    out = tmp_path / "libfory_rowfmt_jni.so"
+    r = subprocess.run(["gcc", "-O1", "-fPIC", "-shared", "-std=c11", "-I", os.path.join(REPO, "tests", "jni_stub"),
+                        "-I", os.path.join(REPO, "include"), SHIM, "-L", os.path.dirname(lib), "-lfory_rowfmt",
+                        "-Wl,--no-undefined", "-Wl,--allow-shlib-undefined", "-o", str(out)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    syms = subprocess.run(["nm", "-D", "--defined-only", str(out)], capture_output=True, text=True).stdout
+    assert "Java_org_apache_fory_format_encoder_BatchRowEncoder_nPlanCreate" in syms
+
+
+def java_natives():
+    src = read(os.path.join(JAVA, "BatchRowEncoder.java"))
+    out = {}
+    for m in re.finditer(r"private static native \w+ (\w+)\(([^)]*)\);", src, re.S):
+        params = [p for p in m.group(2).split(",") if p.strip()]
+        out[m.group(1)] = len(params)
+    return out
+
+
+def c_exports():
+    src = read(SHIM)
+    out = {}
+    for m in re.finditer(r"JNIEXPORT \w+ JNICALL CLS\((\w+)\)\(([^)]*)\)", src, re.S):
+        out[m.group(1)] = len([p for p in m.group(2).split(",") if p.strip()])
+    return out
+
+
+def test_every_native_method_has_its_jni_entry():
+    j, c = java_natives(), c_exports()
+    assert j, "no native methods found"
+    assert set(j) == set(c), f"java only: {set(j) - set(c)}, C only: {set(c) - set(j)}"
+    for name, n in j.items():
+        assert c[name] == n + 2, f"{name}: Java {n} parameters, C {c[name]} (JNIEnv*, jclass + parameters)"
+
+
+def test_upcalls_and_layout_agree():
+    shim = read(SHIM)
+    batch = read(os.path.join(JAVA, "ColumnBatch.java"))
+    assert '"addresses", "()[J"' in shim and re.search(r"public long\[\] addresses\(\)", batch)
+    assert '"allocate", "([J[J)V"' in shim and re.search(r"public void allocate\(long\[\] \w+, long\[\] \w+\)", batch)
+    fields_c = int(re.search(r"#define COLUMN_FIELDS (\d+)", shim).group(1))
+    fields_j = int(re.search(r"FIELDS_PER_COLUMN = (\d+);", batch).group(1))
+    assert fields_c == fields_j == 5  # fory_column: values, offsets, validity, length, capacity
+    from fury_amd.format.types import ArrowType
+    for name, ours in (("UTF8", ArrowType.STRING), ("BINARY", ArrowType.BINARY), ("LIST", ArrowType.LIST),
+                       ("MAP", ArrowType.MAP)):
+        assert int(re.search(rf"static final int {name} = (\d+);", batch).group(1)) == int(ours)
+
+
+def test_integration_points_at_the_sources():
+    doc = read(os.path.join(REPO, "INTEGRATION.md"))
+    for f in ("jni/fory_rowfmt_jni.c", "BatchRowEncoder.java", "ColumnBatch.java", "DeviceSchemas.java",
+              "tests/test_jni_binding.py"):
+        assert f in doc, f
