@@ -603,6 +603,7 @@ int fory_rowfmt_internal_node_layout(const fory_plan* plan, int32_t* kind, int32
   for (size_t i = 0; i < p.nodes.size(); ++i) {
     kind[i] = p.nodes[i].kind;
     width[i] = p.nodes[i].width;
+    if (kind[i] == fory_amd::KIND_DECIMAL) kind[i] = fory_amd::KIND_FIXED, width[i] = 16;  // a 16-byte column
     nullable[i] = p.nodes[i].nullable;
     parent[i] = -1;
   }
@@ -967,6 +968,10 @@ int fory_rowfmt_read_status(const int32_t* d_status, void* stream) {
                      "Please check writer schema.");
     case FORY_ERR_CORRUPT: return fail(h, "Malformed row or frame (size field out of range)");
     case FORY_ERR_CAPACITY: return fail(h, "Output buffer too small (IndexOutOfBounds)");
+    case FORY_ERR_UNSUPPORTED:
+      return fail(h, "BigDecimal precision cannot be greater than that in the Arrow vector "
+                     "(DecimalUtility.checkPrecisionAndScale)");
+    case FORY_ERR_ENCODER: return fail(h, "Encode failed (schema nesting deeper than the device stack)");
     default: return fail(h, "device status " + std::to_string(h));
   }
 }

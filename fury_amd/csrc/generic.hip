@@ -12,6 +12,8 @@
 //            [i64 n][bitmap][n x elemSize padded to 8][element var data]   BinaryArrayWriter.java:93-118
 //   map    : [i64 keyArrayBytes][key array][value array]                 :370-427, BinaryMap.java:62-77
 //   string : bytes at the writerIndex, zero-padded to 8, slot = (rel, n) BinaryWriter.java:162-194
+//   decimal: 32 bytes at the writerIndex (decimal128 sign-extended), slot = (rel, 32)
+//            BinaryWriter.writeDecimal :214-230, DecimalUtils.DECIMAL_BYTE_LENGTH = 32
 // Offsets in slots are relative to the enclosing row's / array's start. Rows are
 // written straight to global memory (the output is not zeroed by the caller, so
 // every fixed part is zeroed first: the bytes Java writes into a fresh buffer).
@@ -103,6 +105,18 @@ __device__ __forceinline__ void g_get_bytes(uint8_t* dst, const uint8_t* src, in
 }
 
 __device__ __forceinline__ bool is_scalar(int kind) { return kind == KIND_FIXED || kind == KIND_BOOL; }
+
+// DecimalUtility.checkPrecisionAndScale: the unscaled value (decimal128 dwords w, little-
+// endian two's complement) has at most `prec` digits, |v| <= 10^prec - 1.
+__device__ __forceinline__ bool g_dec_fits(const uint32_t w[4], int prec) {
+  const unsigned __int128 u = (unsigned __int128)w[0] | ((unsigned __int128)w[1] << 32) |
+                              ((unsigned __int128)w[2] << 64) | ((unsigned __int128)w[3] << 96);
+  const bool neg = (w[3] >> 31) != 0;
+  const unsigned __int128 mag = neg ? ~u + 1 : u;
+  unsigned __int128 lim = 1;
+  for (int k = 0; k < prec; ++k) lim *= 10;
+  return mag <= lim - 1;
+}
 __device__ __forceinline__ int elem_size(const GNode& it) { return is_scalar(it.kind) ? it.width : 8; }
 
 // Frame of an open container. STRUCT: children [ch, end) at position pos, the
@@ -151,6 +165,8 @@ __device__ int64_t g_sizes(const GenLaunch& L, int64_t i, bool* overflow) {
     if ((nd.flags & 1) && !gvalid(c.validity, pos)) return;
     if (nd.kind == KIND_BYTES) {
       total += gr8((int64_t)c.offsets[pos + 1] - c.offsets[pos]);
+    } else if (nd.kind == KIND_DECIMAL) {
+      total += 32;
     } else if (nd.kind == KIND_STRUCT) {
       total += gbm(nd.nchild) + 8LL * nd.nchild;
       if (sp == D) { *overflow = true; return; }
@@ -244,11 +260,12 @@ __global__ __launch_bounds__(kWG) void gen_sizes_kernel(GenLaunch L0, int64_t* s
 // encode
 // ---------------------------------------------------------------------------
 template <int D>
-__device__ bool g_encode(const GenLaunch& L, uint8_t* row, int64_t i) {
+__device__ int32_t g_encode(const GenLaunch& L, uint8_t* row, int64_t i) {
   GFrame st[D];
   int sp = 0;
   int32_t wi = 0;
   bool ok = true;
+  bool prec_ok = true;  // every decimal within its precision
   // BinaryArrayWriter.reset(n) at wi (+ the zeroed bitmap / elements of a fresh buffer)
   auto open_array = [&](int type, int node, int item, int64_t e0, int64_t n, int32_t slot, int32_t rel, int32_t off) {
     if (sp == D) { ok = false; return; }
@@ -297,6 +314,20 @@ __device__ bool g_encode(const GenLaunch& L, uint8_t* row, int64_t i) {
         g_put_bytes(row + wi, c.values + s0, n);
         gput(row + slot, ((uint64_t)rel << 32) | (uint32_t)n, 8);
         wi += (int32_t)gr8(n);
+        return;
+      }
+      case KIND_DECIMAL: {  // BinaryWriter.writeDecimal: checkPrecisionAndScale, 32 LE bytes, (rel, 32)
+        const uint8_t* v = c.values + 16 * pos;
+        const uint32_t w[4] = {ld32(v), ld32(v + 4), ld32(v + 8), ld32(v + 12)};
+        if (!g_dec_fits(w, nd.prec)) {
+          prec_ok = false;
+          return;
+        }
+        const uint32_t ext = (w[3] >> 31) ? 0xffffffffu : 0u;  // sign extension to DECIMAL_BYTE_LENGTH
+        for (int q = 0; q < 4; ++q) st32(row + wi + 4 * q, w[q]);
+        for (int q = 4; q < 8; ++q) st32(row + wi + 4 * q, ext);
+        gput(row + slot, ((uint64_t)rel << 32) | 32u, 8);
+        wi += 32;
         return;
       }
       case KIND_STRUCT: {  // BinaryRowWriter.reset (+ slots of a fresh buffer)
@@ -386,7 +417,7 @@ __device__ bool g_encode(const GenLaunch& L, uint8_t* row, int64_t i) {
     if (f.slot >= 0) gput(row + f.slot, ((uint64_t)(uint32_t)f.rel << 32) | (uint32_t)(wi - f.off), 8);
     --sp;
   }
-  return ok;
+  return !ok ? FORY_ERR_ENCODER : (prec_ok ? 0 : FORY_ERR_UNSUPPORTED);
 }
 
 template <int D, bool TAB>
@@ -412,7 +443,8 @@ __global__ __launch_bounds__(kWG) void gen_encode_kernel(GenLaunch L0, const int
   if (hdr == 12 || hdr == 4) st32(frame, (uint32_t)(size - 4));  // Encoders.encode(MemoryBuffer, T) size field
   if (hdr == 12) gput(frame + 4, (uint64_t)L.schema_hash, 8);    // [i32 8+rowSize][i64 hash]
   if (hdr == 8) gput(frame, (uint64_t)L.schema_hash, 8);         // Encoder.encode(T): [i64 hash]
-  if (!g_encode<D>(L, frame + hdr, i)) set_status(status, FORY_ERR_ENCODER);
+  const int32_t err = g_encode<D>(L, frame + hdr, i);
+  if (err) set_status(status, err);
 }
 
 // ---------------------------------------------------------------------------
@@ -523,6 +555,28 @@ __device__ void g_decode(const GenLaunch& L, const uint8_t* row, int64_t row_len
         if (rel < 0 || start + f.header + 8LL * nd.nchild > row_len) corrupt();
         else f.start = (int32_t)start, f.rel = 1;
       }
+      return;
+    }
+    if (nd.kind == KIND_DECIMAL) {  // UnsafeTrait.getDecimal (UnsafeTrait.java:139-150): 32 bytes
+      if (!values) return;
+      uint32_t w[4] = {0u, 0u, 0u, 0u};  // null: zeros
+      if (!isnull) {
+        const uint64_t os = gget(slot, 8);
+        const int64_t rel = (int64_t)(int32_t)(os >> 32), at = r.start + rel;
+        if (rel < 0 || (uint32_t)os != 32u || at + 32 > row_len || (at & 3)) {
+          corrupt();
+          return;
+        }
+        for (int q = 0; q < 4; ++q) w[q] = ld32(row + at + 4 * q);
+        const uint32_t ext = (w[3] >> 31) ? 0xffffffffu : 0u;
+        bool fits = true;  // a decimal128 output holds it: bytes 16..31 are the sign extension
+        for (int q = 4; q < 8; ++q) fits = fits && ld32(row + at + 4 * q) == ext;
+        if (!fits) {
+          corrupt();
+          return;
+        }
+      }
+      for (int q = 0; q < 4; ++q) st32(c.out_values + 16 * pos + 4 * q, w[q]);
       return;
     }
     // BYTES / LIST / MAP: (offset, size) relative to the enclosing row / array

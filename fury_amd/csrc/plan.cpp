@@ -32,7 +32,7 @@ static bool supported_type(int32_t t) {
     case FORY_TYPE_BOOL: case FORY_TYPE_INT8: case FORY_TYPE_INT16: case FORY_TYPE_INT32:
     case FORY_TYPE_INT64: case FORY_TYPE_FLOAT: case FORY_TYPE_DOUBLE: case FORY_TYPE_STRING:
     case FORY_TYPE_BINARY: case FORY_TYPE_DATE32: case FORY_TYPE_TIMESTAMP: case FORY_TYPE_LIST:
-    case FORY_TYPE_STRUCT: case FORY_TYPE_MAP:
+    case FORY_TYPE_STRUCT: case FORY_TYPE_MAP: case FORY_TYPE_DECIMAL:
       return true;
     default:
       return false;
@@ -50,7 +50,8 @@ static int parse_node(const fory_field_desc* d, int32_t n, int32_t at, Plan* p, 
     return FORY_ERR_UNSUPPORTED;
   }
   const fory_field_desc& f = d[at];
-  if (f.reserved != 0 || f.num_children < 0) {
+  const bool dec = f.type_id == FORY_TYPE_DECIMAL;  // reserved = precision (0 = 38)
+  if ((!dec && f.reserved != 0) || (dec && (f.reserved < 0 || f.reserved > 38)) || f.num_children < 0) {
     *err = "invalid field descriptor at index " + std::to_string(at);
     return FORY_ERR_INVALID_ARGUMENT;
   }
@@ -85,6 +86,10 @@ static int parse_node(const fory_field_desc* d, int32_t n, int32_t at, Plan* p, 
     case FORY_TYPE_STRUCT: nd.kind = KIND_STRUCT; break;
     case FORY_TYPE_LIST: nd.kind = KIND_LIST; break;
     case FORY_TYPE_MAP: nd.kind = KIND_MAP; break;
+    case FORY_TYPE_DECIMAL:  // TypeInference: BigDecimal -> Decimal(38, 18), BigInteger -> Decimal(38, 0)
+      nd.kind = KIND_DECIMAL;
+      nd.prec = f.reserved > 0 ? f.reserved : 38;
+      break;
     default: nd.kind = KIND_FIXED; break;
   }
   int32_t cur = at + 1;
@@ -186,6 +191,9 @@ static int compile_field(const Plan& p, int32_t idx, int32_t ordinal, std::vecto
       prog->push_back({OP_LIST, ordinal, idx, item, flags, elem_width(it) | (iflags << 8)});
       return FORY_OK;
     }
+    case KIND_DECIMAL:  // writeDecimal (BinaryWriter.java:214-230): the tree engine's
+      *err = "decimal fields run on the tree engine";
+      return FORY_ERR_UNSUPPORTED;
     case KIND_MAP: {  // serializeForMap (BaseBinaryEncoderBuilder.java:370-427)
       const int32_t key = nd.children[0], val = nd.children[1];
       const Node& k = p.nodes[key];
@@ -219,6 +227,7 @@ static int32_t fill_gnode(Plan* p, int32_t idx, int32_t cdepth) {
   g.flags = nd.nullable ? 1 : 0;
   g.nchild = (int32_t)nd.children.size();
   g.cdepth = cdepth;
+  g.prec = nd.prec;
   if (cdepth > p->max_cdepth) p->max_cdepth = cdepth;
   const int32_t inner = cdepth + (nd.kind == KIND_LIST || nd.kind == KIND_MAP ? 1 : 0);
   int32_t end = idx + 1;

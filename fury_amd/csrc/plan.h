@@ -29,6 +29,7 @@ enum FieldKind : int32_t {
   KIND_STRUCT = 3,  // nested row inline in the variable section
   KIND_LIST = 4,    // BinaryArray inline in the variable section
   KIND_MAP = 5,     // BinaryMap inline: [i64 keyArrayBytes][key BinaryArray][value BinaryArray]
+  KIND_DECIMAL = 6, // decimal128 column -> 32 sign-extended bytes behind an (offset, 32) slot (tree engine)
 };
 
 // Per top-level field of a fixed-width plan (read by the tiled kernels).
@@ -117,6 +118,7 @@ struct GNode {
   int32_t end;     // index after the subtree
   int32_t nchild;
   int32_t cdepth;  // list / map ancestors: the decode lengths pass that sizes this column
+  int32_t prec;    // KIND_DECIMAL: precision (|unscaled| <= 10^prec - 1), else 0
 };
 
 struct Node {
@@ -124,6 +126,7 @@ struct Node {
   int32_t nullable = 0;
   int32_t width = -1;
   int32_t kind = 0;
+  int32_t prec = 0;               // KIND_DECIMAL: precision (descriptor's reserved word, 0 = 38)
   std::vector<int32_t> children;  // desc indices
 };
 

@@ -76,6 +76,12 @@ def _build(f: Field, vals: Sequence[Any], out: List[HostColumn], absent: Optiona
             if v is not None:
                 arr[i] = (1 if v else 0) if t == ArrowType.BOOL else v
         col.values = arr
+    elif t == ArrowType.DECIMAL128:
+        arr = np.zeros((n, 2), dtype=np.int64)
+        for i, v in enumerate(vals):
+            if v is not None:
+                arr[i] = decimal_words(v, f.type.scale)
+        col.values = arr
     elif t in (ArrowType.STRING, ArrowType.BINARY):
         parts = []
         offs = np.zeros(n + 1, dtype=np.int32)
@@ -116,6 +122,45 @@ def _build(f: Field, vals: Sequence[Any], out: List[HostColumn], absent: Optiona
             _build(c, [None if v is None else v[c.name] for v in vals], out, gone)
     else:
         raise NotImplementedError(f"type {f.type} not supported")
+
+
+def decimal_words(v, scale: int):
+    """An Arrow decimal128 value: the unscaled integer at `scale` (a decimal.Decimal, or an
+    int taken as already unscaled), as (lo, hi) little-endian two's complement int64 words.
+    A Decimal whose scale differs is an error, as DecimalUtility.checkPrecisionAndScale's."""
+    import decimal
+    if isinstance(v, decimal.Decimal):
+        sign, digits, exp = v.as_tuple()
+        if -exp != scale:
+            raise ValueError(f"BigDecimal scale must equal the field's: {-exp} != {scale}")
+        u = int("".join(map(str, digits)) or "0")
+        u = -u if sign else u
+    else:
+        u = int(v)
+    if not -(1 << 127) <= u < (1 << 127):
+        raise ValueError("decimal value exceeds 128 bits")
+    u &= (1 << 128) - 1
+    lo, hi = u & ((1 << 64) - 1), u >> 64
+    return np.array([lo, hi], dtype=np.uint64).view(np.int64)
+
+
+def decimal_value(words, scale: int):
+    """decimal.Decimal of one (lo, hi) decimal128 element."""
+    import decimal
+    lo, hi = (int(x) for x in np.asarray(words, dtype=np.int64).view(np.uint64))
+    u = lo | (hi << 64)
+    if u >= 1 << 127:
+        u -= 1 << 128
+    return decimal.Decimal(u).scaleb(-scale, context=decimal.Context(prec=80))
+
+
+def alloc_values(type_id: int, k: int):
+    """Zeroed values of k elements of a fixed-width or decimal column (None otherwise)."""
+    if type_id in NP_DTYPE:
+        return np.zeros(max(1, k), NP_DTYPE[type_id])
+    if type_id == ArrowType.DECIMAL128:
+        return np.zeros((max(1, k), 2), np.int64)
+    return None
 
 
 def build_columns(schema: Schema, rows: Sequence[Dict[str, Any]]) -> List[HostColumn]:

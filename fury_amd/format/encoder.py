@@ -154,6 +154,8 @@ class RowEncoder:
                 t = f.type.id
                 if t in var_kinds:
                     c.offsets = torch.zeros(npos + 1, dtype=torch.int32, device=self.device)
+                elif t == ArrowType.DECIMAL128:  # decimal128: (lo, hi) int64 words per element
+                    c.values = torch.empty((max(1, npos), 2), dtype=torch.int64, device=self.device)
                 elif t != ArrowType.STRUCT:
                     c.values = torch.empty(max(1, npos), dtype=_torch_dtype(t), device=self.device)
                 if f.nullable:

@@ -7,7 +7,8 @@ for Python classes whose annotations name Java field types:
   primitives (not null):  jboolean jbyte jshort jint jlong jfloat jdouble
   boxed (nullable):       Boolean Byte Short Integer Long Float Double
   nullable other:         String (utf8), LocalDate (date32), Timestamp / Instant
-                          (timestamp), Binary (binary)
+                          (timestamp), Binary (binary), BigDecimal (decimal(38, 18)),
+                          BigInteger (decimal(38, 0))  (TypeInference.java:198-204)
   List[X] / X[]           list (nullable) with element field "item"
   Dict[K, V] / Map<K,V>   map (nullable): key field "key" forced not-null, value "value"
                           (TypeInference.java:228-237, DataTypes.mapField :404-424)
@@ -55,6 +56,12 @@ LocalDate = _jt("LocalDate", ArrowType.DATE32, True)
 Timestamp = _jt("Timestamp", ArrowType.TIMESTAMP, True)
 Instant = _jt("Instant", ArrowType.TIMESTAMP, True)
 Binary = _jt("Binary", ArrowType.BINARY, True)
+# TypeInference.java:198-204: Decimal(DecimalUtils.MAX_PRECISION 38, MAX_SCALE 18) /
+# Decimal(38, 0), nullable
+BigDecimal = type("BigDecimal", (_JavaType,), {"type_id": ArrowType.DECIMAL128, "nullable": True,
+                                               "precision": 38, "scale": 18})
+BigInteger = type("BigInteger", (_JavaType,), {"type_id": ArrowType.DECIMAL128, "nullable": True,
+                                               "precision": 38, "scale": 0})
 
 
 def lower_camel_to_lower_underscore(s: str) -> str:
@@ -94,6 +101,8 @@ def _infer_field(name: str, tp, walked: List[type]) -> Field:
         key = Field(key.name, key.type, False, key.children)  # Map's keys must be non-nullable
         return DataTypes.map_field(name, key, _infer_field("value", vt, walked))
     if isinstance(tp, type) and issubclass(tp, _JavaType):
+        if tp.type_id == ArrowType.DECIMAL128:
+            return Field(name, DataTypes.decimal(tp.precision, tp.scale), tp.nullable)
         return Field(name, DataType(tp.type_id), tp.nullable)
     if isinstance(tp, type) and getattr(tp, "__annotations__", None):
         if tp in walked:  # TypeResolutionContext.checkNoCycle

@@ -304,7 +304,7 @@ class HostPipeline:
     def alloc_columns(self, counts, nbytes):
         """Zeroed host columns for per-column element counts / string bytes (length = count)."""
         import numpy as np
-        from .columns import HostColumn, NP_DTYPE, validity_bytes
+        from .columns import HostColumn, NP_DTYPE, alloc_values, validity_bytes
         from .types import ArrowType, preorder
         fields = preorder(self.plan.schema)
         cols = []
@@ -313,8 +313,8 @@ class HostPipeline:
             c = HostColumn(length=k)
             if t in (ArrowType.STRING, ArrowType.BINARY):
                 c.values = np.zeros(max(1, int(nbytes[i])), np.uint8)
-            elif t in NP_DTYPE:
-                c.values = np.zeros(max(1, k), NP_DTYPE[t])
+            elif t in NP_DTYPE or t == ArrowType.DECIMAL128:
+                c.values = alloc_values(t, k)
             if t in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP):
                 c.offsets = np.zeros(k + 1, np.int32)
             if f.nullable:
@@ -325,7 +325,7 @@ class HostPipeline:
     def decode_var_finish(self, counts, nbytes):
         """fory_rowfmt_host_decode_var: the staged batch into freshly sized host columns."""
         import numpy as np
-        from .columns import HostColumn, NP_DTYPE, validity_bytes
+        from .columns import HostColumn, NP_DTYPE, alloc_values, validity_bytes
         from .types import ArrowType, preorder
         fields = preorder(self.plan.schema)
         cols = []
@@ -334,8 +334,8 @@ class HostPipeline:
             c = HostColumn(length=k)
             if t in (ArrowType.STRING, ArrowType.BINARY):
                 c.values = np.zeros(max(1, int(nbytes[i])), np.uint8)
-            elif t in NP_DTYPE:
-                c.values = np.zeros(max(1, k), NP_DTYPE[t])
+            elif t in NP_DTYPE or t == ArrowType.DECIMAL128:
+                c.values = alloc_values(t, k)
             if t in (ArrowType.STRING, ArrowType.BINARY, ArrowType.LIST, ArrowType.MAP):
                 c.offsets = np.zeros(k + 1, np.int32)
             if f.nullable:

@@ -65,13 +65,22 @@ _NAMES = {v: k.lower() for k, v in vars(ArrowType).items() if not k.startswith("
 @dataclass(frozen=True)
 class DataType:
     id: int
+    precision: int = 0  # DECIMAL128 only (Arrow Decimal(precision, scale)); neither enters the hash
+    scale: int = 0
 
     @property
     def width(self) -> int:
         """DataTypes.getTypeWidth: byte width, -1 for variable-width types."""
         return _WIDTH.get(self.id, -1)
 
+    @property
+    def column_width(self) -> int:
+        """Bytes per element of the Arrow column (decimal128: 16), -1 for var-length."""
+        return 16 if self.id == ArrowType.DECIMAL128 else self.width
+
     def __repr__(self) -> str:
+        if self.id == ArrowType.DECIMAL128:
+            return f"decimal({self.precision}, {self.scale})"
         return _NAMES.get(self.id, str(self.id))
 
 
@@ -153,6 +162,12 @@ class DataTypes:
         return DataType(ArrowType.TIMESTAMP)
 
     @staticmethod
+    def decimal(precision: int = 38, scale: int = 18) -> DataType:
+        """DataTypes.decimal (DataTypes.java:291-298): Decimal(MAX_PRECISION 38, MAX_SCALE 18)
+        by default; DataTypes.bigintDecimal = decimal(38, 0)."""
+        return DataType(ArrowType.DECIMAL128, precision, scale)
+
+    @staticmethod
     def field(name: str, type_: DataType, nullable: bool = True,
               children: Optional[Sequence[Field]] = None) -> Field:
         return Field(name, type_, nullable, list(children or []))
@@ -205,19 +220,24 @@ def flatten(schema: Schema):
     out: List[tuple] = []
 
     def visit(f: Field):
-        out.append((f.type.id, 1 if f.nullable else 0, len(f.children)))
+        out.append((f.type.id, 1 if f.nullable else 0, len(f.children), desc_reserved(f.type)))
         for c in f.children:
             visit(c)
 
     for f in schema.fields:
         visit(f)
     arr = (FieldDesc * max(1, len(out)))()
-    for i, (t, n, k) in enumerate(out):
+    for i, (t, n, k, r) in enumerate(out):
         arr[i].type_id = t
         arr[i].nullable = n
         arr[i].num_children = k
-        arr[i].reserved = 0
+        arr[i].reserved = r
     return arr, len(out)
+
+
+def desc_reserved(t: DataType) -> int:
+    """fory_field_desc.reserved: a decimal's precision (0 = 38), else 0."""
+    return (t.precision or 38) if t.id == ArrowType.DECIMAL128 else 0
 
 
 def preorder(schema: Schema) -> List[Field]:

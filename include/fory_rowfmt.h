@@ -70,6 +70,7 @@ enum fory_type_id {
   FORY_TYPE_BINARY = 14,
   FORY_TYPE_DATE32 = 16,
   FORY_TYPE_TIMESTAMP = 18,
+  FORY_TYPE_DECIMAL = 23,   /* ArrowType.DECIMAL (= DECIMAL128's id): BigDecimal / BigInteger fields */
   FORY_TYPE_LIST = 25,
   FORY_TYPE_STRUCT = 26,
   FORY_TYPE_MAP = 30
@@ -88,7 +89,7 @@ typedef struct fory_field_desc {
   int32_t type_id;       /* enum fory_type_id */
   int32_t nullable;      /* 1 = boxed/String/bean/List (TypeInference.java:182-247) */
   int32_t num_children;  /* STRUCT: >= 0, LIST: 1, MAP: 2, others: 0 */
-  int32_t reserved;      /* must be 0 */
+  int32_t reserved;      /* DECIMAL: the precision (0 = 38, DecimalUtils.MAX_PRECISION); else 0 */
 } fory_field_desc;
 
 /* Column of one field (index = pre-order index of its fory_field_desc).
@@ -98,6 +99,12 @@ typedef struct fory_field_desc {
  *  LIST        : offsets = length+1 int32 Arrow offsets into the child column
  *  MAP         : offsets = length+1 int32 Arrow offsets into the key and value
  *                columns (entries); key/value columns hold one slot per entry
+ *  DECIMAL     : values = length * 16 bytes, Arrow decimal128 (the unscaled value,
+ *                little-endian two's complement, at the field's scale). A row holds it
+ *                out of line as 32 bytes sign-extended behind an (offset, 32) slot
+ *                (BinaryWriter.writeDecimal, BinaryWriter.java:214-230,
+ *                DecimalUtils.DECIMAL_BYTE_LENGTH = 32); |value| > 10^precision - 1
+ *                is FORY_ERR_UNSUPPORTED on encode (DecimalUtility.checkPrecisionAndScale)
  *  STRUCT      : values/offsets unused; children have the same length
  *  validity    : Arrow validity bitmap, LSB-first, 1 = valid; NULL = all valid.
  *                Only read/written for nullable fields.

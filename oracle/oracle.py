@@ -70,16 +70,21 @@ def _desc(schema):
     out = []
 
     def visit(f):
-        out.append((f.type.id, 1 if f.nullable else 0, len(f.children)))
+        # a decimal's descriptor carries its precision (0 = 38); the scale is the column's
+        prec = (getattr(f.type, "precision", 0) or 38) if f.type.id == _DECIMAL else 0
+        out.append((f.type.id, 1 if f.nullable else 0, len(f.children), prec))
         for c in f.children:
             visit(c)
 
     for f in schema.fields:
         visit(f)
     arr = (_Desc * max(1, len(out)))()
-    for i, (t, n, k) in enumerate(out):
-        arr[i].type_id, arr[i].nullable, arr[i].num_children, arr[i].reserved = t, n, k, 0
+    for i, (t, n, k, r) in enumerate(out):
+        arr[i].type_id, arr[i].nullable, arr[i].num_children, arr[i].reserved = t, n, k, r
     return arr, len(out)
+
+
+_DECIMAL = 23  # ArrowType.DECIMAL (DECIMAL128's id)
 
 
 def _p(a: Optional[np.ndarray]):
@@ -109,6 +114,8 @@ def encode(schema, cols, n: int, frame_mode: int) -> Tuple[np.ndarray, np.ndarra
     ca = _cols(cols)
     offs = np.zeros(n + 1, dtype=np.int64)
     total = lib.oracle_encode(d, nd, ca, n, frame_mode, None, 0, offs.ctypes.data)
+    if total == -3:
+        raise OracleUnsupported("decimal precision exceeds the field's (DecimalUtility.checkPrecisionAndScale)")
     if total < 0:
         raise RuntimeError(f"oracle_encode sizing failed: {total}")
     out = np.zeros(max(1, total), dtype=np.uint8)
@@ -116,6 +123,10 @@ def encode(schema, cols, n: int, frame_mode: int) -> Tuple[np.ndarray, np.ndarra
     if got != total:
         raise RuntimeError(f"oracle_encode failed: {got}")
     return out[:total], offs
+
+
+class OracleUnsupported(RuntimeError):
+    """The reference's UnsupportedOperationException on encode (decimal precision)."""
 
 
 class OracleError(RuntimeError):
@@ -147,6 +158,8 @@ def decode(schema, buf: np.ndarray, offsets: Optional[np.ndarray], n: int, frame
         t = f.type.id
         if t in NP_DTYPE:
             c.values = np.zeros(max(1, ln), dtype=NP_DTYPE[t])
+        elif t == ArrowType.DECIMAL128:  # decimal128: (lo, hi) little-endian int64 words
+            c.values = np.zeros((max(1, ln), 2), dtype=np.int64)
         elif t in (ArrowType.STRING, ArrowType.BINARY):
             c.offsets = np.zeros(ln + 1, dtype=np.int32)
             c.values = np.zeros(max(1, int(nbytes[i])), dtype=np.uint8)

@@ -48,6 +48,7 @@ typedef struct onode {
   int type_id;
   int nullable;
   int width;      /* DataTypes.getTypeWidth (DataTypes.java:68-133), -1 = varlen */
+  int precision;  /* DECIMAL: from the descriptor's reserved word (0 = 38) */
   int nchild;
   int child[64];  /* desc indices of children (struct fields / list item) */
 } onode;
@@ -75,6 +76,8 @@ static int parse(const fory_field_desc* d, int n, int at, otree* t) {
   nd->type_id = d[at].type_id;
   nd->nullable = d[at].nullable;
   nd->width = type_width(d[at].type_id);
+  nd->precision = d[at].type_id == FORY_TYPE_DECIMAL ? (d[at].reserved > 0 ? d[at].reserved : 38) : 0;
+  if (nd->precision > 38) return -1;
   nd->nchild = 0;
   int next = at + 1;
   int want = d[at].num_children;
@@ -238,6 +241,32 @@ static void w_write_unaligned(owriter* w, int64_t ordinal, const uint8_t* src, i
   b->wi += rounded;
 }
 
+/* BinaryWriter.writeDecimal (BinaryWriter.java:214-230) of an Arrow decimal128 value
+ * (16 bytes, little-endian two's complement of the unscaled value):
+ * DecimalUtility.checkPrecisionAndScale (|unscaled| <= 10^precision - 1, else
+ * UnsupportedOperationException; the scale is the column's), then
+ * writeBigDecimalToArrowBuf(value, buf, 0, DECIMAL_BYTE_LENGTH = 32): the value's
+ * little-endian bytes sign-extended to 32 (DecimalUtils.java:23), copied at the
+ * writerIndex, slot = (offset, 32), writerIndex += 32 (already a multiple of 8).
+ * Returns 0, or -3 when the precision check fails. */
+static int w_write_decimal(owriter* w, int64_t ordinal, const uint8_t* v16, int precision) {
+  __int128 v;
+  memcpy(&v, v16, 16);
+  unsigned __int128 mag = v < 0 ? (unsigned __int128)(-(v + 1)) + 1 : (unsigned __int128)v;
+  unsigned __int128 lim = 1;
+  for (int k = 0; k < precision; k++) lim *= 10;
+  if (mag > lim - 1) return -3;
+  uint8_t dec[32];
+  memcpy(dec, v16, 16);
+  memset(dec + 16, (v16[15] & 0x80) ? 0xFF : 0x00, 16);
+  obuf* b = w->b;
+  grow(b, 32);
+  putbytes(b, b->wi, dec, 32);
+  w_set_offset_and_size(w, ordinal, b->wi, 32);
+  b->wi += 32;
+  return 0;
+}
+
 /* ---------------------------------------------------------------------- */
 /* column access                                                           */
 /* ---------------------------------------------------------------------- */
@@ -372,6 +401,9 @@ static void write_value(owriter* w, int64_t ordinal, const otree* t, int idx,
       w_write_unaligned(w, ordinal, (const uint8_t*)c->values + s0, s1 - s0); /* :162-194 */
       return;
     }
+    case FORY_TYPE_DECIMAL:
+      if (w_write_decimal(w, ordinal, (const uint8_t*)c->values + 16 * i, nd->precision)) b->overflow = 3;
+      return;
     case FORY_TYPE_STRUCT:
       write_struct_body(w, ordinal, t, idx, cols, i);
       return;
@@ -422,6 +454,7 @@ int64_t oracle_encode(const fory_field_desc* d, int n_desc, const fory_column* c
       else write_map_payload(&b, &t, t.top[0], cols, i);
       put32(&b, frame, (uint32_t)(b.wi - frame - 4));
       if (b.overflow == 2) { free_tree(&t); return -2; }
+      if (b.overflow == 3) { free_tree(&t); return -3; }
       continue;
     }
     if (frame_mode == 3) {                            /* encode(T): buffer.writeInt64(schemaHash) */
@@ -435,6 +468,7 @@ int64_t oracle_encode(const fory_field_desc* d, int n_desc, const fory_column* c
     for (int k = 0; k < t.ntop; k++) write_value(&w, k, &t, t.top[k], cols, i);
     if (frame_mode == 1) put32(&b, frame, (uint32_t)(b.wi - frame - 4)); /* back-patch */
     if (b.overflow == 2) { free_tree(&t); return -2; }
+    if (b.overflow == 3) { free_tree(&t); return -3; }  /* decimal precision */
   }
   if (row_offsets) row_offsets[nrows] = b.wi;
   free_tree(&t);
@@ -484,6 +518,8 @@ static void null_value(odec* D, const otree* t, int idx, const fory_column* cols
   if (nd->nullable) set_valid(c, i, 0);
   if (nd->width > 0) {
     memset((uint8_t*)c->values + i * nd->width, 0, (size_t)nd->width);
+  } else if (nd->type_id == FORY_TYPE_DECIMAL) {
+    memset((uint8_t*)c->values + i * 16, 0, 16);
   } else if (nd->type_id == FORY_TYPE_STRUCT) {
     for (int k = 0; k < nd->nchild; k++) null_value(D, t, nd->child[k], cols, i);
   } else {
@@ -501,7 +537,7 @@ static void read_value(odec* D, const otree* t, int idx, const fory_column* cols
                        int64_t i, int is_null, int64_t slot_at, int64_t base) {
   const onode* nd = &t->nodes[idx];
   const fory_column* c = &cols[idx];
-  if (!D->sizing && i == 0 && nd->width < 0 && nd->type_id != FORY_TYPE_STRUCT)
+  if (!D->sizing && i == 0 && nd->width < 0 && nd->type_id != FORY_TYPE_STRUCT && nd->type_id != FORY_TYPE_DECIMAL)
     c->offsets[0] = (int32_t)D->cursor[idx];
   if (is_null) { null_value(D, t, idx, cols, i); return; }  /* RowEncoderBuilder.java:239-246 */
   D->slots[idx]++;
@@ -535,6 +571,17 @@ static void read_payload(odec* D, const otree* t, int idx, const fory_column* co
         c->offsets[i + 1] = (int32_t)(dst + size);
       }
       D->cursor[idx] = dst + size;
+      return;
+    }
+    case FORY_TYPE_DECIMAL: { /* UnsafeTrait.getDecimal :139-150: DECIMAL_BYTE_LENGTH = 32 bytes at the slot's
+                                 offset, DecimalUtility.getBigDecimalFromArrowBuf; an Arrow decimal128
+                                 output holds it when bytes 16..31 are the sign extension of byte 15 */
+      if (size != 32) { D->bad = 1; return; }
+      const uint8_t* p = D->p + at;
+      const uint8_t ext = (p[15] & 0x80) ? 0xFF : 0x00;
+      for (int k = 16; k < 32; k++)
+        if (p[k] != ext) { D->bad = 1; return; }
+      if (!D->sizing) memcpy((uint8_t*)c->values + 16 * i, p, 16);
       return;
     }
     case FORY_TYPE_STRUCT: { /* getStruct :160-173, then the child codec's fromRow */

@@ -49,6 +49,17 @@ stats = [r for f in glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), rec
 for r in stats:
     out["kernels"][short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                         "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
+# per-kernel resources from the kernel trace (VGPR / AGPR / SGPR, LDS, scratch, workgroup)
+out["resources"] = {}
+for f in glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True):
+    if "pmc_" in os.path.relpath(f, root):
+        continue
+    for r in csv.DictReader(open(f)):
+        k = short(r.get("Kernel_Name", ""))
+        if k in out["resources"]:
+            continue
+        out["resources"][k] = {c: r[c] for c in r
+                               if any(t in c for t in ("VGPR", "SGPR", "LDS", "Scratch", "Segment", "Workgroup_Size"))}
 acc = defaultdict(lambda: defaultdict(list))
 for d in glob.glob(os.path.join(root, "pmc_*")):
     if not os.path.isdir(d):
@@ -62,5 +73,11 @@ for k, cs in acc.items():
         e["fetch_bytes_x2"] = e["FETCH_SIZE"] * 2048
     if "WRITE_SIZE" in e:
         e["write_bytes"] = e["WRITE_SIZE"] * 1024
+    if "SQ_WAVE_CYCLES" in e and e["SQ_WAVE_CYCLES"] > 0:  # where the waves' time goes (quad-cycles)
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
+            if c in e:
+                e[c + "_frac"] = e[c] / e["SQ_WAVE_CYCLES"]
+    if "SQ_LDS_IDX_ACTIVE" in e and e["SQ_LDS_IDX_ACTIVE"] > 0 and "SQ_LDS_BANK_CONFLICT" in e:
+        e["lds_bank_conflict_frac"] = e["SQ_LDS_BANK_CONFLICT"] / e["SQ_LDS_IDX_ACTIVE"]
     out["pmc"][k] = e
 print(json.dumps(out, indent=1))

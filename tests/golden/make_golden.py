@@ -73,13 +73,15 @@ def main():
             typ = pa.struct([to_pa(c) for c in f.children])
         elif t == ArrowType.MAP:
             typ = pa.map_(to_pa(f.children[0]).type, to_pa(f.children[1]).type)
+        elif t == ArrowType.DECIMAL128:  # pa.decimal128's id == ArrowType.DECIMAL (DECIMAL128) = 23
+            typ = pa.decimal128(f.type.precision or 38, f.type.scale)
         else:
             raise ValueError(t)
         return pa.field(f.name, typ, nullable=f.nullable)
 
     from fury_amd.format.types import DataType, DataTypes, Field, Schema
     sys.path.insert(0, os.path.join(REPO, "tests"))
-    from helpers import deep_nested_schema, list_struct_schema, maps_schema, string_elems_schema
+    from helpers import deep_nested_schema, list_struct_schema, maps_schema, nested_schemas, string_elems_schema
 
     edge = {
         "empty": Schema([]),
@@ -95,6 +97,8 @@ def main():
         "deep_nested": deep_nested_schema(),
         "list_struct": list_struct_schema(),
         "string_elems": string_elems_schema(),
+        "decimals": nested_schemas()["decimals"],  # BigDecimal / BigInteger fields (decimal128 ids)
+        "bean_a": nested_schemas()["bean_a"],      # BeanA incl. f16 (BigDecimal)
     }
     schemas = {"struct104": W.struct_schema(), "mixed40": W.mixed_schema(),
                "nested": W.nested_schema(), **edge}

@@ -410,7 +410,7 @@ def collection_cases(n=300, seed=5):
 # Mirrors of the reference's test beans, inferred like Encoders.bean does
 # (TypeInference.java:141-254): RowEncoderTest.Foo / Bar (RowEncoderTest.java:66-95),
 # BeanA / BeanB (fory-test-core .../bean/BeanA.java:34-53, BeanB.java:29-36) without
-# BeanA.f16 (BigDecimal: no device decimal) and the transient f13. Java arrays are
+# the transient f13 (f16 is a BigDecimal: decimal(38, 18)). Java arrays are
 # lists of not-null elements (int[] -> list<int32>, byte[] -> list<int8>,
 # Iterable<BeanB> -> list<struct>).
 def reference_beans():
@@ -424,7 +424,7 @@ def reference_beans():
         "intArr": L[I.jint], "intList": L[I.Integer]}})
     bean_a = type("BeanA", (), {"__annotations__": {
         "f1": I.jshort, "f2": I.Integer, "f3": I.jlong, "f4": I.Float, "f5": I.jdouble, "beanB": bean_b,
-        "intArray": L[I.jint], "bytes": L[I.jbyte], "f12": I.jboolean, "f15": I.Integer, "f17": I.String,
+        "intArray": L[I.jint], "bytes": L[I.jbyte], "f12": I.jboolean, "f15": I.Integer, "f16": I.BigDecimal, "f17": I.String,
         "longStringField": I.String, "doubleList": L[I.Double], "beanBIterable": L[bean_b],
         "beanBList": L[bean_b], "stringBeanBMap": Dict[I.String, bean_b], "int2DArray": L[L[I.jint]],
         "double2DList": L[L[I.Double]]}})
@@ -450,6 +450,14 @@ def nested_schemas():
             Field("s", DataType(ArrowType.STRING), True),
             DataTypes.array_field("l", DataTypes.array_field("item", Field("item", DataType(ArrowType.INT16), True))),
             Field("b", DataType(ArrowType.BOOL), False)]))))
+    # BigDecimal / BigInteger fields (TypeInference.java:198-204) in rows, child rows,
+    # lists and map values; one decimal of precision 10 (out-of-range values are errors)
+    decimals = type("Decimals", (), {"__annotations__": {
+        "amount": I.BigDecimal, "count": I.BigInteger, "prices": L[I.BigDecimal],
+        "byName": Dict[I.String, I.BigDecimal], "inner": type("Inner", (), {"__annotations__": {
+            "d": I.BigDecimal, "n": I.jint}}), "id": I.jlong}})
+    dec_schema = I.infer_schema(decimals)
+    dec_schema.fields.append(Field("small", DataTypes.decimal(10, 2), True))
     chain = Field("item", DataType(ArrowType.INT32), True)
     for k in range(9):  # list^9<int32>: 10 schema levels (the 18-frame instantiation)
         chain = DataTypes.array_field("item" if k < 8 else "chain", chain)
@@ -459,6 +467,7 @@ def nested_schemas():
         "maps_nested": I.infer_schema(maps),
         "foo": I.infer_schema(foo),
         "bean_a": I.infer_schema(B["BeanA"]),
+        "decimals": dec_schema,
         "deep": Schema([Field("id", DataType(ArrowType.INT32), False), deep]),
         "chain": Schema([chain, Field("z", DataType(ArrowType.INT64), True)]),
     }
@@ -478,6 +487,17 @@ def random_value(f: Field, rng, depth: int = 0, null_p: float = 0.12):
             return [random_value(f.children[0], rng, depth + 1, null_p) for _ in range(k)]
         return [(random_value(f.children[0], rng, depth + 1, null_p), random_value(f.children[1], rng, depth + 1, null_p))
                 for _ in range(k)]
+    if t == ArrowType.DECIMAL128:  # the unscaled value: up to `precision` digits, either sign
+        p = f.type.precision or 38
+        r = rng.random()
+        if r < 0.1:  # the extremes of the precision
+            u = 10 ** p - 1
+        elif r < 0.3:
+            u = int(rng.integers(0, 1000))
+        else:
+            digits = int(rng.integers(1, p + 1))
+            u = int("".join(str(int(x)) for x in rng.integers(0, 10, size=digits)))
+        return -u if rng.random() < 0.5 else u
     if t == ArrowType.STRING:
         alphabet = "abcdefghij0123456789 éü中文😀"
         return "".join(alphabet[int(x)] for x in rng.integers(0, len(alphabet), size=rng.integers(0, 24)))

@@ -331,7 +331,7 @@ def test_host_varlen_decode_of_a_sub_range(name):
 
 
 @pytest.mark.parametrize("frame", [0, 1])
-@pytest.mark.parametrize("name", ["holder", "lists", "maps_nested", "bean_a", "deep", "chain"])
+@pytest.mark.parametrize("name", ["holder", "lists", "maps_nested", "bean_a", "deep", "chain", "decimals"])
 def test_host_varlen_nested_collections(name, frame):
     """The tree engine's shapes (list<list<...>>, List<Bean with strings>, Map<K, Bean>,
     BeanA, list^9) through the host path: bytes and offsets == the oracle, decode
@@ -469,7 +469,7 @@ def test_host_varlen_decode_into(name, frame, chunk):
     hp.close()
 
 
-@pytest.mark.parametrize("name", ["holder", "lists", "maps_nested", "bean_a", "deep"])
+@pytest.mark.parametrize("name", ["holder", "lists", "maps_nested", "bean_a", "deep", "decimals"])
 def test_host_varlen_decode_into_nested(name):
     """The tree engine's shapes through the one-call decode, 256-row chunks: every
     nesting level sized per chunk, offsets of every level rebased."""

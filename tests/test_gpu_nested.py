@@ -1,8 +1,8 @@
 """GPU: nested collections on the device (the tree engine, fury_amd/csrc/generic.hip).
 
 Shapes the op programs do not cover — list<list<...>>, List<Bean with strings>,
-Map<String, Bean>, Map<Bean, List<Bean>>, BeanA (minus its BigDecimal), a
-list^9 chain — are encoded on the device byte-identically to the oracle in every
+Map<String, Bean>, Map<Bean, List<Bean>>, BeanA (with its BigDecimal), decimal
+fields in rows / child rows / lists / map values, a list^9 chain — are encoded on the device byte-identically to the oracle in every
 framing, decoded back (with and without row offsets), and the reference's own
 ArrayEncoderTest / MapEncoderTest values produce the byte lengths those tests
 assert (ArrayEncoderTest.java:56,90,124).
@@ -66,7 +66,7 @@ def test_nested_parity(name, n, frame):
     check(schema, encoder_for(name), cols, n, frame)
 
 
-@pytest.mark.parametrize("name", ["holder", "lists", "maps_nested", "bean_a", "deep"])
+@pytest.mark.parametrize("name", ["holder", "lists", "maps_nested", "bean_a", "deep", "decimals"])
 def test_nested_all_null_and_empty(name):
     """Every nullable value null; then every container empty."""
     schema = nested_schemas()[name]
@@ -182,3 +182,43 @@ def test_nested_corrupt_rows_are_reported_not_faulted():
             raised += 1
     assert raised > 0
     assert columns_equal(schema, cols, to_host(enc.decode(rows))) == []
+
+
+# --- decimal fields (BinaryWriter.writeDecimal, BinaryWriter.java:214-230) ------------
+def test_decimal_precision_is_checked_on_the_device():
+    """|unscaled| > 10^precision - 1 is the reference's UnsupportedOperationException
+    (DecimalUtility.checkPrecisionAndScale inside writeDecimal); the oracle agrees."""
+    from fury_amd.format import UnsupportedOperationException
+    from fury_amd.format.types import DataTypes, Field
+    schema = Schema([Field("d", DataTypes.decimal(10, 2), True), Field("id", DataTypes.int64(), False)])
+    rows = [{"d": v, "id": i} for i, v in enumerate([1, 10 ** 10 - 1, -(10 ** 10 - 1), None, 5])]
+    enc = RowEncoder(schema)
+    cols = build_columns(schema, rows)
+    check(schema, enc, cols, len(rows), 1)  # in range: bytes == oracle
+    rows[2]["d"] = -(10 ** 10)  # 11 digits
+    cols = build_columns(schema, rows)
+    with pytest.raises(UnsupportedOperationException):
+        enc.encode(to_device(cols), len(rows), 1)
+    with pytest.raises(oracle.OracleUnsupported):
+        oracle.encode(schema, cols, len(rows), 1)
+
+
+def test_decimal_beyond_decimal128_is_corrupt():
+    """32 row bytes that are not a sign-extended decimal128 cannot land in an Arrow
+    decimal128 column: CorruptRowException (the oracle reports the same)."""
+    schema, cols = nested_columns("decimals", 64, 3)
+    enc = encoder_for("decimals")
+    expect, offs = oracle.encode(schema, cols, 64, 0)
+    bad = expect.copy()
+    # the first non-null top-level decimal of record 0 ("amount", ordinal 0)
+    slot = int.from_bytes(bad[8:16].tobytes(), "little")
+    assert slot & 0xFFFFFFFF == 32 or slot == 0
+    if slot == 0:
+        pytest.skip("record 0's amount is null")
+    at = slot >> 32
+    bad[at + 24] ^= 0x01
+    buf = torch.from_numpy(np.concatenate([bad, np.zeros(16, np.uint8)])).cuda()
+    with pytest.raises(CorruptRowException):
+        enc.decode(buf, 64, 0, torch.from_numpy(offs).cuda())
+    with pytest.raises(oracle.OracleError):
+        oracle.decode(schema, bad, offs, 64, 0)
