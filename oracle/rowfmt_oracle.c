@@ -146,6 +146,7 @@ typedef struct obuf {
   int64_t cap;
   int64_t wi;      /* writerIndex */
   int overflow;
+  int unsupported; /* a decimal beyond its precision (sticky: sizing passes overflow too) */
 } obuf;
 
 static void grow(obuf* b, int64_t need) {
@@ -402,7 +403,7 @@ static void write_value(owriter* w, int64_t ordinal, const otree* t, int idx,
       return;
     }
     case FORY_TYPE_DECIMAL:
-      if (w_write_decimal(w, ordinal, (const uint8_t*)c->values + 16 * i, nd->precision)) b->overflow = 3;
+      if (w_write_decimal(w, ordinal, (const uint8_t*)c->values + 16 * i, nd->precision)) b->unsupported = 1;
       return;
     case FORY_TYPE_STRUCT:
       write_struct_body(w, ordinal, t, idx, cols, i);
@@ -438,7 +439,7 @@ int64_t oracle_encode(const fory_field_desc* d, int n_desc, const fory_column* c
   int64_t hash = 17;
   for (int k = 0; k < t.ntop; k++) hash = hash_node(hash, &t, t.top[k]);
   if (out && cap > 0) memset(out, 0, (size_t)cap);
-  obuf b = {out, out ? cap : 0, 0, 0};
+  obuf b = {out, out ? cap : 0, 0, 0, 0};
   for (int64_t i = 0; i < nrows; i++) {
     if (row_offsets) row_offsets[i] = b.wi;
     int64_t frame = b.wi;
@@ -454,7 +455,7 @@ int64_t oracle_encode(const fory_field_desc* d, int n_desc, const fory_column* c
       else write_map_payload(&b, &t, t.top[0], cols, i);
       put32(&b, frame, (uint32_t)(b.wi - frame - 4));
       if (b.overflow == 2) { free_tree(&t); return -2; }
-      if (b.overflow == 3) { free_tree(&t); return -3; }
+      if (b.unsupported) { free_tree(&t); return -3; }
       continue;
     }
     if (frame_mode == 3) {                            /* encode(T): buffer.writeInt64(schemaHash) */
@@ -468,7 +469,7 @@ int64_t oracle_encode(const fory_field_desc* d, int n_desc, const fory_column* c
     for (int k = 0; k < t.ntop; k++) write_value(&w, k, &t, t.top[k], cols, i);
     if (frame_mode == 1) put32(&b, frame, (uint32_t)(b.wi - frame - 4)); /* back-patch */
     if (b.overflow == 2) { free_tree(&t); return -2; }
-    if (b.overflow == 3) { free_tree(&t); return -3; }  /* decimal precision */
+    if (b.unsupported) { free_tree(&t); return -3; }  /* decimal precision */
   }
   if (row_offsets) row_offsets[nrows] = b.wi;
   free_tree(&t);

@@ -13,3 +13,8 @@ for spec in mixed40:16777216 nested:8388608; do
   OUT=gpurun_out/r03_prof_$cfg BENCH_EXTRA="--config $cfg" ROWS=$rows EXTRA_PMC=$SQ bash scripts/profile.sh > gpurun_out/r03_prof_$cfg.log 2>&1
   rc=$?; echo "prof $cfg exit $rc"; [ $rc -eq 0 ] || exit $rc
 done
+# nullable fixed-width: default vs 512-thread workgroups (FORY_ROWFMT_NULWG, plan-time knob)
+for wg in 0 512; do
+  FORY_ROWFMT_NULWG=$wg timeout -k 10 120 python scripts/bench_nullable_fixed.py > gpurun_out/r03_nul_$wg.json 2>&1
+  rc=$?; echo "nullable wg=$wg exit $rc"; cat gpurun_out/r03_nul_$wg.json; [ $rc -eq 0 ] || exit $rc
+done

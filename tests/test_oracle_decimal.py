@@ -57,6 +57,11 @@ def test_precision_is_checked():
     with pytest.raises(oracle.OracleUnsupported):
         row_of(one(scale=2, precision=10), 10 ** 10)  # 11 digits > 10
     row_of(one(scale=2, precision=10), 10 ** 10 - 1)  # 10 digits: fine
+    # the error survives later rows of the batch (the sizing pass overflows too)
+    s = one(scale=0)
+    cols = build_columns(s, [{"d": v} for v in (1, 2, 10 ** 38, 3, 4)])
+    with pytest.raises(oracle.OracleUnsupported):
+        oracle.encode(s, cols, 5, 1)
 
 
 def test_decimal_words_round_trip():
