@@ -280,7 +280,6 @@ fory_amd::FixedLaunch fixed_launch(const Plan& p, const void* table, int64_t n, 
   L.num_rows = n;
   L.any_nullable = p.any_nullable ? 1 : 0;
   L.frame = frame;
-  L.nul_wg = p.kn.nul_wg;
   // width-group boundaries of the sorted table (bind_fixed)
   const int widths[4] = {8, 4, 2, 1};
   int at = 0;

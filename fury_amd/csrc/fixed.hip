@@ -749,20 +749,10 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
 // XCD-blocked 16.45 / 16.35, + nt column loads 16.38 / 16.12.
 constexpr int kV5R = 64, kV5WG = 1024, kV5K = 3;
 
-// Nullable schemas, A/B (FORY_ROWFMT_NULWG=512): 512-thread workgroups, K = 5 chunk
-// loads per wave, two independent workgroups per CU instead of one of 1024.
-constexpr int kV5WGn = 512, kV5Kn = 5;
-
 template <int HDR, bool NUL>
 hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const int64_t full = L.num_rows / kV5R;
-  if (full > 0 && NUL && L.nul_wg == kV5WGn) {
-    auto* k = &encode_fixed_v5_kernel<kV5R, kV5WGn, kV5Kn, HDR, 1, NUL>;
-    raise_lds_cap(k);
-    const size_t lds = (size_t)kV5R * L.stride;
-    const int64_t grid = persistent_grid(k, lds, full, kV5WGn);
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kV5WGn), lds, s, L, L.fields, out, full, (int64_t)(full / 8));
-  } else if (full > 0) {
+  if (full > 0) {
     auto* k = &encode_fixed_v5_kernel<kV5R, kV5WG, kV5K, HDR, 1, NUL>;
     raise_lds_cap(k);
     const size_t lds = (size_t)kV5R * L.stride;
@@ -786,9 +776,7 @@ hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const size_t lds = (size_t)TR * L.stride;
   if constexpr (TR == 64) {
     // v5: schemas whose chunk instructions fit K per wave (nullable ones: the NUL form)
-    const bool nwg = L.any_nullable && L.nul_wg == kV5WGn;
-    if ((v3_insn_count<kV5R>(L.group) + (nwg ? kV5WGn : kV5WG) / 64 - 1) / ((nwg ? kV5WGn : kV5WG) / 64) <=
-        (nwg ? kV5Kn : kV5K))
+    if ((v3_insn_count<kV5R>(L.group) + kV5WG / 64 - 1) / (kV5WG / 64) <= kV5K)
       return L.any_nullable ? launch_encode_v5<HDR, true>(L, out, s) : launch_encode_v5<HDR, false>(L, out, s);
   }
   auto* k = &encode_fixed_kernel<TR, HDR>;
@@ -802,13 +790,9 @@ hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
 // per wave. In-process A/B at 64Mi Struct104 rows (scripts/microbench/fixed_ab.hip,
 // profiles/r02/ab_dec5.jsonl): 17.51 -> 15.31 ms; WG 512 15.65, WG 256 18.00.
 constexpr int kD5R = 64, kD5WG = 1024, kD5K = 4, kD5K2 = 3;
-constexpr int kD5WGn = 512, kD5Kn = 7, kD5K2n = 5;  // nullable A/B (FORY_ROWFMT_NULWG=512)
 
 template <int HDR>
 bool decode_v5_fits(const FixedLaunch& L) {
-  if (L.any_nullable && L.nul_wg == kD5WGn)
-    return L.cols_aligned16 && kD5R * L.stride <= kD5Kn * kD5WGn * 16 && (kD5R * L.stride) % 16 == 0 &&
-           v3_insn_count<kD5R>(L.group) <= kD5K2n * (kD5WGn / 64);
   return L.cols_aligned16 && kD5R * L.stride <= kD5K * kD5WG * 16 &&
          (kD5R * L.stride) % 16 == 0 && v3_insn_count<kD5R>(L.group) <= kD5K2 * (kD5WG / 64);
 }
@@ -816,13 +800,7 @@ bool decode_v5_fits(const FixedLaunch& L) {
 template <int HDR>
 hipError_t launch_decode_v5(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
   const int64_t full = L.num_rows / kD5R;
-  if (full > 0 && L.any_nullable && L.nul_wg == kD5WGn) {
-    auto* k = &decode_fixed_v5_kernel<kD5R, kD5WGn, kD5Kn, kD5K2n, HDR, 0, true>;
-    raise_lds_cap(k);
-    const size_t lds = (size_t)kD5R * L.stride;
-    const int64_t grid = persistent_grid(k, lds, full, kD5WGn);
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kD5WGn), lds, s, L, L.fields, in, full, status);
-  } else if (full > 0) {
+  if (full > 0) {
     auto* k = L.any_nullable ? &decode_fixed_v5_kernel<kD5R, kD5WG, kD5K, kD5K2, HDR, 0, true>
                              : &decode_fixed_v5_kernel<kD5R, kD5WG, kD5K, kD5K2, HDR, 0, false>;
     raise_lds_cap(k);

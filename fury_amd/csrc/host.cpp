@@ -1470,3 +1470,14 @@ extern "C" int fory_rowfmt_internal_host_copy_path(const void* p, int64_t bytes)
 }
 
 extern "C" int64_t fory_rowfmt_internal_host_staged_pieces(const fory_host_ctx* c) { return c ? c->stage.pieces : -1; }
+
+// Library-internal, for tests: round 2's classification (the first byte's attribute
+// only), kept to show the straddling-range hazard it had next to pinned_range's answer.
+extern "C" int fory_rowfmt_internal_host_first_byte_pinned(const void* p) {
+  hipPointerAttribute_t a{};
+  if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return a.type != hipMemoryTypeUnregistered ? 1 : 0;
+}

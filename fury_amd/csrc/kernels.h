@@ -31,7 +31,7 @@ struct FixedLaunch {
   int64_t tile0;                // first tile of this launch (tail launches after a persistent kernel)
   int64_t xcd_run;              // XCD-grouped tile order: tiles per XCD run (0 = dispatch order)
   int32_t cols_aligned16;       // decode: every output column 16-byte aligned (decode v5's chunk stores)
-  int32_t nul_wg;               // nullable schemas: v5 workgroup size (0 = default; A/B knob FORY_ROWFMT_NULWG)
+  int32_t pad;
 };
 
 hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s);

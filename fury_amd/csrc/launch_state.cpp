@@ -113,9 +113,6 @@ LaunchKnobs knobs_from_env() {
   k.idx_frames = num("FORY_ROWFMT_IDXFRAMES", 0);
   k.prof = num("FORY_ROWFMT_VARPROF", 0) != 0;
   k.diag = set("FORY_ROWFMT_VARDIAG");
-  k.nul_wg = num("FORY_ROWFMT_NULWG", 0);
-  const char* e6 = std::getenv("FORY_ROWFMT_ENC6");
-  k.no_enc6 = e6 && std::atoi(e6) == 0;
   return k;
 }
 

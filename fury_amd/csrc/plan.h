@@ -142,8 +142,6 @@ struct Node {
 //   FORY_ROWFMT_SIZES_PROGRAM  sizes by the op-program walk for flat plans too
 //   FORY_ROWFMT_IDXFRAMES   frames per frame-index chunk
 //   FORY_ROWFMT_VARPROF=1   phase timeline (debug), FORY_ROWFMT_VARDIAG=1 LDS sizing to stderr
-//   FORY_ROWFMT_NULWG=512|1024  workgroup size of the nullable fixed-width v5 kernels
-//   FORY_ROWFMT_ENC6=0      flat plans encode with the tile kernel instead of encode v6
 struct LaunchKnobs {
   int32_t no_tiles;
   int32_t no_flat;
@@ -156,8 +154,7 @@ struct LaunchKnobs {
   int32_t idx_frames;
   int32_t prof;
   int32_t diag;
-  int32_t no_enc6; // FORY_ROWFMT_ENC6=0: the round-2 flat encode kernel for flat plans (A/B, tests)
-  int32_t nul_wg;  // FORY_ROWFMT_NULWG: workgroup size of the nullable fixed-width v5 kernels (A/B)
+  int32_t pad;
 };
 LaunchKnobs knobs_from_env();
 

@@ -1745,338 +1745,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(5, 8)))
 }
 #undef FORY_VAR_ENC_PARAMS
 
-// ---------------------------------------------------------------------------
-// Encode v6 (flat plans without nested structs; Mixed-like schemas): persistent
-// workgroups of 4 waves, one 64-record tile at a time, the NEXT tile's loads in
-// flight while this one is assembled and stored. Per tile t:
-//   M: record bounds, each var field's Arrow offsets + validity (registers, issued
-//      during tile t-G's assembly) -> LDS metadata (e0, length|null, image offsets)
-//   P: fixed columns -> registers (lane = record), every var field's tile span ->
-//      one staging buffer by LDS-DMA (issued before tile t-G's image leaves)
-//   A: wave 0 lays the rows out (frame header, bitmap, var slots / list headers,
-//      payload offsets) from LDS metadata only, all waves write fixed slots,
-//      barrier, var payloads LDS -> LDS (null bits OR-ed here), barrier
-//   S: the tile image leaves with aligned 16-B stores
-// The tile-kernel rounds (var_encode_flat_kernel) wait out a global round trip per
-// phase (bounds, layout loads, each staged field: 18.3 us per Mixed tile at about 4
-// resident, profiles/r02); here a tile waits for one round trip, overlapped with
-// the previous tile's store. Tiles over the image budget or malformed go to the spill
-// list: the flat kernel's big-image launch takes them (per record if still too big).
-constexpr int kV6W = 8;  // register slots per wave: fixed fields (4 waves -> 32; more are loaded in A)
-constexpr int kV6M = 4;  // register slots per wave: var-field metadata (4 waves -> v6 takes <= 16 var fields)
-
-struct V6Lds {
-  int stg, e0, nn, pos, rowo, soff, hdr, total;
-};
-
-__host__ __device__ inline V6Lds v6_lds(int cap, int sb, int num_var) {
-  V6Lds o;
-  o.stg = cap;                     // staging: every var field's span of the tile
-  o.e0 = cap + sb;                 // int32 [num_var][64]: first byte / item of the record's payload
-  o.nn = o.e0 + num_var * 256;     // int32 [num_var][64]: length in bytes / items, bit 31 = null
-  o.pos = o.nn + num_var * 256;    // int32 [num_var][64]: payload offset from the row start, -1 = none
-  o.rowo = o.pos + num_var * 256;  // int32 [64]: frame start of each record in the image
-  o.soff = o.rowo + 64 * 4;        // int32 [num_var][4]: staging offset (-1 = per lane), phase, vofs, span start
-  o.hdr = o.soff + num_var * 16;   // int64 B0, int32 mis, total, class
-  o.total = o.hdr + 32;
-  return o;
-}
-
-// tile classes (hdr[3])
-enum : int32_t { V6_OK = 0, V6_SPILL = 1, V6_CAPBAD = 3 };
-
-template <int HDR>
-__global__ __launch_bounds__(256) void var_encode_flat6_kernel(VarLaunch L, const Op* __restrict__ prog,
-                                                               const ColumnDev* __restrict__ cols,
-                                                               const FixedFieldDev* __restrict__ fix,
-                                                               const VarFieldDev* __restrict__ vf,
-                                                               const int64_t* __restrict__ offs,
-                                                               uint8_t* __restrict__ out, int64_t capacity,
-                                                               int32_t* status, int cap, int sb, SpillArgs sp) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int NW = 4;
-  const V6Lds o = v6_lds(cap, sb, L.num_var);
-  uint8_t* img = lds;
-  uint8_t* stg = lds + o.stg;
-  int32_t* m_e0 = reinterpret_cast<int32_t*>(lds + o.e0);
-  int32_t* m_nn = reinterpret_cast<int32_t*>(lds + o.nn);
-  int32_t* m_pos = reinterpret_cast<int32_t*>(lds + o.pos);
-  int32_t* m_rowo = reinterpret_cast<int32_t*>(lds + o.rowo);
-  int32_t* m_soff = reinterpret_cast<int32_t*>(lds + o.soff);
-  int64_t* h_b0 = reinterpret_cast<int64_t*>(lds + o.hdr);
-  int32_t* h_i = reinterpret_cast<int32_t*>(lds + o.hdr + 8);  // mis, total, class
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t tiles = (L.num_rows + 63) / 64;
-  const int nfix = L.fix_group[4];
-
-  // ---- M: metadata registers of tile t (wave w: var fields w, w+4, ...; wave 0: bounds)
-  int32_t me0[kV6M], me1[kV6M];
-  uint32_t mvb[kV6M];
-  int64_t mbeg = 0, mend = 0, mB0 = 0, mB1 = 0;
-  auto load_meta = [&](int64_t t) {
-    const int64_t r0 = t * 64;
-    const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
-    const bool lv = lane < rows;
-    const int64_t ii = lv ? r0 + lane : r0;
-    if (wave == 0) {
-      mB0 = offs[r0];
-      mB1 = offs[r0 + rows];
-      mbeg = offs[ii];
-      mend = offs[ii + 1];
-    }
-#pragma unroll
-    for (int k = 0; k < kV6M; ++k) {
-      const int v = wave + NW * k;
-      me0[k] = me1[k] = 0;
-      mvb[k] = 0xffu;
-      if (v < L.num_var) {
-        const VarFieldDev& f = vf[v];
-        const int64_t ie = lv ? ii : r0 + rows;  // dead lanes: an empty payload at the tile's end
-        me0[k] = f.offsets[ie];
-        me1[k] = lv ? f.offsets[ie + 1] : me0[k];
-        mvb[k] = f.validity && lv ? load_byte(f.validity + (ii >> 3)) : 0xffu;
-      }
-    }
-  };
-  // metadata registers -> LDS, then wave 0 classifies the tile and plans the staging
-  auto write_meta = [&](int64_t t) {
-    const int64_t r0 = t * 64;
-    const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
-    const bool lv = lane < rows;
-    const int64_t ii = lv ? r0 + lane : r0;
-#pragma unroll
-    for (int k = 0; k < kV6M; ++k) {
-      const int v = wave + NW * k;
-      if (v < L.num_var) {
-        const bool nul = !((mvb[k] >> (ii & 7)) & 1);
-        m_e0[v * 64 + lane] = me0[k];
-        m_nn[v * 64 + lane] = (me1[k] - me0[k]) | (lv && nul ? (int32_t)0x80000000 : 0);
-      }
-    }
-    if (wave == 0) {
-      const bool ok = !lv || (mbeg >= mB0 && mend >= mbeg && mend <= mB1);
-      const bool sane = __ballot(!ok) == 0 && ((mB0 | mB1) & 3) == 0 && mB1 >= mB0;
-      const bool capbad = lv && (mend > capacity || mbeg < 0 || mend < mbeg);
-      const int mis = (int)(reinterpret_cast<uintptr_t>(out + mB0) & 15);
-      const int64_t total = mis + (mB1 - mB0);
-      int32_t cls = V6_OK;
-      if (__ballot(capbad)) cls = V6_CAPBAD;
-      else if (!sane || (mis & 3) || total > cap) cls = V6_SPILL;
-      m_rowo[lane] = lv ? (int32_t)(mis + (mbeg - mB0)) : -1;
-      if (lane == 0) {
-        *h_b0 = mB0;
-        h_i[0] = mis;
-        h_i[1] = (int32_t)(total < 0x7fffffff ? total : 0x7fffffff);
-        h_i[2] = cls;
-      }
-      if (cls == V6_CAPBAD && capbad) set_status(status, FORY_ERR_CAPACITY);
-    }
-    __syncthreads();
-    // staging plan (lane v of wave 0 = var field v; <= 32 fields): region of field v =
-    // its tile span at the span's 16-byte phase, then its item-validity bytes
-    if (wave == 0 && h_i[2] == V6_OK) {
-      int32_t need = 0, phase = 0, vofs = 0, sa32 = 0;
-      bool stageable = false;
-      if (lane < L.num_var) {
-        const VarFieldDev& f = vf[lane];
-        const int last = rows - 1;
-        const int64_t sa = m_e0[lane * 64];
-        const int64_t se = (int64_t)m_e0[lane * 64 + last] + (m_nn[lane * 64 + last] & 0x7fffffff);
-        const int64_t S = (se - sa) * f.w;
-        phase = (int)(reinterpret_cast<uintptr_t>(f.values + sa * f.w) & 15);
-        vofs = staged_vofs(phase, S);
-        int64_t nd = vofs;
-        if (f.item_validity && se > sa) nd += ((((se + 7) >> 3) - ((sa >> 3) & ~int64_t(3)) + 3) & ~int64_t(3)) + 16;
-        nd = (nd + 16 + 15) & ~int64_t(15);  // funnel-copy slack
-        stageable = (f.iflags & 2) == 0 && S >= 0 && se >= sa && nd <= sb;
-        need = stageable ? (int32_t)nd : 0;
-        sa32 = (int32_t)sa;
-      }
-      int32_t incl = need;  // wave prefix of the regions
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int32_t y = __shfl_up(incl, d);
-        if (lane >= d) incl += y;
-      }
-      const int32_t start = incl - need;
-      if (lane < L.num_var) {
-        m_soff[lane * 4] = stageable && incl <= sb ? start : -1;
-        m_soff[lane * 4 + 1] = phase;
-        m_soff[lane * 4 + 2] = vofs;
-        m_soff[lane * 4 + 3] = sa32;
-      }
-    }
-    __syncthreads();
-  };
-
-  // ---- P: fixed columns -> registers (wave w: table entries w, w+4, ...), spans -> staging
-  uint64_t fv[kV6W];
-  uint32_t fb[kV6W];
-  auto issue_payload = [&](int64_t t) {
-    const int64_t r0 = t * 64;
-    const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
-    const int64_t ii = lane < rows ? r0 + lane : r0;
-#pragma unroll
-    for (int k = 0; k < kV6W; ++k) {
-      const int q = wave + NW * k;
-      fv[k] = 0;
-      fb[k] = 0xffu;
-      if (q < nfix) {
-        const FixedFieldDev& f = fix[q];
-        fv[k] = load_elem(f.values, f.width, ii);
-        if (f.validity) fb[k] = load_byte(f.validity + (ii >> 3));
-      }
-    }
-    if (h_i[2] != V6_OK) return;
-    for (int v = wave; v < L.num_var; v += NW) {
-      const int32_t so = m_soff[v * 4];
-      if (so < 0) continue;
-      const VarFieldDev& f = vf[v];
-      const int last = rows - 1;
-      const int64_t sa = m_e0[v * 64];
-      const int64_t se = (int64_t)m_e0[v * 64 + last] + (m_nn[v * 64 + last] & 0x7fffffff);
-      int ph, vo;
-      flat_stage_span(f, sa, se, lane, stg + so, &ph, &vo);
-    }
-  };
-
-  // ---- A + S for tile t (its metadata in LDS, its payload arrived)
-  auto assemble_store = [&](int64_t t) {
-    const int64_t r0 = t * 64;
-    const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
-    const bool live = lane < rows;
-    const int64_t i = r0 + lane;
-    const int32_t cls = h_i[2];
-    if (cls != V6_OK) {  // the flat kernel's spill launch takes it (big image, or per record)
-      if (cls != V6_CAPBAD && tid == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)t;
-      return;
-    }
-    const int total = h_i[1];
-    const int32_t ro = live ? m_rowo[lane] : 0;
-    uint8_t* fp = img + ro;
-    uint8_t* row = fp + HDR;
-    if (wave == 0 && live) {  // Encoders.encode frame header; BinaryRowWriter.reset zeroes the bitmap
-      const int32_t fl = (lane + 1 < rows ? m_rowo[lane + 1] : total) - ro;
-      if (HDR == 12) {
-        st32(fp, (uint32_t)(fl - 4));
-        st64_lds(fp + 4, (uint64_t)L.schema_hash);
-      } else if (HDR == 8) {
-        st64_lds(fp, (uint64_t)L.schema_hash);
-      }
-      for (int b = 0; b < L.bitmap_bytes; b += 4) st32(row + b, 0);
-      // variable-region layout in field order (writeUnaligned / BinaryArrayWriter.reset)
-      int64_t wi = L.fixed_size;
-      uint8_t* slots = row + L.bitmap_bytes;
-      for (int v = 0; v < L.num_var; ++v) {
-        const VarFieldDev& f = vf[v];
-        const int32_t raw = m_nn[v * 64 + lane];
-        const int64_t nn = raw & 0x7fffffff;
-        uint8_t* slot = slots + 8 * f.slot;
-        int32_t p = -1;
-        if (raw < 0) {
-          set_null_bit(row, f.slot);
-          st64_lds(slot, 0);
-        } else if (!f.is_list) {
-          st64_lds(slot, ((uint64_t)wi << 32) | (uint32_t)nn);
-          p = (int32_t)wi;
-          wi += round8(nn);
-        } else {  // LIST: [i64 n][null bitmap][n * w bytes, padded to 8]
-          const int32_t ahdr = 8 + bitmap_bytes(nn);
-          const int64_t size = ahdr + round8(nn * f.w);
-          st64_lds(row + wi, (uint64_t)nn);
-          for (int b = 8; b < ahdr; b += 4) st32(row + wi + b, 0);
-          st64_lds(slot, ((uint64_t)wi << 32) | (uint32_t)size);
-          p = (int32_t)wi;
-          wi += size;
-        }
-        m_pos[v * 64 + lane] = p;
-      }
-    }
-    // fixed slots (all waves): BinaryRowWriter.write(ordinal, v), null -> 0 (bit set below)
-    uint32_t nullmask = 0;  // fixed fields of this wave whose record is null
-#pragma unroll
-    for (int k = 0; k < kV6W; ++k) {
-      const int q = wave + NW * k;
-      if (q < nfix && live) {
-        const FixedFieldDev& f = fix[q];
-        const bool nul = !((fb[k] >> (i & 7)) & 1);
-        uint64_t x = nul ? 0 : fv[k];
-        if (f.flags & 2) x = x ? 1 : 0;
-        st64_lds(row + L.bitmap_bytes + 8 * f.slot, x);
-        if (nul) nullmask |= 1u << k;
-      }
-    }
-    __syncthreads();  // layout, bitmaps zeroed, fixed slots
-#pragma unroll
-    for (int k = 0; k < kV6W; ++k)
-      if ((nullmask >> k) & 1) {
-        const int s = fix[wave + NW * k].slot;  // BinaryWriter.setNullAt (other waves OR into the same dwords)
-        atomicOr(reinterpret_cast<uint32_t*>(row + ((s >> 5) << 2)), 1u << (s & 31));
-      }
-    for (int q = wave + NW * kV6W; q < nfix; q += NW) {  // beyond the register slots: loaded here
-      if (!live) continue;
-      const FixedFieldDev& f = fix[q];
-      const bool nul = f.validity && !((load_byte(f.validity + (i >> 3)) >> (i & 7)) & 1);
-      uint64_t x = nul ? 0 : load_elem(f.values, f.width, i);
-      if (f.flags & 2) x = x ? 1 : 0;
-      st64_lds(row + L.bitmap_bytes + 8 * f.slot, x);
-      if (nul) atomicOr(reinterpret_cast<uint32_t*>(row + ((f.slot >> 5) << 2)), 1u << (f.slot & 31));
-    }
-    // var payloads: each wave its fields, every record at once (staged spans, or per lane)
-    for (int v = wave; v < L.num_var; v += NW) {
-      const VarFieldDev& f = vf[v];
-      const int32_t so = m_soff[v * 4];
-      const int32_t p = live ? m_pos[v * 64 + lane] : -1;
-      const int64_t e0 = m_e0[v * 64 + lane];
-      const int64_t n = m_nn[v * 64 + lane] & 0x7fffffff;
-      if (p >= 0)
-        flat_place(f, so >= 0, stg + (so >= 0 ? so : 0), m_soff[v * 4 + 1], m_soff[v * 4 + 3], m_soff[v * 4 + 2], p, e0,
-                   n, row);
-    }
-    __syncthreads();  // the image is complete
-  };
-
-  int64_t t = blockIdx.x;
-  if (t >= tiles) return;
-  load_meta(t);
-  write_meta(t);
-  issue_payload(t);
-  for (;;) {
-    const int64_t tn = t + gridDim.x;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t's payload (and the last image's stores)
-    __syncthreads();
-    if (tn < tiles) load_meta(tn);
-    assemble_store(t);  // (ends with a barrier when the tile is assembled)
-    const bool ok = h_i[2] == V6_OK;
-    const int mis_t = h_i[0], total_t = h_i[1];
-    const int64_t b0_t = *h_b0;
-    if (tn < tiles) {
-      __syncthreads();  // every wave read tile t's header
-      write_meta(tn);   // (waits for the metadata; barriers inside)
-      issue_payload(tn);
-    }
-    if (ok) {  // tile t's image leaves while tile tn's loads are in flight
-      uint8_t* g = out + b0_t - mis_t;
-      const int nch = (total_t + 15) >> 4;
-      for (int cc = tid; cc < nch; cc += 64 * NW) {
-        const int lo = cc * 16;
-        if (lo >= mis_t && lo + 16 <= total_t) {
-          *gp(reinterpret_cast<u32x4*>(g + lo)) = *reinterpret_cast<const u32x4*>(img + lo);
-        } else {
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const int oo = lo + 4 * d;
-            if (oo >= mis_t && oo + 4 <= total_t) *gp(reinterpret_cast<uint32_t*>(g + oo)) = ld32(img + oo);
-          }
-        }
-      }
-    }
-    if (tn >= tiles) break;
-    t = tn;
-  }
-}
-
 
 __device__ __forceinline__ int64_t wave_incl_scan64(int64_t x, int lane) {
 #pragma unroll
@@ -2766,39 +2434,6 @@ void launch_flat_dec(const VarLaunch& L0, const uint8_t* rows, const int64_t* of
                      L.vf, L.st, rows, offs, tile_tot, status, sp.cap, sp);
 }
 
-// Encode v6 launch: staging for 1.25 x a tile's mean var payload (+ per-field
-// alignment slack), persistent grid at the kernel's residency; tiles over the image
-// go to the flat kernel's big-image spill launch.
-template <int HDR>
-void launch_flat_enc6(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
-                      int cap, hipStream_t s) {
-  VarLaunch L = L0;
-  L.pl_all = 1;
-  auto* k = &var_encode_flat6_kernel<HDR>;
-  raise_lds_cap(k);
-  const int64_t var_row = capacity / L.num_rows - L.fixed_size - frame_header_bytes(L.frame);
-  int64_t sb = 64 * (var_row > 0 ? var_row : 0) * 5 / 4 + 48LL * L.num_var + 256;
-  sb = sb < 2048 ? 2048 : (sb > 48 * 1024 ? 48 * 1024 : sb);
-  sb = (sb + 255) & ~int64_t(255);
-  const V6Lds o = v6_lds(cap, (int)sb, L.num_var);
-  const SpillArgs sp = spill_args(L, cap);
-  (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
-  const int64_t tiles = (L.num_rows + 63) / 64;
-  const int64_t grid = persistent_grid(k, (size_t)o.total, tiles, 256);
-  if (L.kn.diag)
-    fprintf(stderr, "[fory_rowfmt] encode v6: image %d B, staging %d B, LDS %d B, %d workgroups/CU, grid %lld\n", cap,
-            (int)sb, o.total, occupancy_of(k, 256, (size_t)o.total), (long long)grid);
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(256), (size_t)o.total, s, L, L.prog, L.cols, L.fix, L.vf, offs, out,
-                     capacity, status, cap, (int)sb, sp);
-  auto* kd = &var_encode_flat_kernel<HDR, kNW, false, false>;
-  L.stg_bytes = enc_stg_bytes(kd, L, capacity, cap, kNW);
-  auto* k2 = &var_encode_flat_kernel<HDR, kNW, false, true>;
-  raise_lds_cap(k2);
-  hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds_enc(L, sp.cap, kNW), 64 * kNW)), dim3(64 * kNW),
-                     flat_lds_enc(L, sp.cap, kNW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status,
-                     sp.cap, sp);
-}
-
 // Encode: the caller's capacity (normally encoded_size's total) gives the mean
 // row size for free (fit_cap).
 int enc_cap(const VarLaunch& L, int64_t capacity) {
@@ -2851,16 +2486,6 @@ hipError_t launch_var_decode_pass(const VarLaunch& L, const uint8_t* rows, const
 hipError_t launch_var_encode(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity,
                              int32_t* status, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
-  if (var_tiles(L) && var_flat(L) && L.num_struct == 0 && L.num_var <= 4 * kV6M && !L.kn.no_enc6 &&
-      L.num_rows >= 64) {
-    const int cap = enc_cap(L, capacity);
-    switch (frame_header_bytes(L.frame)) {
-      case 12: launch_flat_enc6<12>(L, offs, out, capacity, status, cap, s); break;
-      case 8: launch_flat_enc6<8>(L, offs, out, capacity, status, cap, s); break;
-      default: launch_flat_enc6<0>(L, offs, out, capacity, status, cap, s); break;
-    }
-    return hipGetLastError();
-  }
   if (var_tiles(L) && var_flat(L)) {
     const int cap = enc_cap(L, capacity);
     if (flat_waves(L) == 2) {

@@ -113,6 +113,12 @@ def copy_path(a, nbytes=None):
     return f(a.ctypes.data, a.nbytes if nbytes is None else nbytes)
 
 
+def first_byte_pinned(a):
+    import ctypes
+    f = _internal("fory_rowfmt_internal_host_first_byte_pinned", ctypes.c_int, [ctypes.c_void_p])
+    return f(a.ctypes.data)
+
+
 def staged_pieces(hp):
     import ctypes
     f = _internal("fory_rowfmt_internal_host_staged_pieces", ctypes.c_int64, [ctypes.c_void_p])
@@ -133,6 +139,9 @@ def test_host_copy_classification_is_by_whole_range():
         assert copy_path(head) == 1
         assert copy_path(head[4096:]) == 1  # inside the registration
         assert copy_path(buf) == 0  # starts inside, runs past the end: staged, never a direct DMA
+        # round 2's rule judged the same range by its first byte: "pinned" -> an async DMA
+        # over host pages the device has no mapping for (the fault mechanism)
+        assert first_byte_pinned(buf) == 1
         assert copy_path(buf[(32 << 10) - 8:]) == 0  # the last 8 registered bytes + pageable ones
         assert copy_path(buf[32 << 10:]) == 0  # wholly past it
     finally:

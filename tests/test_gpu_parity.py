@@ -43,27 +43,21 @@ VARLEN = [k for k, (sch, _) in catalog().items()
 FIXED = [k for k in catalog() if k not in VARLEN]
 
 
-@pytest.fixture(params=["flat", "flat_stg256", "tile", "global", "spill", "nocap", "tile_nocap", "waves2", "waves4",
-                        "enc6off", "enc6_spill"])
+@pytest.fixture(params=["flat", "flat_stg256", "tile", "global", "spill", "nocap", "tile_nocap", "waves2", "waves4"])
 def varlen_engine(request, monkeypatch):
     """Varlen engines: flat cooperative tile kernels (default for flat plans), the
     generic one-wave tile interpreter (FORY_ROWFMT_VARFLAT=0), the per-record global
     interpreter (FORY_ROWFMT_VARTILE=0); a 2 KiB LDS image so tiles spill to the second
     (big-image) launch; 2 KiB for both launches so tiles take the per-record global path
     inside the tile kernels (flat and generic); flat with a 256-byte staging buffer
-    (most spans take the per-lane copy); cooperative tiles of 2 / 4 waves forced; the
-    round-2 flat encode kernel instead of encode v6 (flat plans without structs use v6 by
-    default); v6 with a 4 KiB image so most tiles go to the spill launch, and some of
-    those on to the per-record path."""
+    (most spans take the per-lane copy); cooperative tiles of 2 / 4 waves forced."""
     env = {"flat": {}, "flat_stg256": {"FORY_ROWFMT_VARSTG": "256"},
            "tile": {"FORY_ROWFMT_VARFLAT": "0"}, "global": {"FORY_ROWFMT_VARTILE": "0"},
            "spill": {"FORY_ROWFMT_VARCAP": "2048"},
            "nocap": {"FORY_ROWFMT_VARCAP": "2048", "FORY_ROWFMT_SPILLCAP": "2048"},
            "tile_nocap": {"FORY_ROWFMT_VARFLAT": "0", "FORY_ROWFMT_VARCAP": "2048",
                           "FORY_ROWFMT_SPILLCAP": "2048"},
-           "waves2": {"FORY_ROWFMT_VARNW": "2"}, "waves4": {"FORY_ROWFMT_VARNW": "4"},
-           "enc6off": {"FORY_ROWFMT_ENC6": "0"},
-           "enc6_spill": {"FORY_ROWFMT_VARCAP": "4096", "FORY_ROWFMT_SPILLCAP": "8192"}}[request.param]
+           "waves2": {"FORY_ROWFMT_VARNW": "2"}, "waves4": {"FORY_ROWFMT_VARNW": "4"}}[request.param]
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     return request.param
