@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <algorithm>
 #include <cstring>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <string>
@@ -23,8 +24,19 @@ using fory_amd::ColumnDev;
 using fory_amd::FixedFieldDev;
 using fory_amd::Plan;
 
+// Columnar tree engine layout of a plan (treecol.hip): var nodes by depth.
+struct TcInfo {
+  bool ok = false;                  // generic plan of <= kTcMaxNodes nodes
+  std::vector<fory_amd::TcVar> var;  // by depth, pre-order within a depth
+  std::vector<int32_t> vidx;        // node -> var index (-1: scalar)
+  std::vector<int32_t> parent;      // node -> parent node (-1: the row)
+  std::vector<int32_t> phase;       // [0, end of depth 1, ..., end of the last depth]
+};
+
 struct fory_plan {
   Plan p;
+  TcInfo tc;
+  uint64_t id = 0;  // unique per plan_create (the encode memo's key; addresses are reused)
 };
 
 namespace fory_amd {
@@ -72,8 +84,13 @@ bool use_tiled(const Plan& p, int frame) {
   return p.fixed_width && fory_amd::fixed_tiled_supported(p.fixed_size + fory_amd::frame_header_bytes(frame));
 }
 
+void tc_forget(const void* ws);
+
+// keep_memo: encode may reuse the columnar sizes its encoded_size left in the workspace;
+// every other call may overwrite them.
 int check_common(const fory_plan* plan, const fory_column* cols, int64_t n, int frame,
-                 void* ws, int64_t ws_bytes) {
+                 void* ws, int64_t ws_bytes, bool keep_memo = false) {
+  if (!keep_memo) tc_forget(ws);
   if (!plan) return fail(FORY_ERR_INVALID_ARGUMENT, "plan is null");
   if (n < 0) return fail(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
   if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM && frame != FORY_FRAME_COLLECTION &&
@@ -546,6 +563,172 @@ int prepare_gen(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   return FORY_OK;
 }
 
+// --- columnar tree engine (treecol.hip) -------------------------------------
+bool tc_var_kind(int k) { return k != fory_amd::KIND_FIXED && k != fory_amd::KIND_BOOL; }
+
+void build_tc(fory_plan* plan) {
+  const Plan& p = plan->p;
+  TcInfo& t = plan->tc;
+  const int N = (int)p.nodes.size();
+  t.ok = p.generic && N > 0 && N <= fory_amd::kTcMaxNodes;
+  if (!t.ok) return;
+  t.parent.assign(N, -1);
+  for (int i = 0; i < N; ++i)
+    for (int32_t ch : p.nodes[i].children) t.parent[ch] = i;
+  std::vector<int32_t> depth(N, 1);
+  int maxd = 0;
+  for (int i = 0; i < N; ++i) {  // pre-order: parents first
+    depth[i] = t.parent[i] < 0 ? 1 : depth[t.parent[i]] + 1;
+    if (tc_var_kind(p.nodes[i].kind)) maxd = std::max(maxd, depth[i]);
+  }
+  t.vidx.assign(N, -1);
+  t.var.clear();
+  t.phase.assign(1, 0);
+  for (int d = 1; d <= maxd; ++d) {
+    for (int i = 0; i < N; ++i) {
+      if (depth[i] != d || !tc_var_kind(p.nodes[i].kind)) continue;
+      fory_amd::TcVar v{};
+      v.node = i;
+      const int par = t.parent[i];
+      v.parent = par < 0 ? -1 : t.vidx[par];
+      v.items = par >= 0 && p.nodes[par].kind != fory_amd::KIND_STRUCT;
+      v.depth = d;
+      t.vidx[i] = (int32_t)t.var.size();
+      t.var.push_back(v);
+    }
+    t.phase.push_back((int32_t)t.var.size());
+  }
+}
+
+// Instances of every node in this call: the rows at the top, a struct's children share
+// its instances, items / keys / values are their column's length.
+std::vector<int64_t> tc_domains(const fory_plan* plan, const fory_column* cols, int64_t n) {
+  const TcInfo& t = plan->tc;
+  const int N = (int)plan->p.nodes.size();
+  std::vector<int64_t> m(N, 0);
+  for (int i = 0; i < N; ++i) {
+    const int par = t.parent[i];
+    if (par < 0) m[i] = n;
+    else if (plan->p.nodes[par].kind == fory_amd::KIND_STRUCT) m[i] = m[par];
+    else m[i] = cols[i].length < 0 ? 0 : cols[i].length;
+  }
+  return m;
+}
+
+// Workspace after fory_rowfmt_workspace_bytes: the tables, item-scan partials, A arrays.
+int64_t tc_bytes(const fory_plan* plan, const std::vector<int64_t>& m) {
+  const TcInfo& t = plan->tc;
+  int64_t maxm = 0, arrays = 0;
+  for (const fory_amd::TcVar& v : t.var) {
+    arrays += align_up((m[v.node] + 1) * 8);
+    if (v.items) maxm = std::max(maxm, m[v.node]);
+  }
+  return align_up((int64_t)sizeof(fory_amd::TcTables)) + align_up((fory_amd::scan_partials(maxm) + 2) * 8) + arrays;
+}
+
+bool tc_usable(const fory_plan* plan, const fory_column* cols, int64_t n, int64_t ws_bytes, int64_t* need) {
+  if (!plan->tc.ok || !plan->p.kn.tree_col || n <= 0 || !cols) return false;
+  const int64_t w = fory_rowfmt_workspace_bytes(plan, n) + tc_bytes(plan, tc_domains(plan, cols, n));
+  if (need) *need = w;
+  return ws_bytes >= w;
+}
+
+// Sizes of the last columnar encoded_size per workspace: encode reuses them when the
+// plan, columns, rows and framing are the same and no other call used the workspace.
+struct TcMemo {
+  const void* ws = nullptr;
+  uint64_t plan = 0, sig = 0;
+};
+std::mutex g_tc_mu;
+TcMemo g_tc_memo[16];
+int g_tc_next = 0;
+
+uint64_t tc_signature(const fory_plan* plan, const fory_column* cols, int64_t n, int frame) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](uint64_t x) {
+    for (int b = 0; b < 8; ++b) h = (h ^ ((x >> (8 * b)) & 0xff)) * 1099511628211ull;
+  };
+  mix(plan->id);
+  mix((uint64_t)n);
+  mix((uint64_t)frame);
+  for (size_t i = 0; i < plan->p.nodes.size(); ++i) {
+    mix(reinterpret_cast<uintptr_t>(cols[i].values));
+    mix(reinterpret_cast<uintptr_t>(cols[i].offsets));
+    mix(reinterpret_cast<uintptr_t>(cols[i].validity));
+    mix((uint64_t)cols[i].length);
+  }
+  return h;
+}
+
+void tc_forget(const void* ws) {
+  if (!ws) return;
+  std::lock_guard<std::mutex> lock(g_tc_mu);
+  for (TcMemo& e : g_tc_memo)
+    if (e.ws == ws) e = TcMemo{};
+}
+
+void tc_remember(const void* ws, uint64_t plan, uint64_t sig) {
+  std::lock_guard<std::mutex> lock(g_tc_mu);
+  TcMemo* slot = nullptr;
+  for (TcMemo& e : g_tc_memo)
+    if (e.ws == ws) slot = &e;
+  if (!slot) slot = &g_tc_memo[g_tc_next++ & 15];
+  *slot = TcMemo{ws, plan, sig};
+}
+
+bool tc_recall(const void* ws, uint64_t plan, uint64_t sig) {
+  std::lock_guard<std::mutex> lock(g_tc_mu);
+  for (const TcMemo& e : g_tc_memo)
+    if (e.ws == ws && e.plan == plan && e.sig == sig) return true;
+  return false;
+}
+
+// Tables of a columnar call into the workspace (after the per-lane engine's region).
+int tc_prepare(const fory_plan* plan, const fory_column* cols, int64_t n, void* ws, hipStream_t s,
+               fory_amd::TcTables* T, const fory_amd::TcTables** dT, int64_t** partials) {
+  const TcInfo& t = plan->tc;
+  const std::vector<int64_t> m = tc_domains(plan, cols, n);
+  uint8_t* base = static_cast<uint8_t*>(ws) + fory_rowfmt_workspace_bytes(plan, n);
+  std::memset(T, 0, sizeof(*T));
+  int64_t maxm = 0;
+  for (const fory_amd::TcVar& v : t.var)
+    if (v.items) maxm = std::max(maxm, m[v.node]);
+  uint8_t* at = base + align_up((int64_t)sizeof(fory_amd::TcTables));
+  *partials = reinterpret_cast<int64_t*>(at);
+  at += align_up((fory_amd::scan_partials(maxm) + 2) * 8);
+  for (size_t i = 0; i < m.size(); ++i) {
+    T->m[i] = m[i];
+    T->vidx[i] = t.vidx[i];
+  }
+  for (size_t v = 0; v < t.var.size(); ++v) {
+    T->var[v] = t.var[v];
+    T->A[t.var[v].node] = reinterpret_cast<int64_t*>(at);
+    at += align_up((m[t.var[v].node] + 1) * 8);
+  }
+  for (size_t d = 0; d < t.phase.size(); ++d) T->phase[d] = t.phase[d];
+  T->nvar = (int32_t)t.var.size();
+  T->depths = (int32_t)t.phase.size() - 1;
+  *dT = reinterpret_cast<const fory_amd::TcTables*>(base);
+  return upload(base, T, (int64_t)sizeof(*T), s);
+}
+
+// Bottom-up sizes of every var node (children before parents), item nodes scanned.
+int tc_sizes(const fory_plan* plan, const fory_amd::GenLaunch& G, const fory_amd::TcTables& T,
+             const fory_amd::TcTables* dT, int64_t* partials, hipStream_t s) {
+  const TcInfo& t = plan->tc;
+  for (int v = (int)t.var.size() - 1; v >= 0; --v) {  // deepest first
+    const fory_amd::TcVar& tv = t.var[(size_t)v];
+    const int64_t m = T.m[tv.node];
+    hipError_t e = fory_amd::launch_tc_sizes(G, dT, tv.node, m, G.frame == FORY_FRAME_COLLECTION && tv.node == 0, s);
+    if (e != hipSuccess) return hip_fail(e, "tc_sizes");
+    if (!tv.items) continue;
+    e = m > 0 ? fory_amd::launch_scan_i64(T.A[tv.node], m, partials, s)
+              : hipMemsetAsync(T.A[tv.node], 0, sizeof(int64_t), s);
+    if (e != hipSuccess) return hip_fail(e, "tc_scan");
+  }
+  return FORY_OK;
+}
+
 int64_t* elem_partials_ptr(const Plan& p, void* ws, int64_t n) {
   return reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(spill_ptr(p, ws, n)) +
                                     align_up(fory_amd::var_spill_words(n) * 4));
@@ -627,6 +810,9 @@ int fory_rowfmt_plan_create(const fory_field_desc* fields, int32_t num_desc, for
     return fail(FORY_ERR_UNSUPPORTED, "device path supports struct nesting depth <= 8");
   }
   plan->p.kn = fory_amd::knobs_from_env();  // launch knobs fixed for the plan's life
+  build_tc(plan);
+  static std::atomic<uint64_t> next_id{1};
+  plan->id = next_id++;
   *out_plan = plan;
   return FORY_OK;
 }
@@ -654,6 +840,13 @@ int64_t fory_rowfmt_workspace_bytes(const fory_plan* plan, int64_t num_rows) {
          align_up(fory_amd::var_spill_words(n) * 4) + align_up(elem_partials_words(plan->p, n) * 8);
 }
 
+int64_t fory_rowfmt_encode_workspace_bytes(const fory_plan* plan, const fory_column* cols, int64_t num_rows) {
+  if (!plan) return -1;
+  const int64_t base = fory_rowfmt_workspace_bytes(plan, num_rows);
+  if (!plan->tc.ok || !plan->p.kn.tree_col || num_rows <= 0 || !cols) return base;
+  return base + tc_bytes(plan, tc_domains(plan, cols, num_rows));
+}
+
 int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols, int64_t num_rows,
                              int32_t frame_mode, int64_t* d_row_offsets, void* d_workspace,
                              int64_t workspace_bytes, void* stream) {
@@ -675,6 +868,20 @@ int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols, int
     fory_amd::GenLaunch G{};
     rc = prepare_gen(p, cols, num_rows, frame_mode, d_workspace, s, &G, 1 << 20);
     if (rc) return rc;
+    if (tc_usable(plan, cols, num_rows, workspace_bytes, nullptr)) {  // columnar: node sizes, then the rows
+      fory_amd::TcTables T;
+      const fory_amd::TcTables* dT = nullptr;
+      int64_t* tpart = nullptr;
+      rc = tc_prepare(plan, cols, num_rows, d_workspace, s, &T, &dT, &tpart);
+      if (!rc) rc = tc_sizes(plan, G, T, dT, tpart, s);
+      if (rc) return rc;
+      e = fory_amd::launch_tc_rows(G, dT, d_row_offsets, s);
+      if (e != hipSuccess) return hip_fail(e, "tc_rows");
+      e = fory_amd::launch_scan_i64(d_row_offsets, num_rows, partials_ptr(p, d_workspace), s);
+      if (e != hipSuccess) return hip_fail(e, "scan");
+      tc_remember(d_workspace, plan->id, tc_signature(plan, cols, num_rows, frame_mode));
+      return FORY_OK;
+    }
     e = fory_amd::launch_gen_sizes(G, d_row_offsets, s);
     if (e != hipSuccess) return hip_fail(e, "gen_sizes");
     e = fory_amd::launch_scan_i64(d_row_offsets, num_rows, partials_ptr(p, d_workspace), s);
@@ -693,8 +900,9 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
                        int32_t frame_mode, const int64_t* d_row_offsets, void* d_out,
                        int64_t out_capacity, int32_t* d_status, void* d_workspace,
                        int64_t workspace_bytes, void* stream) {
-  int rc = check_common(plan, cols, num_rows, frame_mode, d_workspace, workspace_bytes);
+  int rc = check_common(plan, cols, num_rows, frame_mode, d_workspace, workspace_bytes, true);
   if (rc) return rc;
+  if (!plan->p.generic || !tc_usable(plan, cols, num_rows, workspace_bytes, nullptr)) tc_forget(d_workspace);
   if (num_rows == 0) return FORY_OK;
   if (!d_out) return fail(FORY_ERR_INVALID_ARGUMENT, "d_out is null");
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -724,6 +932,28 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
     fory_amd::GenLaunch G{};
     rc = prepare_gen(p, cols, num_rows, frame_mode, d_workspace, s, &G, 1 << 20);
     if (rc) return rc;
+    if (tc_usable(plan, cols, num_rows, workspace_bytes, nullptr) && !(reinterpret_cast<uintptr_t>(d_out) & 3)) {
+      fory_amd::TcTables T;
+      fory_amd::TcLaunch W{};
+      int64_t* tpart = nullptr;
+      const uint64_t sig = tc_signature(plan, cols, num_rows, frame_mode);
+      rc = tc_prepare(plan, cols, num_rows, d_workspace, s, &T, &W.T, &tpart);
+      if (!rc && !tc_recall(d_workspace, plan->id, sig)) {  // sizes not left by encoded_size
+        rc = tc_sizes(plan, G, T, W.T, tpart, s);
+        if (!rc) tc_remember(d_workspace, plan->id, sig);
+      }
+      if (rc) return rc;
+      // rows per tile: about half the LDS image at the mean row size (out_capacity bounds
+      // the total), and half the position table at the mean instances per row
+      int64_t inst = 0;
+      for (const fory_amd::TcVar& v : plan->tc.var) inst += T.m[v.node];
+      const int64_t mean = std::max<int64_t>(8, out_capacity / num_rows);
+      const int64_t per_row = std::max<int64_t>(1, inst / num_rows);
+      W.tile_rows = std::max<int64_t>(1, std::min<int64_t>({fory_amd::kTcImg / 2 / mean, fory_amd::kTcPl / 2 / per_row, 1024}));
+      W.g = G;
+      e = fory_amd::launch_tc_encode(W, d_row_offsets, static_cast<uint8_t*>(d_out), out_capacity, d_status, s);
+      return e == hipSuccess ? FORY_OK : hip_fail(e, "tc_encode");
+    }
     e = fory_amd::launch_gen_encode(G, d_row_offsets, static_cast<uint8_t*>(d_out), out_capacity, d_status, s);
     return e == hipSuccess ? FORY_OK : hip_fail(e, "gen_encode");
   }
@@ -878,6 +1108,7 @@ int64_t fory_rowfmt_index_workspace_bytes(const fory_plan* plan, int64_t num_row
 int fory_rowfmt_index_frames(const fory_plan* plan, const void* d_rows, int64_t rows_bytes, int64_t num_rows,
                              int32_t frame_mode, int64_t* d_row_offsets, int32_t* d_status, void* d_workspace,
                              int64_t workspace_bytes, void* stream) {
+  tc_forget(d_workspace);
   if (!plan) return fail(FORY_ERR_INVALID_ARGUMENT, "plan is null");
   if (num_rows < 0 || rows_bytes < 0) return fail(FORY_ERR_INVALID_ARGUMENT, "num_rows or rows_bytes < 0");
   if (frame_mode == FORY_FRAME_RAW)

@@ -131,6 +131,41 @@ hipError_t launch_gen_encode(const GenLaunch& L, const int64_t* offs, uint8_t* o
 hipError_t launch_gen_decode(const GenLaunch& L, const uint8_t* rows, const int64_t* offs, int32_t* status,
                              hipStream_t s);
 
+// Columnar tree engine (treecol.hip): the tree engine's encode as per-node passes over
+// instance columns. An instance is one element of a schema node's column (a row of a
+// top-level field, a struct child of an instance, a list item / map entry). Sizes go
+// bottom-up (A[c][j] = bytes instance j of var node c adds to its parent; item nodes
+// are scanned in place, A[x][m] = total), then tiles of rows write their bytes into an
+// LDS image: each instance writes its own fixed part and hands its var children their
+// positions, phase by phase down the tree.
+constexpr int kTcMaxNodes = 128;  // plans with more nodes keep the per-lane engine
+struct TcVar {
+  int32_t node;    // schema node (column index)
+  int32_t parent;  // var index of the parent (-1: the row)
+  int32_t items;   // 1: the parent is a list / map and this node its items / keys / values
+  int32_t depth;   // 1 + the parent's depth (top-level fields: 1)
+};
+struct TcTables {               // device, in the workspace
+  int64_t* A[kTcMaxNodes];      // var nodes: sizes (items: exclusive prefix, total at [m]); else null
+  int64_t m[kTcMaxNodes];       // instances of each node in this call
+  int32_t vidx[kTcMaxNodes];    // node -> var index, -1 for scalars
+  TcVar var[kTcMaxNodes];       // var nodes by depth, pre-order within a depth
+  int32_t phase[kTcMaxNodes + 1];  // var indices of depth d: [phase[d - 1], phase[d]), phase[0] = 0
+  int32_t nvar, depths;
+};
+struct TcLaunch {
+  GenLaunch g;
+  const TcTables* T;   // device
+  int64_t tile_rows;   // rows per workgroup tile
+};
+// LDS image and position-table capacity of one tile (bytes, entries).
+constexpr int kTcImg = 32768;
+constexpr int kTcPl = 4096;
+hipError_t launch_tc_sizes(const GenLaunch& L, const TcTables* T, int node, int64_t m, bool root_coll, hipStream_t s);
+hipError_t launch_tc_rows(const GenLaunch& L, const TcTables* T, int64_t* sizes, hipStream_t s);
+hipError_t launch_tc_encode(const TcLaunch& W, const int64_t* offs, uint8_t* out, int64_t capacity,
+                            int32_t* status, hipStream_t s);
+
 // Frame index of a STREAM batch (frames.hip): the starts of the first num_rows
 // frames of rows_bytes bytes, found on the device from the stream alone.
 struct FrameIndexLaunch {

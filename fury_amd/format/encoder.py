@@ -69,9 +69,9 @@ class RowEncoder:
     def schema_hash(self) -> int:
         return self.plan.schema_hash
 
-    def workspace(self, n: int):
+    def workspace(self, n: int, cols=None):
         import torch
-        need = max(256, self.plan.workspace_bytes(n))
+        need = max(256, self.plan.workspace_bytes(n) if cols is None else self.plan.encode_workspace_bytes(cols, n))
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self._ws
@@ -81,8 +81,8 @@ class RowEncoder:
                frame_mode: int = FRAME_STREAM) -> EncodedRows:
         import torch
         p = self.plan
-        ws = self.workspace(num_rows)
         arr = native.column_array(columns)
+        ws = self.workspace(num_rows, arr)
         status = torch.zeros(1, dtype=torch.int32, device=self.device)
         if p.fixed_width:
             stride = p.stride(frame_mode)

@@ -69,6 +69,10 @@ class NativePlan:
     def workspace_bytes(self, num_rows: int) -> int:
         return int(_lib.load().fory_rowfmt_workspace_bytes(self.handle, num_rows))
 
+    def encode_workspace_bytes(self, cols, num_rows: int) -> int:
+        """Workspace for encode through the columnar tree engine (cols: column_array)."""
+        return int(_lib.load().fory_rowfmt_encode_workspace_bytes(self.handle, cols, num_rows))
+
 
 @dataclass
 class DeviceColumn:

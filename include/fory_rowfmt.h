@@ -173,6 +173,19 @@ int fory_rowfmt_plan_info(const fory_plan* plan, fory_plan_info* out_info);
 /* Device workspace (bytes) every call below needs for `num_rows` rows. */
 int64_t fory_rowfmt_workspace_bytes(const fory_plan* plan, int64_t num_rows);
 
+/* Workspace (bytes, >= fory_rowfmt_workspace_bytes) with which encoded_size / encode
+ * of these columns take the columnar tree engine: plans with list / map nesting beyond
+ * the op programs (BaseBinaryEncoderBuilder.serializeFor's arrays and maps,
+ * :236-351 / :370-427) are sized node by node and written tile by tile, with per-node
+ * temporaries of each column's element count (fory_column.length of list items and map
+ * keys / values: their offsets must lie in [0, length]). A smaller workspace keeps the
+ * per-record engine; the bytes are identical. encode reuses the sizes the preceding
+ * encoded_size of the same plan, columns, rows and framing left in the workspace (any
+ * other call with that workspace discards them), so the columns must not change in
+ * between. Equals fory_rowfmt_workspace_bytes for every other plan. */
+int64_t fory_rowfmt_encode_workspace_bytes(const fory_plan* plan, const fory_column* cols,
+                                           int64_t num_rows);
+
 /* --- encode: replaces N x { writer.reset(); GeneratedRowEncoder.toRow(obj) }
  *     (Encoders.java:92-95 / 213-225, RowEncoderBuilder.java:177-208).
  *

@@ -56,10 +56,16 @@ def check(schema, enc, cols, n, frame):
 NAMES = list(nested_schemas())
 
 
+@pytest.mark.parametrize("engine", ["columnar", "per_lane"])
 @pytest.mark.parametrize("frame", [0, 1, 3])
 @pytest.mark.parametrize("n", [0, 1, 65, 700])
 @pytest.mark.parametrize("name", NAMES)
-def test_nested_parity(name, n, frame):
+def test_nested_parity(name, n, frame, engine, monkeypatch):
+    """Both encode engines: the columnar one (treecol.hip, the default when the
+    workspace is sized by encode_workspace_bytes) and the per-record one
+    (FORY_ROWFMT_TREECOL=0)."""
+    if engine == "per_lane":
+        monkeypatch.setenv("FORY_ROWFMT_TREECOL", "0")
     if name == "chain" and n > 65:
         n = 120  # ~20 KiB per record
     schema, cols = nested_columns(name, n, 100 + n + frame)

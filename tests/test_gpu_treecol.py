@@ -1,0 +1,175 @@
+"""GPU: the columnar tree engine (fury_amd/csrc/treecol.hip) at its edges.
+
+Nested shapes are sized node by node and written by tiles of rows through an LDS
+image; these tests take it where its tiles and tables run out — rows bigger than the
+image and tiles with more instances than the position table (the per-record engine
+encodes those tiles), collection frames, the workspace contract (encode_workspace_bytes
+vs workspace_bytes) and the sizes encode reuses from encoded_size (and must not reuse
+after another call wrote the workspace). Every output is compared byte for byte with the
+oracle (oracle/rowfmt_oracle.c, BaseBinaryEncoderBuilder.serializeFor's layout).
+"""
+from typing import Dict, List
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import oracle  # noqa: E402
+from fury_amd.format import errors, native  # noqa: E402
+from fury_amd.format.columns import build_columns, to_device  # noqa: E402
+from fury_amd.format.encoder import CollectionEncoder, RowEncoder  # noqa: E402
+from fury_amd.format.types import DataTypes, Schema  # noqa: E402
+from fury_amd.format import infer as I  # noqa: E402
+
+from helpers import nested_columns, nested_schemas, random_rows, reference_beans  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_equal(schema, cols, n, frame, rows):
+    expect, offs = oracle.encode(schema, cols, n, frame)
+    got = rows.buffer.cpu().numpy()
+    assert got.nbytes == expect.nbytes
+    bad = np.nonzero(got != expect)[0]
+    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+    assert np.array_equal(rows.offsets.cpu().numpy(), offs)
+
+
+def _big_rows_schema():
+    return I.infer_schema(type("Big", (), {"__annotations__": {
+        "id": I.jint, "names": List[I.String], "grid": List[List[I.jshort]], "tag": I.String}}))
+
+
+@pytest.mark.parametrize("frame", [0, 1, 3])
+def test_rows_larger_than_the_tile_image(frame):
+    """A few rows of ~100 KiB (3000 strings) among small ones: their tiles take the
+    per-record engine, the others the LDS image; one output, oracle bytes."""
+    schema = _big_rows_schema()
+    rng = np.random.default_rng(1)
+    rows = []
+    for i in range(600):
+        big = i % 97 == 5
+        k = 3000 if big else int(rng.integers(0, 4))
+        rows.append({"id": i, "names": [("s%d" % j) * int(rng.integers(1, 8)) for j in range(k)],
+                     "grid": [[int(x) for x in rng.integers(-9, 9, size=int(rng.integers(0, 4)))]
+                              for _ in range(int(rng.integers(0, 3)))],
+                     "tag": None if i % 5 == 0 else "t%d" % i})
+    cols = build_columns(schema, rows)
+    enc = RowEncoder(schema)
+    oracle_equal(schema, cols, len(rows), frame, enc.encode(to_device(cols), len(rows), frame))
+
+
+def test_tiles_with_more_instances_than_the_position_table():
+    """Rows of ~6000 short lists each (more instances than one tile's position table)."""
+    schema = _big_rows_schema()
+    rows = [{"id": i, "names": [], "grid": [[i % 7] for _ in range(6000 if i % 3 == 0 else 2)], "tag": "x"}
+            for i in range(40)]
+    cols = build_columns(schema, rows)
+    enc = RowEncoder(schema)
+    oracle_equal(schema, cols, len(rows), 1, enc.encode(to_device(cols), len(rows), 1))
+
+
+def test_collection_frames_columnar():
+    """ArrayEncoder / MapEncoder frames of nested collections (List<List<String>>,
+    Map<String, List<Bar>>) at 3000 records."""
+    B = reference_beans()
+    for schema in (
+        Schema([DataTypes.array_field("", I._infer_field("item", List[I.String], []))]),
+        Schema([DataTypes.map_field("", type(k := I._infer_field("key", I.String, []))(k.name, k.type, False, k.children),
+                                    I._infer_field("value", List[B["Bar"]], []))]),
+    ):
+        enc = CollectionEncoder(schema)
+        rows = random_rows(schema, 3000, 7)
+        for r in rows:  # collection frames encode a null collection from its (empty) offsets
+            if r[""] is None:
+                r[""] = []
+        cols = build_columns(schema, rows)
+        oracle_equal(schema, cols, 3000, 2, enc.encode(to_device(cols), 3000))
+
+
+def _native_encode(enc, dcols, n, frame, ws, offs_from=None):
+    p = enc.plan
+    arr = native.column_array(dcols)
+    offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    if offs_from is None:
+        native.encoded_size(p, arr, n, frame, offs, ws)
+    else:
+        offs.copy_(offs_from)
+    total = int(offs[n].item())
+    out = torch.empty(max(16, total), dtype=torch.uint8, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    native.encode(p, arr, n, frame, offs, out, status, ws)
+    native.read_status(status)
+    return out[:total], offs
+
+
+@pytest.mark.parametrize("name", ["holder", "bean_a", "maps_nested"])
+def test_workspace_contract_selects_the_engine(name):
+    """workspace_bytes keeps the per-record engine, encode_workspace_bytes enables the
+    columnar one (larger: per-node temporaries); both give the oracle's bytes."""
+    schema, cols = nested_columns(name, 900, 3)
+    enc = RowEncoder(schema)
+    dcols = to_device(cols)
+    arr = native.column_array(dcols)
+    small, big = enc.plan.workspace_bytes(900), enc.plan.encode_workspace_bytes(arr, 900)
+    assert big > small
+    expect, offs = oracle.encode(schema, cols, 900, 1)
+    for nbytes in (small, big):
+        ws = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        out, got_offs = _native_encode(enc, dcols, 900, 1, ws)
+        assert np.array_equal(out.cpu().numpy(), expect)
+        assert np.array_equal(got_offs.cpu().numpy(), offs)
+
+
+def test_encode_does_not_reuse_sizes_another_call_overwrote():
+    """encoded_size(A); encoded_size(B) on the same workspace; encode(A) with A's
+    offsets: the sizes in the workspace are B's, so encode recomputes A's. Likewise
+    after a decode wrote the workspace."""
+    schema = nested_schemas()["holder"]
+    enc = RowEncoder(schema)
+    _, ca = nested_columns("holder", 500, 11)
+    _, cb = nested_columns("holder", 500, 12)
+    da, db = to_device(ca), to_device(cb)
+    arr_a = native.column_array(da)
+    ws = torch.empty(enc.plan.encode_workspace_bytes(arr_a, 500) * 2, dtype=torch.uint8, device="cuda")
+    expect_a, offs_a = oracle.encode(schema, ca, 500, 0)
+    _, offs = _native_encode(enc, da, 500, 0, ws)
+    _native_encode(enc, db, 500, 0, ws)  # B's sizes now in the workspace
+    out, _ = _native_encode(enc, da, 500, 0, ws, offs_from=offs)
+    assert np.array_equal(out.cpu().numpy(), expect_a)
+    # encoded_size(A), then a decode through the same workspace, then encode(A)
+    _, offs = _native_encode(enc, da, 500, 0, ws)
+    rows = enc.encode(db, 500, 0)
+    p = enc.plan
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    outc = enc.decode(rows)  # output columns of the right shape; then a decode_sizes through ws
+    native.decode_sizes(p, rows.buffer, rows.offsets, 500, 0, native.column_array(outc), status, ws)
+    out, _ = _native_encode(enc, da, 500, 0, ws, offs_from=offs)
+    assert np.array_equal(out.cpu().numpy(), expect_a)
+
+
+def test_capacity_short_by_one_row_is_reported():
+    schema, cols = nested_columns("bean_a", 300, 4)
+    enc = RowEncoder(schema)
+    dcols = to_device(cols)
+    p = enc.plan
+    arr = native.column_array(dcols)
+    ws = torch.empty(p.encode_workspace_bytes(arr, 300), dtype=torch.uint8, device="cuda")
+    offs = torch.empty(301, dtype=torch.int64, device="cuda")
+    native.encoded_size(p, arr, 300, 1, offs, ws)
+    total = int(offs[300].item())
+    out = torch.empty(total, dtype=torch.uint8, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    native.encode(p, arr, 300, 1, offs, out, status, ws, capacity=total - 8)
+    with pytest.raises(errors.IndexOutOfBoundsException):
+        native.read_status(status)
+
+
+@pytest.mark.parametrize("name", ["holder", "lists", "maps_nested", "bean_a", "deep", "decimals", "chain"])
+def test_columnar_large_batch(name):
+    """20k records per shape (thousands of tiles) in STREAM frames."""
+    n = 2000 if name == "chain" else 20_000
+    schema, cols = nested_columns(name, n, 21)
+    enc = RowEncoder(schema)
+    oracle_equal(schema, cols, n, 1, enc.encode(to_device(cols), n, 1))
