@@ -584,19 +584,22 @@ void build_tc(fory_plan* plan) {
   t.vidx.assign(N, -1);
   t.var.clear();
   t.phase.assign(1, 0);
-  for (int d = 1; d <= maxd; ++d) {
+  for (int d = 1; d <= maxd + 1; ++d) {  // entries: var nodes and list / map items (scalar ones too)
     for (int i = 0; i < N; ++i) {
-      if (depth[i] != d || !tc_var_kind(p.nodes[i].kind)) continue;
+      const int par = t.parent[i];
+      const bool items = par >= 0 && p.nodes[par].kind != fory_amd::KIND_STRUCT;
+      if (depth[i] != d || (!tc_var_kind(p.nodes[i].kind) && !items)) continue;
       fory_amd::TcVar v{};
       v.node = i;
-      const int par = t.parent[i];
       v.parent = par < 0 ? -1 : t.vidx[par];
-      v.items = par >= 0 && p.nodes[par].kind != fory_amd::KIND_STRUCT;
+      v.items = items;
       v.depth = d;
+      v.var = tc_var_kind(p.nodes[i].kind);
+      v.key = items && p.nodes[par].kind == fory_amd::KIND_MAP ? (i == par + 1 ? 1 : 2) : 0;
       t.vidx[i] = (int32_t)t.var.size();
       t.var.push_back(v);
     }
-    t.phase.push_back((int32_t)t.var.size());
+    if (t.var.size() > (size_t)t.phase.back() || d <= maxd) t.phase.push_back((int32_t)t.var.size());
   }
 }
 
@@ -620,10 +623,13 @@ int64_t tc_bytes(const fory_plan* plan, const std::vector<int64_t>& m) {
   const TcInfo& t = plan->tc;
   int64_t maxm = 0, arrays = 0;
   for (const fory_amd::TcVar& v : t.var) {
+    if (!v.var) continue;
     arrays += align_up((m[v.node] + 1) * 8);
     if (v.items) maxm = std::max(maxm, m[v.node]);
   }
-  return align_up((int64_t)sizeof(fory_amd::TcTables)) + align_up((fory_amd::scan_partials(maxm) + 2) * 8) + arrays;
+  const int64_t n = m.empty() ? 0 : m[0];  // (node 0 is top-level: the rows)
+  return align_up((int64_t)sizeof(fory_amd::TcTables)) + align_up((fory_amd::scan_partials(maxm) + 2) * 8) +
+         align_up((n + 2) * 8) + arrays;
 }
 
 bool tc_usable(const fory_plan* plan, const fory_column* cols, int64_t n, int64_t ws_bytes, int64_t* need) {
@@ -685,23 +691,26 @@ bool tc_recall(const void* ws, uint64_t plan, uint64_t sig) {
 
 // Tables of a columnar call into the workspace (after the per-lane engine's region).
 int tc_prepare(const fory_plan* plan, const fory_column* cols, int64_t n, void* ws, hipStream_t s,
-               fory_amd::TcTables* T, const fory_amd::TcTables** dT, int64_t** partials) {
+               fory_amd::TcTables* T, const fory_amd::TcTables** dT, int64_t** partials, int64_t** tiles) {
   const TcInfo& t = plan->tc;
   const std::vector<int64_t> m = tc_domains(plan, cols, n);
   uint8_t* base = static_cast<uint8_t*>(ws) + fory_rowfmt_workspace_bytes(plan, n);
   std::memset(T, 0, sizeof(*T));
   int64_t maxm = 0;
   for (const fory_amd::TcVar& v : t.var)
-    if (v.items) maxm = std::max(maxm, m[v.node]);
+    if (v.var && v.items) maxm = std::max(maxm, m[v.node]);
   uint8_t* at = base + align_up((int64_t)sizeof(fory_amd::TcTables));
   *partials = reinterpret_cast<int64_t*>(at);
   at += align_up((fory_amd::scan_partials(maxm) + 2) * 8);
+  *tiles = reinterpret_cast<int64_t*>(at);
+  at += align_up((n + 2) * 8);
   for (size_t i = 0; i < m.size(); ++i) {
     T->m[i] = m[i];
     T->vidx[i] = t.vidx[i];
   }
   for (size_t v = 0; v < t.var.size(); ++v) {
     T->var[v] = t.var[v];
+    if (!t.var[v].var) continue;
     T->A[t.var[v].node] = reinterpret_cast<int64_t*>(at);
     at += align_up((m[t.var[v].node] + 1) * 8);
   }
@@ -718,6 +727,7 @@ int tc_sizes(const fory_plan* plan, const fory_amd::GenLaunch& G, const fory_amd
   const TcInfo& t = plan->tc;
   for (int v = (int)t.var.size() - 1; v >= 0; --v) {  // deepest first
     const fory_amd::TcVar& tv = t.var[(size_t)v];
+    if (!tv.var) continue;
     const int64_t m = T.m[tv.node];
     hipError_t e = fory_amd::launch_tc_sizes(G, dT, tv.node, m, G.frame == FORY_FRAME_COLLECTION && tv.node == 0, s);
     if (e != hipSuccess) return hip_fail(e, "tc_sizes");
@@ -872,7 +882,8 @@ int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols, int
       fory_amd::TcTables T;
       const fory_amd::TcTables* dT = nullptr;
       int64_t* tpart = nullptr;
-      rc = tc_prepare(plan, cols, num_rows, d_workspace, s, &T, &dT, &tpart);
+      int64_t* tiles = nullptr;
+      rc = tc_prepare(plan, cols, num_rows, d_workspace, s, &T, &dT, &tpart, &tiles);
       if (!rc) rc = tc_sizes(plan, G, T, dT, tpart, s);
       if (rc) return rc;
       e = fory_amd::launch_tc_rows(G, dT, d_row_offsets, s);
@@ -937,20 +948,20 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
       fory_amd::TcLaunch W{};
       int64_t* tpart = nullptr;
       const uint64_t sig = tc_signature(plan, cols, num_rows, frame_mode);
-      rc = tc_prepare(plan, cols, num_rows, d_workspace, s, &T, &W.T, &tpart);
+      rc = tc_prepare(plan, cols, num_rows, d_workspace, s, &T, &W.T, &tpart, &W.tiles);
       if (!rc && !tc_recall(d_workspace, plan->id, sig)) {  // sizes not left by encoded_size
         rc = tc_sizes(plan, G, T, W.T, tpart, s);
         if (!rc) tc_remember(d_workspace, plan->id, sig);
       }
       if (rc) return rc;
-      // rows per tile: about half the LDS image at the mean row size (out_capacity bounds
-      // the total), and half the position table at the mean instances per row
-      int64_t inst = 0;
-      for (const fory_amd::TcVar& v : plan->tc.var) inst += T.m[v.node];
-      const int64_t mean = std::max<int64_t>(8, out_capacity / num_rows);
-      const int64_t per_row = std::max<int64_t>(1, inst / num_rows);
-      W.tile_rows = std::max<int64_t>(1, std::min<int64_t>({fory_amd::kTcImg / 2 / mean, fory_amd::kTcPl / 2 / per_row, 1024}));
+      // byte tiles: the rows starting in each tile_bytes of the output (<= num_rows + 1
+      // tiles: out_capacity bounds the total)
+      const int64_t cap = std::max<int64_t>(1, out_capacity);
+      W.tile_bytes = std::max<int64_t>(p.kn.tc_tile > 0 ? p.kn.tc_tile : fory_amd::kTcImg / 2, (cap + num_rows) / (num_rows + 1));
+      W.ntiles = (cap + W.tile_bytes - 1) / W.tile_bytes;
       W.g = G;
+      e = fory_amd::launch_tc_tiles(W, d_row_offsets, s);
+      if (e != hipSuccess) return hip_fail(e, "tc_tiles");
       e = fory_amd::launch_tc_encode(W, d_row_offsets, static_cast<uint8_t*>(d_out), out_capacity, d_status, s);
       return e == hipSuccess ? FORY_OK : hip_fail(e, "tc_encode");
     }

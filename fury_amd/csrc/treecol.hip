@@ -107,11 +107,13 @@ __global__ __launch_bounds__(kTcWG) void tc_rows_kernel(GenLaunch L, const TcTab
 // write
 // ---------------------------------------------------------------------------
 // One tile's LDS state: the image (I = the byte of the tile's first position, 16-byte
-// phase of the output kept), per var node its instance range [lo, lo + cnt) and the
-// start of its position entries in pl (image-relative, -1 = absent / null).
+// phase of the output kept), per entry its instance range [lo, lo + cnt), per var entry
+// the start of its position entries in pl (image-relative, -1 = absent / null) and, for
+// lists / maps, aux: each instance's first item relative to the items' range start.
 struct TcTile {
   uint8_t* I;
   int32_t* pl;
+  int32_t* aux;
   const int64_t* lo;
   const int32_t* cnt;
   const int32_t* pb;
@@ -138,7 +140,7 @@ __device__ __forceinline__ void tc_hand(const TcTables* T, const TcTile& t, int 
   if (e >= 0 && e < t.cnt[v]) t.pl[t.pb[v] + e] = at;
 }
 
-// Slot size field of a var value: a string's byte length, a decimal's 32, else its bytes.
+// Slot size field of a var value: a string's byte length, else its bytes (decimals 32).
 __device__ __forceinline__ uint32_t tc_slot_size(const GNode& nd, const ColumnDev& col, int64_t k, int64_t bytes) {
   if (nd.kind == KIND_BYTES) return (uint32_t)(col.offsets[k + 1] - col.offsets[k]);
   return (uint32_t)bytes;
@@ -176,69 +178,21 @@ __device__ __forceinline__ bool tc_fields(const GenLaunch& L, const TcTables* T,
   return true;
 }
 
-// BinaryArrayWriter.reset(n) at P + its elements: items x in [o0, o1). Returns the
-// array's bytes, or -1 when it does not fit.
-__device__ __forceinline__ int64_t tc_array(const GenLaunch& L, const TcTables* T, const TcTile& t, int x,
-                                            int64_t o0, int64_t o1, int32_t P) {
-  const GNode it = L.nodes[x];
-  const ColumnDev col = L.cols[x];
-  const int64_t n = o1 - o0;
-  const int es = elem_size(it);
-  const int32_t hb = 8 + gbm(n);
-  const int64_t fixed = hb + gr8(n * es);
-  if (P + fixed > t.len) return -1;
-  uint8_t* a = t.I + P;
-  st32(a, (uint32_t)n);
-  st32(a + 4, (uint32_t)(n >> 32));
-  const uint8_t* vb = (it.flags & 1) ? col.validity : nullptr;
-  if (is_scalar(it.kind)) {
-    uint8_t* el = a + hb;
-    if (it.kind == KIND_BOOL || es < 4) {
-      for (int64_t q = 0; q < n; ++q) {
-        if (vb && !gvalid(vb, o0 + q)) {
-          a[8 + (q >> 3)] |= (uint8_t)(1u << (q & 7));
-          continue;
-        }
-        uint64_t v = load_elem(col.values, es, o0 + q);
-        if (it.kind == KIND_BOOL) v = v ? 1 : 0;
-        tc_put(el + q * es, v, es);
-      }
-    } else {  // 4 / 8-byte elements: dword copy, then the nulls zeroed
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(col.values + o0 * es);
-      const int64_t nw = n * es / 4;
-      for (int64_t w = 0; w < nw; ++w) st32(el + 4 * w, src[w]);
-      if (vb) {
-        for (int64_t q = 0; q < n; ++q) {
-          if (gvalid(vb, o0 + q)) continue;
-          a[8 + (q >> 3)] |= (uint8_t)(1u << (q & 7));
-          for (int b = 0; b < es; b += 4) st32(el + q * es + b, 0u);
-        }
-      }
-    }
-    return fixed;
-  }
-  const int64_t* A = T->A[x];
-  int32_t at = P + (int32_t)fixed;
-  for (int64_t q = 0; q < n; ++q) {
-    const int64_t e = o0 + q;
-    if (vb && !gvalid(vb, e)) {
-      a[8 + (q >> 3)] |= (uint8_t)(1u << (q & 7));
-      continue;
-    }
-    const int64_t S = A[e + 1] - A[e];
-    if (S < 0 || at + S > t.len) return -1;
-    uint8_t* slot = a + hb + 8 * q;
-    st32(slot, tc_slot_size(it, col, e, S));
-    st32(slot + 4, (uint32_t)(at - P));
-    tc_hand(T, t, x, e, at);
-    at += (int32_t)S;
-  }
-  return at - P;
+// aux of list / map instance g (entry v, node c): its first item relative to the tile's items.
+__device__ __forceinline__ int64_t tc_aux(const GenLaunch& L, const TcTables* T, const TcTile& t, int v, int c,
+                                          int g, int64_t k, int64_t* o1 = nullptr) {
+  int64_t o0, e1;
+  tc_items(L, T, c, k, &o0, &e1);
+  t.aux[t.pb[v] + g] = (int32_t)(o0 - t.lo[T->vidx[c + 1]]);
+  if (o1) *o1 = e1;
+  return o0;
 }
 
-// Instance k of var node c at position P (image-relative).
-__device__ __forceinline__ int32_t tc_instance(const GenLaunch& L, const TcTables* T, const TcTile& t, int c,
-                                               int64_t k, int32_t P) {
+// A var instance's own bytes (step A of a depth): string bytes, a decimal, a bean's fixed
+// part, an array's / map's headers (their elements are step B's). g: the instance's
+// index in the tile, v its entry.
+__device__ __forceinline__ int32_t tc_head(const GenLaunch& L, const TcTables* T, const TcTile& t, int v, int c,
+                                           int g, int64_t k, int32_t P) {
   const GNode nd = L.nodes[c];
   const ColumnDev col = L.cols[c];
   switch (nd.kind) {
@@ -250,8 +204,8 @@ __device__ __forceinline__ int32_t tc_instance(const GenLaunch& L, const TcTable
     }
     case KIND_DECIMAL: {  // BinaryWriter.writeDecimal
       if (P + 32 > t.len) return FORY_ERR_ENCODER;
-      const uint8_t* v = col.values + 16 * k;
-      const uint32_t w[4] = {ld32(v), ld32(v + 4), ld32(v + 8), ld32(v + 12)};
+      const uint8_t* x = col.values + 16 * k;
+      const uint32_t w[4] = {ld32(x), ld32(x + 4), ld32(x + 8), ld32(x + 12)};
       if (!g_dec_fits(w, nd.prec)) return FORY_ERR_UNSUPPORTED;
       const uint32_t ext = (w[3] >> 31) ? 0xffffffffu : 0u;
       for (int q = 0; q < 4; ++q) st32(t.I + P + 4 * q, w[q]);
@@ -260,22 +214,73 @@ __device__ __forceinline__ int32_t tc_instance(const GenLaunch& L, const TcTable
     }
     case KIND_STRUCT:
       return tc_fields(L, T, t, c + 1, nd.end, nd.nchild, gbm(nd.nchild), k, P) ? 0 : FORY_ERR_ENCODER;
-    case KIND_LIST: {
-      int64_t o0, o1;
-      tc_items(L, T, c, k, &o0, &o1);
-      return tc_array(L, T, t, c + 1, o0, o1, P) < 0 ? FORY_ERR_ENCODER : 0;
-    }
-    case KIND_MAP: {  // [i64 key array bytes][key array][value array]
-      int64_t o0, o1;
-      tc_items(L, T, c, k, &o0, &o1);
-      if (P + 8 > t.len) return FORY_ERR_ENCODER;
-      const int64_t kb = tc_array(L, T, t, c + 1, o0, o1, P + 8);
-      if (kb < 0) return FORY_ERR_ENCODER;
+    case KIND_LIST:
+    case KIND_MAP: {  // [i64 n] | [i64 key array bytes][i64 n ...keys][i64 n ...values]
+      int64_t o1;
+      const int64_t o0 = tc_aux(L, T, t, v, c, g, k, &o1);
+      const int64_t n = o1 - o0;
+      const int key = c + 1;
+      if (nd.kind == KIND_LIST) {
+        if (P + 8 + gbm(n) + gr8(n * elem_size(L.nodes[key])) > t.len) return FORY_ERR_ENCODER;
+        tc_put(t.I + P, (uint64_t)n, 8);
+        return 0;
+      }
+      const int val = L.nodes[key].end;
+      const int64_t kb = tc_array_bytes(L, T, key, o0, o1);
+      if (kb < 0 || P + 8 + kb + 8 + gbm(n) + gr8(n * elem_size(L.nodes[val])) > t.len) return FORY_ERR_ENCODER;
       tc_put(t.I + P, (uint64_t)kb, 8);
-      return tc_array(L, T, t, L.nodes[c + 1].end, o0, o1, P + 8 + (int32_t)kb) < 0 ? FORY_ERR_ENCODER : 0;
+      tc_put(t.I + P + 8, (uint64_t)n, 8);
+      tc_put(t.I + P + 8 + kb, (uint64_t)n, 8);
+      return 0;
     }
     default: return 0;
   }
+}
+
+// Item i (tile-relative) of entry xe under list / map entry v (step B): its element —
+// a null bit, a scalar, or a var item's slot + position. which: 0 list items, 1 keys,
+// 2 values.
+__device__ __forceinline__ int32_t tc_item(const GenLaunch& L, const TcTables* T, const TcTile& t, int v, int xe,
+                                           int x, int which, int i) {
+  const int cv = t.cnt[v];
+  const int32_t* aux = t.aux + t.pb[v];
+  int a = 0, b = cv - 1;  // the last instance whose items start at or before i
+  while (a < b) {
+    const int mid = (a + b + 1) >> 1;
+    if (aux[mid] <= i) a = mid;
+    else b = mid - 1;
+  }
+  const int32_t P = t.pl[t.pb[v] + a];
+  if (P < 0) return 0;  // a null / absent container
+  const int32_t o0 = aux[a], o1 = a + 1 < cv ? aux[a + 1] : t.cnt[xe];
+  const int64_t n = o1 - o0;
+  const int64_t q = i - o0;
+  const int32_t Pa = which == 0 ? P : (which == 1 ? P + 8 : P + 8 + (int32_t)ld32(t.I + P));
+  const GNode it = L.nodes[x];
+  const ColumnDev col = L.cols[x];
+  const int es = elem_size(it);
+  const int32_t hb = 8 + gbm(n);
+  if (q < 0 || q >= n || Pa + hb + gr8(n * es) > t.len) return FORY_ERR_ENCODER;
+  const int64_t e = t.lo[xe] + i;
+  if ((it.flags & 1) && !gvalid(col.validity, e)) {  // setNullAt: the element bit
+    atomicOr(reinterpret_cast<uint32_t*>(t.I + Pa + 8) + (q >> 5), 1u << (q & 31));
+    return 0;
+  }
+  if (is_scalar(it.kind)) {
+    uint64_t val = load_elem(col.values, es, e);
+    if (it.kind == KIND_BOOL) val = val ? 1 : 0;
+    tc_put(t.I + Pa + hb + q * es, val, es);
+    return 0;
+  }
+  const int64_t* A = T->A[x];
+  const int64_t S = A[e + 1] - A[e];
+  const int64_t at = Pa + hb + gr8(n * 8) + (A[e] - A[t.lo[xe] + o0]);
+  if (S < 0 || at < 0 || at + S > t.len) return FORY_ERR_ENCODER;
+  uint8_t* slot = t.I + Pa + hb + 8 * q;
+  st32(slot, tc_slot_size(it, col, e, S));
+  st32(slot + 4, (uint32_t)(at - Pa));
+  tc_hand(T, t, x, e, (int32_t)at);
+  return 0;
 }
 
 // Row / frame i: header, then the row's fixed part (or the collection's position).
@@ -317,12 +322,24 @@ __device__ __forceinline__ void tc_row(const GenLaunch& L, const TcTables* T, co
     set_status(status, FORY_ERR_ENCODER);
 }
 
+__global__ __launch_bounds__(kTcWG) void tc_tiles_kernel(TcLaunch W, const int64_t* __restrict__ offs) {
+  const int64_t i = (int64_t)blockIdx.x * kTcWG + threadIdx.x;
+  const int64_t n = W.g.num_rows;
+  if (i > n) return;
+  const int64_t B = W.tile_bytes;
+  const int64_t prev = i == 0 ? -1 : offs[i - 1];
+  int64_t t0 = prev < 0 ? 0 : prev / B + 1;  // tiles t with prev < t x B <= offs[i]
+  int64_t t1 = i == n ? W.ntiles : offs[i] / B;
+  if (t1 > W.ntiles) t1 = W.ntiles;
+  for (int64_t t = t0; t <= t1; ++t) W.tiles[t] = i;
+}
+
 template <int D>
 __global__ __launch_bounds__(kTcWG) void tc_encode_kernel(TcLaunch W, const int64_t* __restrict__ offs,
                                                           uint8_t* __restrict__ out, int64_t capacity,
                                                           int32_t* status) {
   __shared__ __attribute__((aligned(16))) uint8_t s_img[kTcImg + 16];
-  __shared__ int32_t s_pl[kTcPl];
+  __shared__ int32_t s_pl[kTcPl], s_aux[kTcPl];
   __shared__ int64_t s_lo[kTcMaxNodes];
   __shared__ int32_t s_cnt[kTcMaxNodes], s_pb[kTcMaxNodes];
   __shared__ int64_t s_base, s_end;
@@ -330,8 +347,12 @@ __global__ __launch_bounds__(kTcWG) void tc_encode_kernel(TcLaunch W, const int6
   const GenLaunch& L = W.g;
   const TcTables* T = W.T;
   const int tid = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * W.tile_rows;
-  const int64_t r1 = r0 + W.tile_rows < L.num_rows ? r0 + W.tile_rows : L.num_rows;
+  const int64_t r0 = W.tiles[blockIdx.x], r1 = W.tiles[blockIdx.x + 1];
+  if (r0 >= r1) return;  // no row starts in this tile's bytes
+  if (r0 < 0 || r1 > L.num_rows) {  // offsets not ascending
+    if (tid == 0) set_status(status, FORY_ERR_CAPACITY);
+    return;
+  }
   if (tid == 0) {
     s_base = offs[r0];
     s_end = offs[r1];
@@ -356,7 +377,7 @@ __global__ __launch_bounds__(kTcWG) void tc_encode_kernel(TcLaunch W, const int6
         if (hi < lo) hi = lo;
       }
       s_lo[v] = lo;
-      s_cnt[v] = hi - lo > kTcPl ? kTcPl + 1 : (int32_t)(hi - lo);
+      s_cnt[v] = hi - lo > (1 << 30) ? (1 << 30) : (int32_t)(hi - lo);
     }
     __syncthreads();
   }
@@ -365,8 +386,8 @@ __global__ __launch_bounds__(kTcWG) void tc_encode_kernel(TcLaunch W, const int6
     bool fit = true;
     for (int v = 0; v < T->nvar; ++v) {
       s_pb[v] = tot;
-      tot += s_cnt[v];
-      if (tot > kTcPl) {
+      if (T->var[v].var) tot += s_cnt[v];
+      if (s_cnt[v] == (1 << 30) || tot > kTcPl) {
         fit = false;
         tot = kTcPl;
       }
@@ -400,6 +421,7 @@ __global__ __launch_bounds__(kTcWG) void tc_encode_kernel(TcLaunch W, const int6
   TcTile t;
   t.I = s_img + mis;
   t.pl = s_pl;
+  t.aux = s_aux;
   t.lo = s_lo;
   t.cnt = s_cnt;
   t.pb = s_pb;
@@ -407,21 +429,48 @@ __global__ __launch_bounds__(kTcWG) void tc_encode_kernel(TcLaunch W, const int6
   for (int64_t i = r0 + tid; i < r1; i += kTcWG) tc_row(L, T, t, offs, base, i, status);
   __syncthreads();
   for (int d = 1; d <= depths; ++d) {
-    int rot = 0;  // instances of the phase's earlier nodes: spreads the nodes over the waves
-    for (int v = T->phase[d - 1]; v < T->phase[d]; ++v) {
-      const int c = T->var[v].node;
+    const int v0 = T->phase[d - 1], v1 = T->phase[d];
+    // A: the depth's var instances (rot spreads the nodes over the waves)
+    int rot = 0;
+    for (int v = v0; v < v1; ++v) {
+      const TcVar tv = T->var[v];
+      if (!tv.var) continue;
       const int cnt = s_cnt[v];
-      const int64_t lo = s_lo[v];
       const int32_t* pl = s_pl + s_pb[v];
+      const int kind = L.nodes[tv.node].kind;
+      const bool cont = kind == KIND_LIST || kind == KIND_MAP;
       for (int g = (tid - rot) & (kTcWG - 1); g < cnt; g += kTcWG) {
         const int32_t P = pl[g];
-        if (P < 0) continue;
-        const int32_t err = tc_instance(L, T, t, c, lo + g, P);
+        if (P < 0) {  // a null / absent container still delimits the items' search
+          if (cont) tc_aux(L, T, t, v, tv.node, g, s_lo[v] + g);
+          continue;
+        }
+        const int32_t err = tc_head(L, T, t, v, tv.node, g, s_lo[v] + g, P);
         if (err) set_status(status, err);
       }
       rot = (rot + cnt) & (kTcWG - 1);
     }
     __syncthreads();
+    // B: the elements of the depth's arrays and maps, item-parallel
+    bool any = false;
+    for (int v = v0; v < v1; ++v) {
+      const TcVar tv = T->var[v];
+      if (!tv.var) continue;
+      const int kind = L.nodes[tv.node].kind;
+      if (kind != KIND_LIST && kind != KIND_MAP) continue;
+      any = true;
+      for (int which = kind == KIND_LIST ? 0 : 1; which <= (kind == KIND_LIST ? 0 : 2); ++which) {
+        const int x = which == 2 ? L.nodes[tv.node + 1].end : tv.node + 1;
+        const int xe = T->vidx[x];
+        const int cnt = s_cnt[xe];
+        for (int i = (tid - rot) & (kTcWG - 1); i < cnt; i += kTcWG) {
+          const int32_t err = tc_item(L, T, t, v, xe, x, which, i);
+          if (err) set_status(status, err);
+        }
+        rot = (rot + cnt) & (kTcWG - 1);
+      }
+    }
+    if (any) __syncthreads();
   }
   // the image to [base, end): 16-byte stores between dword head / tail
   uint8_t* o = out + base;
@@ -439,8 +488,7 @@ __global__ __launch_bounds__(kTcWG) void tc_encode_kernel(TcLaunch W, const int6
 template <int D>
 hipError_t launch_tc_encode_d(const TcLaunch& W, const int64_t* offs, uint8_t* out, int64_t capacity,
                               int32_t* status, hipStream_t s) {
-  const int64_t tiles = (W.g.num_rows + W.tile_rows - 1) / W.tile_rows;
-  hipLaunchKernelGGL(tc_encode_kernel<D>, dim3((unsigned)tiles), dim3(kTcWG), 0, s, W, offs, out, capacity,
+  hipLaunchKernelGGL(tc_encode_kernel<D>, dim3((unsigned)W.ntiles), dim3(kTcWG), 0, s, W, offs, out, capacity,
                      status);
   return hipGetLastError();
 }
@@ -462,9 +510,15 @@ hipError_t launch_tc_rows(const GenLaunch& L, const TcTables* T, int64_t* sizes,
   return hipGetLastError();
 }
 
+hipError_t launch_tc_tiles(const TcLaunch& W, const int64_t* offs, hipStream_t s) {
+  const int64_t n = W.g.num_rows + 1;
+  hipLaunchKernelGGL(tc_tiles_kernel, dim3((unsigned)((n + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s, W, offs);
+  return hipGetLastError();
+}
+
 hipError_t launch_tc_encode(const TcLaunch& W, const int64_t* offs, uint8_t* out, int64_t capacity,
                             int32_t* status, hipStream_t s) {
-  if (W.g.num_rows <= 0 || W.tile_rows <= 0) return hipSuccess;
+  if (W.g.num_rows <= 0 || W.ntiles <= 0) return hipSuccess;
   if (W.g.max_depth + 1 <= 4) return launch_tc_encode_d<4>(W, offs, out, capacity, status, s);
   if (W.g.max_depth + 1 <= 8) return launch_tc_encode_d<8>(W, offs, out, capacity, status, s);
   return launch_tc_encode_d<18>(W, offs, out, capacity, status, s);
