@@ -30,7 +30,6 @@ struct TcInfo {
   std::vector<fory_amd::TcVar> var;  // by depth, pre-order within a depth
   std::vector<int32_t> vidx;        // node -> var index (-1: scalar)
   std::vector<int32_t> parent;      // node -> parent node (-1: the row)
-  std::vector<int32_t> phase;       // [0, end of depth 1, ..., end of the last depth]
 };
 
 struct fory_plan {
@@ -583,23 +582,18 @@ void build_tc(fory_plan* plan) {
   }
   t.vidx.assign(N, -1);
   t.var.clear();
-  t.phase.assign(1, 0);
-  for (int d = 1; d <= maxd + 1; ++d) {  // entries: var nodes and list / map items (scalar ones too)
+  for (int d = 1; d <= maxd; ++d) {  // var nodes by depth: parents are written before children
     for (int i = 0; i < N; ++i) {
+      if (depth[i] != d || !tc_var_kind(p.nodes[i].kind)) continue;
       const int par = t.parent[i];
-      const bool items = par >= 0 && p.nodes[par].kind != fory_amd::KIND_STRUCT;
-      if (depth[i] != d || (!tc_var_kind(p.nodes[i].kind) && !items)) continue;
       fory_amd::TcVar v{};
       v.node = i;
       v.parent = par < 0 ? -1 : t.vidx[par];
-      v.items = items;
+      v.items = par >= 0 && p.nodes[par].kind != fory_amd::KIND_STRUCT;
       v.depth = d;
-      v.var = tc_var_kind(p.nodes[i].kind);
-      v.key = items && p.nodes[par].kind == fory_amd::KIND_MAP ? (i == par + 1 ? 1 : 2) : 0;
       t.vidx[i] = (int32_t)t.var.size();
       t.var.push_back(v);
     }
-    if (t.var.size() > (size_t)t.phase.back() || d <= maxd) t.phase.push_back((int32_t)t.var.size());
   }
 }
 
@@ -623,13 +617,10 @@ int64_t tc_bytes(const fory_plan* plan, const std::vector<int64_t>& m) {
   const TcInfo& t = plan->tc;
   int64_t maxm = 0, arrays = 0;
   for (const fory_amd::TcVar& v : t.var) {
-    if (!v.var) continue;
-    arrays += align_up((m[v.node] + 1) * 8);
+    arrays += 2 * align_up((m[v.node] + 1) * 8);  // sizes, positions
     if (v.items) maxm = std::max(maxm, m[v.node]);
   }
-  const int64_t n = m.empty() ? 0 : m[0];  // (node 0 is top-level: the rows)
-  return align_up((int64_t)sizeof(fory_amd::TcTables)) + align_up((fory_amd::scan_partials(maxm) + 2) * 8) +
-         align_up((n + 2) * 8) + arrays;
+  return align_up((int64_t)sizeof(fory_amd::TcTables)) + align_up((fory_amd::scan_partials(maxm) + 2) * 8) + arrays;
 }
 
 bool tc_usable(const fory_plan* plan, const fory_column* cols, int64_t n, int64_t ws_bytes, int64_t* need) {
@@ -691,32 +682,31 @@ bool tc_recall(const void* ws, uint64_t plan, uint64_t sig) {
 
 // Tables of a columnar call into the workspace (after the per-lane engine's region).
 int tc_prepare(const fory_plan* plan, const fory_column* cols, int64_t n, void* ws, hipStream_t s,
-               fory_amd::TcTables* T, const fory_amd::TcTables** dT, int64_t** partials, int64_t** tiles) {
+               fory_amd::TcTables* T, const fory_amd::TcTables** dT, int64_t** partials) {
   const TcInfo& t = plan->tc;
   const std::vector<int64_t> m = tc_domains(plan, cols, n);
   uint8_t* base = static_cast<uint8_t*>(ws) + fory_rowfmt_workspace_bytes(plan, n);
   std::memset(T, 0, sizeof(*T));
   int64_t maxm = 0;
   for (const fory_amd::TcVar& v : t.var)
-    if (v.var && v.items) maxm = std::max(maxm, m[v.node]);
+    if (v.items) maxm = std::max(maxm, m[v.node]);
   uint8_t* at = base + align_up((int64_t)sizeof(fory_amd::TcTables));
   *partials = reinterpret_cast<int64_t*>(at);
   at += align_up((fory_amd::scan_partials(maxm) + 2) * 8);
-  *tiles = reinterpret_cast<int64_t*>(at);
-  at += align_up((n + 2) * 8);
   for (size_t i = 0; i < m.size(); ++i) {
     T->m[i] = m[i];
     T->vidx[i] = t.vidx[i];
   }
   for (size_t v = 0; v < t.var.size(); ++v) {
     T->var[v] = t.var[v];
-    if (!t.var[v].var) continue;
-    T->A[t.var[v].node] = reinterpret_cast<int64_t*>(at);
-    at += align_up((m[t.var[v].node] + 1) * 8);
+    const int node = t.var[v].node;
+    T->A[node] = reinterpret_cast<int64_t*>(at);
+    at += align_up((m[node] + 1) * 8);
+    T->P[node] = reinterpret_cast<int64_t*>(at);
+    at += align_up((m[node] + 1) * 8);
   }
-  for (size_t d = 0; d < t.phase.size(); ++d) T->phase[d] = t.phase[d];
   T->nvar = (int32_t)t.var.size();
-  T->depths = (int32_t)t.phase.size() - 1;
+  T->depths = t.var.empty() ? 0 : t.var.back().depth;
   *dT = reinterpret_cast<const fory_amd::TcTables*>(base);
   return upload(base, T, (int64_t)sizeof(*T), s);
 }
@@ -727,7 +717,6 @@ int tc_sizes(const fory_plan* plan, const fory_amd::GenLaunch& G, const fory_amd
   const TcInfo& t = plan->tc;
   for (int v = (int)t.var.size() - 1; v >= 0; --v) {  // deepest first
     const fory_amd::TcVar& tv = t.var[(size_t)v];
-    if (!tv.var) continue;
     const int64_t m = T.m[tv.node];
     hipError_t e = fory_amd::launch_tc_sizes(G, dT, tv.node, m, G.frame == FORY_FRAME_COLLECTION && tv.node == 0, s);
     if (e != hipSuccess) return hip_fail(e, "tc_sizes");
@@ -882,8 +871,7 @@ int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols, int
       fory_amd::TcTables T;
       const fory_amd::TcTables* dT = nullptr;
       int64_t* tpart = nullptr;
-      int64_t* tiles = nullptr;
-      rc = tc_prepare(plan, cols, num_rows, d_workspace, s, &T, &dT, &tpart, &tiles);
+      rc = tc_prepare(plan, cols, num_rows, d_workspace, s, &T, &dT, &tpart);
       if (!rc) rc = tc_sizes(plan, G, T, dT, tpart, s);
       if (rc) return rc;
       e = fory_amd::launch_tc_rows(G, dT, d_row_offsets, s);
@@ -945,25 +933,22 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
     if (rc) return rc;
     if (tc_usable(plan, cols, num_rows, workspace_bytes, nullptr) && !(reinterpret_cast<uintptr_t>(d_out) & 3)) {
       fory_amd::TcTables T;
-      fory_amd::TcLaunch W{};
+      const fory_amd::TcTables* dT = nullptr;
       int64_t* tpart = nullptr;
       const uint64_t sig = tc_signature(plan, cols, num_rows, frame_mode);
-      rc = tc_prepare(plan, cols, num_rows, d_workspace, s, &T, &W.T, &tpart, &W.tiles);
+      rc = tc_prepare(plan, cols, num_rows, d_workspace, s, &T, &dT, &tpart);
       if (!rc && !tc_recall(d_workspace, plan->id, sig)) {  // sizes not left by encoded_size
-        rc = tc_sizes(plan, G, T, W.T, tpart, s);
+        rc = tc_sizes(plan, G, T, dT, tpart, s);
         if (!rc) tc_remember(d_workspace, plan->id, sig);
       }
       if (rc) return rc;
-      // byte tiles: the rows starting in each tile_bytes of the output (<= num_rows + 1
-      // tiles: out_capacity bounds the total)
-      const int64_t cap = std::max<int64_t>(1, out_capacity);
-      W.tile_bytes = std::max<int64_t>(p.kn.tc_tile > 0 ? p.kn.tc_tile : fory_amd::kTcImg / 2, (cap + num_rows) / (num_rows + 1));
-      W.ntiles = (cap + W.tile_bytes - 1) / W.tile_bytes;
-      W.g = G;
-      e = fory_amd::launch_tc_tiles(W, d_row_offsets, s);
-      if (e != hipSuccess) return hip_fail(e, "tc_tiles");
-      e = fory_amd::launch_tc_encode(W, d_row_offsets, static_cast<uint8_t*>(d_out), out_capacity, d_status, s);
-      return e == hipSuccess ? FORY_OK : hip_fail(e, "tc_encode");
+      uint8_t* out = static_cast<uint8_t*>(d_out);
+      e = fory_amd::launch_tc_write_rows(G, dT, d_row_offsets, out, out_capacity, d_status, s);
+      for (size_t v = 0; v < plan->tc.var.size() && e == hipSuccess; ++v) {
+        const int node = plan->tc.var[v].node;
+        e = fory_amd::launch_tc_write_node(G, dT, node, T.m[node], out, out_capacity, d_status, s, p.nodes[node].kind);
+      }
+      return e == hipSuccess ? FORY_OK : hip_fail(e, "tc_write");
     }
     e = fory_amd::launch_gen_encode(G, d_row_offsets, static_cast<uint8_t*>(d_out), out_capacity, d_status, s);
     return e == hipSuccess ? FORY_OK : hip_fail(e, "gen_encode");

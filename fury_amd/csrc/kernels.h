@@ -135,43 +135,32 @@ hipError_t launch_gen_decode(const GenLaunch& L, const uint8_t* rows, const int6
 // instance columns. An instance is one element of a schema node's column (a row of a
 // top-level field, a struct child of an instance, a list item / map entry). Sizes go
 // bottom-up (A[c][j] = bytes instance j of var node c adds to its parent; item nodes
-// are scanned in place, A[x][m] = total), then tiles of rows write their bytes into an
-// LDS image, depth by depth: each instance writes its own fixed part and hands its var
-// children their positions.
+// are scanned in place, A[x][m] = total); then the writes go top-down, one pass per var
+// node: each instance writes its whole fixed part at its position P[c][j] and hands its
+// var children theirs (-1: absent or null), so every output byte is written once.
 constexpr int kTcMaxNodes = 128;  // plans with more nodes keep the per-lane engine
-struct TcVar {     // a node the tile writer ranges over: every var node and every list / map item node
+struct TcVar {     // a var node (string / decimal / struct / list / map)
   int32_t node;    // schema node (column index)
   int32_t parent;  // entry of the parent (-1: the row)
   int32_t items;   // 1: the parent is a list / map and this node its items / keys / values
   int32_t depth;   // 1 + the parent's depth (top-level fields: 1)
-  int32_t var;     // 1: a var node (has positions); 0: scalar items
-  int32_t key;     // items of a map: 1 keys, 2 values; 0 otherwise
 };
 struct TcTables {               // device, in the workspace
   int64_t* A[kTcMaxNodes];      // var nodes: sizes (items: exclusive prefix, total at [m]); else null
+  int64_t* P[kTcMaxNodes];      // var nodes: output positions of the instances (-1 = none); else null
   int64_t m[kTcMaxNodes];       // instances of each node in this call
-  int32_t vidx[kTcMaxNodes];    // node -> entry, -1 for nodes not ranged over
+  int32_t vidx[kTcMaxNodes];    // node -> entry, -1 for scalars
   TcVar var[kTcMaxNodes];       // entries by depth, pre-order within a depth
-  int32_t phase[kTcMaxNodes + 1];  // entries of depth d: [phase[d - 1], phase[d]), phase[0] = 0
   int32_t nvar, depths;
 };
-struct TcLaunch {
-  GenLaunch g;
-  const TcTables* T;   // device
-  int64_t* tiles;      // workspace: first row of each byte tile (ntiles + 1 entries)
-  int64_t tile_bytes;  // a tile = the rows starting in [t x tile_bytes, (t + 1) x tile_bytes)
-  int64_t ntiles;
-};
-// LDS image of one tile (bytes) and its position-table entries: a var instance owns at
-// least 8 bytes of its parent's fixed part, so an image that fits holds <= kTcImg / 8.
-constexpr int kTcImg = 16384;
-constexpr int kTcPl = kTcImg / 8;
 hipError_t launch_tc_sizes(const GenLaunch& L, const TcTables* T, int node, int64_t m, bool root_coll, hipStream_t s);
 hipError_t launch_tc_rows(const GenLaunch& L, const TcTables* T, int64_t* sizes, hipStream_t s);
-// Tile table: tiles[t] = the first row whose offset is >= t x tile_bytes (t <= ntiles).
-hipError_t launch_tc_tiles(const TcLaunch& W, const int64_t* offs, hipStream_t s);
-hipError_t launch_tc_encode(const TcLaunch& W, const int64_t* offs, uint8_t* out, int64_t capacity,
-                            int32_t* status, hipStream_t s);
+// Writes: the rows (frame headers, fixed parts, top-level positions), then each var node's
+// instances (node, m = its instance count), parents before children.
+hipError_t launch_tc_write_rows(const GenLaunch& L, const TcTables* T, const int64_t* offs, uint8_t* out,
+                                int64_t capacity, int32_t* status, hipStream_t s);
+hipError_t launch_tc_write_node(const GenLaunch& L, const TcTables* T, int node, int64_t m, uint8_t* out,
+                                int64_t capacity, int32_t* status, hipStream_t s, int kind);
 
 // Frame index of a STREAM batch (frames.hip): the starts of the first num_rows
 // frames of rows_bytes bytes, found on the device from the stream alone.

@@ -114,7 +114,6 @@ LaunchKnobs knobs_from_env() {
   k.prof = num("FORY_ROWFMT_VARPROF", 0) != 0;
   k.diag = set("FORY_ROWFMT_VARDIAG");
   k.tree_col = num("FORY_ROWFMT_TREECOL", 1);
-  k.tc_tile = num("FORY_ROWFMT_TCTILE", 0);
   return k;
 }
 

@@ -154,7 +154,7 @@ struct LaunchKnobs {
   int32_t idx_frames;
   int32_t prof;
   int32_t diag;
-  int32_t tc_tile;   // FORY_ROWFMT_TCTILE: columnar writer tile bytes (0 = half the LDS image)
+  int32_t pad;
   int32_t tree_col;  // FORY_ROWFMT_TREECOL: 0 = tree-engine encode per lane only; else the columnar engine when the workspace allows
 };
 LaunchKnobs knobs_from_env();

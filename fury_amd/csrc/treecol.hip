@@ -3,8 +3,8 @@
 // The per-lane engine (generic.hip) walks one record per lane, serially through a
 // frame stack, so a wave runs as long as its deepest record and every column access is
 // a lane-private gather. Here the same bytes (BaseBinaryEncoderBuilder.serializeFor,
-// :236-351 arrays, :370-427 maps, :436-490 beans) come from three kinds of passes over
-// instance columns (one instance = one element of a schema node's column):
+// :236-351 arrays, :370-427 maps, :436-490 beans) come from passes over instance columns
+// (one instance = one element of a schema node's column), each a full-occupancy grid:
 //   sizes   bottom-up, one launch per var node (children first), lane per instance:
 //           A[c][j] = the bytes instance j adds to its parent — strings round8(len),
 //           decimals 32, beans bitmap + 8 x fields + their var children, arrays
@@ -14,16 +14,18 @@
 //           items before k, A[x][m] = all of them.
 //   rows    row / frame size = header + fixed part + the top-level var fields' sizes;
 //           scanned into the row offsets (encoded_size's output).
-//   write   one workgroup per tile of rows: the tile's bytes [offs[r0], offs[r1]) are
-//           assembled in an LDS image and stored once, coalesced. Phase 0 writes the
-//           rows' frame headers and fixed parts; phase d the instances of depth-d var
-//           nodes: each reads its position (handed down by its parent in phase d-1),
-//           writes its own fixed part (bean slots, array header / bitmap / elements,
-//           map key-array size, string bytes, decimal) and hands its var children their
-//           positions. Tiles too large for the image (a row bigger than the tile
-//           budget) are encoded by the per-lane engine instead, row by row.
-// The instance ranges of a tile follow from the row range: a struct child has its
-// parent's range, items the parent's offsets at the range ends.
+//   write   top-down, one launch per var node (parents first). Lane per row: frame
+//           header, null bits, slots, and the top-level var fields' positions. Lane per
+//           string / decimal / bean instance at its position: its bytes, or its fixed
+//           part and its children's positions. Lists / maps: a workgroup per 256
+//           containers writes their headers (count, null bitmap from the items'
+//           validity, element padding), then their elements item-parallel — each item
+//           finds its container by a binary search over the workgroup's item starts in
+//           LDS, writes its element (value, zero, or var slot) and a var item's position
+//           (the container's data start + the items' scanned sizes before it).
+// Every byte of a record is written once (fixed parts whole, zero slots included), so
+// the output needs no clearing. Absent instances (under a null parent) get position -1
+// and write nothing.
 #include "gen_device.h"
 
 namespace fory_amd {
@@ -106,20 +108,6 @@ __global__ __launch_bounds__(kTcWG) void tc_rows_kernel(GenLaunch L, const TcTab
 // ---------------------------------------------------------------------------
 // write
 // ---------------------------------------------------------------------------
-// One tile's LDS state: the image (I = the byte of the tile's first position, 16-byte
-// phase of the output kept), per entry its instance range [lo, lo + cnt), per var entry
-// the start of its position entries in pl (image-relative, -1 = absent / null) and, for
-// lists / maps, aux: each instance's first item relative to the items' range start.
-struct TcTile {
-  uint8_t* I;
-  int32_t* pl;
-  int32_t* aux;
-  const int64_t* lo;
-  const int32_t* cnt;
-  const int32_t* pb;
-  int32_t len;  // image bytes
-};
-
 // The `w` low bytes of v at p (4-byte aligned for w = 8; naturally aligned otherwise).
 __device__ __forceinline__ void tc_put(uint8_t* p, uint64_t v, int w) {
   switch (w) {
@@ -133,364 +121,286 @@ __device__ __forceinline__ void tc_put(uint8_t* p, uint64_t v, int w) {
   }
 }
 
-// Hands var child / item instance k of node `node` its position `at` (if in the tile).
-__device__ __forceinline__ void tc_hand(const TcTables* T, const TcTile& t, int node, int64_t k, int32_t at) {
-  const int v = T->vidx[node];
-  const int64_t e = k - t.lo[v];
-  if (e >= 0 && e < t.cnt[v]) t.pl[t.pb[v] + e] = at;
-}
-
 // Slot size field of a var value: a string's byte length, else its bytes (decimals 32).
 __device__ __forceinline__ uint32_t tc_slot_size(const GNode& nd, const ColumnDev& col, int64_t k, int64_t bytes) {
   if (nd.kind == KIND_BYTES) return (uint32_t)(col.offsets[k + 1] - col.offsets[k]);
   return (uint32_t)bytes;
 }
 
-// A bean's (or the row's) fixed part at P: null bits, scalar slots (the value's bytes,
-// zero-extended: the image is zeroed), var slots (rel, size) + their children's positions.
-// Fields [first, end) of the schema, instance k. Returns false when they do not fit.
-__device__ __forceinline__ bool tc_fields(const GenLaunch& L, const TcTables* T, const TcTile& t, int first,
-                                          int end, int nf, int bm, int64_t k, int32_t P) {
-  int32_t at = P + bm + 8 * nf;
-  if (at > t.len) return false;
-  int q = 0;
+// A bean's (or the row's) fixed part at P — null bitmap, slots (scalars zero-extended,
+// nulls zero, var values (rel, size)) — and the positions of its var children; with
+// P < 0 (absent) only the children's -1. Fields [first, end) of the schema, instance k.
+__device__ __forceinline__ bool tc_fields(const GenLaunch& L, const TcTables* T, uint8_t* out, int64_t cap,
+                                          int first, int end, int nf, int bm, int64_t k, int64_t P) {
+  if (P < 0 || P + bm + 8LL * nf > cap) {
+    for (int ch = first; ch < end; ch = L.nodes[ch].end)
+      if (tc_is_var(L.nodes[ch].kind)) T->P[ch][k] = -1;
+    return P < 0;
+  }
+  int64_t at = P + bm + 8LL * nf;
+  uint32_t word = 0;  // null bits of fields [32 wq, 32 wq + 32)
+  int wq = 0, q = 0;
+  bool ok = true;
   for (int ch = first; ch < end; ch = L.nodes[ch].end, ++q) {
+    if ((q >> 5) != wq) {
+      st32(out + P + 4 * wq, word);
+      word = 0;
+      ++wq;
+    }
     const GNode nd = L.nodes[ch];
     const ColumnDev col = L.cols[ch];
-    uint8_t* slot = t.I + P + bm + 8 * q;
+    uint8_t* slot = out + P + bm + 8 * q;
+    const bool var = tc_is_var(nd.kind);
     if ((nd.flags & 1) && !gvalid(col.validity, k)) {  // setNullAt: bit, slot zero
-      t.I[P + (q >> 3)] |= (uint8_t)(1u << (q & 7));
+      word |= 1u << (q & 31);
+      tc_put(slot, 0, 8);
+      if (var) T->P[ch][k] = -1;
       continue;
     }
-    if (is_scalar(nd.kind)) {
+    if (!var) {  // putInt64(slot, 0) then the value: zero-extended to the slot
       uint64_t v = load_elem(col.values, nd.width, k);
       if (nd.kind == KIND_BOOL) v = v ? 1 : 0;
-      tc_put(slot, v, nd.width);
+      tc_put(slot, v, 8);
       continue;
     }
     const int64_t S = T->A[ch][k];
-    if (S < 0 || at + S > t.len) return false;
-    st32(slot, tc_slot_size(nd, col, k, S));
-    st32(slot + 4, (uint32_t)(at - P));
-    tc_hand(T, t, ch, k, at);
-    at += (int32_t)S;
+    if (S < 0 || at + S > cap) {
+      ok = false;
+      tc_put(slot, 0, 8);
+      T->P[ch][k] = -1;
+      continue;
+    }
+    tc_put(slot, ((uint64_t)(at - P) << 32) | tc_slot_size(nd, col, k, S), 8);
+    T->P[ch][k] = at;
+    at += S;
   }
-  return true;
+  st32(out + P + 4 * wq, word);
+  for (int w = wq + 1; w < bm / 4; ++w) st32(out + P + 4 * w, 0u);
+  return ok;
 }
 
-// aux of list / map instance g (entry v, node c): its first item relative to the tile's items.
-__device__ __forceinline__ int64_t tc_aux(const GenLaunch& L, const TcTables* T, const TcTile& t, int v, int c,
-                                          int g, int64_t k, int64_t* o1 = nullptr) {
-  int64_t o0, e1;
-  tc_items(L, T, c, k, &o0, &e1);
-  t.aux[t.pb[v] + g] = (int32_t)(o0 - t.lo[T->vidx[c + 1]]);
-  if (o1) *o1 = e1;
-  return o0;
+// Row / frame i: header, the row's fixed part and the top-level positions (or the
+// collection's position).
+__global__ __launch_bounds__(kTcWG) void tc_write_rows_kernel(GenLaunch L, const TcTables* __restrict__ T,
+                                                              const int64_t* __restrict__ offs,
+                                                              uint8_t* __restrict__ out, int64_t cap,
+                                                              int32_t* status) {
+  const int64_t i = (int64_t)blockIdx.x * kTcWG + threadIdx.x;
+  if (i >= L.num_rows) return;
+  const int64_t beg = offs[i], end = offs[i + 1];
+  const int coll = L.frame == FORY_FRAME_COLLECTION;
+  const int hdr = coll ? 4 : frame_header_bytes(L.frame);
+  const int64_t size = end - beg;
+  bool bad = beg < 0 || end > cap || size < hdr || size - hdr > 0x7fffffffLL || (beg & 3);
+  int64_t need = hdr + (coll ? 0 : L.fixed_size);
+  if (coll) need += T->A[0][i];
+  else
+    for (int c = 0; c < L.num_nodes; c = L.nodes[c].end)
+      if (tc_is_var(L.nodes[c].kind)) need += T->A[c][i];
+  if (need > size) bad = true;  // offsets not from these columns' sizes
+  if (bad) set_status(status, FORY_ERR_CAPACITY);
+  uint8_t* f = out + beg;
+  if (coll) {
+    if (!bad) st32(f, (uint32_t)(size - 4));
+    T->P[0][i] = bad ? -1 : beg + 4;
+    return;
+  }
+  if (!bad && hdr == 12) {  // Encoders.encode(MemoryBuffer, T): [i32 8 + rowSize][i64 hash]
+    st32(f, (uint32_t)(size - 4));
+    tc_put(f + 4, (uint64_t)L.schema_hash, 8);
+  } else if (!bad && hdr == 8) {  // Encoder.encode(T): [i64 hash]
+    tc_put(f, (uint64_t)L.schema_hash, 8);
+  }
+  const int nf = (L.fixed_size - L.bitmap_bytes) / 8;
+  if (!tc_fields(L, T, out, cap, 0, L.num_nodes, nf, L.bitmap_bytes, i, bad ? -1 : beg + hdr))
+    set_status(status, FORY_ERR_ENCODER);
 }
 
-// A var instance's own bytes (step A of a depth): string bytes, a decimal, a bean's fixed
-// part, an array's / map's headers (their elements are step B's). g: the instance's
-// index in the tile, v its entry.
-__device__ __forceinline__ int32_t tc_head(const GenLaunch& L, const TcTables* T, const TcTile& t, int v, int c,
-                                           int g, int64_t k, int32_t P) {
+// Strings, decimals, beans: lane per instance.
+__global__ __launch_bounds__(kTcWG) void tc_write_node_kernel(GenLaunch L, const TcTables* __restrict__ T, int c,
+                                                              int64_t m, uint8_t* __restrict__ out, int64_t cap,
+                                                              int32_t* status) {
+  const int64_t k = (int64_t)blockIdx.x * kTcWG + threadIdx.x;
+  if (k >= m) return;
   const GNode nd = L.nodes[c];
   const ColumnDev col = L.cols[c];
-  switch (nd.kind) {
-    case KIND_BYTES: {  // writeUnaligned + zeroOutPaddingBytes
-      const int64_t s0 = col.offsets[k], n = (int64_t)col.offsets[k + 1] - s0;
-      if (n < 0 || P + gr8(n) > t.len) return FORY_ERR_ENCODER;
-      g_put_bytes(t.I + P, col.values + s0, n);
-      return 0;
-    }
-    case KIND_DECIMAL: {  // BinaryWriter.writeDecimal
-      if (P + 32 > t.len) return FORY_ERR_ENCODER;
-      const uint8_t* x = col.values + 16 * k;
-      const uint32_t w[4] = {ld32(x), ld32(x + 4), ld32(x + 8), ld32(x + 12)};
-      if (!g_dec_fits(w, nd.prec)) return FORY_ERR_UNSUPPORTED;
+  const int64_t P = T->P[c][k];
+  int32_t err = 0;
+  if (nd.kind == KIND_STRUCT) {
+    if (!tc_fields(L, T, out, cap, c + 1, nd.end, nd.nchild, gbm(nd.nchild), k, P)) err = FORY_ERR_ENCODER;
+  } else if (P >= 0 && nd.kind == KIND_BYTES) {  // writeUnaligned + zeroOutPaddingBytes
+    const int64_t s0 = col.offsets[k], n = (int64_t)col.offsets[k + 1] - s0;
+    if (n < 0 || P + gr8(n) > cap) err = FORY_ERR_ENCODER;
+    else g_put_bytes(out + P, col.values + s0, n);
+  } else if (P >= 0 && nd.kind == KIND_DECIMAL) {  // BinaryWriter.writeDecimal
+    const uint8_t* x = col.values + 16 * k;
+    const uint32_t w[4] = {ld32(x), ld32(x + 4), ld32(x + 8), ld32(x + 12)};
+    if (P + 32 > cap) {
+      err = FORY_ERR_ENCODER;
+    } else if (!g_dec_fits(w, nd.prec)) {
+      err = FORY_ERR_UNSUPPORTED;
+    } else {
       const uint32_t ext = (w[3] >> 31) ? 0xffffffffu : 0u;
-      for (int q = 0; q < 4; ++q) st32(t.I + P + 4 * q, w[q]);
-      for (int q = 4; q < 8; ++q) st32(t.I + P + 4 * q, ext);
-      return 0;
+      for (int q = 0; q < 4; ++q) st32(out + P + 4 * q, w[q]);
+      for (int q = 4; q < 8; ++q) st32(out + P + 4 * q, ext);
     }
-    case KIND_STRUCT:
-      return tc_fields(L, T, t, c + 1, nd.end, nd.nchild, gbm(nd.nchild), k, P) ? 0 : FORY_ERR_ENCODER;
-    case KIND_LIST:
-    case KIND_MAP: {  // [i64 n] | [i64 key array bytes][i64 n ...keys][i64 n ...values]
-      int64_t o1;
-      const int64_t o0 = tc_aux(L, T, t, v, c, g, k, &o1);
-      const int64_t n = o1 - o0;
-      const int key = c + 1;
-      if (nd.kind == KIND_LIST) {
-        if (P + 8 + gbm(n) + gr8(n * elem_size(L.nodes[key])) > t.len) return FORY_ERR_ENCODER;
-        tc_put(t.I + P, (uint64_t)n, 8);
-        return 0;
-      }
-      const int val = L.nodes[key].end;
-      const int64_t kb = tc_array_bytes(L, T, key, o0, o1);
-      if (kb < 0 || P + 8 + kb + 8 + gbm(n) + gr8(n * elem_size(L.nodes[val])) > t.len) return FORY_ERR_ENCODER;
-      tc_put(t.I + P, (uint64_t)kb, 8);
-      tc_put(t.I + P + 8, (uint64_t)n, 8);
-      tc_put(t.I + P + 8 + kb, (uint64_t)n, 8);
-      return 0;
+  }
+  if (err) set_status(status, err);
+}
+
+// The null bitmap of items [o0, o0 + n) (1 = null, BinaryArrayWriter.setNullAt) from their
+// Arrow validity (1 = valid, none = all valid) at dst: gbm(n) bytes.
+__device__ __forceinline__ void tc_bitmap(uint8_t* dst, const uint8_t* validity, int64_t o0, int64_t n) {
+  const int nw = gbm(n) / 4;
+  for (int w = 0; w < nw; ++w) {
+    const int64_t rem = n - 32LL * w;
+    uint32_t bits = 0;
+    if (rem > 0 && validity) {
+      const int64_t b = o0 + 32LL * w;
+      const int sh = (int)(b & 7);
+      const int take = rem < 32 ? (int)rem : 32;
+      const int nb = (sh + take + 7) >> 3;
+      const uint8_t* v = validity + (b >> 3);
+      uint64_t win = 0;
+      for (int q = 0; q < nb; ++q) win |= (uint64_t)v[q] << (8 * q);
+      const uint32_t mask = take == 32 ? 0xffffffffu : ((1u << take) - 1u);
+      bits = ~(uint32_t)(win >> sh) & mask;
     }
-    default: return 0;
+    st32(dst + 4 * w, bits);
   }
 }
 
-// Item i (tile-relative) of entry xe under list / map entry v (step B): its element —
-// a null bit, a scalar, or a var item's slot + position. which: 0 list items, 1 keys,
-// 2 values.
-__device__ __forceinline__ int32_t tc_item(const GenLaunch& L, const TcTables* T, const TcTile& t, int v, int xe,
-                                           int x, int which, int i) {
-  const int cv = t.cnt[v];
-  const int32_t* aux = t.aux + t.pb[v];
-  int a = 0, b = cv - 1;  // the last instance whose items start at or before i
-  while (a < b) {
-    const int mid = (a + b + 1) >> 1;
-    if (aux[mid] <= i) a = mid;
-    else b = mid - 1;
-  }
-  const int32_t P = t.pl[t.pb[v] + a];
-  if (P < 0) return 0;  // a null / absent container
-  const int32_t o0 = aux[a], o1 = a + 1 < cv ? aux[a + 1] : t.cnt[xe];
-  const int64_t n = o1 - o0;
-  const int64_t q = i - o0;
-  const int32_t Pa = which == 0 ? P : (which == 1 ? P + 8 : P + 8 + (int32_t)ld32(t.I + P));
+// An array header at Pa: [i64 n][null bitmap][element padding]; returns its fixed bytes.
+__device__ __forceinline__ int64_t tc_array_head(const GenLaunch& L, uint8_t* out, int x, int64_t o0, int64_t n,
+                                                 int64_t Pa) {
+  const GNode it = L.nodes[x];
+  const int es = elem_size(it);
+  const int64_t hb = 8 + gbm(n), data = n * es, fixed = hb + gr8(data);
+  tc_put(out + Pa, (uint64_t)n, 8);
+  tc_bitmap(out + Pa + 8, (it.flags & 1) ? L.cols[x].validity : nullptr, o0, n);
+  for (int64_t b = data; b < gr8(data); ++b) out[Pa + hb + b] = 0;  // zeroOutPaddingBytes
+  return fixed;
+}
+
+// Element q of the array at Pa (n items from o0) of item node x: item e = o0 + q.
+__device__ __forceinline__ int32_t tc_element(const GenLaunch& L, const TcTables* T, uint8_t* out, int64_t cap,
+                                              int x, int64_t o0, int64_t n, int64_t Pa, int64_t e) {
   const GNode it = L.nodes[x];
   const ColumnDev col = L.cols[x];
   const int es = elem_size(it);
-  const int32_t hb = 8 + gbm(n);
-  if (q < 0 || q >= n || Pa + hb + gr8(n * es) > t.len) return FORY_ERR_ENCODER;
-  const int64_t e = t.lo[xe] + i;
-  if ((it.flags & 1) && !gvalid(col.validity, e)) {  // setNullAt: the element bit
-    atomicOr(reinterpret_cast<uint32_t*>(t.I + Pa + 8) + (q >> 5), 1u << (q & 31));
+  const int64_t q = e - o0;
+  const int64_t hb = 8 + gbm(n);
+  uint8_t* el = out + Pa + hb + q * es;
+  const bool var = tc_is_var(it.kind);
+  if ((it.flags & 1) && !gvalid(col.validity, e)) {  // null: zero element (the header set the bit)
+    tc_put(el, 0, es);
+    if (var) T->P[x][e] = -1;
     return 0;
   }
-  if (is_scalar(it.kind)) {
-    uint64_t val = load_elem(col.values, es, e);
-    if (it.kind == KIND_BOOL) val = val ? 1 : 0;
-    tc_put(t.I + Pa + hb + q * es, val, es);
+  if (!var) {
+    uint64_t v = load_elem(col.values, es, e);
+    if (it.kind == KIND_BOOL) v = v ? 1 : 0;
+    tc_put(el, v, es);
     return 0;
   }
   const int64_t* A = T->A[x];
   const int64_t S = A[e + 1] - A[e];
-  const int64_t at = Pa + hb + gr8(n * 8) + (A[e] - A[t.lo[xe] + o0]);
-  if (S < 0 || at < 0 || at + S > t.len) return FORY_ERR_ENCODER;
-  uint8_t* slot = t.I + Pa + hb + 8 * q;
-  st32(slot, tc_slot_size(it, col, e, S));
-  st32(slot + 4, (uint32_t)(at - Pa));
-  tc_hand(T, t, x, e, (int32_t)at);
+  const int64_t at = Pa + hb + gr8(n * 8) + (A[e] - A[o0]);
+  if (S < 0 || at + S > cap) {
+    tc_put(el, 0, 8);
+    T->P[x][e] = -1;
+    return FORY_ERR_ENCODER;
+  }
+  tc_put(el, ((uint64_t)(at - Pa) << 32) | tc_slot_size(it, col, e, S), 8);
+  T->P[x][e] = at;
   return 0;
 }
 
-// Row / frame i: header, then the row's fixed part (or the collection's position).
-__device__ __forceinline__ void tc_row(const GenLaunch& L, const TcTables* T, const TcTile& t,
-                                       const int64_t* offs, int64_t base, int64_t i, int32_t* status) {
-  const int64_t fb = offs[i] - base, fe = offs[i + 1] - base;
-  const int coll = L.frame == FORY_FRAME_COLLECTION;
-  const int hdr = coll ? 4 : frame_header_bytes(L.frame);
-  const int64_t size = fe - fb;
-  if (fb < 0 || fe > t.len || size < hdr || size - hdr > 0x7fffffffLL) {
-    set_status(status, FORY_ERR_CAPACITY);
-    return;
-  }
-  uint8_t* f = t.I + fb;
-  if (coll) {
-    if (4 + T->A[0][i] > size) {  // offsets not from these columns' sizes
-      set_status(status, FORY_ERR_CAPACITY);
-      return;
-    }
-    st32(f, (uint32_t)(size - 4));
-    tc_hand(T, t, 0, i, (int32_t)fb + 4);
-    return;
-  }
-  int64_t need = hdr + L.fixed_size;
-  for (int c = 0; c < L.num_nodes; c = L.nodes[c].end)
-    if (tc_is_var(L.nodes[c].kind)) need += T->A[c][i];
-  if (need > size) {
-    set_status(status, FORY_ERR_CAPACITY);
-    return;
-  }
-  if (hdr == 12) {  // Encoders.encode(MemoryBuffer, T): [i32 8 + rowSize][i64 hash]
-    st32(f, (uint32_t)(size - 4));
-    tc_put(f + 4, (uint64_t)L.schema_hash, 8);
-  } else if (hdr == 8) {  // Encoder.encode(T): [i64 hash]
-    tc_put(f, (uint64_t)L.schema_hash, 8);
-  }
-  const int nf = (L.fixed_size - L.bitmap_bytes) / 8;
-  if (!tc_fields(L, T, t, 0, L.num_nodes, nf, L.bitmap_bytes, i, (int32_t)(fb + hdr)))
-    set_status(status, FORY_ERR_ENCODER);
-}
-
-__global__ __launch_bounds__(kTcWG) void tc_tiles_kernel(TcLaunch W, const int64_t* __restrict__ offs) {
-  const int64_t i = (int64_t)blockIdx.x * kTcWG + threadIdx.x;
-  const int64_t n = W.g.num_rows;
-  if (i > n) return;
-  const int64_t B = W.tile_bytes;
-  const int64_t prev = i == 0 ? -1 : offs[i - 1];
-  int64_t t0 = prev < 0 ? 0 : prev / B + 1;  // tiles t with prev < t x B <= offs[i]
-  int64_t t1 = i == n ? W.ntiles : offs[i] / B;
-  if (t1 > W.ntiles) t1 = W.ntiles;
-  for (int64_t t = t0; t <= t1; ++t) W.tiles[t] = i;
-}
-
-template <int D>
-__global__ __launch_bounds__(kTcWG) void tc_encode_kernel(TcLaunch W, const int64_t* __restrict__ offs,
-                                                          uint8_t* __restrict__ out, int64_t capacity,
-                                                          int32_t* status) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_img[kTcImg + 16];
-  __shared__ int32_t s_pl[kTcPl], s_aux[kTcPl];
-  __shared__ int64_t s_lo[kTcMaxNodes];
-  __shared__ int32_t s_cnt[kTcMaxNodes], s_pb[kTcMaxNodes];
-  __shared__ int64_t s_base, s_end;
-  __shared__ int32_t s_mode, s_tot;
-  const GenLaunch& L = W.g;
-  const TcTables* T = W.T;
+// Lists / maps: a workgroup per kTcWG containers. Headers lane per container, then the
+// elements item-parallel over the workgroup's items.
+__global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const TcTables* __restrict__ T, int c,
+                                                              int64_t m, uint8_t* __restrict__ out, int64_t cap,
+                                                              int32_t* status) {
+  __shared__ int64_t sP[kTcWG];   // container position (-1: absent / null / does not fit)
+  __shared__ int32_t sO[kTcWG + 1];  // first item of each container (+ the end)
+  __shared__ int32_t sK[kTcWG];   // maps: key array bytes
   const int tid = threadIdx.x;
-  const int64_t r0 = W.tiles[blockIdx.x], r1 = W.tiles[blockIdx.x + 1];
-  if (r0 >= r1) return;  // no row starts in this tile's bytes
-  if (r0 < 0 || r1 > L.num_rows) {  // offsets not ascending
-    if (tid == 0) set_status(status, FORY_ERR_CAPACITY);
-    return;
-  }
-  if (tid == 0) {
-    s_base = offs[r0];
-    s_end = offs[r1];
-  }
-  // instance ranges, depth by depth (an item range reads the parent's offsets)
-  const int depths = T->depths;
-  for (int d = 1; d <= depths; ++d) {
-    for (int v = T->phase[d - 1] + tid; v < T->phase[d]; v += kTcWG) {
-      const TcVar tv = T->var[v];
-      int64_t lo, hi;
-      if (tv.parent < 0) {
-        lo = r0;
-        hi = r1;
-      } else if (!tv.items) {
-        lo = s_lo[tv.parent];
-        hi = lo + s_cnt[tv.parent];
+  const int64_t j0 = (int64_t)blockIdx.x * kTcWG;
+  const int cnt = m - j0 < kTcWG ? (int)(m - j0) : kTcWG;
+  const GNode nd = L.nodes[c];
+  const bool map = nd.kind == KIND_MAP;
+  const int key = c + 1, val = map ? L.nodes[key].end : -1;
+  const int64_t mx = T->m[key];
+  int32_t err = 0;
+  if (tid < cnt) {
+    const int64_t j = j0 + tid;
+    int64_t o0, o1;
+    tc_items(L, T, c, j, &o0, &o1);
+    const int64_t n = o1 - o0;
+    int64_t P = T->P[c][j];
+    int64_t kb = 0;
+    if (P >= 0) {
+      const int64_t need = map ? 8 + tc_array_bytes(L, T, key, o0, o1) + tc_array_bytes(L, T, val, o0, o1)
+                               : tc_array_bytes(L, T, key, o0, o1);
+      if (P + need > cap) {
+        err = FORY_ERR_ENCODER;
+        P = -1;
+      }
+    }
+    if (P >= 0) {
+      if (map) {  // [i64 key array bytes][key array][value array]
+        kb = tc_array_bytes(L, T, key, o0, o1);
+        tc_put(out + P, (uint64_t)kb, 8);
+        tc_array_head(L, out, key, o0, n, P + 8);
+        tc_array_head(L, out, val, o0, n, P + 8 + kb);
       } else {
-        const int32_t* po = L.cols[T->var[tv.parent].node].offsets;
-        const int64_t mx = T->m[tv.node], a = s_lo[tv.parent];
-        lo = tc_clamp(po[a], mx);
-        hi = tc_clamp(po[a + s_cnt[tv.parent]], mx);
-        if (hi < lo) hi = lo;
-      }
-      s_lo[v] = lo;
-      s_cnt[v] = hi - lo > (1 << 30) ? (1 << 30) : (int32_t)(hi - lo);
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    int32_t tot = 0;
-    bool fit = true;
-    for (int v = 0; v < T->nvar; ++v) {
-      s_pb[v] = tot;
-      if (T->var[v].var) tot += s_cnt[v];
-      if (s_cnt[v] == (1 << 30) || tot > kTcPl) {
-        fit = false;
-        tot = kTcPl;
+        tc_array_head(L, out, key, o0, n, P);
       }
     }
-    const int64_t base = s_base, end = s_end;
-    int mode = 0;
-    if (base < 0 || end < base || end > capacity) {
-      set_status(status, FORY_ERR_CAPACITY);
-      mode = 2;
-    } else if (!fit || ((base | end) & 3) ||
-               end - base + (int64_t)((reinterpret_cast<uintptr_t>(out) + base) & 15) > kTcImg) {
-      mode = 1;
-    }
-    s_mode = mode;
-    s_tot = tot;
+    sP[tid] = P;
+    sO[tid] = (int32_t)o0;
+    sK[tid] = (int32_t)kb;
+    if (tid == cnt - 1) sO[cnt] = (int32_t)o1;
   }
   __syncthreads();
-  const int mode = s_mode;
-  if (mode == 2) return;
-  if (mode == 1) {  // too large for the image: the per-lane engine, row by row
-    for (int64_t i = r0 + tid; i < r1; i += kTcWG) gen_encode_one<D>(L, offs, out, capacity, status, i);
-    return;
-  }
-  const int64_t base = s_base;
-  const int mis = (int)((reinterpret_cast<uintptr_t>(out) + base) & 15);
-  const int32_t len = (int32_t)(s_end - base);
-  const int zn = (mis + len + 15) >> 4;
-  for (int q = tid; q < zn; q += kTcWG) reinterpret_cast<u32x4*>(s_img)[q] = u32x4{0u, 0u, 0u, 0u};
-  for (int q = tid; q < s_tot; q += kTcWG) s_pl[q] = -1;
-  __syncthreads();
-  TcTile t;
-  t.I = s_img + mis;
-  t.pl = s_pl;
-  t.aux = s_aux;
-  t.lo = s_lo;
-  t.cnt = s_cnt;
-  t.pb = s_pb;
-  t.len = len;
-  for (int64_t i = r0 + tid; i < r1; i += kTcWG) tc_row(L, T, t, offs, base, i, status);
-  __syncthreads();
-  for (int d = 1; d <= depths; ++d) {
-    const int v0 = T->phase[d - 1], v1 = T->phase[d];
-    // A: the depth's var instances (rot spreads the nodes over the waves)
-    int rot = 0;
-    for (int v = v0; v < v1; ++v) {
-      const TcVar tv = T->var[v];
-      if (!tv.var) continue;
-      const int cnt = s_cnt[v];
-      const int32_t* pl = s_pl + s_pb[v];
-      const int kind = L.nodes[tv.node].kind;
-      const bool cont = kind == KIND_LIST || kind == KIND_MAP;
-      for (int g = (tid - rot) & (kTcWG - 1); g < cnt; g += kTcWG) {
-        const int32_t P = pl[g];
-        if (P < 0) {  // a null / absent container still delimits the items' search
-          if (cont) tc_aux(L, T, t, v, tv.node, g, s_lo[v] + g);
-          continue;
-        }
-        const int32_t err = tc_head(L, T, t, v, tv.node, g, s_lo[v] + g, P);
-        if (err) set_status(status, err);
-      }
-      rot = (rot + cnt) & (kTcWG - 1);
+  const int64_t e0 = sO[0], e1 = sO[cnt];
+  const bool kvar = tc_is_var(L.nodes[key].kind), vvar = map && tc_is_var(L.nodes[val].kind);
+  for (int64_t e = e0 + tid; e < e1; e += kTcWG) {
+    int a = 0, b = cnt - 1;  // the last container whose items start at or before e
+    while (a < b) {
+      const int mid = (a + b + 1) >> 1;
+      if (sO[mid] <= e) a = mid;
+      else b = mid - 1;
     }
-    __syncthreads();
-    // B: the elements of the depth's arrays and maps, item-parallel
-    bool any = false;
-    for (int v = v0; v < v1; ++v) {
-      const TcVar tv = T->var[v];
-      if (!tv.var) continue;
-      const int kind = L.nodes[tv.node].kind;
-      if (kind != KIND_LIST && kind != KIND_MAP) continue;
-      any = true;
-      for (int which = kind == KIND_LIST ? 0 : 1; which <= (kind == KIND_LIST ? 0 : 2); ++which) {
-        const int x = which == 2 ? L.nodes[tv.node + 1].end : tv.node + 1;
-        const int xe = T->vidx[x];
-        const int cnt = s_cnt[xe];
-        for (int i = (tid - rot) & (kTcWG - 1); i < cnt; i += kTcWG) {
-          const int32_t err = tc_item(L, T, t, v, xe, x, which, i);
-          if (err) set_status(status, err);
-        }
-        rot = (rot + cnt) & (kTcWG - 1);
-      }
+    const int64_t P = sP[a];
+    const int64_t o0 = sO[a], n = sO[a + 1] - o0;
+    if (P < 0 || e >= o0 + n) {  // absent container (or items between non-adjacent ranges)
+      if (kvar) T->P[key][e] = -1;
+      if (vvar) T->P[val][e] = -1;
+      continue;
     }
-    if (any) __syncthreads();
+    int32_t r;
+    if (map) {
+      r = tc_element(L, T, out, cap, key, o0, n, P + 8, e);
+      const int32_t r2 = tc_element(L, T, out, cap, val, o0, n, P + 8 + sK[a], e);
+      if (!r) r = r2;
+    } else {
+      r = tc_element(L, T, out, cap, key, o0, n, P, e);
+    }
+    if (r) err = r;
   }
-  // the image to [base, end): 16-byte stores between dword head / tail
-  uint8_t* o = out + base;
-  const int head = (16 - mis) & 15;  // bytes before the first 16-byte boundary
-  const int h = head < len ? head : len;
-  if (tid < (h >> 2)) st32(o + 4 * tid, ld32(t.I + 4 * tid));
-  const int body = (len - h) >> 4;
-  for (int q = tid; q < body; q += kTcWG)
-    *gp(reinterpret_cast<u32x4*>(o + h) + q) = reinterpret_cast<const u32x4*>(t.I + h)[q];
-  const int tail0 = h + 16 * body;
-  const int tw = (len - tail0) >> 2;
-  if (tid < tw) st32(o + tail0 + 4 * tid, ld32(t.I + tail0 + 4 * tid));
-}
-
-template <int D>
-hipError_t launch_tc_encode_d(const TcLaunch& W, const int64_t* offs, uint8_t* out, int64_t capacity,
-                              int32_t* status, hipStream_t s) {
-  hipLaunchKernelGGL(tc_encode_kernel<D>, dim3((unsigned)W.ntiles), dim3(kTcWG), 0, s, W, offs, out, capacity,
-                     status);
-  return hipGetLastError();
+  // items no container of the call references: no position
+  if (blockIdx.x == 0 && (kvar || vvar))
+    for (int64_t e = tid; e < e0; e += kTcWG) {
+      if (kvar) T->P[key][e] = -1;
+      if (vvar) T->P[val][e] = -1;
+    }
+  if (j0 + cnt == m && (kvar || vvar))
+    for (int64_t e = e1 + tid; e < mx; e += kTcWG) {
+      if (kvar) T->P[key][e] = -1;
+      if (vvar) T->P[val][e] = -1;
+    }
+  if (err) set_status(status, err);
 }
 
 }  // namespace
@@ -510,18 +420,23 @@ hipError_t launch_tc_rows(const GenLaunch& L, const TcTables* T, int64_t* sizes,
   return hipGetLastError();
 }
 
-hipError_t launch_tc_tiles(const TcLaunch& W, const int64_t* offs, hipStream_t s) {
-  const int64_t n = W.g.num_rows + 1;
-  hipLaunchKernelGGL(tc_tiles_kernel, dim3((unsigned)((n + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s, W, offs);
+hipError_t launch_tc_write_rows(const GenLaunch& L, const TcTables* T, const int64_t* offs, uint8_t* out,
+                                int64_t capacity, int32_t* status, hipStream_t s) {
+  if (L.num_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tc_write_rows_kernel, dim3((unsigned)((L.num_rows + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s, L,
+                     T, offs, out, capacity, status);
   return hipGetLastError();
 }
 
-hipError_t launch_tc_encode(const TcLaunch& W, const int64_t* offs, uint8_t* out, int64_t capacity,
-                            int32_t* status, hipStream_t s) {
-  if (W.g.num_rows <= 0 || W.ntiles <= 0) return hipSuccess;
-  if (W.g.max_depth + 1 <= 4) return launch_tc_encode_d<4>(W, offs, out, capacity, status, s);
-  if (W.g.max_depth + 1 <= 8) return launch_tc_encode_d<8>(W, offs, out, capacity, status, s);
-  return launch_tc_encode_d<18>(W, offs, out, capacity, status, s);
+hipError_t launch_tc_write_node(const GenLaunch& L, const TcTables* T, int node, int64_t m, uint8_t* out,
+                                int64_t capacity, int32_t* status, hipStream_t s, int kind) {
+  if (m <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((m + kTcWG - 1) / kTcWG));
+  if (kind == KIND_LIST || kind == KIND_MAP)
+    hipLaunchKernelGGL(tc_write_cont_kernel, grid, dim3(kTcWG), 0, s, L, T, node, m, out, capacity, status);
+  else
+    hipLaunchKernelGGL(tc_write_node_kernel, grid, dim3(kTcWG), 0, s, L, T, node, m, out, capacity, status);
+  return hipGetLastError();
 }
 
 }  // namespace fory_amd

@@ -1,11 +1,11 @@
 """GPU: the columnar tree engine (fury_amd/csrc/treecol.hip) at its edges.
 
-Nested shapes are sized node by node and written by tiles of rows through an LDS
-image; these tests take it where its tiles and tables run out — rows bigger than the
-image and tiles with more instances than the position table (the per-record engine
-encodes those tiles), collection frames, the workspace contract (encode_workspace_bytes
-vs workspace_bytes) and the sizes encode reuses from encoded_size (and must not reuse
-after another call wrote the workspace). Every output is compared byte for byte with the
+Nested shapes are sized node by node and written node by node (rows, then each var
+node's instances at the positions their parents handed down); these tests take it to
+rows of ~100 KiB among small ones, containers of thousands of items, collection
+frames, the workspace contract (encode_workspace_bytes vs workspace_bytes) and the
+sizes encode reuses from encoded_size (and must not reuse after another call wrote the
+workspace). Every output is compared byte for byte with the
 oracle (oracle/rowfmt_oracle.c, BaseBinaryEncoderBuilder.serializeFor's layout).
 """
 from typing import Dict, List
@@ -42,9 +42,9 @@ def _big_rows_schema():
 
 
 @pytest.mark.parametrize("frame", [0, 1, 3])
-def test_rows_larger_than_the_tile_image(frame):
-    """A few rows of ~100 KiB (3000 strings) among small ones: their tiles take the
-    per-record engine, the others the LDS image; one output, oracle bytes."""
+def test_rows_of_100k_among_small_ones(frame):
+    """A few rows of ~100 KiB (3000 strings) among small ones (one workgroup's items
+    span thousands of elements); oracle bytes."""
     schema = _big_rows_schema()
     rng = np.random.default_rng(1)
     rows = []
@@ -60,8 +60,8 @@ def test_rows_larger_than_the_tile_image(frame):
     oracle_equal(schema, cols, len(rows), frame, enc.encode(to_device(cols), len(rows), frame))
 
 
-def test_tiles_with_more_instances_than_the_position_table():
-    """Rows of ~6000 short lists each (more instances than one tile's position table)."""
+def test_rows_of_thousands_of_lists():
+    """Rows of ~6000 short lists each (inner lists of one item, 6000 per outer list)."""
     schema = _big_rows_schema()
     rows = [{"id": i, "names": [], "grid": [[i % 7] for _ in range(6000 if i % 3 == 0 else 2)], "tag": "x"}
             for i in range(40)]
