@@ -564,6 +564,10 @@ int prepare_gen(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
 
 // --- columnar tree engine (treecol.hip) -------------------------------------
 bool tc_var_kind(int k) { return k != fory_amd::KIND_FIXED && k != fory_amd::KIND_BOOL; }
+bool tc_leaf_kind(int k) { return k == fory_amd::KIND_BYTES || k == fory_amd::KIND_DECIMAL; }
+// Sizes (A): beans / lists / maps and item nodes; positions (P): beans / lists / maps.
+bool tc_needs_sizes(const Plan& p, const fory_amd::TcVar& v) { return v.items || !tc_leaf_kind(p.nodes[v.node].kind); }
+bool tc_needs_pos(const Plan& p, const fory_amd::TcVar& v) { return !tc_leaf_kind(p.nodes[v.node].kind); }
 
 void build_tc(fory_plan* plan) {
   const Plan& p = plan->p;
@@ -617,7 +621,8 @@ int64_t tc_bytes(const fory_plan* plan, const std::vector<int64_t>& m) {
   const TcInfo& t = plan->tc;
   int64_t maxm = 0, arrays = 0;
   for (const fory_amd::TcVar& v : t.var) {
-    arrays += 2 * align_up((m[v.node] + 1) * 8);  // sizes, positions
+    if (tc_needs_sizes(plan->p, v)) arrays += align_up((m[v.node] + 1) * 8);
+    if (tc_needs_pos(plan->p, v)) arrays += align_up((m[v.node] + 1) * 8);
     if (v.items) maxm = std::max(maxm, m[v.node]);
   }
   return align_up((int64_t)sizeof(fory_amd::TcTables)) + align_up((fory_amd::scan_partials(maxm) + 2) * 8) + arrays;
@@ -700,10 +705,14 @@ int tc_prepare(const fory_plan* plan, const fory_column* cols, int64_t n, void* 
   for (size_t v = 0; v < t.var.size(); ++v) {
     T->var[v] = t.var[v];
     const int node = t.var[v].node;
-    T->A[node] = reinterpret_cast<int64_t*>(at);
-    at += align_up((m[node] + 1) * 8);
-    T->P[node] = reinterpret_cast<int64_t*>(at);
-    at += align_up((m[node] + 1) * 8);
+    if (tc_needs_sizes(plan->p, t.var[v])) {
+      T->A[node] = reinterpret_cast<int64_t*>(at);
+      at += align_up((m[node] + 1) * 8);
+    }
+    if (tc_needs_pos(plan->p, t.var[v])) {
+      T->P[node] = reinterpret_cast<int64_t*>(at);
+      at += align_up((m[node] + 1) * 8);
+    }
   }
   T->nvar = (int32_t)t.var.size();
   T->depths = t.var.empty() ? 0 : t.var.back().depth;
@@ -717,6 +726,7 @@ int tc_sizes(const fory_plan* plan, const fory_amd::GenLaunch& G, const fory_amd
   const TcInfo& t = plan->tc;
   for (int v = (int)t.var.size() - 1; v >= 0; --v) {  // deepest first
     const fory_amd::TcVar& tv = t.var[(size_t)v];
+    if (!tc_needs_sizes(plan->p, tv)) continue;  // strings / decimals in rows and beans: sized in place
     const int64_t m = T.m[tv.node];
     hipError_t e = fory_amd::launch_tc_sizes(G, dT, tv.node, m, G.frame == FORY_FRAME_COLLECTION && tv.node == 0, s);
     if (e != hipSuccess) return hip_fail(e, "tc_sizes");
@@ -946,6 +956,7 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
       e = fory_amd::launch_tc_write_rows(G, dT, d_row_offsets, out, out_capacity, d_status, s);
       for (size_t v = 0; v < plan->tc.var.size() && e == hipSuccess; ++v) {
         const int node = plan->tc.var[v].node;
+        if (!tc_needs_pos(p, plan->tc.var[v])) continue;  // written by their parents
         e = fory_amd::launch_tc_write_node(G, dT, node, T.m[node], out, out_capacity, d_status, s, p.nodes[node].kind);
       }
       return e == hipSuccess ? FORY_OK : hip_fail(e, "tc_write");

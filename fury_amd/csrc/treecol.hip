@@ -14,15 +14,16 @@
 //           items before k, A[x][m] = all of them.
 //   rows    row / frame size = header + fixed part + the top-level var fields' sizes;
 //           scanned into the row offsets (encoded_size's output).
-//   write   top-down, one launch per var node (parents first). Lane per row: frame
-//           header, null bits, slots, and the top-level var fields' positions. Lane per
-//           string / decimal / bean instance at its position: its bytes, or its fixed
-//           part and its children's positions. Lists / maps: a workgroup per 256
+//   write   top-down, one launch per bean / list / map node (parents first). Lane per
+//           row: frame header, null bits, slots, strings and decimals in place, and the
+//           positions of the top-level beans / lists / maps. Lane per bean instance at its
+//           position: the same for its fields. Lists / maps: a workgroup per 256
 //           containers writes their headers (count, null bitmap from the items'
 //           validity, element padding), then their elements item-parallel — each item
 //           finds its container by a binary search over the workgroup's item starts in
 //           LDS, writes its element (value, zero, or var slot) and a var item's position
-//           (the container's data start + the items' scanned sizes before it).
+//           (the container's data start + the items' scanned sizes before it), a
+//           string / decimal item in place.
 // Every byte of a record is written once (fixed parts whole, zero slots included), so
 // the output needs no clearing. Absent instances (under a null parent) get position -1
 // and write nothing.
@@ -34,6 +35,20 @@ namespace {
 constexpr int kTcWG = 256;
 
 __device__ __forceinline__ bool tc_is_var(int kind) { return !is_scalar(kind); }
+// Strings and decimals are leaves: their parent writes them in place (no positions) and
+// sizes them from their own column unless they are items (whose sizes are scanned).
+__device__ __forceinline__ bool tc_leaf(int kind) { return kind == KIND_BYTES || kind == KIND_DECIMAL; }
+__device__ __forceinline__ bool tc_has_pos(int kind) { return tc_is_var(kind) && !tc_leaf(kind); }
+
+// Bytes var value k of (non-item) node c adds to its parent; 0 when null.
+__device__ __forceinline__ int64_t tc_size(const TcTables* T, int c, const GNode& nd, const ColumnDev& col,
+                                           int64_t k) {
+  if (nd.kind == KIND_BYTES || nd.kind == KIND_DECIMAL) {
+    if ((nd.flags & 1) && !gvalid(col.validity, k)) return 0;
+    return nd.kind == KIND_DECIMAL ? 32 : gr8((int64_t)col.offsets[k + 1] - col.offsets[k]);
+  }
+  return T->A[c][k];
+}
 
 __device__ __forceinline__ int64_t tc_clamp(int64_t k, int64_t m) { return k < 0 ? 0 : (k > m ? m : k); }
 
@@ -73,8 +88,10 @@ __global__ __launch_bounds__(kTcWG) void tc_sizes_kernel(GenLaunch L, const TcTa
       case KIND_DECIMAL: s = 32; break;
       case KIND_STRUCT:
         s = gbm(nd.nchild) + 8LL * nd.nchild;
-        for (int ch = c + 1; ch < nd.end; ch = L.nodes[ch].end)
-          if (tc_is_var(L.nodes[ch].kind)) s += T->A[ch][j];
+        for (int ch = c + 1; ch < nd.end; ch = L.nodes[ch].end) {
+          const GNode cn = L.nodes[ch];
+          if (tc_is_var(cn.kind)) s += tc_size(T, ch, cn, L.cols[ch], j);
+        }
         break;
       case KIND_LIST:
       case KIND_MAP: {
@@ -99,8 +116,10 @@ __global__ __launch_bounds__(kTcWG) void tc_rows_kernel(GenLaunch L, const TcTab
     s = 4 + T->A[0][i];
   } else {
     s = frame_header_bytes(L.frame) + L.fixed_size;
-    for (int t = 0; t < L.num_nodes; t = L.nodes[t].end)
-      if (tc_is_var(L.nodes[t].kind)) s += T->A[t][i];
+    for (int t = 0; t < L.num_nodes; t = L.nodes[t].end) {
+      const GNode tn = L.nodes[t];
+      if (tc_is_var(tn.kind)) s += tc_size(T, t, tn, L.cols[t], i);
+    }
   }
   sizes[i] = s;
 }
@@ -127,20 +146,38 @@ __device__ __forceinline__ uint32_t tc_slot_size(const GNode& nd, const ColumnDe
   return (uint32_t)bytes;
 }
 
+// A leaf value at `at` (room checked by the caller): writeUnaligned + zeroOutPaddingBytes,
+// or BinaryWriter.writeDecimal (checkPrecisionAndScale: FORY_ERR_UNSUPPORTED).
+__device__ __forceinline__ int32_t tc_leaf_write(uint8_t* out, const GNode& nd, const ColumnDev& col, int64_t k,
+                                                 int64_t at) {
+  if (nd.kind == KIND_BYTES) {
+    const int64_t s0 = col.offsets[k];
+    g_put_bytes(out + at, col.values + s0, (int64_t)col.offsets[k + 1] - s0);
+    return 0;
+  }
+  const uint8_t* x = col.values + 16 * k;
+  const uint32_t w[4] = {ld32(x), ld32(x + 4), ld32(x + 8), ld32(x + 12)};
+  if (!g_dec_fits(w, nd.prec)) return FORY_ERR_UNSUPPORTED;
+  const uint32_t ext = (w[3] >> 31) ? 0xffffffffu : 0u;
+  for (int q = 0; q < 4; ++q) st32(out + at + 4 * q, w[q]);
+  for (int q = 4; q < 8; ++q) st32(out + at + 4 * q, ext);
+  return 0;
+}
+
 // A bean's (or the row's) fixed part at P — null bitmap, slots (scalars zero-extended,
 // nulls zero, var values (rel, size)) — and the positions of its var children; with
 // P < 0 (absent) only the children's -1. Fields [first, end) of the schema, instance k.
-__device__ __forceinline__ bool tc_fields(const GenLaunch& L, const TcTables* T, uint8_t* out, int64_t cap,
-                                          int first, int end, int nf, int bm, int64_t k, int64_t P) {
+__device__ __forceinline__ int32_t tc_fields(const GenLaunch& L, const TcTables* T, uint8_t* out, int64_t cap,
+                                             int first, int end, int nf, int bm, int64_t k, int64_t P) {
   if (P < 0 || P + bm + 8LL * nf > cap) {
     for (int ch = first; ch < end; ch = L.nodes[ch].end)
-      if (tc_is_var(L.nodes[ch].kind)) T->P[ch][k] = -1;
-    return P < 0;
+      if (tc_has_pos(L.nodes[ch].kind)) T->P[ch][k] = -1;
+    return P < 0 ? 0 : FORY_ERR_ENCODER;
   }
   int64_t at = P + bm + 8LL * nf;
   uint32_t word = 0;  // null bits of fields [32 wq, 32 wq + 32)
   int wq = 0, q = 0;
-  bool ok = true;
+  int32_t err = 0;
   for (int ch = first; ch < end; ch = L.nodes[ch].end, ++q) {
     if ((q >> 5) != wq) {
       st32(out + P + 4 * wq, word);
@@ -154,7 +191,7 @@ __device__ __forceinline__ bool tc_fields(const GenLaunch& L, const TcTables* T,
     if ((nd.flags & 1) && !gvalid(col.validity, k)) {  // setNullAt: bit, slot zero
       word |= 1u << (q & 31);
       tc_put(slot, 0, 8);
-      if (var) T->P[ch][k] = -1;
+      if (tc_has_pos(nd.kind)) T->P[ch][k] = -1;
       continue;
     }
     if (!var) {  // putInt64(slot, 0) then the value: zero-extended to the slot
@@ -163,20 +200,26 @@ __device__ __forceinline__ bool tc_fields(const GenLaunch& L, const TcTables* T,
       tc_put(slot, v, 8);
       continue;
     }
-    const int64_t S = T->A[ch][k];
+    const bool leaf = tc_leaf(nd.kind);
+    const int64_t S = tc_size(T, ch, nd, col, k);
     if (S < 0 || at + S > cap) {
-      ok = false;
+      err = FORY_ERR_ENCODER;
       tc_put(slot, 0, 8);
-      T->P[ch][k] = -1;
+      if (!leaf) T->P[ch][k] = -1;
       continue;
     }
     tc_put(slot, ((uint64_t)(at - P) << 32) | tc_slot_size(nd, col, k, S), 8);
-    T->P[ch][k] = at;
+    if (leaf) {
+      const int32_t r = tc_leaf_write(out, nd, col, k, at);
+      if (r) err = r;
+    } else {
+      T->P[ch][k] = at;
+    }
     at += S;
   }
   st32(out + P + 4 * wq, word);
   for (int w = wq + 1; w < bm / 4; ++w) st32(out + P + 4 * w, 0u);
-  return ok;
+  return err;
 }
 
 // Row / frame i: header, the row's fixed part and the top-level positions (or the
@@ -195,8 +238,10 @@ __global__ __launch_bounds__(kTcWG) void tc_write_rows_kernel(GenLaunch L, const
   int64_t need = hdr + (coll ? 0 : L.fixed_size);
   if (coll) need += T->A[0][i];
   else
-    for (int c = 0; c < L.num_nodes; c = L.nodes[c].end)
-      if (tc_is_var(L.nodes[c].kind)) need += T->A[c][i];
+    for (int c = 0; c < L.num_nodes; c = L.nodes[c].end) {
+      const GNode cn = L.nodes[c];
+      if (tc_is_var(cn.kind)) need += tc_size(T, c, cn, L.cols[c], i);
+    }
   if (need > size) bad = true;  // offsets not from these columns' sizes
   if (bad) set_status(status, FORY_ERR_CAPACITY);
   uint8_t* f = out + beg;
@@ -212,39 +257,18 @@ __global__ __launch_bounds__(kTcWG) void tc_write_rows_kernel(GenLaunch L, const
     tc_put(f, (uint64_t)L.schema_hash, 8);
   }
   const int nf = (L.fixed_size - L.bitmap_bytes) / 8;
-  if (!tc_fields(L, T, out, cap, 0, L.num_nodes, nf, L.bitmap_bytes, i, bad ? -1 : beg + hdr))
-    set_status(status, FORY_ERR_ENCODER);
+  const int32_t err = tc_fields(L, T, out, cap, 0, L.num_nodes, nf, L.bitmap_bytes, i, bad ? -1 : beg + hdr);
+  if (err) set_status(status, err);
 }
 
-// Strings, decimals, beans: lane per instance.
+// Beans: lane per instance.
 __global__ __launch_bounds__(kTcWG) void tc_write_node_kernel(GenLaunch L, const TcTables* __restrict__ T, int c,
                                                               int64_t m, uint8_t* __restrict__ out, int64_t cap,
                                                               int32_t* status) {
   const int64_t k = (int64_t)blockIdx.x * kTcWG + threadIdx.x;
   if (k >= m) return;
   const GNode nd = L.nodes[c];
-  const ColumnDev col = L.cols[c];
-  const int64_t P = T->P[c][k];
-  int32_t err = 0;
-  if (nd.kind == KIND_STRUCT) {
-    if (!tc_fields(L, T, out, cap, c + 1, nd.end, nd.nchild, gbm(nd.nchild), k, P)) err = FORY_ERR_ENCODER;
-  } else if (P >= 0 && nd.kind == KIND_BYTES) {  // writeUnaligned + zeroOutPaddingBytes
-    const int64_t s0 = col.offsets[k], n = (int64_t)col.offsets[k + 1] - s0;
-    if (n < 0 || P + gr8(n) > cap) err = FORY_ERR_ENCODER;
-    else g_put_bytes(out + P, col.values + s0, n);
-  } else if (P >= 0 && nd.kind == KIND_DECIMAL) {  // BinaryWriter.writeDecimal
-    const uint8_t* x = col.values + 16 * k;
-    const uint32_t w[4] = {ld32(x), ld32(x + 4), ld32(x + 8), ld32(x + 12)};
-    if (P + 32 > cap) {
-      err = FORY_ERR_ENCODER;
-    } else if (!g_dec_fits(w, nd.prec)) {
-      err = FORY_ERR_UNSUPPORTED;
-    } else {
-      const uint32_t ext = (w[3] >> 31) ? 0xffffffffu : 0u;
-      for (int q = 0; q < 4; ++q) st32(out + P + 4 * q, w[q]);
-      for (int q = 4; q < 8; ++q) st32(out + P + 4 * q, ext);
-    }
-  }
+  const int32_t err = tc_fields(L, T, out, cap, c + 1, nd.end, nd.nchild, gbm(nd.nchild), k, T->P[c][k]);
   if (err) set_status(status, err);
 }
 
@@ -291,10 +315,10 @@ __device__ __forceinline__ int32_t tc_element(const GenLaunch& L, const TcTables
   const int64_t q = e - o0;
   const int64_t hb = 8 + gbm(n);
   uint8_t* el = out + Pa + hb + q * es;
-  const bool var = tc_is_var(it.kind);
+  const bool var = tc_is_var(it.kind), leaf = tc_leaf(it.kind);
   if ((it.flags & 1) && !gvalid(col.validity, e)) {  // null: zero element (the header set the bit)
     tc_put(el, 0, es);
-    if (var) T->P[x][e] = -1;
+    if (var && !leaf) T->P[x][e] = -1;
     return 0;
   }
   if (!var) {
@@ -308,10 +332,11 @@ __device__ __forceinline__ int32_t tc_element(const GenLaunch& L, const TcTables
   const int64_t at = Pa + hb + gr8(n * 8) + (A[e] - A[o0]);
   if (S < 0 || at + S > cap) {
     tc_put(el, 0, 8);
-    T->P[x][e] = -1;
+    if (!leaf) T->P[x][e] = -1;
     return FORY_ERR_ENCODER;
   }
   tc_put(el, ((uint64_t)(at - Pa) << 32) | tc_slot_size(it, col, e, S), 8);
+  if (leaf) return tc_leaf_write(out, it, col, e, at);
   T->P[x][e] = at;
   return 0;
 }
@@ -364,7 +389,7 @@ __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const
   }
   __syncthreads();
   const int64_t e0 = sO[0], e1 = sO[cnt];
-  const bool kvar = tc_is_var(L.nodes[key].kind), vvar = map && tc_is_var(L.nodes[val].kind);
+  const bool kvar = tc_has_pos(L.nodes[key].kind), vvar = map && tc_has_pos(L.nodes[val].kind);
   for (int64_t e = e0 + tid; e < e1; e += kTcWG) {
     int a = 0, b = cnt - 1;  // the last container whose items start at or before e
     while (a < b) {
