@@ -716,6 +716,14 @@ int tc_prepare(const fory_plan* plan, const fory_column* cols, int64_t n, void* 
   }
   T->nvar = (int32_t)t.var.size();
   T->depths = t.var.empty() ? 0 : t.var.back().depth;
+  int nk = 0;  // fields by parent: the rows', then each bean's
+  for (int32_t f : plan->p.top) T->kids[nk++] = f;
+  T->nroot = nk;
+  for (size_t i = 0; i < plan->p.nodes.size(); ++i) {
+    if (plan->p.nodes[i].kind != fory_amd::KIND_STRUCT) continue;
+    T->kid0[i] = nk;
+    for (int32_t ch : plan->p.nodes[i].children) T->kids[nk++] = ch;
+  }
   *dT = reinterpret_cast<const fory_amd::TcTables*>(base);
   return upload(base, T, (int64_t)sizeof(*T), s);
 }
@@ -953,11 +961,12 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
       }
       if (rc) return rc;
       uint8_t* out = static_cast<uint8_t*>(d_out);
-      e = fory_amd::launch_tc_write_rows(G, dT, d_row_offsets, out, out_capacity, d_status, s);
+      e = fory_amd::launch_tc_write_rows(G, dT, T.nroot, d_row_offsets, out, out_capacity, d_status, s);
       for (size_t v = 0; v < plan->tc.var.size() && e == hipSuccess; ++v) {
         const int node = plan->tc.var[v].node;
         if (!tc_needs_pos(p, plan->tc.var[v])) continue;  // written by their parents
-        e = fory_amd::launch_tc_write_node(G, dT, node, T.m[node], out, out_capacity, d_status, s, p.nodes[node].kind);
+        e = fory_amd::launch_tc_write_node(G, dT, node, T.m[node], out, out_capacity, d_status, s, p.nodes[node].kind,
+                                           (int)p.nodes[node].children.size());
       }
       return e == hipSuccess ? FORY_OK : hip_fail(e, "tc_write");
     }

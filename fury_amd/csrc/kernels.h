@@ -151,16 +151,18 @@ struct TcTables {               // device, in the workspace
   int64_t m[kTcMaxNodes];       // instances of each node in this call
   int32_t vidx[kTcMaxNodes];    // node -> entry, -1 for scalars
   TcVar var[kTcMaxNodes];       // entries by depth, pre-order within a depth
-  int32_t nvar, depths;
+  int32_t kids[kTcMaxNodes];    // fields by parent: the rows' top-level fields, then each bean's
+  int32_t kid0[kTcMaxNodes];    // bean node -> its first field in kids
+  int32_t nvar, depths, nroot;  // nroot: top-level fields
 };
 hipError_t launch_tc_sizes(const GenLaunch& L, const TcTables* T, int node, int64_t m, bool root_coll, hipStream_t s);
 hipError_t launch_tc_rows(const GenLaunch& L, const TcTables* T, int64_t* sizes, hipStream_t s);
 // Writes: the rows (frame headers, fixed parts, top-level positions), then each var node's
 // instances (node, m = its instance count), parents before children.
-hipError_t launch_tc_write_rows(const GenLaunch& L, const TcTables* T, const int64_t* offs, uint8_t* out,
+hipError_t launch_tc_write_rows(const GenLaunch& L, const TcTables* T, int nroot, const int64_t* offs, uint8_t* out,
                                 int64_t capacity, int32_t* status, hipStream_t s);
 hipError_t launch_tc_write_node(const GenLaunch& L, const TcTables* T, int node, int64_t m, uint8_t* out,
-                                int64_t capacity, int32_t* status, hipStream_t s, int kind);
+                                int64_t capacity, int32_t* status, hipStream_t s, int kind, int nchild);
 
 // Frame index of a STREAM batch (frames.hip): the starts of the first num_rows
 // frames of rows_bytes bytes, found on the device from the stream alone.

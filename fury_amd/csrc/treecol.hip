@@ -146,13 +146,40 @@ __device__ __forceinline__ uint32_t tc_slot_size(const GNode& nd, const ColumnDe
   return (uint32_t)bytes;
 }
 
+// g_put_bytes (n bytes + zero padding to 8 at a 4-byte aligned dst) with a short string's
+// source dwords all loaded before any store: one memory latency, not one per dword.
+__device__ __forceinline__ void tc_copy(uint8_t* dst, const uint8_t* src, int64_t n) {
+  constexpr int kW = 16;  // n <= 60: <= 16 source dwords, <= 16 output dwords with the padding
+  if (n > 60) {
+    g_put_bytes(dst, src, n);
+    return;
+  }
+  const int sh = (int)(reinterpret_cast<uintptr_t>(src) & 3);
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(src - sh);
+  const int nin = (sh + (int)n + 3) >> 2;  // source dwords holding string bytes
+  const int nout = (int)(gr8(n) >> 2);     // output dwords (string + padding)
+  uint32_t w[kW + 1];
+#pragma unroll
+  for (int k = 0; k < kW; ++k) w[k] = k < nin ? s[k] : 0u;
+  w[kW] = 0u;
+#pragma unroll
+  for (int k = 0; k < kW; ++k) {
+    if (k >= nout) break;
+    uint32_t v = sh ? (uint32_t)((((uint64_t)w[k + 1] << 32) | w[k]) >> (8 * sh)) : w[k];
+    const int left = (int)n - 4 * k;
+    if (left <= 0) v = 0u;
+    else if (left < 4) v &= (1u << (8 * left)) - 1u;
+    st32(dst + 4 * k, v);
+  }
+}
+
 // A leaf value at `at` (room checked by the caller): writeUnaligned + zeroOutPaddingBytes,
 // or BinaryWriter.writeDecimal (checkPrecisionAndScale: FORY_ERR_UNSUPPORTED).
 __device__ __forceinline__ int32_t tc_leaf_write(uint8_t* out, const GNode& nd, const ColumnDev& col, int64_t k,
                                                  int64_t at) {
   if (nd.kind == KIND_BYTES) {
     const int64_t s0 = col.offsets[k];
-    g_put_bytes(out + at, col.values + s0, (int64_t)col.offsets[k + 1] - s0);
+    tc_copy(out + at, col.values + s0, (int64_t)col.offsets[k + 1] - s0);
     return 0;
   }
   const uint8_t* x = col.values + 16 * k;
@@ -164,112 +191,128 @@ __device__ __forceinline__ int32_t tc_leaf_write(uint8_t* out, const GNode& nd, 
   return 0;
 }
 
-// A bean's (or the row's) fixed part at P — null bitmap, slots (scalars zero-extended,
-// nulls zero, var values (rel, size)) — and the positions of its var children; with
-// P < 0 (absent) only the children's -1. Fields [first, end) of the schema, instance k.
-__device__ __forceinline__ int32_t tc_fields(const GenLaunch& L, const TcTables* T, uint8_t* out, int64_t cap,
-                                             int first, int end, int nf, int bm, int64_t k, int64_t P) {
-  if (P < 0 || P + bm + 8LL * nf > cap) {
-    for (int ch = first; ch < end; ch = L.nodes[ch].end)
-      if (tc_has_pos(L.nodes[ch].kind)) T->P[ch][k] = -1;
-    return P < 0 ? 0 : FORY_ERR_ENCODER;
+// Rows and beans, field-parallel: one lane per (instance k, field q) writes the field's
+// slot — scalar zero-extended (putInt64(slot, 0) then the value), null zero, var
+// (rel, size) — and a string / decimal in place at its position (the fixed part's end +
+// the sizes of the var fields before it), or hands a bean / list / map field its
+// position. Lane q = 0 writes the null bitmap (and for rows the frame header, after the
+// row's size is checked against its offsets). Adjacent lanes write adjacent slots.
+// ROWS: instances are the rows (c unused); else bean node c at T->P[c] (-1: absent, its
+// bean / list / map fields get -1).
+template <bool ROWS>
+__global__ __launch_bounds__(kTcWG) void tc_write_fields_kernel(GenLaunch L, const TcTables* __restrict__ T, int c,
+                                                                int64_t m, const int64_t* __restrict__ offs,
+                                                                uint8_t* __restrict__ out, int64_t cap,
+                                                                int32_t* status) {
+  __shared__ GNode s_nd[kTcMaxNodes];
+  __shared__ ColumnDev s_col[kTcMaxNodes];
+  __shared__ int32_t s_kid[kTcMaxNodes];
+  const int tid = threadIdx.x;
+  const int nf = ROWS ? T->nroot : L.nodes[c].nchild;
+  const int bm = ROWS ? L.bitmap_bytes : gbm(nf);
+  const int k0 = ROWS ? 0 : T->kid0[c];
+  for (int q = tid; q < nf; q += kTcWG) {
+    const int kid = T->kids[k0 + q];
+    s_kid[q] = kid;
+    s_nd[q] = L.nodes[kid];
+    s_col[q] = L.cols[kid];
   }
-  int64_t at = P + bm + 8LL * nf;
-  uint32_t word = 0;  // null bits of fields [32 wq, 32 wq + 32)
-  int wq = 0, q = 0;
-  int32_t err = 0;
-  for (int ch = first; ch < end; ch = L.nodes[ch].end, ++q) {
-    if ((q >> 5) != wq) {
+  __syncthreads();
+  const uint64_t w = (uint64_t)blockIdx.x * kTcWG + tid;
+  if (w >= (uint64_t)m * (uint64_t)nf) return;
+  const int64_t k = (int64_t)(w / (uint64_t)nf);
+  const int q = (int)(w - (uint64_t)k * (uint64_t)nf);
+  int64_t P;
+  int hdr = 0;
+  int64_t beg = 0, size = 0;
+  if (ROWS) {
+    beg = offs[k];
+    const int64_t end = offs[k + 1];
+    hdr = frame_header_bytes(L.frame);
+    size = end - beg;
+    const bool bad = beg < 0 || end > cap || size < hdr + L.fixed_size || size - hdr > 0x7fffffffLL || (beg & 3);
+    if (bad && q == 0) set_status(status, FORY_ERR_CAPACITY);
+    P = bad ? -1 : beg + hdr;
+  } else {
+    P = T->P[c][k];
+    if (P >= 0 && P + bm + 8LL * nf > cap) {
+      if (q == 0) set_status(status, FORY_ERR_ENCODER);
+      P = -1;
+    }
+  }
+  const GNode nd = s_nd[q];
+  const ColumnDev col = s_col[q];
+  const int kid = s_kid[q];
+  const bool has_pos = tc_has_pos(nd.kind);
+  if (P < 0) {
+    if (has_pos) T->P[kid][k] = -1;
+    return;
+  }
+  const int64_t fixed_end = P + bm + 8LL * nf;
+  if (q == 0) {
+    if (ROWS) {  // the row's size against its offsets, then the frame header
+      int64_t need = hdr + L.fixed_size;
+      for (int f = 0; f < nf; ++f)
+        if (tc_is_var(s_nd[f].kind)) need += tc_size(T, s_kid[f], s_nd[f], s_col[f], k);
+      if (need > size) set_status(status, FORY_ERR_CAPACITY);  // offsets not from these columns' sizes
+      if (hdr == 12) {  // Encoders.encode(MemoryBuffer, T): [i32 8 + rowSize][i64 hash]
+        st32(out + beg, (uint32_t)(size - 4));
+        tc_put(out + beg + 4, (uint64_t)L.schema_hash, 8);
+      } else if (hdr == 8) {  // Encoder.encode(T): [i64 hash]
+        tc_put(out + beg, (uint64_t)L.schema_hash, 8);
+      }
+    }
+    for (int wq = 0; wq < bm / 4; ++wq) {  // setNullAt bits of fields [32 wq, 32 wq + 32)
+      uint32_t word = 0;
+      for (int f = 32 * wq; f < nf && f < 32 * wq + 32; ++f)
+        if ((s_nd[f].flags & 1) && !gvalid(s_col[f].validity, k)) word |= 1u << (f & 31);
       st32(out + P + 4 * wq, word);
-      word = 0;
-      ++wq;
     }
-    const GNode nd = L.nodes[ch];
-    const ColumnDev col = L.cols[ch];
-    uint8_t* slot = out + P + bm + 8 * q;
-    const bool var = tc_is_var(nd.kind);
-    if ((nd.flags & 1) && !gvalid(col.validity, k)) {  // setNullAt: bit, slot zero
-      word |= 1u << (q & 31);
-      tc_put(slot, 0, 8);
-      if (tc_has_pos(nd.kind)) T->P[ch][k] = -1;
-      continue;
-    }
-    if (!var) {  // putInt64(slot, 0) then the value: zero-extended to the slot
-      uint64_t v = load_elem(col.values, nd.width, k);
-      if (nd.kind == KIND_BOOL) v = v ? 1 : 0;
-      tc_put(slot, v, 8);
-      continue;
-    }
-    const bool leaf = tc_leaf(nd.kind);
-    const int64_t S = tc_size(T, ch, nd, col, k);
-    if (S < 0 || at + S > cap) {
-      err = FORY_ERR_ENCODER;
-      tc_put(slot, 0, 8);
-      if (!leaf) T->P[ch][k] = -1;
-      continue;
-    }
-    tc_put(slot, ((uint64_t)(at - P) << 32) | tc_slot_size(nd, col, k, S), 8);
-    if (leaf) {
-      const int32_t r = tc_leaf_write(out, nd, col, k, at);
-      if (r) err = r;
-    } else {
-      T->P[ch][k] = at;
-    }
-    at += S;
   }
-  st32(out + P + 4 * wq, word);
-  for (int w = wq + 1; w < bm / 4; ++w) st32(out + P + 4 * w, 0u);
-  return err;
+  uint8_t* slot = out + P + bm + 8 * q;
+  if ((nd.flags & 1) && !gvalid(col.validity, k)) {  // null: slot zero
+    tc_put(slot, 0, 8);
+    if (has_pos) T->P[kid][k] = -1;
+    return;
+  }
+  if (!tc_is_var(nd.kind)) {
+    uint64_t v = load_elem(col.values, nd.width, k);
+    if (nd.kind == KIND_BOOL) v = v ? 1 : 0;
+    tc_put(slot, v, 8);
+    return;
+  }
+  int64_t at = fixed_end;
+  for (int f = 0; f < q; ++f)
+    if (tc_is_var(s_nd[f].kind)) at += tc_size(T, s_kid[f], s_nd[f], s_col[f], k);
+  const int64_t S = tc_size(T, kid, nd, col, k);
+  if (S < 0 || at + S > cap) {
+    set_status(status, FORY_ERR_ENCODER);
+    tc_put(slot, 0, 8);
+    if (has_pos) T->P[kid][k] = -1;
+    return;
+  }
+  tc_put(slot, ((uint64_t)(at - P) << 32) | tc_slot_size(nd, col, k, S), 8);
+  if (has_pos) {
+    T->P[kid][k] = at;
+  } else {
+    const int32_t r = tc_leaf_write(out, nd, col, k, at);
+    if (r) set_status(status, r);
+  }
 }
 
-// Row / frame i: header, the row's fixed part and the top-level positions (or the
-// collection's position).
-__global__ __launch_bounds__(kTcWG) void tc_write_rows_kernel(GenLaunch L, const TcTables* __restrict__ T,
+// Collection frames: [i32 size] and the collection's position.
+__global__ __launch_bounds__(kTcWG) void tc_write_coll_kernel(GenLaunch L, const TcTables* __restrict__ T,
                                                               const int64_t* __restrict__ offs,
                                                               uint8_t* __restrict__ out, int64_t cap,
                                                               int32_t* status) {
   const int64_t i = (int64_t)blockIdx.x * kTcWG + threadIdx.x;
   if (i >= L.num_rows) return;
-  const int64_t beg = offs[i], end = offs[i + 1];
-  const int coll = L.frame == FORY_FRAME_COLLECTION;
-  const int hdr = coll ? 4 : frame_header_bytes(L.frame);
-  const int64_t size = end - beg;
-  bool bad = beg < 0 || end > cap || size < hdr || size - hdr > 0x7fffffffLL || (beg & 3);
-  int64_t need = hdr + (coll ? 0 : L.fixed_size);
-  if (coll) need += T->A[0][i];
-  else
-    for (int c = 0; c < L.num_nodes; c = L.nodes[c].end) {
-      const GNode cn = L.nodes[c];
-      if (tc_is_var(cn.kind)) need += tc_size(T, c, cn, L.cols[c], i);
-    }
-  if (need > size) bad = true;  // offsets not from these columns' sizes
+  const int64_t beg = offs[i], end = offs[i + 1], size = end - beg;
+  const bool bad = beg < 0 || end > cap || size < 4 || size - 4 > 0x7fffffffLL || (beg & 3) ||
+                   4 + T->A[0][i] > size;
   if (bad) set_status(status, FORY_ERR_CAPACITY);
-  uint8_t* f = out + beg;
-  if (coll) {
-    if (!bad) st32(f, (uint32_t)(size - 4));
-    T->P[0][i] = bad ? -1 : beg + 4;
-    return;
-  }
-  if (!bad && hdr == 12) {  // Encoders.encode(MemoryBuffer, T): [i32 8 + rowSize][i64 hash]
-    st32(f, (uint32_t)(size - 4));
-    tc_put(f + 4, (uint64_t)L.schema_hash, 8);
-  } else if (!bad && hdr == 8) {  // Encoder.encode(T): [i64 hash]
-    tc_put(f, (uint64_t)L.schema_hash, 8);
-  }
-  const int nf = (L.fixed_size - L.bitmap_bytes) / 8;
-  const int32_t err = tc_fields(L, T, out, cap, 0, L.num_nodes, nf, L.bitmap_bytes, i, bad ? -1 : beg + hdr);
-  if (err) set_status(status, err);
-}
-
-// Beans: lane per instance.
-__global__ __launch_bounds__(kTcWG) void tc_write_node_kernel(GenLaunch L, const TcTables* __restrict__ T, int c,
-                                                              int64_t m, uint8_t* __restrict__ out, int64_t cap,
-                                                              int32_t* status) {
-  const int64_t k = (int64_t)blockIdx.x * kTcWG + threadIdx.x;
-  if (k >= m) return;
-  const GNode nd = L.nodes[c];
-  const int32_t err = tc_fields(L, T, out, cap, c + 1, nd.end, nd.nchild, gbm(nd.nchild), k, T->P[c][k]);
-  if (err) set_status(status, err);
+  else st32(out + beg, (uint32_t)(size - 4));
+  T->P[0][i] = bad ? -1 : beg + 4;
 }
 
 // The null bitmap of items [o0, o0 + n) (1 = null, BinaryArrayWriter.setNullAt) from their
@@ -279,14 +322,13 @@ __device__ __forceinline__ void tc_bitmap(uint8_t* dst, const uint8_t* validity,
   for (int w = 0; w < nw; ++w) {
     const int64_t rem = n - 32LL * w;
     uint32_t bits = 0;
-    if (rem > 0 && validity) {
+    if (rem > 0 && validity) {  // the 32 bits from bit b: one or two aligned dwords (Arrow pads to 8 bytes)
       const int64_t b = o0 + 32LL * w;
-      const int sh = (int)(b & 7);
+      const uint32_t* v = reinterpret_cast<const uint32_t*>(validity) + (b >> 5);
+      const int sh = (int)(b & 31);
       const int take = rem < 32 ? (int)rem : 32;
-      const int nb = (sh + take + 7) >> 3;
-      const uint8_t* v = validity + (b >> 3);
-      uint64_t win = 0;
-      for (int q = 0; q < nb; ++q) win |= (uint64_t)v[q] << (8 * q);
+      uint64_t win = v[0];
+      if (sh + take > 32) win |= (uint64_t)v[1] << 32;
       const uint32_t mask = take == 32 ? 0xffffffffu : ((1u << take) - 1u);
       bits = ~(uint32_t)(win >> sh) & mask;
     }
@@ -445,22 +487,31 @@ hipError_t launch_tc_rows(const GenLaunch& L, const TcTables* T, int64_t* sizes,
   return hipGetLastError();
 }
 
-hipError_t launch_tc_write_rows(const GenLaunch& L, const TcTables* T, const int64_t* offs, uint8_t* out,
+hipError_t launch_tc_write_rows(const GenLaunch& L, const TcTables* T, int nroot, const int64_t* offs, uint8_t* out,
                                 int64_t capacity, int32_t* status, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(tc_write_rows_kernel, dim3((unsigned)((L.num_rows + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s, L,
-                     T, offs, out, capacity, status);
+  if (L.frame == FORY_FRAME_COLLECTION) {
+    hipLaunchKernelGGL(tc_write_coll_kernel, dim3((unsigned)((L.num_rows + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s,
+                       L, T, offs, out, capacity, status);
+    return hipGetLastError();
+  }
+  const int64_t work = L.num_rows * nroot;
+  hipLaunchKernelGGL(tc_write_fields_kernel<true>, dim3((unsigned)((work + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s,
+                     L, T, -1, L.num_rows, offs, out, capacity, status);
   return hipGetLastError();
 }
 
 hipError_t launch_tc_write_node(const GenLaunch& L, const TcTables* T, int node, int64_t m, uint8_t* out,
-                                int64_t capacity, int32_t* status, hipStream_t s, int kind) {
+                                int64_t capacity, int32_t* status, hipStream_t s, int kind, int nchild) {
   if (m <= 0) return hipSuccess;
-  const dim3 grid((unsigned)((m + kTcWG - 1) / kTcWG));
-  if (kind == KIND_LIST || kind == KIND_MAP)
-    hipLaunchKernelGGL(tc_write_cont_kernel, grid, dim3(kTcWG), 0, s, L, T, node, m, out, capacity, status);
-  else
-    hipLaunchKernelGGL(tc_write_node_kernel, grid, dim3(kTcWG), 0, s, L, T, node, m, out, capacity, status);
+  if (kind == KIND_LIST || kind == KIND_MAP) {
+    hipLaunchKernelGGL(tc_write_cont_kernel, dim3((unsigned)((m + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s, L, T,
+                       node, m, out, capacity, status);
+  } else {
+    const int64_t work = m * (nchild > 0 ? nchild : 1);
+    hipLaunchKernelGGL(tc_write_fields_kernel<false>, dim3((unsigned)((work + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0,
+                       s, L, T, node, m, nullptr, out, capacity, status);
+  }
   return hipGetLastError();
 }
 
