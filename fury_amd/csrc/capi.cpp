@@ -625,7 +625,9 @@ int64_t tc_bytes(const fory_plan* plan, const std::vector<int64_t>& m) {
     if (tc_needs_pos(plan->p, v)) arrays += align_up((m[v.node] + 1) * 8);
     if (v.items) maxm = std::max(maxm, m[v.node]);
   }
-  return align_up((int64_t)sizeof(fory_amd::TcTables)) + align_up((fory_amd::scan_partials(maxm) + 2) * 8) + arrays;
+  const int64_t n = m.empty() ? 0 : m[0];  // (node 0 is top-level: the rows)
+  return align_up((int64_t)sizeof(fory_amd::TcTables)) + align_up(fory_amd::tc_scan_flag_words(std::max(maxm, n)) * 8) +
+         arrays;
 }
 
 bool tc_usable(const fory_plan* plan, const fory_column* cols, int64_t n, int64_t ws_bytes, int64_t* need) {
@@ -696,8 +698,8 @@ int tc_prepare(const fory_plan* plan, const fory_column* cols, int64_t n, void* 
   for (const fory_amd::TcVar& v : t.var)
     if (v.items) maxm = std::max(maxm, m[v.node]);
   uint8_t* at = base + align_up((int64_t)sizeof(fory_amd::TcTables));
-  *partials = reinterpret_cast<int64_t*>(at);
-  at += align_up((fory_amd::scan_partials(maxm) + 2) * 8);
+  *partials = reinterpret_cast<int64_t*>(at);  // look-back flags of the fused size scans
+  at += align_up(fory_amd::tc_scan_flag_words(std::max(maxm, n)) * 8);
   for (size_t i = 0; i < m.size(); ++i) {
     T->m[i] = m[i];
     T->vidx[i] = t.vidx[i];
@@ -736,12 +738,11 @@ int tc_sizes(const fory_plan* plan, const fory_amd::GenLaunch& G, const fory_amd
     const fory_amd::TcVar& tv = t.var[(size_t)v];
     if (!tc_needs_sizes(plan->p, tv)) continue;  // strings / decimals in rows and beans: sized in place
     const int64_t m = T.m[tv.node];
-    hipError_t e = fory_amd::launch_tc_sizes(G, dT, tv.node, m, G.frame == FORY_FRAME_COLLECTION && tv.node == 0, s);
+    const bool root_coll = G.frame == FORY_FRAME_COLLECTION && tv.node == 0;
+    const hipError_t e = tv.items ? fory_amd::launch_tc_size_scan(G, dT, tv.node, m, root_coll, T.A[tv.node],
+                                                                  reinterpret_cast<uint64_t*>(partials), s)
+                                  : fory_amd::launch_tc_sizes(G, dT, tv.node, m, root_coll, s);
     if (e != hipSuccess) return hip_fail(e, "tc_sizes");
-    if (!tv.items) continue;
-    e = m > 0 ? fory_amd::launch_scan_i64(T.A[tv.node], m, partials, s)
-              : hipMemsetAsync(T.A[tv.node], 0, sizeof(int64_t), s);
-    if (e != hipSuccess) return hip_fail(e, "tc_scan");
   }
   return FORY_OK;
 }
@@ -892,10 +893,8 @@ int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols, int
       rc = tc_prepare(plan, cols, num_rows, d_workspace, s, &T, &dT, &tpart);
       if (!rc) rc = tc_sizes(plan, G, T, dT, tpart, s);
       if (rc) return rc;
-      e = fory_amd::launch_tc_rows(G, dT, d_row_offsets, s);
+      e = fory_amd::launch_tc_size_scan(G, dT, -1, num_rows, false, d_row_offsets, reinterpret_cast<uint64_t*>(tpart), s);
       if (e != hipSuccess) return hip_fail(e, "tc_rows");
-      e = fory_amd::launch_scan_i64(d_row_offsets, num_rows, partials_ptr(p, d_workspace), s);
-      if (e != hipSuccess) return hip_fail(e, "scan");
       tc_remember(d_workspace, plan->id, tc_signature(plan, cols, num_rows, frame_mode));
       return FORY_OK;
     }

@@ -75,53 +75,132 @@ __device__ __forceinline__ void tc_items(const GenLaunch& L, const TcTables* T, 
 // ---------------------------------------------------------------------------
 // sizes
 // ---------------------------------------------------------------------------
+// Bytes instance j of var node c adds to its parent (root_coll: node 0 of a collection
+// frame, present whatever its validity).
+__device__ __forceinline__ int64_t tc_node_size(const GenLaunch& L, const TcTables* T, int c, int64_t j,
+                                                int root_coll) {
+  const GNode nd = L.nodes[c];
+  const ColumnDev col = L.cols[c];
+  if (!root_coll && (nd.flags & 1) && !gvalid(col.validity, j)) return 0;
+  switch (nd.kind) {
+    case KIND_BYTES: return gr8((int64_t)col.offsets[j + 1] - col.offsets[j]);
+    case KIND_DECIMAL: return 32;
+    case KIND_STRUCT: {
+      int64_t s = gbm(nd.nchild) + 8LL * nd.nchild;
+      for (int ch = c + 1; ch < nd.end; ch = L.nodes[ch].end) {
+        const GNode cn = L.nodes[ch];
+        if (tc_is_var(cn.kind)) s += tc_size(T, ch, cn, L.cols[ch], j);
+      }
+      return s;
+    }
+    case KIND_LIST:
+    case KIND_MAP: {
+      int64_t o0, o1;
+      tc_items(L, T, c, j, &o0, &o1);
+      if (nd.kind == KIND_LIST) return tc_array_bytes(L, T, c + 1, o0, o1);
+      return 8 + tc_array_bytes(L, T, c + 1, o0, o1) + tc_array_bytes(L, T, L.nodes[c + 1].end, o0, o1);
+    }
+    default: return 0;
+  }
+}
+
+// Row / frame i's bytes.
+__device__ __forceinline__ int64_t tc_row_size(const GenLaunch& L, const TcTables* T, int64_t i) {
+  if (L.frame == FORY_FRAME_COLLECTION) return 4 + T->A[0][i];
+  int64_t s = frame_header_bytes(L.frame) + L.fixed_size;
+  for (int t = 0; t < L.num_nodes; t = L.nodes[t].end) {
+    const GNode tn = L.nodes[t];
+    if (tc_is_var(tn.kind)) s += tc_size(T, t, tn, L.cols[t], i);
+  }
+  return s;
+}
+
 __global__ __launch_bounds__(kTcWG) void tc_sizes_kernel(GenLaunch L, const TcTables* __restrict__ T, int c,
                                                          int64_t m, int root_coll) {
   const int64_t j = (int64_t)blockIdx.x * kTcWG + threadIdx.x;
   if (j >= m) return;
-  const GNode nd = L.nodes[c];
-  const ColumnDev col = L.cols[c];
-  int64_t s = 0;
-  if (root_coll || !(nd.flags & 1) || gvalid(col.validity, j)) {
-    switch (nd.kind) {
-      case KIND_BYTES: s = gr8((int64_t)col.offsets[j + 1] - col.offsets[j]); break;
-      case KIND_DECIMAL: s = 32; break;
-      case KIND_STRUCT:
-        s = gbm(nd.nchild) + 8LL * nd.nchild;
-        for (int ch = c + 1; ch < nd.end; ch = L.nodes[ch].end) {
-          const GNode cn = L.nodes[ch];
-          if (tc_is_var(cn.kind)) s += tc_size(T, ch, cn, L.cols[ch], j);
+  T->A[c][j] = tc_node_size(L, T, c, j, root_coll);
+}
+
+// Sizes + exclusive scan in one pass (decoupled look-back): tiles of kTcScanTile values
+// in ticket order; a tile publishes its sum, then its inclusive prefix once the tiles
+// before it are resolved. out[m] = the total. node >= 0: that node's instance sizes;
+// node < 0: the rows' sizes.
+constexpr int kTcScanPer = 8;
+constexpr int kTcScanTile = kTcWG * kTcScanPer;
+constexpr uint64_t kTcAgg = 1ull << 62, kTcInc = 2ull << 62, kTcVal = (1ull << 62) - 1;
+
+__global__ __launch_bounds__(kTcWG) void tc_size_scan_kernel(GenLaunch L, const TcTables* __restrict__ T, int c,
+                                                             int64_t m, int root_coll, int64_t* __restrict__ out,
+                                                             uint64_t* __restrict__ flags,
+                                                             uint32_t* __restrict__ ticket) {
+  __shared__ int64_t s_wave[kTcWG / 64];
+  __shared__ int64_t s_base;
+  __shared__ uint32_t s_tile;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t j0 = tile * kTcScanTile + (int64_t)tid * kTcScanPer;
+  int64_t v[kTcScanPer];
+  int64_t sum = 0;
+#pragma unroll
+  for (int u = 0; u < kTcScanPer; ++u) {
+    const int64_t j = j0 + u;
+    v[u] = j < m ? (c >= 0 ? tc_node_size(L, T, c, j, root_coll) : tc_row_size(L, T, j)) : 0;
+    sum += v[u];
+  }
+  int64_t inc = sum;  // inclusive scan of the lanes' sums within the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += y;
+  }
+  if (lane == 63) s_wave[wv] = inc;
+  __syncthreads();
+  int64_t wbase = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < kTcWG / 64; ++w) {
+    if (w < wv) wbase += s_wave[w];
+    total += s_wave[w];
+  }
+  if (tid == 0) {  // publish, then look back
+    if (tile == 0) {
+      __hip_atomic_store(&flags[0], kTcInc | (uint64_t)total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      s_base = 0;
+    } else {
+      __hip_atomic_store(&flags[tile], kTcAgg | (uint64_t)total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t base = 0;
+      for (int64_t t = tile - 1;; ) {
+        const uint64_t f = __hip_atomic_load(&flags[t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (f & kTcInc) {
+          base += (int64_t)(f & kTcVal);
+          break;
         }
-        break;
-      case KIND_LIST:
-      case KIND_MAP: {
-        int64_t o0, o1;
-        tc_items(L, T, c, j, &o0, &o1);
-        if (nd.kind == KIND_LIST) s = tc_array_bytes(L, T, c + 1, o0, o1);
-        else s = 8 + tc_array_bytes(L, T, c + 1, o0, o1) + tc_array_bytes(L, T, L.nodes[c + 1].end, o0, o1);
-        break;
+        if (f & kTcAgg) {
+          base += (int64_t)(f & kTcVal);
+          --t;
+        }
       }
-      default: break;
+      __hip_atomic_store(&flags[tile], kTcInc | (uint64_t)(base + total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      s_base = base;
     }
   }
-  T->A[c][j] = s;
+  __syncthreads();
+  int64_t at = s_base + wbase + inc - sum;
+#pragma unroll
+  for (int u = 0; u < kTcScanPer; ++u) {
+    const int64_t j = j0 + u;
+    if (j < m) out[j] = at;
+    at += v[u];
+  }
+  if (j0 <= m - 1 && m - 1 < j0 + kTcScanPer) out[m] = at;  // the lane holding the last value
 }
 
 __global__ __launch_bounds__(kTcWG) void tc_rows_kernel(GenLaunch L, const TcTables* __restrict__ T,
                                                         int64_t* __restrict__ sizes) {
   const int64_t i = (int64_t)blockIdx.x * kTcWG + threadIdx.x;
-  if (i >= L.num_rows) return;
-  int64_t s;
-  if (L.frame == FORY_FRAME_COLLECTION) {
-    s = 4 + T->A[0][i];
-  } else {
-    s = frame_header_bytes(L.frame) + L.fixed_size;
-    for (int t = 0; t < L.num_nodes; t = L.nodes[t].end) {
-      const GNode tn = L.nodes[t];
-      if (tc_is_var(tn.kind)) s += tc_size(T, t, tn, L.cols[t], i);
-    }
-  }
-  sizes[i] = s;
+  if (i < L.num_rows) sizes[i] = tc_row_size(L, T, i);
 }
 
 // ---------------------------------------------------------------------------
@@ -477,6 +556,20 @@ hipError_t launch_tc_sizes(const GenLaunch& L, const TcTables* T, int node, int6
   if (m <= 0) return hipSuccess;
   hipLaunchKernelGGL(tc_sizes_kernel, dim3((unsigned)((m + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s, L, T, node, m,
                      root_coll ? 1 : 0);
+  return hipGetLastError();
+}
+
+int64_t tc_scan_flag_words(int64_t m) { return (m + kTcScanTile - 1) / kTcScanTile + 2; }
+
+hipError_t launch_tc_size_scan(const GenLaunch& L, const TcTables* T, int node, int64_t m, bool root_coll,
+                               int64_t* out, uint64_t* flags, hipStream_t s) {
+  const int64_t tiles = (m + kTcScanTile - 1) / kTcScanTile;
+  hipError_t e = hipMemsetAsync(flags, 0, (size_t)tc_scan_flag_words(m) * 8, s);
+  if (e != hipSuccess) return e;
+  if (m <= 0) return hipMemsetAsync(out, 0, sizeof(int64_t), s);
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(flags + tiles + 1);
+  hipLaunchKernelGGL(tc_size_scan_kernel, dim3((unsigned)tiles), dim3(kTcWG), 0, s, L, T, node, m, root_coll ? 1 : 0,
+                     out, flags, ticket);
   return hipGetLastError();
 }
 

@@ -1,7 +1,7 @@
 """Throughput of the tree engine (fury_amd/csrc/generic.hip) on the nested test shapes:
 device-resident encode (sizes + scan + encode) and decode (level-by-level sizes +
 values), bytes = row bytes + column bytes per direction. Diagnostic, not the bench.
-Usage: python scripts/bench_nested_shapes.py [rows]"""
+Usage: python scripts/bench_nested_shapes.py [rows] [shape,shape...] [--encode-only]"""
 import json
 import os
 import sys
@@ -38,7 +38,9 @@ from fury_amd.format.encoder import RowEncoder  # noqa: E402
 
 n0 = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
 out = {}
-for name in ("holder", "lists", "maps_nested", "bean_a"):
+shapes = sys.argv[2].split(",") if len(sys.argv) > 2 and not sys.argv[2].startswith("-") else ["holder", "lists", "maps_nested", "bean_a"]
+encode_only = "--encode-only" in sys.argv
+for name in shapes:
     base = 16384  # generated once (the Python row generator is slow), then tiled
     print("generating", name, n0, flush=True)
     schema, cols = nested_columns(name, base, 5)
@@ -56,7 +58,8 @@ for name in ("holder", "lists", "maps_nested", "bean_a"):
         e0.record()
         rows = enc.encode(dcols, n, 1)
         e1.record()
-        enc.decode(rows)
+        if not encode_only:
+            enc.decode(rows)
         e2.record()
         torch.cuda.synchronize()
         te.append(e0.elapsed_time(e1))
