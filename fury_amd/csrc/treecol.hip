@@ -164,25 +164,29 @@ __global__ __launch_bounds__(kTcWG) void tc_size_scan_kernel(GenLaunch L, const 
     if (w < wv) wbase += s_wave[w];
     total += s_wave[w];
   }
-  if (tid == 0) {  // publish, then look back
-    if (tile == 0) {
-      __hip_atomic_store(&flags[0], kTcInc | (uint64_t)total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      s_base = 0;
-    } else {
-      __hip_atomic_store(&flags[tile], kTcAgg | (uint64_t)total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      int64_t base = 0;
-      for (int64_t t = tile - 1;; ) {
-        const uint64_t f = __hip_atomic_load(&flags[t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        if (f & kTcInc) {
-          base += (int64_t)(f & kTcVal);
-          break;
-        }
-        if (f & kTcAgg) {
-          base += (int64_t)(f & kTcVal);
-          --t;
-        }
-      }
-      __hip_atomic_store(&flags[tile], kTcInc | (uint64_t)(base + total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (wv == 0) {  // publish the tile's sum, then look back 64 tiles at a time
+    if (lane == 0)
+      __hip_atomic_store(&flags[tile], (tile == 0 ? kTcInc : kTcAgg) | (uint64_t)total, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    int64_t base = 0;
+    for (int64_t t_end = tile - 1; t_end >= 0;) {
+      const int64_t t = t_end - lane;
+      const uint64_t f = t >= 0 ? __hip_atomic_load(&flags[t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : kTcInc;
+      const uint64_t incs = __ballot((f & kTcInc) != 0);
+      const int first = incs ? __ffsll((unsigned long long)incs) - 1 : 64;  // nearest resolved tile
+      const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
+      if (__ballot(f == 0) & need) continue;  // a tile before it has not published yet
+      int64_t x = lane <= first ? (int64_t)(f & kTcVal) : 0;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+      base += x;
+      if (first < 64) break;
+      t_end -= 64;
+    }
+    if (lane == 0) {
+      if (tile > 0)
+        __hip_atomic_store(&flags[tile], kTcInc | (uint64_t)(base + total), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
       s_base = base;
     }
   }
