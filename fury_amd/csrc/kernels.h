@@ -157,8 +157,8 @@ struct TcTables {               // device, in the workspace
 };
 hipError_t launch_tc_sizes(const GenLaunch& L, const TcTables* T, int node, int64_t m, bool root_coll, hipStream_t s);
 hipError_t launch_tc_rows(const GenLaunch& L, const TcTables* T, int64_t* sizes, hipStream_t s);
-// Sizes + exclusive scan in one pass (node < 0: the rows' sizes): out[0..m], out[m] the
-// total. flags: tc_scan_flag_words(m) words of workspace (cleared here).
+// Sizes + exclusive scan (node < 0: the rows' sizes): out[0..m], out[m] the total.
+// flags: tc_scan_flag_words(m) words of workspace (the tile sums).
 int64_t tc_scan_flag_words(int64_t m);
 hipError_t launch_tc_size_scan(const GenLaunch& L, const TcTables* T, int node, int64_t m, bool root_coll,
                                int64_t* out, uint64_t* flags, hipStream_t s);

@@ -122,35 +122,18 @@ __global__ __launch_bounds__(kTcWG) void tc_sizes_kernel(GenLaunch L, const TcTa
   T->A[c][j] = tc_node_size(L, T, c, j, root_coll);
 }
 
-// Sizes + exclusive scan in one pass (decoupled look-back): tiles of kTcScanTile values
-// in ticket order; a tile publishes its sum, then its inclusive prefix once the tiles
-// before it are resolved. out[m] = the total. node >= 0: that node's instance sizes;
-// node < 0: the rows' sizes.
+// Sizes + exclusive scan, reduce-then-scan in three launches (no cross-workgroup waits:
+// the L2s are per XCD, so a look-back chain pays a memory round trip per hop):
+// sums    tiles of kTcScanTile: each value's size into out[j], the tile's sum into part[t]
+// part    one workgroup scans the tile sums (exclusive, part[tiles] = total)
+// down    each tile scans its values in place from its base; out[m] = the total.
+// node >= 0: that node's instance sizes; node < 0: the rows' sizes.
 constexpr int kTcScanPer = 8;
 constexpr int kTcScanTile = kTcWG * kTcScanPer;
-constexpr uint64_t kTcAgg = 1ull << 62, kTcInc = 2ull << 62, kTcVal = (1ull << 62) - 1;
 
-__global__ __launch_bounds__(kTcWG) void tc_size_scan_kernel(GenLaunch L, const TcTables* __restrict__ T, int c,
-                                                             int64_t m, int root_coll, int64_t* __restrict__ out,
-                                                             uint64_t* __restrict__ flags,
-                                                             uint32_t* __restrict__ ticket) {
-  __shared__ int64_t s_wave[kTcWG / 64];
-  __shared__ int64_t s_base;
-  __shared__ uint32_t s_tile;
+__device__ __forceinline__ int64_t tc_block_excl(int64_t x, int64_t* s_wave, int64_t* total) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
-  __syncthreads();
-  const int64_t tile = s_tile;
-  const int64_t j0 = tile * kTcScanTile + (int64_t)tid * kTcScanPer;
-  int64_t v[kTcScanPer];
-  int64_t sum = 0;
-#pragma unroll
-  for (int u = 0; u < kTcScanPer; ++u) {
-    const int64_t j = j0 + u;
-    v[u] = j < m ? (c >= 0 ? tc_node_size(L, T, c, j, root_coll) : tc_row_size(L, T, j)) : 0;
-    sum += v[u];
-  }
-  int64_t inc = sum;  // inclusive scan of the lanes' sums within the wave
+  int64_t inc = x;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const int64_t y = __shfl_up(inc, d, 64);
@@ -158,40 +141,65 @@ __global__ __launch_bounds__(kTcWG) void tc_size_scan_kernel(GenLaunch L, const 
   }
   if (lane == 63) s_wave[wv] = inc;
   __syncthreads();
-  int64_t wbase = 0, total = 0;
+  int64_t wbase = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < kTcWG / 64; ++w) {
     if (w < wv) wbase += s_wave[w];
-    total += s_wave[w];
-  }
-  if (wv == 0) {  // publish the tile's sum, then look back 64 tiles at a time
-    if (lane == 0)
-      __hip_atomic_store(&flags[tile], (tile == 0 ? kTcInc : kTcAgg) | (uint64_t)total, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    int64_t base = 0;
-    for (int64_t t_end = tile - 1; t_end >= 0;) {
-      const int64_t t = t_end - lane;
-      const uint64_t f = t >= 0 ? __hip_atomic_load(&flags[t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : kTcInc;
-      const uint64_t incs = __ballot((f & kTcInc) != 0);
-      const int first = incs ? __ffsll((unsigned long long)incs) - 1 : 64;  // nearest resolved tile
-      const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
-      if (__ballot(f == 0) & need) continue;  // a tile before it has not published yet
-      int64_t x = lane <= first ? (int64_t)(f & kTcVal) : 0;
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-      base += x;
-      if (first < 64) break;
-      t_end -= 64;
-    }
-    if (lane == 0) {
-      if (tile > 0)
-        __hip_atomic_store(&flags[tile], kTcInc | (uint64_t)(base + total), __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      s_base = base;
-    }
+    tot += s_wave[w];
   }
   __syncthreads();
-  int64_t at = s_base + wbase + inc - sum;
+  *total = tot;
+  return wbase + inc - x;
+}
+
+__global__ __launch_bounds__(kTcWG) void tc_size_sums_kernel(GenLaunch L, const TcTables* __restrict__ T, int c,
+                                                             int64_t m, int root_coll, int64_t* __restrict__ out,
+                                                             int64_t* __restrict__ part) {
+  __shared__ int64_t s_wave[kTcWG / 64];
+  const int64_t j0 = (int64_t)blockIdx.x * kTcScanTile + (int64_t)threadIdx.x * kTcScanPer;
+  int64_t sum = 0;
+#pragma unroll
+  for (int u = 0; u < kTcScanPer; ++u) {
+    const int64_t j = j0 + u;
+    if (j < m) {
+      const int64_t v = c >= 0 ? tc_node_size(L, T, c, j, root_coll) : tc_row_size(L, T, j);
+      out[j] = v;
+      sum += v;
+    }
+  }
+  int64_t tot;
+  tc_block_excl(sum, s_wave, &tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kTcWG) void tc_part_scan_kernel(int64_t* __restrict__ part, int64_t nb) {
+  __shared__ int64_t s_wave[kTcWG / 64];
+  int64_t carry = 0;
+  for (int64_t b0 = 0; b0 < nb; b0 += kTcWG) {
+    const int64_t b = b0 + threadIdx.x;
+    const int64_t x = b < nb ? part[b] : 0;
+    int64_t tot;
+    const int64_t ex = tc_block_excl(x, s_wave, &tot);
+    if (b < nb) part[b] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) part[nb] = carry;
+}
+
+__global__ __launch_bounds__(kTcWG) void tc_scan_down_kernel(int64_t* __restrict__ out, int64_t m,
+                                                             const int64_t* __restrict__ part) {
+  __shared__ int64_t s_wave[kTcWG / 64];
+  const int64_t j0 = (int64_t)blockIdx.x * kTcScanTile + (int64_t)threadIdx.x * kTcScanPer;
+  int64_t v[kTcScanPer];
+  int64_t sum = 0;
+#pragma unroll
+  for (int u = 0; u < kTcScanPer; ++u) {
+    const int64_t j = j0 + u;
+    v[u] = j < m ? out[j] : 0;
+    sum += v[u];
+  }
+  int64_t tot;
+  int64_t at = part[blockIdx.x] + tc_block_excl(sum, s_wave, &tot);
 #pragma unroll
   for (int u = 0; u < kTcScanPer; ++u) {
     const int64_t j = j0 + u;
@@ -567,13 +575,13 @@ int64_t tc_scan_flag_words(int64_t m) { return (m + kTcScanTile - 1) / kTcScanTi
 
 hipError_t launch_tc_size_scan(const GenLaunch& L, const TcTables* T, int node, int64_t m, bool root_coll,
                                int64_t* out, uint64_t* flags, hipStream_t s) {
-  const int64_t tiles = (m + kTcScanTile - 1) / kTcScanTile;
-  hipError_t e = hipMemsetAsync(flags, 0, (size_t)tc_scan_flag_words(m) * 8, s);
-  if (e != hipSuccess) return e;
   if (m <= 0) return hipMemsetAsync(out, 0, sizeof(int64_t), s);
-  uint32_t* ticket = reinterpret_cast<uint32_t*>(flags + tiles + 1);
-  hipLaunchKernelGGL(tc_size_scan_kernel, dim3((unsigned)tiles), dim3(kTcWG), 0, s, L, T, node, m, root_coll ? 1 : 0,
-                     out, flags, ticket);
+  const int64_t tiles = (m + kTcScanTile - 1) / kTcScanTile;
+  int64_t* part = reinterpret_cast<int64_t*>(flags);
+  hipLaunchKernelGGL(tc_size_sums_kernel, dim3((unsigned)tiles), dim3(kTcWG), 0, s, L, T, node, m, root_coll ? 1 : 0,
+                     out, part);
+  hipLaunchKernelGGL(tc_part_scan_kernel, dim3(1), dim3(kTcWG), 0, s, part, tiles);
+  hipLaunchKernelGGL(tc_scan_down_kernel, dim3((unsigned)tiles), dim3(kTcWG), 0, s, out, m, part);
   return hipGetLastError();
 }
 
