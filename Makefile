@@ -4,7 +4,7 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
 LIB := fury_amd/lib/libfory_rowfmt.so
 ORACLE := oracle/_build/liboracle.so
-KOBJS := fury_amd/lib/fixed.o fury_amd/lib/scan.o fury_amd/lib/varlen.o fury_amd/lib/frames.o fury_amd/lib/generic.o fury_amd/lib/treecol.o fury_amd/lib/launch_state.o \
+KOBJS := fury_amd/lib/fixed.o fury_amd/lib/scan.o fury_amd/lib/varlen.o fury_amd/lib/frames.o fury_amd/lib/generic.o fury_amd/lib/treecol.o fury_amd/lib/treedec.o fury_amd/lib/launch_state.o \
          fury_amd/lib/capi.o fury_amd/lib/plan.o fury_amd/lib/host.o
 HDRS := fury_amd/csrc/kernels.h fury_amd/csrc/kcommon.h fury_amd/csrc/gen_device.h fury_amd/csrc/plan.h include/fory_rowfmt.h
 

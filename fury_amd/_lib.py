@@ -72,6 +72,7 @@ PROTOTYPES = {
     "fory_rowfmt_plan_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(PlanInfo)]),
     "fory_rowfmt_workspace_bytes": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int64]),
     "fory_rowfmt_encode_workspace_bytes": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
+    "fory_rowfmt_decode_workspace_bytes": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
     "fory_rowfmt_encoded_size": (
         ctypes.c_int,
         [ctypes.c_void_p, ctypes.POINTER(Column), ctypes.c_int64, ctypes.c_int32,

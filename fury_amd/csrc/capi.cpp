@@ -747,6 +747,69 @@ int tc_sizes(const fory_plan* plan, const fory_amd::GenLaunch& G, const fory_amd
   return FORY_OK;
 }
 
+// --- columnar decode (treedec.hip) ------------------------------------------------
+// Positions (P, SZ, TL) of the bean / list / map instances known in this call.
+int64_t td_bytes(const fory_plan* plan, const std::vector<int64_t>& m) {
+  int64_t b = align_up((int64_t)sizeof(fory_amd::TdTables));
+  for (const fory_amd::TcVar& v : plan->tc.var)
+    if (tc_needs_pos(plan->p, v)) b += align_up((m[v.node] + 1) * 8) + 2 * align_up((m[v.node] + 1) * 4);
+  return b;
+}
+
+bool td_usable(const fory_plan* plan, const fory_column* out_cols, int64_t n, int64_t ws_bytes) {
+  if (!plan->tc.ok || !plan->p.kn.tree_col || n <= 0 || !out_cols) return false;
+  return ws_bytes >= fory_rowfmt_workspace_bytes(plan, n) + td_bytes(plan, tc_domains(plan, out_cols, n));
+}
+
+int td_prepare(const fory_plan* plan, const fory_column* out_cols, int64_t n, void* ws, hipStream_t s,
+               const fory_amd::TdTables** dT, std::vector<int64_t>* m) {
+  *m = tc_domains(plan, out_cols, n);
+  uint8_t* base = static_cast<uint8_t*>(ws) + fory_rowfmt_workspace_bytes(plan, n);
+  fory_amd::TdTables T;
+  std::memset(&T, 0, sizeof(T));
+  uint8_t* at = base + align_up((int64_t)sizeof(fory_amd::TdTables));
+  for (const fory_amd::TcVar& v : plan->tc.var) {
+    if (!tc_needs_pos(plan->p, v)) continue;
+    const int64_t k = (*m)[v.node] + 1;
+    T.P[v.node] = reinterpret_cast<int64_t*>(at);
+    at += align_up(k * 8);
+    T.SZ[v.node] = reinterpret_cast<int32_t*>(at);
+    at += align_up(k * 4);
+    T.TL[v.node] = reinterpret_cast<int32_t*>(at);
+    at += align_up(k * 4);
+  }
+  int nk = 0;
+  for (int32_t f : plan->p.top) T.kids[nk++] = f;
+  T.nroot = nk;
+  for (size_t i = 0; i < plan->p.nodes.size(); ++i) {
+    if (plan->p.nodes[i].kind != fory_amd::KIND_STRUCT) continue;
+    T.kid0[i] = nk;
+    for (int32_t ch : plan->p.nodes[i].children) T.kids[nk++] = ch;
+  }
+  *dT = reinterpret_cast<const fory_amd::TdTables*>(base);
+  return upload(base, &T, (int64_t)sizeof(T), s);
+}
+
+// The passes of one decode level (level >= 0: its counts; -1: the values): the rows, then
+// every bean / list / map node the level needs, parents first.
+int td_run(const fory_plan* plan, fory_amd::GenLaunch G, const fory_amd::TdTables* dT, const std::vector<int64_t>& m,
+           int level, const void* rows, const int64_t* offs, int32_t* status, hipStream_t s) {
+  const Plan& p = plan->p;
+  G.fill_level = level;
+  const uint8_t* r = static_cast<const uint8_t*>(rows);
+  hipError_t e = fory_amd::launch_td_rows(G, dT, (int)p.top.size(), r, offs, status, s);
+  for (size_t v = 0; v < plan->tc.var.size() && e == hipSuccess; ++v) {
+    const int node = plan->tc.var[v].node;
+    const int kind = p.nodes[node].kind;
+    const int cd = p.gnodes[node].cdepth;
+    if (!tc_needs_pos(p, plan->tc.var[v])) continue;
+    if (level >= 0 && (kind == fory_amd::KIND_STRUCT ? cd > level : cd >= level)) continue;
+    if (G.frame == FORY_FRAME_COLLECTION && node == 0 && level == 0) continue;  // the frames pass counted it
+    e = fory_amd::launch_td_node(G, dT, node, m[node], kind, (int)p.nodes[node].children.size(), r, status, s);
+  }
+  return e == hipSuccess ? FORY_OK : hip_fail(e, "td_decode");
+}
+
 int64_t* elem_partials_ptr(const Plan& p, void* ws, int64_t n) {
   return reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(spill_ptr(p, ws, n)) +
                                     align_up(fory_amd::var_spill_words(n) * 4));
@@ -863,6 +926,13 @@ int64_t fory_rowfmt_encode_workspace_bytes(const fory_plan* plan, const fory_col
   const int64_t base = fory_rowfmt_workspace_bytes(plan, num_rows);
   if (!plan->tc.ok || !plan->p.kn.tree_col || num_rows <= 0 || !cols) return base;
   return base + tc_bytes(plan, tc_domains(plan, cols, num_rows));
+}
+
+int64_t fory_rowfmt_decode_workspace_bytes(const fory_plan* plan, const fory_column* out_cols, int64_t num_rows) {
+  if (!plan) return -1;
+  const int64_t base = fory_rowfmt_workspace_bytes(plan, num_rows);
+  if (!plan->tc.ok || !plan->p.kn.tree_col || num_rows <= 0 || !out_cols) return base;
+  return base + td_bytes(plan, tc_domains(plan, out_cols, num_rows));
 }
 
 int fory_rowfmt_encoded_size(const fory_plan* plan, const fory_column* cols, int64_t num_rows,
@@ -1015,9 +1085,18 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
         if (!out_cols[idx].offsets || out_cols[idx].length < 0) ready = false;
       }
       if (!any || !ready) break;
-      G.fill_level = level;
-      hipError_t e = fory_amd::launch_gen_decode(G, static_cast<const uint8_t*>(d_rows), d_row_offsets, d_status, s);
-      if (e != hipSuccess) return hip_fail(e, "gen_decode (lengths)");
+      hipError_t e = hipSuccess;
+      if (td_usable(plan, out_cols, num_rows, workspace_bytes)) {  // columnar: the passes down to this level
+        const fory_amd::TdTables* dT = nullptr;
+        std::vector<int64_t> m;
+        rc = td_prepare(plan, out_cols, num_rows, d_workspace, s, &dT, &m);
+        if (!rc) rc = td_run(plan, G, dT, m, level, d_rows, d_row_offsets, d_status, s);
+        if (rc) return rc;
+      } else {
+        G.fill_level = level;
+        e = fory_amd::launch_gen_decode(G, static_cast<const uint8_t*>(d_rows), d_row_offsets, d_status, s);
+        if (e != hipSuccess) return hip_fail(e, "gen_decode (lengths)");
+      }
       for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
         if (!is_var_kind(p.nodes[idx].kind) || p.gnodes[idx].cdepth != level) continue;
         e = level == 0 ? fory_amd::launch_scan_offsets_i32(out_cols[idx].offsets, num_rows,
@@ -1104,6 +1183,12 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows, const int64_t*
     fory_amd::GenLaunch G{};
     rc = prepare_gen(p, out_cols, num_rows, frame_mode, d_workspace, s, &G, 1 << 20);
     if (rc) return rc;
+    if (td_usable(plan, out_cols, num_rows, workspace_bytes)) {  // columnar: every node's values
+      const fory_amd::TdTables* dT = nullptr;
+      std::vector<int64_t> m;
+      rc = td_prepare(plan, out_cols, num_rows, d_workspace, s, &dT, &m);
+      return rc ? rc : td_run(plan, G, dT, m, -1, d_rows, d_row_offsets, d_status, s);
+    }
     e = fory_amd::launch_gen_decode(G, static_cast<const uint8_t*>(d_rows), d_row_offsets, d_status, s);
     return e == hipSuccess ? FORY_OK : hip_fail(e, "gen_decode");
   }

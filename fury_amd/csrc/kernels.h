@@ -169,6 +169,24 @@ hipError_t launch_tc_write_rows(const GenLaunch& L, const TcTables* T, int nroot
 hipError_t launch_tc_write_node(const GenLaunch& L, const TcTables* T, int node, int64_t m, uint8_t* out,
                                 int64_t capacity, int32_t* status, hipStream_t s, int kind, int nchild);
 
+// Columnar decode (treedec.hip): per-node passes over instances, field-major for rows and
+// beans, item-parallel for lists / maps. Positions of the bean / list / map instances:
+// P (start, -1 = absent / null), SZ (slot size), TL (record end - start).
+struct TdTables {
+  int64_t* P[kTcMaxNodes];
+  int32_t* SZ[kTcMaxNodes];
+  int32_t* TL[kTcMaxNodes];
+  int32_t kids[kTcMaxNodes];  // fields by parent: the rows' top-level fields, then each bean's
+  int32_t kid0[kTcMaxNodes];
+  int32_t nroot;
+};
+// The rows' fields (or collection frames), then one bean / list / map node (m instances);
+// L.fill_level >= 0: that level's counts, -1: the values.
+hipError_t launch_td_rows(const GenLaunch& L, const TdTables* T, int nroot, const uint8_t* rows, const int64_t* offs,
+                          int32_t* status, hipStream_t s);
+hipError_t launch_td_node(const GenLaunch& L, const TdTables* T, int node, int64_t m, int kind, int nchild,
+                          const uint8_t* rows, int32_t* status, hipStream_t s);
+
 // Frame index of a STREAM batch (frames.hip): the starts of the first num_rows
 // frames of rows_bytes bytes, found on the device from the stream alone.
 struct FrameIndexLaunch {

@@ -1,0 +1,354 @@
+// treedec.hip — the columnar tree engine's decode: rows of any nesting to Arrow columns
+// by per-node passes, the inverse of treecol.hip's encode.
+//
+// The per-lane decoder (generic.hip, g_decode) walks each record through a frame stack,
+// once per container depth for the counts and once for the values. Here every pass is a
+// grid over one node's instances (BaseBinaryEncoderBuilder's layout read back as
+// RowEncoderBuilder.fromRow / ArrayDataForEach do, RowEncoderBuilder.java:215-318):
+//   fields  rows (and each bean node): a lane per (field, instance), field-major, so the
+//           lanes of a wave write consecutive elements of one output column. The lane
+//           reads the field's null bit and slot and writes the value (scalars: the slot's
+//           low bytes; strings: the bytes at the slot's (offset, size); decimals: 32
+//           bytes, the high 16 the sign extension), the count of a string / list / map
+//           at this decode level, or hands a bean / list / map its position.
+//   items   each list / map node: a workgroup per 256 containers reads their headers
+//           (count, and for maps the key array's bytes), checks the count against the
+//           Arrow offsets the sizes passes wrote, then the elements item-parallel (the
+//           container found by binary search over the workgroup's offsets in LDS); each
+//           element is read like a field, its slot relative to its array.
+// Positions (the instance's start, its extent and its record's end) live in the
+// workspace for the call; decode_sizes at level L re-derives them for the levels above L
+// (nothing persists between calls). Every read is bounded by the record's end, with the
+// per-lane decoder's checks (FORY_ERR_CORRUPT).
+#include "gen_device.h"
+
+namespace fory_amd {
+namespace {
+
+constexpr int kTdWG = 256;
+
+__device__ __forceinline__ bool td_leaf(int kind) { return kind == KIND_BYTES || kind == KIND_DECIMAL; }
+
+// Validity bit pos of an Arrow bitmap (words shared between workgroups).
+__device__ __forceinline__ void td_valid_bit(uint8_t* validity, int64_t pos, bool valid) {
+  uint32_t* word = reinterpret_cast<uint32_t*>(validity) + (pos >> 5);
+  const uint32_t bit = 1u << (pos & 31);
+  if (valid) atomicOr(word, bit);
+  else atomicAnd(word, ~bit);
+}
+
+// Array header at `at` bounded by lim: numElements, or -1 (g_array_n).
+__device__ __forceinline__ int64_t td_array_n(const GenLaunch& L, const uint8_t* rows, int item, int64_t at,
+                                              int64_t lim) {
+  if (at < 0 || at + 8 > lim) return -1;
+  const int64_t n = (int64_t)gget(rows + at, 8);
+  if (n < 0 || n > 0x7fffffffLL || at + 8 + gbm(n) + n * elem_size(L.nodes[item]) > lim) return -1;
+  return n;
+}
+
+// A list / map payload at [at, at + size): its element count, or -1; *kat / *vat the (key)
+// array and the value array (g_container_n; BinaryMap.pointTo, BinaryMap.java:62-77).
+__device__ __forceinline__ int64_t td_container_n(const GenLaunch& L, const uint8_t* rows, int node, int64_t at,
+                                                  int64_t size, int64_t* kat, int64_t* vat) {
+  if (L.nodes[node].kind == KIND_LIST) {
+    *kat = at;
+    *vat = at;
+    return td_array_n(L, rows, node + 1, at, at + size);
+  }
+  if (size < 8) return -1;
+  const int64_t kb = (int64_t)gget(rows + at, 8);
+  const int key = node + 1, val = L.nodes[key].end;
+  *kat = at + 8;
+  *vat = at + 8 + kb;
+  if (kb < 8 || *vat + 8 > at + size) return -1;
+  const int64_t nk = td_array_n(L, rows, key, *kat, *vat);
+  const int64_t nv = td_array_n(L, rows, val, *vat, at + size);
+  return nk < 0 || nk != nv ? -1 : nk;
+}
+
+// One value of node f, instance k, read through `slot` of the row / array starting at
+// `origin` (slots' offsets are relative to it), in a record ending at rend. Scalars and
+// validity are the caller's. level >= 0: the counts of that decode level (and the positions
+// the levels below need); -1: the values.
+__device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, int f, const GNode& nd,
+                                         const ColumnDev& col, int64_t k, const uint8_t* rows, const uint8_t* slot,
+                                         int64_t origin, int64_t rend, bool isnull, int level, int32_t* status) {
+  const bool values = level < 0;
+  if (nd.kind == KIND_STRUCT) {
+    if (!values && nd.cdepth > level) return;
+    int64_t P = -1;
+    if (!isnull) {  // BinaryRow.getStruct: the child row at the slot's offset
+      const int64_t rel = (int32_t)(gget(slot, 8) >> 32);
+      const int64_t start = origin + rel;
+      if (rel < 0 || start + gbm(nd.nchild) + 8LL * nd.nchild > rend) set_status(status, FORY_ERR_CORRUPT);
+      else P = start;
+    }
+    T->P[f][k] = P;
+    T->TL[f][k] = P < 0 ? 0 : (int32_t)(rend - P);
+    return;
+  }
+  if (nd.kind == KIND_DECIMAL) {  // UnsafeTrait.getDecimal: 32 bytes, the high 16 the sign extension
+    if (!values) return;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (!isnull) {
+      const uint64_t os = gget(slot, 8);
+      const int64_t rel = (int64_t)(int32_t)(os >> 32), at = origin + rel;
+      if (rel < 0 || (uint32_t)os != 32u || at + 32 > rend || (at & 3)) {
+        set_status(status, FORY_ERR_CORRUPT);
+        return;
+      }
+      for (int q = 0; q < 4; ++q) w[q] = ld32(rows + at + 4 * q);
+      const uint32_t ext = (w[3] >> 31) ? 0xffffffffu : 0u;
+      bool fits = true;
+      for (int q = 4; q < 8; ++q) fits = fits && ld32(rows + at + 4 * q) == ext;
+      if (!fits) {
+        set_status(status, FORY_ERR_CORRUPT);
+        return;
+      }
+    }
+    for (int q = 0; q < 4; ++q) st32(col.out_values + 16 * k + 4 * q, w[q]);
+    return;
+  }
+  // BYTES / LIST / MAP: (offset, size) relative to the enclosing row / array
+  int64_t at = 0, size = 0;
+  if (!isnull) {
+    const uint64_t os = gget(slot, 8);
+    at = origin + (int64_t)(int32_t)(os >> 32);
+    size = (int64_t)(int32_t)(uint32_t)os;
+    if ((int32_t)(os >> 32) < 0 || size < 0 || at + size > rend) {
+      set_status(status, FORY_ERR_CORRUPT);
+      if (nd.kind != KIND_BYTES && (values || nd.cdepth < level)) T->P[f][k] = -1;
+      return;
+    }
+  }
+  if (!values) {
+    if (nd.cdepth == level) {  // this level's counts
+      if (!col.out_offsets) return;
+      int64_t cnt = 0;
+      if (!isnull) {
+        if (nd.kind == KIND_BYTES) {
+          cnt = size;
+        } else {
+          int64_t kat, vat;
+          cnt = td_container_n(L, rows, f, at, size, &kat, &vat);
+          if (cnt < 0) {
+            set_status(status, FORY_ERR_CORRUPT);
+            cnt = 0;
+          }
+        }
+      }
+      col.out_offsets[k + 1] = (int32_t)cnt;
+      return;
+    }
+    if (nd.kind == KIND_BYTES || nd.cdepth > level) return;
+  }
+  if (nd.kind == KIND_BYTES) {
+    if (isnull) return;
+    const int64_t o0 = col.out_offsets[k];
+    if ((int64_t)col.out_offsets[k + 1] - o0 != size) {  // differs from the sizes pass
+      set_status(status, FORY_ERR_CORRUPT);
+      return;
+    }
+    g_get_bytes(col.out_values + o0, rows + at, size);
+    return;
+  }
+  T->P[f][k] = isnull ? -1 : at;
+  T->SZ[f][k] = (int32_t)size;
+  T->TL[f][k] = isnull ? 0 : (int32_t)(rend - at);
+}
+
+// A scalar of width w from the slot's low bytes (UnsafeTrait.getX), 0 for nulls.
+__device__ __forceinline__ void td_scalar(const GNode& nd, const ColumnDev& col, int64_t k, const uint8_t* slot,
+                                          bool isnull) {
+  uint64_t v = isnull ? 0 : gget(slot, nd.width);
+  if (nd.kind == KIND_BOOL) v = (v & 0xff) ? 1 : 0;
+  store_elem(col.out_values, nd.width, k, v);
+}
+
+// Rows (ROWS) or bean node s: grid (instances / kTdWG, fields).
+template <bool ROWS>
+__global__ __launch_bounds__(kTdWG) void td_fields_kernel(GenLaunch L, const TdTables* __restrict__ T, int s,
+                                                          int64_t m, const uint8_t* __restrict__ rows,
+                                                          const int64_t* __restrict__ offs, int32_t* status) {
+  const int q = blockIdx.y;
+  const int f = T->kids[(ROWS ? 0 : T->kid0[s]) + q];
+  const GNode nd = L.nodes[f];
+  const ColumnDev col = L.cols[f];
+  const int nf = ROWS ? T->nroot : L.nodes[s].nchild;
+  const int bm = ROWS ? L.bitmap_bytes : gbm(nf);
+  const int level = L.fill_level;
+  const bool values = level < 0;
+  const int64_t k = (int64_t)blockIdx.x * kTdWG + threadIdx.x;
+  const bool inb = k < m;
+  int64_t base = -1, rend = 0;
+  if (inb) {
+    if (ROWS) {  // the frame checks of gen_decode_kernel; errors reported by field 0's lanes
+      const int64_t beg = offs[k], end = offs[k + 1];
+      const uint8_t* frame = rows + beg;
+      const int64_t len = end - beg;
+      const bool report = level <= 0 && q == 0;
+      int32_t err = 0;
+      const int hdr = frame_header_bytes(L.frame);
+      if (end < beg || len > 0x7fffffffLL + 12) err = FORY_ERR_CORRUPT;
+      else if (hdr == 12) {
+        if (len < 12) err = FORY_ERR_CORRUPT;
+        else if (gget(frame + 4, 8) != (uint64_t)L.schema_hash) err = FORY_ERR_SCHEMA_MISMATCH;
+        else if ((int64_t)ld32(frame) + 4 != len || len < 12 + L.fixed_size) err = FORY_ERR_CORRUPT;
+      } else if (hdr == 8) {
+        if (len < 8) err = FORY_ERR_CORRUPT;
+        else if (gget(frame, 8) != (uint64_t)L.schema_hash) err = FORY_ERR_SCHEMA_MISMATCH;
+        else if (len < 8 + L.fixed_size) err = FORY_ERR_CORRUPT;
+      } else if (len < L.fixed_size) {
+        err = FORY_ERR_CORRUPT;
+      }
+      if (err && report) set_status(status, err);
+      if (!err) {
+        base = beg + hdr;
+        rend = end;
+      }
+    } else {
+      base = T->P[s][k];
+      rend = base >= 0 ? base + T->TL[s][k] : 0;
+    }
+  }
+  const bool present = base >= 0;
+  const bool isnull = !present || ((rows[base + (q >> 3)] >> (q & 7)) & 1);  // isNullAt
+  if (values && (nd.flags & 1) && col.out_validity) {  // this wave's 64 instances: two words
+    const uint64_t bits = __ballot(inb && !isnull);
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (k - lane) >> 5;
+    if (lane == 0 && k < m) reinterpret_cast<uint32_t*>(col.out_validity)[w0] = (uint32_t)bits;
+    if (lane == 32 && k < m) reinterpret_cast<uint32_t*>(col.out_validity)[w0 + 1] = (uint32_t)(bits >> 32);
+  }
+  if (!inb) return;
+  const uint8_t* slot = rows + (present ? base : 0) + bm + 8 * q;
+  if (is_scalar(nd.kind)) {
+    if (values) td_scalar(nd, col, k, slot, isnull);
+    return;
+  }
+  td_value(L, T, f, nd, col, k, rows, slot, present ? base : 0, rend, isnull, level, status);
+}
+
+// Collection frames: [i32 size][the collection]: its position (COLLECTION frames).
+__global__ __launch_bounds__(kTdWG) void td_coll_kernel(GenLaunch L, const TdTables* __restrict__ T,
+                                                        const uint8_t* __restrict__ rows,
+                                                        const int64_t* __restrict__ offs, int32_t* status) {
+  const int64_t i = (int64_t)blockIdx.x * kTdWG + threadIdx.x;
+  if (i >= L.num_rows) return;
+  const int level = L.fill_level;
+  const int64_t beg = offs[i], end = offs[i + 1], len = end - beg;
+  bool present = !(end < beg || len > 0x7fffffffLL + 12);
+  if (present) {
+    const int64_t size = len >= 4 ? (int64_t)ld32(rows + beg) : -1;
+    if (size < 8 || size + 4 != len) present = false;
+  }
+  if (!present && level <= 0) set_status(status, FORY_ERR_CORRUPT);
+  const ColumnDev col = L.cols[0];
+  if (level < 0 && (L.nodes[0].flags & 1) && col.out_validity) td_valid_bit(col.out_validity, i, present);
+  if (level == 0) {
+    int64_t cnt = 0;
+    if (present) {
+      int64_t kat, vat;
+      cnt = td_container_n(L, rows, 0, beg + 4, len - 4, &kat, &vat);
+      if (cnt < 0) {
+        set_status(status, FORY_ERR_CORRUPT);
+        cnt = 0;
+      }
+    }
+    if (col.out_offsets) col.out_offsets[i + 1] = (int32_t)cnt;
+    return;
+  }
+  T->P[0][i] = present ? beg + 4 : -1;
+  T->SZ[0][i] = present ? (int32_t)(len - 4) : 0;
+  T->TL[0][i] = present ? (int32_t)(len - 4) : 0;
+}
+
+// List / map node c: a workgroup per kTdWG containers; headers, then the elements.
+__global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTables* __restrict__ T, int c,
+                                                         int64_t m, const uint8_t* __restrict__ rows,
+                                                         int32_t* status) {
+  __shared__ int64_t sK[kTdWG], sV[kTdWG], sE[kTdWG];  // key / value array starts (-1: none), record end
+  __shared__ int32_t sO[kTdWG + 1];                     // Arrow offsets of the workgroup's containers
+  const int tid = threadIdx.x;
+  const int64_t j0 = (int64_t)blockIdx.x * kTdWG;
+  const int cnt = m - j0 < kTdWG ? (int)(m - j0) : kTdWG;
+  const GNode nd = L.nodes[c];
+  const ColumnDev col = L.cols[c];
+  const bool map = nd.kind == KIND_MAP;
+  const int key = c + 1, val = map ? L.nodes[key].end : -1;
+  const int level = L.fill_level;
+  if (tid < cnt) {
+    const int64_t j = j0 + tid;
+    const int64_t P = T->P[c][j];
+    const int64_t o0 = col.out_offsets[j], o1 = col.out_offsets[j + 1];
+    int64_t kat = -1, vat = -1;
+    if (P >= 0) {
+      const int64_t n = td_container_n(L, rows, c, P, T->SZ[c][j], &kat, &vat);
+      if (n < 0 || n != o1 - o0) {  // corrupt, or the rows changed since the sizes pass
+        set_status(status, FORY_ERR_CORRUPT);
+        kat = vat = -1;
+      }
+    }
+    sK[tid] = kat;
+    sV[tid] = vat;
+    sE[tid] = P >= 0 ? P + T->TL[c][j] : 0;
+    sO[tid] = (int32_t)o0;
+    if (tid == cnt - 1) sO[cnt] = (int32_t)o1;
+  }
+  __syncthreads();
+  const int64_t e0 = sO[0], e1 = sO[cnt];
+  const int ends = map ? 2 : 1;
+  for (int64_t e = e0 + tid; e < e1; e += kTdWG) {
+    int a = 0, b = cnt - 1;  // the last container whose items start at or before e
+    while (a < b) {
+      const int mid = (a + b + 1) >> 1;
+      if (sO[mid] <= e) a = mid;
+      else b = mid - 1;
+    }
+    const int64_t n = sO[a + 1] - sO[a], q = e - sO[a];
+    for (int w = 0; w < ends; ++w) {
+      const int x = w ? val : key;
+      const GNode it = L.nodes[x];
+      const ColumnDev ic = L.cols[x];
+      const int64_t arr = w ? sV[a] : sK[a];
+      const bool present = arr >= 0 && q < n;
+      const bool isnull = !present || ((rows[arr + 8 + (q >> 3)] >> (q & 7)) & 1);
+      if (level < 0 && (it.flags & 1) && ic.out_validity) td_valid_bit(ic.out_validity, e, !isnull);
+      const uint8_t* slot = rows + (present ? arr + 8 + gbm(n) + q * elem_size(it) : 0);
+      if (is_scalar(it.kind)) {
+        if (level < 0) td_scalar(it, ic, e, slot, isnull);
+        continue;
+      }
+      if (!present && td_leaf(it.kind)) continue;
+      td_value(L, T, x, it, ic, e, rows, slot, present ? arr : 0, sE[a], isnull, level, status);
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_td_rows(const GenLaunch& L, const TdTables* T, int nroot, const uint8_t* rows, const int64_t* offs,
+                          int32_t* status, hipStream_t s) {
+  if (L.num_rows <= 0) return hipSuccess;
+  const unsigned gx = (unsigned)((L.num_rows + kTdWG - 1) / kTdWG);
+  if (L.frame == FORY_FRAME_COLLECTION)
+    hipLaunchKernelGGL(td_coll_kernel, dim3(gx), dim3(kTdWG), 0, s, L, T, rows, offs, status);
+  else
+    hipLaunchKernelGGL(td_fields_kernel<true>, dim3(gx, (unsigned)nroot), dim3(kTdWG), 0, s, L, T, -1, L.num_rows,
+                       rows, offs, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_td_node(const GenLaunch& L, const TdTables* T, int node, int64_t m, int kind, int nchild,
+                          const uint8_t* rows, int32_t* status, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  const unsigned gx = (unsigned)((m + kTdWG - 1) / kTdWG);
+  if (kind == KIND_LIST || kind == KIND_MAP)
+    hipLaunchKernelGGL(td_items_kernel, dim3(gx), dim3(kTdWG), 0, s, L, T, node, m, rows, status);
+  else if (nchild > 0)
+    hipLaunchKernelGGL(td_fields_kernel<false>, dim3(gx, (unsigned)nchild), dim3(kTdWG), 0, s, L, T, node, m, rows,
+                       nullptr, status);
+  return hipGetLastError();
+}
+
+}  // namespace fory_amd

@@ -69,9 +69,15 @@ class RowEncoder:
     def schema_hash(self) -> int:
         return self.plan.schema_hash
 
-    def workspace(self, n: int, cols=None):
+    def workspace(self, n: int, cols=None, decode: bool = False):
         import torch
-        need = max(256, self.plan.workspace_bytes(n) if cols is None else self.plan.encode_workspace_bytes(cols, n))
+        if cols is None:
+            need = self.plan.workspace_bytes(n)
+        elif decode:
+            need = self.plan.decode_workspace_bytes(cols, n)
+        else:
+            need = self.plan.encode_workspace_bytes(cols, n)
+        need = max(256, need)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self._ws
@@ -171,7 +177,9 @@ class RowEncoder:
             var_idx = [i for i, f in enumerate(fields) if cdepth[i] == level and f.type.id in var_kinds]
             if not var_idx:
                 break
-            native.decode_sizes(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
+            arr = native.column_array(cols)
+            ws = self.workspace(n, arr, decode=True)
+            native.decode_sizes(p, buf, offsets, n, frame_mode, arr, status, ws)
             last = torch.stack([cols[i].offsets[cols[i].length] for i in var_idx]).cpu().tolist()
             native.read_status(status)
             totals.update(zip(var_idx, last))
@@ -179,7 +187,9 @@ class RowEncoder:
                 if fields[i].type.id in (ArrowType.STRING, ArrowType.BINARY):
                     cols[i].values = torch.empty(max(1, int(totals[i])), dtype=torch.uint8, device=self.device)
             alloc(level + 1)
-        native.decode(p, buf, offsets, n, frame_mode, native.column_array(cols), status, ws)
+        arr = native.column_array(cols)
+        ws = self.workspace(n, arr, decode=True)
+        native.decode(p, buf, offsets, n, frame_mode, arr, status, ws)
         native.read_status(status)
         return cols
 

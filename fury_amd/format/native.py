@@ -73,6 +73,10 @@ class NativePlan:
         """Workspace for encode through the columnar tree engine (cols: column_array)."""
         return int(_lib.load().fory_rowfmt_encode_workspace_bytes(self.handle, cols, num_rows))
 
+    def decode_workspace_bytes(self, out_cols, num_rows: int) -> int:
+        """Workspace for the columnar decode given the levels allocated in out_cols (column_array)."""
+        return int(_lib.load().fory_rowfmt_decode_workspace_bytes(self.handle, out_cols, num_rows))
+
 
 @dataclass
 class DeviceColumn:

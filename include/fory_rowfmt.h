@@ -186,6 +186,15 @@ int64_t fory_rowfmt_workspace_bytes(const fory_plan* plan, int64_t num_rows);
 int64_t fory_rowfmt_encode_workspace_bytes(const fory_plan* plan, const fory_column* cols,
                                            int64_t num_rows);
 
+/* Workspace (bytes, >= fory_rowfmt_workspace_bytes) with which decode_sizes / decode of
+ * such plans take the columnar decode: per-node passes (rows and beans field by field,
+ * lists and maps element by element) with the positions of every bean / list / map
+ * instance of the levels allocated so far in out_cols (their fory_column.length) as
+ * temporaries. Ask again after allocating a deeper level: the need grows with it. A smaller
+ * workspace keeps the per-record decoder; the columns are identical. */
+int64_t fory_rowfmt_decode_workspace_bytes(const fory_plan* plan, const fory_column* out_cols,
+                                           int64_t num_rows);
+
 /* --- encode: replaces N x { writer.reset(); GeneratedRowEncoder.toRow(obj) }
  *     (Encoders.java:92-95 / 213-225, RowEncoderBuilder.java:177-208).
  *
