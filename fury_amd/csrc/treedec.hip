@@ -5,9 +5,9 @@
 // once per container depth for the counts and once for the values. Here every pass is a
 // grid over one node's instances (BaseBinaryEncoderBuilder's layout read back as
 // RowEncoderBuilder.fromRow / ArrayDataForEach do, RowEncoderBuilder.java:215-318):
-//   fields  rows (and each bean node): a lane per (field, instance), field-major, so the
-//           lanes of a wave write consecutive elements of one output column. The lane
-//           reads the field's null bit and slot and writes the value (scalars: the slot's
+//   fields  rows (and each bean node): a lane per instance, its fields in order; the
+//           lanes of a wave write consecutive elements of each output column. Per field
+//           the lane reads the null bit and slot and writes the value (scalars: the slot's
 //           low bytes; strings: the bytes at the slot's (offset, size); decimals: 32
 //           bytes, the high 16 the sign extension), the count of a string / list / map
 //           at this decode level, or hands a bean / list / map its position.
@@ -165,16 +165,15 @@ __device__ __forceinline__ void td_scalar(const GNode& nd, const ColumnDev& col,
   store_elem(col.out_values, nd.width, k, v);
 }
 
-// Rows (ROWS) or bean node s: grid (instances / kTdWG, fields).
+// Rows (ROWS) or bean node s: a lane per instance, its fields in order (the row's
+// header, bitmap and slots are one or two lines, read once); the lanes of a wave write
+// consecutive elements of each field's column, validity a word per 32 lanes by ballot.
 template <bool ROWS>
 __global__ __launch_bounds__(kTdWG) void td_fields_kernel(GenLaunch L, const TdTables* __restrict__ T, int s,
                                                           int64_t m, const uint8_t* __restrict__ rows,
                                                           const int64_t* __restrict__ offs, int32_t* status) {
-  const int q = blockIdx.y;
-  const int f = T->kids[(ROWS ? 0 : T->kid0[s]) + q];
-  const GNode nd = L.nodes[f];
-  const ColumnDev col = L.cols[f];
   const int nf = ROWS ? T->nroot : L.nodes[s].nchild;
+  const int k0 = ROWS ? 0 : T->kid0[s];
   const int bm = ROWS ? L.bitmap_bytes : gbm(nf);
   const int level = L.fill_level;
   const bool values = level < 0;
@@ -182,11 +181,10 @@ __global__ __launch_bounds__(kTdWG) void td_fields_kernel(GenLaunch L, const TdT
   const bool inb = k < m;
   int64_t base = -1, rend = 0;
   if (inb) {
-    if (ROWS) {  // the frame checks of gen_decode_kernel; errors reported by field 0's lanes
+    if (ROWS) {  // the frame checks of gen_decode_kernel
       const int64_t beg = offs[k], end = offs[k + 1];
       const uint8_t* frame = rows + beg;
       const int64_t len = end - beg;
-      const bool report = level <= 0 && q == 0;
       int32_t err = 0;
       const int hdr = frame_header_bytes(L.frame);
       if (end < beg || len > 0x7fffffffLL + 12) err = FORY_ERR_CORRUPT;
@@ -201,7 +199,7 @@ __global__ __launch_bounds__(kTdWG) void td_fields_kernel(GenLaunch L, const TdT
       } else if (len < L.fixed_size) {
         err = FORY_ERR_CORRUPT;
       }
-      if (err && report) set_status(status, err);
+      if (err && level <= 0) set_status(status, err);  // each error once
       if (!err) {
         base = beg + hdr;
         rend = end;
@@ -212,21 +210,28 @@ __global__ __launch_bounds__(kTdWG) void td_fields_kernel(GenLaunch L, const TdT
     }
   }
   const bool present = base >= 0;
-  const bool isnull = !present || ((rows[base + (q >> 3)] >> (q & 7)) & 1);  // isNullAt
-  if (values && (nd.flags & 1) && col.out_validity) {  // this wave's 64 instances: two words
-    const uint64_t bits = __ballot(inb && !isnull);
-    const int lane = threadIdx.x & 63;
-    const int64_t w0 = (k - lane) >> 5;
-    if (lane == 0 && k < m) reinterpret_cast<uint32_t*>(col.out_validity)[w0] = (uint32_t)bits;
-    if (lane == 32 && k < m) reinterpret_cast<uint32_t*>(col.out_validity)[w0 + 1] = (uint32_t)(bits >> 32);
+  const int lane = threadIdx.x & 63;
+  uint64_t nulls = 0;  // the bitmap word of fields [64 b, 64 b + 64)
+  for (int q = 0; q < nf; ++q) {
+    const int f = T->kids[k0 + q];
+    const GNode nd = L.nodes[f];
+    const ColumnDev col = L.cols[f];
+    if ((q & 63) == 0) nulls = present ? gget(rows + base + (q >> 3), bm - (q >> 3) >= 8 ? 8 : 4) : ~0ull;
+    const bool isnull = !present || ((nulls >> (q & 63)) & 1);  // isNullAt
+    if (values && (nd.flags & 1) && col.out_validity) {  // this wave's 64 instances: two words
+      const uint64_t bits = __ballot(inb && !isnull);
+      const int64_t w0 = (k - lane) >> 5;
+      if (lane == 0 && inb) reinterpret_cast<uint32_t*>(col.out_validity)[w0] = (uint32_t)bits;
+      if (lane == 32 && inb) reinterpret_cast<uint32_t*>(col.out_validity)[w0 + 1] = (uint32_t)(bits >> 32);
+    }
+    if (!inb) continue;
+    const uint8_t* slot = rows + (present ? base : 0) + bm + 8 * q;
+    if (is_scalar(nd.kind)) {
+      if (values) td_scalar(nd, col, k, slot, isnull);
+      continue;
+    }
+    td_value(L, T, f, nd, col, k, rows, slot, present ? base : 0, rend, isnull, level, status);
   }
-  if (!inb) return;
-  const uint8_t* slot = rows + (present ? base : 0) + bm + 8 * q;
-  if (is_scalar(nd.kind)) {
-    if (values) td_scalar(nd, col, k, slot, isnull);
-    return;
-  }
-  td_value(L, T, f, nd, col, k, rows, slot, present ? base : 0, rend, isnull, level, status);
 }
 
 // Collection frames: [i32 size][the collection]: its position (COLLECTION frames).
@@ -334,8 +339,7 @@ hipError_t launch_td_rows(const GenLaunch& L, const TdTables* T, int nroot, cons
   if (L.frame == FORY_FRAME_COLLECTION)
     hipLaunchKernelGGL(td_coll_kernel, dim3(gx), dim3(kTdWG), 0, s, L, T, rows, offs, status);
   else
-    hipLaunchKernelGGL(td_fields_kernel<true>, dim3(gx, (unsigned)nroot), dim3(kTdWG), 0, s, L, T, -1, L.num_rows,
-                       rows, offs, status);
+    hipLaunchKernelGGL(td_fields_kernel<true>, dim3(gx), dim3(kTdWG), 0, s, L, T, -1, L.num_rows, rows, offs, status);
   return hipGetLastError();
 }
 
@@ -346,8 +350,7 @@ hipError_t launch_td_node(const GenLaunch& L, const TdTables* T, int node, int64
   if (kind == KIND_LIST || kind == KIND_MAP)
     hipLaunchKernelGGL(td_items_kernel, dim3(gx), dim3(kTdWG), 0, s, L, T, node, m, rows, status);
   else if (nchild > 0)
-    hipLaunchKernelGGL(td_fields_kernel<false>, dim3(gx, (unsigned)nchild), dim3(kTdWG), 0, s, L, T, node, m, rows,
-                       nullptr, status);
+    hipLaunchKernelGGL(td_fields_kernel<false>, dim3(gx), dim3(kTdWG), 0, s, L, T, node, m, rows, nullptr, status);
   return hipGetLastError();
 }
 
