@@ -84,12 +84,16 @@ bool use_tiled(const Plan& p, int frame) {
 }
 
 void tc_forget(const void* ws);
+void td_forget(const void* ws);
 
-// keep_memo: encode may reuse the columnar sizes its encoded_size left in the workspace;
-// every other call may overwrite them.
+// Workspace memos of the columnar engine: encode may reuse the sizes its encoded_size
+// left in the workspace (KEEP_TC), decode_sizes the positions of the levels the previous
+// decode_sizes ran (KEEP_TD); every other call may overwrite them.
+enum { KEEP_NONE = 0, KEEP_TC = 1, KEEP_TD = 2 };
 int check_common(const fory_plan* plan, const fory_column* cols, int64_t n, int frame,
-                 void* ws, int64_t ws_bytes, bool keep_memo = false) {
-  if (!keep_memo) tc_forget(ws);
+                 void* ws, int64_t ws_bytes, int keep_memo = KEEP_NONE) {
+  if (keep_memo != KEEP_TC) tc_forget(ws);
+  if (keep_memo != KEEP_TD) td_forget(ws);
   if (!plan) return fail(FORY_ERR_INVALID_ARGUMENT, "plan is null");
   if (n < 0) return fail(FORY_ERR_INVALID_ARGUMENT, "num_rows < 0");
   if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM && frame != FORY_FRAME_COLLECTION &&
@@ -497,10 +501,16 @@ int64_t* partials_ptr(const Plan& p, void* ws) {
   return reinterpret_cast<int64_t*>(static_cast<uint8_t*>(ws) + table_bytes(p));
 }
 
+// Scan partials: one scan over the rows, or the flat decode's tile-total scans of
+// every var field at once.
+int64_t partials_bytes(const Plan& p, int64_t n) {
+  return align_up(std::max(fory_amd::scan_partials(n) + 2,
+                           fory_amd::scan_multi_partials((n + 63) / 64, (int)num_var_ops(p))) * 8);
+}
+
 // Per-tile payload totals of the flat decode (after the scan partials).
 int64_t* tile_totals_ptr(const Plan& p, void* ws, int64_t n) {
-  return reinterpret_cast<int64_t*>(static_cast<uint8_t*>(ws) + table_bytes(p) +
-                                    align_up((fory_amd::scan_partials(n) + 2) * 8));
+  return reinterpret_cast<int64_t*>(static_cast<uint8_t*>(ws) + table_bytes(p) + partials_bytes(p, n));
 }
 
 // Spill list of the tile engines (after the tile totals): [count][pad x3][tiles].
@@ -568,6 +578,13 @@ bool tc_leaf_kind(int k) { return k == fory_amd::KIND_BYTES || k == fory_amd::KI
 // Sizes (A): beans / lists / maps and item nodes; positions (P): beans / lists / maps.
 bool tc_needs_sizes(const Plan& p, const fory_amd::TcVar& v) { return v.items || !tc_leaf_kind(p.nodes[v.node].kind); }
 bool tc_needs_pos(const Plan& p, const fory_amd::TcVar& v) { return !tc_leaf_kind(p.nodes[v.node].kind); }
+// Beans of leaf fields under a list / map: read by their container's items pass (decode).
+// (Written inline by the encode's items pass they were not faster: measured 37.1 + 9.7 ms
+// against 27.2 + 18.9 ms of tc_write_cont + tc_write_fields over the nested-shape bench,
+// and the items kernel's extra registers slowed the lists of every plan.)
+bool tc_inline_bean(const Plan& p, const fory_amd::TcVar& v) {
+  return v.items && (p.gnodes[v.node].flags & fory_amd::kGNodeFlatBean);
+}
 
 void build_tc(fory_plan* plan) {
   const Plan& p = plan->p;
@@ -749,11 +766,19 @@ int tc_sizes(const fory_plan* plan, const fory_amd::GenLaunch& G, const fory_amd
 
 // --- columnar decode (treedec.hip) ------------------------------------------------
 // Positions (P, SZ, TL) of the bean / list / map instances known in this call.
+// (then the scan partials of a level's Arrow offsets columns, scanned together)
+int64_t td_partials_words(const fory_plan* plan, const std::vector<int64_t>& m) {
+  int64_t w = 0;
+  for (size_t i = 0; i < plan->p.nodes.size(); ++i)
+    if (is_var_kind(plan->p.nodes[i].kind)) w += fory_amd::scan_batch_partials(m[i]);
+  return w;
+}
+
 int64_t td_bytes(const fory_plan* plan, const std::vector<int64_t>& m) {
   int64_t b = align_up((int64_t)sizeof(fory_amd::TdTables));
   for (const fory_amd::TcVar& v : plan->tc.var)
     if (tc_needs_pos(plan->p, v)) b += align_up((m[v.node] + 1) * 8) + 2 * align_up((m[v.node] + 1) * 4);
-  return b;
+  return b + align_up(td_partials_words(plan, m) * 8);
 }
 
 bool td_usable(const fory_plan* plan, const fory_column* out_cols, int64_t n, int64_t ws_bytes) {
@@ -762,22 +787,25 @@ bool td_usable(const fory_plan* plan, const fory_column* out_cols, int64_t n, in
 }
 
 int td_prepare(const fory_plan* plan, const fory_column* out_cols, int64_t n, void* ws, hipStream_t s,
-               const fory_amd::TdTables** dT, std::vector<int64_t>* m) {
+               const fory_amd::TdTables** dT, std::vector<int64_t>* m, int64_t** partials = nullptr) {
   *m = tc_domains(plan, out_cols, n);
   uint8_t* base = static_cast<uint8_t*>(ws) + fory_rowfmt_workspace_bytes(plan, n);
   fory_amd::TdTables T;
   std::memset(&T, 0, sizeof(T));
   uint8_t* at = base + align_up((int64_t)sizeof(fory_amd::TdTables));
-  for (const fory_amd::TcVar& v : plan->tc.var) {
-    if (!tc_needs_pos(plan->p, v)) continue;
-    const int64_t k = (*m)[v.node] + 1;
-    T.P[v.node] = reinterpret_cast<int64_t*>(at);
-    at += align_up(k * 8);
-    T.SZ[v.node] = reinterpret_cast<int32_t*>(at);
-    at += align_up(k * 4);
-    T.TL[v.node] = reinterpret_cast<int32_t*>(at);
-    at += align_up(k * 4);
-  }
+  // by decode level: a level's arrays stay where they are when deeper levels are allocated
+  for (int32_t cd = 0; cd <= plan->p.max_cdepth; ++cd)
+    for (const fory_amd::TcVar& v : plan->tc.var) {
+      if (!tc_needs_pos(plan->p, v) || plan->p.gnodes[v.node].cdepth != cd) continue;
+      const int64_t k = (*m)[v.node] + 1;
+      T.P[v.node] = reinterpret_cast<int64_t*>(at);
+      at += align_up(k * 8);
+      T.SZ[v.node] = reinterpret_cast<int32_t*>(at);
+      at += align_up(k * 4);
+      T.TL[v.node] = reinterpret_cast<int32_t*>(at);
+      at += align_up(k * 4);
+    }
+  if (partials) *partials = reinterpret_cast<int64_t*>(at);
   int nk = 0;
   for (int32_t f : plan->p.top) T.kids[nk++] = f;
   T.nroot = nk;
@@ -790,21 +818,87 @@ int td_prepare(const fory_plan* plan, const fory_column* out_cols, int64_t n, vo
   return upload(base, &T, (int64_t)sizeof(T), s);
 }
 
-// The passes of one decode level (level >= 0: its counts; -1: the values): the rows, then
-// every bean / list / map node the level needs, parents first.
+// Levels the last columnar decode_sizes on a workspace ran: the next call with the same
+// plan, rows, row offsets and the same columns down to that level resumes after it
+// (the Python mirror and a JNI caller size one level per call).
+struct TdMemo {
+  const void* ws = nullptr;
+  uint64_t plan = 0, sig = 0;
+  int32_t level = -1;
+};
+std::mutex g_td_mu;
+TdMemo g_td_memo[16];
+int g_td_next = 0;
+
+uint64_t td_signature(const fory_plan* plan, const void* rows, const int64_t* offs, int64_t n, int frame,
+                      const fory_column* cols, int32_t level) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](uint64_t x) {
+    for (int b = 0; b < 8; ++b) h = (h ^ ((x >> (8 * b)) & 0xff)) * 1099511628211ull;
+  };
+  mix(plan->id);
+  mix(reinterpret_cast<uintptr_t>(rows));
+  mix(reinterpret_cast<uintptr_t>(offs));
+  mix((uint64_t)n);
+  mix((uint64_t)frame);
+  mix((uint64_t)(int64_t)level);
+  for (size_t i = 0; i < plan->p.nodes.size(); ++i) {
+    if (plan->p.gnodes[i].cdepth > level) continue;
+    // string / binary bytes are allocated after their level is sized: not an input here
+    if (plan->p.nodes[i].kind != fory_amd::KIND_BYTES) mix(reinterpret_cast<uintptr_t>(cols[i].values));
+    mix(reinterpret_cast<uintptr_t>(cols[i].offsets));
+    mix(reinterpret_cast<uintptr_t>(cols[i].validity));
+    mix((uint64_t)cols[i].length);
+  }
+  return h;
+}
+
+void td_forget(const void* ws) {
+  if (!ws) return;
+  std::lock_guard<std::mutex> lock(g_td_mu);
+  for (TdMemo& e : g_td_memo)
+    if (e.ws == ws) e = TdMemo{};
+}
+
+void td_remember(const fory_plan* plan, const void* ws, const void* rows, const int64_t* offs, int64_t n, int frame,
+                 const fory_column* cols, int32_t level) {
+  td_forget(ws);
+  if (level < 0) return;
+  const uint64_t sig = td_signature(plan, rows, offs, n, frame, cols, level);
+  std::lock_guard<std::mutex> lock(g_td_mu);
+  g_td_memo[g_td_next++ & 15] = TdMemo{ws, plan->id, sig, level};
+}
+
+// The last level done on this workspace for these inputs, or -1.
+int32_t td_recall(const fory_plan* plan, const void* ws, const void* rows, const int64_t* offs, int64_t n, int frame,
+                  const fory_column* cols) {
+  TdMemo e;
+  {
+    std::lock_guard<std::mutex> lock(g_td_mu);
+    for (const TdMemo& x : g_td_memo)
+      if (x.ws == ws && x.plan == plan->id) e = x;
+  }
+  if (!e.ws || td_signature(plan, rows, offs, n, frame, cols, e.level) != e.sig) return -1;
+  return e.level;
+}
+
+// The passes of one decode level, parents first. level >= 0: its counts (and the
+// positions of its beans / lists / maps) from the rows (level 0), the items of the
+// level-(L-1) lists / maps and the level-L beans, given the positions the passes of the
+// levels before it left in the workspace in this call; -1: every value, every pass.
 int td_run(const fory_plan* plan, fory_amd::GenLaunch G, const fory_amd::TdTables* dT, const std::vector<int64_t>& m,
            int level, const void* rows, const int64_t* offs, int32_t* status, hipStream_t s) {
   const Plan& p = plan->p;
   G.fill_level = level;
   const uint8_t* r = static_cast<const uint8_t*>(rows);
-  hipError_t e = fory_amd::launch_td_rows(G, dT, (int)p.top.size(), r, offs, status, s);
+  hipError_t e = hipSuccess;
+  if (level <= 0) e = fory_amd::launch_td_rows(G, dT, (int)p.top.size(), r, offs, status, s);
   for (size_t v = 0; v < plan->tc.var.size() && e == hipSuccess; ++v) {
     const int node = plan->tc.var[v].node;
     const int kind = p.nodes[node].kind;
     const int cd = p.gnodes[node].cdepth;
-    if (!tc_needs_pos(p, plan->tc.var[v])) continue;
-    if (level >= 0 && (kind == fory_amd::KIND_STRUCT ? cd > level : cd >= level)) continue;
-    if (G.frame == FORY_FRAME_COLLECTION && node == 0 && level == 0) continue;  // the frames pass counted it
+    if (!tc_needs_pos(p, plan->tc.var[v]) || tc_inline_bean(p, plan->tc.var[v])) continue;
+    if (level >= 0 && (kind == fory_amd::KIND_STRUCT ? cd != level : cd != level - 1)) continue;
     e = fory_amd::launch_td_node(G, dT, node, m[node], kind, (int)p.nodes[node].children.size(), r, status, s);
   }
   return e == hipSuccess ? FORY_OK : hip_fail(e, "td_decode");
@@ -916,7 +1010,7 @@ int fory_rowfmt_plan_info(const fory_plan* plan, fory_plan_info* info) {
 int64_t fory_rowfmt_workspace_bytes(const fory_plan* plan, int64_t num_rows) {
   if (!plan) return -1;
   const int64_t n = num_rows < 0 ? 0 : num_rows;
-  return table_bytes(plan->p) + align_up((fory_amd::scan_partials(n) + 2) * 8) +
+  return table_bytes(plan->p) + partials_bytes(plan->p, n) +
          align_up(fory_amd::var_tile_totals_words(num_var_ops(plan->p), n) * 8) +
          align_up(fory_amd::var_spill_words(n) * 4) + align_up(elem_partials_words(plan->p, n) * 8);
 }
@@ -986,7 +1080,7 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
                        int32_t frame_mode, const int64_t* d_row_offsets, void* d_out,
                        int64_t out_capacity, int32_t* d_status, void* d_workspace,
                        int64_t workspace_bytes, void* stream) {
-  int rc = check_common(plan, cols, num_rows, frame_mode, d_workspace, workspace_bytes, true);
+  int rc = check_common(plan, cols, num_rows, frame_mode, d_workspace, workspace_bytes, KEEP_TC);
   if (rc) return rc;
   if (!plan->p.generic || !tc_usable(plan, cols, num_rows, workspace_bytes, nullptr)) tc_forget(d_workspace);
   if (num_rows == 0) return FORY_OK;
@@ -1053,7 +1147,7 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
                              int64_t num_rows, int32_t frame_mode, const fory_column* out_cols,
                              int32_t* d_status, void* d_workspace, int64_t workspace_bytes,
                              void* stream) {
-  int rc = check_common(plan, out_cols, num_rows, frame_mode, d_workspace, workspace_bytes);
+  int rc = check_common(plan, out_cols, num_rows, frame_mode, d_workspace, workspace_bytes, KEEP_TD);
   if (rc) return rc;
   const Plan& p = plan->p;
   if (p.fixed_width || num_rows == 0) {
@@ -1077,6 +1171,21 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
     fory_amd::GenLaunch G{};
     rc = prepare_gen(p, out_cols, num_rows, frame_mode, d_workspace, s, &G, 0);
     if (rc) return rc;
+    const bool columnar = td_usable(plan, out_cols, num_rows, workspace_bytes);
+    const fory_amd::TdTables* dT = nullptr;
+    std::vector<int64_t> m;
+    int64_t* td_part = nullptr;
+    // columnar: the levels run in order, each from the positions the one before left; the
+    // levels the previous call on this workspace ran (same plan, rows and columns) are done
+    int32_t first = 0, last = -1;
+    if (columnar) {
+      rc = td_prepare(plan, out_cols, num_rows, d_workspace, s, &dT, &m, &td_part);
+      if (rc) return rc;
+      first = td_recall(plan, d_workspace, d_rows, d_row_offsets, num_rows, frame_mode, out_cols) + 1;
+      last = first - 1;
+    } else {
+      td_forget(d_workspace);
+    }
     for (int32_t level = 0; level <= p.max_cdepth; ++level) {
       bool any = false, ready = true;
       for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
@@ -1085,17 +1194,28 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
         if (!out_cols[idx].offsets || out_cols[idx].length < 0) ready = false;
       }
       if (!any || !ready) break;
+      if (level < first) continue;  // counts and positions left by the previous call
       hipError_t e = hipSuccess;
-      if (td_usable(plan, out_cols, num_rows, workspace_bytes)) {  // columnar: the passes down to this level
-        const fory_amd::TdTables* dT = nullptr;
-        std::vector<int64_t> m;
-        rc = td_prepare(plan, out_cols, num_rows, d_workspace, s, &dT, &m);
-        if (!rc) rc = td_run(plan, G, dT, m, level, d_rows, d_row_offsets, d_status, s);
+      if (columnar) {  // columnar: this level's passes
+        rc = td_run(plan, G, dT, m, level, d_rows, d_row_offsets, d_status, s);
         if (rc) return rc;
+        last = level;
       } else {
         G.fill_level = level;
         e = fory_amd::launch_gen_decode(G, static_cast<const uint8_t*>(d_rows), d_row_offsets, d_status, s);
         if (e != hipSuccess) return hip_fail(e, "gen_decode (lengths)");
+      }
+      if (columnar) {  // the level's offsets columns in one set of launches
+        std::vector<int32_t*> cs;
+        std::vector<int64_t> ns;
+        for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
+          if (!is_var_kind(p.nodes[idx].kind) || p.gnodes[idx].cdepth != level) continue;
+          cs.push_back(out_cols[idx].offsets);
+          ns.push_back(m[idx]);  // the instances of the column (the workspace's partials are sized by them)
+        }
+        e = fory_amd::launch_scan_offsets_batch(cs.data(), ns.data(), (int)cs.size(), td_part, d_status, s);
+        if (e != hipSuccess) return hip_fail(e, "scan offsets");
+        continue;
       }
       for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
         if (!is_var_kind(p.nodes[idx].kind) || p.gnodes[idx].cdepth != level) continue;
@@ -1107,6 +1227,7 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
         if (e != hipSuccess) return hip_fail(e, "scan offsets");
       }
     }
+    if (columnar) td_remember(plan, d_workspace, d_rows, d_row_offsets, num_rows, frame_mode, out_cols, last);
     return FORY_OK;
   }
   fory_amd::VarLaunch L{};

@@ -99,6 +99,25 @@ int64_t scan_partials(int64_t n);
 uint64_t* var_prof_buffer(int64_t tiles, bool on);
 int64_t var_prof_copy(uint64_t* host, int64_t max_words);
 hipError_t launch_scan_i64(int64_t* data, int64_t n, int64_t* partials, hipStream_t s);
+// `count` scans of n int64 at data + y * stride in one set of launches; partials:
+// scan_multi_partials(n, count) words.
+hipError_t launch_scan_i64_multi(int64_t* data, int64_t n, int64_t stride, int count, int64_t* partials,
+                                 hipStream_t s);
+int64_t scan_multi_partials(int64_t n, int count);
+// Arrow offsets columns of one decode level scanned together (lengths at [1..n]).
+constexpr int kMaxScanSeg = 16;
+struct OffsScanSeg {
+  int32_t* offs;
+  int64_t n;
+  int64_t pofs;  // first partials word
+};
+struct OffsScanBatch {
+  OffsScanSeg seg[kMaxScanSeg];
+  int32_t count;
+};
+int64_t scan_batch_partials(int64_t n);
+hipError_t launch_scan_offsets_batch(int32_t* const* cols, const int64_t* n, int count, int64_t* partials,
+                                     int32_t* status, hipStream_t s);
 // Arrow offsets: offs[1..n] hold lengths; writes offs[0]=0 and inclusive
 // prefix into offs[1..n] (int32). Overflow past INT32_MAX sets *status.
 hipError_t launch_scan_offsets_i32(int32_t* offs, int64_t n, int64_t* partials,

@@ -225,6 +225,14 @@ static int32_t fill_gnode(Plan* p, int32_t idx, int32_t cdepth) {
   g.kind = nd.kind;
   g.width = nd.width;
   g.flags = nd.nullable ? 1 : 0;
+  if (nd.kind == KIND_STRUCT && !nd.children.empty()) {  // a bean of leaf fields only
+    bool flat = true;
+    for (int32_t ch : nd.children) {
+      const int32_t k = p->nodes[ch].kind;
+      flat = flat && (k == KIND_FIXED || k == KIND_BOOL || k == KIND_BYTES || k == KIND_DECIMAL);
+    }
+    if (flat) g.flags |= kGNodeFlatBean;
+  }
   g.nchild = (int32_t)nd.children.size();
   g.cdepth = cdepth;
   g.prec = nd.prec;

@@ -111,10 +111,13 @@ struct ColumnDev {  // per-column device view (bound per call)
 
 // Schema tree node of the tree engine (generic.hip), one per pre-order
 // descriptor: a node's children follow it, its subtree ends at `end`.
+// GNode.flags: a struct whose fields are all leaves (fixed, bool, string / binary,
+// decimal): the columnar engine writes / reads it inside its container's items pass.
+constexpr int32_t kGNodeFlatBean = 2;
 struct GNode {
   int32_t kind;    // FieldKind
   int32_t width;   // 1/2/4/8 for fixed width, else -1
-  int32_t flags;   // bit0 nullable
+  int32_t flags;   // bit0 nullable; kGNodeFlatBean
   int32_t end;     // index after the subtree
   int32_t nchild;
   int32_t cdepth;  // list / map ancestors: the decode lengths pass that sizes this column

@@ -52,9 +52,14 @@ __device__ __forceinline__ int64_t scan_load(void* data, int64_t i) {
   return reinterpret_cast<const int32_t*>(data)[i + 1];
 }
 
+// Batched scans (blockIdx.y = segment): data and partials of segment y start at
+// y * dstride elements / y * pstride words (0 / 0: one scan).
 template <int MODE>
-__global__ __launch_bounds__(kWG) void scan_reduce_kernel(void* data, int64_t n, int64_t* partials) {
+__global__ __launch_bounds__(kWG) void scan_reduce_kernel(void* data, int64_t n, int64_t* partials, int64_t dstride = 0,
+                                                          int64_t pstride = 0) {
   __shared__ int64_t smem[kWaves];
+  if (MODE == 0) data = reinterpret_cast<int64_t*>(data) + blockIdx.y * dstride;
+  partials += blockIdx.y * pstride;
   const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
   int64_t s = 0;
 #pragma unroll
@@ -66,7 +71,7 @@ __global__ __launch_bounds__(kWG) void scan_reduce_kernel(void* data, int64_t n,
 }
 
 // Single workgroup: exclusive scan of the partials in place (any count).
-__global__ __launch_bounds__(kWG) void scan_partials_kernel(int64_t* partials, int64_t nb) {
+__device__ __forceinline__ void scan_partials_body(int64_t* partials, int64_t nb) {
   __shared__ int64_t smem[kWaves];
   int64_t carry = 0;
   for (int64_t b0 = 0; b0 < nb; b0 += kScanTile) {
@@ -91,12 +96,18 @@ __global__ __launch_bounds__(kWG) void scan_partials_kernel(int64_t* partials, i
   if (threadIdx.x == 0) partials[nb] = carry;
 }
 
+__global__ __launch_bounds__(kWG) void scan_partials_kernel(int64_t* partials, int64_t nb, int64_t pstride = 0) {
+  scan_partials_body(partials + blockIdx.y * pstride, nb);
+}
+
 // SEG (MODE 1): a segment of a longer offsets array: data[0] already holds the
 // previous segment's last offset (the carry; 0 for the first) and is left as is.
 template <int MODE, bool SEG = false>
 __global__ __launch_bounds__(kWG) void scan_down_kernel(void* data, int64_t n, const int64_t* partials,
-                                                        int32_t* status) {
+                                                        int32_t* status, int64_t dstride = 0, int64_t pstride = 0) {
   __shared__ int64_t smem[kWaves];
+  if (MODE == 0) data = reinterpret_cast<int64_t*>(data) + blockIdx.y * dstride;
+  partials += blockIdx.y * pstride;
   const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
   int64_t v[kScanItems];
   int64_t s = 0;
@@ -125,6 +136,53 @@ __global__ __launch_bounds__(kWG) void scan_down_kernel(void* data, int64_t n, c
     if (MODE == 0) reinterpret_cast<int64_t*>(data)[n] = partials[gridDim.x];
     else if (!SEG) reinterpret_cast<int32_t*>(data)[0] = 0;
   }
+}
+
+// Batched Arrow offsets scans (blockIdx.y = column): each column's lengths at
+// offs[1..n] scanned inclusive in place, offs[0] = 0; partials at seg.pofs.
+__global__ __launch_bounds__(kWG) void scan_reduce_batch_kernel(OffsScanBatch B, int64_t* partials) {
+  __shared__ int64_t smem[kWaves];
+  const OffsScanSeg g = B.seg[blockIdx.y];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  if ((int64_t)blockIdx.x * kScanTile >= g.n) return;  // (uniform per workgroup)
+  int64_t x = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k)
+    if (base + k < g.n) x += g.offs[base + k + 1];
+  int64_t tot;
+  block_excl_scan(x, smem, &tot);
+  if (threadIdx.x == 0) partials[g.pofs + blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kWG) void scan_partials_batch_kernel(OffsScanBatch B, int64_t* partials) {
+  const OffsScanSeg g = B.seg[blockIdx.y];
+  scan_partials_body(partials + g.pofs, (g.n + kScanTile - 1) / kScanTile);
+}
+
+__global__ __launch_bounds__(kWG) void scan_down_batch_kernel(OffsScanBatch B, const int64_t* partials,
+                                                              int32_t* status) {
+  __shared__ int64_t smem[kWaves];
+  const OffsScanSeg g = B.seg[blockIdx.y];
+  if ((int64_t)blockIdx.x * kScanTile >= g.n) return;
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int64_t v[kScanItems];
+  int64_t x = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    v[k] = base + k < g.n ? g.offs[base + k + 1] : 0;
+    x += v[k];
+  }
+  int64_t tot;
+  int64_t pre = block_excl_scan(x, smem, &tot) + partials[g.pofs + blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    if (base + k < g.n) {
+      pre += v[k];
+      if (pre > 0x7fffffffLL) set_status(status, FORY_ERR_CAPACITY);
+      g.offs[base + k + 1] = (int32_t)pre;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) g.offs[0] = 0;
 }
 
 // Host decode pipeline (host.cpp): a chunk's Arrow offsets (0-based) moved to their
@@ -185,6 +243,54 @@ hipError_t launch_scan_i64(int64_t* data, int64_t n, int64_t* partials, hipStrea
                      (const int64_t*)partials, (int32_t*)nullptr);
   return hipGetLastError();
 }
+
+// `count` exclusive int64 scans at once: segment y = data[y * stride .. + n) (data[y * stride
+// + n] = its total), partials: count * (scan_partials(n) + 1) words.
+hipError_t launch_scan_i64_multi(int64_t* data, int64_t n, int64_t stride, int count, int64_t* partials,
+                                 hipStream_t s) {
+  if (count <= 0) return hipSuccess;
+  const int64_t nb = (n + kScanTile - 1) / kScanTile;
+  const int64_t ps = nb + 2;
+  if (n <= 0) {
+    for (int y = 0; y < count; ++y) (void)hipMemsetAsync(data + y * stride, 0, sizeof(int64_t), s);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(scan_reduce_kernel<0>, dim3((unsigned)nb, (unsigned)count), dim3(kWG), 0, s, (void*)data, n,
+                     partials, stride, ps);
+  hipLaunchKernelGGL(scan_partials_kernel, dim3(1, (unsigned)count), dim3(kWG), 0, s, partials, nb, ps);
+  hipLaunchKernelGGL(scan_down_kernel<0>, dim3((unsigned)nb, (unsigned)count), dim3(kWG), 0, s, (void*)data, n,
+                     (const int64_t*)partials, (int32_t*)nullptr, stride, ps);
+  return hipGetLastError();
+}
+
+int64_t scan_batch_partials(int64_t n) { return (n + kScanTile - 1) / kScanTile + 2; }
+
+// Scans `count` Arrow offsets columns (cols[i] with lengths at [1..n[i]]) in three launches
+// per kMaxScanSeg columns; partials: the sum of scan_batch_partials(n[i]) words.
+hipError_t launch_scan_offsets_batch(int32_t* const* cols, const int64_t* n, int count, int64_t* partials,
+                                     int32_t* status, hipStream_t s) {
+  for (int c0 = 0; c0 < count; c0 += kMaxScanSeg) {
+    OffsScanBatch B{};
+    int64_t pofs = 0, maxnb = 0;
+    B.count = count - c0 < kMaxScanSeg ? count - c0 : kMaxScanSeg;
+    for (int y = 0; y < B.count; ++y) {
+      B.seg[y] = OffsScanSeg{cols[c0 + y], n[c0 + y], pofs};
+      pofs += scan_batch_partials(n[c0 + y]);
+      const int64_t nb = (n[c0 + y] + kScanTile - 1) / kScanTile;
+      maxnb = nb > maxnb ? nb : maxnb;
+      if (n[c0 + y] <= 0) (void)hipMemsetAsync(cols[c0 + y], 0, sizeof(int32_t), s);
+    }
+    if (maxnb == 0) continue;
+    hipLaunchKernelGGL(scan_reduce_batch_kernel, dim3((unsigned)maxnb, (unsigned)B.count), dim3(kWG), 0, s, B, partials);
+    hipLaunchKernelGGL(scan_partials_batch_kernel, dim3(1, (unsigned)B.count), dim3(kWG), 0, s, B, partials);
+    hipLaunchKernelGGL(scan_down_batch_kernel, dim3((unsigned)maxnb, (unsigned)B.count), dim3(kWG), 0, s, B,
+                       (const int64_t*)partials, status);
+    partials += pofs;
+  }
+  return hipGetLastError();
+}
+
+int64_t scan_multi_partials(int64_t n, int count) { return (int64_t)count * ((n + kScanTile - 1) / kScanTile + 2); }
 
 hipError_t launch_scan_offsets_i32(int32_t* offs, int64_t n, int64_t* partials, int32_t* status,
                                    hipStream_t s) {

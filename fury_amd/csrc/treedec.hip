@@ -17,9 +17,12 @@
 //           container found by binary search over the workgroup's offsets in LDS); each
 //           element is read like a field, its slot relative to its array.
 // Positions (the instance's start, its extent and its record's end) live in the
-// workspace for the call; decode_sizes at level L re-derives them for the levels above L
-// (nothing persists between calls). Every read is bounded by the record's end, with the
-// per-lane decoder's checks (FORY_ERR_CORRUPT).
+// workspace for the call. decode_sizes runs level by level: level L's passes (the rows
+// at L = 0, the items of the lists / maps of level L - 1, the beans of level L) write
+// level L's counts and the positions of its beans / lists / maps, which the next
+// level's passes start from (nothing persists between calls: each call starts at level
+// 0). Every read is bounded by the record's end, with the per-lane decoder's checks
+// (FORY_ERR_CORRUPT).
 #include "gen_device.h"
 
 namespace fory_amd {
@@ -29,12 +32,23 @@ constexpr int kTdWG = 256;
 
 __device__ __forceinline__ bool td_leaf(int kind) { return kind == KIND_BYTES || kind == KIND_DECIMAL; }
 
-// Validity bit pos of an Arrow bitmap (words shared between workgroups).
-__device__ __forceinline__ void td_valid_bit(uint8_t* validity, int64_t pos, bool valid) {
+// Validity of a wave's 64 consecutive positions from a 64-aligned base (lane l = base + l):
+// a word per half wave by ballot. inr: the lane's position is this workgroup's; a word
+// wholly inside the range is stored, a word shared with a neighbour's range (or past
+// the column's items) takes only this range's bits, by atomics.
+__device__ __forceinline__ void td_valid_words(uint8_t* validity, int64_t pos, bool inr, bool valid) {
+  const uint64_t vb = __ballot(inr && valid), rb = __ballot(inr);
+  const int lane = threadIdx.x & 63;
+  if (lane & 31) return;
+  const uint32_t v = (uint32_t)(vb >> (lane & 32)), r = (uint32_t)(rb >> (lane & 32));
+  if (!r) return;
   uint32_t* word = reinterpret_cast<uint32_t*>(validity) + (pos >> 5);
-  const uint32_t bit = 1u << (pos & 31);
-  if (valid) atomicOr(word, bit);
-  else atomicAnd(word, ~bit);
+  if (r == 0xffffffffu) {
+    *word = v;
+    return;
+  }
+  if (v) atomicOr(word, v);
+  if (r & ~v) atomicAnd(word, ~(r & ~v));
 }
 
 // Array header at `at` bounded by lim: numElements, or -1 (g_array_n).
@@ -117,13 +131,13 @@ __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, 
     size = (int64_t)(int32_t)(uint32_t)os;
     if ((int32_t)(os >> 32) < 0 || size < 0 || at + size > rend) {
       set_status(status, FORY_ERR_CORRUPT);
-      if (nd.kind != KIND_BYTES && (values || nd.cdepth < level)) T->P[f][k] = -1;
+      if (nd.kind != KIND_BYTES && (values || nd.cdepth <= level)) T->P[f][k] = -1;
       return;
     }
   }
   if (!values) {
-    if (nd.cdepth == level) {  // this level's counts
-      if (!col.out_offsets) return;
+    if (nd.cdepth > level) return;
+    if (nd.cdepth == level && col.out_offsets) {  // this level's counts
       int64_t cnt = 0;
       if (!isnull) {
         if (nd.kind == KIND_BYTES) {
@@ -138,9 +152,9 @@ __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, 
         }
       }
       col.out_offsets[k + 1] = (int32_t)cnt;
-      return;
     }
-    if (nd.kind == KIND_BYTES || nd.cdepth > level) return;
+    if (nd.kind == KIND_BYTES) return;
+    // a list / map: its position too, for the next level's items pass
   }
   if (nd.kind == KIND_BYTES) {
     if (isnull) return;
@@ -165,6 +179,34 @@ __device__ __forceinline__ void td_scalar(const GNode& nd, const ColumnDev& col,
   store_elem(col.out_values, nd.width, k, v);
 }
 
+// The fields of instance k (a row, or a bean at base; base < 0: absent, its fields null)
+// in order: nf fields kids[k0..], bm bitmap bytes. Lanes of a wave hold consecutive
+// instances from a 64-aligned one (inb: the lane's instance is in this call's range);
+// every lane runs it (validity by ballot).
+__device__ __forceinline__ void td_instance(const GenLaunch& L, const TdTables* T, int nf, int k0, int bm, int64_t k,
+                                            bool inb, int64_t base, int64_t rend, const uint8_t* rows,
+                                            int32_t* status) {
+  const int level = L.fill_level;
+  const bool values = level < 0;
+  const bool present = base >= 0;
+  uint64_t nulls = 0;  // the bitmap word of fields [64 b, 64 b + 64)
+  for (int q = 0; q < nf; ++q) {
+    const int f = T->kids[k0 + q];
+    const GNode nd = L.nodes[f];
+    const ColumnDev col = L.cols[f];
+    if ((q & 63) == 0) nulls = present ? gget(rows + base + (q >> 3), bm - (q >> 3) >= 8 ? 8 : 4) : ~0ull;
+    const bool isnull = !present || ((nulls >> (q & 63)) & 1);  // isNullAt
+    if (values && (nd.flags & 1) && col.out_validity) td_valid_words(col.out_validity, k, inb, !isnull);
+    if (!inb) continue;
+    const uint8_t* slot = rows + (present ? base : 0) + bm + 8 * q;
+    if (is_scalar(nd.kind)) {
+      if (values) td_scalar(nd, col, k, slot, isnull);
+      continue;
+    }
+    td_value(L, T, f, nd, col, k, rows, slot, present ? base : 0, rend, isnull, level, status);
+  }
+}
+
 // Rows (ROWS) or bean node s: a lane per instance, its fields in order (the row's
 // header, bitmap and slots are one or two lines, read once); the lanes of a wave write
 // consecutive elements of each field's column, validity a word per 32 lanes by ballot.
@@ -176,7 +218,6 @@ __global__ __launch_bounds__(kTdWG) void td_fields_kernel(GenLaunch L, const TdT
   const int k0 = ROWS ? 0 : T->kid0[s];
   const int bm = ROWS ? L.bitmap_bytes : gbm(nf);
   const int level = L.fill_level;
-  const bool values = level < 0;
   const int64_t k = (int64_t)blockIdx.x * kTdWG + threadIdx.x;
   const bool inb = k < m;
   int64_t base = -1, rend = 0;
@@ -209,29 +250,7 @@ __global__ __launch_bounds__(kTdWG) void td_fields_kernel(GenLaunch L, const TdT
       rend = base >= 0 ? base + T->TL[s][k] : 0;
     }
   }
-  const bool present = base >= 0;
-  const int lane = threadIdx.x & 63;
-  uint64_t nulls = 0;  // the bitmap word of fields [64 b, 64 b + 64)
-  for (int q = 0; q < nf; ++q) {
-    const int f = T->kids[k0 + q];
-    const GNode nd = L.nodes[f];
-    const ColumnDev col = L.cols[f];
-    if ((q & 63) == 0) nulls = present ? gget(rows + base + (q >> 3), bm - (q >> 3) >= 8 ? 8 : 4) : ~0ull;
-    const bool isnull = !present || ((nulls >> (q & 63)) & 1);  // isNullAt
-    if (values && (nd.flags & 1) && col.out_validity) {  // this wave's 64 instances: two words
-      const uint64_t bits = __ballot(inb && !isnull);
-      const int64_t w0 = (k - lane) >> 5;
-      if (lane == 0 && inb) reinterpret_cast<uint32_t*>(col.out_validity)[w0] = (uint32_t)bits;
-      if (lane == 32 && inb) reinterpret_cast<uint32_t*>(col.out_validity)[w0 + 1] = (uint32_t)(bits >> 32);
-    }
-    if (!inb) continue;
-    const uint8_t* slot = rows + (present ? base : 0) + bm + 8 * q;
-    if (is_scalar(nd.kind)) {
-      if (values) td_scalar(nd, col, k, slot, isnull);
-      continue;
-    }
-    td_value(L, T, f, nd, col, k, rows, slot, present ? base : 0, rend, isnull, level, status);
-  }
+  td_instance(L, T, nf, k0, bm, k, inb, base, rend, rows, status);
 }
 
 // Collection frames: [i32 size][the collection]: its position (COLLECTION frames).
@@ -239,17 +258,25 @@ __global__ __launch_bounds__(kTdWG) void td_coll_kernel(GenLaunch L, const TdTab
                                                         const uint8_t* __restrict__ rows,
                                                         const int64_t* __restrict__ offs, int32_t* status) {
   const int64_t i = (int64_t)blockIdx.x * kTdWG + threadIdx.x;
-  if (i >= L.num_rows) return;
+  const bool inb = i < L.num_rows;
   const int level = L.fill_level;
-  const int64_t beg = offs[i], end = offs[i + 1], len = end - beg;
-  bool present = !(end < beg || len > 0x7fffffffLL + 12);
-  if (present) {
-    const int64_t size = len >= 4 ? (int64_t)ld32(rows + beg) : -1;
-    if (size < 8 || size + 4 != len) present = false;
+  bool present = false;
+  int64_t beg = 0, len = 0;
+  if (inb) {
+    beg = offs[i];
+    const int64_t end = offs[i + 1];
+    len = end - beg;
+    present = !(end < beg || len > 0x7fffffffLL + 12);
+    if (present) {
+      const int64_t size = len >= 4 ? (int64_t)ld32(rows + beg) : -1;
+      if (size < 8 || size + 4 != len) present = false;
+    }
   }
+  if (level < 0 && (L.nodes[0].flags & 1) && L.cols[0].out_validity)
+    td_valid_words(L.cols[0].out_validity, i, inb, present);
+  if (!inb) return;
   if (!present && level <= 0) set_status(status, FORY_ERR_CORRUPT);
   const ColumnDev col = L.cols[0];
-  if (level < 0 && (L.nodes[0].flags & 1) && col.out_validity) td_valid_bit(col.out_validity, i, present);
   if (level == 0) {
     int64_t cnt = 0;
     if (present) {
@@ -261,7 +288,6 @@ __global__ __launch_bounds__(kTdWG) void td_coll_kernel(GenLaunch L, const TdTab
       }
     }
     if (col.out_offsets) col.out_offsets[i + 1] = (int32_t)cnt;
-    return;
   }
   T->P[0][i] = present ? beg + 4 : -1;
   T->SZ[0][i] = present ? (int32_t)(len - 4) : 0;
@@ -303,23 +329,40 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
   __syncthreads();
   const int64_t e0 = sO[0], e1 = sO[cnt];
   const int ends = map ? 2 : 1;
-  for (int64_t e = e0 + tid; e < e1; e += kTdWG) {
-    int a = 0, b = cnt - 1;  // the last container whose items start at or before e
-    while (a < b) {
-      const int mid = (a + b + 1) >> 1;
-      if (sO[mid] <= e) a = mid;
-      else b = mid - 1;
+  // waves walk 64-aligned groups of items (uniform trip count: validity by ballot)
+  for (int64_t eb = e0 & ~int64_t(63); eb < e1; eb += kTdWG) {
+    const int64_t e = eb + tid;
+    const bool inr = e >= e0 && e < e1;
+    int a = 0;
+    if (inr) {
+      int b = cnt - 1;  // the last container whose items start at or before e
+      while (a < b) {
+        const int mid = (a + b + 1) >> 1;
+        if (sO[mid] <= e) a = mid;
+        else b = mid - 1;
+      }
     }
     const int64_t n = sO[a + 1] - sO[a], q = e - sO[a];
     for (int w = 0; w < ends; ++w) {
       const int x = w ? val : key;
       const GNode it = L.nodes[x];
       const ColumnDev ic = L.cols[x];
-      const int64_t arr = w ? sV[a] : sK[a];
+      const int64_t arr = inr ? (w ? sV[a] : sK[a]) : -1;
       const bool present = arr >= 0 && q < n;
       const bool isnull = !present || ((rows[arr + 8 + (q >> 3)] >> (q & 7)) & 1);
-      if (level < 0 && (it.flags & 1) && ic.out_validity) td_valid_bit(ic.out_validity, e, !isnull);
+      if (level < 0 && (it.flags & 1) && ic.out_validity) td_valid_words(ic.out_validity, e, inr, !isnull);
       const uint8_t* slot = rows + (present ? arr + 8 + gbm(n) + q * elem_size(it) : 0);
+      if (it.flags & kGNodeFlatBean) {  // a bean of leaf fields: read here, no pass of its own
+        int64_t P = -1;
+        if (!isnull) {  // BinaryArray.getStruct: the child row at the element's offset
+          const int64_t rel = (int32_t)(gget(slot, 8) >> 32);
+          if (rel < 0 || arr + rel + gbm(it.nchild) + 8LL * it.nchild > sE[a]) set_status(status, FORY_ERR_CORRUPT);
+          else P = arr + rel;
+        }
+        td_instance(L, T, it.nchild, T->kid0[x], gbm(it.nchild), e, inr, P, P < 0 ? 0 : sE[a], rows, status);
+        continue;
+      }
+      if (!inr) continue;
       if (is_scalar(it.kind)) {
         if (level < 0) td_scalar(it, ic, e, slot, isnull);
         continue;

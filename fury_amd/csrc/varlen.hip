@@ -2533,10 +2533,8 @@ hipError_t launch_var_decode_lengths(const VarLaunch& L, const uint8_t* rows, co
   hipError_t e = launch_var_decode_pass<false>(L, rows, offs, tile_tot, status, s);
   if (e != hipSuccess || !var_decode_tiled_offsets(L)) return e;
   const int64_t tiles = (L.num_rows + 63) / 64;
-  for (int v = 0; v < L.num_var; ++v) {  // exclusive scan of each field's tile totals
-    e = launch_scan_i64(tile_tot + v * (tiles + 1), tiles, partials, s);
-    if (e != hipSuccess) return e;
-  }
+  e = launch_scan_i64_multi(tile_tot, tiles, tiles + 1, L.num_var, partials, s);  // each field's tile totals
+  if (e != hipSuccess) return e;
   const int64_t words = (int64_t)L.num_var * (tiles + 1);
   hipLaunchKernelGGL(flat_tile_bases_kernel, dim3((unsigned)((words + kWG - 1) / kWG)), dim3(kWG), 0, s, L.vf,
                      L.num_var, tile_tot, L.num_rows, status);

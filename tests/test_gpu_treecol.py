@@ -173,3 +173,44 @@ def test_columnar_large_batch(name):
     schema, cols = nested_columns(name, n, 21)
     enc = RowEncoder(schema)
     oracle_equal(schema, cols, n, 1, enc.encode(to_device(cols), n, 1))
+
+
+@pytest.mark.parametrize("name", ["holder", "lists", "maps_nested", "bean_a", "chain"])
+def test_decode_levels_resume_from_the_previous_call(name):
+    """decode_sizes sizes one level per call; on one workspace a call resumes after the
+    levels the previous call ran (same plan, rows and columns). The columns equal the
+    input with: one big workspace (every call resumes), a fresh workspace per call (none
+    does), and a decode of other rows through the same workspace between the levels (its
+    positions must not be taken for these rows')."""
+    from helpers import columns_equal
+    from fury_amd.format.columns import to_host
+    n = 60 if name == "chain" else 700
+    schema, cols = nested_columns(name, n, 31)
+    _, other = nested_columns(name, n, 32)
+    enc = RowEncoder(schema)
+    rows = enc.encode(to_device(cols), n, 1)
+    rows_b = enc.encode(to_device(other), n, 1)
+    enc._ws = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+    assert columns_equal(schema, cols, to_host(enc.decode(rows))) == []
+    keep = []
+
+    def fresh(m, c=None, decode=False):
+        need = enc.plan.decode_workspace_bytes(c, m) if decode else enc.plan.workspace_bytes(m)
+        keep.append(torch.empty(max(256, need), dtype=torch.uint8, device="cuda"))
+        return keep[-1]
+
+    big = enc._ws
+    enc.workspace = fresh
+    assert columns_equal(schema, cols, to_host(enc.decode(rows))) == []
+    calls = []
+
+    def interleaved(m, c=None, decode=False):  # every other call: a full decode of rows_b first
+        calls.append(1)
+        if decode and len(calls) % 2 == 0:
+            enc.workspace = lambda *a, **k: big
+            enc.decode(rows_b)
+            enc.workspace = interleaved
+        return big
+
+    enc.workspace = interleaved
+    assert columns_equal(schema, cols, to_host(enc.decode(rows))) == []
