@@ -899,7 +899,12 @@ int td_run(const fory_plan* plan, fory_amd::GenLaunch G, const fory_amd::TdTable
     const int cd = p.gnodes[node].cdepth;
     if (!tc_needs_pos(p, plan->tc.var[v]) || tc_inline_bean(p, plan->tc.var[v])) continue;
     if (level >= 0 && (kind == fory_amd::KIND_STRUCT ? cd != level : cd != level - 1)) continue;
-    e = fory_amd::launch_td_node(G, dT, node, m[node], kind, (int)p.nodes[node].children.size(), r, status, s);
+    int iflags = 0;  // the item nodes' flags (a list's item, a map's key and value)
+    if (kind == fory_amd::KIND_LIST || kind == fory_amd::KIND_MAP) {
+      iflags = p.gnodes[node + 1].flags;
+      if (kind == fory_amd::KIND_MAP) iflags |= p.gnodes[p.gnodes[node + 1].end].flags;
+    }
+    e = fory_amd::launch_td_node(G, dT, node, m[node], kind, (int)p.nodes[node].children.size(), iflags, r, status, s);
   }
   return e == hipSuccess ? FORY_OK : hip_fail(e, "td_decode");
 }

@@ -204,7 +204,7 @@ struct TdTables {
 hipError_t launch_td_rows(const GenLaunch& L, const TdTables* T, int nroot, const uint8_t* rows, const int64_t* offs,
                           int32_t* status, hipStream_t s);
 hipError_t launch_td_node(const GenLaunch& L, const TdTables* T, int node, int64_t m, int kind, int nchild,
-                          const uint8_t* rows, int32_t* status, hipStream_t s);
+                          int item_flags, const uint8_t* rows, int32_t* status, hipStream_t s);
 
 // Frame index of a STREAM batch (frames.hip): the starts of the first num_rows
 // frames of rows_bytes bytes, found on the device from the stream alone.

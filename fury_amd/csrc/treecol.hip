@@ -476,6 +476,7 @@ __device__ __forceinline__ int32_t tc_element(const GenLaunch& L, const TcTables
 
 // Lists / maps: a workgroup per kTcWG containers. Headers lane per container, then the
 // elements item-parallel over the workgroup's items.
+template <bool MAP>  // per container kind: a list's instantiation carries no value-array path
 __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const TcTables* __restrict__ T, int c,
                                                               int64_t m, uint8_t* __restrict__ out, int64_t cap,
                                                               int32_t* status) {
@@ -485,8 +486,7 @@ __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const
   const int tid = threadIdx.x;
   const int64_t j0 = (int64_t)blockIdx.x * kTcWG;
   const int cnt = m - j0 < kTcWG ? (int)(m - j0) : kTcWG;
-  const GNode nd = L.nodes[c];
-  const bool map = nd.kind == KIND_MAP;
+  constexpr bool map = MAP;
   const int key = c + 1, val = map ? L.nodes[key].end : -1;
   const int64_t mx = T->m[key];
   int32_t err = 0;
@@ -610,8 +610,9 @@ hipError_t launch_tc_write_node(const GenLaunch& L, const TcTables* T, int node,
                                 int64_t capacity, int32_t* status, hipStream_t s, int kind, int nchild) {
   if (m <= 0) return hipSuccess;
   if (kind == KIND_LIST || kind == KIND_MAP) {
-    hipLaunchKernelGGL(tc_write_cont_kernel, dim3((unsigned)((m + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s, L, T,
-                       node, m, out, capacity, status);
+    hipLaunchKernelGGL(kind == KIND_MAP ? tc_write_cont_kernel<true> : tc_write_cont_kernel<false>,
+                       dim3((unsigned)((m + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s, L, T, node, m, out, capacity,
+                       status);
   } else {
     const int64_t work = m * (nchild > 0 ? nchild : 1);
     hipLaunchKernelGGL(tc_write_fields_kernel<false>, dim3((unsigned)((work + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0,

@@ -29,6 +29,7 @@ namespace fory_amd {
 namespace {
 
 constexpr int kTdWG = 256;
+constexpr int kTdBatch = 4;  // fields whose slot words an instance loads together
 
 __device__ __forceinline__ bool td_leaf(int kind) { return kind == KIND_BYTES || kind == KIND_DECIMAL; }
 
@@ -80,19 +81,19 @@ __device__ __forceinline__ int64_t td_container_n(const GenLaunch& L, const uint
   return nk < 0 || nk != nv ? -1 : nk;
 }
 
-// One value of node f, instance k, read through `slot` of the row / array starting at
+// One value of node f, instance k, from its slot word sv in the row / array starting at
 // `origin` (slots' offsets are relative to it), in a record ending at rend. Scalars and
 // validity are the caller's. level >= 0: the counts of that decode level (and the positions
 // the levels below need); -1: the values.
 __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, int f, const GNode& nd,
-                                         const ColumnDev& col, int64_t k, const uint8_t* rows, const uint8_t* slot,
+                                         const ColumnDev& col, int64_t k, const uint8_t* rows, uint64_t sv,
                                          int64_t origin, int64_t rend, bool isnull, int level, int32_t* status) {
   const bool values = level < 0;
   if (nd.kind == KIND_STRUCT) {
     if (!values && nd.cdepth > level) return;
     int64_t P = -1;
     if (!isnull) {  // BinaryRow.getStruct: the child row at the slot's offset
-      const int64_t rel = (int32_t)(gget(slot, 8) >> 32);
+      const int64_t rel = (int32_t)(sv >> 32);
       const int64_t start = origin + rel;
       if (rel < 0 || start + gbm(nd.nchild) + 8LL * nd.nchild > rend) set_status(status, FORY_ERR_CORRUPT);
       else P = start;
@@ -105,7 +106,7 @@ __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, 
     if (!values) return;
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     if (!isnull) {
-      const uint64_t os = gget(slot, 8);
+      const uint64_t os = sv;
       const int64_t rel = (int64_t)(int32_t)(os >> 32), at = origin + rel;
       if (rel < 0 || (uint32_t)os != 32u || at + 32 > rend || (at & 3)) {
         set_status(status, FORY_ERR_CORRUPT);
@@ -126,7 +127,7 @@ __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, 
   // BYTES / LIST / MAP: (offset, size) relative to the enclosing row / array
   int64_t at = 0, size = 0;
   if (!isnull) {
-    const uint64_t os = gget(slot, 8);
+    const uint64_t os = sv;
     at = origin + (int64_t)(int32_t)(os >> 32);
     size = (int64_t)(int32_t)(uint32_t)os;
     if ((int32_t)(os >> 32) < 0 || size < 0 || at + size > rend) {
@@ -172,9 +173,8 @@ __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, 
 }
 
 // A scalar of width w from the slot's low bytes (UnsafeTrait.getX), 0 for nulls.
-__device__ __forceinline__ void td_scalar(const GNode& nd, const ColumnDev& col, int64_t k, const uint8_t* slot,
-                                          bool isnull) {
-  uint64_t v = isnull ? 0 : gget(slot, nd.width);
+__device__ __forceinline__ void td_scalar(const GNode& nd, const ColumnDev& col, int64_t k, uint64_t sv, bool isnull) {
+  uint64_t v = isnull ? 0 : (nd.width >= 8 ? sv : sv & ((1ull << (8 * nd.width)) - 1));
   if (nd.kind == KIND_BOOL) v = (v & 0xff) ? 1 : 0;
   store_elem(col.out_values, nd.width, k, v);
 }
@@ -189,21 +189,34 @@ __device__ __forceinline__ void td_instance(const GenLaunch& L, const TdTables* 
   const int level = L.fill_level;
   const bool values = level < 0;
   const bool present = base >= 0;
+  const bool rd = inb && present;
   uint64_t nulls = 0;  // the bitmap word of fields [64 b, 64 b + 64)
-  for (int q = 0; q < nf; ++q) {
-    const int f = T->kids[k0 + q];
-    const GNode nd = L.nodes[f];
-    const ColumnDev col = L.cols[f];
-    if ((q & 63) == 0) nulls = present ? gget(rows + base + (q >> 3), bm - (q >> 3) >= 8 ? 8 : 4) : ~0ull;
-    const bool isnull = !present || ((nulls >> (q & 63)) & 1);  // isNullAt
-    if (values && (nd.flags & 1) && col.out_validity) td_valid_words(col.out_validity, k, inb, !isnull);
-    if (!inb) continue;
-    const uint8_t* slot = rows + (present ? base : 0) + bm + 8 * q;
-    if (is_scalar(nd.kind)) {
-      if (values) td_scalar(nd, col, k, slot, isnull);
-      continue;
+  // fields in batches: the batch's slot words (and the bitmap word) are loaded together
+  // before any is used, so an instance costs one memory latency per batch, not per field
+  for (int q0 = 0; q0 < nf; q0 += kTdBatch) {
+    uint64_t sv[kTdBatch];
+    if ((q0 & 63) == 0) nulls = rd ? gget(rows + base + (q0 >> 3), bm - (q0 >> 3) >= 8 ? 8 : 4) : ~0ull;
+#pragma unroll
+    for (int u = 0; u < kTdBatch; ++u) sv[u] = rd && q0 + u < nf ? gget(rows + base + bm + 8 * (q0 + u), 8) : 0;
+#pragma unroll 1
+    for (int u = 0; u < kTdBatch; ++u) {  // rolled: one copy of the field body
+      const int q = q0 + u;
+      if (q >= nf) break;
+      uint64_t w = sv[0];
+#pragma unroll
+      for (int t = 1; t < kTdBatch; ++t) w = u == t ? sv[t] : w;
+      const int f = T->kids[k0 + q];
+      const GNode nd = L.nodes[f];
+      const ColumnDev col = L.cols[f];
+      const bool isnull = !present || ((nulls >> (q & 63)) & 1);  // isNullAt
+      if (values && (nd.flags & 1) && col.out_validity) td_valid_words(col.out_validity, k, inb, !isnull);
+      if (!inb) continue;
+      if (is_scalar(nd.kind)) {
+        if (values) td_scalar(nd, col, k, w, isnull);
+        continue;
+      }
+      td_value(L, T, f, nd, col, k, rows, w, present ? base : 0, rend, isnull, level, status);
     }
-    td_value(L, T, f, nd, col, k, rows, slot, present ? base : 0, rend, isnull, level, status);
   }
 }
 
@@ -295,6 +308,9 @@ __global__ __launch_bounds__(kTdWG) void td_coll_kernel(GenLaunch L, const TdTab
 }
 
 // List / map node c: a workgroup per kTdWG containers; headers, then the elements.
+// MAP: node c is a map (keys and values); FLAT: some item node is a bean of leaf fields
+// (read inline). Instantiated per shape: each carries only the paths it takes.
+template <bool MAP, bool FLAT>
 __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTables* __restrict__ T, int c,
                                                          int64_t m, const uint8_t* __restrict__ rows,
                                                          int32_t* status) {
@@ -303,9 +319,8 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
   const int tid = threadIdx.x;
   const int64_t j0 = (int64_t)blockIdx.x * kTdWG;
   const int cnt = m - j0 < kTdWG ? (int)(m - j0) : kTdWG;
-  const GNode nd = L.nodes[c];
   const ColumnDev col = L.cols[c];
-  const bool map = nd.kind == KIND_MAP;
+  constexpr bool map = MAP;
   const int key = c + 1, val = map ? L.nodes[key].end : -1;
   const int level = L.fill_level;
   if (tid < cnt) {
@@ -351,11 +366,12 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
       const bool present = arr >= 0 && q < n;
       const bool isnull = !present || ((rows[arr + 8 + (q >> 3)] >> (q & 7)) & 1);
       if (level < 0 && (it.flags & 1) && ic.out_validity) td_valid_words(ic.out_validity, e, inr, !isnull);
-      const uint8_t* slot = rows + (present ? arr + 8 + gbm(n) + q * elem_size(it) : 0);
-      if (it.flags & kGNodeFlatBean) {  // a bean of leaf fields: read here, no pass of its own
+      const int es = elem_size(it);
+      const uint64_t sv = isnull ? 0 : gget(rows + arr + 8 + gbm(n) + q * es, es);
+      if (FLAT && (it.flags & kGNodeFlatBean)) {  // a bean of leaf fields: read here, no pass of its own
         int64_t P = -1;
         if (!isnull) {  // BinaryArray.getStruct: the child row at the element's offset
-          const int64_t rel = (int32_t)(gget(slot, 8) >> 32);
+          const int64_t rel = (int32_t)(sv >> 32);
           if (rel < 0 || arr + rel + gbm(it.nchild) + 8LL * it.nchild > sE[a]) set_status(status, FORY_ERR_CORRUPT);
           else P = arr + rel;
         }
@@ -364,11 +380,11 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
       }
       if (!inr) continue;
       if (is_scalar(it.kind)) {
-        if (level < 0) td_scalar(it, ic, e, slot, isnull);
+        if (level < 0) td_scalar(it, ic, e, sv, isnull);
         continue;
       }
       if (!present && td_leaf(it.kind)) continue;
-      td_value(L, T, x, it, ic, e, rows, slot, present ? arr : 0, sE[a], isnull, level, status);
+      td_value(L, T, x, it, ic, e, rows, sv, present ? arr : 0, sE[a], isnull, level, status);
     }
   }
 }
@@ -387,13 +403,17 @@ hipError_t launch_td_rows(const GenLaunch& L, const TdTables* T, int nroot, cons
 }
 
 hipError_t launch_td_node(const GenLaunch& L, const TdTables* T, int node, int64_t m, int kind, int nchild,
-                          const uint8_t* rows, int32_t* status, hipStream_t s) {
+                          int item_flags, const uint8_t* rows, int32_t* status, hipStream_t s) {
   if (m <= 0) return hipSuccess;
   const unsigned gx = (unsigned)((m + kTdWG - 1) / kTdWG);
-  if (kind == KIND_LIST || kind == KIND_MAP)
-    hipLaunchKernelGGL(td_items_kernel, dim3(gx), dim3(kTdWG), 0, s, L, T, node, m, rows, status);
-  else if (nchild > 0)
+  if (kind == KIND_LIST || kind == KIND_MAP) {
+    const bool map = kind == KIND_MAP, flat = (item_flags & kGNodeFlatBean) != 0;
+    auto* k = map ? (flat ? &td_items_kernel<true, true> : &td_items_kernel<true, false>)
+                  : (flat ? &td_items_kernel<false, true> : &td_items_kernel<false, false>);
+    hipLaunchKernelGGL(k, dim3(gx), dim3(kTdWG), 0, s, L, T, node, m, rows, status);
+  } else if (nchild > 0) {
     hipLaunchKernelGGL(td_fields_kernel<false>, dim3(gx), dim3(kTdWG), 0, s, L, T, node, m, rows, nullptr, status);
+  }
   return hipGetLastError();
 }
 
