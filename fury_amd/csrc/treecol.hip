@@ -313,6 +313,33 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_kernel(GenLaunch L, con
   if (w >= (uint64_t)m * (uint64_t)nf) return;
   const int64_t k = (int64_t)(w / (uint64_t)nf);
   const int q = (int)(w - (uint64_t)k * (uint64_t)nf);
+  const GNode nd = s_nd[q];
+  const ColumnDev col = s_col[q];
+  const int kid = s_kid[q];
+  const bool has_pos = tc_has_pos(nd.kind), var = tc_is_var(nd.kind);
+  // Everything that does not depend on the instance's position is loaded first, so the
+  // lane waits one memory latency for all of it (the position is one more load):
+  // null bit, value or (bytes of the var fields before this one, this one's bytes), and
+  // lane 0's bitmap words (and, for rows, the row's var bytes to check its size).
+  const bool isnull = (nd.flags & 1) && !gvalid(col.validity, k);
+  uint64_t v = 0;
+  int64_t rel = 0, S = 0;
+  if (!var) {
+    v = load_elem(col.values, nd.width, k);
+    if (nd.kind == KIND_BOOL) v = v ? 1 : 0;
+  } else {
+    for (int f = 0; f < q; ++f)
+      if (tc_is_var(s_nd[f].kind)) rel += tc_size(T, s_kid[f], s_nd[f], s_col[f], k);
+    S = tc_size(T, kid, nd, col, k);
+  }
+  uint32_t bw[kTcMaxNodes / 32] = {0u, 0u, 0u, 0u};  // lane q = 0: setNullAt bits of every field
+  int64_t need = 0;
+  if (q == 0) {
+    for (int f = 0; f < nf; ++f) {
+      if ((s_nd[f].flags & 1) && !gvalid(s_col[f].validity, k)) bw[f >> 5] |= 1u << (f & 31);
+      if (ROWS && tc_is_var(s_nd[f].kind)) need += tc_size(T, s_kid[f], s_nd[f], s_col[f], k);
+    }
+  }
   int64_t P;
   int hdr = 0;
   int64_t beg = 0, size = 0;
@@ -331,10 +358,6 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_kernel(GenLaunch L, con
       P = -1;
     }
   }
-  const GNode nd = s_nd[q];
-  const ColumnDev col = s_col[q];
-  const int kid = s_kid[q];
-  const bool has_pos = tc_has_pos(nd.kind);
   if (P < 0) {
     if (has_pos) T->P[kid][k] = -1;
     return;
@@ -342,10 +365,7 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_kernel(GenLaunch L, con
   const int64_t fixed_end = P + bm + 8LL * nf;
   if (q == 0) {
     if (ROWS) {  // the row's size against its offsets, then the frame header
-      int64_t need = hdr + L.fixed_size;
-      for (int f = 0; f < nf; ++f)
-        if (tc_is_var(s_nd[f].kind)) need += tc_size(T, s_kid[f], s_nd[f], s_col[f], k);
-      if (need > size) set_status(status, FORY_ERR_CAPACITY);  // offsets not from these columns' sizes
+      if (hdr + L.fixed_size + need > size) set_status(status, FORY_ERR_CAPACITY);  // offsets not from these columns
       if (hdr == 12) {  // Encoders.encode(MemoryBuffer, T): [i32 8 + rowSize][i64 hash]
         st32(out + beg, (uint32_t)(size - 4));
         tc_put(out + beg + 4, (uint64_t)L.schema_hash, 8);
@@ -353,29 +373,21 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_kernel(GenLaunch L, con
         tc_put(out + beg, (uint64_t)L.schema_hash, 8);
       }
     }
-    for (int wq = 0; wq < bm / 4; ++wq) {  // setNullAt bits of fields [32 wq, 32 wq + 32)
-      uint32_t word = 0;
-      for (int f = 32 * wq; f < nf && f < 32 * wq + 32; ++f)
-        if ((s_nd[f].flags & 1) && !gvalid(s_col[f].validity, k)) word |= 1u << (f & 31);
-      st32(out + P + 4 * wq, word);
-    }
+#pragma unroll
+    for (int wq = 0; wq < kTcMaxNodes / 32; ++wq)
+      if (wq < bm / 4) st32(out + P + 4 * wq, bw[wq]);
   }
   uint8_t* slot = out + P + bm + 8 * q;
-  if ((nd.flags & 1) && !gvalid(col.validity, k)) {  // null: slot zero
+  if (isnull) {  // BinaryWriter.setNullAt: slot zero
     tc_put(slot, 0, 8);
     if (has_pos) T->P[kid][k] = -1;
     return;
   }
-  if (!tc_is_var(nd.kind)) {
-    uint64_t v = load_elem(col.values, nd.width, k);
-    if (nd.kind == KIND_BOOL) v = v ? 1 : 0;
+  if (!var) {
     tc_put(slot, v, 8);
     return;
   }
-  int64_t at = fixed_end;
-  for (int f = 0; f < q; ++f)
-    if (tc_is_var(s_nd[f].kind)) at += tc_size(T, s_kid[f], s_nd[f], s_col[f], k);
-  const int64_t S = tc_size(T, kid, nd, col, k);
+  const int64_t at = fixed_end + rel;
   if (S < 0 || at + S > cap) {
     set_status(status, FORY_ERR_ENCODER);
     tc_put(slot, 0, 8);
@@ -427,14 +439,42 @@ __device__ __forceinline__ void tc_bitmap(uint8_t* dst, const uint8_t* validity,
   }
 }
 
+// The validity dwords of items [o0, o1) from o0's dword: up to three, those the range
+// reaches (a bitmap of <= 64 items needs no more), loaded with the container's sizes.
+struct TcVwin {
+  uint32_t w[3];
+};
+__device__ __forceinline__ TcVwin tc_vwin(const uint8_t* validity, int64_t o0, int64_t o1) {
+  TcVwin r{{0u, 0u, 0u}};
+  if (!validity) return r;
+  const uint32_t* v = reinterpret_cast<const uint32_t*>(validity) + (o0 >> 5);
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+    if (((o0 >> 5) + t) * 32 < o1) r.w[t] = v[t];
+  return r;
+}
+
 // An array header at Pa: [i64 n][null bitmap][element padding]; returns its fixed bytes.
+// vw: the items' validity window (tc_vwin) when n <= 64.
 __device__ __forceinline__ int64_t tc_array_head(const GenLaunch& L, uint8_t* out, int x, int64_t o0, int64_t n,
-                                                 int64_t Pa) {
+                                                 int64_t Pa, const TcVwin& vw) {
   const GNode it = L.nodes[x];
   const int es = elem_size(it);
   const int64_t hb = 8 + gbm(n), data = n * es, fixed = hb + gr8(data);
   tc_put(out + Pa, (uint64_t)n, 8);
-  tc_bitmap(out + Pa + 8, (it.flags & 1) ? L.cols[x].validity : nullptr, o0, n);
+  if (n > 64) {
+    tc_bitmap(out + Pa + 8, (it.flags & 1) ? L.cols[x].validity : nullptr, o0, n);
+  } else if (n > 0) {  // [8, 16) bytes of bitmap: two words from the window
+    const int sh = (int)(o0 & 31);
+    const uint64_t lo = (uint64_t)vw.w[0] | ((uint64_t)vw.w[1] << 32);
+    const uint32_t b0 = (uint32_t)(lo >> sh);
+    const uint32_t b1 = (uint32_t)((((uint64_t)vw.w[1] | ((uint64_t)vw.w[2] << 32)) >> sh));
+    const bool nul = (it.flags & 1) && L.cols[x].validity;
+    const uint32_t m0 = n >= 32 ? 0xffffffffu : ((1u << n) - 1u);
+    const uint32_t m1 = n <= 32 ? 0u : (n >= 64 ? 0xffffffffu : ((1u << (n - 32)) - 1u));
+    st32(out + Pa + 8, nul ? ~b0 & m0 : 0u);
+    st32(out + Pa + 12, nul ? ~b1 & m1 : 0u);
+  }
   for (int64_t b = data; b < gr8(data); ++b) out[Pa + hb + b] = 0;  // zeroOutPaddingBytes
   return fixed;
 }
@@ -449,20 +489,30 @@ __device__ __forceinline__ int32_t tc_element(const GenLaunch& L, const TcTables
   const int64_t hb = 8 + gbm(n);
   uint8_t* el = out + Pa + hb + q * es;
   const bool var = tc_is_var(it.kind), leaf = tc_leaf(it.kind);
-  if ((it.flags & 1) && !gvalid(col.validity, e)) {  // null: zero element (the header set the bit)
+  // the validity bit, the value or the item's scanned sizes: loaded together, then used
+  const bool isnull = (it.flags & 1) && !gvalid(col.validity, e);
+  uint64_t v = 0;
+  int64_t a0 = 0, a1 = 0, ab = 0;
+  if (!var) {
+    v = load_elem(col.values, es, e);
+  } else {
+    const int64_t* A = T->A[x];
+    a0 = A[e];
+    a1 = A[e + 1];
+    ab = A[o0];
+  }
+  if (isnull) {  // null: zero element (the header set the bit)
     tc_put(el, 0, es);
     if (var && !leaf) T->P[x][e] = -1;
     return 0;
   }
   if (!var) {
-    uint64_t v = load_elem(col.values, es, e);
     if (it.kind == KIND_BOOL) v = v ? 1 : 0;
     tc_put(el, v, es);
     return 0;
   }
-  const int64_t* A = T->A[x];
-  const int64_t S = A[e + 1] - A[e];
-  const int64_t at = Pa + hb + gr8(n * 8) + (A[e] - A[o0]);
+  const int64_t S = a1 - a0;
+  const int64_t at = Pa + hb + gr8(n * 8) + (a0 - ab);
   if (S < 0 || at + S > cap) {
     tc_put(el, 0, 8);
     if (!leaf) T->P[x][e] = -1;
@@ -497,6 +547,9 @@ __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const
     const int64_t n = o1 - o0;
     int64_t P = T->P[c][j];
     int64_t kb = 0;
+    // the items' validity windows, loaded with the array sizes (the bitmaps need them next)
+    const TcVwin vk = tc_vwin((L.nodes[key].flags & 1) ? L.cols[key].validity : nullptr, o0, o1);
+    const TcVwin vv = map ? tc_vwin((L.nodes[val].flags & 1) ? L.cols[val].validity : nullptr, o0, o1) : TcVwin{};
     if (P >= 0) {
       const int64_t need = map ? 8 + tc_array_bytes(L, T, key, o0, o1) + tc_array_bytes(L, T, val, o0, o1)
                                : tc_array_bytes(L, T, key, o0, o1);
@@ -509,10 +562,10 @@ __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const
       if (map) {  // [i64 key array bytes][key array][value array]
         kb = tc_array_bytes(L, T, key, o0, o1);
         tc_put(out + P, (uint64_t)kb, 8);
-        tc_array_head(L, out, key, o0, n, P + 8);
-        tc_array_head(L, out, val, o0, n, P + 8 + kb);
+        tc_array_head(L, out, key, o0, n, P + 8, vk);
+        tc_array_head(L, out, val, o0, n, P + 8 + kb, vv);
       } else {
-        tc_array_head(L, out, key, o0, n, P);
+        tc_array_head(L, out, key, o0, n, P, vk);
       }
     }
     sP[tid] = P;
