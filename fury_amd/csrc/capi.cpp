@@ -776,8 +776,10 @@ int64_t td_partials_words(const fory_plan* plan, const std::vector<int64_t>& m) 
 
 int64_t td_bytes(const fory_plan* plan, const std::vector<int64_t>& m) {
   int64_t b = align_up((int64_t)sizeof(fory_amd::TdTables));
-  for (const fory_amd::TcVar& v : plan->tc.var)
+  for (const fory_amd::TcVar& v : plan->tc.var) {
     if (tc_needs_pos(plan->p, v)) b += align_up((m[v.node] + 1) * 8) + 2 * align_up((m[v.node] + 1) * 4);
+    if (plan->p.nodes[v.node].kind == fory_amd::KIND_BYTES) b += align_up((m[v.node] + 1) * 8);
+  }
   return b + align_up(td_partials_words(plan, m) * 8);
 }
 
@@ -787,17 +789,24 @@ bool td_usable(const fory_plan* plan, const fory_column* out_cols, int64_t n, in
 }
 
 int td_prepare(const fory_plan* plan, const fory_column* out_cols, int64_t n, void* ws, hipStream_t s,
-               const fory_amd::TdTables** dT, std::vector<int64_t>* m, int64_t** partials = nullptr) {
+               const fory_amd::TdTables** dT, std::vector<int64_t>* m, int64_t** partials = nullptr,
+               fory_amd::TdTables* host = nullptr) {
   *m = tc_domains(plan, out_cols, n);
   uint8_t* base = static_cast<uint8_t*>(ws) + fory_rowfmt_workspace_bytes(plan, n);
   fory_amd::TdTables T;
   std::memset(&T, 0, sizeof(T));
   uint8_t* at = base + align_up((int64_t)sizeof(fory_amd::TdTables));
   // by decode level: a level's arrays stay where they are when deeper levels are allocated
+  // (string sources with their level: td_strings copies them in the decode call)
   for (int32_t cd = 0; cd <= plan->p.max_cdepth; ++cd)
     for (const fory_amd::TcVar& v : plan->tc.var) {
-      if (!tc_needs_pos(plan->p, v) || plan->p.gnodes[v.node].cdepth != cd) continue;
+      if (plan->p.gnodes[v.node].cdepth != cd) continue;
       const int64_t k = (*m)[v.node] + 1;
+      if (plan->p.nodes[v.node].kind == fory_amd::KIND_BYTES) {
+        T.SRC[v.node] = reinterpret_cast<int64_t*>(at);
+        at += align_up(k * 8);
+      }
+      if (!tc_needs_pos(plan->p, v)) continue;
       T.P[v.node] = reinterpret_cast<int64_t*>(at);
       at += align_up(k * 8);
       T.SZ[v.node] = reinterpret_cast<int32_t*>(at);
@@ -815,6 +824,7 @@ int td_prepare(const fory_plan* plan, const fory_column* out_cols, int64_t n, vo
     for (int32_t ch : plan->p.nodes[i].children) T.kids[nk++] = ch;
   }
   *dT = reinterpret_cast<const fory_amd::TdTables*>(base);
+  if (host) *host = T;
   return upload(base, &T, (int64_t)sizeof(T), s);
 }
 
@@ -1178,13 +1188,14 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
     if (rc) return rc;
     const bool columnar = td_usable(plan, out_cols, num_rows, workspace_bytes);
     const fory_amd::TdTables* dT = nullptr;
+    fory_amd::TdTables Th{};
     std::vector<int64_t> m;
     int64_t* td_part = nullptr;
     // columnar: the levels run in order, each from the positions the one before left; the
     // levels the previous call on this workspace ran (same plan, rows and columns) are done
     int32_t first = 0, last = -1;
     if (columnar) {
-      rc = td_prepare(plan, out_cols, num_rows, d_workspace, s, &dT, &m, &td_part);
+      rc = td_prepare(plan, out_cols, num_rows, d_workspace, s, &dT, &m, &td_part, &Th);
       if (rc) return rc;
       first = td_recall(plan, d_workspace, d_rows, d_row_offsets, num_rows, frame_mode, out_cols) + 1;
       last = first - 1;
@@ -1202,6 +1213,11 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
       if (level < first) continue;  // counts and positions left by the previous call
       hipError_t e = hipSuccess;
       if (columnar) {  // columnar: this level's passes
+        for (size_t idx = 0; idx < p.nodes.size(); ++idx)  // string sources: -1 until a pass records one
+          if (p.nodes[idx].kind == fory_amd::KIND_BYTES && p.gnodes[idx].cdepth == level && Th.SRC[idx]) {
+            e = hipMemsetAsync(Th.SRC[idx], 0xff, (size_t)(m[idx] + 1) * 8, s);
+            if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+          }
         rc = td_run(plan, G, dT, m, level, d_rows, d_row_offsets, d_status, s);
         if (rc) return rc;
         last = level;
@@ -1280,7 +1296,8 @@ int fory_rowfmt_decode_sizes(const fory_plan* plan, const void* d_rows, const in
 int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows, const int64_t* d_row_offsets,
                        int64_t num_rows, int32_t frame_mode, const fory_column* out_cols,
                        int32_t* d_status, void* d_workspace, int64_t workspace_bytes, void* stream) {
-  int rc = check_common(plan, out_cols, num_rows, frame_mode, d_workspace, workspace_bytes);
+  int rc = check_common(plan, out_cols, num_rows, frame_mode, d_workspace, workspace_bytes, KEEP_TD);
+  if (rc || !plan->p.generic || !td_usable(plan, out_cols, num_rows, workspace_bytes)) td_forget(d_workspace);
   if (rc) return rc;
   if (num_rows == 0) return FORY_OK;
   if (!d_rows) return fail(FORY_ERR_INVALID_ARGUMENT, "d_rows is null");
@@ -1309,11 +1326,32 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows, const int64_t*
     fory_amd::GenLaunch G{};
     rc = prepare_gen(p, out_cols, num_rows, frame_mode, d_workspace, s, &G, 1 << 20);
     if (rc) return rc;
-    if (td_usable(plan, out_cols, num_rows, workspace_bytes)) {  // columnar: every node's values
+    if (td_usable(plan, out_cols, num_rows, workspace_bytes)) {  // columnar
       const fory_amd::TdTables* dT = nullptr;
+      fory_amd::TdTables Th;
       std::vector<int64_t> m;
-      rc = td_prepare(plan, out_cols, num_rows, d_workspace, s, &dT, &m);
-      return rc ? rc : td_run(plan, G, dT, m, -1, d_rows, d_row_offsets, d_status, s);
+      rc = td_prepare(plan, out_cols, num_rows, d_workspace, s, &dT, &m, nullptr, &Th);
+      if (rc) return rc;
+      // decode_sizes on this workspace ran every level with var columns: their passes
+      // wrote all but the string bytes. Run the levels below them (fixed-width items
+      // only), then copy the bytes from the recorded positions. Else every node's values.
+      const int32_t done = td_recall(plan, d_workspace, d_rows, d_row_offsets, num_rows, frame_mode, out_cols);
+      td_forget(d_workspace);
+      bool rest_fixed = done >= 0;
+      for (size_t idx = 0; idx < p.nodes.size() && rest_fixed; ++idx)
+        if (is_var_kind(p.nodes[idx].kind) && p.gnodes[idx].cdepth > done) rest_fixed = false;
+      if (!rest_fixed) return td_run(plan, G, dT, m, -1, d_rows, d_row_offsets, d_status, s);
+      for (int32_t level = done + 1; level <= p.max_cdepth; ++level) {
+        rc = td_run(plan, G, dT, m, level, d_rows, d_row_offsets, d_status, s);
+        if (rc) return rc;
+      }
+      for (size_t idx = 0; idx < p.nodes.size(); ++idx) {
+        if (p.nodes[idx].kind != fory_amd::KIND_BYTES) continue;
+        e = fory_amd::launch_td_strings(static_cast<uint8_t*>(out_cols[idx].values), out_cols[idx].offsets,
+                                        Th.SRC[idx], m[idx], static_cast<const uint8_t*>(d_rows), s);
+        if (e != hipSuccess) return hip_fail(e, "td_strings");
+      }
+      return FORY_OK;
     }
     e = fory_amd::launch_gen_decode(G, static_cast<const uint8_t*>(d_rows), d_row_offsets, d_status, s);
     return e == hipSuccess ? FORY_OK : hip_fail(e, "gen_decode");

@@ -195,6 +195,7 @@ struct TdTables {
   int64_t* P[kTcMaxNodes];
   int32_t* SZ[kTcMaxNodes];
   int32_t* TL[kTcMaxNodes];
+  int64_t* SRC[kTcMaxNodes];  // string / binary nodes: each value's bytes in the rows (-1: null)
   int32_t kids[kTcMaxNodes];  // fields by parent: the rows' top-level fields, then each bean's
   int32_t kid0[kTcMaxNodes];
   int32_t nroot;
@@ -203,6 +204,10 @@ struct TdTables {
 // L.fill_level >= 0: that level's counts, -1: the values.
 hipError_t launch_td_rows(const GenLaunch& L, const TdTables* T, int nroot, const uint8_t* rows, const int64_t* offs,
                           int32_t* status, hipStream_t s);
+// The string / binary bytes of node `node` (m values) from the positions its level's
+// pass recorded (TdTables.SRC) to the Arrow values at its scanned offsets.
+hipError_t launch_td_strings(uint8_t* out_values, int32_t* out_offsets, const int64_t* src, int64_t m,
+                             const uint8_t* rows, hipStream_t s);
 hipError_t launch_td_node(const GenLaunch& L, const TdTables* T, int node, int64_t m, int kind, int nchild,
                           int item_flags, const uint8_t* rows, int32_t* status, hipStream_t s);
 

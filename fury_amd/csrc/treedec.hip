@@ -103,7 +103,7 @@ __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, 
     return;
   }
   if (nd.kind == KIND_DECIMAL) {  // UnsafeTrait.getDecimal: 32 bytes, the high 16 the sign extension
-    if (!values) return;
+    if (!col.out_values || (!values && nd.cdepth != level)) return;
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     if (!isnull) {
       const uint64_t os = sv;
@@ -138,6 +138,7 @@ __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, 
   }
   if (!values) {
     if (nd.cdepth > level) return;
+    if (nd.kind == KIND_BYTES && nd.cdepth == level && T->SRC[f]) T->SRC[f][k] = isnull ? -1 : at;  // for td_strings
     if (nd.cdepth == level && col.out_offsets) {  // this level's counts
       int64_t cnt = 0;
       if (!isnull) {
@@ -209,10 +210,12 @@ __device__ __forceinline__ void td_instance(const GenLaunch& L, const TdTables* 
       const GNode nd = L.nodes[f];
       const ColumnDev col = L.cols[f];
       const bool isnull = !present || ((nulls >> (q & 63)) & 1);  // isNullAt
-      if (values && (nd.flags & 1) && col.out_validity) td_valid_words(col.out_validity, k, inb, !isnull);
+      // values, and every level's own fields (all but string bytes: td_strings copies those)
+      const bool mine = values || nd.cdepth == level;
+      if (mine && (nd.flags & 1) && col.out_validity) td_valid_words(col.out_validity, k, inb, !isnull);
       if (!inb) continue;
       if (is_scalar(nd.kind)) {
-        if (values) td_scalar(nd, col, k, w, isnull);
+        if (mine && col.out_values) td_scalar(nd, col, k, w, isnull);
         continue;
       }
       td_value(L, T, f, nd, col, k, rows, w, present ? base : 0, rend, isnull, level, status);
@@ -285,7 +288,7 @@ __global__ __launch_bounds__(kTdWG) void td_coll_kernel(GenLaunch L, const TdTab
       if (size < 8 || size + 4 != len) present = false;
     }
   }
-  if (level < 0 && (L.nodes[0].flags & 1) && L.cols[0].out_validity)
+  if (level <= 0 && (L.nodes[0].flags & 1) && L.cols[0].out_validity)
     td_valid_words(L.cols[0].out_validity, i, inb, present);
   if (!inb) return;
   if (!present && level <= 0) set_status(status, FORY_ERR_CORRUPT);
@@ -365,7 +368,8 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
       const int64_t arr = inr ? (w ? sV[a] : sK[a]) : -1;
       const bool present = arr >= 0 && q < n;
       const bool isnull = !present || ((rows[arr + 8 + (q >> 3)] >> (q & 7)) & 1);
-      if (level < 0 && (it.flags & 1) && ic.out_validity) td_valid_words(ic.out_validity, e, inr, !isnull);
+      if ((level < 0 || it.cdepth == level) && (it.flags & 1) && ic.out_validity)
+        td_valid_words(ic.out_validity, e, inr, !isnull);
       const int es = elem_size(it);
       const uint64_t sv = isnull ? 0 : gget(rows + arr + 8 + gbm(n) + q * es, es);
       if (FLAT && (it.flags & kGNodeFlatBean)) {  // a bean of leaf fields: read here, no pass of its own
@@ -380,7 +384,7 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
       }
       if (!inr) continue;
       if (is_scalar(it.kind)) {
-        if (level < 0) td_scalar(it, ic, e, sv, isnull);
+        if ((level < 0 || it.cdepth == level) && ic.out_values) td_scalar(it, ic, e, sv, isnull);
         continue;
       }
       if (!present && td_leaf(it.kind)) continue;
@@ -389,7 +393,30 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
   }
 }
 
+// A lane per value: its bytes from the rows to the Arrow values (the sizes pass checked
+// them against the record; a null has no bytes).
+__global__ __launch_bounds__(kTdWG) void td_strings_kernel(ColumnDev col, const int64_t* __restrict__ src, int64_t m,
+                                                           const uint8_t* __restrict__ rows) {
+  const int64_t k = (int64_t)blockIdx.x * kTdWG + threadIdx.x;
+  if (k >= m) return;
+  const int64_t at = src[k];
+  if (at < 0) return;
+  const int64_t o0 = col.out_offsets[k];
+  g_get_bytes(col.out_values + o0, rows + at, (int64_t)col.out_offsets[k + 1] - o0);
+}
+
 }  // namespace
+
+hipError_t launch_td_strings(uint8_t* out_values, int32_t* out_offsets, const int64_t* src, int64_t m,
+                             const uint8_t* rows, hipStream_t s) {
+  if (m <= 0 || !out_values || !out_offsets || !src) return hipSuccess;
+  ColumnDev col{};
+  col.out_values = out_values;
+  col.out_offsets = out_offsets;
+  hipLaunchKernelGGL(td_strings_kernel, dim3((unsigned)((m + kTdWG - 1) / kTdWG)), dim3(kTdWG), 0, s, col, src, m,
+                     rows);
+  return hipGetLastError();
+}
 
 hipError_t launch_td_rows(const GenLaunch& L, const TdTables* T, int nroot, const uint8_t* rows, const int64_t* offs,
                           int32_t* status, hipStream_t s) {
