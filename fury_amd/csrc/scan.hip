@@ -60,14 +60,50 @@ __global__ __launch_bounds__(kWG) void scan_reduce_kernel(void* data, int64_t n,
   __shared__ int64_t smem[kWaves];
   if (MODE == 0) data = reinterpret_cast<int64_t*>(data) + blockIdx.y * dstride;
   partials += blockIdx.y * pstride;
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + threadIdx.x;  // lanes in element order: a sum needs no runs
   int64_t s = 0;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k)
-    if (base + k < n) s += scan_load<MODE>(data, base + k);
+    if (base + k * kWG < n) s += scan_load<MODE>(data, base + k * kWG);
   int64_t tot;
   block_excl_scan(s, smem, &tot);
   if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+}
+
+// A tile's elements through LDS: read and written by lanes in element order (coalesced),
+// scanned by threads as runs of kScanItems consecutive elements (a padded run per thread:
+// no bank is hit by every lane).
+constexpr int kRunPad = kScanItems + 1;
+__device__ __forceinline__ int tile_pos(int e) { return (e / kScanItems) * kRunPad + e % kScanItems; }
+
+// Inclusive (INCL) or exclusive prefix + base of each element of the tile at `base`
+// (n elements from 0), in place in the LDS tile; returns nothing, the tile holds them.
+template <int MODE>
+__device__ __forceinline__ void tile_scan(void* data, int64_t base, int64_t n, int64_t add, int64_t* tile,
+                                          int64_t* smem) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const int e = k * kWG + tid;
+    tile[tile_pos(e)] = base + e < n ? scan_load<MODE>(data, base + e) : 0;
+  }
+  __syncthreads();
+  int64_t v[kScanItems];
+  int64_t x = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    v[k] = tile[tid * kRunPad + k];
+    x += v[k];
+  }
+  int64_t tot;
+  int64_t pre = block_excl_scan(x, smem, &tot) + add;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    if (MODE == 1) pre += v[k];  // Arrow offsets: inclusive
+    tile[tid * kRunPad + k] = pre;
+    if (MODE == 0) pre += v[k];
+  }
+  __syncthreads();
 }
 
 // Single workgroup: exclusive scan of the partials in place (any count).
@@ -106,32 +142,27 @@ template <int MODE, bool SEG = false>
 __global__ __launch_bounds__(kWG) void scan_down_kernel(void* data, int64_t n, const int64_t* partials,
                                                         int32_t* status, int64_t dstride = 0, int64_t pstride = 0) {
   __shared__ int64_t smem[kWaves];
+  __shared__ int64_t tile[kWG * kRunPad];
   if (MODE == 0) data = reinterpret_cast<int64_t*>(data) + blockIdx.y * dstride;
   partials += blockIdx.y * pstride;
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-  int64_t v[kScanItems];
-  int64_t s = 0;
+  const int64_t base = (int64_t)blockIdx.x * kScanTile;
+  int64_t add = partials[blockIdx.x];
+  if (SEG) add += reinterpret_cast<const int32_t*>(data)[0];
+  tile_scan<MODE>(data, base, n, add, tile, smem);
+  bool over = false;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
-    v[k] = base + k < n ? scan_load<MODE>(data, base + k) : 0;
-    s += v[k];
-  }
-  int64_t tot;
-  int64_t pre = block_excl_scan(s, smem, &tot) + partials[blockIdx.x];
-  if (SEG) pre += reinterpret_cast<const int32_t*>(data)[0];
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    if (base + k < n) {
-      if (MODE == 0) {
-        reinterpret_cast<int64_t*>(data)[base + k] = pre;
-        pre += v[k];
-      } else {
-        pre += v[k];
-        if (pre > 0x7fffffffLL) set_status(status, FORY_ERR_CAPACITY);
-        reinterpret_cast<int32_t*>(data)[base + k + 1] = (int32_t)pre;
-      }
+    const int e = k * kWG + threadIdx.x;
+    if (base + e >= n) continue;
+    const int64_t pre = tile[tile_pos(e)];
+    if (MODE == 0) {
+      reinterpret_cast<int64_t*>(data)[base + e] = pre;
+    } else {
+      over = over || pre > 0x7fffffffLL;
+      reinterpret_cast<int32_t*>(data)[base + e + 1] = (int32_t)pre;
     }
   }
+  if (over) set_status(status, FORY_ERR_CAPACITY);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (MODE == 0) reinterpret_cast<int64_t*>(data)[n] = partials[gridDim.x];
     else if (!SEG) reinterpret_cast<int32_t*>(data)[0] = 0;
@@ -143,12 +174,12 @@ __global__ __launch_bounds__(kWG) void scan_down_kernel(void* data, int64_t n, c
 __global__ __launch_bounds__(kWG) void scan_reduce_batch_kernel(OffsScanBatch B, int64_t* partials) {
   __shared__ int64_t smem[kWaves];
   const OffsScanSeg g = B.seg[blockIdx.y];
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + threadIdx.x;
   if ((int64_t)blockIdx.x * kScanTile >= g.n) return;  // (uniform per workgroup)
   int64_t x = 0;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k)
-    if (base + k < g.n) x += g.offs[base + k + 1];
+    if (base + k * kWG < g.n) x += g.offs[base + k * kWG + 1];
   int64_t tot;
   block_excl_scan(x, smem, &tot);
   if (threadIdx.x == 0) partials[g.pofs + blockIdx.x] = tot;
@@ -162,26 +193,21 @@ __global__ __launch_bounds__(kWG) void scan_partials_batch_kernel(OffsScanBatch 
 __global__ __launch_bounds__(kWG) void scan_down_batch_kernel(OffsScanBatch B, const int64_t* partials,
                                                               int32_t* status) {
   __shared__ int64_t smem[kWaves];
+  __shared__ int64_t tile[kWG * kRunPad];
   const OffsScanSeg g = B.seg[blockIdx.y];
   if ((int64_t)blockIdx.x * kScanTile >= g.n) return;
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-  int64_t v[kScanItems];
-  int64_t x = 0;
+  const int64_t base = (int64_t)blockIdx.x * kScanTile;
+  tile_scan<1>(g.offs, base, g.n, partials[g.pofs + blockIdx.x], tile, smem);
+  bool over = false;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
-    v[k] = base + k < g.n ? g.offs[base + k + 1] : 0;
-    x += v[k];
+    const int e = k * kWG + threadIdx.x;
+    if (base + e >= g.n) continue;
+    const int64_t pre = tile[tile_pos(e)];
+    over = over || pre > 0x7fffffffLL;
+    g.offs[base + e + 1] = (int32_t)pre;
   }
-  int64_t tot;
-  int64_t pre = block_excl_scan(x, smem, &tot) + partials[g.pofs + blockIdx.x];
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    if (base + k < g.n) {
-      pre += v[k];
-      if (pre > 0x7fffffffLL) set_status(status, FORY_ERR_CAPACITY);
-      g.offs[base + k + 1] = (int32_t)pre;
-    }
-  }
+  if (over) set_status(status, FORY_ERR_CAPACITY);
   if (blockIdx.x == 0 && threadIdx.x == 0) g.offs[0] = 0;
 }
 

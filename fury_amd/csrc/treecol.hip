@@ -156,11 +156,11 @@ __global__ __launch_bounds__(kTcWG) void tc_size_sums_kernel(GenLaunch L, const 
                                                              int64_t m, int root_coll, int64_t* __restrict__ out,
                                                              int64_t* __restrict__ part) {
   __shared__ int64_t s_wave[kTcWG / 64];
-  const int64_t j0 = (int64_t)blockIdx.x * kTcScanTile + (int64_t)threadIdx.x * kTcScanPer;
+  const int64_t j0 = (int64_t)blockIdx.x * kTcScanTile + threadIdx.x;  // lanes in instance order (coalesced)
   int64_t sum = 0;
 #pragma unroll
   for (int u = 0; u < kTcScanPer; ++u) {
-    const int64_t j = j0 + u;
+    const int64_t j = j0 + u * kTcWG;
     if (j < m) {
       const int64_t v = c >= 0 ? tc_node_size(L, T, c, j, root_coll) : tc_row_size(L, T, j);
       out[j] = v;
@@ -189,24 +189,37 @@ __global__ __launch_bounds__(kTcWG) void tc_part_scan_kernel(int64_t* __restrict
 __global__ __launch_bounds__(kTcWG) void tc_scan_down_kernel(int64_t* __restrict__ out, int64_t m,
                                                              const int64_t* __restrict__ part) {
   __shared__ int64_t s_wave[kTcWG / 64];
-  const int64_t j0 = (int64_t)blockIdx.x * kTcScanTile + (int64_t)threadIdx.x * kTcScanPer;
+  __shared__ int64_t tile[kTcWG * (kTcScanPer + 1)];  // runs of kTcScanPer, padded: lanes read / write in order
+  const int tid = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * kTcScanTile;
+  auto pos = [](int e) { return (e / kTcScanPer) * (kTcScanPer + 1) + e % kTcScanPer; };
+#pragma unroll
+  for (int u = 0; u < kTcScanPer; ++u) {
+    const int e = u * kTcWG + tid;
+    tile[pos(e)] = b0 + e < m ? out[b0 + e] : 0;
+  }
+  __syncthreads();
   int64_t v[kTcScanPer];
   int64_t sum = 0;
 #pragma unroll
   for (int u = 0; u < kTcScanPer; ++u) {
-    const int64_t j = j0 + u;
-    v[u] = j < m ? out[j] : 0;
+    v[u] = tile[tid * (kTcScanPer + 1) + u];
     sum += v[u];
   }
   int64_t tot;
   int64_t at = part[blockIdx.x] + tc_block_excl(sum, s_wave, &tot);
 #pragma unroll
   for (int u = 0; u < kTcScanPer; ++u) {
-    const int64_t j = j0 + u;
-    if (j < m) out[j] = at;
+    tile[tid * (kTcScanPer + 1) + u] = at;
     at += v[u];
   }
-  if (j0 <= m - 1 && m - 1 < j0 + kTcScanPer) out[m] = at;  // the lane holding the last value
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kTcScanPer; ++u) {
+    const int e = u * kTcWG + tid;
+    if (b0 + e < m) out[b0 + e] = tile[pos(e)];
+  }
+  if (blockIdx.x == gridDim.x - 1 && tid == 0) out[m] = part[gridDim.x];  // the total
 }
 
 __global__ __launch_bounds__(kTcWG) void tc_rows_kernel(GenLaunch L, const TcTables* __restrict__ T,

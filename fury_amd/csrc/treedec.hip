@@ -393,16 +393,60 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
   }
 }
 
-// A lane per value: its bytes from the rows to the Arrow values (the sizes pass checked
-// them against the record; a null has no bytes).
+// String / binary bytes of a column, a workgroup per kTdWG values: lanes take the
+// dwords of the values' contiguous Arrow byte range in order (coalesced stores), each
+// finding its value by binary search over the workgroup's offsets in LDS and reading its
+// bytes where the value's pass recorded them (aligned dwords, funnel-shifted; a string's
+// bytes are padded to 8 in the row, so the dwords read stay inside it). Dwords that
+// straddle two values go byte by byte; those shared with a neighbour workgroup store
+// only their own bytes.
 __global__ __launch_bounds__(kTdWG) void td_strings_kernel(ColumnDev col, const int64_t* __restrict__ src, int64_t m,
                                                            const uint8_t* __restrict__ rows) {
-  const int64_t k = (int64_t)blockIdx.x * kTdWG + threadIdx.x;
-  if (k >= m) return;
-  const int64_t at = src[k];
-  if (at < 0) return;
-  const int64_t o0 = col.out_offsets[k];
-  g_get_bytes(col.out_values + o0, rows + at, (int64_t)col.out_offsets[k + 1] - o0);
+  __shared__ int32_t sO[kTdWG + 1];
+  __shared__ int64_t sS[kTdWG];
+  const int tid = threadIdx.x;
+  const int64_t k0 = (int64_t)blockIdx.x * kTdWG;
+  const int cnt = m - k0 < kTdWG ? (int)(m - k0) : kTdWG;
+  if (tid < cnt) {
+    sO[tid] = col.out_offsets[k0 + tid];
+    sS[tid] = src[k0 + tid];
+    if (tid == cnt - 1) sO[cnt] = col.out_offsets[k0 + cnt];
+  }
+  __syncthreads();
+  const int64_t b0 = sO[0], b1 = sO[cnt];
+  auto owner = [&](int64_t p) {  // the value whose bytes hold output byte p (b0 <= p < b1)
+    int lo = 0, hi = cnt - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (sO[mid] <= p) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
+  };
+  uint8_t* out = col.out_values;
+  const bool al = !(reinterpret_cast<uintptr_t>(out) & 3);  // (else every byte alone)
+  for (int64_t d = (b0 & ~int64_t(3)) + 4 * tid; d < b1; d += 4 * kTdWG) {
+    const int64_t p0 = d < b0 ? b0 : d, p1 = d + 4 < b1 ? d + 4 : b1;
+    int a = owner(p0);
+    if (al && d >= b0 && d + 4 <= b1 && sO[a + 1] >= d + 4) {  // one value's four bytes
+      const int64_t s0 = sS[a] + (d - sO[a]);
+      const int ph = (int)(s0 & 3);
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(rows + (s0 - ph));
+      uint32_t v = w[0];
+      if (ph) v = (uint32_t)((((uint64_t)w[1] << 32) | v) >> (8 * ph));  // (w[1] only when needed)
+      st32(out + d, v);
+      continue;
+    }
+    uint32_t word = 0;
+    for (int64_t q = p0; q < p1; ++q) {
+      while (sO[a + 1] <= q) ++a;
+      const uint8_t v = rows[sS[a] + (q - sO[a])];
+      word |= (uint32_t)v << (8 * (q - d));
+    }
+    if (al && p0 == d && p1 == d + 4) st32(out + d, word);
+    else
+      for (int64_t q = p0; q < p1; ++q) out[q] = (uint8_t)(word >> (8 * (q - d)));
+  }
 }
 
 }  // namespace
