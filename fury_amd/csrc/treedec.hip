@@ -393,27 +393,62 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
   }
 }
 
-// String / binary bytes of a column, a workgroup per kTdWG values: lanes take the
-// dwords of the values' contiguous Arrow byte range in order (coalesced stores), each
-// finding its value by binary search over the workgroup's offsets in LDS and reading its
-// bytes where the value's pass recorded them (aligned dwords, funnel-shifted; a string's
-// bytes are padded to 8 in the row, so the dwords read stay inside it). Dwords that
-// straddle two values go byte by byte; those shared with a neighbour workgroup store
-// only their own bytes.
+// String / binary bytes of a column, a workgroup per kTdWG values. The values' Arrow
+// bytes are one contiguous range: when it fits kTdStage, each lane reads its value's
+// bytes (aligned dwords, all issued before any is used: a string's bytes start 4-aligned
+// in the row and are padded to 8 there) into an LDS image of the range, and the
+// workgroup stores the image with coalesced dword stores (edge dwords shared with a
+// neighbour take only their own bytes). A larger range goes dword by dword, each lane
+// finding its value by binary search over the offsets.
+constexpr int kTdStage = 8192;
+
 __global__ __launch_bounds__(kTdWG) void td_strings_kernel(ColumnDev col, const int64_t* __restrict__ src, int64_t m,
                                                            const uint8_t* __restrict__ rows) {
   __shared__ int32_t sO[kTdWG + 1];
   __shared__ int64_t sS[kTdWG];
+  __shared__ uint32_t stage[kTdStage / 4];
   const int tid = threadIdx.x;
   const int64_t k0 = (int64_t)blockIdx.x * kTdWG;
   const int cnt = m - k0 < kTdWG ? (int)(m - k0) : kTdWG;
+  int64_t my_o0 = 0, my_o1 = 0, my_s = -1;
   if (tid < cnt) {
-    sO[tid] = col.out_offsets[k0 + tid];
-    sS[tid] = src[k0 + tid];
-    if (tid == cnt - 1) sO[cnt] = col.out_offsets[k0 + cnt];
+    my_o0 = col.out_offsets[k0 + tid];
+    my_o1 = col.out_offsets[k0 + tid + 1];
+    my_s = src[k0 + tid];
+    sO[tid] = (int32_t)my_o0;
+    sS[tid] = my_s;
+    if (tid == cnt - 1) sO[cnt] = (int32_t)my_o1;
   }
   __syncthreads();
   const int64_t b0 = sO[0], b1 = sO[cnt];
+  const int64_t base = b0 & ~int64_t(3);
+  uint8_t* out = col.out_values;
+  const bool al = !(reinterpret_cast<uintptr_t>(out) & 3);  // (else every byte alone)
+  if (al && b1 - base <= kTdStage) {
+    uint8_t* st = reinterpret_cast<uint8_t*>(stage);
+    if (my_s >= 0) {
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(rows + my_s);
+      const int64_t len = my_o1 - my_o0;
+      for (int64_t j = 0; j < len; j += 16) {
+        uint32_t x[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) x[t] = j + 4 * t < len ? w[(j >> 2) + t] : 0u;
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+          if (j + t < len) st[my_o0 - base + j + t] = (uint8_t)(x[t >> 2] >> (8 * (t & 3)));
+      }
+    }
+    __syncthreads();
+    for (int64_t d = base + 4 * tid; d < b1; d += 4 * kTdWG) {
+      if (d >= b0 && d + 4 <= b1) {
+        st32(out + d, stage[(d - base) >> 2]);
+      } else {
+        const uint32_t v = stage[(d - base) >> 2];
+        for (int64_t q = d < b0 ? b0 : d; q < d + 4 && q < b1; ++q) out[q] = (uint8_t)(v >> (8 * (q - d)));
+      }
+    }
+    return;
+  }
   auto owner = [&](int64_t p) {  // the value whose bytes hold output byte p (b0 <= p < b1)
     int lo = 0, hi = cnt - 1;
     while (lo < hi) {
@@ -423,9 +458,7 @@ __global__ __launch_bounds__(kTdWG) void td_strings_kernel(ColumnDev col, const 
     }
     return lo;
   };
-  uint8_t* out = col.out_values;
-  const bool al = !(reinterpret_cast<uintptr_t>(out) & 3);  // (else every byte alone)
-  for (int64_t d = (b0 & ~int64_t(3)) + 4 * tid; d < b1; d += 4 * kTdWG) {
+  for (int64_t d = base + 4 * tid; d < b1; d += 4 * kTdWG) {
     const int64_t p0 = d < b0 ? b0 : d, p1 = d + 4 < b1 ? d + 4 : b1;
     int a = owner(p0);
     if (al && d >= b0 && d + 4 <= b1 && sO[a + 1] >= d + 4) {  // one value's four bytes
