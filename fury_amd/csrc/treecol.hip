@@ -322,35 +322,64 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_kernel(GenLaunch L, con
     s_col[q] = L.cols[kid];
   }
   __syncthreads();
+  // An instance's fields are a group of NP = pow2(nf) <= 64 adjacent lanes inside one
+  // wave: the bytes of the var fields before a field are a prefix sum over the group and
+  // the null bitmap a ballot of it (one size load per lane). Wider beans: NP = nf, each
+  // lane sums its predecessors' sizes itself.
+  int lg = 0;
+  while ((1 << lg) < nf) ++lg;
+  const bool grp = lg <= 6;
+  const int np = grp ? 1 << lg : nf;
   const uint64_t w = (uint64_t)blockIdx.x * kTcWG + tid;
-  if (w >= (uint64_t)m * (uint64_t)nf) return;
-  const int64_t k = (int64_t)(w / (uint64_t)nf);
-  const int q = (int)(w - (uint64_t)k * (uint64_t)nf);
-  const GNode nd = s_nd[q];
-  const ColumnDev col = s_col[q];
-  const int kid = s_kid[q];
+  if (!grp && w >= (uint64_t)m * (uint64_t)nf) return;
+  const int64_t k = grp ? (int64_t)(w >> lg) : (int64_t)(w / (uint64_t)nf);
+  const int q = grp ? (int)(w & (uint64_t)(np - 1)) : (int)(w - (uint64_t)k * (uint64_t)nf);
+  const bool live = k < m && q < nf;  // (grouped lanes past the fields / instances only shuffle)
+  const int qq = live ? q : 0;
+  const GNode nd = s_nd[qq];
+  const ColumnDev col = s_col[qq];
+  const int kid = s_kid[qq];
+  const int64_t kk = live ? k : 0;
   const bool has_pos = tc_has_pos(nd.kind), var = tc_is_var(nd.kind);
   // Everything that does not depend on the instance's position is loaded first, so the
   // lane waits one memory latency for all of it (the position is one more load):
-  // null bit, value or (bytes of the var fields before this one, this one's bytes), and
-  // lane 0's bitmap words (and, for rows, the row's var bytes to check its size).
-  const bool isnull = (nd.flags & 1) && !gvalid(col.validity, k);
+  // null bit, value or this var field's bytes (and the group's prefix of them), and the
+  // bitmap words (and, for rows, the row's var bytes to check its size).
+  const bool isnull = live && (nd.flags & 1) && !gvalid(col.validity, kk);
   uint64_t v = 0;
   int64_t rel = 0, S = 0;
   if (!var) {
-    v = load_elem(col.values, nd.width, k);
+    v = load_elem(col.values, nd.width, kk);
     if (nd.kind == KIND_BOOL) v = v ? 1 : 0;
   } else {
-    for (int f = 0; f < q; ++f)
-      if (tc_is_var(s_nd[f].kind)) rel += tc_size(T, s_kid[f], s_nd[f], s_col[f], k);
-    S = tc_size(T, kid, nd, col, k);
+    S = tc_size(T, kid, nd, col, kk);
   }
   uint32_t bw[kTcMaxNodes / 32] = {0u, 0u, 0u, 0u};  // lane q = 0: setNullAt bits of every field
   int64_t need = 0;
-  if (q == 0) {
-    for (int f = 0; f < nf; ++f) {
-      if ((s_nd[f].flags & 1) && !gvalid(s_col[f].validity, k)) bw[f >> 5] |= 1u << (f & 31);
-      if (ROWS && tc_is_var(s_nd[f].kind)) need += tc_size(T, s_kid[f], s_nd[f], s_col[f], k);
+  if (grp) {
+    const int64_t mine = live && var ? S : 0;
+    int64_t x = mine;
+    for (int d = 1; d < np; d <<= 1) {
+      const int64_t y = __shfl_up(x, d, np);
+      if (q >= d) x += y;
+    }
+    rel = x - mine;
+    need = __shfl(x, np - 1, np);
+    const uint64_t nb = __ballot(isnull);
+    const int g0 = (threadIdx.x & 63) & ~(np - 1);  // the group's first lane in the wave
+    const uint64_t bits = np == 64 ? nb : (nb >> g0) & ((1ull << np) - 1);
+    bw[0] = (uint32_t)bits;
+    bw[1] = (uint32_t)(bits >> 32);
+    if (!live) return;
+  } else {
+    if (var)
+      for (int f = 0; f < q; ++f)
+        if (tc_is_var(s_nd[f].kind)) rel += tc_size(T, s_kid[f], s_nd[f], s_col[f], k);
+    if (q == 0) {
+      for (int f = 0; f < nf; ++f) {
+        if ((s_nd[f].flags & 1) && !gvalid(s_col[f].validity, k)) bw[f >> 5] |= 1u << (f & 31);
+        if (ROWS && tc_is_var(s_nd[f].kind)) need += tc_size(T, s_kid[f], s_nd[f], s_col[f], k);
+      }
     }
   }
   int64_t P;
@@ -627,6 +656,14 @@ __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const
   if (err) set_status(status, err);
 }
 
+// Lanes per instance of tc_write_fields_kernel: the fields rounded up to a power of two
+// (<= 64, a group inside one wave), or the fields themselves beyond 64.
+int64_t tc_group_lanes(int nf) {
+  int np = 1;
+  while (np < nf) np <<= 1;
+  return np <= 64 ? np : nf;
+}
+
 }  // namespace
 
 hipError_t launch_tc_sizes(const GenLaunch& L, const TcTables* T, int node, int64_t m, bool root_coll,
@@ -666,7 +703,7 @@ hipError_t launch_tc_write_rows(const GenLaunch& L, const TcTables* T, int nroot
                        L, T, offs, out, capacity, status);
     return hipGetLastError();
   }
-  const int64_t work = L.num_rows * nroot;
+  const int64_t work = L.num_rows * tc_group_lanes(nroot);
   hipLaunchKernelGGL(tc_write_fields_kernel<true>, dim3((unsigned)((work + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s,
                      L, T, -1, L.num_rows, offs, out, capacity, status);
   return hipGetLastError();
@@ -680,7 +717,7 @@ hipError_t launch_tc_write_node(const GenLaunch& L, const TcTables* T, int node,
                        dim3((unsigned)((m + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s, L, T, node, m, out, capacity,
                        status);
   } else {
-    const int64_t work = m * (nchild > 0 ? nchild : 1);
+    const int64_t work = m * tc_group_lanes(nchild > 0 ? nchild : 1);
     hipLaunchKernelGGL(tc_write_fields_kernel<false>, dim3((unsigned)((work + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0,
                        s, L, T, node, m, nullptr, out, capacity, status);
   }
