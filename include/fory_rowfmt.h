@@ -251,6 +251,13 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols,
  * shapes, a tree engine for list<list<...>>, List<Bean> with var fields,
  * Map<K, Bean> and the like).
  *
+ * The columnar tree engine (a workspace of fory_rowfmt_decode_workspace_bytes) may also
+ * write the values and validity of the levels a decode_sizes call sizes (all but string /
+ * binary bytes); pass the same columns to the later calls. On one workspace, a
+ * decode_sizes call resumes after the levels the previous one ran for the same plan,
+ * rows, offsets and columns, and decode then only copies the string bytes; any other
+ * call on the workspace drops that (the result is the same either way).
+ *
  * fory_rowfmt_decode: writes values/offsets/validity of out_cols. Null
  * values decode to 0 (RowEncoderBuilder.java:239-246 leaves the Java default).
  * In STREAM mode every frame's int32 size and int64 schema hash are checked
