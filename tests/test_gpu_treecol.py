@@ -214,3 +214,28 @@ def test_decode_levels_resume_from_the_previous_call(name):
 
     enc.workspace = interleaved
     assert columns_equal(schema, cols, to_host(enc.decode(rows))) == []
+
+
+@pytest.mark.parametrize("frame", [0, 1])
+def test_long_strings_decode_both_copy_paths(frame):
+    """String columns whose 256-value workgroups span more than the LDS image (values of
+    100-300 bytes: the dword-by-dword copy) next to short ones (the staged copy), with
+    nulls and empty strings; encode bytes and the decoded columns equal the oracle's."""
+    from helpers import columns_equal
+    from fury_amd.format.columns import to_host
+    schema = I.infer_schema(type("LongStrings", (), {"__annotations__": {
+        "id": I.jint, "long": List[List[I.String]], "short": List[I.String], "tag": I.String}}))  # (list<list<>>: the tree engine)
+    rng = np.random.default_rng(7)
+    rows = []
+    for i in range(1500):
+        rows.append({"id": i,
+                     "long": [[None if rng.random() < 0.1 else "x" * int(rng.integers(100, 300))
+                               for _ in range(int(rng.integers(0, 4)))] for _ in range(int(rng.integers(0, 3)))],
+                     "short": ["" if rng.random() < 0.2 else "s%d" % int(rng.integers(0, 999))
+                               for _ in range(int(rng.integers(0, 9)))],
+                     "tag": None if i % 7 == 0 else "t" * (i % 300)})
+    cols = build_columns(schema, rows)
+    enc = RowEncoder(schema)
+    encoded = enc.encode(to_device(cols), len(rows), frame)
+    oracle_equal(schema, cols, len(rows), frame, encoded)
+    assert columns_equal(schema, cols, to_host(enc.decode(encoded))) == []
