@@ -445,6 +445,151 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_kernel(GenLaunch L, con
   }
 }
 
+// Rows and beans, a lane per instance (the column loads of a wave are consecutive
+// elements), fields in batches of kTcBatch whose loads are issued together: each lane
+// builds its instance's frame header, null bitmap and slots in an LDS image (FS bytes
+// per lane), hands its bean / list / map fields their positions (consecutive per wave)
+// and writes its strings / decimals in place; then each wave stores its 64 images as
+// consecutive dwords of each instance (coalesced). Same bytes as tc_write_fields_kernel,
+// which stays for images beyond kTcStageMax.
+constexpr int kTcBatch = 4;
+constexpr int kTcStageMax = 280;  // frame header + bitmap + slots of up to 32 fields
+
+template <bool ROWS>
+__global__ __launch_bounds__(kTcWG) void tc_write_fields_lds_kernel(GenLaunch L, const TcTables* __restrict__ T,
+                                                                    int c, int64_t m,
+                                                                    const int64_t* __restrict__ offs,
+                                                                    uint8_t* __restrict__ out, int64_t cap,
+                                                                    int32_t* status, int FS) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t tc_stage[];
+  __shared__ GNode s_nd[kTcMaxNodes];
+  __shared__ ColumnDev s_col[kTcMaxNodes];
+  __shared__ int32_t s_kid[kTcMaxNodes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int nf = ROWS ? T->nroot : L.nodes[c].nchild;
+  const int bm = ROWS ? L.bitmap_bytes : gbm(nf);
+  const int k0 = ROWS ? 0 : T->kid0[c];
+  for (int q = tid; q < nf; q += kTcWG) {
+    const int kid = T->kids[k0 + q];
+    s_kid[q] = kid;
+    s_nd[q] = L.nodes[kid];
+    s_col[q] = L.cols[kid];
+  }
+  __syncthreads();
+  const int64_t k = (int64_t)blockIdx.x * kTcWG + tid;
+  const bool inb = k < m;
+  const int64_t kk = inb ? k : 0;
+  const int hdr = ROWS ? frame_header_bytes(L.frame) : 0;
+  uint8_t* img = tc_stage + (size_t)tid * FS;  // [frame header][bitmap][slots]
+  int64_t P = -1, beg = 0, size = 0;
+  if (inb) {
+    if (ROWS) {
+      beg = offs[k];
+      const int64_t end = offs[k + 1];
+      size = end - beg;
+      const bool bad = beg < 0 || end > cap || size < hdr + L.fixed_size || size - hdr > 0x7fffffffLL || (beg & 3);
+      if (bad) set_status(status, FORY_ERR_CAPACITY);
+      else P = beg + hdr;
+    } else {
+      P = T->P[c][k];
+      if (P >= 0 && P + bm + 8LL * nf > cap) {
+        set_status(status, FORY_ERR_ENCODER);
+        P = -1;
+      }
+    }
+  }
+  const int64_t fixed_end = P + bm + 8LL * nf;
+  int64_t rel = 0;  // bytes of the var fields so far
+  for (int w = 0; w < bm / 4; ++w) st32(img + hdr + 4 * w, 0u);
+  for (int q0 = 0; q0 < nf; q0 += kTcBatch) {
+    bool nul[kTcBatch];
+    uint64_t v[kTcBatch];
+    int64_t S[kTcBatch];
+#pragma unroll
+    for (int u = 0; u < kTcBatch; ++u) {  // the batch's loads, issued together
+      const int q = q0 + u < nf ? q0 + u : nf - 1;
+      const GNode nd = s_nd[q];
+      const ColumnDev col = s_col[q];
+      nul[u] = (nd.flags & 1) && !gvalid(col.validity, kk);
+      v[u] = 0;
+      S[u] = 0;
+      if (!tc_is_var(nd.kind)) v[u] = load_elem(col.values, nd.width, kk);
+      else S[u] = tc_size(T, s_kid[q], nd, col, kk);
+    }
+#pragma unroll 1
+    for (int u = 0; u < kTcBatch; ++u) {  // rolled: one copy of the field body
+      const int q = q0 + u;
+      if (q >= nf) break;
+      bool nu = nul[0];
+      uint64_t vu = v[0];
+      int64_t Su = S[0];
+#pragma unroll
+      for (int t = 1; t < kTcBatch; ++t) {
+        nu = u == t ? nul[t] : nu;
+        vu = u == t ? v[t] : vu;
+        Su = u == t ? S[t] : Su;
+      }
+      const GNode nd = s_nd[q];
+      const int kid = s_kid[q];
+      const bool has_pos = tc_has_pos(nd.kind);
+      uint8_t* slot = img + hdr + bm + 8 * q;
+      if (P < 0 || nu) {  // BinaryWriter.setNullAt: bit set, slot zero (absent: no position)
+        if (nu) img[hdr + (q >> 3)] |= (uint8_t)(1u << (q & 7));
+        st32(slot, 0u);
+        st32(slot + 4, 0u);
+        if (inb && has_pos) T->P[kid][k] = -1;
+        continue;
+      }
+      if (!tc_is_var(nd.kind)) {
+        const uint64_t x = nd.kind == KIND_BOOL ? (vu ? 1 : 0) : vu;
+        st32(slot, (uint32_t)x);
+        st32(slot + 4, (uint32_t)(x >> 32));
+        continue;
+      }
+      const int64_t at = fixed_end + rel;
+      if (Su < 0 || at + Su > cap) {
+        set_status(status, FORY_ERR_ENCODER);
+        st32(slot, 0u);
+        st32(slot + 4, 0u);
+        if (has_pos) T->P[kid][k] = -1;
+        continue;
+      }
+      const uint64_t sw = ((uint64_t)(at - P) << 32) | tc_slot_size(nd, s_col[q], kk, Su);
+      st32(slot, (uint32_t)sw);
+      st32(slot + 4, (uint32_t)(sw >> 32));
+      rel += Su;
+      if (has_pos) {
+        T->P[kid][k] = at;
+      } else {
+        const int32_t r = tc_leaf_write(out, nd, s_col[q], kk, at);
+        if (r) set_status(status, r);
+      }
+    }
+  }
+  if (ROWS && P >= 0) {  // the row's size against its offsets, then the frame header
+    if (hdr + L.fixed_size + rel > size) set_status(status, FORY_ERR_CAPACITY);  // offsets not from these columns
+    if (hdr == 12) {  // Encoders.encode(MemoryBuffer, T): [i32 8 + rowSize][i64 hash]
+      st32(img, (uint32_t)(size - 4));
+      st32(img + 4, (uint32_t)(uint64_t)L.schema_hash);
+      st32(img + 8, (uint32_t)((uint64_t)L.schema_hash >> 32));
+    } else if (hdr == 8) {  // Encoder.encode(T): [i64 hash]
+      st32(img, (uint32_t)(uint64_t)L.schema_hash);
+      st32(img + 4, (uint32_t)((uint64_t)L.schema_hash >> 32));
+    }
+  }
+  // this wave's images out: consecutive dwords of each instance (its start: P - hdr)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int nd4 = (hdr + bm + 8 * nf) >> 2;  // dwords per image
+  const uint8_t* wimg = tc_stage + (size_t)(tid - lane) * FS;
+  for (int t = lane; t < 64 * nd4; t += 64) {  // (every lane the same trip count: shuffles are uniform)
+    const int r = t / nd4, j = t - r * nd4;
+    const int64_t pr = __shfl(P, r);
+    if (pr >= 0) st32(out + pr - hdr + 4 * j, ld32(wimg + (size_t)r * FS + 4 * j));
+  }
+}
+
 // Collection frames: [i32 size] and the collection's position.
 __global__ __launch_bounds__(kTcWG) void tc_write_coll_kernel(GenLaunch L, const TcTables* __restrict__ T,
                                                               const int64_t* __restrict__ offs,
@@ -579,7 +724,7 @@ __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const
   const int64_t j0 = (int64_t)blockIdx.x * kTcWG;
   const int cnt = m - j0 < kTcWG ? (int)(m - j0) : kTcWG;
   constexpr bool map = MAP;
-  const int key = c + 1, val = map ? L.nodes[key].end : -1;
+  const int key = c + 1, val = map ? L.nodes[key].end : key;  // (val: maps only)
   const int64_t mx = T->m[key];
   int32_t err = 0;
   if (tid < cnt) {
@@ -703,6 +848,13 @@ hipError_t launch_tc_write_rows(const GenLaunch& L, const TcTables* T, int nroot
                        L, T, offs, out, capacity, status);
     return hipGetLastError();
   }
+  const int fs = frame_header_bytes(L.frame) + L.bitmap_bytes + 8 * nroot;
+  if (fs <= kTcStageMax) {
+    raise_lds_cap(&tc_write_fields_lds_kernel<true>);
+    hipLaunchKernelGGL(tc_write_fields_lds_kernel<true>, dim3((unsigned)((L.num_rows + kTcWG - 1) / kTcWG)),
+                       dim3(kTcWG), (size_t)kTcWG * fs, s, L, T, -1, L.num_rows, offs, out, capacity, status, fs);
+    return hipGetLastError();
+  }
   const int64_t work = L.num_rows * tc_group_lanes(nroot);
   hipLaunchKernelGGL(tc_write_fields_kernel<true>, dim3((unsigned)((work + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s,
                      L, T, -1, L.num_rows, offs, out, capacity, status);
@@ -717,6 +869,13 @@ hipError_t launch_tc_write_node(const GenLaunch& L, const TcTables* T, int node,
                        dim3((unsigned)((m + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s, L, T, node, m, out, capacity,
                        status);
   } else {
+    const int fs = (((nchild + 63) >> 6) << 3) + 8 * nchild;  // bitmap + slots
+    if (nchild > 0 && fs <= kTcStageMax) {
+      raise_lds_cap(&tc_write_fields_lds_kernel<false>);
+      hipLaunchKernelGGL(tc_write_fields_lds_kernel<false>, dim3((unsigned)((m + kTcWG - 1) / kTcWG)), dim3(kTcWG),
+                         (size_t)kTcWG * fs, s, L, T, node, m, nullptr, out, capacity, status, fs);
+      return hipGetLastError();
+    }
     const int64_t work = m * tc_group_lanes(nchild > 0 ? nchild : 1);
     hipLaunchKernelGGL(tc_write_fields_kernel<false>, dim3((unsigned)((work + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0,
                        s, L, T, node, m, nullptr, out, capacity, status);

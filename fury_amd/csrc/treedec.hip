@@ -29,7 +29,8 @@ namespace fory_amd {
 namespace {
 
 constexpr int kTdWG = 256;
-constexpr int kTdBatch = 4;  // fields whose slot words an instance loads together
+constexpr int kTdBatch = 4;
+constexpr int kTdStageMax = 264;  // bitmap + slots of up to 32 fields staged per lane  // fields whose slot words an instance loads together
 
 __device__ __forceinline__ bool td_leaf(int kind) { return kind == KIND_BYTES || kind == KIND_DECIMAL; }
 
@@ -186,19 +187,20 @@ __device__ __forceinline__ void td_scalar(const GNode& nd, const ColumnDev& col,
 // every lane runs it (validity by ballot).
 __device__ __forceinline__ void td_instance(const GenLaunch& L, const TdTables* T, int nf, int k0, int bm, int64_t k,
                                             bool inb, int64_t base, int64_t rend, const uint8_t* rows,
-                                            int32_t* status) {
+                                            int32_t* status, const uint8_t* img = nullptr) {
   const int level = L.fill_level;
   const bool values = level < 0;
   const bool present = base >= 0;
   const bool rd = inb && present;
+  const uint8_t* hb = img ? img : rows + (present ? base : 0);  // bitmap + slots (img: staged in LDS)
   uint64_t nulls = 0;  // the bitmap word of fields [64 b, 64 b + 64)
   // fields in batches: the batch's slot words (and the bitmap word) are loaded together
   // before any is used, so an instance costs one memory latency per batch, not per field
   for (int q0 = 0; q0 < nf; q0 += kTdBatch) {
     uint64_t sv[kTdBatch];
-    if ((q0 & 63) == 0) nulls = rd ? gget(rows + base + (q0 >> 3), bm - (q0 >> 3) >= 8 ? 8 : 4) : ~0ull;
+    if ((q0 & 63) == 0) nulls = rd ? gget(hb + (q0 >> 3), bm - (q0 >> 3) >= 8 ? 8 : 4) : ~0ull;
 #pragma unroll
-    for (int u = 0; u < kTdBatch; ++u) sv[u] = rd && q0 + u < nf ? gget(rows + base + bm + 8 * (q0 + u), 8) : 0;
+    for (int u = 0; u < kTdBatch; ++u) sv[u] = rd && q0 + u < nf ? gget(hb + bm + 8 * (q0 + u), 8) : 0;
 #pragma unroll 1
     for (int u = 0; u < kTdBatch; ++u) {  // rolled: one copy of the field body
       const int q = q0 + u;
@@ -226,10 +228,13 @@ __device__ __forceinline__ void td_instance(const GenLaunch& L, const TdTables* 
 // Rows (ROWS) or bean node s: a lane per instance, its fields in order (the row's
 // header, bitmap and slots are one or two lines, read once); the lanes of a wave write
 // consecutive elements of each field's column, validity a word per 32 lanes by ballot.
+// FS > 0: each wave first loads its instances' bitmaps + slots as consecutive dwords of
+// each (coalesced) into an LDS image of FS bytes per lane; FS = 0: each lane reads its own.
 template <bool ROWS>
 __global__ __launch_bounds__(kTdWG) void td_fields_kernel(GenLaunch L, const TdTables* __restrict__ T, int s,
                                                           int64_t m, const uint8_t* __restrict__ rows,
-                                                          const int64_t* __restrict__ offs, int32_t* status) {
+                                                          const int64_t* __restrict__ offs, int32_t* status,
+                                                          int FS) {
   const int nf = ROWS ? T->nroot : L.nodes[s].nchild;
   const int k0 = ROWS ? 0 : T->kid0[s];
   const int bm = ROWS ? L.bitmap_bytes : gbm(nf);
@@ -265,6 +270,22 @@ __global__ __launch_bounds__(kTdWG) void td_fields_kernel(GenLaunch L, const TdT
       base = T->P[s][k];
       rend = base >= 0 ? base + T->TL[s][k] : 0;
     }
+  }
+  if (FS > 0) {  // the wave's bitmaps + slots staged by consecutive dwords of each instance
+    extern __shared__ __attribute__((aligned(16))) uint8_t td_stage[];
+    const int lane = threadIdx.x & 63;
+    const int nd4 = (bm + 8 * nf) >> 2;
+    uint8_t* wimg = td_stage + (size_t)(threadIdx.x - lane) * FS;
+    for (int t = lane; t < 64 * nd4; t += 64) {  // (uniform trip count: the shuffles are)
+      const int r = t / nd4, j = t - r * nd4;
+      const int64_t br = __shfl(base, r);
+      if (br >= 0) st32(wimg + (size_t)r * FS + 4 * j, ld32(rows + br + 4 * j));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    td_instance(L, T, nf, k0, bm, k, inb, base, rend, rows, status, wimg + (size_t)lane * FS);
+    return;
   }
   td_instance(L, T, nf, k0, bm, k, inb, base, rend, rows, status);
 }
@@ -502,7 +523,13 @@ hipError_t launch_td_rows(const GenLaunch& L, const TdTables* T, int nroot, cons
   if (L.frame == FORY_FRAME_COLLECTION)
     hipLaunchKernelGGL(td_coll_kernel, dim3(gx), dim3(kTdWG), 0, s, L, T, rows, offs, status);
   else
-    hipLaunchKernelGGL(td_fields_kernel<true>, dim3(gx), dim3(kTdWG), 0, s, L, T, -1, L.num_rows, rows, offs, status);
+  {
+    const int fs = L.bitmap_bytes + 8 * nroot;
+    const int FS = fs <= kTdStageMax ? fs : 0;
+    if (FS) raise_lds_cap(&td_fields_kernel<true>);
+    hipLaunchKernelGGL(td_fields_kernel<true>, dim3(gx), dim3(kTdWG), (size_t)kTdWG * FS, s, L, T, -1, L.num_rows, rows,
+                       offs, status, FS);
+  }
   return hipGetLastError();
 }
 
@@ -516,7 +543,11 @@ hipError_t launch_td_node(const GenLaunch& L, const TdTables* T, int node, int64
                   : (flat ? &td_items_kernel<false, true> : &td_items_kernel<false, false>);
     hipLaunchKernelGGL(k, dim3(gx), dim3(kTdWG), 0, s, L, T, node, m, rows, status);
   } else if (nchild > 0) {
-    hipLaunchKernelGGL(td_fields_kernel<false>, dim3(gx), dim3(kTdWG), 0, s, L, T, node, m, rows, nullptr, status);
+    const int fs = (((nchild + 63) >> 6) << 3) + 8 * nchild;  // bitmap + slots
+    const int FS = fs <= kTdStageMax ? fs : 0;
+    if (FS) raise_lds_cap(&td_fields_kernel<false>);
+    hipLaunchKernelGGL(td_fields_kernel<false>, dim3(gx), dim3(kTdWG), (size_t)kTdWG * FS, s, L, T, node, m, rows,
+                       nullptr, status, FS);
   }
   return hipGetLastError();
 }
