@@ -2377,12 +2377,30 @@ void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, i
   L.pl_all = 1;
   auto* kd = &var_encode_flat_kernel<HDR, NW, NEST, false>;
   auto* kl = &var_encode_flat_lean_kernel<HDR, NW, NEST, false>;
+  // Staging first, then the image grown while the residency holds. When that leaves the
+  // staging >= 4 KiB per slot (small rows: staging is plentiful), the image is grown
+  // first instead (<= +12 %, at the same residency) and the staging takes the rest:
+  // fewer tiles spill to the big-image launch (Nested encode 0.79 -> 0.73 ms in
+  // alternating runs; Mixed keeps its sizing, its staging is the scarce part).
   auto size_for = [&](decltype(kd) kk, int* stg, int* c) {
     VarLaunch T = L;
     *stg = enc_stg_bytes(kk, T, capacity, cap, NW);
     T.stg_bytes = *stg;
     *c = grow_cap(T, kk, 64 * NW, cap, [&](int x) { return flat_lds_enc(T, x, NW); });
-    return occupancy_of(kk, 64 * NW, flat_lds_enc(T, *c, NW));
+    const int occ = occupancy_of(kk, 64 * NW, flat_lds_enc(T, *c, NW));
+    if (*stg < 4096 || occ <= 0 || L.kn.var_cap || L.kn.var_fit || L.kn.var_stg) return occ;
+    VarLaunch U = L;
+    U.stg_bytes = 1024;
+    int cc = cap;
+    const int lim = cap * 112 / 100 < 64 * 1024 ? cap * 112 / 100 : 64 * 1024;
+    while (cc + 256 <= lim && occupancy_of(kk, 64 * NW, flat_lds_enc(U, cc + 256, NW)) >= occ) cc += 256;
+    U.stg_bytes = L.stg_bytes;
+    const int s2 = enc_stg_bytes(kk, U, capacity, cc, NW);
+    U.stg_bytes = s2;
+    if (cc <= *c || occupancy_of(kk, 64 * NW, flat_lds_enc(U, cc, NW)) < occ) return occ;
+    *stg = s2;
+    *c = cc;
+    return occ;
   };
   int stg_d = 0, cap_d = cap, stg_l = 0, cap_l = cap;
   const int occ_d = size_for(kd, &stg_d, &cap_d);
