@@ -64,6 +64,8 @@ def parse():
                     help="process group backend (gloo: rehearsal of the multi-rank path)")
     ap.add_argument("--oversubscribe", action="store_true",
                     help="allow more ranks than visible GPUs (rank -> cuda:(local_rank %% count)); rehearsal only")
+    ap.add_argument("--init-dist", action="store_true",
+                    help="initialise the process group even for one rank (rehearses the RCCL branch on a 1-GPU box)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads of the CPU baseline")
@@ -108,7 +110,7 @@ def setup_dist(args):
     dev = local % max(1, have)
     torch.cuda.set_device(dev)
     dist = None
-    if world > 1:
+    if world > 1 or args.init_dist:
         import torch.distributed as dist
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
@@ -311,7 +313,7 @@ def jdk_probe():
 
 def main():
     args = parse()
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.init_dist):
         sys.exit(launch_ranks(args))
     import torch
     dist, world, rank, dev = setup_dist(args)

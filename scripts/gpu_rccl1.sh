@@ -1,0 +1,11 @@
+#!/bin/bash
+# RCCL rehearsal on a 1-GPU box: bench.py --gpus 1 --init-dist starts one torchrun rank that
+# initialises the nccl (RCCL) process group and runs the line's collectives on the device
+# (init all_reduce, device all_gather_object, barriers, MAX over ranks); Struct104 16Mi rows.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/rccl1
+timeout -k 10 300 python bench.py --gpus 1 --init-dist --backend nccl --total-rows 16777216 --weak-rows 0 \
+  --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/rccl1/bench_rccl1.json 2> gpurun_out/rccl1/bench_rccl1.err
+rc=$?; echo "rccl 1-rank bench exit $rc"; cut -c1-400 gpurun_out/rccl1/bench_rccl1.json; tail -3 gpurun_out/rccl1/bench_rccl1.err
+exit $rc
