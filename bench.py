@@ -78,6 +78,9 @@ DEFAULT_TOTAL = {"struct104": 256 * MI, "mixed40": 16 * MI, "nested": 8 * MI,
                  "mixed40_long": 8 * MI}  # mixed40_long: strings 0..128 B (robustness, not a BASELINE config)
 
 
+_LINE_OUT = sys.stdout
+
+
 def launch_ranks(args) -> int:
     """Parent of an N-rank run: torchrun as a child process (no GPU touched here;
     device_count() does not initialise the GPU)."""
@@ -315,6 +318,13 @@ def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.init_dist):
         sys.exit(launch_ranks(args))
+    # the JSON line is the only thing on stdout: RCCL's init banner and gloo's connection
+    # notices are written to fd 1 by native code, so fd 1 is pointed at stderr for the run
+    # and the line goes to a saved copy of the original stdout
+    global _LINE_OUT
+    sys.stdout.flush()
+    _LINE_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     dist, world, rank, dev = setup_dist(args)
     device = torch.device("cuda", dev)
@@ -575,7 +585,7 @@ def main():
                                               "rows_per_s": single["rows_per_s"], "sample": single["sample"]}
         res["cpu_baseline"]["reference_jvm"] = jdk_probe()
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=_LINE_OUT, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
