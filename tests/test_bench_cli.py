@@ -60,3 +60,23 @@ def test_pmc_traffic_needs_the_same_build(tmp_path):
     assert bench.pmc_traffic(str(p), "struct104", 64, 0, "encode") == 123
     json.dump({"struct104:64:0": {"encode": 123}}, open(p, "w"))  # unstamped
     assert bench.pmc_traffic(str(p), "struct104", 64, 0, "encode") is None
+
+
+def test_init_dist_goes_through_the_rank_launcher():
+    # --init-dist starts torchrun ranks even for --gpus 1, so it is refused the same way
+    # when the GPU is not there
+    import torch
+    if torch.cuda.device_count() >= 1:
+        pytest.skip("this host has a GPU")
+    r = run_bench(["--gpus", "1", "--init-dist", "--steps", "1", "--warmup", "0"])
+    assert r.returncode != 0
+    assert "refusing" in r.stderr
+
+
+def test_stdout_carries_nothing_but_the_line():
+    # a rank that fails before measuring prints nothing on stdout (fd 1 points at stderr
+    # for the run; only the JSON line goes to the saved stdout)
+    r = run_bench(["--gpus", "1", "--steps", "1", "--warmup", "0"],
+                  {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert r.stdout == ""
