@@ -67,6 +67,11 @@ def parse():
     ap.add_argument("--init-dist", action="store_true",
                     help="initialise the process group even for one rank (rehearses the RCCL branch on a 1-GPU box)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--extras", type=int, default=-1,
+                    help="struct104: also time BASELINE C2/C3 (Mixed 16Mi, Nested 8Mi; raw + frame) in the same run "
+                         "(-1 = at N=1 only, 0 = off, 1 = on)")
+    ap.add_argument("--extra-steps", type=int, default=5)
+    ap.add_argument("--extra-warmup", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads of the CPU baseline")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_latest.json"),
@@ -197,16 +202,20 @@ def make_batch(config, n, row0, device):
         torch.cuda.synchronize()
         return schema, cols, col_bytes
     mixed = config.startswith("mixed40")
-    mk = W.mixed_host_columns if mixed else W.nested_host_columns
     seed = (23 if mixed else 29) + row0
-    host = mk(n, seed=seed, max_len=128) if config == "mixed40_long" else mk(n, seed=seed)
-    cols = to_device(host, device)
+    if mixed:
+        cols = W.mixed_device_columns(n, seed=seed, device=device, max_len=128 if config == "mixed40_long" else 32)
+    else:
+        cols = W.nested_device_columns(n, seed=seed, device=device)
     col_bytes = 0
-    for c in host:
-        for a in (c.values, c.offsets, c.validity):
+    for c in cols:
+        for a in (c.offsets, c.validity):
             if a is not None:
-                col_bytes += a.nbytes
-    # string/item value buffers carry 8 bytes of generator padding: not algorithmic
+                col_bytes += a.numel() * a.element_size()
+        if c.values is not None:
+            col_bytes += c.values.numel() * c.values.element_size()
+            if c.offsets is not None:  # string bytes: 8 bytes of generator padding are not algorithmic
+                col_bytes -= 8
     torch.cuda.synchronize()
     return (W.mixed_schema() if mixed else W.nested_schema()), cols, col_bytes
 
@@ -446,7 +455,9 @@ def main():
             "data": "synthetic (java.util.Random per record, as Struct.createPOJO)",
             "config": {"workload": f"struct104 {'frame-stream' if frame else 'raw rows'}: BASELINE C4, "
                                    f"{total_rows} records split over {world} rank(s), windows of <= "
-                                   f"{args.window_rows} records (the 64M-row headline batch)",
+                                   f"{args.window_rows} records (the 64M-row headline batch); each rank generates "
+                                   f"one window of {wmax} records and encodes + decodes it {len(wins)} time(s) "
+                                   f"per step (its share), the columns resident in HBM",
                        "total_rows": total_rows, "rows_per_gpu": share, "windows_per_gpu": len(wins),
                        "window_rows": wmax, "row_bytes_total": row_bytes_step,
                        "column_bytes_per_record": col_row, "frame_mode": "stream" if frame else "raw",
@@ -457,6 +468,8 @@ def main():
                            "decode_min": round(min(dec_ms), 4) if dec_ms else None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "frac_basis": "hipEvent time of the launch (average over the timed windows)",
+                         "trace": trace_frac(args.pmc, config, wmax, frame, dom, algo),
                          "traffic": pmc_traffic(args.pmc, config, wmax, frame, dom),
                          "traffic_source": "profiles/pmc_latest.json (rocprofv3 --pmc pass of this command, "
                                            "same lib_sha16; null when the build differs)",
@@ -469,110 +482,22 @@ def main():
             res["weak"] = res_weak
     # ------------------------------------------------------------------ varlen
     else:
-        n = share
-        cols = cols_all
-        col_bytes = col_bytes_all
-        arr = native.column_array(cols)
-        offs = torch.empty(n + 1, dtype=torch.int64, device=device)
-        native.encoded_size(plan, arr, n, frame, offs, ws, stream)
-        total = int(offs[n].item())
-        out = torch.empty(max(16, total), dtype=torch.uint8, device=device)
-        native.encode(plan, arr, n, frame, offs, out, status, ws, stream)
-        dcols = enc.decode(out[:total], n, frame, offs)
-        darr = native.column_array(dcols)
-
-        # frame streams decode from the stream alone (a receiver has no row offsets):
-        # the device frame index (fory_rowfmt_index_frames) runs inside the decode
-        ioffs, iws = offs, None
-        if frame:
-            ioffs = torch.empty(n + 1, dtype=torch.int64, device=device)
-            iws = torch.empty(max(256, native.index_workspace_bytes(plan, n, total)), dtype=torch.uint8,
-                              device=device)
-
-        def step(ev=None):
-            # events: 0 | encoded_size | 3 | encode | 1 | index_frames | 5 | decode_sizes | 4 | decode | 2
-            if ev:
-                ev[0].record()
-            native.encoded_size(plan, arr, n, frame, offs, ws, stream)
-            if ev:
-                ev[3].record()
-            native.encode(plan, arr, n, frame, offs, out, status, ws, stream)
-            if ev:
-                ev[1].record()
-            if frame:
-                native.index_frames(plan, out, total, n, frame, ioffs, status, iws, stream)
-            if ev:
-                ev[5].record()
-            native.decode_sizes(plan, out, ioffs, n, frame, darr, status, ws, stream)
-            if ev:
-                ev[4].record()
-            native.decode(plan, out, ioffs, n, frame, darr, status, ws, stream)
-            if ev:
-                ev[2].record()
-
-        for _ in range(args.warmup):
-            step()
-        native.read_status(status, stream)
-        bad = check_round_trip(plan, cols, dcols, n)
-        if bad:
-            raise SystemExit(f"round-trip mismatch on the benchmark batch: {bad}")
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
-        barrier(dist)
-        t0 = time.perf_counter()
-        for k in range(args.steps):
-            step(evs[k])
-        barrier(dist)
-        el = max_over_ranks(dist, time.perf_counter() - t0, args.backend)
-        native.read_status(status, stream)
-        enc_avg = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)  # sizes + scan + encode
-        dec_avg = sum(e[1].elapsed_time(e[2]) for e in evs) / len(evs)  # [index] + decode_sizes + decode
-        idx_avg = sum(e[1].elapsed_time(e[5]) for e in evs) / len(evs)  # frame index (stream mode)
-        enc_k = sum(e[3].elapsed_time(e[1]) for e in evs) / len(evs)    # encode call alone
-        dec_k = sum(e[4].elapsed_time(e[2]) for e in evs) / len(evs)    # decode call alone
-        algo = col_bytes + total
-        dom, dom_ms = ("encode", enc_avg) if enc_avg >= dec_avg else ("decode", dec_avg)
-        achieved = algo / (dom_ms * 1e-3) / 1e9
-        row_bytes_all = total
-        if dist is not None:
-            t = torch.tensor([float(total)], dtype=torch.float64,
-                             device="cuda" if args.backend == "nccl" else "cpu")
-            dist.all_reduce(t)
-            row_bytes_all = int(t.item())
-        value = 2 * row_bytes_all * args.steps / el / 2**30
-        res = {
-            "metric": "row-format encode+decode GiB/s (device-resident), 64M Struct(100 prim) rows",
-            "value": round(value, 3),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(el * 1000 / args.steps, 4),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (numpy seeded)",
-            "config": {"workload": f"{config} {'frame-stream (decoded from the stream alone)' if frame else 'raw rows'}, "
-                                   f"{total_rows} records split over {world} rank(s)",
-                       "total_rows": total_rows, "rows_per_gpu": n, "row_bytes_total_per_gpu": total,
-                       "column_bytes_per_gpu": col_bytes, "frame_mode": "stream" if frame else "raw",
-                       "schema_hash": plan.schema_hash,
-                       "parallelism": f"record-sharded x{world} (contiguous ranges), no collective"},
-            "kernels_ms": {"encode_avg": round(enc_avg, 4), "decode_avg": round(dec_avg, 4),
-                           "encode_call_avg": round(enc_k, 4), "decode_call_avg": round(dec_k, 4),
-                           "frame_index_avg": round(idx_avg, 4) if frame else None},
-            "roofline": {"bound": "hbm", "kernel": dom + " (sizing passes included)",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "call_frac": {"encode": round(algo / (enc_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                       "decode": round(algo / (dec_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-                         "traffic": pmc_traffic(args.pmc, config, n, frame, dom),
-                         "traffic_source": "profiles/pmc_latest.json (rocprofv3 --pmc pass of this command, "
-                                           "same lib_sha16; null when the build differs)",
-                         "algorithmic_bytes_per_launch": algo},
-            "lib_sha16": lib_sha16(),
-            "step_hbm_frac": round(2 * algo / ((enc_avg + dec_avg) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-        }
+        res = measure_varlen(args, config, frame, total_rows, dist, world, device, args.steps, args.warmup,
+                             batch=(schema, cols_all, col_bytes_all, enc, ws, status, stream))
+        res = {"metric": METRIC, **res}
+    if plan.fixed_width and config == "struct104" and extras_on(args, world):
+        # BASELINE C2 / C3 (Mixed 16Mi, Nested 8Mi), raw rows and frame streams decoded from the
+        # stream alone: timed in the same default run, so the driver observes them too; the
+        # headline line above is unchanged by them (measured before, in its own batch)
+        del cols_all, dcols_all, out, arrs
+        torch.cuda.empty_cache()
+        res["extra_configs"] = []
+        for cfg in ("mixed40", "nested"):
+            for fr in (0, 1):
+                x = measure_varlen(args, cfg, fr, DEFAULT_TOTAL[cfg], dist, world, device, args.extra_steps,
+                                   args.extra_warmup)
+                res["extra_configs"].append(x)
+                torch.cuda.empty_cache()
     res["devices"] = devices
     if args.oversubscribe:
         res["oversubscribed"] = True
@@ -589,6 +514,140 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+METRIC = "row-format encode+decode GiB/s (device-resident), 64M Struct(100 prim) rows"
+
+
+def extras_on(args, world) -> bool:
+    """C2 / C3 lines beside the headline: on by default at N = 1 (the driver's BENCH run);
+    --extras 1 forces them on multi-GPU runs too, --extras 0 off."""
+    return args.extras == 1 or (args.extras < 0 and world == 1)
+
+
+def measure_varlen(args, config, frame, total_rows, dist, world, device, steps, warmup, batch=None):
+    """One varlen config (Mixed / Nested): every timed step = encoded_size + encode, then
+    [frame index +] decode_sizes + decode of this rank's share, inputs resident in HBM;
+    HIP events on the launch stream around each call. Returns the line's fields."""
+    import torch
+    from fury_amd.format.encoder import RowEncoder
+    from fury_amd.format import native
+    from fury_amd.shard import shard_range
+    rank = dist.get_rank() if dist is not None else 0
+    b, e = shard_range(total_rows, world, rank)
+    n = e - b
+    if batch is None:
+        schema, cols, col_bytes = make_batch(config, n, b, device)
+        enc = RowEncoder(schema, device=device)
+        ws = enc.workspace(n)
+        status = torch.zeros(1, dtype=torch.int32, device=device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+    else:
+        schema, cols, col_bytes, enc, ws, status, stream = batch
+    plan = enc.plan
+    arr = native.column_array(cols)
+    offs = torch.empty(n + 1, dtype=torch.int64, device=device)
+    native.encoded_size(plan, arr, n, frame, offs, ws, stream)
+    total = int(offs[n].item())
+    out = torch.empty(max(16, total), dtype=torch.uint8, device=device)
+    native.encode(plan, arr, n, frame, offs, out, status, ws, stream)
+    dcols = enc.decode(out[:total], n, frame, offs)
+    darr = native.column_array(dcols)
+
+    # frame streams decode from the stream alone (a receiver has no row offsets):
+    # the device frame index (fory_rowfmt_index_frames) runs inside the decode
+    ioffs, iws = offs, None
+    if frame:
+        ioffs = torch.empty(n + 1, dtype=torch.int64, device=device)
+        iws = torch.empty(max(256, native.index_workspace_bytes(plan, n, total)), dtype=torch.uint8,
+                          device=device)
+
+    def step(ev=None):
+        # events: 0 | encoded_size | 3 | encode | 1 | index_frames | 5 | decode_sizes | 4 | decode | 2
+        if ev:
+            ev[0].record()
+        native.encoded_size(plan, arr, n, frame, offs, ws, stream)
+        if ev:
+            ev[3].record()
+        native.encode(plan, arr, n, frame, offs, out, status, ws, stream)
+        if ev:
+            ev[1].record()
+        if frame:
+            native.index_frames(plan, out, total, n, frame, ioffs, status, iws, stream)
+        if ev:
+            ev[5].record()
+        native.decode_sizes(plan, out, ioffs, n, frame, darr, status, ws, stream)
+        if ev:
+            ev[4].record()
+        native.decode(plan, out, ioffs, n, frame, darr, status, ws, stream)
+        if ev:
+            ev[2].record()
+
+    for _ in range(warmup):
+        step()
+    native.read_status(status, stream)
+    bad = check_round_trip(plan, cols, dcols, n)
+    if bad:
+        raise SystemExit(f"round-trip mismatch on the benchmark batch: {bad}")
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(steps)]
+    barrier(dist)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(evs[k])
+    barrier(dist)
+    el = max_over_ranks(dist, time.perf_counter() - t0, args.backend)
+    native.read_status(status, stream)
+    enc_avg = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)  # sizes + scan + encode
+    dec_avg = sum(e[1].elapsed_time(e[2]) for e in evs) / len(evs)  # [index] + decode_sizes + decode
+    idx_avg = sum(e[1].elapsed_time(e[5]) for e in evs) / len(evs)  # frame index (stream mode)
+    enc_k = sum(e[3].elapsed_time(e[1]) for e in evs) / len(evs)    # encode call alone
+    dec_k = sum(e[4].elapsed_time(e[2]) for e in evs) / len(evs)    # decode call alone
+    algo = col_bytes + total
+    dom, dom_ms = ("encode", enc_avg) if enc_avg >= dec_avg else ("decode", dec_avg)
+    achieved = algo / (dom_ms * 1e-3) / 1e9
+    row_bytes_all = total
+    if dist is not None:
+        t = torch.tensor([float(total)], dtype=torch.float64,
+                         device="cuda" if args.backend == "nccl" else "cpu")
+        dist.all_reduce(t)
+        row_bytes_all = int(t.item())
+    value = 2 * row_bytes_all * steps / el / 2**30
+    res = {
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(el * 1000 / steps, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (torch generator on the device, seeded; uniform string / list lengths as the config)",
+        "config": {"workload": f"{config} {'frame-stream (decoded from the stream alone)' if frame else 'raw rows'}, "
+                               f"{total_rows} records split over {world} rank(s)",
+                   "total_rows": total_rows, "rows_per_gpu": n, "row_bytes_total_per_gpu": total,
+                   "column_bytes_per_gpu": col_bytes, "frame_mode": "stream" if frame else "raw",
+                   "schema_hash": plan.schema_hash,
+                   "parallelism": f"record-sharded x{world} (contiguous ranges), no collective"},
+        "kernels_ms": {"encode_avg": round(enc_avg, 4), "decode_avg": round(dec_avg, 4),
+                       "encode_call_avg": round(enc_k, 4), "decode_call_avg": round(dec_k, 4),
+                       "frame_index_avg": round(idx_avg, 4) if frame else None},
+        "roofline": {"bound": "hbm", "kernel": dom + " (sizing passes included)",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "call_frac": {"encode": round(algo / (enc_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                   "decode": round(algo / (dec_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                     "frac_basis": "hipEvent time of the calls incl. sizing passes (call_frac: the call alone)",
+                     "trace": trace_frac(args.pmc, config, n, frame, "encode" if enc_k >= dec_k else "decode", algo),
+                     "traffic": pmc_traffic(args.pmc, config, n, frame, dom),
+                     "traffic_source": "profiles/pmc_latest.json (rocprofv3 --pmc pass of this command, "
+                                       "same lib_sha16; null when the build differs)",
+                     "algorithmic_bytes_per_launch": algo},
+        "lib_sha16": lib_sha16(),
+        "step_hbm_frac": round(2 * algo / ((enc_avg + dec_avg) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+    }
+    return res
 
 
 def lib_sha16() -> str:
@@ -615,6 +674,24 @@ def pmc_traffic(path, config, n, frame, dom):
     except (OSError, ValueError):
         pass
     return None
+
+
+def trace_frac(path, config, n, frame, kern, algo):
+    """The same fraction from the rocprofv3 kernel trace of this command (average launch
+    duration of the call's main kernel, profiles/*/rocprof_kernel_stats.csv) when that
+    trace measured THIS library build; else null. The stamped entry names the kernel."""
+    try:
+        with open(path) as fh:
+            ent = json.load(fh).get(f"{config}:{n}:{frame}")
+        if not ent or ent.get("lib_sha16") != lib_sha16():
+            return None
+        ms = (ent.get("trace_ms") or {}).get(kern)
+        if not ms:
+            return None
+        return {"kernel": ent.get(kern + "_kernel"), "avg_ms": ms,
+                "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "source": ent.get("trace_source")}
+    except (OSError, ValueError):
+        return None
 
 
 if __name__ == "__main__":

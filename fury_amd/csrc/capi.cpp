@@ -815,6 +815,7 @@ int td_prepare(const fory_plan* plan, const fory_column* out_cols, int64_t n, vo
       at += align_up(k * 4);
     }
   if (partials) *partials = reinterpret_cast<int64_t*>(at);
+  for (size_t i = 0; i < m->size(); ++i) T.m[i] = (*m)[i];
   int nk = 0;
   for (int32_t f : plan->p.top) T.kids[nk++] = f;
   T.nroot = nk;
@@ -1133,10 +1134,11 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
       int64_t* tpart = nullptr;
       const uint64_t sig = tc_signature(plan, cols, num_rows, frame_mode);
       rc = tc_prepare(plan, cols, num_rows, d_workspace, s, &T, &dT, &tpart);
-      if (!rc && !tc_recall(d_workspace, plan->id, sig)) {  // sizes not left by encoded_size
-        rc = tc_sizes(plan, G, T, dT, tpart, s);
-        if (!rc) tc_remember(d_workspace, plan->id, sig);
-      }
+      // sizes the preceding encoded_size left for these columns are used once: encode
+      // never leaves sizes of its own, so a later encode of refilled columns re-sizes them
+      const bool left = !rc && tc_recall(d_workspace, plan->id, sig);
+      tc_forget(d_workspace);
+      if (!rc && !left) rc = tc_sizes(plan, G, T, dT, tpart, s);
       if (rc) return rc;
       uint8_t* out = static_cast<uint8_t*>(d_out);
       e = fory_amd::launch_tc_write_rows(G, dT, T.nroot, d_row_offsets, out, out_capacity, d_status, s);
@@ -1372,7 +1374,9 @@ int64_t fory_rowfmt_index_workspace_bytes(const fory_plan* plan, int64_t num_row
 int fory_rowfmt_index_frames(const fory_plan* plan, const void* d_rows, int64_t rows_bytes, int64_t num_rows,
                              int32_t frame_mode, int64_t* d_row_offsets, int32_t* d_status, void* d_workspace,
                              int64_t workspace_bytes, void* stream) {
+  // the index overwrites the workspace: neither engine's memo survives it
   tc_forget(d_workspace);
+  td_forget(d_workspace);
   if (!plan) return fail(FORY_ERR_INVALID_ARGUMENT, "plan is null");
   if (num_rows < 0 || rows_bytes < 0) return fail(FORY_ERR_INVALID_ARGUMENT, "num_rows or rows_bytes < 0");
   if (frame_mode == FORY_FRAME_RAW)
@@ -1439,17 +1443,44 @@ int fory_rowfmt_split_windows(const int64_t* row_offsets, int64_t stride, int64_
   return FORY_OK;
 }
 
+}  // extern "C"
+
+namespace {
+std::mutex g_status_words_mu;
+std::vector<int32_t*> g_status_words;  // pinned status words of threads that ended
+}  // namespace
+
+extern "C" {
+
 int fory_rowfmt_read_status(const int32_t* d_status, void* stream) {
   if (!d_status) return FORY_OK;
   // the status word lands in pinned memory of this thread (an async DMA; never the
-  // runtime's pageable path), allocated once per thread and kept for its life
-  thread_local int32_t* pinned_word = nullptr;
+  // runtime's pageable path): a word taken from a process-wide pool on the thread's first
+  // call and handed back when the thread ends (no HIP call in a thread-exit destructor),
+  // so JNI worker pools that come and go reuse words instead of pinning new ones
+  struct PinnedWord {
+    int32_t* p = nullptr;
+    ~PinnedWord() {
+      if (!p) return;
+      std::lock_guard<std::mutex> lock(g_status_words_mu);
+      g_status_words.push_back(p);
+    }
+  };
+  thread_local PinnedWord word;
+  if (!word.p) {
+    std::lock_guard<std::mutex> lock(g_status_words_mu);
+    if (!g_status_words.empty()) {
+      word.p = g_status_words.back();
+      g_status_words.pop_back();
+    }
+  }
   hipError_t e = hipSuccess;
-  if (!pinned_word) e = hipHostMalloc(reinterpret_cast<void**>(&pinned_word), 64, hipHostMallocPortable);
+  if (!word.p) e = hipHostMalloc(reinterpret_cast<void**>(&word.p), 64, hipHostMallocPortable);
   if (e != hipSuccess) {
-    pinned_word = nullptr;
+    word.p = nullptr;
     return hip_fail(e, "read_status (pinned word)");
   }
+  int32_t* pinned_word = word.p;
   hipStream_t s = static_cast<hipStream_t>(stream);
   *pinned_word = 0;
   e = hipMemcpyAsync(pinned_word, d_status, sizeof(int32_t), hipMemcpyDeviceToHost, s);

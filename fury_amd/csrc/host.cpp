@@ -182,11 +182,24 @@ int stage_alloc(Staging& st) {
   return rc;
 }
 
+// After a failed wait on a staging event: no owed D2H copy of this call may be made
+// later (its caller buffers may be gone by the context's next call), and no block is
+// waited for again. The context's next call starts with clean staging.
+void stage_abandon(Staging& st) {
+  for (int j = 0; j < Staging::kBlocks; ++j) {
+    st.inflight[j] = false;
+    st.owed[j] = Staging::Owed{};
+  }
+}
+
 // Block j free for a new piece: its last DMA done, an owed D2H host copy made.
 int stage_retire(Staging& st, int j) {
   if (st.inflight[j]) {
     int rc = hip_check(hipEventSynchronize(st.ev[j]), "hipEventSynchronize(staging)");
-    if (rc) return rc;
+    if (rc) {
+      stage_abandon(st);
+      return rc;
+    }
     st.inflight[j] = false;
   }
   if (st.owed[j].dst) {
@@ -199,12 +212,11 @@ int stage_retire(Staging& st, int j) {
 // Every staged piece complete, every owed D2H copy in caller memory (oldest first).
 int stage_drain(Staging& st) {
   if (!st.mem) return FORY_OK;
-  int rc = FORY_OK;
   for (int i = 0; i < Staging::kBlocks; ++i) {
-    const int r = stage_retire(st, (st.next + i) % Staging::kBlocks);
-    if (!rc) rc = r;
+    const int rc = stage_retire(st, (st.next + i) % Staging::kBlocks);
+    if (rc) return rc;  // (stage_abandon cleared every block)
   }
-  return rc;
+  return FORY_OK;
 }
 
 // One copy between caller host memory and the device, queued on stream s. Pinned

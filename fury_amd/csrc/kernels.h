@@ -196,6 +196,7 @@ struct TdTables {
   int32_t* SZ[kTcMaxNodes];
   int32_t* TL[kTcMaxNodes];
   int64_t* SRC[kTcMaxNodes];  // string / binary nodes: each value's bytes in the rows (-1: null)
+  int64_t m[kTcMaxNodes];     // instances of each node in this call (the output columns' lengths)
   int32_t kids[kTcMaxNodes];  // fields by parent: the rows' top-level fields, then each bean's
   int32_t kid0[kTcMaxNodes];
   int32_t nroot;

@@ -62,14 +62,19 @@ __device__ __forceinline__ int64_t tc_array_bytes(const GenLaunch& L, const TcTa
   return b;
 }
 
-// Item range [o0, o1) of container instance j of node c (offsets clamped to the items' column).
-__device__ __forceinline__ void tc_items(const GenLaunch& L, const TcTables* T, int c, int64_t j, int64_t* o0,
+// Item range [o0, o1) of container instance j of node c (offsets clamped to the items' column,
+// so no pass reads or writes past it). Returns false when the offsets did not fit the items'
+// column length the caller passed (or decrease): the write pass reports that as
+// FORY_ERR_INVALID_ARGUMENT instead of dropping the items silently.
+__device__ __forceinline__ bool tc_items(const GenLaunch& L, const TcTables* T, int c, int64_t j, int64_t* o0,
                                          int64_t* o1) {
   const int32_t* off = L.cols[c].offsets;
   const int64_t mx = T->m[c + 1];
-  const int64_t a = tc_clamp(off[j], mx), b = tc_clamp(off[j + 1], mx);
+  const int64_t ra = off[j], rb = off[j + 1];
+  const int64_t a = tc_clamp(ra, mx), b = tc_clamp(rb, mx);
   *o0 = a;
   *o1 = b < a ? a : b;
+  return ra >= 0 && rb >= ra && rb <= mx;
 }
 
 // ---------------------------------------------------------------------------
@@ -277,15 +282,19 @@ __device__ __forceinline__ void tc_copy(uint8_t* dst, const uint8_t* src, int64_
   }
 }
 
-// A leaf value at `at` (room checked by the caller): writeUnaligned + zeroOutPaddingBytes,
-// or BinaryWriter.writeDecimal (checkPrecisionAndScale: FORY_ERR_UNSUPPORTED).
+// A leaf value at `at`, S bytes allotted (room for S checked by the caller):
+// writeUnaligned + zeroOutPaddingBytes, or BinaryWriter.writeDecimal
+// (checkPrecisionAndScale: FORY_ERR_UNSUPPORTED). A string whose padded length is not S
+// (sizes from an encoded_size call over other contents) is not written: FORY_ERR_ENCODER.
 __device__ __forceinline__ int32_t tc_leaf_write(uint8_t* out, const GNode& nd, const ColumnDev& col, int64_t k,
-                                                 int64_t at) {
+                                                 int64_t at, int64_t S) {
   if (nd.kind == KIND_BYTES) {
-    const int64_t s0 = col.offsets[k];
-    tc_copy(out + at, col.values + s0, (int64_t)col.offsets[k + 1] - s0);
+    const int64_t s0 = col.offsets[k], n = (int64_t)col.offsets[k + 1] - s0;
+    if (n < 0 || gr8(n) != S) return FORY_ERR_ENCODER;
+    tc_copy(out + at, col.values + s0, n);
     return 0;
   }
+  if (S != 32) return FORY_ERR_ENCODER;
   const uint8_t* x = col.values + 16 * k;
   const uint32_t w[4] = {ld32(x), ld32(x + 4), ld32(x + 8), ld32(x + 12)};
   if (!g_dec_fits(w, nd.prec)) return FORY_ERR_UNSUPPORTED;
@@ -440,7 +449,7 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_kernel(GenLaunch L, con
   if (has_pos) {
     T->P[kid][k] = at;
   } else {
-    const int32_t r = tc_leaf_write(out, nd, col, k, at);
+    const int32_t r = tc_leaf_write(out, nd, col, k, at, S);
     if (r) set_status(status, r);
   }
 }
@@ -561,7 +570,7 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_lds_kernel(GenLaunch L,
       if (has_pos) {
         T->P[kid][k] = at;
       } else {
-        const int32_t r = tc_leaf_write(out, nd, s_col[q], kk, at);
+        const int32_t r = tc_leaf_write(out, nd, s_col[q], kk, at, Su);
         if (r) set_status(status, r);
       }
     }
@@ -706,7 +715,7 @@ __device__ __forceinline__ int32_t tc_element(const GenLaunch& L, const TcTables
     return FORY_ERR_ENCODER;
   }
   tc_put(el, ((uint64_t)(at - Pa) << 32) | tc_slot_size(it, col, e, S), 8);
-  if (leaf) return tc_leaf_write(out, it, col, e, at);
+  if (leaf) return tc_leaf_write(out, it, col, e, at, S);
   T->P[x][e] = at;
   return 0;
 }
@@ -730,9 +739,11 @@ __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const
   if (tid < cnt) {
     const int64_t j = j0 + tid;
     int64_t o0, o1;
-    tc_items(L, T, c, j, &o0, &o1);
-    const int64_t n = o1 - o0;
     int64_t P = T->P[c][j];
+    // offsets past the items' column length (a short fory_column.length): an error, not a
+    // silently shorter array (present containers only: absent ones read no items)
+    if (!tc_items(L, T, c, j, &o0, &o1) && P >= 0) err = FORY_ERR_INVALID_ARGUMENT;
+    const int64_t n = o1 - o0;
     int64_t kb = 0;
     // the items' validity windows, loaded with the array sizes (the bitmaps need them next)
     const TcVwin vk = tc_vwin((L.nodes[key].flags & 1) ? L.cols[key].validity : nullptr, o0, o1);

@@ -371,9 +371,9 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
   // waves walk 64-aligned groups of items (uniform trip count: validity by ballot)
   for (int64_t eb = e0 & ~int64_t(63); eb < e1; eb += kTdWG) {
     const int64_t e = eb + tid;
-    const bool inr = e >= e0 && e < e1;
+    const bool inr_all = e >= e0 && e < e1;
     int a = 0;
-    if (inr) {
+    if (inr_all) {
       int b = cnt - 1;  // the last container whose items start at or before e
       while (a < b) {
         const int mid = (a + b + 1) >> 1;
@@ -386,6 +386,11 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
       const int x = w ? val : key;
       const GNode it = L.nodes[x];
       const ColumnDev ic = L.cols[x];
+      // an item past its output column's length (a short fory_column.length): nothing is
+      // written for it (its arrays end there) and the call reports FORY_ERR_CAPACITY
+      const bool inr = inr_all && e < T->m[x];
+      if (inr_all && !inr && (level < 0 || it.cdepth == level || !is_scalar(it.kind)))
+        set_status(status, FORY_ERR_CAPACITY);
       const int64_t arr = inr ? (w ? sV[a] : sK[a]) : -1;
       const bool present = arr >= 0 && q < n;
       const bool isnull = !present || ((rows[arr + 8 + (q >> 3)] >> (q & 7)) & 1);

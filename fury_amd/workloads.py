@@ -225,3 +225,81 @@ def row_bytes_fixed(schema: Schema) -> int:
 
 def column_bytes(schema: Schema) -> int:
     return sum(f.type.width for f in schema.fields)
+
+
+# ---------------------------------------------------------------------------
+# Device-side generators of M and N for bench.py (the same shapes and length
+# distributions as the host generators above, drawn with torch on the device so a
+# 16M-record batch is ready in milliseconds; values differ, the bytes moved do not).
+# ---------------------------------------------------------------------------
+def _dev_validity(valid, device):
+    """Arrow validity (LSB-first) of a bool tensor, padded to 4 bytes."""
+    import torch
+    n = valid.numel()
+    nb = max(4, ((n + 7) // 8 + 3) // 4 * 4)
+    bits = torch.zeros(nb * 8, dtype=torch.uint8, device=device)
+    bits[:n] = valid.to(torch.uint8)
+    w = (1 << torch.arange(8, device=device, dtype=torch.int32)).to(torch.uint8)
+    return (bits.view(nb, 8) * w).sum(dim=1, dtype=torch.int32).to(torch.uint8)
+
+
+def _dev_strings(n, max_len, gen, device):
+    import torch
+    lens = torch.randint(0, max_len + 1, (n,), generator=gen, device=device, dtype=torch.int64)
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    torch.cumsum(lens, 0, out=offs[1:])
+    total = int(offs[n].item())
+    if total > 0x7FFFFFFF:
+        raise ValueError("string column beyond int32 Arrow offsets")
+    data = torch.randint(32, 127, (total + 8,), generator=gen, device=device, dtype=torch.uint8)
+    return data, offs.to(torch.int32)
+
+
+def mixed_device_columns(n: int, seed: int = 23, device="cuda", max_len: int = 32):
+    """M on the device: DeviceColumns in schema order (strings nullable, all valid)."""
+    import torch
+    from .format.native import DeviceColumn
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    cols = []
+    for f in mixed_schema().fields:
+        t = f.type.id
+        if t == ArrowType.STRING:
+            data, offs = _dev_strings(n, max_len, gen, device)
+            valid = _dev_validity(torch.ones(n, dtype=torch.bool, device=device), device)
+            cols.append(DeviceColumn(data, offs, valid, n))
+        elif t == ArrowType.DOUBLE:
+            cols.append(DeviceColumn(torch.randn(n, generator=gen, device=device, dtype=torch.float64), None, None, n))
+        else:
+            dt = torch.int32 if t == ArrowType.INT32 else torch.int64
+            lo, hi = (-2**31, 2**31 - 1) if dt == torch.int32 else (-2**63, 2**63 - 1)
+            cols.append(DeviceColumn(torch.randint(lo, hi, (n,), generator=gen, device=device, dtype=dt), None, None, n))
+    return cols
+
+
+def nested_device_columns(n: int, seed: int = 29, device="cuda", max_len: int = 16):
+    """N on the device, pre-order: a, b, c(struct), x, y, z(list), item (no nulls)."""
+    import torch
+    from .format.native import DeviceColumn
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    i64 = (-2**63, 2**63 - 1)
+    a = torch.randint(*i64, (n,), generator=gen, device=device, dtype=torch.int64)
+    b = torch.randn(n, generator=gen, device=device, dtype=torch.float64)
+    x = torch.randint(-2**31, 2**31 - 1, (n,), generator=gen, device=device, dtype=torch.int32)
+    y = torch.randint(*i64, (n,), generator=gen, device=device, dtype=torch.int64)
+    lens = torch.randint(0, max_len + 1, (n,), generator=gen, device=device, dtype=torch.int64)
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    torch.cumsum(lens, 0, out=offs[1:])
+    m = int(offs[n].item())
+    items = torch.randint(*i64, (max(1, m),), generator=gen, device=device, dtype=torch.int64)
+    ones = torch.ones(n, dtype=torch.bool, device=device)
+    return [
+        DeviceColumn(a, None, None, n),
+        DeviceColumn(b, None, None, n),
+        DeviceColumn(None, None, _dev_validity(ones, device), n),
+        DeviceColumn(x, None, None, n),
+        DeviceColumn(y, None, None, n),
+        DeviceColumn(None, offs.to(torch.int32), _dev_validity(ones, device), n),
+        DeviceColumn(items, None, _dev_validity(torch.ones(m, dtype=torch.bool, device=device), device), m),
+    ]

@@ -179,10 +179,12 @@ int64_t fory_rowfmt_workspace_bytes(const fory_plan* plan, int64_t num_rows);
  * :236-351 / :370-427) are sized node by node and written tile by tile, with per-node
  * temporaries of each column's element count (fory_column.length of list items and map
  * keys / values: their offsets must lie in [0, length]). A smaller workspace keeps the
- * per-record engine; the bytes are identical. encode reuses the sizes the preceding
- * encoded_size of the same plan, columns, rows and framing left in the workspace (any
- * other call with that workspace discards them), so the columns must not change in
- * between. Equals fory_rowfmt_workspace_bytes for every other plan. */
+ * per-record engine; the bytes are identical. The encode that directly follows an
+ * encoded_size of the same plan, columns, rows and framing on the same workspace uses the
+ * sizes that call left there, once (the columns must not change in between: a string
+ * whose length no longer matches is not written and sets FORY_ERR_ENCODER); encode leaves
+ * no sizes of its own, and any other call with that workspace discards them. Equals
+ * fory_rowfmt_workspace_bytes for every other plan. */
 int64_t fory_rowfmt_encode_workspace_bytes(const fory_plan* plan, const fory_column* cols,
                                            int64_t num_rows);
 
@@ -254,9 +256,13 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols,
  * The columnar tree engine (a workspace of fory_rowfmt_decode_workspace_bytes) may also
  * write the values and validity of the levels a decode_sizes call sizes (all but string /
  * binary bytes); pass the same columns to the later calls. On one workspace, a
- * decode_sizes call resumes after the levels the previous one ran for the same plan,
- * rows, offsets and columns, and decode then only copies the string bytes; any other
- * call on the workspace drops that (the result is the same either way).
+ * decode_sizes call resumes after the levels the directly preceding decode_sizes ran for
+ * the same plan, rows, offsets and columns, and a decode directly after them only copies
+ * the string bytes; each call consumes what the previous one left, and any other call on
+ * the workspace drops it (the result is the same either way when the rows and columns
+ * did not change in between). A list / map item column shorter than its items
+ * (fory_column.length) is not written past its length: FORY_ERR_CAPACITY; on encode,
+ * offsets past an item column's length are FORY_ERR_INVALID_ARGUMENT.
  *
  * fory_rowfmt_decode: writes values/offsets/validity of out_cols. Null
  * values decode to 0 (RowEncoderBuilder.java:239-246 leaves the Java default).

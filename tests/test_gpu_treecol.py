@@ -239,3 +239,125 @@ def test_long_strings_decode_both_copy_paths(frame):
     encoded = enc.encode(to_device(cols), len(rows), frame)
     oracle_equal(schema, cols, len(rows), frame, encoded)
     assert columns_equal(schema, cols, to_host(enc.decode(encoded))) == []
+
+
+def _refilled(rows, seed):
+    """The same rows with every string replaced by one of another length (list / map
+    lengths unchanged, so every column keeps its length)."""
+    import copy
+    rng = np.random.default_rng(seed)
+
+    def walk(v):
+        if isinstance(v, str):
+            return "r" * int(rng.integers(0, 40))
+        if isinstance(v, list):
+            return [walk(x) for x in v]
+        if isinstance(v, tuple):  # map entries
+            return tuple(walk(x) for x in v)
+        if isinstance(v, dict):
+            return {k: walk(x) for k, x in v.items()}
+        if hasattr(v, "__dict__"):
+            o = copy.copy(v)
+            o.__dict__.update({k: walk(x) for k, x in v.__dict__.items()})
+            return o
+        return v
+
+    return [walk(r) for r in rows]
+
+
+def test_encode_after_in_place_refill_uses_current_sizes():
+    """encode(A, ws); A refilled in place (same pointers and lengths, other string sizes);
+    encoded_size on another workspace; encode(A, ws): the bytes are the refilled rows'
+    (encode leaves no sizes of its own for a later encode to reuse)."""
+    schema = nested_schemas()["holder"]
+    enc = RowEncoder(schema)
+    rows_a = random_rows(schema, 400, 41)
+    rows_b = _refilled(rows_a, 42)
+    ca, cb = build_columns(schema, rows_a), build_columns(schema, rows_b)
+    for a, b in zip(ca, cb):
+        assert a.length == b.length
+    # device buffers big enough for either contents: pad every values array to the larger
+    for a, b in zip(ca, cb):
+        if a.values is not None and b.values is not None and b.values.nbytes > a.values.nbytes:
+            a.values = np.concatenate([a.values, np.zeros(b.values.nbytes - a.values.nbytes, np.uint8).view(a.values.dtype)])
+    da = to_device(ca)
+    arr = native.column_array(da)
+    ws = torch.empty(enc.plan.encode_workspace_bytes(arr, 400), dtype=torch.uint8, device="cuda")
+    ws2 = torch.empty_like(ws)
+    out, _ = _native_encode(enc, da, 400, 1, ws)
+    expect_a, _ = oracle.encode(schema, ca, 400, 1)
+    assert np.array_equal(out.cpu().numpy(), expect_a)
+    # refill A in place with B's contents
+    for d, b in zip(da, cb):
+        for name in ("values", "offsets", "validity"):
+            t, h = getattr(d, name), getattr(b, name)
+            if t is not None and h is not None:
+                src = torch.from_numpy(np.ascontiguousarray(h).view(np.uint8).copy()).cuda()
+                t.view(torch.uint8)[:src.numel()].copy_(src)
+    _, offs_b = _native_encode(enc, da, 400, 1, ws2)  # sizes of the refilled columns, elsewhere
+    out, _ = _native_encode(enc, da, 400, 1, ws, offs_from=offs_b)
+    expect_b, _ = oracle.encode(schema, cb, 400, 1)
+    assert np.array_equal(out.cpu().numpy(), expect_b)
+
+
+def test_short_item_column_is_an_error_not_a_shorter_array():
+    """An item column whose fory_column.length is shorter than its list's offsets reach:
+    encode reports FORY_ERR_INVALID_ARGUMENT (the items were dropped with
+    FORY_OK), decode reports FORY_ERR_CAPACITY and writes nothing past the column."""
+    schema = nested_schemas()["holder"]
+    enc = RowEncoder(schema)
+    rows = random_rows(schema, 300, 43)
+    cols = build_columns(schema, rows)
+    dcols = to_device(cols)
+    p = enc.plan
+    # the deepest list-item column with items: shorten its length by one
+    kinds = [f for f in _preorder_fields(schema)]
+    items = [i for i, f in enumerate(kinds) if i > 0 and kinds[i - 1].type.id == 25 and cols[i].length > 1]
+    assert items
+    it = items[0]
+    short = [native.DeviceColumn(c.values, c.offsets, c.validity, c.length) for c in dcols]
+    short[it] = native.DeviceColumn(dcols[it].values, dcols[it].offsets, dcols[it].validity, cols[it].length - 1)
+    arr = native.column_array(short)
+    ws = torch.empty(p.encode_workspace_bytes(arr, 300), dtype=torch.uint8, device="cuda")
+    offs = torch.empty(301, dtype=torch.int64, device="cuda")
+    native.encoded_size(p, arr, 300, 0, offs, ws)
+    total = int(offs[300].item())
+    out = torch.empty(max(16, total), dtype=torch.uint8, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    native.encode(p, arr, 300, 0, offs, out, status, ws)
+    with pytest.raises(errors.IllegalArgumentException):  # FORY_ERR_INVALID_ARGUMENT
+        native.read_status(status)
+    # decode into output columns whose item column is one short, with a guard behind it
+    good = enc.encode(dcols, 300, 0)
+    outc = enc.decode(good)
+    guard = torch.full((4096,), 0x5A, dtype=torch.uint8, device="cuda")
+    oc = list(outc)
+    w = outc[it].values.element_size() if outc[it].values is not None else 0
+    if w:
+        buf = torch.cat([outc[it].values.view(torch.uint8)[:(cols[it].length - 1) * w], guard])
+        oc[it] = native.DeviceColumn(buf.view(outc[it].values.dtype) if w in (1, 2, 4, 8) else buf, outc[it].offsets,
+                                     outc[it].validity, cols[it].length - 1)
+    else:
+        oc[it] = native.DeviceColumn(outc[it].values, outc[it].offsets, outc[it].validity, cols[it].length - 1)
+    darr = native.column_array(oc)
+    dws = torch.empty(max(p.decode_workspace_bytes(darr, 300), 1 << 20), dtype=torch.uint8, device="cuda")
+    status.zero_()
+    native.decode_sizes(p, good.buffer, good.offsets, 300, 0, darr, status, dws)
+    native.decode(p, good.buffer, good.offsets, 300, 0, darr, status, dws)
+    with pytest.raises(errors.IndexOutOfBoundsException):  # FORY_ERR_CAPACITY
+        native.read_status(status)
+    if w:
+        assert bool((buf[(cols[it].length - 1) * w:] == 0x5A).all())
+
+
+def _preorder_fields(schema):
+    out = []
+
+    def walk(f):
+        out.append(f)
+        for c in f.children:
+            walk(c)
+
+    for f in schema.fields:
+        walk(f)
+    return out
