@@ -113,6 +113,7 @@ LaunchKnobs knobs_from_env() {
   k.idx_frames = num("FORY_ROWFMT_IDXFRAMES", 0);
   k.prof = num("FORY_ROWFMT_VARPROF", 0) != 0;
   k.diag = set("FORY_ROWFMT_VARDIAG");
+  k.var_enc = num("FORY_ROWFMT_VARENC", 0);
   k.tree_col = num("FORY_ROWFMT_TREECOL", 1);
   return k;
 }

@@ -145,6 +145,7 @@ struct Node {
 //   FORY_ROWFMT_SIZES_PROGRAM  sizes by the op-program walk for flat plans too
 //   FORY_ROWFMT_IDXFRAMES   frames per frame-index chunk
 //   FORY_ROWFMT_VARPROF=1   phase timeline (debug), FORY_ROWFMT_VARDIAG=1 LDS sizing to stderr
+//   FORY_ROWFMT_VARENC=1    flat plans encode with the round-3 tile kernel instead of encode v7
 struct LaunchKnobs {
   int32_t no_tiles;
   int32_t no_flat;
@@ -157,7 +158,7 @@ struct LaunchKnobs {
   int32_t idx_frames;
   int32_t prof;
   int32_t diag;
-  int32_t pad;
+  int32_t var_enc;   // FORY_ROWFMT_VARENC=1: flat plans keep the round-3 encode tile kernel (A/B), else encode v7
   int32_t tree_col;  // FORY_ROWFMT_TREECOL: 0 = tree-engine encode per lane only; else the columnar engine when the workspace allows
 };
 LaunchKnobs knobs_from_env();

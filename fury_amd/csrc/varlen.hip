@@ -1745,6 +1745,254 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(5, 8)))
 }
 #undef FORY_VAR_ENC_PARAMS
 
+// ---------------------------------------------------------------------------
+// Encode v7: flat plans (fixed fields, strings / binary, list<fixed>; no nested
+// struct fields), one global round trip before the payload copies.
+//
+// The tile kernel above is latency-bound: its tile runs a chain of
+// dependent global round trips (row bounds -> wave 0's layout loads -> fixed batches
+// -> the var spans, field after field per wave) separated by barriers, ~16 us per
+// Mixed tile at 4 tiles per CU. Here every wave issues ALL of its loads at once --
+// the row bounds, the Arrow offsets and validity of the var fields it owns
+// (v = wave + k*NW), its first fixed-field batch -- and right after they land it
+// puts every owned field's tile span in flight (LDS-DMA into its staging slot).
+// The layout needs no walk: each wave writes its fields' padded payload sizes and
+// null bits to LDS tables, one barrier, and every wave derives its fields' positions
+// (BinaryWriter.writeUnaligned appends in field order: the fixed part plus the sizes
+// of the var fields before it) from the table. Chain per tile: bounds + columns ->
+// spans (overlapping the slot fills) -> copies -> barrier -> 16-B stores.
+// Bytes are those of var_encode_flat_kernel (BinaryRowWriter.java:76-84 reset,
+// BinaryWriter.java:106-194 write/writeUnaligned, BinaryArrayWriter.java:93-118 reset).
+// ---------------------------------------------------------------------------
+constexpr int kOwnVar = 4;  // var fields a wave owns: plans with num_var <= kOwnVar * NW
+
+// Fixed-field batch j of the width-sorted table (groups 8, 4, 2, 1 bytes; kFixBatch
+// fields per batch, numbered across the groups): fields [k0, k1) of width w.
+__device__ __forceinline__ bool fix_batch(const VarLaunch& L, int j, int* k0, int* k1, int* w) {
+  for (int g = 0; g < 4; ++g) {
+    const int a = L.fix_group[g], b = L.fix_group[g + 1];
+    const int nb = (b - a + kFixBatch - 1) / kFixBatch;
+    if (j < nb) {
+      *k0 = a + j * kFixBatch;
+      *k1 = *k0 + kFixBatch < b ? *k0 + kFixBatch : b;
+      *w = 8 >> g;
+      return true;
+    }
+    j -= nb;
+  }
+  return false;
+}
+
+struct FixRegs {
+  uint64_t v[kFixBatch];
+  uint32_t vb[kFixBatch];
+};
+
+// The batch's values and validity bytes of record ii, all loads issued together.
+__device__ __forceinline__ void fix_load(const FixedFieldDev* __restrict__ fix, int k0, int k1, int w, int64_t ii,
+                                         FixRegs& R) {
+#pragma unroll
+  for (int k = 0; k < kFixBatch; ++k) {
+    const FixedFieldDev& f = fix[k0 + k < k1 ? k0 + k : k1 - 1];
+    R.v[k] = load_elem(f.values, w, ii);
+    R.vb[k] = f.validity ? load_byte(f.validity + (ii >> 3)) : 0xffu;
+  }
+}
+
+// BinaryRowWriter.write(ordinal, v) into the row image's slots (zero-extended; a null
+// value writes 0 and sets its bit in the record's bitmap words, BinaryWriter.setNullAt).
+__device__ __forceinline__ void fix_store(const FixedFieldDev* __restrict__ fix, int k0, int k1, const FixRegs& R,
+                                          bool live, int64_t ii, uint8_t* slots, uint32_t* bmrow) {
+#pragma unroll
+  for (int k = 0; k < kFixBatch; ++k) {
+    if (k0 + k >= k1 || !live) continue;
+    const FixedFieldDev& f = fix[k0 + k];
+    const bool valid = (R.vb[k] >> (ii & 7)) & 1;
+    uint64_t x = valid ? R.v[k] : 0;
+    if (f.flags & 2) x = x ? 1 : 0;
+    st64_lds(slots + 8 * f.slot, x);
+    if (!valid) atomicOr(bmrow + (f.slot >> 5), 1u << (f.slot & 31));
+  }
+}
+
+template <int HDR, int NW>
+__global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, const Op* __restrict__ prog,
+                                                                   const ColumnDev* __restrict__ cols,
+                                                                   const FixedFieldDev* __restrict__ fix,
+                                                                   const VarFieldDev* __restrict__ vf,
+                                                                   const int64_t* __restrict__ offs,
+                                                                   uint8_t* __restrict__ out, int64_t capacity,
+                                                                   int32_t* status, int cap, int slot, SpillArgs sp) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* img = lds;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint8_t* stg = lds + cap + wave * slot;                                      // this wave's staging
+  int32_t* sz = reinterpret_cast<int32_t*>(lds + cap + NW * slot);             // [num_var][64] payload bytes, -1 null
+  uint32_t* bmt = reinterpret_cast<uint32_t*>(sz + L.num_var * 64);            // [64][bmw] null bits
+  const int bmw = L.bitmap_bytes >> 2;
+  const int64_t tile = blockIdx.x;
+  const int64_t r0 = tile * 64;
+  const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
+  const bool lv = lane < rows;
+  const int64_t i = r0 + lane;
+  const int64_t ii = lv ? i : r0;
+  for (int k = tid; k < 64 * bmw; k += 64 * NW) bmt[k] = 0u;
+  // ---- one round trip: this wave's var fields (offsets, validity), its first fixed
+  // batch and the row bounds, all issued before any is used
+  int32_t e0[kOwnVar], e1[kOwnVar];
+  uint32_t vvb[kOwnVar];
+#pragma unroll
+  for (int k = 0; k < kOwnVar; ++k) {
+    const int v = wave + k * NW;
+    e0[k] = e1[k] = 0;
+    vvb[k] = 0xffu;
+    if (v < L.num_var) {
+      const VarFieldDev& f = vf[v];
+      e0[k] = f.offsets[lv ? i : r0 + rows];  // dead lanes: the tile's end (empty ranges)
+      e1[k] = f.offsets[lv ? i + 1 : r0 + rows];
+      vvb[k] = f.validity ? load_byte(f.validity + (ii >> 3)) : 0xffu;
+    }
+  }
+  int fk0 = 0, fk1 = 0, fw = 8;
+  const bool has_fix = fix_batch(L, wave, &fk0, &fk1, &fw);
+  FixRegs R;
+  if (has_fix) fix_load(fix, fk0, fk1, fw, ii, R);
+  int64_t B0, B1, beg, end;
+  bool live;
+  const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
+  const bool capbad = live && (end > capacity || beg < 0 || end < beg);
+  if (__ballot(capbad)) {  // (every wave sees the same bounds: the whole workgroup leaves)
+    if (wave == 0 && capbad) set_status(status, FORY_ERR_CAPACITY);
+    return;
+  }
+  const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
+  const int64_t total = mis + (B1 - B0);
+  if (!sane || (mis & 3) || total > cap) {
+    if (sane && !(mis & 3) && total <= sp.cap) {  // the big-image spill launch takes it
+      if (tid == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
+      return;
+    }
+    if (wave == 0 && live) enc_record(L, prog, cols, r0 + lane, out + beg, end - beg);
+    return;
+  }
+  uint8_t* fp = img + mis + (int)(beg - B0);
+  uint8_t* row = fp + HDR;
+  uint8_t* slots = row + L.bitmap_bytes;
+  uint32_t* bmrow = bmt + lane * bmw;
+  // ---- owned var fields: payload sizes + null bits to the tables, tile spans in flight
+  int so = 0;
+  int sphase[kOwnVar], svofs[kOwnVar], soff[kOwnVar];
+  int32_t sbase[kOwnVar];
+  bool staged[kOwnVar];
+#pragma unroll
+  for (int k = 0; k < kOwnVar; ++k) {
+    const int v = wave + k * NW;
+    staged[k] = false;
+    sphase[k] = svofs[k] = soff[k] = 0;
+    sbase[k] = 0;
+    if (v >= L.num_var) continue;
+    const VarFieldDev& f = vf[v];
+    const bool valid = (vvb[k] >> (ii & 7)) & 1;
+    const int64_t n = (int64_t)e1[k] - e0[k];
+    const int32_t s = !valid ? -1 : (int32_t)(f.is_list ? 8 + bitmap_bytes(n) + round8(n * f.w) : round8(n));
+    sz[v * 64 + lane] = live ? s : 0;
+    if (live && !valid) atomicOr(bmrow + (f.slot >> 5), 1u << (f.slot & 31));
+    const int32_t E0 = __shfl(e0[k], 0), E1 = __shfl(e1[k], 63);  // lane 0 is live; lane 63's end is the tile's
+    sbase[k] = E0;
+    int64_t need = (int64_t)(E1 - E0) * f.w + 16 + 4 + 16;  // phase + funnel-copy slack + vofs rounding
+    if (f.item_validity) need += ((E1 + 7) >> 3) - ((E0 >> 3) & ~3) + 4;
+    need = (need + 15) & ~int64_t(15);
+    if ((f.iflags & 2) == 0 && E1 > E0 && so + need <= slot) {  // bool items: per lane (0/1 normalised)
+      flat_stage_span(f, E0, E1, lane, stg + so, &sphase[k], &svofs[k]);
+      staged[k] = true;
+      soff[k] = so;
+      so += (int)need;
+    }
+  }
+  // ---- fixed slots: the preloaded batch, then the wave's further batches
+  if (has_fix) fix_store(fix, fk0, fk1, R, live, ii, slots, bmrow);
+  for (int j = wave + NW;; j += NW) {
+    int a, b, w;
+    if (!fix_batch(L, j, &a, &b, &w)) break;
+    FixRegs Q;
+    fix_load(fix, a, b, w, ii, Q);
+    fix_store(fix, a, b, Q, live, ii, slots, bmrow);
+  }
+  __syncthreads();  // every field's payload size and null bits
+  if (wave == 0 && live) {  // Encoders.encode frame header; the bitmap (BinaryRowWriter.reset + setNullAt)
+    if (HDR == 12) {
+      st32(fp, (uint32_t)(end - beg - 4));
+      st64_lds(fp + 4, (uint64_t)L.schema_hash);
+    } else if (HDR == 8) {
+      st64_lds(fp, (uint64_t)L.schema_hash);
+    }
+    for (int b = 0; b < bmw; ++b) st32(row + 4 * b, bmrow[b]);
+  }
+  // positions: the fixed part + the payloads of the var fields before it (field order)
+  int32_t pos[kOwnVar];
+  {
+    int32_t acc = L.fixed_size;
+    int u = 0;
+#pragma unroll
+    for (int k = 0; k < kOwnVar; ++k) {
+      const int v = wave + k * NW;
+      pos[k] = -1;
+      if (v >= L.num_var) continue;
+      for (; u < v; ++u) {
+        const int32_t s = sz[u * 64 + lane];
+        acc += s > 0 ? s : 0;
+      }
+      pos[k] = live && sz[v * 64 + lane] >= 0 ? acc : -1;
+    }
+  }
+  // var slots (offset << 32 | size) and list headers (BinaryArrayWriter.reset(n): [i64 n][zero bitmap])
+#pragma unroll
+  for (int k = 0; k < kOwnVar; ++k) {
+    const int v = wave + k * NW;
+    if (v >= L.num_var || !live) continue;
+    const VarFieldDev& f = vf[v];
+    uint8_t* sl = slots + 8 * f.slot;
+    const int64_t n = (int64_t)e1[k] - e0[k];
+    if (pos[k] < 0) {
+      st64_lds(sl, 0);
+    } else if (!f.is_list) {
+      st64_lds(sl, ((uint64_t)(uint32_t)pos[k] << 32) | (uint32_t)n);
+    } else {
+      const int32_t ahdr = 8 + bitmap_bytes(n);
+      st64_lds(row + pos[k], (uint64_t)n);
+      for (int b = 8; b < ahdr; b += 4) st32(row + pos[k] + b, 0);
+      st64_lds(sl, ((uint64_t)(uint32_t)pos[k] << 32) | (uint32_t)(ahdr + round8(n * f.w)));
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's spans
+  wave_lds_sync();
+#pragma unroll
+  for (int k = 0; k < kOwnVar; ++k) {
+    const int v = wave + k * NW;
+    if (v >= L.num_var) continue;
+    if (live && pos[k] >= 0)
+      flat_place(vf[v], staged[k], stg + soff[k], sphase[k], sbase[k], svofs[k], pos[k], e0[k],
+                 (int64_t)e1[k] - e0[k], row);
+  }
+  __syncthreads();
+  uint8_t* g = out + B0 - mis;  // 16-byte aligned
+  const int tot = (int)total;
+  const int nch = (tot + 15) >> 4;
+  for (int cc = tid; cc < nch; cc += 64 * NW) {
+    const int lo = cc * 16;
+    if (lo >= mis && lo + 16 <= tot) {
+      *gp(reinterpret_cast<u32x4*>(g + lo)) = *reinterpret_cast<const u32x4*>(img + lo);
+    } else {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int o = lo + 4 * d;
+        if (o >= mis && o + 4 <= tot) *gp(reinterpret_cast<uint32_t*>(g + o)) = ld32(img + o);
+      }
+    }
+  }
+}
+
 
 __device__ __forceinline__ int64_t wave_incl_scan64(int64_t x, int lane) {
 #pragma unroll
@@ -2422,12 +2670,57 @@ void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, i
                      sp);
 }
 
+// Encode v7 LDS: row image, NW staging slots, the payload-size table, the null-bit table.
+size_t flat7_lds(const VarLaunch& L, int cap, int slot, int nw) {
+  return (size_t)cap + (size_t)nw * slot + (size_t)L.num_var * 64 * sizeof(int32_t) +
+         (size_t)64 * (L.bitmap_bytes >> 2) * sizeof(uint32_t);
+}
+
+// Staging slot of a wave in encode v7: the tile spans of the fields it owns at 1.25x
+// the batch's mean var bytes per field (the caller's capacity, normally encoded_size's
+// total, gives the mean row), + per-field slack; 256-B granular, [1, 32] KiB. A field
+// whose span does not fit is copied per lane from global (correct, slower).
+int flat7_slot(const VarLaunch& L, int64_t capacity, int nw) {
+  if (L.kn.var_stg) return L.kn.var_stg;
+  const int own = (L.num_var + nw - 1) / nw;
+  int64_t var_row = L.num_rows > 0 ? capacity / L.num_rows - L.fixed_size - frame_header_bytes(L.frame) : 0;
+  if (var_row < 0) var_row = 0;
+  const int64_t per = L.num_var > 0 ? 64 * var_row / L.num_var : 0;
+  int64_t b = own * (per * 5 / 4 + 64);
+  b = (b + 255) & ~int64_t(255);
+  return (int)(b < 1024 ? 1024 : (b > 32768 ? 32768 : b));
+}
+
+template <int HDR, int NW>
+void launch_flat_enc7(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
+                      int cap, hipStream_t s) {
+  VarLaunch L = L0;
+  L.pl_all = 1;
+  auto* k = &var_encode_flat7_kernel<HDR, NW>;
+  const int slot = flat7_slot(L, capacity, NW);
+  const size_t lds = flat7_lds(L, cap, slot, NW);
+  raise_lds_cap(k);
+  // tiles beyond the image: the tile kernel's big-image spill launch (its own staging)
+  auto* k2 = &var_encode_flat_kernel<HDR, NW, false, true>;
+  L.stg_bytes = enc_stg_bytes(k2, L, capacity, cap, NW);
+  const SpillArgs sp = spill_args(L, cap);
+  (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
+  var_diag(L, "encode v7", k, 64 * NW, cap, slot, lds);
+  hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
+                     L.vf, offs, out, capacity, status, cap, slot, sp);
+  raise_lds_cap(k2);
+  hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds_enc(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
+                     flat_lds_enc(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status,
+                     sp.cap, sp);
+}
+
 template <int HDR, int NW>
 void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                      int cap, hipStream_t s) {
   // plans with nested struct fields and flat ones get their own instantiations: each
   // carries only its layout path (the other one's registers would count against it)
   if (L.num_struct) launch_flat_enc_t<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
+  else if (!L.kn.var_enc && L.num_var <= kOwnVar * NW) launch_flat_enc7<HDR, NW>(L, offs, out, capacity, status, cap, s);
   else launch_flat_enc_t<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
 }
 
