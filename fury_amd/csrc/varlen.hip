@@ -1815,11 +1815,19 @@ __device__ __forceinline__ void fix_store(const FixedFieldDev* __restrict__ fix,
   }
 }
 
-template <int HDR, int NW>
+// NEST: plans with nested struct fields. A struct field's child row is reserved at the
+// writerIndex its field is reached and its var fields follow (BinaryRowWriter(schema,
+// parent), BaseBinaryEncoderBuilder.java:436-490), so positions are a prefix over the
+// program's var fields and struct begins: after the size table, wave 0 walks the program
+// once over LDS values only (no loads) into a position table, zeroes the bitmaps and
+// writes the struct slots; every wave then writes its fields' slots and null bits into
+// the image (null bits by LDS atomics: a bitmap is shared by the fields of its row).
+template <int HDR, int NW, bool NEST>
 __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, const Op* __restrict__ prog,
                                                                    const ColumnDev* __restrict__ cols,
                                                                    const FixedFieldDev* __restrict__ fix,
                                                                    const VarFieldDev* __restrict__ vf,
+                                                                   const StructDev* __restrict__ st,
                                                                    const int64_t* __restrict__ offs,
                                                                    uint8_t* __restrict__ out, int64_t capacity,
                                                                    int32_t* status, int cap, int slot, SpillArgs sp) {
@@ -1828,8 +1836,9 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint8_t* stg = lds + cap + wave * slot;                                      // this wave's staging
-  int32_t* sz = reinterpret_cast<int32_t*>(lds + cap + NW * slot);             // [num_var][64] payload bytes, -1 null
-  uint32_t* bmt = reinterpret_cast<uint32_t*>(sz + L.num_var * 64);            // [64][bmw] null bits
+  int32_t* sz = reinterpret_cast<int32_t*>(lds + cap + NW * slot);             // [num_var][64] payload bytes
+  uint32_t* bmt = reinterpret_cast<uint32_t*>(sz + L.num_var * 64);            // flat: [64][bmw] null bits
+  int32_t* sbs = reinterpret_cast<int32_t*>(sz + L.num_var * 64);              // NEST: [1 + num_struct][64] child rows
   const int bmw = L.bitmap_bytes >> 2;
   const int64_t tile = blockIdx.x;
   const int64_t r0 = tile * 64;
@@ -1837,9 +1846,10 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   const bool lv = lane < rows;
   const int64_t i = r0 + lane;
   const int64_t ii = lv ? i : r0;
-  for (int k = tid; k < 64 * bmw; k += 64 * NW) bmt[k] = 0u;
+  if constexpr (!NEST)
+    for (int k = tid; k < 64 * bmw; k += 64 * NW) bmt[k] = 0u;
   // ---- one round trip: this wave's var fields (offsets, validity), its first fixed
-  // batch and the row bounds, all issued before any is used
+  // batch, the struct validity (NEST) and the row bounds, all issued before any is used
   int32_t e0[kOwnVar], e1[kOwnVar];
   uint32_t vvb[kOwnVar];
 #pragma unroll
@@ -1853,6 +1863,12 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
       e1[k] = f.offsets[lv ? i + 1 : r0 + rows];
       vvb[k] = f.validity ? load_byte(f.validity + (ii >> 3)) : 0xffu;
     }
+  }
+  uint32_t svb[NEST ? kMaxTileStructs : 1];
+  if constexpr (NEST) {
+#pragma unroll
+    for (int s = 0; s < kMaxTileStructs; ++s)
+      svb[s] = s < L.num_struct && (st[s].flags & 1) && st[s].validity ? load_byte(st[s].validity + (ii >> 3)) : 0xffu;
   }
   int fk0 = 0, fk1 = 0, fw = 8;
   const bool has_fix = fix_batch(L, wave, &fk0, &fk1, &fw);
@@ -1880,7 +1896,15 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   uint8_t* row = fp + HDR;
   uint8_t* slots = row + L.bitmap_bytes;
   uint32_t* bmrow = bmt + lane * bmw;
-  // ---- owned var fields: payload sizes + null bits to the tables, tile spans in flight
+  // NEST: structs present in this record (bit s: struct id s, bit 0 the row), pre-order
+  uint32_t pm = 1;
+  if constexpr (NEST) {
+#pragma unroll
+    for (int s = 0; s < kMaxTileStructs; ++s)
+      if (s < L.num_struct && ((svb[s] >> (ii & 7)) & 1) && ((pm >> st[s].parent) & 1)) pm |= 1u << (s + 1);
+  }
+  // ---- owned var fields: payload sizes (-1 null, -2 under an absent struct), null bits
+  // (flat), tile spans in flight
   int so = 0;
   int sphase[kOwnVar], svofs[kOwnVar], soff[kOwnVar];
   int32_t sbase[kOwnVar];
@@ -1894,10 +1918,11 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
     if (v >= L.num_var) continue;
     const VarFieldDev& f = vf[v];
     const bool valid = (vvb[k] >> (ii & 7)) & 1;
+    const bool absent = NEST && !((pm >> f.parent) & 1);
     const int64_t n = (int64_t)e1[k] - e0[k];
-    const int32_t s = !valid ? -1 : (int32_t)(f.is_list ? 8 + bitmap_bytes(n) + round8(n * f.w) : round8(n));
-    sz[v * 64 + lane] = live ? s : 0;
-    if (live && !valid) atomicOr(bmrow + (f.slot >> 5), 1u << (f.slot & 31));
+    const int32_t s = absent ? -2 : !valid ? -1 : (int32_t)(f.is_list ? 8 + bitmap_bytes(n) + round8(n * f.w) : round8(n));
+    sz[v * 64 + lane] = live ? s : -2;
+    if (!NEST && live && !valid) atomicOr(bmrow + (f.slot >> 5), 1u << (f.slot & 31));
     const int32_t E0 = __shfl(e0[k], 0), E1 = __shfl(e1[k], 63);  // lane 0 is live; lane 63's end is the tile's
     sbase[k] = E0;
     int64_t need = (int64_t)(E1 - E0) * f.w + 16 + 4 + 16;  // phase + funnel-copy slack + vofs rounding
@@ -1910,16 +1935,17 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
       so += (int)need;
     }
   }
-  // ---- fixed slots: the preloaded batch, then the wave's further batches
-  if (has_fix) fix_store(fix, fk0, fk1, R, live, ii, slots, bmrow);
-  for (int j = wave + NW;; j += NW) {
-    int a, b, w;
-    if (!fix_batch(L, j, &a, &b, &w)) break;
-    FixRegs Q;
-    fix_load(fix, a, b, w, ii, Q);
-    fix_store(fix, a, b, Q, live, ii, slots, bmrow);
+  if constexpr (!NEST) {  // fixed slots of the row: the preloaded batch, then the wave's further batches
+    if (has_fix) fix_store(fix, fk0, fk1, R, live, ii, slots, bmrow);
+    for (int j = wave + NW;; j += NW) {
+      int a, b, w;
+      if (!fix_batch(L, j, &a, &b, &w)) break;
+      FixRegs Q;
+      fix_load(fix, a, b, w, ii, Q);
+      fix_store(fix, a, b, Q, live, ii, slots, bmrow);
+    }
   }
-  __syncthreads();  // every field's payload size and null bits
+  __syncthreads();  // every field's payload size (flat: and null bits)
   if (wave == 0 && live) {  // Encoders.encode frame header; the bitmap (BinaryRowWriter.reset + setNullAt)
     if (HDR == 12) {
       st32(fp, (uint32_t)(end - beg - 4));
@@ -1927,11 +1953,14 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
     } else if (HDR == 8) {
       st64_lds(fp, (uint64_t)L.schema_hash);
     }
-    for (int b = 0; b < bmw; ++b) st32(row + 4 * b, bmrow[b]);
+    if constexpr (!NEST) {
+      for (int b = 0; b < bmw; ++b) st32(row + 4 * b, bmrow[b]);
+    } else {
+      for (int b = 0; b < bmw; ++b) st32(row + 4 * b, 0u);
+    }
   }
-  // positions: the fixed part + the payloads of the var fields before it (field order)
   int32_t pos[kOwnVar];
-  {
+  if constexpr (!NEST) {  // positions: the fixed part + the payloads of the var fields before it (field order)
     int32_t acc = L.fixed_size;
     int u = 0;
 #pragma unroll
@@ -1945,6 +1974,82 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
       }
       pos[k] = live && sz[v * 64 + lane] >= 0 ? acc : -1;
     }
+  } else {
+    // wave 0: one walk of the program over the size table -> positions (in place of the
+    // sizes: -1 null, -2 absent), child-row starts, zeroed child bitmaps, struct slots
+    // ((offset from the parent row) << 32 | size) and null structs' bits
+    if (wave == 0) {
+      int32_t acc = L.fixed_size;
+      int cur = 0, vi = 0, si = 0;
+      if (lane < 64) sbs[lane] = 0;
+      for (int pc = 0; pc < L.num_ops; ++pc) {
+        const Op op = prog[pc];
+        if (op.code == OP_BYTES || op.code == OP_LIST) {
+          const int32_t s = sz[vi * 64 + lane];
+          sz[vi * 64 + lane] = s >= 0 ? acc : s;
+          acc += s > 0 ? s : 0;
+          ++vi;
+        } else if (op.code == OP_STRUCT_BEGIN) {
+          ++si;
+          cur = si;
+          const StructDev& sd = st[si - 1];
+          int32_t b = -1;
+          if (live && ((pm >> si) & 1)) {
+            b = acc;
+            for (int q = 0; q < sd.hdr; q += 4) st32(row + b + q, 0u);
+            acc += sd.hdr + 8 * sd.nfields;
+          }
+          sbs[si * 64 + lane] = b;
+        } else if (op.code == OP_STRUCT_END) {
+          cur = __builtin_amdgcn_readfirstlane(cur);  // uniform by construction
+          const StructDev& sd = st[cur - 1];
+          const int par = sd.parent;
+          const int32_t pb = sbs[par * 64 + lane];
+          if (live && pb >= 0) {
+            const int32_t ph = par ? st[par - 1].hdr : L.bitmap_bytes;
+            const int32_t b = sbs[cur * 64 + lane];
+            uint8_t* sl = row + pb + ph + 8 * sd.slot;
+            if (b >= 0) {
+              st64_lds(sl, ((uint64_t)(uint32_t)(b - pb) << 32) | (uint32_t)(acc - b));
+            } else {  // a null struct (its parent is present): setNullAt
+              st64_lds(sl, 0);
+              set_null_bit(row + pb, sd.slot);
+            }
+          }
+          cur = par;
+        }
+      }
+    }
+    __syncthreads();  // positions, child rows, zeroed bitmaps
+#pragma unroll
+    for (int k = 0; k < kOwnVar; ++k) {
+      const int v = wave + k * NW;
+      pos[k] = v < L.num_var ? sz[v * 64 + lane] : -2;
+    }
+    // fixed fields at their row / child row: value or 0 + null bit (absent: nothing)
+    auto put_fixed = [&](int a, int b, const FixRegs& Q) {
+#pragma unroll
+      for (int k = 0; k < kFixBatch; ++k) {
+        if (a + k >= b || !live) continue;
+        const FixedFieldDev& f = fix[a + k];
+        const int32_t base = sbs[f.parent * 64 + lane];
+        if (base < 0) continue;
+        const int32_t hdr = f.parent ? st[f.parent - 1].hdr : L.bitmap_bytes;
+        const bool valid = (Q.vb[k] >> (ii & 7)) & 1;
+        uint64_t x = valid ? Q.v[k] : 0;
+        if (f.flags & 2) x = x ? 1 : 0;
+        st64_lds(row + base + hdr + 8 * f.slot, x);
+        if (!valid) atomicOr(reinterpret_cast<uint32_t*>(row + base) + (f.slot >> 5), 1u << (f.slot & 31));
+      }
+    };
+    if (has_fix) put_fixed(fk0, fk1, R);
+    for (int j = wave + NW;; j += NW) {
+      int a, b, w;
+      if (!fix_batch(L, j, &a, &b, &w)) break;
+      FixRegs Q;
+      fix_load(fix, a, b, w, ii, Q);
+      put_fixed(a, b, Q);
+    }
   }
   // var slots (offset << 32 | size) and list headers (BinaryArrayWriter.reset(n): [i64 n][zero bitmap])
 #pragma unroll
@@ -1952,17 +2057,24 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
     const int v = wave + k * NW;
     if (v >= L.num_var || !live) continue;
     const VarFieldDev& f = vf[v];
-    uint8_t* sl = slots + 8 * f.slot;
+    int32_t base = 0, hdr = L.bitmap_bytes;
+    if constexpr (NEST) {
+      if (pos[k] == -2) continue;  // under an absent struct
+      base = sbs[f.parent * 64 + lane];
+      if (f.parent) hdr = st[f.parent - 1].hdr;
+    }
+    uint8_t* sl = row + base + hdr + 8 * f.slot;
     const int64_t n = (int64_t)e1[k] - e0[k];
     if (pos[k] < 0) {
       st64_lds(sl, 0);
+      if (NEST) atomicOr(reinterpret_cast<uint32_t*>(row + base) + (f.slot >> 5), 1u << (f.slot & 31));
     } else if (!f.is_list) {
-      st64_lds(sl, ((uint64_t)(uint32_t)pos[k] << 32) | (uint32_t)n);
+      st64_lds(sl, ((uint64_t)(uint32_t)(pos[k] - base) << 32) | (uint32_t)n);
     } else {
       const int32_t ahdr = 8 + bitmap_bytes(n);
       st64_lds(row + pos[k], (uint64_t)n);
       for (int b = 8; b < ahdr; b += 4) st32(row + pos[k] + b, 0);
-      st64_lds(sl, ((uint64_t)(uint32_t)pos[k] << 32) | (uint32_t)(ahdr + round8(n * f.w)));
+      st64_lds(sl, ((uint64_t)(uint32_t)(pos[k] - base) << 32) | (uint32_t)(ahdr + round8(n * f.w)));
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's spans
@@ -2670,10 +2782,12 @@ void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, i
                      sp);
 }
 
-// Encode v7 LDS: row image, NW staging slots, the payload-size table, the null-bit table.
+// Encode v7 LDS: row image, NW staging slots, the payload-size table (NEST: positions),
+// then the null-bit table (flat) or the child-row starts (NEST).
 size_t flat7_lds(const VarLaunch& L, int cap, int slot, int nw) {
-  return (size_t)cap + (size_t)nw * slot + (size_t)L.num_var * 64 * sizeof(int32_t) +
-         (size_t)64 * (L.bitmap_bytes >> 2) * sizeof(uint32_t);
+  const size_t tail = L.num_struct ? (size_t)(1 + L.num_struct) * 64 * sizeof(int32_t)
+                                   : (size_t)64 * (L.bitmap_bytes >> 2) * sizeof(uint32_t);
+  return (size_t)cap + (size_t)nw * slot + (size_t)L.num_var * 64 * sizeof(int32_t) + tail;
 }
 
 // Staging slot of a wave in encode v7: the tile spans of the fields it owns at 1.25x
@@ -2683,7 +2797,8 @@ size_t flat7_lds(const VarLaunch& L, int cap, int slot, int nw) {
 int flat7_slot(const VarLaunch& L, int64_t capacity, int nw) {
   if (L.kn.var_stg) return L.kn.var_stg;
   const int own = (L.num_var + nw - 1) / nw;
-  int64_t var_row = L.num_rows > 0 ? capacity / L.num_rows - L.fixed_size - frame_header_bytes(L.frame) : 0;
+  int64_t var_row =
+      L.num_rows > 0 ? capacity / L.num_rows - L.fixed_size - frame_header_bytes(L.frame) - L.nested_fixed : 0;
   if (var_row < 0) var_row = 0;
   const int64_t per = L.num_var > 0 ? 64 * var_row / L.num_var : 0;
   int64_t b = own * (per * 5 / 4 + 64);
@@ -2691,23 +2806,23 @@ int flat7_slot(const VarLaunch& L, int64_t capacity, int nw) {
   return (int)(b < 1024 ? 1024 : (b > 32768 ? 32768 : b));
 }
 
-template <int HDR, int NW>
+template <int HDR, int NW, bool NEST>
 void launch_flat_enc7(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                       int cap, hipStream_t s) {
   VarLaunch L = L0;
   L.pl_all = 1;
-  auto* k = &var_encode_flat7_kernel<HDR, NW>;
+  auto* k = &var_encode_flat7_kernel<HDR, NW, NEST>;
   const int slot = flat7_slot(L, capacity, NW);
   const size_t lds = flat7_lds(L, cap, slot, NW);
   raise_lds_cap(k);
   // tiles beyond the image: the tile kernel's big-image spill launch (its own staging)
-  auto* k2 = &var_encode_flat_kernel<HDR, NW, false, true>;
+  auto* k2 = &var_encode_flat_kernel<HDR, NW, NEST, true>;
   L.stg_bytes = enc_stg_bytes(k2, L, capacity, cap, NW);
   const SpillArgs sp = spill_args(L, cap);
   (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
   var_diag(L, "encode v7", k, 64 * NW, cap, slot, lds);
   hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
-                     L.vf, offs, out, capacity, status, cap, slot, sp);
+                     L.vf, L.st, offs, out, capacity, status, cap, slot, sp);
   raise_lds_cap(k2);
   hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds_enc(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
                      flat_lds_enc(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status,
@@ -2719,9 +2834,14 @@ void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int6
                      int cap, hipStream_t s) {
   // plans with nested struct fields and flat ones get their own instantiations: each
   // carries only its layout path (the other one's registers would count against it)
-  if (L.num_struct) launch_flat_enc_t<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
-  else if (!L.kn.var_enc && L.num_var <= kOwnVar * NW) launch_flat_enc7<HDR, NW>(L, offs, out, capacity, status, cap, s);
-  else launch_flat_enc_t<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
+  const bool v7 = !L.kn.var_enc && L.num_var <= kOwnVar * NW;
+  if (L.num_struct) {
+    if (v7) launch_flat_enc7<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
+    else launch_flat_enc_t<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
+  } else {
+    if (v7) launch_flat_enc7<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
+    else launch_flat_enc_t<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
+  }
 }
 
 template <int HDR, bool WRITE, int NW>
