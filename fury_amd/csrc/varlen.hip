@@ -2193,14 +2193,21 @@ __device__ __forceinline__ bool flat_var_slot(const VarLaunch& L, const VarField
   return false;
 }
 
-// Fixed fields of width W: slot (LDS) -> column, validity by ballot.
+// Fixed fields of width W: slot (LDS) -> column, validity by ballot. Batches of
+// kDecBatch fields numbered across the width groups from j0; batch j belongs to wave
+// (j + num_var) % NW: the round robin starts after the waves that hold one var field
+// more than the others (v = wave + k NW), so every wave gets about the same number of
+// fields (it was per group from wave 0: Mixed's 32 fixed fields went 16 / 11 / 5 / 0).
+constexpr int kDecBatch = 4;
 template <int W, int NW>
-__device__ __forceinline__ void flat_dec_fixed(const VarLaunch& L, const FixedFieldDev* __restrict__ fix, int g0, int g1, int wave, int lane, bool live,
+__device__ __forceinline__ void flat_dec_fixed(const VarLaunch& L, const FixedFieldDev* __restrict__ fix, int g0, int g1,
+                                               int j0, int wave, int lane, bool live,
                                                bool bad, int64_t i, int64_t r0, int rows, const uint8_t* row,
                                                const StructDev* __restrict__ st, const int32_t* sbase) {
-  for (int k0 = g0 + wave * kFixBatch; k0 < g1; k0 += NW * kFixBatch) {
+  for (int k0 = g0, j = j0; k0 < g1; k0 += kDecBatch, ++j) {
+    if ((j + L.num_var) % NW != wave) continue;
 #pragma unroll
-    for (int k = 0; k < kFixBatch; ++k) {
+    for (int k = 0; k < kDecBatch; ++k) {
       if (k0 + k < g1) {
         const FixedFieldDev& f = fix[k0 + k];
         int32_t hdr;
@@ -2380,10 +2387,19 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   }
   DEC_STAMP(2);
   // fixed fields: slot -> column (UnsafeTrait.getInt32/... ; null -> 0), validity by ballot
-  flat_dec_fixed<8, NW>(L, fix, L.fix_group[0], L.fix_group[1], wave, lane, live, bad, i, r0, rows, row, st, sbase);
-  flat_dec_fixed<4, NW>(L, fix, L.fix_group[1], L.fix_group[2], wave, lane, live, bad, i, r0, rows, row, st, sbase);
-  flat_dec_fixed<2, NW>(L, fix, L.fix_group[2], L.fix_group[3], wave, lane, live, bad, i, r0, rows, row, st, sbase);
-  flat_dec_fixed<1, NW>(L, fix, L.fix_group[3], L.fix_group[4], wave, lane, live, bad, i, r0, rows, row, st, sbase);
+  {
+    int jb[4];
+    jb[0] = 0;
+    for (int g = 0; g < 3; ++g) jb[g + 1] = jb[g] + (L.fix_group[g + 1] - L.fix_group[g] + kDecBatch - 1) / kDecBatch;
+    flat_dec_fixed<8, NW>(L, fix, L.fix_group[0], L.fix_group[1], jb[0], wave, lane, live, bad, i, r0, rows, row, st,
+                          sbase);
+    flat_dec_fixed<4, NW>(L, fix, L.fix_group[1], L.fix_group[2], jb[1], wave, lane, live, bad, i, r0, rows, row, st,
+                          sbase);
+    flat_dec_fixed<2, NW>(L, fix, L.fix_group[2], L.fix_group[3], jb[2], wave, lane, live, bad, i, r0, rows, row, st,
+                          sbase);
+    flat_dec_fixed<1, NW>(L, fix, L.fix_group[3], L.fix_group[4], jb[3], wave, lane, live, bad, i, r0, rows, row, st,
+                          sbase);
+  }
   if (WRITE && L.prof) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   DEC_STAMP(3);
   // var fields: one per wave at a time, output span staged in LDS
@@ -2459,12 +2475,20 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
       const int nch = (tot + 15) >> 4;
       for (int cc = lane; cc < nch; cc += 64) {
         const int lo = cc * 16;
+        const u32x4 c = *reinterpret_cast<const u32x4*>(stg + lo);
         if (lo >= phase && lo + 16 <= tot) {
-          *gp(reinterpret_cast<u32x4*>(g + lo)) = *reinterpret_cast<const u32x4*>(stg + lo);
-        } else {
-          for (int b = 0; b < 16; ++b) {
-            const int o2 = lo + b;
-            if (o2 >= phase && o2 < tot) store_byte(g + o2, stg[o2]);
+          *gp(reinterpret_cast<u32x4*>(g + lo)) = c;
+        } else {  // an edge chunk: its bytes from registers (no LDS read per byte), stores back to back
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const int o = lo + 4 * d;
+            if (o >= phase && o + 4 <= tot) {
+              *gp(reinterpret_cast<uint32_t*>(g + o)) = c[d];
+            } else {
+#pragma unroll
+              for (int b = 0; b < 4; ++b)
+                if (o + b >= phase && o + b < tot) store_byte(g + o + b, (uint8_t)(c[d] >> (8 * b)));
+            }
           }
         }
       }
