@@ -146,6 +146,41 @@ JNIEXPORT jlong JNICALL CLS(nEncodedBytes)(JNIEnv* env, jclass cls, jlong ctx, j
   return (jlong)total;
 }
 
+/* The exact bytes of each <= max_window window of the batch's frames (varlen plans): the
+   device sizes every row (an encode into no room reports the row offsets with
+   FORY_ERR_CAPACITY), fory_rowfmt_split_windows places whole frames greedily. */
+JNIEXPORT jlongArray JNICALL CLS(nWindowBytes)(JNIEnv* env, jclass cls, jlong ctx, jlongArray cols, jint n, jint frame,
+                                               jlong max_window) {
+  (void)cls;
+  int ncol = 0;
+  fory_column* hc = unpack_array(env, cols, &ncol);
+  if (!hc) return NULL;
+  int64_t* offs = (int64_t*)calloc((size_t)n + 1, sizeof(int64_t));
+  int64_t* first = (int64_t*)calloc((size_t)n + 2, sizeof(int64_t));
+  int64_t total = 0;
+  int32_t nw = 0;
+  int rc = offs && first ? fory_rowfmt_host_encode_var(as_ctx(ctx), hc, n, frame, NULL, 0, offs, &total)
+                         : FORY_ERR_DEVICE;
+  if (rc == FORY_ERR_CAPACITY) rc = FORY_OK;  /* sizes only: no room given */
+  if (!rc) rc = fory_rowfmt_split_windows(offs, 0, n, (int64_t)max_window, n > 0 ? n : 1, first, &nw);
+  jlongArray out = NULL;
+  if (!rc) {
+    const int32_t k = nw > 0 ? nw : 1;
+    out = (*env)->NewLongArray(env, k);
+    if (out) {
+      for (int32_t w = 0; w < k; ++w) {
+        const jlong b = nw > 0 ? (jlong)(offs[first[w + 1]] - offs[first[w]]) : 0;
+        (*env)->SetLongArrayRegion(env, out, w, 1, &b);
+      }
+    }
+  }
+  free(hc);
+  free(offs);
+  free(first);
+  if (rc) throw_for(env, rc);
+  return out;
+}
+
 JNIEXPORT void JNICALL CLS(nEncodeWindows)(JNIEnv* env, jclass cls, jlong ctx, jlongArray cols, jint n, jint frame,
                                            jlongArray addrs, jlongArray caps, jlongArray bytes) {
   (void)cls;

@@ -4,6 +4,7 @@
  */
 package org.apache.fory.format.encoder;
 
+import java.nio.ByteBuffer;
 import java.util.ArrayList;
 import java.util.List;
 import org.apache.arrow.vector.types.pojo.Schema;
@@ -32,6 +33,17 @@ import org.apache.fory.util.Preconditions;
  * one {@code Encoders.bean(beanClass)} uses, so field order and schema hash agree. Like a
  * reference encoder, an instance is single-threaded; instances on different threads or
  * devices are independent.
+ *
+ * <p>The object-level surface is {@code Encoder<T>}'s four methods (Encoder.java:31-39)
+ * over a batch of N objects: {@link #encode(MemoryBuffer, List)}, {@link #encode(List)},
+ * {@link #decode(MemoryBuffer, int)}, {@link #decode(byte[][])}. The objects become
+ * columns through {@link BeanColumns} (the generated codec's per-field conversions), so a
+ * caller of {@code Encoders.bean(Foo.class)} swaps one line:
+ *
+ * <pre>{@code
+ * // RowEncoder<Foo> enc = Encoders.bean(Foo.class);  for (Foo f : foos) enc.encode(buf, f);
+ * BatchRowEncoder<Foo> enc = new BatchRowEncoder<>(Foo.class);  enc.encode(buf, foos);
+ * }</pre>
  */
 public final class BatchRowEncoder<T> implements AutoCloseable {
   static {
@@ -45,6 +57,8 @@ public final class BatchRowEncoder<T> implements AutoCloseable {
   public static final int FRAME_HASHED = 3;
 
   private final Schema schema;
+  private final BeanColumns<T> beans; // objects <-> columns
+  private ByteBuffer scratch; // heap MemoryBuffers: staged through this direct buffer
   private final long plan; // fory_plan*
   private final long hostCtx; // fory_host_ctx*: three HIP streams + device chunk slots
   private final long schemaHash;
@@ -57,6 +71,7 @@ public final class BatchRowEncoder<T> implements AutoCloseable {
   /** @param device HIP device ordinal; @param chunkRows records per pipelined chunk */
   public BatchRowEncoder(Class<T> beanClass, int device, long chunkRows) {
     this.schema = TypeInference.inferSchema(beanClass);
+    this.beans = new BeanColumns<>(beanClass, schema);
     this.plan = nPlanCreate(DeviceSchemas.flatten(schema)); // EncoderException / UnsupportedOperation
     this.schemaHash = nSchemaHash(plan);
     this.rowSize = nRowSize(plan);
@@ -72,6 +87,103 @@ public final class BatchRowEncoder<T> implements AutoCloseable {
   public long schemaHash() {
     return schemaHash;
   }
+
+  // ------------------------------------------------------------ Encoder<T> over batches
+
+  /**
+   * N x {@code encode(MemoryBuffer, T)} (Encoders.java:213-225): the N frames {@code [i32
+   * 8+size][i64 hash][row]} appended at the buffer's writerIndex, which ends past them. The
+   * buffer grows as a MemoryBuffer does ({@code ensure}); an off-heap buffer receives the
+   * frames straight from the device, a heap one through a direct staging buffer.
+   * IndexOutOfBoundsException when the frames do not fit an int-sized buffer.
+   */
+  public void encode(MemoryBuffer buffer, List<T> objs) {
+    ColumnBatch cols = new ColumnBatch(schema);
+    beans.fill(objs, cols);
+    appendFrames(buffer, cols, objs.size(), FRAME_STREAM);
+  }
+
+  /** N x {@code encode(T)} (Encoders.java:203-210): one {@code [i64 hash][row]} array each. */
+  public byte[][] encode(List<T> objs) {
+    ColumnBatch cols = new ColumnBatch(schema);
+    beans.fill(objs, cols);
+    return encodeEach(cols, objs.size());
+  }
+
+  /**
+   * N x {@code decode(MemoryBuffer)} (Encoders.java:177-193): N objects from the frames at
+   * the buffer's readerIndex, which ends past them. ClassNotCompatibleException on a
+   * schema-hash mismatch.
+   */
+  public List<T> decode(MemoryBuffer buffer, int numRows) {
+    ColumnBatch out = new ColumnBatch(schema);
+    decode(buffer, numRows, out);
+    return beans.read(out, numRows);
+  }
+
+  /** N x {@code decode(byte[])} (Encoders.java:195-197), one {@code [i64 hash][row]} each. */
+  public List<T> decode(byte[][] each) {
+    int n = each.length;
+    long[] offs = new long[n + 1];
+    for (int i = 0; i < n; i++) offs[i + 1] = offs[i] + each[i].length;
+    if (offs[n] > Integer.MAX_VALUE - 16) {
+      throw new IndexOutOfBoundsException("decode batch of " + offs[n] + " bytes: split the batch");
+    }
+    ByteBuffer buf = scratch(offs[n]);
+    for (byte[] b : each) buf.put(b);
+    long addr = MemoryBuffer.fromByteBuffer(buf).getUnsafeAddress();
+    ColumnBatch out = new ColumnBatch(schema);
+    if (rowSize >= 0) {
+      for (byte[] b : each) {
+        if (b.length != rowSize + 8) throw new EncoderException("row of " + b.length + " bytes, expected " + (rowSize + 8));
+      }
+      nDecodeFixed(hostCtx, addr, offs[n], n, FRAME_HASHED, out);
+    } else {
+      nDecodeInto(hostCtx, addr, offs, n, FRAME_HASHED, out);
+    }
+    return beans.read(out, n);
+  }
+
+  /** The bytes of N frames (fixed-width plans: computed; else a sizing pass on the device). */
+  private long frameBytes(long[] cols, int numRows, int frame) {
+    int hdr = frame == FRAME_STREAM ? 12 : frame == FRAME_HASHED ? 8 : 0;
+    return rowSize >= 0 ? (long) numRows * (rowSize + hdr) : nEncodedBytes(hostCtx, cols, numRows, frame);
+  }
+
+  private void appendFrames(MemoryBuffer buffer, ColumnBatch columns, int numRows, int frame) {
+    long[] cols = columns.addresses();
+    long need = frameBytes(cols, numRows, frame);
+    int at = buffer.writerIndex();
+    if (at + need > Integer.MAX_VALUE - 8) {
+      throw new IndexOutOfBoundsException(
+          "writerIndex " + at + " + " + need + " bytes of frames exceed an int-sized MemoryBuffer");
+    }
+    buffer.ensure((int) (at + need));
+    long[] bytes = new long[1];
+    if (buffer.isOffHeap()) {
+      nEncodeWindows(hostCtx, cols, numRows, frame, new long[] {buffer.getUnsafeAddress() + at}, new long[] {need}, bytes);
+    } else {
+      ByteBuffer tmp = scratch(need);
+      long ta = MemoryBuffer.fromByteBuffer(tmp).getUnsafeAddress();
+      nEncodeWindows(hostCtx, cols, numRows, frame, new long[] {ta}, new long[] {need}, bytes);
+      buffer.copyFromUnsafe(at, null, ta, need);
+    }
+    buffer.writerIndex((int) (at + bytes[0]));
+  }
+
+  /** A direct staging buffer of at least {@code bytes} (kept, grown), position 0. */
+  private ByteBuffer scratch(long bytes) {
+    if (bytes > Integer.MAX_VALUE - 16) {
+      throw new IndexOutOfBoundsException(bytes + " bytes exceed a direct buffer");
+    }
+    if (scratch == null || scratch.capacity() < bytes) {
+      scratch = ByteBuffer.allocateDirect((int) Math.max(bytes + bytes / 4 + 16, 4096));
+    }
+    scratch.clear();
+    return scratch;
+  }
+
+  // ------------------------------------------------------------ column batches
 
   /**
    * N x encode(MemoryBuffer, T). A MemoryBuffer is int-sized (MemoryBuffer.java:87): the
@@ -90,16 +202,22 @@ public final class BatchRowEncoder<T> implements AutoCloseable {
 
   private List<MemoryBuffer> encodeWindows(ColumnBatch columns, int numRows, int frame) {
     long[] cols = columns.addresses();
-    long need =
-        rowSize >= 0
-            ? (long) numRows * (rowSize + (frame == FRAME_STREAM ? 12 : frame == FRAME_HASHED ? 8 : 0))
-            : nEncodedBytes(hostCtx, cols, numRows, frame); // a sizing pass on the device
-    int windows = (int) Math.max(1, (need + Integer.MAX_VALUE - 1) / Integer.MAX_VALUE + 1);
+    long[] sizes; // the exact bytes of each window: whole frames, greedily, <= 2^31 - 1 each
+    if (rowSize >= 0) {
+      long stride = rowSize + (frame == FRAME_STREAM ? 12 : frame == FRAME_HASHED ? 8 : 0);
+      long perWindow = Integer.MAX_VALUE / stride;
+      int windows = (int) Math.max(1, (numRows + perWindow - 1) / perWindow);
+      sizes = new long[windows];
+      for (int w = 0; w < windows; w++) sizes[w] = Math.min(perWindow, numRows - w * perWindow) * stride;
+    } else { // the device sizes the rows, fory_rowfmt_split_windows places them
+      sizes = nWindowBytes(hostCtx, cols, numRows, frame, Integer.MAX_VALUE);
+    }
+    int windows = sizes.length;
     List<MemoryBuffer> out = new ArrayList<>(windows);
     long[] addrs = new long[windows];
     long[] caps = new long[windows];
     for (int w = 0; w < windows; w++) {
-      int cap = (int) Math.min(Integer.MAX_VALUE, Math.max(need, 1));
+      int cap = (int) Math.max(sizes[w], 1);
       MemoryBuffer b = MemoryBuffer.fromByteBuffer(java.nio.ByteBuffer.allocateDirect(cap));
       out.add(b);
       addrs[w] = b.getUnsafeAddress();
@@ -147,6 +265,16 @@ public final class BatchRowEncoder<T> implements AutoCloseable {
    * mismatch (Encoders.java:182-190).
    */
   public void decode(MemoryBuffer in, int numRows, ColumnBatch out) {
+    if (!in.isOffHeap()) { // a heap buffer has no native address: staged through a direct buffer
+      int len = in.remaining();
+      ByteBuffer tmp = scratch(len);
+      in.copyToUnsafe(in.readerIndex(), null, MemoryBuffer.fromByteBuffer(tmp).getUnsafeAddress(), len);
+      tmp.limit(len);
+      MemoryBuffer staged = MemoryBuffer.fromByteBuffer(tmp);
+      decode(staged, numRows, out);
+      in.readerIndex(in.readerIndex() + staged.readerIndex());
+      return;
+    }
     long addr = in.getUnsafeAddress() + in.readerIndex();
     long consumed;
     if (rowSize >= 0) { // fixed width: every frame is rowSize + 12 bytes
@@ -194,6 +322,8 @@ public final class BatchRowEncoder<T> implements AutoCloseable {
   private static native void nHostCtxDestroy(long ctx);
 
   private static native long nEncodedBytes(long ctx, long[] cols, int n, int frame);
+
+  private static native long[] nWindowBytes(long ctx, long[] cols, int n, int frame, long maxWindow);
 
   private static native void nEncodeWindows(
       long ctx, long[] cols, int n, int frame, long[] addrs, long[] caps, long[] bytes);

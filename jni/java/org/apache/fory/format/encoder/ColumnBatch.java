@@ -66,7 +66,9 @@ public final class ColumnBatch {
   }
 
   private boolean hasValues(int i) {
-    return widths[i] > 0 || typeIds[i] == ArrowTypeIds.UTF8 || typeIds[i] == ArrowTypeIds.BINARY;
+    // decimal: Arrow decimal128, 16 bytes per value (getTypeWidth says -1: 32 bytes out of line in a row)
+    return widths[i] > 0 || typeIds[i] == ArrowTypeIds.UTF8 || typeIds[i] == ArrowTypeIds.BINARY
+        || typeIds[i] == ArrowTypeIds.DECIMAL;
   }
 
   /**
@@ -78,7 +80,7 @@ public final class ColumnBatch {
     for (int i = 0; i < typeIds.length; i++) {
       long k = counts[i];
       if (hasValues(i)) {
-        long need = widths[i] > 0 ? k * widths[i] : bytes[i];
+        long need = widths[i] > 0 ? k * widths[i] : typeIds[i] == ArrowTypeIds.DECIMAL ? 16 * k : bytes[i];
         values[i] = grow(values[i], need);
       }
       if (hasOffsets(i)) {
@@ -99,6 +101,18 @@ public final class ColumnBatch {
       return b;
     }
     return ByteBuffer.allocateDirect((int) Math.max(need, 16)).order(ByteOrder.LITTLE_ENDIAN);
+  }
+
+  /**
+   * Column i's buffers and slot count, as BeanColumns built them from beans (direct,
+   * little-endian; validity with at least 4 bytes of slack past its last bit, the device
+   * path reads whole dwords). Buffers a column does not use are dropped.
+   */
+  void set(int i, ByteBuffer v, ByteBuffer o, ByteBuffer valid, long len) {
+    values[i] = hasValues(i) ? v : null;
+    offsets[i] = hasOffsets(i) ? o : null;
+    validity[i] = nullable[i] ? valid : null;
+    length[i] = len;
   }
 
   /** Per column {values, offsets, validity, length, value capacity}: native addresses (0 = none). */
@@ -141,5 +155,6 @@ public final class ColumnBatch {
     static final int BINARY = 14;
     static final int LIST = 25;
     static final int MAP = 30;
+    static final int DECIMAL = 23;
   }
 }

@@ -52,7 +52,7 @@ def test_shim_links_against_the_library(tmp_path):
 def java_natives():
     src = read(os.path.join(JAVA, "BatchRowEncoder.java"))
     out = {}
-    for m in re.finditer(r"private static native \w+ (\w+)\(([^)]*)\);", src, re.S):
+    for m in re.finditer(r"private static native [\w\[\]]+ (\w+)\(([^)]*)\);", src, re.S):
         params = [p for p in m.group(2).split(",") if p.strip()]
         out[m.group(1)] = len(params)
     return out
@@ -93,3 +93,34 @@ def test_integration_points_at_the_sources():
     for f in ("jni/fory_rowfmt_jni.c", "BatchRowEncoder.java", "ColumnBatch.java", "DeviceSchemas.java",
               "tests/test_jni_binding.py"):
         assert f in doc, f
+
+
+def test_encoder_methods_over_batches():
+    """BatchRowEncoder exposes Encoder<T>'s four methods (reference Encoder.java:31-39:
+    decode(MemoryBuffer), decode(byte[]), encode(T), encode(MemoryBuffer, T)) over a batch
+    of N objects, through BeanColumns (objects <-> columns)."""
+    src = read(os.path.join(JAVA, "BatchRowEncoder.java"))
+    for sig in (r"public void encode\(MemoryBuffer \w+, List<T> \w+\)",
+                r"public byte\[\]\[\] encode\(List<T> \w+\)",
+                r"public List<T> decode\(MemoryBuffer \w+, int \w+\)",
+                r"public List<T> decode\(byte\[\]\[\] \w+\)"):
+        assert re.search(sig, src), sig
+    assert "new BeanColumns<>(beanClass, schema)" in src
+    assert "beans.fill(" in src and "beans.read(" in src
+    # no spare full-size window: windows are sized from the frames (exact)
+    assert "nWindowBytes(hostCtx" in src and "Integer.MAX_VALUE - 1) / Integer.MAX_VALUE + 1" not in src
+
+
+def test_bean_columns_conversions():
+    """BeanColumns restates the generated codec's per-field conversions
+    (BaseBinaryEncoderBuilder.serializeFor / deserializeFor) with fory-core's own helpers."""
+    src = read(os.path.join(JAVA, "BeanColumns.java"))
+    for call in ("DateTimeUtils.localDateToDays", "DateTimeUtils.fromJavaDate", "DateTimeUtils.fromJavaTimestamp",
+                 "DateTimeUtils.instantToMicros", "DateTimeUtils.daysToLocalDate", "DateTimeUtils.toJavaDate",
+                 "DateTimeUtils.toJavaTimestamp", "DateTimeUtils.microsToInstant", "Descriptor.getDescriptors",
+                 "FieldAccessor.createAccessor", "Platform.newInstance", "TypeUtils.getElementType",
+                 "TypeUtils.getMapKeyValueType", "unscaledValue()", "name()", "Enum.valueOf"):
+        assert call in src, call
+    batch = read(os.path.join(JAVA, "ColumnBatch.java"))
+    assert re.search(r"void set\(int \w+, ByteBuffer \w+, ByteBuffer \w+, ByteBuffer \w+, long \w+\)", batch)
+    assert "static final int DECIMAL = 23;" in batch
