@@ -1846,6 +1846,16 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   const bool lv = lane < rows;
   const int64_t i = r0 + lane;
   const int64_t ii = lv ? i : r0;
+  // debug timeline (the plan's FORY_ROWFMT_VARPROF=1): thread 0 stamps s_memrealtime at
+  // phase boundaries, waiting for its outstanding memory first (a uniform branch when off)
+#define V7_STAMP(k)                                                                              \
+  do {                                                                                          \
+    if (L.prof) {                                                                               \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                               \
+      if (tid == 0) L.prof[tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                  \
+    }                                                                                           \
+  } while (0)
+  V7_STAMP(0);
   if constexpr (!NEST)
     for (int k = tid; k < 64 * bmw; k += 64 * NW) bmt[k] = 0u;
   // ---- one round trip: this wave's var fields (offsets, validity), its first fixed
@@ -1884,6 +1894,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   }
   const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
   const int64_t total = mis + (B1 - B0);
+  V7_STAMP(1);
   if (!sane || (mis & 3) || total > cap) {
     if (sane && !(mis & 3) && total <= sp.cap) {  // the big-image spill launch takes it
       if (tid == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
@@ -1945,7 +1956,9 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
       fix_store(fix, a, b, Q, live, ii, slots, bmrow);
     }
   }
+  if (L.prof && tid == 0) L.prof[tile * 8 + 2] = __builtin_amdgcn_s_memrealtime();  // (spans in flight)
   __syncthreads();  // every field's payload size (flat: and null bits)
+  if (L.prof && tid == 0) L.prof[tile * 8 + 3] = __builtin_amdgcn_s_memrealtime();
   if (wave == 0 && live) {  // Encoders.encode frame header; the bitmap (BinaryRowWriter.reset + setNullAt)
     if (HDR == 12) {
       st32(fp, (uint32_t)(end - beg - 4));
@@ -2077,8 +2090,10 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
       st64_lds(sl, ((uint64_t)(uint32_t)(pos[k] - base) << 32) | (uint32_t)(ahdr + round8(n * f.w)));
     }
   }
+  if (L.prof && tid == 0) L.prof[tile * 8 + 4] = __builtin_amdgcn_s_memrealtime();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's spans
   wave_lds_sync();
+  if (L.prof && tid == 0) L.prof[tile * 8 + 5] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
   for (int k = 0; k < kOwnVar; ++k) {
     const int v = wave + k * NW;
@@ -2088,6 +2103,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
                  (int64_t)e1[k] - e0[k], row);
   }
   __syncthreads();
+  V7_STAMP(6);
   uint8_t* g = out + B0 - mis;  // 16-byte aligned
   const int tot = (int)total;
   const int nch = (tot + 15) >> 4;
@@ -2103,6 +2119,8 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
       }
     }
   }
+  V7_STAMP(7);
+#undef V7_STAMP
 }
 
 

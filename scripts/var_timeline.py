@@ -31,6 +31,9 @@ lib = _lib.load()
 lib.fory_rowfmt_debug_timeline.restype = ctypes.c_int64
 lib.fory_rowfmt_debug_timeline.argtypes = [ctypes.c_void_p, ctypes.c_int64]
 names = ["bounds+stage0", "wave0 layout", "fixed", "barrier1", "var place", "barrier2", "flush"]
+if os.environ.get("FORY_ROWFMT_VARENC", "0") != "1":  # encode v7's stamps
+    names = ["RT1 (bounds, offsets, fixed)", "sizes+spans issued+fixed slots", "barrier A",
+             "positions+slots (NEST: walk, barrier B)", "span wait", "copies+barrier C", "store (to completion)"]
 for frame in (0, 1):
     offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
     native.encoded_size(plan, arr, n, frame, offs, ws)
