@@ -457,6 +457,13 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   for (const fory_amd::VarFieldDev& v : var) est = std::max(est, v.is_list ? 16 * v.w + 2 : 32);
   L->var_est_row = est;
   L->iv_split = var.size() == 1 && var[0].is_list && var[0].out_item_validity ? 1 : 0;
+  L->num_list = 0;
+  L->list_mask = 0;
+  for (size_t v = 0; v < var.size(); ++v)
+    if (var[v].is_list) {
+      ++L->num_list;
+      if (v < 32) L->list_mask |= 1u << v;
+    }
   L->cols = static_cast<const ColumnDev*>(ws);
   L->prog = reinterpret_cast<const fory_amd::Op*>(static_cast<uint8_t*>(ws) + col_bytes);
   L->num_ops = (int32_t)p.program.size();

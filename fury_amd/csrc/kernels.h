@@ -72,6 +72,8 @@ struct VarLaunch {
   int32_t level2;               // decode lengths pass 2: sizes of string/binary list/map
                                 // elements (container offsets already scanned)
   LaunchKnobs kn;               // the plan's knobs (host-side launch decisions only)
+  int32_t num_list;             // list fields among the var fields
+  uint32_t list_mask;           // bit v: var field v is a list (v < 32)
 };
 
 // sizes -> d_row_offsets[0..n-1] (row/frame byte sizes), then exclusive scan.

@@ -1766,21 +1766,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(5, 8)))
 // ---------------------------------------------------------------------------
 constexpr int kOwnVar = 4;  // var fields a wave owns: plans with num_var <= kOwnVar * NW
 
-// Fixed-field batch j of the width-sorted table (groups 8, 4, 2, 1 bytes; kFixBatch
-// fields per batch, numbered across the groups): fields [k0, k1) of width w.
-__device__ __forceinline__ bool fix_batch(const VarLaunch& L, int j, int* k0, int* k1, int* w) {
-  for (int g = 0; g < 4; ++g) {
-    const int a = L.fix_group[g], b = L.fix_group[g + 1];
-    const int nb = (b - a + kFixBatch - 1) / kFixBatch;
-    if (j < nb) {
-      *k0 = a + j * kFixBatch;
-      *k1 = *k0 + kFixBatch < b ? *k0 + kFixBatch : b;
-      *w = 8 >> g;
-      return true;
-    }
-    j -= nb;
-  }
-  return false;
+// Fixed-field batch j: kFixBatch consecutive fields [k0, k1) of the width-sorted table
+// (widths mixed; each field loads at its own width), so a plan with <= kFixBatch * NW
+// fixed fields gives every wave at most one batch, loaded with the row bounds.
+__device__ __forceinline__ bool fix_batch(const VarLaunch& L, int j, int* k0, int* k1) {
+  const int nf = L.fix_group[4];
+  *k0 = j * kFixBatch;
+  *k1 = *k0 + kFixBatch < nf ? *k0 + kFixBatch : nf;
+  return *k0 < nf;
 }
 
 struct FixRegs {
@@ -1789,12 +1782,12 @@ struct FixRegs {
 };
 
 // The batch's values and validity bytes of record ii, all loads issued together.
-__device__ __forceinline__ void fix_load(const FixedFieldDev* __restrict__ fix, int k0, int k1, int w, int64_t ii,
+__device__ __forceinline__ void fix_load(const FixedFieldDev* __restrict__ fix, int k0, int k1, int64_t ii,
                                          FixRegs& R) {
 #pragma unroll
   for (int k = 0; k < kFixBatch; ++k) {
     const FixedFieldDev& f = fix[k0 + k < k1 ? k0 + k : k1 - 1];
-    R.v[k] = load_elem(f.values, w, ii);
+    R.v[k] = load_elem(f.values, f.width, ii);
     R.vb[k] = f.validity ? load_byte(f.validity + (ii >> 3)) : 0xffu;
   }
 }
@@ -1815,6 +1808,50 @@ __device__ __forceinline__ void fix_store(const FixedFieldDev* __restrict__ fix,
   }
 }
 
+// Strings / binary per lane through registers: 32 output bytes per chunk, from the
+// kStrDw aligned source dwords that hold them at any alignment (each holds a byte of the
+// string, so none lies past the column's end), all loads of a chunk issued together.
+constexpr int kStrDw = 9;
+struct StrRegs {
+  uint32_t d[kStrDw];
+};
+
+__device__ __forceinline__ void str_load(const uint8_t* src, int64_t n, int c, StrRegs& S) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(src) + 32 * c;
+  const int sb = (int)(a & 3);
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(a - sb);
+  const int64_t left = n - 32 * c;
+  const int nd = left <= 0 ? 0 : (int)((sb + (left < 32 ? left : 32) + 3) >> 2);
+#pragma unroll
+  for (int q = 0; q < kStrDw; ++q) S.d[q] = q < nd ? *gp(p + q) : 0u;
+}
+
+// Chunk c of writeUnaligned + zeroOutPaddingBytes (BinaryWriter.java:117-121,162-194):
+// the string's bytes [32c, 32c + 32), zeros past n, the dwords inside round8(n), to the
+// 4-byte aligned LDS image at dst.
+__device__ __forceinline__ void str_store(uint8_t* dst, const uint8_t* src, int64_t n, int c, const StrRegs& S) {
+  const int sb = (int)((reinterpret_cast<uintptr_t>(src) + 32 * c) & 3);
+  const int64_t left = n - 32 * c;
+  const int64_t outb = round8(n) - 32 * c;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if (4 * q < outb) {
+      uint32_t w = sb ? funnel(S.d[q], S.d[q + 1], sb) : S.d[q];
+      const int64_t valid = left - 4 * q;
+      if (valid <= 0) w = 0u;
+      else if (valid < 4) w &= (1u << (8 * valid)) - 1u;
+      st32(dst + 32 * c + 4 * q, w);
+    }
+  }
+}
+
+// List fields owned by wave w of nw (var field v belongs to wave v % nw): a bit mask.
+__host__ __device__ __forceinline__ uint32_t flat7_wave_lists(uint32_t list_mask, int w, int nw) {
+  uint32_t m = 0;
+  for (int v = w; v < 32; v += nw) m |= list_mask & (1u << v);
+  return m;
+}
+
 // NEST: plans with nested struct fields. A struct field's child row is reserved at the
 // writerIndex its field is reached and its var fields follow (BinaryRowWriter(schema,
 // parent), BaseBinaryEncoderBuilder.java:436-490), so positions are a prefix over the
@@ -1822,7 +1859,10 @@ __device__ __forceinline__ void fix_store(const FixedFieldDev* __restrict__ fix,
 // once over LDS values only (no loads) into a position table, zeroes the bitmaps and
 // writes the struct slots; every wave then writes its fields' slots and null bits into
 // the image (null bits by LDS atomics: a bitmap is shared by the fields of its row).
-template <int HDR, int NW, bool NEST>
+// OWN: var fields per wave (2 or kOwnVar): registers for what the plan needs.
+// Strings go lane by lane through registers (no staging LDS: the image alone sets the
+// residency); lists (items + item validity) are staged per tile span by LDS-DMA.
+template <int HDR, int NW, bool NEST, int OWN>
 __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, const Op* __restrict__ prog,
                                                                    const ColumnDev* __restrict__ cols,
                                                                    const FixedFieldDev* __restrict__ fix,
@@ -1835,8 +1875,15 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   uint8_t* img = lds;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint8_t* stg = lds + cap + wave * slot;                                      // this wave's staging
-  int32_t* sz = reinterpret_cast<int32_t*>(lds + cap + NW * slot);             // [num_var][64] payload bytes
+  // list staging: one slot per wave that owns a list field, in wave order
+  int sidx = 0, nslot = 0;
+  for (int w = 0; w < NW; ++w) {
+    const bool owns = (flat7_wave_lists(L.list_mask, w, NW)) != 0;
+    sidx += owns && w < wave;
+    nslot += owns;
+  }
+  uint8_t* stg = lds + cap + sidx * slot;                                      // this wave's list staging
+  int32_t* sz = reinterpret_cast<int32_t*>(lds + cap + nslot * slot);          // [num_var][64] payload bytes
   uint32_t* bmt = reinterpret_cast<uint32_t*>(sz + L.num_var * 64);            // flat: [64][bmw] null bits
   int32_t* sbs = reinterpret_cast<int32_t*>(sz + L.num_var * 64);              // NEST: [1 + num_struct][64] child rows
   const int bmw = L.bitmap_bytes >> 2;
@@ -1860,10 +1907,10 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
     for (int k = tid; k < 64 * bmw; k += 64 * NW) bmt[k] = 0u;
   // ---- one round trip: this wave's var fields (offsets, validity), its first fixed
   // batch, the struct validity (NEST) and the row bounds, all issued before any is used
-  int32_t e0[kOwnVar], e1[kOwnVar];
-  uint32_t vvb[kOwnVar];
+  int32_t e0[OWN], e1[OWN];
+  uint32_t vvb[OWN];
 #pragma unroll
-  for (int k = 0; k < kOwnVar; ++k) {
+  for (int k = 0; k < OWN; ++k) {
     const int v = wave + k * NW;
     e0[k] = e1[k] = 0;
     vvb[k] = 0xffu;
@@ -1880,13 +1927,20 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
     for (int s = 0; s < kMaxTileStructs; ++s)
       svb[s] = s < L.num_struct && (st[s].flags & 1) && st[s].validity ? load_byte(st[s].validity + (ii >> 3)) : 0xffu;
   }
-  int fk0 = 0, fk1 = 0, fw = 8;
-  const bool has_fix = fix_batch(L, wave, &fk0, &fk1, &fw);
+  int fk0 = 0, fk1 = 0;
+  const bool has_fix = fix_batch(L, wave, &fk0, &fk1);
   FixRegs R;
-  if (has_fix) fix_load(fix, fk0, fk1, fw, ii, R);
+  if (has_fix) fix_load(fix, fk0, fk1, ii, R);
   int64_t B0, B1, beg, end;
   bool live;
   const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
+  // strings: the first 32 bytes of each owned field in flight now (they need only e0, e1)
+  StrRegs S[OWN];
+#pragma unroll
+  for (int k = 0; k < OWN; ++k) {
+    const int v = wave + k * NW;
+    if (v < L.num_var && !vf[v].is_list) str_load(vf[v].values + e0[k], (int64_t)e1[k] - e0[k], 0, S[k]);
+  }
   const bool capbad = live && (end > capacity || beg < 0 || end < beg);
   if (__ballot(capbad)) {  // (every wave sees the same bounds: the whole workgroup leaves)
     if (wave == 0 && capbad) set_status(status, FORY_ERR_CAPACITY);
@@ -1915,13 +1969,13 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
       if (s < L.num_struct && ((svb[s] >> (ii & 7)) & 1) && ((pm >> st[s].parent) & 1)) pm |= 1u << (s + 1);
   }
   // ---- owned var fields: payload sizes (-1 null, -2 under an absent struct), null bits
-  // (flat), tile spans in flight
+  // (flat), list tile spans in flight
   int so = 0;
-  int sphase[kOwnVar], svofs[kOwnVar], soff[kOwnVar];
-  int32_t sbase[kOwnVar];
-  bool staged[kOwnVar];
+  int sphase[OWN], svofs[OWN], soff[OWN];
+  int32_t sbase[OWN];
+  bool staged[OWN];
 #pragma unroll
-  for (int k = 0; k < kOwnVar; ++k) {
+  for (int k = 0; k < OWN; ++k) {
     const int v = wave + k * NW;
     staged[k] = false;
     sphase[k] = svofs[k] = soff[k] = 0;
@@ -1934,6 +1988,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
     const int32_t s = absent ? -2 : !valid ? -1 : (int32_t)(f.is_list ? 8 + bitmap_bytes(n) + round8(n * f.w) : round8(n));
     sz[v * 64 + lane] = live ? s : -2;
     if (!NEST && live && !valid) atomicOr(bmrow + (f.slot >> 5), 1u << (f.slot & 31));
+    if (!f.is_list) continue;
     const int32_t E0 = __shfl(e0[k], 0), E1 = __shfl(e1[k], 63);  // lane 0 is live; lane 63's end is the tile's
     sbase[k] = E0;
     int64_t need = (int64_t)(E1 - E0) * f.w + 16 + 4 + 16;  // phase + funnel-copy slack + vofs rounding
@@ -1949,10 +2004,10 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   if constexpr (!NEST) {  // fixed slots of the row: the preloaded batch, then the wave's further batches
     if (has_fix) fix_store(fix, fk0, fk1, R, live, ii, slots, bmrow);
     for (int j = wave + NW;; j += NW) {
-      int a, b, w;
-      if (!fix_batch(L, j, &a, &b, &w)) break;
+      int a, b;
+      if (!fix_batch(L, j, &a, &b)) break;
       FixRegs Q;
-      fix_load(fix, a, b, w, ii, Q);
+      fix_load(fix, a, b, ii, Q);
       fix_store(fix, a, b, Q, live, ii, slots, bmrow);
     }
   }
@@ -1972,12 +2027,12 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
       for (int b = 0; b < bmw; ++b) st32(row + 4 * b, 0u);
     }
   }
-  int32_t pos[kOwnVar];
+  int32_t pos[OWN];
   if constexpr (!NEST) {  // positions: the fixed part + the payloads of the var fields before it (field order)
     int32_t acc = L.fixed_size;
     int u = 0;
 #pragma unroll
-    for (int k = 0; k < kOwnVar; ++k) {
+    for (int k = 0; k < OWN; ++k) {
       const int v = wave + k * NW;
       pos[k] = -1;
       if (v >= L.num_var) continue;
@@ -1994,7 +2049,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
     if (wave == 0) {
       int32_t acc = L.fixed_size;
       int cur = 0, vi = 0, si = 0;
-      if (lane < 64) sbs[lane] = 0;
+      sbs[lane] = 0;
       for (int pc = 0; pc < L.num_ops; ++pc) {
         const Op op = prog[pc];
         if (op.code == OP_BYTES || op.code == OP_LIST) {
@@ -2035,7 +2090,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
     }
     __syncthreads();  // positions, child rows, zeroed bitmaps
 #pragma unroll
-    for (int k = 0; k < kOwnVar; ++k) {
+    for (int k = 0; k < OWN; ++k) {
       const int v = wave + k * NW;
       pos[k] = v < L.num_var ? sz[v * 64 + lane] : -2;
     }
@@ -2057,16 +2112,17 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
     };
     if (has_fix) put_fixed(fk0, fk1, R);
     for (int j = wave + NW;; j += NW) {
-      int a, b, w;
-      if (!fix_batch(L, j, &a, &b, &w)) break;
+      int a, b;
+      if (!fix_batch(L, j, &a, &b)) break;
       FixRegs Q;
-      fix_load(fix, a, b, w, ii, Q);
+      fix_load(fix, a, b, ii, Q);
       put_fixed(a, b, Q);
     }
   }
-  // var slots (offset << 32 | size) and list headers (BinaryArrayWriter.reset(n): [i64 n][zero bitmap])
+  // var slots (offset << 32 | size), list headers (BinaryArrayWriter.reset(n): [i64 n][zero
+  // bitmap]) and the strings' first chunks (already in registers)
 #pragma unroll
-  for (int k = 0; k < kOwnVar; ++k) {
+  for (int k = 0; k < OWN; ++k) {
     const int v = wave + k * NW;
     if (v >= L.num_var || !live) continue;
     const VarFieldDev& f = vf[v];
@@ -2083,6 +2139,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
       if (NEST) atomicOr(reinterpret_cast<uint32_t*>(row + base) + (f.slot >> 5), 1u << (f.slot & 31));
     } else if (!f.is_list) {
       st64_lds(sl, ((uint64_t)(uint32_t)(pos[k] - base) << 32) | (uint32_t)n);
+      str_store(row + pos[k], f.values + e0[k], n, 0, S[k]);
     } else {
       const int32_t ahdr = 8 + bitmap_bytes(n);
       st64_lds(row + pos[k], (uint64_t)n);
@@ -2090,14 +2147,27 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
       st64_lds(sl, ((uint64_t)(uint32_t)(pos[k] - base) << 32) | (uint32_t)(ahdr + round8(n * f.w)));
     }
   }
+  // strings longer than 32 bytes: their further chunks (a round trip each)
+#pragma unroll
+  for (int k = 0; k < OWN; ++k) {
+    const int v = wave + k * NW;
+    if (v >= L.num_var || vf[v].is_list) continue;
+    const int64_t n = live && pos[k] >= 0 ? (int64_t)e1[k] - e0[k] : 0;
+    const int nc = (int)((n + 31) >> 5);
+    for (int c = 1; __ballot(c < nc); ++c) {
+      StrRegs T;
+      str_load(vf[v].values + e0[k], c < nc ? n : 0, c, T);
+      if (c < nc) str_store(row + pos[k], vf[v].values + e0[k], n, c, T);
+    }
+  }
   if (L.prof && tid == 0) L.prof[tile * 8 + 4] = __builtin_amdgcn_s_memrealtime();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's spans
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's list spans
   wave_lds_sync();
   if (L.prof && tid == 0) L.prof[tile * 8 + 5] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
-  for (int k = 0; k < kOwnVar; ++k) {
+  for (int k = 0; k < OWN; ++k) {
     const int v = wave + k * NW;
-    if (v >= L.num_var) continue;
+    if (v >= L.num_var || !vf[v].is_list) continue;
     if (live && pos[k] >= 0)
       flat_place(vf[v], staged[k], stg + soff[k], sphase[k], sbase[k], svofs[k], pos[k], e0[k],
                  (int64_t)e1[k] - e0[k], row);
@@ -2829,16 +2899,24 @@ void launch_flat_enc_t(const VarLaunch& L0, const int64_t* offs, uint8_t* out, i
 size_t flat7_lds(const VarLaunch& L, int cap, int slot, int nw) {
   const size_t tail = L.num_struct ? (size_t)(1 + L.num_struct) * 64 * sizeof(int32_t)
                                    : (size_t)64 * (L.bitmap_bytes >> 2) * sizeof(uint32_t);
-  return (size_t)cap + (size_t)nw * slot + (size_t)L.num_var * 64 * sizeof(int32_t) + tail;
+  int nslot = 0;  // waves that own a list field
+  for (int w = 0; w < nw; ++w) nslot += flat7_wave_lists(L.list_mask, w, nw) != 0;
+  return (size_t)cap + (size_t)nslot * slot + (size_t)L.num_var * 64 * sizeof(int32_t) + tail;
 }
 
-// Staging slot of a wave in encode v7: the tile spans of the fields it owns at 1.25x
-// the batch's mean var bytes per field (the caller's capacity, normally encoded_size's
-// total, gives the mean row), + per-field slack; 256-B granular, [1, 32] KiB. A field
-// whose span does not fit is copied per lane from global (correct, slower).
+// List staging slot of a wave in encode v7 (strings need none: they go through
+// registers): the tile spans of the list fields it owns at 1.25x the batch's mean bytes
+// per var field (the caller's capacity, normally encoded_size's total, gives the mean row)
+// + slack; 256-B granular, [1, 32] KiB; 0 for plans without list fields. A span that does
+// not fit is copied per lane from global (correct, slower).
 int flat7_slot(const VarLaunch& L, int64_t capacity, int nw) {
+  if (!L.num_list) return 0;
   if (L.kn.var_stg) return L.kn.var_stg;
-  const int own = (L.num_var + nw - 1) / nw;
+  int own = 0;  // list fields of the wave that owns the most
+  for (int w = 0; w < nw; ++w) {
+    const int c = __builtin_popcount(flat7_wave_lists(L.list_mask, w, nw));
+    own = own > c ? own : c;
+  }
   int64_t var_row =
       L.num_rows > 0 ? capacity / L.num_rows - L.fixed_size - frame_header_bytes(L.frame) - L.nested_fixed : 0;
   if (var_row < 0) var_row = 0;
@@ -2848,12 +2926,12 @@ int flat7_slot(const VarLaunch& L, int64_t capacity, int nw) {
   return (int)(b < 1024 ? 1024 : (b > 32768 ? 32768 : b));
 }
 
-template <int HDR, int NW, bool NEST>
+template <int HDR, int NW, bool NEST, int OWN>
 void launch_flat_enc7(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                       int cap, hipStream_t s) {
   VarLaunch L = L0;
   L.pl_all = 1;
-  auto* k = &var_encode_flat7_kernel<HDR, NW, NEST>;
+  auto* k = &var_encode_flat7_kernel<HDR, NW, NEST, OWN>;
   const int slot = flat7_slot(L, capacity, NW);
   const size_t lds = flat7_lds(L, cap, slot, NW);
   raise_lds_cap(k);
@@ -2871,6 +2949,13 @@ void launch_flat_enc7(const VarLaunch& L0, const int64_t* offs, uint8_t* out, in
                      sp.cap, sp);
 }
 
+template <int HDR, int NW, bool NEST>
+void launch_flat_enc7_own(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
+                          int cap, hipStream_t s) {
+  if (L.num_var <= 2 * NW) launch_flat_enc7<HDR, NW, NEST, 2>(L, offs, out, capacity, status, cap, s);
+  else launch_flat_enc7<HDR, NW, NEST, kOwnVar>(L, offs, out, capacity, status, cap, s);
+}
+
 template <int HDR, int NW>
 void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                      int cap, hipStream_t s) {
@@ -2878,10 +2963,10 @@ void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int6
   // carries only its layout path (the other one's registers would count against it)
   const bool v7 = !L.kn.var_enc && L.num_var <= kOwnVar * NW;
   if (L.num_struct) {
-    if (v7) launch_flat_enc7<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
+    if (v7) launch_flat_enc7_own<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
     else launch_flat_enc_t<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
   } else {
-    if (v7) launch_flat_enc7<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
+    if (v7) launch_flat_enc7_own<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
     else launch_flat_enc_t<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
   }
 }
