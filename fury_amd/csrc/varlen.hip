@@ -2441,14 +2441,32 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
      // edge chunks' bytes outside the tile (same 16-B blocks) are never read
     const uint8_t* g = in + B0 - mis;
     const int nch = (int)((total + 15) >> 4);
-    for (int c0 = 0; c0 < nch; c0 += 64 * NW) {
-      const int cc = c0 + tid;
-      if (cc < nch)
-        __builtin_amdgcn_global_load_lds((const GAS void*)(g + (int64_t)cc * 16),
-                                         (__attribute__((address_space(3))) void*)(img + (c0 + wave * 64) * 16), 16,
-                                         0, 2);
+    if (L.kn.dec_regs) {  // A/B: non-temporal 16-B loads into registers, kDecRegs per thread in flight, then LDS
+      constexpr int kDecRegs = 8;
+      const u32x4* g16 = reinterpret_cast<const u32x4*>(g);
+      for (int c0 = 0; c0 < nch; c0 += 64 * NW * kDecRegs) {
+        u32x4 r[kDecRegs];
+#pragma unroll
+        for (int q = 0; q < kDecRegs; ++q) {
+          const int cc = c0 + q * 64 * NW + tid;
+          r[q] = cc < nch ? __builtin_nontemporal_load(gp(g16 + cc)) : u32x4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int q = 0; q < kDecRegs; ++q) {
+          const int cc = c0 + q * 64 * NW + tid;
+          if (cc < nch) *reinterpret_cast<u32x4*>(img + cc * 16) = r[q];
+        }
+      }
+    } else {
+      for (int c0 = 0; c0 < nch; c0 += 64 * NW) {
+        const int cc = c0 + tid;
+        if (cc < nch)
+          __builtin_amdgcn_global_load_lds((const GAS void*)(g + (int64_t)cc * 16),
+                                           (__attribute__((address_space(3))) void*)(img + (c0 + wave * 64) * 16), 16,
+                                           0, 2);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
   DEC_STAMP(1);

@@ -9,9 +9,10 @@ export PYTHONUNBUFFERED=1
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_frames.py tests/test_gpu_nested.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -2 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 for rep in 1 2; do
-  for enc in 0 1; do
+  for enc in 0 1 2; do
     for cfg in mixed40 nested; do
-      FORY_ROWFMT_VARENC=$enc FORY_ROWFMT_VARDIAG=1 timeout -k 10 200 python bench.py --config $cfg --steps 10 --warmup 3 --no-cpu-baseline > $O/ab_${cfg}_enc${enc}_$rep.json 2> $O/ab_${cfg}_enc${enc}_$rep.err
+      # enc 2: encode v7 + the decode staging its rows through registers (FORY_ROWFMT_DECREGS=1)
+      FORY_ROWFMT_DECREGS=$([ $enc -eq 2 ] && echo 1 || echo 0) FORY_ROWFMT_VARENC=$([ $enc -eq 1 ] && echo 1 || echo 0) FORY_ROWFMT_VARDIAG=1 timeout -k 10 200 python bench.py --config $cfg --steps 10 --warmup 3 --no-cpu-baseline > $O/ab_${cfg}_enc${enc}_$rep.json 2> $O/ab_${cfg}_enc${enc}_$rep.err
       rc=$?; [ $rc -eq 0 ] || exit $rc
       python -c "import json,sys; d=json.load(open('$O/ab_${cfg}_enc${enc}_$rep.json')); print('$cfg enc$enc rep$rep', d['value'], d['kernels_ms'])"
     done
