@@ -2531,106 +2531,137 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
     const int64_t e0 = O0 + incl - n;
     if (live) f.out_offsets[i] = (int32_t)e0;
     const int64_t S = (O1 - O0) * w;
-    uint8_t* gdst = f.out_values + O0 * w;
-    const int phase = (int)(reinterpret_cast<uintptr_t>(gdst) & 15);
     const uint8_t* src = row + rel + (islist ? 8 + bitmap_bytes(n) : 0);
-    if ((iflags & 2) == 0 && S >= 0 && S + 32 <= stg_bytes) {
-      if (live && n > 0) {
-        uint8_t* d = stg + phase + (e0 - O0) * w;
-        if (!islist) {
-          lds_copy_any(d, src, (int)n);
-        } else {  // BinaryArray.toXArray; null items (BinaryArray.isNullAt) read as 0
-          const uint8_t* abm = row + rel + 8;
-          if (w == 8 || w == 4) {  // src 4-byte aligned (8-padded row offsets), d w-aligned
-            // a bitmap byte (8 items) at a time: items of a null-free byte move as up to
-            // 16 dwords, all loads before the stores; bytes with nulls item by item
-            for (int64_t j = 0; j < n; j += 8) {
-              const int take = n - j < 8 ? (int)(n - j) : 8;
-              const uint32_t nb = abm[j >> 3] & ((1u << take) - 1u);
-              const uint8_t* sp = src + j * w;
-              uint8_t* dp = d + j * w;
-              if (!nb) {
-                const int nd = take * w / 4;
-                for (int h = 0; h < nd; h += 8) {
-                  uint32_t t[8];
+    // this lane's payload into the staging at d (BinaryArray.toXArray; null items,
+    // BinaryArray.isNullAt, read as 0)
+    auto stage_lane = [&](uint8_t* d) {
+      if (!islist) {
+        lds_copy_any(d, src, (int)n);
+        return;
+      }
+      const uint8_t* abm = row + rel + 8;
+      if (w == 8 || w == 4) {  // src 4-byte aligned (8-padded row offsets), d w-aligned
+        // a bitmap byte (8 items) at a time: items of a null-free byte move as up to
+        // 16 dwords, all loads before the stores; bytes with nulls item by item
+        for (int64_t j = 0; j < n; j += 8) {
+          const int take = n - j < 8 ? (int)(n - j) : 8;
+          const uint32_t nb = abm[j >> 3] & ((1u << take) - 1u);
+          const uint8_t* sp = src + j * w;
+          uint8_t* dp = d + j * w;
+          if (!nb) {
+            const int nd = take * w / 4;
+            for (int h = 0; h < nd; h += 8) {
+              uint32_t t[8];
 #pragma unroll
-                  for (int u = 0; u < 8; ++u) t[u] = h + u < nd ? ld32(sp + 4 * (h + u)) : 0u;
+              for (int u = 0; u < 8; ++u) t[u] = h + u < nd ? ld32(sp + 4 * (h + u)) : 0u;
 #pragma unroll
-                  for (int u = 0; u < 8; ++u)
-                    if (h + u < nd) st32(dp + 4 * (h + u), t[u]);
-                }
-              } else {
-                for (int t = 0; t < take; ++t) {
-                  const bool en = (nb >> t) & 1;
-                  st32(dp + t * w, en ? 0u : ld32(sp + t * w));
-                  if (w == 8) st32(dp + t * w + 4, en ? 0u : ld32(sp + t * w + 4));
-                }
-              }
+              for (int u = 0; u < 8; ++u)
+                if (h + u < nd) st32(dp + 4 * (h + u), t[u]);
             }
           } else {
-            for (int64_t j = 0; j < n; ++j) {
-              const bool en = (abm[j >> 3] >> (j & 7)) & 1;
-              for (int b = 0; b < w; ++b) d[j * w + b] = en ? 0 : src[j * w + b];
+            for (int t = 0; t < take; ++t) {
+              const bool en = (nb >> t) & 1;
+              st32(dp + t * w, en ? 0u : ld32(sp + t * w));
+              if (w == 8) st32(dp + t * w + 4, en ? 0u : ld32(sp + t * w + 4));
             }
           }
         }
-      }
-      wave_lds_sync();
-      uint8_t* g = gdst - phase;
-      const int tot = (int)(phase + S);
-      const int nch = (tot + 15) >> 4;
-      for (int cc = lane; cc < nch; cc += 64) {
-        const int lo = cc * 16;
-        const u32x4 c = *reinterpret_cast<const u32x4*>(stg + lo);
-        if (lo >= phase && lo + 16 <= tot) {
-          *gp(reinterpret_cast<u32x4*>(g + lo)) = c;
-        } else {  // an edge chunk: its bytes from registers (no LDS read per byte), stores back to back
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const int o = lo + 4 * d;
-            if (o >= phase && o + 4 <= tot) {
-              *gp(reinterpret_cast<uint32_t*>(g + o)) = c[d];
-            } else {
-#pragma unroll
-              for (int b = 0; b < 4; ++b)
-                if (o + b >= phase && o + b < tot) store_byte(g + o + b, (uint8_t)(c[d] >> (8 * b)));
-            }
-          }
+      } else {
+        for (int64_t j = 0; j < n; ++j) {
+          const bool en = (abm[j >> 3] >> (j & 7)) & 1;
+          for (int b = 0; b < w; ++b) d[j * w + b] = en ? 0 : src[j * w + b];
         }
       }
-      wave_lds_sync();
-      // the span's item validity, assembled in LDS (staging reused); with one var field
-      // and an idle second wave, that wave does it (below) while this one copies
-      if (islist && f.out_item_validity && !ivs)
-        dec_item_validity(f, O0, O1, e0, n, row + rel + 8, live, lane, reinterpret_cast<uint32_t*>(stg));
-    } else if (live && n > 0) {
+    };
+    // this lane's payload straight to the column (bool items, records beyond the staging)
+    auto lane_global = [&]() {
       if (!islist) {
         copy_out(f.out_values + e0, src, n);
-      } else {
-        const uint8_t* arr = row + rel;
-        for (int64_t j = 0; j < n; ++j) {
-          const bool en = (arr[8 + (j >> 3)] >> (j & 7)) & 1;
-          uint64_t x = 0;
-          if (!en) {
-            const uint8_t* pp = src + j * w;
-            switch (w) {
-              case 8: x = (uint64_t)ld32(pp) | ((uint64_t)ld32(pp + 4) << 32); break;
-              case 4: x = ld32(pp); break;
-              case 2: x = (uint64_t)pp[0] | ((uint64_t)pp[1] << 8); break;
-              default: x = pp[0]; break;
-            }
-          }
-          if (iflags & 2) x = (x & 0xff) ? 1 : 0;
-          store_elem(f.out_values, w, e0 + j, x);
-          if (f.out_item_validity) {
-            const int64_t q = e0 + j;
-            const uint32_t bit = 1u << (q & 31);
-            uint32_t* word = reinterpret_cast<uint32_t*>(f.out_item_validity) + (q >> 5);
-            if (en) atomicAnd(word, ~bit);
-            else atomicOr(word, bit);
+        return;
+      }
+      const uint8_t* arr = row + rel;
+      for (int64_t j = 0; j < n; ++j) {
+        const bool en = (arr[8 + (j >> 3)] >> (j & 7)) & 1;
+        uint64_t x = 0;
+        if (!en) {
+          const uint8_t* pp = src + j * w;
+          switch (w) {
+            case 8: x = (uint64_t)ld32(pp) | ((uint64_t)ld32(pp + 4) << 32); break;
+            case 4: x = ld32(pp); break;
+            case 2: x = (uint64_t)pp[0] | ((uint64_t)pp[1] << 8); break;
+            default: x = pp[0]; break;
           }
         }
+        if (iflags & 2) x = (x & 0xff) ? 1 : 0;
+        store_elem(f.out_values, w, e0 + j, x);
+        if (f.out_item_validity) {
+          const int64_t q = e0 + j;
+          const uint32_t bit = 1u << (q & 31);
+          uint32_t* word = reinterpret_cast<uint32_t*>(f.out_item_validity) + (q >> 5);
+          if (en) atomicAnd(word, ~bit);
+          else atomicOr(word, bit);
+        }
       }
+    };
+    const bool fits_all = S >= 0 && S + 32 <= stg_bytes;
+    if ((iflags & 2) == 0 && S >= 0) {
+      // record groups whose output span fits the staging: the whole tile when it does,
+      // else the longest runs of records from lo (a span beyond the staging once took
+      // the per-item global path for the whole tile: Nested frame streams, whose bigger
+      // image leaves a staging the mean tile span just exceeds, wrote 1.36x the columns)
+      for (int lo = 0; lo < rows;) {
+        int hi = rows;
+        if (!fits_all) {
+          const int64_t base = __shfl(e0, lo);
+          const int64_t ph = (int64_t)(reinterpret_cast<uintptr_t>(f.out_values + base * w) & 15);
+          const bool ok = lane >= lo && lane < rows && ph + (e0 + n - base) * w + 32 <= stg_bytes;
+          const uint64_t m = __ballot(ok) >> lo;  // a prefix of the lanes from lo (e0 + n nondecreasing)
+          hi = lo + (~m == 0 ? 64 - lo : (int)__builtin_ctzll(~m));
+        }
+        if (hi == lo) {  // record lo alone exceeds the staging
+          if (lane == lo && live && n > 0) lane_global();
+          lo = lo + 1;
+          continue;
+        }
+        const bool mine = lane >= lo && lane < hi;
+        const int64_t G0 = __shfl(e0, lo), G1 = __shfl(e0 + n, hi - 1);
+        const int64_t GS = (G1 - G0) * w;
+        uint8_t* gdst = f.out_values + G0 * w;
+        const int phase = (int)(reinterpret_cast<uintptr_t>(gdst) & 15);
+        if (mine && live && n > 0) stage_lane(stg + phase + (e0 - G0) * w);
+        wave_lds_sync();
+        uint8_t* g = gdst - phase;
+        const int tot = (int)(phase + GS);
+        const int nch = (tot + 15) >> 4;
+        for (int cc = lane; cc < nch; cc += 64) {
+          const int lo16 = cc * 16;
+          const u32x4 c = *reinterpret_cast<const u32x4*>(stg + lo16);
+          if (lo16 >= phase && lo16 + 16 <= tot) {
+            *gp(reinterpret_cast<u32x4*>(g + lo16)) = c;
+          } else {  // an edge chunk: its bytes from registers (no LDS read per byte), stores back to back
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              const int o = lo16 + 4 * d;
+              if (o >= phase && o + 4 <= tot) {
+                *gp(reinterpret_cast<uint32_t*>(g + o)) = c[d];
+              } else {
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                  if (o + b >= phase && o + b < tot) store_byte(g + o + b, (uint8_t)(c[d] >> (8 * b)));
+              }
+            }
+          }
+        }
+        wave_lds_sync();
+        // the group's item validity, assembled in LDS (staging reused); with one var field,
+        // a whole-tile span and an idle second wave, that wave does it (below) while this
+        // one copies
+        if (islist && f.out_item_validity && !(ivs && fits_all))
+          dec_item_validity(f, G0, G1, e0, n, row + rel + 8, live && mine, lane, reinterpret_cast<uint32_t*>(stg));
+        lo = hi;
+      }
+    } else if (live && n > 0) {
+      lane_global();
     }
   }
   if (ivs && wave == 1) {  // field 0's item validity (the staged span of wave 0's pass)

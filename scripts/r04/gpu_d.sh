@@ -20,6 +20,12 @@ for rep in 1 2; do
 done
 grep -h "encode" $O/ab_*_1.err | sort | uniq -c
 for cfg in mixed40 nested; do
+  FORY_ROWFMT_VARDIAG=1 timeout -k 10 200 python bench.py --config $cfg --frame --steps 10 --warmup 3 --no-cpu-baseline > $O/frame_${cfg}.json 2> $O/frame_${cfg}.err
+  rc=$?; [ $rc -eq 0 ] || exit $rc
+  python -c "import json,sys; d=json.load(open('$O/frame_${cfg}.json')); print('$cfg frame', d['value'], d['kernels_ms'])"
+  grep -h "decode" $O/frame_${cfg}.err | sort | uniq -c
+done
+for cfg in mixed40 nested; do
   timeout -k 10 200 python scripts/var_timeline.py $cfg > $O/timeline_${cfg}.json 2> $O/timeline_${cfg}.err
   rc=$?; [ $rc -eq 0 ] || { tail -5 $O/timeline_${cfg}.err; exit $rc; }
   python3 -c "
