@@ -115,6 +115,7 @@ LaunchKnobs knobs_from_env() {
   k.diag = set("FORY_ROWFMT_VARDIAG");
   k.var_enc = num("FORY_ROWFMT_VARENC", 0);
   k.dec_regs = num("FORY_ROWFMT_DECREGS", 0);
+  k.dbg_skip = num("FORY_ROWFMT_DBGSKIP", 0);
   k.tree_col = num("FORY_ROWFMT_TREECOL", 1);
   return k;
 }

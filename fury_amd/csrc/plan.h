@@ -159,6 +159,7 @@ struct LaunchKnobs {
   int32_t prof;
   int32_t diag;
   int32_t var_enc;   // FORY_ROWFMT_VARENC=1: flat plans keep the round-3 encode tile kernel (A/B), else encode v7
+  int32_t dbg_skip;  // FORY_ROWFMT_DBGSKIP (debug, timing only; output wrong): 1 = tile kernels stop after their loads, 2 = encode v7 skips its image store
   int32_t dec_regs;  // FORY_ROWFMT_DECREGS=1: varlen decode stages its tile rows through registers, not LDS-DMA (A/B)
   int32_t tree_col;  // FORY_ROWFMT_TREECOL: 0 = tree-engine encode per lane only; else the columnar engine when the workspace allows
 };

@@ -1949,6 +1949,10 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
   const int64_t total = mis + (B1 - B0);
   V7_STAMP(1);
+  if (L.kn.dbg_skip == 1) {  // debug: the loads alone (timing); keep them live
+    if (tid == 0 && B1 == -7) L.prof[0] = (uint64_t)(e0[0] + R.v[0] + S[0].d[0] + (uint32_t)beg);
+    return;
+  }
   if (!sane || (mis & 3) || total > cap) {
     if (sane && !(mis & 3) && total <= sp.cap) {  // the big-image spill launch takes it
       if (tid == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
@@ -2174,6 +2178,10 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   }
   __syncthreads();
   V7_STAMP(6);
+  if (L.kn.dbg_skip == 2) {  // debug: everything but the image store (timing); keep the image live
+    if (tid == 0 && B1 == -7) L.prof[0] = ld32(img);
+    return;
+  }
   uint8_t* g = out + B0 - mis;  // 16-byte aligned
   const int tot = (int)total;
   const int nch = (tot + 15) >> 4;
@@ -2469,6 +2477,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
     }
   }
   __syncthreads();
+  if (WRITE && L.kn.dbg_skip == 1) return;  // debug: the staging alone (timing)
   DEC_STAMP(1);
   const int64_t i = r0 + lane;
   const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
