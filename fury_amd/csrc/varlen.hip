@@ -1903,8 +1903,10 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
     }                                                                                           \
   } while (0)
   V7_STAMP(0);
-  if constexpr (!NEST)
+  if constexpr (!NEST) {  // zeroed before any wave ORs a null bit into it (other waves' words included)
     for (int k = tid; k < 64 * bmw; k += 64 * NW) bmt[k] = 0u;
+    __syncthreads();
+  }
   // ---- one round trip: this wave's var fields (offsets, validity), its first fixed
   // batch, the struct validity (NEST) and the row bounds, all issued before any is used
   int32_t e0[OWN], e1[OWN];
@@ -2199,6 +2201,326 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   }
   V7_STAMP(7);
 #undef V7_STAMP
+}
+
+// ---------------------------------------------------------------------------
+// Encode v8: flat plans without nested structs whose fixed columns are 16-byte aligned.
+// Every global access is a 16-byte-per-lane one where the data allows it:
+//  - fixed columns: the tile's segment of each column (64 x w bytes) read as 16-B chunks,
+//    one 1 KiB wave instruction per 16/w fields (chunk -> field by lane / (4w)), held in
+//    registers until the row positions are known, then scattered into the row image's
+//    slots (BinaryRowWriter.write: zero-extended, null -> 0 + setNullAt);
+//  - strings / lists: each owned field's tile span by LDS-DMA, its bounds (offsets[r0],
+//    offsets[r0 + 64]) loaded first so the span is in flight with the rest;
+//  - the image leaves as aligned 16-B stores.
+// Encode v7's per-lane 4- and 8-byte column loads are what held it at ~3 TB/s of reads
+// (its loads alone, FORY_ROWFMT_DBGSKIP=1: 2.08 ms for Mixed's 6.3 GB of columns).
+// Partial tiles and tiles near the end of the offsets arrays take the per-record path.
+// ---------------------------------------------------------------------------
+constexpr int kFix16 = 4;  // fixed-column 1 KiB instructions per wave held in registers
+
+// Fixed-column instruction j of the width-sorted table: group g (width w = 8 >> g), its
+// first field kf and the group's end; false past the last.
+__device__ __forceinline__ bool fix16_instr(const VarLaunch& L, int j, int* kf, int* kend, int* w) {
+  for (int g = 0; g < 4; ++g) {
+    const int a = L.fix_group[g], b = L.fix_group[g + 1];
+    const int ww = 8 >> g, fpi = 16 / ww;  // fields per 1 KiB instruction
+    const int ni = (b - a + fpi - 1) / fpi;
+    if (j < ni) {
+      *kf = a + j * fpi;
+      *kend = b;
+      *w = ww;
+      return true;
+    }
+    j -= ni;
+  }
+  return false;
+}
+
+// Lane's field of instruction (kf, kend, w): k = kf + lane / (4w); its descriptor by a
+// select over the instruction's <= 16/w fields (scalar loads: no per-lane table gather).
+struct Fix16Lane {
+  const uint8_t* values;
+  const uint8_t* validity;
+  int32_t slot, flags;
+  bool ok;
+  int sub;  // 16-B chunk of the field's 64-record segment
+};
+__device__ __forceinline__ Fix16Lane fix16_lane(const FixedFieldDev* __restrict__ fix, int kf, int kend, int w,
+                                                int lane) {
+  const int lg = w == 8 ? 5 : w == 4 ? 4 : w == 2 ? 3 : 2;  // log2(4w): chunks per field
+  const int fi = lane >> lg;
+  Fix16Lane r;
+  r.sub = lane & ((1 << lg) - 1);
+  r.ok = kf + fi < kend;
+  r.values = fix[kf].values;
+  r.validity = fix[kf].validity;
+  r.slot = fix[kf].slot;
+  r.flags = fix[kf].flags;
+  const int fpi = 16 / w;
+#pragma unroll
+  for (int q = 1; q < 16; ++q) {
+    if (q >= fpi || kf + q >= kend) break;
+    const FixedFieldDev& f = fix[kf + q];
+    if (fi == q) {
+      r.values = f.values;
+      r.validity = f.validity;
+      r.slot = f.slot;
+      r.flags = f.flags;
+    }
+  }
+  return r;
+}
+
+// The 16/W values of a lane's chunk (records sub * 16/W + e) into their rows' slots.
+template <int W>
+__device__ __forceinline__ void fix16_scatter(uint8_t* img, const int32_t* rs, int bm, const Fix16Lane& d,
+                                              const u32x4& c, uint64_t vbits) {
+  constexpr int E = 16 / W;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int rr = d.sub * E + e;
+    uint64_t x;
+    if constexpr (W == 8) {
+      x = ((uint64_t)c[2 * e + 1] << 32) | c[2 * e];
+    } else if constexpr (W == 4) {
+      x = c[e];
+    } else if constexpr (W == 2) {
+      x = (c[e >> 1] >> (16 * (e & 1))) & 0xffffu;
+    } else {
+      x = (c[e >> 2] >> (8 * (e & 3))) & 0xffu;
+    }
+    const bool valid = !d.validity || ((vbits >> rr) & 1);
+    if (!valid) x = 0;
+    if (d.flags & 2) x = x ? 1 : 0;
+    uint8_t* rw = img + rs[rr];
+    st64_lds(rw + bm + 8 * d.slot, x);
+    if (!valid) atomicOr(reinterpret_cast<uint32_t*>(rw) + (d.slot >> 5), 1u << (d.slot & 31));
+  }
+}
+
+template <int HDR, int NW, int OWN>
+__global__ __launch_bounds__(64 * NW) void var_encode_flat8_kernel(VarLaunch L, const Op* __restrict__ prog,
+                                                                   const ColumnDev* __restrict__ cols,
+                                                                   const FixedFieldDev* __restrict__ fix,
+                                                                   const VarFieldDev* __restrict__ vf,
+                                                                   const int64_t* __restrict__ offs,
+                                                                   uint8_t* __restrict__ out, int64_t capacity,
+                                                                   int32_t* status, int cap, int slot, SpillArgs sp) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* img = lds;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint8_t* stg = lds + cap + wave * slot;                                // this wave's span staging
+  int32_t* sz = reinterpret_cast<int32_t*>(lds + cap + NW * slot);       // [num_var][64] payload bytes, -1 null
+  int32_t* rs = sz + L.num_var * 64;                                     // [64] row starts in the image
+  const int64_t tile = blockIdx.x;
+  const int64_t r0 = tile * 64;
+  const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
+  const int64_t i = r0 + lane;
+  if (rows < 64 || r0 + 68 > L.num_rows) {  // the last tiles: per record (offsets read as whole 16-B chunks elsewhere)
+    if (wave == 0 && lane < rows) {
+      const int64_t beg = offs[i], end = offs[i + 1];
+      if (end > capacity || beg < 0 || end < beg) set_status(status, FORY_ERR_CAPACITY);
+      else enc_record(L, prog, cols, i, out + beg, end - beg);
+    }
+    return;
+  }
+  // ---- one round trip. First the span bounds of the owned var fields (used to put the
+  // spans in flight before the rest lands), then their per-record offsets and validity,
+  // the fixed-column chunks and the row bounds
+  int32_t E0[OWN], E1[OWN];
+#pragma unroll
+  for (int k = 0; k < OWN; ++k) {
+    const int v = wave + k * NW;
+    E0[k] = E1[k] = 0;
+    if (v < L.num_var) {
+      E0[k] = vf[v].offsets[r0];
+      E1[k] = vf[v].offsets[r0 + 64];
+    }
+  }
+  int32_t e0[OWN], e1[OWN];
+  uint32_t vvb[OWN];
+#pragma unroll
+  for (int k = 0; k < OWN; ++k) {
+    const int v = wave + k * NW;
+    e0[k] = e1[k] = 0;
+    vvb[k] = 0xffu;
+    if (v < L.num_var) {
+      const VarFieldDev& f = vf[v];
+      e0[k] = f.offsets[i];
+      e1[k] = f.offsets[i + 1];
+      vvb[k] = f.validity ? load_byte(f.validity + (i >> 3)) : 0xffu;
+    }
+  }
+  u32x4 fc[kFix16];
+  uint64_t fv[kFix16];  // the chunk field's validity bits of the tile (nullable fields)
+#pragma unroll
+  for (int q = 0; q < kFix16; ++q) {
+    int kf, kend, w;
+    fc[q] = u32x4{0u, 0u, 0u, 0u};
+    fv[q] = ~0ull;
+    if (!fix16_instr(L, wave + q * NW, &kf, &kend, &w)) continue;
+    const Fix16Lane c = fix16_lane(fix, kf, kend, w, lane);
+    const uint8_t* p = c.values + r0 * w + (c.ok ? c.sub * 16 : 0);
+    fc[q] = __builtin_nontemporal_load(gp(reinterpret_cast<const u32x4*>(p)));
+    if (c.validity) fv[q] = *gp(reinterpret_cast<const uint64_t*>(c.validity + (r0 >> 3)));
+  }
+  const int64_t B0 = offs[r0], B1 = offs[r0 + 64];
+  const int64_t beg = offs[i], end = offs[i + 1];
+  // ---- the spans in flight (their bounds are the first loads: the wait leaves the rest in flight)
+  int so = 0;
+  int sphase[OWN], svofs[OWN], soff[OWN];
+  bool staged[OWN];
+#pragma unroll
+  for (int k = 0; k < OWN; ++k) {
+    const int v = wave + k * NW;
+    staged[k] = false;
+    sphase[k] = svofs[k] = soff[k] = 0;
+    if (v >= L.num_var) continue;
+    const VarFieldDev& f = vf[v];
+    int64_t need = (int64_t)(E1[k] - E0[k]) * f.w + 16 + 4 + 16;  // phase + funnel-copy slack + vofs rounding
+    if (f.item_validity) need += ((E1[k] + 7) >> 3) - ((E0[k] >> 3) & ~3) + 4;
+    need = (need + 15) & ~int64_t(15);
+    if ((f.iflags & 2) == 0 && E1[k] > E0[k] && E1[k] >= E0[k] && so + need <= slot) {
+      flat_stage_span(f, E0[k], E1[k], lane, stg + so, &sphase[k], &svofs[k]);
+      staged[k] = true;
+      soff[k] = so;
+      so += (int)need;
+    }
+  }
+  // ---- row bounds: the tile's rows are one run [B0, B1) of the output
+  const bool inrun = beg >= B0 && end >= beg && end <= B1;
+  const bool capbad = end > capacity || beg < 0 || end < beg;
+  if (__ballot(capbad)) {  // (every wave sees the same bounds: the whole workgroup leaves)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (spans land before the LDS is another workgroup's)
+    if (wave == 0 && capbad) set_status(status, FORY_ERR_CAPACITY);
+    return;
+  }
+  const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
+  const int64_t total = mis + (B1 - B0);
+  const bool sane = __ballot(!inrun) == 0 && ((B0 | B1) & 3) == 0 && B1 >= B0;
+  if (!sane || (mis & 3) || total > cap) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (spans land before the LDS is another workgroup's)
+    if (sane && !(mis & 3) && total <= sp.cap) {      // the big-image spill launch takes it
+      if (tid == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
+      return;
+    }
+    if (wave == 0) enc_record(L, prog, cols, i, out + beg, end - beg);
+    return;
+  }
+  uint8_t* fp = img + mis + (int)(beg - B0);
+  uint8_t* row = fp + HDR;
+  uint8_t* slots = row + L.bitmap_bytes;
+  const int bm = L.bitmap_bytes;
+  // owned var fields: payload sizes (-1 null)
+#pragma unroll
+  for (int k = 0; k < OWN; ++k) {
+    const int v = wave + k * NW;
+    if (v >= L.num_var) continue;
+    const VarFieldDev& f = vf[v];
+    const bool valid = (vvb[k] >> (i & 7)) & 1;
+    const int64_t n = (int64_t)e1[k] - e0[k];
+    sz[v * 64 + lane] = !valid ? -1 : (int32_t)(f.is_list ? 8 + bitmap_bytes(n) + round8(n * f.w) : round8(n));
+  }
+  if (wave == 0) {  // row starts, the frame header, the zeroed bitmap (BinaryRowWriter.reset)
+    rs[lane] = mis + (int)(beg - B0) + HDR;
+    if (HDR == 12) {
+      st32(fp, (uint32_t)(end - beg - 4));
+      st64_lds(fp + 4, (uint64_t)L.schema_hash);
+    } else if (HDR == 8) {
+      st64_lds(fp, (uint64_t)L.schema_hash);
+    }
+    for (int b = 0; b < bm; b += 4) st32(row + b, 0u);
+  }
+  __syncthreads();  // sizes, row starts, zeroed bitmaps
+  // fixed slots from the chunks (null -> 0 + the bit, bool -> 0/1)
+  auto scatter = [&](int kf, int kend, int w, const u32x4& c, uint64_t vbits) {
+    const Fix16Lane d = fix16_lane(fix, kf, kend, w, lane);
+    if (!d.ok) return;
+    switch (w) {  // a compile-time width per case: the chunk's dwords indexed statically
+      case 8: fix16_scatter<8>(img, rs, bm, d, c, vbits); break;
+      case 4: fix16_scatter<4>(img, rs, bm, d, c, vbits); break;
+      case 2: fix16_scatter<2>(img, rs, bm, d, c, vbits); break;
+      default: fix16_scatter<1>(img, rs, bm, d, c, vbits); break;
+    }
+  };
+#pragma unroll
+  for (int q = 0; q < kFix16; ++q) {
+    int kf, kend, w;
+    if (fix16_instr(L, wave + q * NW, &kf, &kend, &w)) scatter(kf, kend, w, fc[q], fv[q]);
+  }
+  for (int j = wave + kFix16 * NW;; j += NW) {  // plans with more fixed fields: a round trip per instruction
+    int kf, kend, w;
+    if (!fix16_instr(L, j, &kf, &kend, &w)) break;
+    const Fix16Lane c = fix16_lane(fix, kf, kend, w, lane);
+    const u32x4 v = __builtin_nontemporal_load(gp(reinterpret_cast<const u32x4*>(c.values + r0 * w + (c.ok ? c.sub * 16 : 0))));
+    const uint64_t vb = c.validity ? *gp(reinterpret_cast<const uint64_t*>(c.validity + (r0 >> 3))) : ~0ull;
+    scatter(kf, kend, w, v, vb);
+  }
+  // var fields: positions (the fixed part + the payloads before, field order), slots, list
+  // headers, null bits, then the payloads from the staged spans
+  int32_t pos[OWN];
+  {
+    int32_t acc = L.fixed_size;
+    int u = 0;
+#pragma unroll
+    for (int k = 0; k < OWN; ++k) {
+      const int v = wave + k * NW;
+      pos[k] = -1;
+      if (v >= L.num_var) continue;
+      for (; u < v; ++u) {
+        const int32_t s = sz[u * 64 + lane];
+        acc += s > 0 ? s : 0;
+      }
+      pos[k] = sz[v * 64 + lane] >= 0 ? acc : -1;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < OWN; ++k) {
+    const int v = wave + k * NW;
+    if (v >= L.num_var) continue;
+    const VarFieldDev& f = vf[v];
+    uint8_t* sl = slots + 8 * f.slot;
+    const int64_t n = (int64_t)e1[k] - e0[k];
+    if (pos[k] < 0) {
+      st64_lds(sl, 0);
+      atomicOr(reinterpret_cast<uint32_t*>(row) + (f.slot >> 5), 1u << (f.slot & 31));
+    } else if (!f.is_list) {
+      st64_lds(sl, ((uint64_t)(uint32_t)pos[k] << 32) | (uint32_t)n);
+    } else {
+      const int32_t ahdr = 8 + bitmap_bytes(n);
+      st64_lds(row + pos[k], (uint64_t)n);
+      for (int b = 8; b < ahdr; b += 4) st32(row + pos[k] + b, 0);
+      st64_lds(sl, ((uint64_t)(uint32_t)pos[k] << 32) | (uint32_t)(ahdr + round8(n * f.w)));
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's spans
+  wave_lds_sync();
+#pragma unroll
+  for (int k = 0; k < OWN; ++k) {
+    const int v = wave + k * NW;
+    if (v >= L.num_var) continue;
+    if (pos[k] >= 0)
+      flat_place(vf[v], staged[k], stg + soff[k], sphase[k], E0[k], svofs[k], pos[k], e0[k],
+                 (int64_t)e1[k] - e0[k], row);
+  }
+  __syncthreads();
+  uint8_t* g = out + B0 - mis;  // 16-byte aligned
+  const int tot = (int)total;
+  const int nch = (tot + 15) >> 4;
+  for (int cc = tid; cc < nch; cc += 64 * NW) {
+    const int lo = cc * 16;
+    if (lo >= mis && lo + 16 <= tot) {
+      *gp(reinterpret_cast<u32x4*>(g + lo)) = *reinterpret_cast<const u32x4*>(img + lo);
+    } else {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int o = lo + 4 * d;
+        if (o >= mis && o + 4 <= tot) *gp(reinterpret_cast<uint32_t*>(g + o)) = ld32(img + o);
+      }
+    }
+  }
 }
 
 
@@ -3007,6 +3329,46 @@ void launch_flat_enc7(const VarLaunch& L0, const int64_t* offs, uint8_t* out, in
                      sp.cap, sp);
 }
 
+// Encode v8 LDS: row image, NW span staging slots, the payload-size table, row starts.
+size_t flat8_lds(const VarLaunch& L, int cap, int slot, int nw) {
+  return (size_t)cap + (size_t)nw * slot + (size_t)L.num_var * 64 * sizeof(int32_t) + 64 * sizeof(int32_t);
+}
+
+// Span staging slot of a wave in encode v8: the tile spans of the var fields it owns at
+// 1.25x the batch's mean var bytes per field, + slack; 256-B granular, [1, 32] KiB.
+int flat8_slot(const VarLaunch& L, int64_t capacity, int nw) {
+  if (L.kn.var_stg) return L.kn.var_stg;
+  const int own = (L.num_var + nw - 1) / nw;
+  int64_t var_row = L.num_rows > 0 ? capacity / L.num_rows - L.fixed_size - frame_header_bytes(L.frame) : 0;
+  if (var_row < 0) var_row = 0;
+  const int64_t per = L.num_var > 0 ? 64 * var_row / L.num_var : 0;
+  int64_t b = own * (per * 5 / 4 + 64);
+  b = (b + 255) & ~int64_t(255);
+  return (int)(b < 1024 ? 1024 : (b > 32768 ? 32768 : b));
+}
+
+template <int HDR, int NW, int OWN>
+void launch_flat_enc8(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
+                      int cap, hipStream_t s) {
+  VarLaunch L = L0;
+  L.pl_all = 1;
+  auto* k = &var_encode_flat8_kernel<HDR, NW, OWN>;
+  const int slot = flat8_slot(L, capacity, NW);
+  const size_t lds = flat8_lds(L, cap, slot, NW);
+  raise_lds_cap(k);
+  auto* k2 = &var_encode_flat_kernel<HDR, NW, false, true>;  // tiles beyond the image
+  L.stg_bytes = enc_stg_bytes(k2, L, capacity, cap, NW);
+  const SpillArgs sp = spill_args(L, cap);
+  (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
+  var_diag(L, "encode v8", k, 64 * NW, cap, slot, lds);
+  hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
+                     L.vf, offs, out, capacity, status, cap, slot, sp);
+  raise_lds_cap(k2);
+  hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds_enc(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
+                     flat_lds_enc(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status,
+                     sp.cap, sp);
+}
+
 template <int HDR, int NW, bool NEST>
 void launch_flat_enc7_own(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                           int cap, hipStream_t s) {
@@ -3019,10 +3381,13 @@ void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int6
                      int cap, hipStream_t s) {
   // plans with nested struct fields and flat ones get their own instantiations: each
   // carries only its layout path (the other one's registers would count against it)
-  const bool v7 = !L.kn.var_enc && L.num_var <= kOwnVar * NW;
+  const bool v7 = L.kn.var_enc != 1 && L.num_var <= kOwnVar * NW;
   if (L.num_struct) {
     if (v7) launch_flat_enc7_own<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
     else launch_flat_enc_t<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
+  } else if (v7 && L.fix16 && L.kn.var_enc != 7 && L.num_rows >= 128) {
+    if (L.num_var <= 2 * NW) launch_flat_enc8<HDR, NW, 2>(L, offs, out, capacity, status, cap, s);
+    else launch_flat_enc8<HDR, NW, kOwnVar>(L, offs, out, capacity, status, cap, s);
   } else {
     if (v7) launch_flat_enc7_own<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
     else launch_flat_enc_t<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
