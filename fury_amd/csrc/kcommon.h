@@ -43,6 +43,14 @@ template <typename T>
 __device__ __forceinline__ const GAS T* gp(const T* p) { return (const GAS T*)p; }
 template <typename T>
 __device__ __forceinline__ GAS T* gp(T* p) { return (GAS T*)p; }
+// Bit updates of global words (no-return atomics on the global pointer: a generic one is a
+// flat atomic, which makes every later wait a full vmcnt(0) + lgkmcnt(0) drain).
+__device__ __forceinline__ void g_or(uint32_t* p, uint32_t v) {
+  __hip_atomic_fetch_or(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void g_and(uint32_t* p, uint32_t v) {
+  __hip_atomic_fetch_and(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Loads the `width` low bytes of element `i` (little-endian, zero-extended).
 __device__ __forceinline__ uint64_t load_elem(const uint8_t* base, int width, int64_t i) {

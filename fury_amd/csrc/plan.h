@@ -160,6 +160,7 @@ struct LaunchKnobs {
   int32_t diag;
   int32_t var_enc;   // FORY_ROWFMT_VARENC=1: flat plans keep the round-3 encode tile kernel, =7: encode v7 (A/B); else v8 where it applies
   int32_t dbg_skip;  // FORY_ROWFMT_DBGSKIP (debug, timing only; output wrong): 1 = tile kernels stop after their loads, 2 = encode v7 skips its image store
+  int32_t var_xcd;   // FORY_ROWFMT_VARXCD=C: varlen tile kernels take tiles in XCD runs of C (-1: one run per XCD), 0 = dispatch order
   int32_t dec_regs;  // FORY_ROWFMT_DECREGS=1: varlen decode stages its tile rows through registers, not LDS-DMA (A/B)
   int32_t tree_col;  // FORY_ROWFMT_TREECOL: 0 = tree-engine encode per lane only; else the columnar engine when the workspace allows
 };

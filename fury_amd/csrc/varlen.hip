@@ -283,8 +283,8 @@ __device__ __forceinline__ void dec_bytes_array(const uint8_t* row, int64_t row_
       if ((iflags & 1) && it.out_validity) {
         const uint32_t bit = 1u << (q & 31);
         uint32_t* word = reinterpret_cast<uint32_t*>(it.out_validity) + (q >> 5);
-        if (en) atomicAnd(word, ~bit);
-        else atomicOr(word, bit);
+        if (en) g_and(word, ~bit);
+        else g_or(word, bit);
       }
     }
   }
@@ -764,8 +764,8 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
                   const int64_t q = e0 + j;
                   const uint32_t bit = 1u << (q & 31);
                   uint32_t* word = reinterpret_cast<uint32_t*>(it.out_validity) + (q >> 5);
-                  if (en) atomicAnd(word, ~bit);
-                  else atomicOr(word, bit);
+                  if (en) g_and(word, ~bit);
+                  else g_or(word, bit);
                 }
               }
             }
@@ -816,8 +816,8 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
               const uint32_t bit = 1u << (q & 31);
               if ((op.d & 4) && sc.out_validity) {
                 uint32_t* word = reinterpret_cast<uint32_t*>(sc.out_validity) + (q >> 5);
-                if (en) atomicAnd(word, ~bit);
-                else atomicOr(word, bit);
+                if (en) g_and(word, ~bit);
+                else g_or(word, bit);
               }
               for (int f = 0; f < nf; ++f) {
                 const Op o = prog[pc + 1 + f];
@@ -829,8 +829,8 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
                 store_elem(cc.out_values, o.c, q, v);
                 if ((o.d & 1) && cc.out_validity) {
                   uint32_t* word = reinterpret_cast<uint32_t*>(cc.out_validity) + (q >> 5);
-                  if (nul) atomicAnd(word, ~bit);
-                  else atomicOr(word, bit);
+                  if (nul) g_and(word, ~bit);
+                  else g_or(word, bit);
                 }
               }
             }
@@ -908,8 +908,8 @@ __device__ __forceinline__ void dec_record(const VarLaunch& L, const Op* __restr
                   const int64_t q = e0 + j;
                   const uint32_t bit = 1u << (q & 31);
                   uint32_t* word = reinterpret_cast<uint32_t*>(it.out_validity) + (q >> 5);
-                  if (en) atomicAnd(word, ~bit);
-                  else atomicOr(word, bit);
+                  if (en) g_and(word, ~bit);
+                  else g_or(word, bit);
                 }
               }
             }
@@ -974,6 +974,18 @@ __device__ __forceinline__ bool var_tile_bounds(const int64_t* offs, int64_t n, 
   return __ballot(!ok) == 0 && ((*B0 | *B1) & 3) == 0 && *B1 >= *B0;
 }
 
+// logical tile of workgroup b under FORY_ROWFMT_VARXCD=C (A/B): dispatch b runs on XCD
+// b % 8, so runs of C consecutive tiles per XCD keep each XCD's concurrent tiles
+// adjacent (its L2 and TLB see one region); C < 0: one run per XCD over the grid
+__device__ __forceinline__ int64_t var_tile(int64_t b, int64_t tiles, int64_t C) {
+  if (C < 0) C = tiles / 8;
+  if (C <= 0) return b;
+  const int64_t blk = b / (8 * C);
+  if ((blk + 1) * 8 * C > tiles) return b;
+  const int64_t x = b - blk * 8 * C;
+  return blk * 8 * C + (x % 8) * C + x / 8;
+}
+
 template <bool SPILL>
 __global__ __launch_bounds__(64) void var_encode_tile_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols, const int64_t* __restrict__ offs,
                                                              uint8_t* __restrict__ out, int64_t capacity,
@@ -1016,7 +1028,7 @@ __global__ __launch_bounds__(64) void var_encode_tile_kernel(VarLaunch L, const 
   }
   };
   if (!SPILL) {
-    body(blockIdx.x);
+    body(var_tile(blockIdx.x, gridDim.x, L.kn.var_xcd));
     return;
   }
   const int64_t count = *sp.count;  // tiles the main launch spilled
@@ -1060,7 +1072,7 @@ __global__ __launch_bounds__(64) void var_decode_tile_kernel(VarLaunch L, const 
   dec_record<WRITE>(L, prog, cols, r0 + lane, live, lds + mis + (beg - B0), end - beg, status);
   };
   if (!SPILL) {
-    body(blockIdx.x);
+    body(var_tile(blockIdx.x, gridDim.x, L.kn.var_xcd));
     return;
   }
   const int64_t count = *sp.count;  // tiles the main launch spilled
@@ -1295,7 +1307,7 @@ __device__ __forceinline__ void flat_place(const VarFieldDev& f, bool staged, co
   } else {
     uint8_t* arr = row + p;
     for (int64_t j = 0; j < n; ++j) {
-      const bool enull = f.item_validity && !((f.item_validity[(e0 + j) >> 3] >> ((e0 + j) & 7)) & 1);
+      const bool enull = f.item_validity && !((*gp(f.item_validity + ((e0 + j) >> 3)) >> ((e0 + j) & 7)) & 1);
       uint64_t x = 0;
       if (enull) arr[8 + (j >> 3)] |= (uint8_t)(1u << (j & 7));
       else x = load_elem(f.values, w, e0 + j);
@@ -1347,7 +1359,7 @@ __device__ __forceinline__ void flat_enc_layout_nested(const VarLaunch& L, const
         const ColumnDev& c = cols[op.b];
         if ((op.d & 1) && op.code != OP_STRUCT_END && c.validity)
           nul[k] = !((load_byte(c.validity + (ii >> 3)) >> (ii & 7)) & 1);
-        if (op.code == OP_BYTES || op.code == OP_LIST) nn[k] = c.offsets[ii + 1] - c.offsets[ii];
+        if (op.code == OP_BYTES || op.code == OP_LIST) nn[k] = *gp(c.offsets + ii + 1) - *gp(c.offsets + ii);
       }
     }
 #pragma unroll
@@ -1503,9 +1515,9 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
   int64_t pf_e0 = 0, pf_e1 = 0;
   if (wave != 0 && v_first < L.num_var) {
     const VarFieldDev& f = vf[v_first];
-    const int64_t ee = f.offsets[r0 + rows];
-    pf_e0 = lv ? f.offsets[i] : ee;
-    pf_e1 = lv ? f.offsets[i + 1] : ee;
+    const int64_t ee = *gp(f.offsets + r0 + rows);
+    pf_e0 = lv ? *gp(f.offsets + i) : ee;
+    pf_e1 = lv ? *gp(f.offsets + i + 1) : ee;
   }
   constexpr int kPre = 3;
   int64_t pe0[kPre], pe1[kPre];
@@ -1515,9 +1527,9 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
     pe0[k] = pe1[k] = 0;
     if (v < L.num_var) {
       const VarFieldDev& f = vf[v];
-      const int64_t ee = f.offsets[r0 + rows];
-      pe0[k] = lv ? f.offsets[i] : ee;
-      pe1[k] = lv ? f.offsets[i + 1] : ee;
+      const int64_t ee = *gp(f.offsets + r0 + rows);
+      pe0[k] = lv ? *gp(f.offsets + i) : ee;
+      pe1[k] = lv ? *gp(f.offsets + i + 1) : ee;
     }
   }
   const bool pre_layout = !NEST && wave == 0 && L.num_var > 0;
@@ -1667,9 +1679,9 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
       for (int k = 0; k < kPre; ++k)
         if (kv == k + 1) e0 = pe0[k], e1 = pe1[k];
     } else if (kv > kPre || wave == 0) {
-      const int64_t ee = f.offsets[r0 + rows];
-      e0 = live ? f.offsets[i] : ee;
-      e1 = live ? f.offsets[i + 1] : ee;
+      const int64_t ee = *gp(f.offsets + r0 + rows);
+      e0 = live ? *gp(f.offsets + i) : ee;
+      e1 = live ? *gp(f.offsets + i + 1) : ee;
     }
     const int p = live ? pos[v * 64 + lane] : -1;
     for (int lo = 0; lo < rows;) {
@@ -1719,7 +1731,7 @@ __device__ __forceinline__ void var_encode_flat_body(VarLaunch L, const Op* __re
   FLAT_STAMP(7);
   };
   if (!SPILL) {
-    body(blockIdx.x);
+    body(var_tile(blockIdx.x, gridDim.x, L.kn.var_xcd));
     return;
   }
   const int64_t count = *sp.count;  // tiles the main launch spilled
@@ -1776,20 +1788,68 @@ __device__ __forceinline__ bool fix_batch(const VarLaunch& L, int j, int* k0, in
   return *k0 < nf;
 }
 
+// Fixed values through registers, loaded branch-free: every lane issues the same two
+// dword loads whatever the field's width -- the element's dword(s): for w = 8 the two
+// halves (any alignment), for w <= 4 the aligned dwords holding its first and last
+// bytes (never past the page of a byte of the column). A switch over widths instead
+// merges differently typed loads, and the compiler then waits for each load before
+// the next (a round trip per field).
 struct FixRegs {
-  uint64_t v[kFixBatch];
-  uint32_t vb[kFixBatch];
+  uint32_t lo[kFixBatch], hi[kFixBatch];
+  uint32_t vb[kFixBatch];  // validity byte (fields without validity: any byte, unused)
 };
 
-// The batch's values and validity bytes of record ii, all loads issued together.
+__device__ __forceinline__ void elem_issue(const uint8_t* base, int w, int64_t i, uint32_t* lo, uint32_t* hi) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(base) + (uintptr_t)(i * w);
+  const bool w8 = w == 8;
+  const uintptr_t la = w8 ? a : a & ~uintptr_t(3);
+  const uintptr_t ha = w8 ? a + 4 : (a + w - 1) & ~uintptr_t(3);
+  *lo = *gp(reinterpret_cast<const uint32_t*>(la));
+  *hi = *gp(reinterpret_cast<const uint32_t*>(ha));
+}
+
+__device__ __forceinline__ uint64_t elem_value(const uint8_t* base, int w, int64_t i, uint32_t lo, uint32_t hi) {
+  const uint64_t d = ((uint64_t)hi << 32) | lo;
+  if (w == 8) return d;
+  const int sh = (int)((reinterpret_cast<uintptr_t>(base) + (uintptr_t)(i * w)) & 3) * 8;
+  return (d >> sh) & ((1ull << (8 * w)) - 1);
+}
+
+// The batch's values and validity bytes of record ii, all loads issued together
+// (`safe`: any readable byte, the address of fields without validity).
+template <bool VB = true>
 __device__ __forceinline__ void fix_load(const FixedFieldDev* __restrict__ fix, int k0, int k1, int64_t ii,
-                                         FixRegs& R) {
+                                         FixRegs& R, const void* safe) {
 #pragma unroll
   for (int k = 0; k < kFixBatch; ++k) {
-    const FixedFieldDev& f = fix[k0 + k < k1 ? k0 + k : k1 - 1];
-    R.v[k] = load_elem(f.values, f.width, ii);
-    R.vb[k] = f.validity ? load_byte(f.validity + (ii >> 3)) : 0xffu;
+    const FixedFieldDev& f = fix[min(k0 + k, k1 - 1)];
+    elem_issue(f.values, f.width, ii, &R.lo[k], &R.hi[k]);
+    if constexpr (VB) {
+      const uint8_t* vp = f.validity ? f.validity + (ii >> 3) : reinterpret_cast<const uint8_t*>(safe);
+      R.vb[k] = load_byte(vp);
+    }
   }
+}
+
+// Software-pipeline fences (encode v9): ready(x) marks where loaded registers are first
+// needed -- the compiler inserts its wait here and cannot hoist work on x above it --
+// and sched_fence() keeps the scheduler from moving loads and work across a phase.
+__device__ __forceinline__ void ready(uint32_t& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void ready(int32_t& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void ready(int64_t& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+
+// A validity byte as the aligned dword holding it (a byte load's zero-extension would
+// be placed by the compiler right after the load, waiting for it there).
+__device__ __forceinline__ uint32_t vbyte_issue(const uint8_t* p) {
+  return *gp(reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(3)));
+}
+__device__ __forceinline__ uint32_t vbyte_get(uint32_t w, const uint8_t* p) {
+  return w >> (8 * (reinterpret_cast<uintptr_t>(p) & 3));
+}
+
+__device__ __forceinline__ bool fix_valid(const FixedFieldDev& f, const FixRegs& R, int k, int64_t ii) {
+  return !f.validity || ((R.vb[k] >> (ii & 7)) & 1);
 }
 
 // BinaryRowWriter.write(ordinal, v) into the row image's slots (zero-extended; a null
@@ -1800,8 +1860,8 @@ __device__ __forceinline__ void fix_store(const FixedFieldDev* __restrict__ fix,
   for (int k = 0; k < kFixBatch; ++k) {
     if (k0 + k >= k1 || !live) continue;
     const FixedFieldDev& f = fix[k0 + k];
-    const bool valid = (R.vb[k] >> (ii & 7)) & 1;
-    uint64_t x = valid ? R.v[k] : 0;
+    const bool valid = fix_valid(f, R, k, ii);
+    uint64_t x = valid ? elem_value(f.values, f.width, ii, R.lo[k], R.hi[k]) : 0;
     if (f.flags & 2) x = x ? 1 : 0;
     st64_lds(slots + 8 * f.slot, x);
     if (!valid) atomicOr(bmrow + (f.slot >> 5), 1u << (f.slot & 31));
@@ -1824,6 +1884,22 @@ __device__ __forceinline__ void str_load(const uint8_t* src, int64_t n, int c, S
   const int nd = left <= 0 ? 0 : (int)((sb + (left < 32 ? left : 32) + 3) >> 2);
 #pragma unroll
   for (int q = 0; q < kStrDw; ++q) S.d[q] = q < nd ? *gp(p + q) : 0u;
+}
+
+// str_load without per-lane branches (encode v9: every lane issues the same kStrDw
+// loads, so the compiler can count them): dwords past the string's re-read its last one
+// (an empty string reads `safe`); str_store masks the bytes past the string.
+__device__ __forceinline__ void str_load_all(const uint8_t* src, int64_t n, int c, StrRegs& S, const void* safe) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(src) + 32 * c;
+  const int sb = (int)(a & 3);
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(a - sb);
+  const int64_t left = n - 32 * c;
+  const int nd = left <= 0 ? 0 : (int)((sb + (left < 32 ? left : 32) + 3) >> 2);
+#pragma unroll
+  for (int q = 0; q < kStrDw; ++q) {
+    const uint32_t* at = nd > 0 ? p + (q < nd ? q : nd - 1) : reinterpret_cast<const uint32_t*>(safe);
+    S.d[q] = *gp(at);
+  }
 }
 
 // Chunk c of writeUnaligned + zeroOutPaddingBytes (BinaryWriter.java:117-121,162-194):
@@ -1887,7 +1963,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   uint32_t* bmt = reinterpret_cast<uint32_t*>(sz + L.num_var * 64);            // flat: [64][bmw] null bits
   int32_t* sbs = reinterpret_cast<int32_t*>(sz + L.num_var * 64);              // NEST: [1 + num_struct][64] child rows
   const int bmw = L.bitmap_bytes >> 2;
-  const int64_t tile = blockIdx.x;
+  const int64_t tile = var_tile(blockIdx.x, gridDim.x, L.kn.var_xcd);
   const int64_t r0 = tile * 64;
   const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
   const bool lv = lane < rows;
@@ -1918,8 +1994,8 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
     vvb[k] = 0xffu;
     if (v < L.num_var) {
       const VarFieldDev& f = vf[v];
-      e0[k] = f.offsets[lv ? i : r0 + rows];  // dead lanes: the tile's end (empty ranges)
-      e1[k] = f.offsets[lv ? i + 1 : r0 + rows];
+      e0[k] = *gp(f.offsets + (lv ? i : r0 + rows));  // dead lanes: the tile's end (empty ranges)
+      e1[k] = *gp(f.offsets + (lv ? i + 1 : r0 + rows));
       vvb[k] = f.validity ? load_byte(f.validity + (ii >> 3)) : 0xffu;
     }
   }
@@ -1932,7 +2008,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   int fk0 = 0, fk1 = 0;
   const bool has_fix = fix_batch(L, wave, &fk0, &fk1);
   FixRegs R;
-  if (has_fix) fix_load(fix, fk0, fk1, ii, R);
+  if (has_fix) fix_load(fix, fk0, fk1, ii, R, offs);
   int64_t B0, B1, beg, end;
   bool live;
   const bool sane = var_tile_bounds(offs, L.num_rows, r0, lane, &B0, &B1, &beg, &end, &live);
@@ -1952,7 +2028,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   const int64_t total = mis + (B1 - B0);
   V7_STAMP(1);
   if (L.kn.dbg_skip == 1) {  // debug: the loads alone (timing); keep them live
-    if (tid == 0 && B1 == -7) L.prof[0] = (uint64_t)(e0[0] + R.v[0] + S[0].d[0] + (uint32_t)beg);
+    if (tid == 0 && B1 == -7) L.prof[0] = (uint64_t)(e0[0] + R.lo[0] + R.hi[0] + S[0].d[0] + (uint32_t)beg);
     return;
   }
   if (!sane || (mis & 3) || total > cap) {
@@ -2013,7 +2089,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
       int a, b;
       if (!fix_batch(L, j, &a, &b)) break;
       FixRegs Q;
-      fix_load(fix, a, b, ii, Q);
+      fix_load(fix, a, b, ii, Q, offs);
       fix_store(fix, a, b, Q, live, ii, slots, bmrow);
     }
   }
@@ -2109,8 +2185,8 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
         const int32_t base = sbs[f.parent * 64 + lane];
         if (base < 0) continue;
         const int32_t hdr = f.parent ? st[f.parent - 1].hdr : L.bitmap_bytes;
-        const bool valid = (Q.vb[k] >> (ii & 7)) & 1;
-        uint64_t x = valid ? Q.v[k] : 0;
+        const bool valid = fix_valid(f, Q, k, ii);
+        uint64_t x = valid ? elem_value(f.values, f.width, ii, Q.lo[k], Q.hi[k]) : 0;
         if (f.flags & 2) x = x ? 1 : 0;
         st64_lds(row + base + hdr + 8 * f.slot, x);
         if (!valid) atomicOr(reinterpret_cast<uint32_t*>(row + base) + (f.slot >> 5), 1u << (f.slot & 31));
@@ -2121,7 +2197,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
       int a, b;
       if (!fix_batch(L, j, &a, &b)) break;
       FixRegs Q;
-      fix_load(fix, a, b, ii, Q);
+      fix_load(fix, a, b, ii, Q, offs);
       put_fixed(a, b, Q);
     }
   }
@@ -2314,7 +2390,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat8_kernel(VarLaunch L, 
   uint8_t* stg = lds + cap + wave * slot;                                // this wave's span staging
   int32_t* sz = reinterpret_cast<int32_t*>(lds + cap + NW * slot);       // [num_var][64] payload bytes, -1 null
   int32_t* rs = sz + L.num_var * 64;                                     // [64] row starts in the image
-  const int64_t tile = blockIdx.x;
+  const int64_t tile = var_tile(blockIdx.x, gridDim.x, L.kn.var_xcd);
   const int64_t r0 = tile * 64;
   const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
   const int64_t i = r0 + lane;
@@ -2524,6 +2600,321 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat8_kernel(VarLaunch L, 
 }
 
 
+// ---------------------------------------------------------------------------
+// Encode v9: encode v7's tile as a persistent, software-pipelined loop (flat plans of
+// fixed fields and strings / binary: no list or nested struct fields, <= kFixBatch * NW
+// fixed fields, <= OWN * NW var fields, a bitmap of <= kV9Bmw words).
+//
+// v7 spends a tile's whole life (~16 us at 4 tiles per CU) on a chain of dependent
+// round trips -- row bounds and offsets -> string bytes -> copies -> stores -- so each
+// CU has a tile's loads in flight only part of the time. Here a workgroup walks tiles
+// t, t + G, ... and the next tile's loads fly while this one is assembled:
+//   P1  sizes, null bits (partial words per wave) and row starts of tile t -> LDS
+//       (its offsets, validity and row bounds were loaded during tile t - G)
+//   B1  barrier (the previous image has left: its stores were issued before it)
+//   P2  wave 0: header + bitmap; every wave: its fields' positions (prefix of sizes)
+//   P3  fixed values (loaded during tile t - G) and the strings' first 32 bytes
+//       (loaded during P3 of tile t - G) into the image; longer strings: a trip per chunk
+//   --  tile t + G: its strings' first 32 bytes in flight (its offsets have landed)
+//   B2  barrier; the image leaves as 16-B stores
+//   --  tile t + 2G: offsets, validity, row bounds; tile t + G: fixed values, in flight
+// Every wait is on loads issued a phase or more earlier; the stores are older than
+// anything waited on after them. Bytes are those of var_encode_flat7_kernel.
+// ---------------------------------------------------------------------------
+constexpr int kV9Bmw = 4;  // bitmap words per row (<= 128 fields)
+
+template <int OWN>
+struct V9Cols {            // one tile's per-lane column registers
+  int32_t e0[OWN], e1[OWN];
+  uint32_t vvb[OWN];       // owned var fields: the dword holding the record's validity byte
+  uint32_t fvb[kFixBatch]; // the wave's fixed batch: the same
+  int64_t beg, end;        // the record's row bounds
+};
+
+#define FORY_V9_PARAMS                                                                                   \
+  VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,                          \
+      const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,                         \
+      const int64_t* __restrict__ offs, uint8_t* __restrict__ out, int64_t capacity, int32_t* status, int cap, \
+      SpillArgs sp
+
+template <int HDR, int NW, int OWN, int K>
+__device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* img = lds;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int32_t* sz = reinterpret_cast<int32_t*>(lds + cap);                 // [num_var][64] payload bytes
+  uint32_t* pbt = reinterpret_cast<uint32_t*>(sz + L.num_var * 64);     // [NW][64][bmw] partial null bits
+  const int bmw = L.bitmap_bytes >> 2;
+  const int64_t ntiles = (L.num_rows + 63) / 64;
+  int fk0 = 0, fk1 = 0;
+  const bool has_fix = fix_batch(L, wave, &fk0, &fk1);
+  // the fields whose words the loads read (a wave without a batch: the last field's, unused)
+  const int fa = has_fix ? fk0 : L.fix_group[4] - 1, fb = has_fix ? fk1 : fa + 1;
+
+  // tile tl's offsets, validity bytes and row bounds (tiles past the end: the last one);
+  // branch-free (fields past num_var load field num_var - 1's words, unused): see FixRegs
+  auto load_cols = [&](int64_t tl, V9Cols<OWN>& C) {
+    tl = tl < ntiles ? tl : ntiles - 1;  // (past the end: the last tile, unused)
+    const int64_t q0 = tl * 64;
+    const int rw = L.num_rows - q0 < 64 ? (int)(L.num_rows - q0) : 64;
+    const bool lq = lane < rw;
+    const int64_t iq = lq ? q0 + lane : q0;
+#pragma unroll
+    for (int k = 0; k < OWN; ++k) {
+      const int v = wave + k * NW < L.num_var ? wave + k * NW : L.num_var - 1;
+      const VarFieldDev& f = vf[v];
+      C.e0[k] = *gp(f.offsets + (lq ? iq : q0 + rw));  // dead lanes: the tile's end (empty ranges)
+      C.e1[k] = *gp(f.offsets + (lq ? iq + 1 : q0 + rw));
+      C.vvb[k] = vbyte_issue(f.validity ? f.validity + (iq >> 3) : reinterpret_cast<const uint8_t*>(offs));
+    }
+#pragma unroll
+    for (int k = 0; k < kFixBatch; ++k) {
+      const FixedFieldDev& f = fix[min(fa + k, fb - 1)];
+      C.fvb[k] = vbyte_issue(f.validity ? f.validity + (iq >> 3) : reinterpret_cast<const uint8_t*>(offs));
+    }
+    C.beg = offs[iq];
+    C.end = offs[lq ? iq + 1 : q0];
+  };
+  auto load_fixed = [&](int64_t tl, FixRegs& F) {
+    tl = tl < ntiles ? tl : ntiles - 1;
+    const int64_t q0 = tl * 64;
+    const int64_t iq = q0 + lane < L.num_rows ? q0 + lane : q0;
+    fix_load<false>(fix, fa, fb, iq, F, offs);
+  };
+  auto load_strs = [&](const V9Cols<OWN>& C, StrRegs (&S)[OWN]) {
+#pragma unroll
+    for (int k = 0; k < OWN; ++k) {
+      const int v = wave + k * NW < L.num_var ? wave + k * NW : L.num_var - 1;
+      str_load_all(vf[v].values + C.e0[k], (int64_t)C.e1[k] - C.e0[k], 0, S[k], offs);
+    }
+  };
+
+  const int64_t tb = (int64_t)blockIdx.x * K;  // this workgroup's tiles tb .. tb + K - 1
+  if (tb >= ntiles) return;
+  V9Cols<OWN> C[K];
+  FixRegs F[K];
+  StrRegs S[OWN];
+  auto ready_cols = [&](V9Cols<OWN>& C) {
+#pragma unroll
+    for (int k = 0; k < OWN; ++k) {
+      ready(C.e0[k]);
+      ready(C.e1[k]);
+      ready(C.vvb[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kFixBatch; ++k) ready(C.fvb[k]);
+    ready(C.beg);
+    ready(C.end);
+  };
+  auto ready_vals = [&](FixRegs& R) {
+#pragma unroll
+    for (int k = 0; k < kFixBatch; ++k) {
+      ready(R.lo[k]);
+      ready(R.hi[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < OWN; ++k)
+#pragma unroll
+      for (int q = 0; q < kStrDw; ++q) ready(S[k].d[q]);
+  };
+  load_cols(tb, C[0]);
+  load_fixed(tb, F[0]);
+  sched_fence();
+  ready_cols(C[0]);
+  load_strs(C[0], S);
+  sched_fence();
+#pragma unroll
+  for (int j = 1; j < K; ++j) {
+    load_cols(tb + j, C[j]);
+    load_fixed(tb + j, F[j]);
+  }
+  sched_fence();
+#define V9_STAMP(k)                                                                             \
+  do {                                                                                         \
+    if (L.prof && tid == 0) L.prof[t * 8 + (k)] = __builtin_amdgcn_s_memrealtime();            \
+  } while (0)
+  // tile t from its column registers C0 / FV and the strings' registers; then (more) the
+  // next tile's strings in flight from C1
+  auto step = [&](int64_t t, V9Cols<OWN>& C0, FixRegs& FV, V9Cols<OWN>& C1, bool more) {
+    sched_fence();
+    ready_cols(C0);
+    V9_STAMP(0);
+    const int64_t r0 = t * 64;
+    const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
+    const bool live = lane < rows;
+    const int64_t ii = live ? r0 + lane : r0;
+    // ---- P1: bounds checks (uniform over the workgroup: every wave sees the same rows)
+    const int64_t B0 = __shfl(C0.beg, 0), B1 = __shfl(C0.end, rows - 1);
+    const bool ok = !live || (C0.beg >= B0 && C0.end >= C0.beg && C0.end <= B1);
+    const bool sane = __ballot(!ok) == 0 && ((B0 | B1) & 3) == 0 && B1 >= B0;
+    const bool capbad = live && (C0.end > capacity || C0.beg < 0 || C0.end < C0.beg);
+    const bool skip = __ballot(capbad) != 0;
+    if (skip && wave == 0 && capbad) set_status(status, FORY_ERR_CAPACITY);
+    const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
+    const int64_t total = mis + (B1 - B0);
+    const bool tiled = !skip && sane && !(mis & 3) && total <= cap;
+    uint8_t* fp = img + mis + (int)(C0.beg - B0);
+    uint8_t* row = fp + HDR;
+    uint8_t* slots = row + L.bitmap_bytes;
+    if (tiled) {  // sizes (-1 null, -2 dead lane) and this wave's null bits of the record
+      uint64_t pl = 0, ph = 0;  // this wave's null bits of the record (no indexed array: registers)
+      auto null_bit = [&](int slot) {
+        const uint64_t bit = 1ull << (slot & 63);
+        if (slot < 64) pl |= bit;
+        else ph |= bit;
+      };
+#pragma unroll
+      for (int k = 0; k < OWN; ++k) {
+        const int v = wave + k * NW;
+        if (v >= L.num_var) continue;
+        const bool valid = !vf[v].validity || ((vbyte_get(C0.vvb[k], vf[v].validity + (ii >> 3)) >> (ii & 7)) & 1);
+        const int64_t n = (int64_t)C0.e1[k] - C0.e0[k];
+        sz[v * 64 + lane] = !live ? -2 : !valid ? -1 : (int32_t)round8(n);
+        if (live && !valid) null_bit(vf[v].slot);
+      }
+#pragma unroll
+      for (int k = 0; k < kFixBatch; ++k)
+        if (fk0 + k < fk1 && live && fix[fk0 + k].validity &&
+            !((vbyte_get(C0.fvb[k], fix[fk0 + k].validity + (ii >> 3)) >> (ii & 7)) & 1))
+          null_bit(fix[fk0 + k].slot);
+      uint32_t* pw = pbt + (wave * 64 + lane) * bmw;
+      pw[0] = (uint32_t)pl;
+      if (bmw > 1) pw[1] = (uint32_t)(pl >> 32);
+      if (bmw > 2) pw[2] = (uint32_t)ph;
+      if (bmw > 3) pw[3] = (uint32_t)(ph >> 32);
+    }
+    V9_STAMP(1);
+    __syncthreads();  // B1
+    V9_STAMP(2);
+    if (tiled) {
+      // ---- P2: header and bitmap (wave 0), positions
+      if (wave == 0 && live) {  // Encoders.encode frame header; BinaryRowWriter.reset + setNullAt
+        if (HDR == 12) {
+          st32(fp, (uint32_t)(C0.end - C0.beg - 4));
+          st64_lds(fp + 4, (uint64_t)L.schema_hash);
+        } else if (HDR == 8) {
+          st64_lds(fp, (uint64_t)L.schema_hash);
+        }
+        for (int b = 0; b < bmw; ++b) {
+          uint32_t w = 0;
+          for (int q = 0; q < NW; ++q) w |= pbt[(q * 64 + lane) * bmw + b];
+          st32(row + 4 * b, w);
+        }
+      }
+      int32_t pos[OWN];
+      {
+        int32_t acc = L.fixed_size;
+        int u = 0;
+#pragma unroll
+        for (int k = 0; k < OWN; ++k) {
+          const int v = wave + k * NW;
+          pos[k] = -1;
+          if (v >= L.num_var) continue;
+          for (; u < v; ++u) {
+            const int32_t s = sz[u * 64 + lane];
+            acc += s > 0 ? s : 0;
+          }
+          pos[k] = live && sz[v * 64 + lane] >= 0 ? acc : -1;
+        }
+      }
+      // ---- P3: fixed slots (BinaryRowWriter.write: zero-extended; null -> 0)
+      sched_fence();
+      ready_vals(FV);
+      if (has_fix && live) {
+#pragma unroll
+        for (int k = 0; k < kFixBatch; ++k) {
+          if (fk0 + k >= fk1) continue;
+          const FixedFieldDev& f = fix[fk0 + k];
+          const bool valid = !f.validity || ((vbyte_get(C0.fvb[k], f.validity + (ii >> 3)) >> (ii & 7)) & 1);
+          uint64_t x = valid ? elem_value(f.values, f.width, ii, FV.lo[k], FV.hi[k]) : 0;
+          if (f.flags & 2) x = x ? 1 : 0;
+          st64_lds(slots + 8 * f.slot, x);
+        }
+      }
+      // var slots (offset << 32 | size) and the strings' first chunks
+#pragma unroll
+      for (int k = 0; k < OWN; ++k) {
+        const int v = wave + k * NW;
+        if (v >= L.num_var || !live) continue;
+        const VarFieldDev& f = vf[v];
+        uint8_t* sl = slots + 8 * f.slot;
+        const int64_t n = (int64_t)C0.e1[k] - C0.e0[k];
+        if (pos[k] < 0) {
+          st64_lds(sl, 0);
+        } else {
+          st64_lds(sl, ((uint64_t)(uint32_t)pos[k] << 32) | (uint32_t)n);
+          str_store(row + pos[k], f.values + C0.e0[k], n, 0, S[k]);
+        }
+      }
+      // strings longer than 32 bytes: their further chunks (a round trip each)
+#pragma unroll
+      for (int k = 0; k < OWN; ++k) {
+        const int v = wave + k * NW;
+        if (v >= L.num_var) continue;
+        const int64_t n = live && pos[k] >= 0 ? (int64_t)C0.e1[k] - C0.e0[k] : 0;
+        const int nc = (int)((n + 31) >> 5);
+        for (int c = 1; __ballot(c < nc); ++c) {
+          StrRegs T;
+          str_load(vf[v].values + C0.e0[k], c < nc ? n : 0, c, T);
+          if (c < nc) str_store(row + pos[k], vf[v].values + C0.e0[k], n, c, T);
+        }
+      }
+    } else if (!skip) {  // unaligned or big tile: the spill launch, or per record from global
+      if (sane && !(mis & 3) && total <= sp.cap) {
+        if (tid == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)t;
+      } else if (wave == 0 && live) {
+        enc_record(L, prog, cols, r0 + lane, out + C0.beg, C0.end - C0.beg);
+      }
+    }
+    V9_STAMP(3);
+    sched_fence();
+    if (more) {  // the next tile: its strings' first 32 bytes
+      ready_cols(C1);
+      load_strs(C1, S);
+    }
+    sched_fence();
+    V9_STAMP(4);
+    __syncthreads();  // B2: the image is complete
+    V9_STAMP(5);
+    if (tiled && L.kn.dbg_skip != 2) {
+      uint8_t* g = out + B0 - mis;  // 16-byte aligned
+      const int tot = (int)total;
+      const int nch = (tot + 15) >> 4;
+      for (int cc = tid; cc < nch; cc += 64 * NW) {
+        const int lo = cc * 16;
+        if (lo >= mis && lo + 16 <= tot) {
+          *gp(reinterpret_cast<u32x4*>(g + lo)) = *reinterpret_cast<const u32x4*>(img + lo);
+        } else {
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const int o = lo + 4 * d;
+            if (o >= mis && o + 4 <= tot) *gp(reinterpret_cast<uint32_t*>(g + o)) = ld32(img + o);
+          }
+        }
+      }
+    }
+    V9_STAMP(6);
+  };
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    if (tb + j < ntiles) step(tb + j, C[j], F[j], C[j + 1 < K ? j + 1 : j], j + 1 < K);  // (past the end: clamped)
+#undef V9_STAMP
+}
+
+template <int HDR, int NW, int OWN, int K>
+__global__ __launch_bounds__(64 * NW) void var_encode_flat9_kernel(FORY_V9_PARAMS) {
+  var_encode_flat9_body<HDR, NW, OWN, K>(L, prog, cols, fix, vf, offs, out, capacity, status, cap, sp);
+}
+
+// (A/B, FORY_ROWFMT_VARENC=10) the same held to 128 VGPRs: 4 workgroups per CU, some spilled
+template <int HDR, int NW, int OWN, int K>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) void var_encode_flat9_lean_kernel(
+    FORY_V9_PARAMS) {
+  var_encode_flat9_body<HDR, NW, OWN, K>(L, prog, cols, fix, vf, offs, out, capacity, status, cap, sp);
+}
+
+
 __device__ __forceinline__ int64_t wave_incl_scan64(int64_t x, int lane) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -2692,8 +3083,8 @@ __device__ __forceinline__ void dec_item_validity(const VarFieldDev& f, int64_t 
     if (span == ~0u) {
       *gp(gv + k) = bw[k];
     } else {  // word shared with a neighbouring tile: touch only this span's bits
-      atomicAnd(gv + k, ~span);
-      atomicOr(gv + k, bw[k]);
+      g_and(gv + k, ~span);
+      g_or(gv + k, bw[k]);
     }
   }
   wave_lds_sync();
@@ -2753,9 +3144,9 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
           const int64_t sum = wave_sum64(n);
           if (lane == 0) tile_tot[v * (tiles + 1) + tile] = sum;
         } else {
-          const int64_t base = vf[v].out_offsets[r0];
+          const int64_t base = *gp(vf[v].out_offsets + r0);
           const int64_t excl = wave_incl_scan64(n, lane) - n;
-          if (live) vf[v].out_offsets[r0 + lane] = (int32_t)(base + excl);
+          if (live) *gp(vf[v].out_offsets + r0 + lane) = (int32_t)(base + excl);
         }
       }
       if (WRITE) dec_record<true>(L, prog, cols, r0 + lane, live, in + beg, end - beg, status);
@@ -2765,7 +3156,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   // tile-start Arrow offsets of every var field (written by decode_sizes): loaded
   // now so their latency hides under the staging loads (lane v holds field v's)
   int64_t obase = 0;
-  if (WRITE && lane < L.num_var) obase = vf[lane].out_offsets[r0];
+  if (WRITE && lane < L.num_var) obase = *gp(vf[lane].out_offsets + r0);
   {  // stage the tile's rows: LDS-DMA of whole 16-B chunks (1 KiB per wave
      // instruction, all in flight at once, nt policy for the once-read rows); the
      // edge chunks' bytes outside the tile (same 16-B blocks) are never read
@@ -2860,7 +3251,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
     const int64_t incl = wave_incl_scan64(n, lane);
     const int64_t O1 = O0 + __shfl(incl, 63);
     const int64_t e0 = O0 + incl - n;
-    if (live) f.out_offsets[i] = (int32_t)e0;
+    if (live) *gp(f.out_offsets + i) = (int32_t)e0;
     const int64_t S = (O1 - O0) * w;
     const uint8_t* src = row + rel + (islist ? 8 + bitmap_bytes(n) : 0);
     // this lane's payload into the staging at d (BinaryArray.toXArray; null items,
@@ -2929,8 +3320,8 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
           const int64_t q = e0 + j;
           const uint32_t bit = 1u << (q & 31);
           uint32_t* word = reinterpret_cast<uint32_t*>(f.out_item_validity) + (q >> 5);
-          if (en) atomicAnd(word, ~bit);
-          else atomicOr(word, bit);
+          if (en) g_and(word, ~bit);
+          else g_or(word, bit);
         }
       }
     };
@@ -3016,7 +3407,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   }
   };
   if (!SPILL) {
-    body(blockIdx.x);
+    body(var_tile(blockIdx.x, gridDim.x, L.kn.var_xcd));
     return;
   }
   const int64_t count = *sp.count;  // tiles the main launch spilled
@@ -3369,6 +3760,44 @@ void launch_flat_enc8(const VarLaunch& L0, const int64_t* offs, uint8_t* out, in
                      sp.cap, sp);
 }
 
+// Encode v9 LDS: row image, the payload-size table, the partial null-bit words.
+size_t flat9_lds(const VarLaunch& L, int cap, int nw) {
+  return (size_t)cap + (size_t)L.num_var * 64 * sizeof(int32_t) + (size_t)nw * 64 * (L.bitmap_bytes >> 2) * 4;
+}
+
+// Plans encode v9 takes: fixed fields and strings / binary only, one fixed batch per wave.
+bool flat9_fits(const VarLaunch& L, int nw) {
+  return !L.num_struct && !L.num_list && L.num_var >= 1 && L.num_var <= 2 * nw && L.fix_group[4] >= 1 &&
+         L.fix_group[4] <= kFixBatch * nw &&
+         L.bitmap_bytes <= 4 * kV9Bmw;
+}
+
+template <int HDR, int NW>
+void launch_flat_enc9(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
+                      int cap, hipStream_t s) {
+  VarLaunch L = L0;
+  L.pl_all = 1;
+  // FORY_ROWFMT_VARENC=9: 2 tiles per workgroup, =11: 3, =10: 2 held to 4 workgroups per CU
+  auto* k = L.kn.var_enc == 10   ? &var_encode_flat9_lean_kernel<HDR, NW, 2, 2>
+            : L.kn.var_enc == 11 ? &var_encode_flat9_kernel<HDR, NW, 2, 3>
+                                 : &var_encode_flat9_kernel<HDR, NW, 2, 2>;
+  const int K = L.kn.var_enc == 11 ? 3 : 2;
+  const size_t lds = flat9_lds(L, cap, NW);
+  raise_lds_cap(k);
+  auto* k2 = &var_encode_flat_kernel<HDR, NW, false, true>;  // tiles beyond the image
+  L.stg_bytes = enc_stg_bytes(k2, L, capacity, cap, NW);
+  const SpillArgs sp = spill_args(L, cap);
+  (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
+  var_diag(L, "encode v9", k, 64 * NW, cap, 0, lds);
+  const unsigned grid = (unsigned)(((L.num_rows + 63) / 64 + K - 1) / K);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix, L.vf, offs, out, capacity,
+                     status, cap, sp);
+  raise_lds_cap(k2);
+  hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds_enc(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
+                     flat_lds_enc(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status,
+                     sp.cap, sp);
+}
+
 template <int HDR, int NW, bool NEST>
 void launch_flat_enc7_own(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                           int cap, hipStream_t s) {
@@ -3385,7 +3814,9 @@ void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int6
   if (L.num_struct) {
     if (v7) launch_flat_enc7_own<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
     else launch_flat_enc_t<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
-  } else if (v7 && L.fix16 && L.kn.var_enc != 7 && L.num_rows >= 128) {
+  } else if (L.kn.var_enc >= 9 && L.kn.var_enc <= 11 && flat9_fits(L, NW)) {
+    launch_flat_enc9<HDR, NW>(L, offs, out, capacity, status, cap, s);
+  } else if (v7 && L.fix16 && L.kn.var_enc == 8 && L.num_rows >= 128) {
     if (L.num_var <= 2 * NW) launch_flat_enc8<HDR, NW, 2>(L, offs, out, capacity, status, cap, s);
     else launch_flat_enc8<HDR, NW, kOwnVar>(L, offs, out, capacity, status, cap, s);
   } else {
