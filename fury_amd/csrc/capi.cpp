@@ -457,6 +457,9 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   for (const fory_amd::VarFieldDev& v : var) est = std::max(est, v.is_list ? 16 * v.w + 2 : 32);
   L->var_est_row = est;
   L->iv_split = var.size() == 1 && var[0].is_list && var[0].out_item_validity ? 1 : 0;
+  L->nullable = 0;
+  for (const FixedFieldDev& f : fix) L->nullable |= f.validity ? 1 : 0;
+  for (const fory_amd::VarFieldDev& v : var) L->nullable |= v.validity ? 2 : 0;
   L->fix16 = 1;
   for (const FixedFieldDev& f : fix)
     if ((reinterpret_cast<uintptr_t>(f.values) & 15) || (reinterpret_cast<uintptr_t>(f.validity) & 7)) L->fix16 = 0;

@@ -12,7 +12,7 @@ __device__ __forceinline__ int32_t gbm(int64_t n) { return (int32_t)(((n + 63) >
 __device__ __forceinline__ int64_t gr8(int64_t n) { return (n + 7) & ~int64_t(7); }
 
 __device__ __forceinline__ bool gvalid(const uint8_t* validity, int64_t i) {
-  return !validity || ((validity[i >> 3] >> (i & 7)) & 1);
+  return !validity || ((gp(validity)[i >> 3] >> (i & 7)) & 1);
 }
 
 // Row bytes at p: 8-byte values are 4-byte aligned at least (frame rows start 12
@@ -47,7 +47,7 @@ __device__ __forceinline__ void gzero(uint8_t* p, int64_t n) {  // p 4-byte alig
 // the string (never outside the mapped buffer), funnel-shifted into dword stores.
 __device__ __forceinline__ void g_put_bytes(uint8_t* dst, const uint8_t* src, int64_t n) {
   const int sh = (int)(reinterpret_cast<uintptr_t>(src) & 3);
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(src - sh);
+  const GAS uint32_t* s = gp(reinterpret_cast<const uint32_t*>(src - sh));  // (an Arrow column)
   const int64_t nw = (n + 3) >> 2;
   uint32_t lo = nw > 0 ? s[0] : 0u;
   for (int64_t k = 0; k < nw; ++k) {
@@ -68,15 +68,16 @@ __device__ __forceinline__ void g_put_bytes(uint8_t* dst, const uint8_t* src, in
 
 // Row bytes (4-byte aligned source) to an Arrow values buffer of any alignment:
 // byte head to a 4-byte boundary, dword body (funnel-shifted source), byte tail.
-__device__ __forceinline__ void g_get_bytes(uint8_t* dst, const uint8_t* src, int64_t n) {
+__device__ __forceinline__ void g_get_bytes(uint8_t* dst0, const uint8_t* src, int64_t n) {
+  GAS uint8_t* dst = gp(dst0);  // (an Arrow values buffer)
   int64_t b = 0;
-  for (; b < n && (reinterpret_cast<uintptr_t>(dst + b) & 3); ++b) dst[b] = src[b];
+  for (; b < n && (reinterpret_cast<uintptr_t>(dst0 + b) & 3); ++b) dst[b] = src[b];
   const int ph = (int)(b & 3);  // src + b phase (src aligned)
   const uint32_t* s = reinterpret_cast<const uint32_t*>(src + b - ph);
   for (int64_t k = 0; b + 4 <= n; b += 4, ++k) {
     uint32_t w = s[k];
     if (ph) w = (uint32_t)((((uint64_t)s[k + 1] << 32) | w) >> (8 * ph));
-    st32(dst + b, w);
+    *reinterpret_cast<GAS uint32_t*>(dst + b) = w;
   }
   for (; b < n; ++b) dst[b] = src[b];
 }
@@ -141,7 +142,7 @@ __device__ int64_t g_sizes(const GenLaunch& L, int64_t i, bool* overflow) {
     const ColumnDev& c = L.cols[node];
     if ((nd.flags & 1) && !gvalid(c.validity, pos)) return;
     if (nd.kind == KIND_BYTES) {
-      total += gr8((int64_t)c.offsets[pos + 1] - c.offsets[pos]);
+      total += gr8((int64_t)gp(c.offsets)[pos + 1] - gp(c.offsets)[pos]);
     } else if (nd.kind == KIND_DECIMAL) {
       total += 32;
     } else if (nd.kind == KIND_STRUCT) {
@@ -153,7 +154,7 @@ __device__ int64_t g_sizes(const GenLaunch& L, int64_t i, bool* overflow) {
       f.end = nd.end;
       f.pos = pos;
     } else if (nd.kind == KIND_LIST || nd.kind == KIND_MAP) {
-      const int64_t e0 = c.offsets[pos], n = (int64_t)c.offsets[pos + 1] - e0;
+      const int64_t e0 = gp(c.offsets)[pos], n = (int64_t)gp(c.offsets)[pos + 1] - e0;
       if (nd.kind == KIND_LIST) {
         array(node + 1, e0, n);
       } else {
@@ -166,7 +167,7 @@ __device__ int64_t g_sizes(const GenLaunch& L, int64_t i, bool* overflow) {
   };
   if (L.frame == FORY_FRAME_COLLECTION) {  // [i32 size][the single field's BinaryArray / BinaryMap]
     const ColumnDev& c = L.cols[0];
-    const int64_t e0 = c.offsets[i], n = (int64_t)c.offsets[i + 1] - e0;
+    const int64_t e0 = gp(c.offsets)[i], n = (int64_t)gp(c.offsets)[i + 1] - e0;
     total = 4;
     if (L.nodes[0].kind == KIND_LIST) {
       array(1, e0, n);
@@ -277,7 +278,7 @@ __device__ int32_t g_encode(const GenLaunch& L, uint8_t* row, int64_t i) {
         return;
       }
       case KIND_BYTES: {
-        const int64_t s0 = c.offsets[pos], n = (int64_t)c.offsets[pos + 1] - s0;
+        const int64_t s0 = gp(c.offsets)[pos], n = (int64_t)gp(c.offsets)[pos + 1] - s0;
         g_put_bytes(row + wi, c.values + s0, n);
         gput(row + slot, ((uint64_t)rel << 32) | (uint32_t)n, 8);
         wi += (int32_t)gr8(n);
@@ -317,12 +318,12 @@ __device__ int32_t g_encode(const GenLaunch& L, uint8_t* row, int64_t i) {
         return;
       }
       case KIND_LIST: {
-        const int64_t e0 = c.offsets[pos], n = (int64_t)c.offsets[pos + 1] - e0;
+        const int64_t e0 = gp(c.offsets)[pos], n = (int64_t)gp(c.offsets)[pos + 1] - e0;
         open_array(F_ARRAY, node, node + 1, e0, n, slot, rel, wi);
         return;
       }
       case KIND_MAP: {  // serializeForMap: reserve 8 bytes, key array, back-patch, value array
-        const int64_t e0 = c.offsets[pos], n = (int64_t)c.offsets[pos + 1] - e0;
+        const int64_t e0 = gp(c.offsets)[pos], n = (int64_t)gp(c.offsets)[pos + 1] - e0;
         const int32_t off = wi;
         wi += 8;
         open_array(F_MAP_KEYS, node, node + 1, e0, n, slot, rel, off);
@@ -333,7 +334,7 @@ __device__ int32_t g_encode(const GenLaunch& L, uint8_t* row, int64_t i) {
   };
   if (L.frame == FORY_FRAME_COLLECTION) {  // ArrayEncoder / MapEncoder.encode(MemoryBuffer, T)
     const ColumnDev& c = L.cols[0];
-    const int64_t e0 = c.offsets[i], n = (int64_t)c.offsets[i + 1] - e0;
+    const int64_t e0 = gp(c.offsets)[i], n = (int64_t)gp(c.offsets)[i + 1] - e0;
     if (L.nodes[0].kind == KIND_LIST) {
       open_array(F_ARRAY, 0, 1, e0, n, -1, 0, 0);
     } else {

@@ -145,7 +145,7 @@ struct Node {
 //   FORY_ROWFMT_SIZES_PROGRAM  sizes by the op-program walk for flat plans too
 //   FORY_ROWFMT_IDXFRAMES   frames per frame-index chunk
 //   FORY_ROWFMT_VARPROF=1   phase timeline (debug), FORY_ROWFMT_VARDIAG=1 LDS sizing to stderr
-//   FORY_ROWFMT_VARENC=1|7  flat plans encode with the round-3 tile kernel / encode v7 instead of v8
+//   FORY_ROWFMT_VARENC=1|7|8|9|10  encode with the round-3 tile kernel / v7 / v8 / v9 / v9 at 128 VGPRs
 struct LaunchKnobs {
   int32_t no_tiles;
   int32_t no_flat;
@@ -158,7 +158,7 @@ struct LaunchKnobs {
   int32_t idx_frames;
   int32_t prof;
   int32_t diag;
-  int32_t var_enc;   // FORY_ROWFMT_VARENC=1: flat plans keep the round-3 encode tile kernel, =7: encode v7 (A/B); else v8 where it applies
+  int32_t var_enc;   // FORY_ROWFMT_VARENC (A/B): 0 = defaults of launch_flat_enc, 1 / 7 / 8 / 9 force a kernel
   int32_t dbg_skip;  // FORY_ROWFMT_DBGSKIP (debug, timing only; output wrong): 1 = tile kernels stop after their loads, 2 = encode v7 skips its image store
   int32_t var_xcd;   // FORY_ROWFMT_VARXCD=C: varlen tile kernels take tiles in XCD runs of C (-1: one run per XCD), 0 = dispatch order
   int32_t dec_regs;  // FORY_ROWFMT_DECREGS=1: varlen decode stages its tile rows through registers, not LDS-DMA (A/B)

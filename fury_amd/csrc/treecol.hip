@@ -45,9 +45,9 @@ __device__ __forceinline__ int64_t tc_size(const TcTables* T, int c, const GNode
                                            int64_t k) {
   if (nd.kind == KIND_BYTES || nd.kind == KIND_DECIMAL) {
     if ((nd.flags & 1) && !gvalid(col.validity, k)) return 0;
-    return nd.kind == KIND_DECIMAL ? 32 : gr8((int64_t)col.offsets[k + 1] - col.offsets[k]);
+    return nd.kind == KIND_DECIMAL ? 32 : gr8((int64_t)gp(col.offsets)[k + 1] - gp(col.offsets)[k]);
   }
-  return T->A[c][k];
+  return gp(T->A[c])[k];
 }
 
 __device__ __forceinline__ int64_t tc_clamp(int64_t k, int64_t m) { return k < 0 ? 0 : (k > m ? m : k); }
@@ -58,7 +58,7 @@ __device__ __forceinline__ int64_t tc_array_bytes(const GenLaunch& L, const TcTa
   const GNode it = L.nodes[x];
   const int64_t n = o1 - o0;
   int64_t b = 8 + gbm(n) + gr8(n * elem_size(it));
-  if (tc_is_var(it.kind)) b += T->A[x][o1] - T->A[x][o0];
+  if (tc_is_var(it.kind)) b += gp(T->A[x])[o1] - gp(T->A[x])[o0];
   return b;
 }
 
@@ -70,7 +70,7 @@ __device__ __forceinline__ bool tc_items(const GenLaunch& L, const TcTables* T, 
                                          int64_t* o1) {
   const int32_t* off = L.cols[c].offsets;
   const int64_t mx = T->m[c + 1];
-  const int64_t ra = off[j], rb = off[j + 1];
+  const int64_t ra = gp(off)[j], rb = gp(off)[j + 1];
   const int64_t a = tc_clamp(ra, mx), b = tc_clamp(rb, mx);
   *o0 = a;
   *o1 = b < a ? a : b;
@@ -88,7 +88,7 @@ __device__ __forceinline__ int64_t tc_node_size(const GenLaunch& L, const TcTabl
   const ColumnDev col = L.cols[c];
   if (!root_coll && (nd.flags & 1) && !gvalid(col.validity, j)) return 0;
   switch (nd.kind) {
-    case KIND_BYTES: return gr8((int64_t)col.offsets[j + 1] - col.offsets[j]);
+    case KIND_BYTES: return gr8((int64_t)gp(col.offsets)[j + 1] - gp(col.offsets)[j]);
     case KIND_DECIMAL: return 32;
     case KIND_STRUCT: {
       int64_t s = gbm(nd.nchild) + 8LL * nd.nchild;
@@ -111,7 +111,7 @@ __device__ __forceinline__ int64_t tc_node_size(const GenLaunch& L, const TcTabl
 
 // Row / frame i's bytes.
 __device__ __forceinline__ int64_t tc_row_size(const GenLaunch& L, const TcTables* T, int64_t i) {
-  if (L.frame == FORY_FRAME_COLLECTION) return 4 + T->A[0][i];
+  if (L.frame == FORY_FRAME_COLLECTION) return 4 + gp(T->A[0])[i];
   int64_t s = frame_header_bytes(L.frame) + L.fixed_size;
   for (int t = 0; t < L.num_nodes; t = L.nodes[t].end) {
     const GNode tn = L.nodes[t];
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(kTcWG) void tc_sizes_kernel(GenLaunch L, const TcTa
                                                          int64_t m, int root_coll) {
   const int64_t j = (int64_t)blockIdx.x * kTcWG + threadIdx.x;
   if (j >= m) return;
-  T->A[c][j] = tc_node_size(L, T, c, j, root_coll);
+  gp(T->A[c])[j] = tc_node_size(L, T, c, j, root_coll);
 }
 
 // Sizes + exclusive scan, reduce-then-scan in three launches (no cross-workgroup waits:
@@ -251,7 +251,7 @@ __device__ __forceinline__ void tc_put(uint8_t* p, uint64_t v, int w) {
 
 // Slot size field of a var value: a string's byte length, else its bytes (decimals 32).
 __device__ __forceinline__ uint32_t tc_slot_size(const GNode& nd, const ColumnDev& col, int64_t k, int64_t bytes) {
-  if (nd.kind == KIND_BYTES) return (uint32_t)(col.offsets[k + 1] - col.offsets[k]);
+  if (nd.kind == KIND_BYTES) return (uint32_t)(gp(col.offsets)[k + 1] - gp(col.offsets)[k]);
   return (uint32_t)bytes;
 }
 
@@ -264,7 +264,7 @@ __device__ __forceinline__ void tc_copy(uint8_t* dst, const uint8_t* src, int64_
     return;
   }
   const int sh = (int)(reinterpret_cast<uintptr_t>(src) & 3);
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(src - sh);
+  const GAS uint32_t* s = gp(reinterpret_cast<const uint32_t*>(src - sh));  // (an Arrow column)
   const int nin = (sh + (int)n + 3) >> 2;  // source dwords holding string bytes
   const int nout = (int)(gr8(n) >> 2);     // output dwords (string + padding)
   uint32_t w[kW + 1];
@@ -289,14 +289,15 @@ __device__ __forceinline__ void tc_copy(uint8_t* dst, const uint8_t* src, int64_
 __device__ __forceinline__ int32_t tc_leaf_write(uint8_t* out, const GNode& nd, const ColumnDev& col, int64_t k,
                                                  int64_t at, int64_t S) {
   if (nd.kind == KIND_BYTES) {
-    const int64_t s0 = col.offsets[k], n = (int64_t)col.offsets[k + 1] - s0;
+    const int64_t s0 = gp(col.offsets)[k], n = (int64_t)gp(col.offsets)[k + 1] - s0;
     if (n < 0 || gr8(n) != S) return FORY_ERR_ENCODER;
     tc_copy(out + at, col.values + s0, n);
     return 0;
   }
   if (S != 32) return FORY_ERR_ENCODER;
   const uint8_t* x = col.values + 16 * k;
-  const uint32_t w[4] = {ld32(x), ld32(x + 4), ld32(x + 8), ld32(x + 12)};
+  const GAS uint32_t* xg = gp(reinterpret_cast<const uint32_t*>(x));  // (an Arrow decimal column)
+  const uint32_t w[4] = {xg[0], xg[1], xg[2], xg[3]};
   if (!g_dec_fits(w, nd.prec)) return FORY_ERR_UNSUPPORTED;
   const uint32_t ext = (w[3] >> 31) ? 0xffffffffu : 0u;
   for (int q = 0; q < 4; ++q) st32(out + at + 4 * q, w[q]);
@@ -403,14 +404,14 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_kernel(GenLaunch L, con
     if (bad && q == 0) set_status(status, FORY_ERR_CAPACITY);
     P = bad ? -1 : beg + hdr;
   } else {
-    P = T->P[c][k];
+    P = gp(T->P[c])[k];
     if (P >= 0 && P + bm + 8LL * nf > cap) {
       if (q == 0) set_status(status, FORY_ERR_ENCODER);
       P = -1;
     }
   }
   if (P < 0) {
-    if (has_pos) T->P[kid][k] = -1;
+    if (has_pos) gp(T->P[kid])[k] = -1;
     return;
   }
   const int64_t fixed_end = P + bm + 8LL * nf;
@@ -431,7 +432,7 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_kernel(GenLaunch L, con
   uint8_t* slot = out + P + bm + 8 * q;
   if (isnull) {  // BinaryWriter.setNullAt: slot zero
     tc_put(slot, 0, 8);
-    if (has_pos) T->P[kid][k] = -1;
+    if (has_pos) gp(T->P[kid])[k] = -1;
     return;
   }
   if (!var) {
@@ -442,12 +443,12 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_kernel(GenLaunch L, con
   if (S < 0 || at + S > cap) {
     set_status(status, FORY_ERR_ENCODER);
     tc_put(slot, 0, 8);
-    if (has_pos) T->P[kid][k] = -1;
+    if (has_pos) gp(T->P[kid])[k] = -1;
     return;
   }
   tc_put(slot, ((uint64_t)(at - P) << 32) | tc_slot_size(nd, col, k, S), 8);
   if (has_pos) {
-    T->P[kid][k] = at;
+    gp(T->P[kid])[k] = at;
   } else {
     const int32_t r = tc_leaf_write(out, nd, col, k, at, S);
     if (r) set_status(status, r);
@@ -500,7 +501,7 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_lds_kernel(GenLaunch L,
       if (bad) set_status(status, FORY_ERR_CAPACITY);
       else P = beg + hdr;
     } else {
-      P = T->P[c][k];
+      P = gp(T->P[c])[k];
       if (P >= 0 && P + bm + 8LL * nf > cap) {
         set_status(status, FORY_ERR_ENCODER);
         P = -1;
@@ -546,7 +547,7 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_lds_kernel(GenLaunch L,
         if (nu) img[hdr + (q >> 3)] |= (uint8_t)(1u << (q & 7));
         st32(slot, 0u);
         st32(slot + 4, 0u);
-        if (inb && has_pos) T->P[kid][k] = -1;
+        if (inb && has_pos) gp(T->P[kid])[k] = -1;
         continue;
       }
       if (!tc_is_var(nd.kind)) {
@@ -560,7 +561,7 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_lds_kernel(GenLaunch L,
         set_status(status, FORY_ERR_ENCODER);
         st32(slot, 0u);
         st32(slot + 4, 0u);
-        if (has_pos) T->P[kid][k] = -1;
+        if (has_pos) gp(T->P[kid])[k] = -1;
         continue;
       }
       const uint64_t sw = ((uint64_t)(at - P) << 32) | tc_slot_size(nd, s_col[q], kk, Su);
@@ -568,7 +569,7 @@ __global__ __launch_bounds__(kTcWG) void tc_write_fields_lds_kernel(GenLaunch L,
       st32(slot + 4, (uint32_t)(sw >> 32));
       rel += Su;
       if (has_pos) {
-        T->P[kid][k] = at;
+        gp(T->P[kid])[k] = at;
       } else {
         const int32_t r = tc_leaf_write(out, nd, s_col[q], kk, at, Su);
         if (r) set_status(status, r);
@@ -608,10 +609,10 @@ __global__ __launch_bounds__(kTcWG) void tc_write_coll_kernel(GenLaunch L, const
   if (i >= L.num_rows) return;
   const int64_t beg = offs[i], end = offs[i + 1], size = end - beg;
   const bool bad = beg < 0 || end > cap || size < 4 || size - 4 > 0x7fffffffLL || (beg & 3) ||
-                   4 + T->A[0][i] > size;
+                   4 + gp(T->A[0])[i] > size;
   if (bad) set_status(status, FORY_ERR_CAPACITY);
   else st32(out + beg, (uint32_t)(size - 4));
-  T->P[0][i] = bad ? -1 : beg + 4;
+  gp(T->P[0])[i] = bad ? -1 : beg + 4;
 }
 
 // The null bitmap of items [o0, o0 + n) (1 = null, BinaryArrayWriter.setNullAt) from their
@@ -643,7 +644,7 @@ struct TcVwin {
 __device__ __forceinline__ TcVwin tc_vwin(const uint8_t* validity, int64_t o0, int64_t o1) {
   TcVwin r{{0u, 0u, 0u}};
   if (!validity) return r;
-  const uint32_t* v = reinterpret_cast<const uint32_t*>(validity) + (o0 >> 5);
+  const GAS uint32_t* v = gp(reinterpret_cast<const uint32_t*>(validity)) + (o0 >> 5);
 #pragma unroll
   for (int t = 0; t < 3; ++t)
     if (((o0 >> 5) + t) * 32 < o1) r.w[t] = v[t];
@@ -699,7 +700,7 @@ __device__ __forceinline__ int32_t tc_element(const GenLaunch& L, const TcTables
   }
   if (isnull) {  // null: zero element (the header set the bit)
     tc_put(el, 0, es);
-    if (var && !leaf) T->P[x][e] = -1;
+    if (var && !leaf) gp(T->P[x])[e] = -1;
     return 0;
   }
   if (!var) {
@@ -711,12 +712,12 @@ __device__ __forceinline__ int32_t tc_element(const GenLaunch& L, const TcTables
   const int64_t at = Pa + hb + gr8(n * 8) + (a0 - ab);
   if (S < 0 || at + S > cap) {
     tc_put(el, 0, 8);
-    if (!leaf) T->P[x][e] = -1;
+    if (!leaf) gp(T->P[x])[e] = -1;
     return FORY_ERR_ENCODER;
   }
   tc_put(el, ((uint64_t)(at - Pa) << 32) | tc_slot_size(it, col, e, S), 8);
   if (leaf) return tc_leaf_write(out, it, col, e, at, S);
-  T->P[x][e] = at;
+  gp(T->P[x])[e] = at;
   return 0;
 }
 
@@ -739,7 +740,7 @@ __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const
   if (tid < cnt) {
     const int64_t j = j0 + tid;
     int64_t o0, o1;
-    int64_t P = T->P[c][j];
+    int64_t P = gp(T->P[c])[j];
     // offsets past the items' column length (a short fory_column.length): an error, not a
     // silently shorter array (present containers only: absent ones read no items)
     if (!tc_items(L, T, c, j, &o0, &o1) && P >= 0) err = FORY_ERR_INVALID_ARGUMENT;
@@ -784,8 +785,8 @@ __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const
     const int64_t P = sP[a];
     const int64_t o0 = sO[a], n = sO[a + 1] - o0;
     if (P < 0 || e >= o0 + n) {  // absent container (or items between non-adjacent ranges)
-      if (kvar) T->P[key][e] = -1;
-      if (vvar) T->P[val][e] = -1;
+      if (kvar) gp(T->P[key])[e] = -1;
+      if (vvar) gp(T->P[val])[e] = -1;
       continue;
     }
     int32_t r;
@@ -801,13 +802,13 @@ __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const
   // items no container of the call references: no position
   if (blockIdx.x == 0 && (kvar || vvar))
     for (int64_t e = tid; e < e0; e += kTcWG) {
-      if (kvar) T->P[key][e] = -1;
-      if (vvar) T->P[val][e] = -1;
+      if (kvar) gp(T->P[key])[e] = -1;
+      if (vvar) gp(T->P[val])[e] = -1;
     }
   if (j0 + cnt == m && (kvar || vvar))
     for (int64_t e = e1 + tid; e < mx; e += kTcWG) {
-      if (kvar) T->P[key][e] = -1;
-      if (vvar) T->P[val][e] = -1;
+      if (kvar) gp(T->P[key])[e] = -1;
+      if (vvar) gp(T->P[val])[e] = -1;
     }
   if (err) set_status(status, err);
 }

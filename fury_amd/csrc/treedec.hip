@@ -46,11 +46,11 @@ __device__ __forceinline__ void td_valid_words(uint8_t* validity, int64_t pos, b
   if (!r) return;
   uint32_t* word = reinterpret_cast<uint32_t*>(validity) + (pos >> 5);
   if (r == 0xffffffffu) {
-    *word = v;
+    *gp(word) = v;
     return;
   }
-  if (v) atomicOr(word, v);
-  if (r & ~v) atomicAnd(word, ~(r & ~v));
+  if (v) g_or(word, v);
+  if (r & ~v) g_and(word, ~(r & ~v));
 }
 
 // Array header at `at` bounded by lim: numElements, or -1 (g_array_n).
@@ -99,8 +99,8 @@ __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, 
       if (rel < 0 || start + gbm(nd.nchild) + 8LL * nd.nchild > rend) set_status(status, FORY_ERR_CORRUPT);
       else P = start;
     }
-    T->P[f][k] = P;
-    T->TL[f][k] = P < 0 ? 0 : (int32_t)(rend - P);
+    gp(T->P[f])[k] = P;
+    gp(T->TL[f])[k] = P < 0 ? 0 : (int32_t)(rend - P);
     return;
   }
   if (nd.kind == KIND_DECIMAL) {  // UnsafeTrait.getDecimal: 32 bytes, the high 16 the sign extension
@@ -122,7 +122,7 @@ __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, 
         return;
       }
     }
-    for (int q = 0; q < 4; ++q) st32(col.out_values + 16 * k + 4 * q, w[q]);
+    for (int q = 0; q < 4; ++q) *gp(reinterpret_cast<uint32_t*>(col.out_values + 16 * k + 4 * q)) = w[q];
     return;
   }
   // BYTES / LIST / MAP: (offset, size) relative to the enclosing row / array
@@ -133,13 +133,13 @@ __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, 
     size = (int64_t)(int32_t)(uint32_t)os;
     if ((int32_t)(os >> 32) < 0 || size < 0 || at + size > rend) {
       set_status(status, FORY_ERR_CORRUPT);
-      if (nd.kind != KIND_BYTES && (values || nd.cdepth <= level)) T->P[f][k] = -1;
+      if (nd.kind != KIND_BYTES && (values || nd.cdepth <= level)) gp(T->P[f])[k] = -1;
       return;
     }
   }
   if (!values) {
     if (nd.cdepth > level) return;
-    if (nd.kind == KIND_BYTES && nd.cdepth == level && T->SRC[f]) T->SRC[f][k] = isnull ? -1 : at;  // for td_strings
+    if (nd.kind == KIND_BYTES && nd.cdepth == level && T->SRC[f]) gp(T->SRC[f])[k] = isnull ? -1 : at;  // for td_strings
     if (nd.cdepth == level && col.out_offsets) {  // this level's counts
       int64_t cnt = 0;
       if (!isnull) {
@@ -154,24 +154,24 @@ __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, 
           }
         }
       }
-      col.out_offsets[k + 1] = (int32_t)cnt;
+      gp(col.out_offsets)[k + 1] = (int32_t)cnt;
     }
     if (nd.kind == KIND_BYTES) return;
     // a list / map: its position too, for the next level's items pass
   }
   if (nd.kind == KIND_BYTES) {
     if (isnull) return;
-    const int64_t o0 = col.out_offsets[k];
-    if ((int64_t)col.out_offsets[k + 1] - o0 != size) {  // differs from the sizes pass
+    const int64_t o0 = gp(col.out_offsets)[k];
+    if ((int64_t)gp(col.out_offsets)[k + 1] - o0 != size) {  // differs from the sizes pass
       set_status(status, FORY_ERR_CORRUPT);
       return;
     }
     g_get_bytes(col.out_values + o0, rows + at, size);
     return;
   }
-  T->P[f][k] = isnull ? -1 : at;
-  T->SZ[f][k] = (int32_t)size;
-  T->TL[f][k] = isnull ? 0 : (int32_t)(rend - at);
+  gp(T->P[f])[k] = isnull ? -1 : at;
+  gp(T->SZ[f])[k] = (int32_t)size;
+  gp(T->TL[f])[k] = isnull ? 0 : (int32_t)(rend - at);
 }
 
 // A scalar of width w from the slot's low bytes (UnsafeTrait.getX), 0 for nulls.
@@ -267,8 +267,8 @@ __global__ __launch_bounds__(kTdWG) void td_fields_kernel(GenLaunch L, const TdT
         rend = end;
       }
     } else {
-      base = T->P[s][k];
-      rend = base >= 0 ? base + T->TL[s][k] : 0;
+      base = gp(T->P[s])[k];
+      rend = base >= 0 ? base + gp(T->TL[s])[k] : 0;
     }
   }
   if (FS > 0) {  // the wave's bitmaps + slots staged by consecutive dwords of each instance
@@ -324,11 +324,11 @@ __global__ __launch_bounds__(kTdWG) void td_coll_kernel(GenLaunch L, const TdTab
         cnt = 0;
       }
     }
-    if (col.out_offsets) col.out_offsets[i + 1] = (int32_t)cnt;
+    if (col.out_offsets) gp(col.out_offsets)[i + 1] = (int32_t)cnt;
   }
-  T->P[0][i] = present ? beg + 4 : -1;
-  T->SZ[0][i] = present ? (int32_t)(len - 4) : 0;
-  T->TL[0][i] = present ? (int32_t)(len - 4) : 0;
+  gp(T->P[0])[i] = present ? beg + 4 : -1;
+  gp(T->SZ[0])[i] = present ? (int32_t)(len - 4) : 0;
+  gp(T->TL[0])[i] = present ? (int32_t)(len - 4) : 0;
 }
 
 // List / map node c: a workgroup per kTdWG containers; headers, then the elements.
@@ -349,11 +349,11 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
   const int level = L.fill_level;
   if (tid < cnt) {
     const int64_t j = j0 + tid;
-    const int64_t P = T->P[c][j];
-    const int64_t o0 = col.out_offsets[j], o1 = col.out_offsets[j + 1];
+    const int64_t P = gp(T->P[c])[j];
+    const int64_t o0 = gp(col.out_offsets)[j], o1 = gp(col.out_offsets)[j + 1];
     int64_t kat = -1, vat = -1;
     if (P >= 0) {
-      const int64_t n = td_container_n(L, rows, c, P, T->SZ[c][j], &kat, &vat);
+      const int64_t n = td_container_n(L, rows, c, P, gp(T->SZ[c])[j], &kat, &vat);
       if (n < 0 || n != o1 - o0) {  // corrupt, or the rows changed since the sizes pass
         set_status(status, FORY_ERR_CORRUPT);
         kat = vat = -1;
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
     }
     sK[tid] = kat;
     sV[tid] = vat;
-    sE[tid] = P >= 0 ? P + T->TL[c][j] : 0;
+    sE[tid] = P >= 0 ? P + gp(T->TL[c])[j] : 0;
     sO[tid] = (int32_t)o0;
     if (tid == cnt - 1) sO[cnt] = (int32_t)o1;
   }
@@ -438,8 +438,8 @@ __global__ __launch_bounds__(kTdWG) void td_strings_kernel(ColumnDev col, const 
   const int cnt = m - k0 < kTdWG ? (int)(m - k0) : kTdWG;
   int64_t my_o0 = 0, my_o1 = 0, my_s = -1;
   if (tid < cnt) {
-    my_o0 = col.out_offsets[k0 + tid];
-    my_o1 = col.out_offsets[k0 + tid + 1];
+    my_o0 = gp(col.out_offsets)[k0 + tid];
+    my_o1 = gp(col.out_offsets)[k0 + tid + 1];
     my_s = src[k0 + tid];
     sO[tid] = (int32_t)my_o0;
     sS[tid] = my_s;

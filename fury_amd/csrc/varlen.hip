@@ -2626,8 +2626,8 @@ constexpr int kV9Bmw = 4;  // bitmap words per row (<= 128 fields)
 template <int OWN>
 struct V9Cols {            // one tile's per-lane column registers
   int32_t e0[OWN], e1[OWN];
-  uint32_t vvb[OWN];       // owned var fields: the dword holding the record's validity byte
-  uint32_t fvb[kFixBatch]; // the wave's fixed batch: the same
+  uint32_t vvb[OWN];       // owned var fields: the dword holding the record's validity byte (NUL & 2)
+  uint32_t fvb[kFixBatch]; // the wave's fixed batch: the same (NUL & 1)
   int64_t beg, end;        // the record's row bounds
 };
 
@@ -2637,7 +2637,7 @@ struct V9Cols {            // one tile's per-lane column registers
       const int64_t* __restrict__ offs, uint8_t* __restrict__ out, int64_t capacity, int32_t* status, int cap, \
       SpillArgs sp
 
-template <int HDR, int NW, int OWN, int K>
+template <int HDR, int NW, int OWN, int K, int NUL>
 __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t* img = lds;
@@ -2666,12 +2666,15 @@ __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
       const VarFieldDev& f = vf[v];
       C.e0[k] = *gp(f.offsets + (lq ? iq : q0 + rw));  // dead lanes: the tile's end (empty ranges)
       C.e1[k] = *gp(f.offsets + (lq ? iq + 1 : q0 + rw));
-      C.vvb[k] = vbyte_issue(f.validity ? f.validity + (iq >> 3) : reinterpret_cast<const uint8_t*>(offs));
+      if constexpr ((NUL & 2) != 0)
+        C.vvb[k] = vbyte_issue(f.validity ? f.validity + (iq >> 3) : reinterpret_cast<const uint8_t*>(offs));
     }
+    if constexpr ((NUL & 1) != 0) {
 #pragma unroll
-    for (int k = 0; k < kFixBatch; ++k) {
-      const FixedFieldDev& f = fix[min(fa + k, fb - 1)];
-      C.fvb[k] = vbyte_issue(f.validity ? f.validity + (iq >> 3) : reinterpret_cast<const uint8_t*>(offs));
+      for (int k = 0; k < kFixBatch; ++k) {
+        const FixedFieldDev& f = fix[min(fa + k, fb - 1)];
+        C.fvb[k] = vbyte_issue(f.validity ? f.validity + (iq >> 3) : reinterpret_cast<const uint8_t*>(offs));
+      }
     }
     C.beg = offs[iq];
     C.end = offs[lq ? iq + 1 : q0];
@@ -2700,10 +2703,12 @@ __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
     for (int k = 0; k < OWN; ++k) {
       ready(C.e0[k]);
       ready(C.e1[k]);
-      ready(C.vvb[k]);
+      if constexpr ((NUL & 2) != 0) ready(C.vvb[k]);
     }
+    if constexpr ((NUL & 1) != 0) {
 #pragma unroll
-    for (int k = 0; k < kFixBatch; ++k) ready(C.fvb[k]);
+      for (int k = 0; k < kFixBatch; ++k) ready(C.fvb[k]);
+    }
     ready(C.beg);
     ready(C.end);
   };
@@ -2768,14 +2773,15 @@ __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
       for (int k = 0; k < OWN; ++k) {
         const int v = wave + k * NW;
         if (v >= L.num_var) continue;
-        const bool valid = !vf[v].validity || ((vbyte_get(C0.vvb[k], vf[v].validity + (ii >> 3)) >> (ii & 7)) & 1);
+        const bool valid =
+            (NUL & 2) == 0 || !vf[v].validity || ((vbyte_get(C0.vvb[k], vf[v].validity + (ii >> 3)) >> (ii & 7)) & 1);
         const int64_t n = (int64_t)C0.e1[k] - C0.e0[k];
         sz[v * 64 + lane] = !live ? -2 : !valid ? -1 : (int32_t)round8(n);
         if (live && !valid) null_bit(vf[v].slot);
       }
 #pragma unroll
       for (int k = 0; k < kFixBatch; ++k)
-        if (fk0 + k < fk1 && live && fix[fk0 + k].validity &&
+        if ((NUL & 1) && fk0 + k < fk1 && live && fix[fk0 + k].validity &&
             !((vbyte_get(C0.fvb[k], fix[fk0 + k].validity + (ii >> 3)) >> (ii & 7)) & 1))
           null_bit(fix[fk0 + k].slot);
       uint32_t* pw = pbt + (wave * 64 + lane) * bmw;
@@ -2826,7 +2832,8 @@ __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
         for (int k = 0; k < kFixBatch; ++k) {
           if (fk0 + k >= fk1) continue;
           const FixedFieldDev& f = fix[fk0 + k];
-          const bool valid = !f.validity || ((vbyte_get(C0.fvb[k], f.validity + (ii >> 3)) >> (ii & 7)) & 1);
+          const bool valid =
+              (NUL & 1) == 0 || !f.validity || ((vbyte_get(C0.fvb[k], f.validity + (ii >> 3)) >> (ii & 7)) & 1);
           uint64_t x = valid ? elem_value(f.values, f.width, ii, FV.lo[k], FV.hi[k]) : 0;
           if (f.flags & 2) x = x ? 1 : 0;
           st64_lds(slots + 8 * f.slot, x);
@@ -2860,12 +2867,8 @@ __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
           if (c < nc) str_store(row + pos[k], vf[v].values + C0.e0[k], n, c, T);
         }
       }
-    } else if (!skip) {  // unaligned or big tile: the spill launch, or per record from global
-      if (sane && !(mis & 3) && total <= sp.cap) {
-        if (tid == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)t;
-      } else if (wave == 0 && live) {
-        enc_record(L, prog, cols, r0 + lane, out + C0.beg, C0.end - C0.beg);
-      }
+    } else if (!skip && tid == 0) {  // unaligned or big tile: the spill launch (which takes tiles
+      sp.list[atomicAdd(sp.count, 1)] = (int32_t)t;  // beyond its own image per record)
     }
     V9_STAMP(3);
     sched_fence();
@@ -2902,16 +2905,16 @@ __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
 #undef V9_STAMP
 }
 
-template <int HDR, int NW, int OWN, int K>
+template <int HDR, int NW, int OWN, int K, int NUL>
 __global__ __launch_bounds__(64 * NW) void var_encode_flat9_kernel(FORY_V9_PARAMS) {
-  var_encode_flat9_body<HDR, NW, OWN, K>(L, prog, cols, fix, vf, offs, out, capacity, status, cap, sp);
+  var_encode_flat9_body<HDR, NW, OWN, K, NUL>(L, prog, cols, fix, vf, offs, out, capacity, status, cap, sp);
 }
 
 // (A/B, FORY_ROWFMT_VARENC=10) the same held to 128 VGPRs: 4 workgroups per CU, some spilled
-template <int HDR, int NW, int OWN, int K>
+template <int HDR, int NW, int OWN, int K, int NUL>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) void var_encode_flat9_lean_kernel(
     FORY_V9_PARAMS) {
-  var_encode_flat9_body<HDR, NW, OWN, K>(L, prog, cols, fix, vf, offs, out, capacity, status, cap, sp);
+  var_encode_flat9_body<HDR, NW, OWN, K, NUL>(L, prog, cols, fix, vf, offs, out, capacity, status, cap, sp);
 }
 
 
@@ -3777,11 +3780,17 @@ void launch_flat_enc9(const VarLaunch& L0, const int64_t* offs, uint8_t* out, in
                       int cap, hipStream_t s) {
   VarLaunch L = L0;
   L.pl_all = 1;
-  // FORY_ROWFMT_VARENC=9: 2 tiles per workgroup, =11: 3, =10: 2 held to 4 workgroups per CU
-  auto* k = L.kn.var_enc == 10   ? &var_encode_flat9_lean_kernel<HDR, NW, 2, 2>
-            : L.kn.var_enc == 11 ? &var_encode_flat9_kernel<HDR, NW, 2, 3>
-                                 : &var_encode_flat9_kernel<HDR, NW, 2, 2>;
-  const int K = L.kn.var_enc == 11 ? 3 : 2;
+  // FORY_ROWFMT_VARENC=9: 2 tiles per workgroup, =10: the same held to 4 workgroups per CU
+  using KFn = decltype(&var_encode_flat9_kernel<HDR, NW, 2, 2, 3>);
+  const bool lean = L.kn.var_enc == 10;
+  KFn k;
+  switch (L.nullable & 3) {
+    case 0: k = lean ? &var_encode_flat9_lean_kernel<HDR, NW, 2, 2, 0> : &var_encode_flat9_kernel<HDR, NW, 2, 2, 0>; break;
+    case 1: k = lean ? &var_encode_flat9_lean_kernel<HDR, NW, 2, 2, 1> : &var_encode_flat9_kernel<HDR, NW, 2, 2, 1>; break;
+    case 2: k = lean ? &var_encode_flat9_lean_kernel<HDR, NW, 2, 2, 2> : &var_encode_flat9_kernel<HDR, NW, 2, 2, 2>; break;
+    default: k = lean ? &var_encode_flat9_lean_kernel<HDR, NW, 2, 2, 3> : &var_encode_flat9_kernel<HDR, NW, 2, 2, 3>;
+  }
+  const int K = 2;
   const size_t lds = flat9_lds(L, cap, NW);
   raise_lds_cap(k);
   auto* k2 = &var_encode_flat_kernel<HDR, NW, false, true>;  // tiles beyond the image
@@ -3810,11 +3819,16 @@ void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int6
                      int cap, hipStream_t s) {
   // plans with nested struct fields and flat ones get their own instantiations: each
   // carries only its layout path (the other one's registers would count against it)
-  const bool v7 = L.kn.var_enc != 1 && L.num_var <= kOwnVar * NW;
+  // defaults (measured): plans with nested structs -> the round-3 tile kernel
+  // (Nested 0.74 vs v7 0.79 ms); flat plans of fixed fields + strings -> v9 (Mixed 3.2 vs
+  // v7 3.6, round 3 4.5 ms); other flat plans (lists) -> v7. FORY_ROWFMT_VARENC=1 / 7 / 9
+  // force round 3 / v7 / v9 where they apply, =8 encode v8.
+  const int e = L.kn.var_enc;
+  const bool v7 = e != 1 && L.num_var <= kOwnVar * NW;
   if (L.num_struct) {
-    if (v7) launch_flat_enc7_own<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
+    if (v7 && e == 7) launch_flat_enc7_own<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
     else launch_flat_enc_t<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
-  } else if (L.kn.var_enc >= 9 && L.kn.var_enc <= 11 && flat9_fits(L, NW)) {
+  } else if ((e == 0 || e == 9 || e == 10) && flat9_fits(L, NW)) {
     launch_flat_enc9<HDR, NW>(L, offs, out, capacity, status, cap, s);
   } else if (v7 && L.fix16 && L.kn.var_enc == 8 && L.num_rows >= 128) {
     if (L.num_var <= 2 * NW) launch_flat_enc8<HDR, NW, 2>(L, offs, out, capacity, status, cap, s);
