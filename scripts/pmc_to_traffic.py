@@ -1,7 +1,8 @@
 """profiles/pmc_latest.json from a scripts/profile.sh summary: per-launch HBM bytes of the
 bench's encode and decode kernels = FETCH_SIZE*1024*2 (gfx950 half-count correction,
 MI355X_MICROARCH.md §HBM; calibrated here: it equals the algorithmic read bytes exactly)
-+ WRITE_SIZE*1024. Usage: python scripts/pmc_to_traffic.py SUMMARY KEY [OUT]
++ WRITE_SIZE*1024, and the kernel trace's average launch duration of the same kernels
+(trace_ms). Usage: python scripts/pmc_to_traffic.py SUMMARY KEY [OUT [TRACE_SOURCE]]
 Each entry is stamped with lib_sha16 (the profiled libfory_rowfmt.so): bench.py reports
 the traffic only when the running build has the same hash."""
 import hashlib
@@ -28,6 +29,17 @@ for name, e in summ["pmc"].items():
         ent[role + "_kernel"] = name
         ent[role + "_fetch_bytes_x2"] = int(e["fetch_bytes_x2"])
         ent[role + "_write_bytes"] = int(e["write_bytes"])
+# the kernel trace of the same command (profile.sh's first pass): average launch duration
+# of each role's kernel, read by bench.py's roofline "trace" (trace_frac)
+kern = summ.get("kernels", {})
+tr = {}
+for role in ("encode", "decode"):
+    k = ent.get(role + "_kernel")
+    if k and k in kern:
+        tr[role] = round(kern[k]["avg_ns"] / 1e6, 4)
+if tr:
+    ent["trace_ms"] = tr
+    ent["trace_source"] = sys.argv[4] if len(sys.argv) > 4 else os.path.dirname(sys.argv[1])
 lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "fury_amd", "lib", "libfory_rowfmt.so")
 ent["lib_sha16"] = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
 cur[key] = ent

@@ -21,13 +21,13 @@ def rows(pattern):
 def short(name):
     import re
     m = re.search(r"(encode_fixed_\w*?kernel|decode_fixed_\w*?kernel|var_encode_kernel|var_decode_kernelILb[01]|"
-                  r"var_encode_tile_kernel|var_decode_tile_kernelILb[01]|var_encode_flat_lean_kernel|var_encode_flat_kernel|"
+                  r"var_encode_tile_kernel|var_decode_tile_kernelILb[01]|var_encode_flat\d?_lean_kernel|var_encode_flat\d?_kernel|"
                   r"var_decode_flat_kernel|"
                   r"var_sizes_kernel|scan_\w+?_kernel|fill_offsets_kernel|frame_\w+?_kernel|flat_tile_bases_kernel|"
                   r"gen_\w+?_kernel)", name)
     if m:
         k = m.group(1)
-        t = re.search(r"var_(?:en|de)code_flat_(?:lean_)?kernel<([^>]*)>", name)
+        t = re.search(r"var_(?:en|de)code_flat_(?:lean_)?kernel<([^>]*)>", name)  # (v7 / v9 have no spill form)
         if t and t.group(1).split(",")[-1].strip() == "true":
             k += "<spill>"  # the small big-image launch: kept apart from the main launch's averages
             if k.startswith("var_decode_flat_kernel"):
