@@ -15,9 +15,12 @@ from fury_amd import workloads as W  # noqa: E402
 from fury_amd.format.columns import HostColumn  # noqa: E402
 from fury_amd.format.native import HostPipeline, NativePlan, host_register, host_unregister  # noqa: E402
 
+# HOST_MEM=pageable: plain (unregistered) numpy buffers, so every copy goes through the
+# context's pinned staging blocks; default: the buffers are registered
+PAGEABLE = os.environ.get("HOST_MEM", "registered") == "pageable"
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8 * 1024 * 1024
 chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
-res = {"metric": "row-format encode+decode GiB/s, host-inclusive (C-ABI host path: pinned H2D + kernel + D2H)",
+res = {"host_memory": "pageable (staged)" if PAGEABLE else "registered", "metric": "row-format encode+decode GiB/s, host-inclusive (C-ABI host path: pinned H2D + kernel + D2H)",
        "rows": n, "chunk_rows": chunk}
 plan = NativePlan(W.struct_schema())
 vals = W.gen_struct_device(n)
@@ -30,7 +33,8 @@ for frame in (0, 1):
     rows = np.empty(n * stride, np.uint8)
     bufs = [c.values for c in host] + [c.values for c in back] + [rows]
     for b in bufs:
-        host_register(b)
+        if not PAGEABLE:
+            host_register(b)
     hp = HostPipeline(plan, chunk_rows=chunk)
     hp.encode(host, n, frame, rows)  # warm-up
     hp.decode(rows, n, frame, back)
@@ -45,7 +49,8 @@ for frame in (0, 1):
     ok = all(np.array_equal(a.values.view(np.uint8), b.values.view(np.uint8)) for a, b in zip(host, back))
     hp.close()
     for b in bufs:
-        host_unregister(b)
+        if not PAGEABLE:
+            host_unregister(b)
     t_enc, t_dec = min(te), min(td)
     col_bytes = sum(c.values.nbytes for c in host)
     row_bytes = n * stride

@@ -18,9 +18,12 @@ from fury_amd.format.columns import HostColumn, NP_DTYPE, validity_bytes  # noqa
 from fury_amd.format.native import HostPipeline, NativePlan, _check, host_register, host_unregister  # noqa: E402
 from fury_amd.format.types import ArrowType, preorder  # noqa: E402
 
+# HOST_MEM=pageable: plain (unregistered) numpy buffers, so every copy goes through the
+# context's pinned staging blocks; default: the buffers are registered
+PAGEABLE = os.environ.get("HOST_MEM", "registered") == "pageable"
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4 * 1024 * 1024
 lib = _lib.load()
-res = {"metric": "row-format encode+decode GiB/s, host-inclusive (C-ABI varlen host path, whole batch)", "rows": n}
+res = {"host_memory": "pageable (staged)" if PAGEABLE else "registered", "metric": "row-format encode+decode GiB/s, host-inclusive (C-ABI varlen host path, whole batch)", "rows": n}
 for config in ("mixed40", "nested"):
     schema = W.mixed_schema() if config == "mixed40" else W.nested_schema()
     host = W.mixed_host_columns(n, seed=23) if config == "mixed40" else W.nested_host_columns(n, seed=29)
@@ -50,7 +53,8 @@ for config in ("mixed40", "nested"):
     ro = np.empty(n + 1, np.int64)
     arrays += [out, ro]
     for a in arrays:
-        host_register(a)
+        if not PAGEABLE:
+            host_register(a)
     hin, hback = hp._host_array(host), hp._host_array(back)
     total = ctypes.c_int64(0)
     te, td, ti = [], [], []
@@ -73,7 +77,8 @@ for config in ("mixed40", "nested"):
         ti.append(time.perf_counter() - t0)
     ok = bool(np.array_equal(out, rows))
     for a in arrays:
-        host_unregister(a)
+        if not PAGEABLE:
+            host_unregister(a)
     hp.close()
     t_enc, t_dec, t_into = min(te[1:]), min(td[1:]), min(ti[1:])
     col_bytes = sum(a.nbytes for c in host for a in (c.values, c.offsets, c.validity) if a is not None)
