@@ -1323,6 +1323,15 @@ __device__ __forceinline__ void flat_place(const VarFieldDev& f, bool staged, co
   }
 }
 
+// A validity byte as the aligned dword holding it (a byte load's zero-extension would
+// be placed by the compiler right after the load, waiting for it there).
+__device__ __forceinline__ uint32_t vbyte_issue(const uint8_t* p) {
+  return *gp(reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(3)));
+}
+__device__ __forceinline__ uint32_t vbyte_get(uint32_t w, const uint8_t* p) {
+  return w >> (8 * (reinterpret_cast<uintptr_t>(p) & 3));
+}
+
 // Layout of record i for plans with nested struct fields (wave 0 of the encode
 // tile kernel): the per-record program walk of enc_record without the value
 // copies. One writerIndex is shared by the row and its child rows
@@ -1839,14 +1848,6 @@ __device__ __forceinline__ void ready(int32_t& x) { asm volatile("" : "+v"(x)); 
 __device__ __forceinline__ void ready(int64_t& x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
 
-// A validity byte as the aligned dword holding it (a byte load's zero-extension would
-// be placed by the compiler right after the load, waiting for it there).
-__device__ __forceinline__ uint32_t vbyte_issue(const uint8_t* p) {
-  return *gp(reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(3)));
-}
-__device__ __forceinline__ uint32_t vbyte_get(uint32_t w, const uint8_t* p) {
-  return w >> (8 * (reinterpret_cast<uintptr_t>(p) & 3));
-}
 
 __device__ __forceinline__ bool fix_valid(const FixedFieldDev& f, const FixRegs& R, int k, int64_t ii) {
   return !f.validity || ((R.vb[k] >> (ii & 7)) & 1);
@@ -3156,16 +3157,14 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
     }
     return;
   }
-  // tile-start Arrow offsets of every var field (written by decode_sizes): loaded
-  // now so their latency hides under the staging loads (lane v holds field v's)
-  int64_t obase = 0;
-  if (WRITE && lane < L.num_var) obase = *gp(vf[lane].out_offsets + r0);
+  int64_t obase = 0;  // tile-start Arrow offsets of every var field (lane v: field v's)
   {  // stage the tile's rows: LDS-DMA of whole 16-B chunks (1 KiB per wave
      // instruction, all in flight at once, nt policy for the once-read rows); the
      // edge chunks' bytes outside the tile (same 16-B blocks) are never read
     const uint8_t* g = in + B0 - mis;
     const int nch = (int)((total + 15) >> 4);
     if (L.kn.dec_regs) {  // A/B: non-temporal 16-B loads into registers, kDecRegs per thread in flight, then LDS
+      if (WRITE && lane < L.num_var) obase = *gp(vf[lane].out_offsets + r0);
       constexpr int kDecRegs = 8;
       const u32x4* g16 = reinterpret_cast<const u32x4*>(g);
       for (int c0 = 0; c0 < nch; c0 += 64 * NW * kDecRegs) {
@@ -3189,6 +3188,9 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
                                            (__attribute__((address_space(3))) void*)(img + (c0 + wave * 64) * 16), 16,
                                            0, 2);
       }
+      // the tile-start Arrow offsets (written by decode_sizes) behind the DMA: their
+      // table-pointer load and then the value load overlap the staging
+      if (WRITE && lane < L.num_var) obase = *gp(vf[lane].out_offsets + r0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
