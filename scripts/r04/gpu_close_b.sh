@@ -12,10 +12,12 @@ cp profiles/pmc_latest.json $O/pmc_latest.json
 for spec in struct104:67108864: mixed40:16777216: mixed40:16777216:--frame nested:8388608: nested:8388608:--frame; do
   cfg=${spec%%:*}; rest=${spec#*:}; rows=${rest%%:*}; fr=${rest#*:}
   tag=$cfg${fr:+_frame}; fbit=${fr:+1}; fbit=${fbit:-0}
-  OUT=$O/prof_$tag BENCH_EXTRA="--config $cfg $fr" ROWS=$rows bash scripts/profile.sh > $O/prof_$tag.log 2>&1
+  ex=""; [ "$cfg" = struct104 ] && ex="--extras 0"  # (its extra configs' kernels would mix into its summary)
+  OUT=$O/prof_$tag BENCH_EXTRA="--config $cfg $fr $ex" ROWS=$rows bash scripts/profile.sh > $O/prof_$tag.log 2>&1
   rc=$?; echo "prof $tag exit $rc"; [ $rc -eq 0 ] || exit $rc
   python3 scripts/pmc_to_traffic.py $O/prof_$tag/summary.json $cfg:$rows:$fbit $O/pmc_latest.json profiles/r04/prof_$tag || exit 1
 done
 cp $O/pmc_latest.json profiles/pmc_latest.json
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
-rc=$?; echo "bench exit $rc"; cut -c1-400 $O/bench.json; exit $rc
+rc=$?; echo "bench exit $rc"; cut -c1-400 $O/bench.json; [ $rc -eq 0 ] || exit $rc
+bash scripts/r04/gpu_host.sh
