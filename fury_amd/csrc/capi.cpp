@@ -460,11 +460,6 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   L->nullable = 0;
   for (const FixedFieldDev& f : fix) L->nullable |= f.validity ? 1 : 0;
   for (const fory_amd::VarFieldDev& v : var) L->nullable |= v.validity ? 2 : 0;
-  L->fix16 = 1;
-  for (const FixedFieldDev& f : fix)
-    if ((reinterpret_cast<uintptr_t>(f.values) & 15) || (reinterpret_cast<uintptr_t>(f.validity) & 7)) L->fix16 = 0;
-  for (const fory_amd::VarFieldDev& v : var)
-    if (reinterpret_cast<uintptr_t>(v.offsets) & 3) L->fix16 = 0;
   L->num_list = 0;
   L->list_mask = 0;
   for (size_t v = 0; v < var.size(); ++v)

@@ -97,6 +97,59 @@ __device__ __forceinline__ bool g_dec_fits(const uint32_t w[4], int prec) {
 }
 __device__ __forceinline__ int elem_size(const GNode& it) { return is_scalar(it.kind) ? it.width : 8; }
 
+// A decimal node that holds a java.math.BigInteger field (descriptor FORY_DECIMAL_BIGINTEGER).
+__device__ __forceinline__ bool g_bigint(const GNode& nd) { return nd.kind == KIND_DECIMAL && nd.prec == 0; }
+
+__device__ __forceinline__ void g_load_dec(const uint8_t* values, int64_t k, uint32_t w[4]) {
+  const GAS uint32_t* x = gp(reinterpret_cast<const uint32_t*>(values + 16 * k));  // (an Arrow decimal column)
+  w[0] = x[0];
+  w[1] = x[1];
+  w[2] = x[2];
+  w[3] = x[3];
+}
+
+// BigInteger.toByteArray().length of a decimal128 value: bitLength() / 8 + 1, where bitLength
+// counts the bits of the minimal two's complement without the sign (of ~v for negatives):
+// 0 -> 1 (00), -1 -> 1 (ff), 128 -> 2 (00 80), -129 -> 2 (ff 7f), +-2^127 -> 16.
+__device__ __forceinline__ int g_bigint_len(const uint32_t w[4]) {
+  const uint32_t s = (w[3] >> 31) ? 0xffffffffu : 0u;
+  int bits = 0;
+  for (int q = 3; q >= 0; --q) {
+    const uint32_t x = w[q] ^ s;
+    if (x) {
+      bits = 32 * q + 32 - __clz(x);
+      break;
+    }
+  }
+  return bits / 8 + 1;
+}
+// Row bytes a BigInteger value takes: writeUnaligned's round8(len).
+__device__ __forceinline__ int64_t g_bigint_bytes(const uint32_t w[4]) { return gr8(g_bigint_len(w)); }
+
+// toByteArray()'s len bytes (big-endian, most significant first) + zero padding to 8 at a
+// 4-byte aligned dst (BinaryWriter.writeUnaligned + zeroOutPaddingBytes).
+__device__ __forceinline__ void g_put_bigint(uint8_t* dst, const uint32_t w[4], int len) {
+  // the value's 16 bytes big-endian in memory order, shifted so the last len of them lead
+  unsigned __int128 b = (unsigned __int128)__builtin_bswap32(w[3]) |
+                        ((unsigned __int128)__builtin_bswap32(w[2]) << 32) |
+                        ((unsigned __int128)__builtin_bswap32(w[1]) << 64) |
+                        ((unsigned __int128)__builtin_bswap32(w[0]) << 96);
+  b >>= 8 * (16 - len);
+  const int nw = (int)(gr8(len) >> 2);
+  for (int q = 0; q < nw; ++q) st32(dst + 4 * q, (uint32_t)(b >> (32 * q)));
+}
+
+// new BigInteger(bytes) of the len row bytes at src into decimal128 dwords: sign-extended
+// big-endian. len outside 1..16 does not fit a decimal128 (0: Java's "Zero length
+// BigInteger"): returns false.
+__device__ __forceinline__ bool g_get_bigint(const uint8_t* src, int64_t len, uint32_t w[4]) {
+  if (len < 1 || len > 16) return false;
+  unsigned __int128 v = (src[0] & 0x80) ? ~(unsigned __int128)0 : 0;
+  for (int j = 0; j < (int)len; ++j) v = (v << 8) | src[j];
+  for (int q = 0; q < 4; ++q) w[q] = (uint32_t)(v >> (32 * q));
+  return true;
+}
+
 // Frame of an open container. STRUCT: children [ch, end) at position pos, the
 // child row at `start`. ARRAY: elements k..n-1 of node `item` at positions pos + k,
 // the array at `start`. MAP_KEYS / MAP_VALS: the key / value array of map `node`.
@@ -144,7 +197,13 @@ __device__ int64_t g_sizes(const GenLaunch& L, int64_t i, bool* overflow) {
     if (nd.kind == KIND_BYTES) {
       total += gr8((int64_t)gp(c.offsets)[pos + 1] - gp(c.offsets)[pos]);
     } else if (nd.kind == KIND_DECIMAL) {
-      total += 32;
+      if (g_bigint(nd)) {
+        uint32_t w[4];
+        g_load_dec(c.values, pos, w);
+        total += g_bigint_bytes(w);
+      } else {
+        total += 32;
+      }
     } else if (nd.kind == KIND_STRUCT) {
       total += gbm(nd.nchild) + 8LL * nd.nchild;
       if (sp == D) { *overflow = true; return; }
@@ -287,6 +346,13 @@ __device__ int32_t g_encode(const GenLaunch& L, uint8_t* row, int64_t i) {
       case KIND_DECIMAL: {  // BinaryWriter.writeDecimal: checkPrecisionAndScale, 32 LE bytes, (rel, 32)
         const uint8_t* v = c.values + 16 * pos;
         const uint32_t w[4] = {ld32(v), ld32(v + 4), ld32(v + 8), ld32(v + 12)};
+        if (g_bigint(nd)) {  // BigInteger: write(ordinal, value.toByteArray()) -> writeUnaligned
+          const int len = g_bigint_len(w);
+          g_put_bigint(row + wi, w, len);
+          gput(row + slot, ((uint64_t)rel << 32) | (uint32_t)len, 8);
+          wi += (int32_t)gr8(len);
+          return;
+        }
         if (!g_dec_fits(w, nd.prec)) {
           prec_ok = false;
           return;

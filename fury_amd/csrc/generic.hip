@@ -14,6 +14,7 @@
 //   string : bytes at the writerIndex, zero-padded to 8, slot = (rel, n) BinaryWriter.java:162-194
 //   decimal: 32 bytes at the writerIndex (decimal128 sign-extended), slot = (rel, 32)
 //            BinaryWriter.writeDecimal :214-230, DecimalUtils.DECIMAL_BYTE_LENGTH = 32
+//   BigInteger: toByteArray() as bytes (writeUnaligned), slot = (rel, len)  :192-194, :559-560
 // Offsets in slots are relative to the enclosing row's / array's start. Rows are
 // written straight to global memory (the output is not zeroed by the caller, so
 // every fixed part is zeroed first: the bytes Java writes into a fresh buffer).
@@ -166,7 +167,14 @@ __device__ void g_decode(const GenLaunch& L, const uint8_t* row, int64_t row_len
     if (nd.kind == KIND_DECIMAL) {  // UnsafeTrait.getDecimal (UnsafeTrait.java:139-150): 32 bytes
       if (!values) return;
       uint32_t w[4] = {0u, 0u, 0u, 0u};  // null: zeros
-      if (!isnull) {
+      if (!isnull && g_bigint(nd)) {  // new BigInteger(getBinary(ordinal)): sign-extended big-endian bytes
+        const uint64_t os = gget(slot, 8);
+        const int64_t rel = (int64_t)(int32_t)(os >> 32), at = r.start + rel, len = (int64_t)(int32_t)(uint32_t)os;
+        if (rel < 0 || len < 0 || at + len > row_len || !g_get_bigint(row + at, len, w)) {
+          corrupt();
+          return;
+        }
+      } else if (!isnull) {
         const uint64_t os = gget(slot, 8);
         const int64_t rel = (int64_t)(int32_t)(os >> 32), at = r.start + rel;
         if (rel < 0 || (uint32_t)os != 32u || at + 32 > row_len || (at & 3)) {

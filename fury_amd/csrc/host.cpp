@@ -11,8 +11,12 @@
 // capi.cpp (plan_info / workspace_bytes / encode / decode / read_status).
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstdint>
+#include <map>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <mutex>
@@ -130,6 +134,34 @@ extern "C" int fory_rowfmt_internal_node_layout(const fory_plan* plan, int32_t* 
 namespace {
 
 int fail_host(int code, const std::string& msg) { return fory_rowfmt_internal_set_error(code, msg.c_str()); }
+
+// Ranges registered through fory_rowfmt_host_register (base -> bytes).
+std::mutex g_reg_mu;
+std::map<uintptr_t, size_t> g_regs;
+
+uintptr_t page_size() {
+  static const uintptr_t p = [] {
+    const long v = sysconf(_SC_PAGESIZE);
+    return (uintptr_t)(v > 0 ? v : 4096);
+  }();
+  return p;
+}
+uintptr_t page_down(uintptr_t a) { return a & ~(page_size() - 1); }
+std::string hex(uintptr_t a) {
+  char b[32];
+  std::snprintf(b, sizeof b, "0x%llx", (unsigned long long)a);
+  return b;
+}
+
+// Does the runtime still treat host address p as registered (pinned, device-mapped)?
+bool still_mapped(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type != hipMemoryTypeUnregistered && a.devicePointer != nullptr;
+}
 
 int64_t validity_bytes(int64_t rows) { return ((rows + 7) / 8 + 3) / 4 * 4; }
 
@@ -407,12 +439,45 @@ void fory_rowfmt_host_ctx_destroy(fory_host_ctx* c) {
 
 int fory_rowfmt_host_register(void* host_ptr, int64_t bytes) {
   if (!host_ptr || bytes <= 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "null pointer or empty range");
-  return hip_check(hipHostRegister(host_ptr, (size_t)bytes, hipHostRegisterDefault), "hipHostRegister");
+  const uintptr_t b = reinterpret_cast<uintptr_t>(host_ptr);
+  const uintptr_t p0 = page_down(b), p1 = page_down(b + (uintptr_t)bytes - 1) + page_size();
+  std::lock_guard<std::mutex> lock(g_reg_mu);
+  // a registration pins whole pages: two of them on one page would leave that page's
+  // pinning to whichever is unregistered last, and a copy judged by one of them could
+  // reach the other's bytes -- refused (the caller registers page-exclusive buffers)
+  for (const auto& r : g_regs) {
+    const uintptr_t q0 = page_down(r.first), q1 = page_down(r.first + r.second - 1) + page_size();
+    if (p0 < q1 && q0 < p1)
+      return fail_host(FORY_ERR_INVALID_ARGUMENT,
+                       "range shares a page with a registered range at " + hex(r.first) + " (" +
+                           std::to_string(r.second) + " bytes): register page-exclusive buffers");
+  }
+  const int rc = hip_check(hipHostRegister(host_ptr, (size_t)bytes, hipHostRegisterDefault), "hipHostRegister");
+  if (!rc) g_regs[b] = (size_t)bytes;
+  return rc;
 }
 
 int fory_rowfmt_host_unregister(void* host_ptr) {
   if (!host_ptr) return fail_host(FORY_ERR_INVALID_ARGUMENT, "null pointer");
-  return hip_check(hipHostUnregister(host_ptr), "hipHostUnregister");
+  const uintptr_t b = reinterpret_cast<uintptr_t>(host_ptr);
+  std::lock_guard<std::mutex> lock(g_reg_mu);
+  auto it = g_regs.find(b);
+  if (it == g_regs.end())
+    return fail_host(FORY_ERR_INVALID_ARGUMENT, "not the start of a range fory_rowfmt_host_register registered");
+  const size_t bytes = it->second;
+  int rc = hip_check(hipHostUnregister(host_ptr), "hipHostUnregister");
+  if (rc) return rc;  // (still registered: kept in the table)
+  g_regs.erase(it);
+  // the runtime must no longer map either end of the range: a copy through it would be
+  // handed to the DMA engine as pinned memory the device no longer maps
+  if (still_mapped(host_ptr) || still_mapped(static_cast<uint8_t*>(host_ptr) + (bytes - 1)))
+    return fail_host(FORY_ERR_DEVICE, "range still reads as registered after hipHostUnregister");
+  return FORY_OK;
+}
+
+int fory_rowfmt_internal_host_registered_ranges(void) {
+  std::lock_guard<std::mutex> lock(g_reg_mu);
+  return (int)g_regs.size();
 }
 
 }  // extern "C"

@@ -74,7 +74,6 @@ struct VarLaunch {
   LaunchKnobs kn;               // the plan's knobs (host-side launch decisions only)
   int32_t num_list;             // list fields among the var fields
   uint32_t list_mask;           // bit v: var field v is a list (v < 32)
-  int32_t fix16;                // every fixed column 16-B aligned, its validity 8-B aligned (encode v8)
   int32_t nullable;             // bit 0: some fixed column has validity, bit 1: some var column (encode v9)
 };
 

@@ -116,7 +116,6 @@ LaunchKnobs knobs_from_env() {
   k.var_enc = num("FORY_ROWFMT_VARENC", 0);
   k.var_xcd = num("FORY_ROWFMT_VARXCD", 0);
   k.dec_regs = num("FORY_ROWFMT_DECREGS", 0);
-  k.dbg_skip = num("FORY_ROWFMT_DBGSKIP", 0);
   k.tree_col = num("FORY_ROWFMT_TREECOL", 1);
   return k;
 }

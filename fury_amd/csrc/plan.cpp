@@ -50,8 +50,12 @@ static int parse_node(const fory_field_desc* d, int32_t n, int32_t at, Plan* p, 
     return FORY_ERR_UNSUPPORTED;
   }
   const fory_field_desc& f = d[at];
-  const bool dec = f.type_id == FORY_TYPE_DECIMAL;  // reserved = precision (0 = 38)
-  if ((!dec && f.reserved != 0) || (dec && (f.reserved < 0 || f.reserved > 38)) || f.num_children < 0) {
+  const bool dec = f.type_id == FORY_TYPE_DECIMAL;  // reserved = precision (0 = 38) | FORY_DECIMAL_BIGINTEGER
+  const int32_t dprec = f.reserved & 0xff;
+  const bool bigint = dec && (f.reserved & FORY_DECIMAL_BIGINTEGER);
+  const bool dec_ok = (f.reserved & ~(int32_t)(0xff | FORY_DECIMAL_BIGINTEGER)) == 0 && dprec <= 38 &&
+                      (!bigint || dprec == 0 || dprec == 38);
+  if ((!dec && f.reserved != 0) || (dec && !dec_ok) || f.num_children < 0) {
     *err = "invalid field descriptor at index " + std::to_string(at);
     return FORY_ERR_INVALID_ARGUMENT;
   }
@@ -88,7 +92,7 @@ static int parse_node(const fory_field_desc* d, int32_t n, int32_t at, Plan* p, 
     case FORY_TYPE_MAP: nd.kind = KIND_MAP; break;
     case FORY_TYPE_DECIMAL:  // TypeInference: BigDecimal -> Decimal(38, 18), BigInteger -> Decimal(38, 0)
       nd.kind = KIND_DECIMAL;
-      nd.prec = f.reserved > 0 ? f.reserved : 38;
+      nd.prec = bigint ? 0 : (dprec > 0 ? dprec : 38);  // 0: BigInteger.toByteArray() bytes
       break;
     default: nd.kind = KIND_FIXED; break;
   }

@@ -29,7 +29,8 @@ enum FieldKind : int32_t {
   KIND_STRUCT = 3,  // nested row inline in the variable section
   KIND_LIST = 4,    // BinaryArray inline in the variable section
   KIND_MAP = 5,     // BinaryMap inline: [i64 keyArrayBytes][key BinaryArray][value BinaryArray]
-  KIND_DECIMAL = 6, // decimal128 column -> 32 sign-extended bytes behind an (offset, 32) slot (tree engine)
+  KIND_DECIMAL = 6, // decimal128 column -> 32 sign-extended bytes behind an (offset, 32) slot (tree engine);
+                    // prec 0: a BigInteger field -> toByteArray()'s 1..16 big-endian bytes, (offset, len)
 };
 
 // Per top-level field of a fixed-width plan (read by the tiled kernels).
@@ -121,7 +122,7 @@ struct GNode {
   int32_t end;     // index after the subtree
   int32_t nchild;
   int32_t cdepth;  // list / map ancestors: the decode lengths pass that sizes this column
-  int32_t prec;    // KIND_DECIMAL: precision (|unscaled| <= 10^prec - 1), else 0
+  int32_t prec;    // KIND_DECIMAL: precision (|unscaled| <= 10^prec - 1); 0: BigInteger bytes; else 0
 };
 
 struct Node {
@@ -129,7 +130,8 @@ struct Node {
   int32_t nullable = 0;
   int32_t width = -1;
   int32_t kind = 0;
-  int32_t prec = 0;               // KIND_DECIMAL: precision (descriptor's reserved word, 0 = 38)
+  int32_t prec = 0;               // KIND_DECIMAL: precision (descriptor's reserved word, 0 = 38);
+                                  // 0 for FORY_DECIMAL_BIGINTEGER (java.math.BigInteger)
   std::vector<int32_t> children;  // desc indices
 };
 
@@ -145,7 +147,9 @@ struct Node {
 //   FORY_ROWFMT_SIZES_PROGRAM  sizes by the op-program walk for flat plans too
 //   FORY_ROWFMT_IDXFRAMES   frames per frame-index chunk
 //   FORY_ROWFMT_VARPROF=1   phase timeline (debug), FORY_ROWFMT_VARDIAG=1 LDS sizing to stderr
-//   FORY_ROWFMT_VARENC=1|7|8|9|10  encode with the round-3 tile kernel / v7 / v8 / v9 / v9 at 128 VGPRs
+//   FORY_ROWFMT_VARENC=1|7|9  encode with the round-3 tile kernel / v7 / v9 (each byte-identical)
+// No knob changes the bytes or skips work (tests/test_kernel_isa.py checks the product reads
+// no debug knob that could).
 struct LaunchKnobs {
   int32_t no_tiles;
   int32_t no_flat;
@@ -158,8 +162,7 @@ struct LaunchKnobs {
   int32_t idx_frames;
   int32_t prof;
   int32_t diag;
-  int32_t var_enc;   // FORY_ROWFMT_VARENC (A/B): 0 = defaults of launch_flat_enc, 1 / 7 / 8 / 9 force a kernel
-  int32_t dbg_skip;  // FORY_ROWFMT_DBGSKIP (debug, timing only; output wrong): 1 = tile kernels stop after their loads, 2 = encode v7 skips its image store
+  int32_t var_enc;   // FORY_ROWFMT_VARENC (A/B): 0 = defaults of launch_flat_enc, 1 / 7 / 9 force a kernel
   int32_t var_xcd;   // FORY_ROWFMT_VARXCD=C: varlen tile kernels take tiles in XCD runs of C (-1: one run per XCD), 0 = dispatch order
   int32_t dec_regs;  // FORY_ROWFMT_DECREGS=1: varlen decode stages its tile rows through registers, not LDS-DMA (A/B)
   int32_t tree_col;  // FORY_ROWFMT_TREECOL: 0 = tree-engine encode per lane only; else the columnar engine when the workspace allows

@@ -7,7 +7,7 @@
 // (one instance = one element of a schema node's column), each a full-occupancy grid:
 //   sizes   bottom-up, one launch per var node (children first), lane per instance:
 //           A[c][j] = the bytes instance j adds to its parent — strings round8(len),
-//           decimals 32, beans bitmap + 8 x fields + their var children, arrays
+//           decimals 32 (BigIntegers round8 of their toByteArray() length), beans bitmap + 8 x fields + their var children, arrays
 //           8 + bitmap + round8(n x elemSize) + their var items (a difference of the
 //           items' scanned sizes), maps 8 + key array + value array. Item nodes (list
 //           items, map keys / values) are scanned in place: A[x][k] = bytes of the
@@ -40,12 +40,20 @@ __device__ __forceinline__ bool tc_is_var(int kind) { return !is_scalar(kind); }
 __device__ __forceinline__ bool tc_leaf(int kind) { return kind == KIND_BYTES || kind == KIND_DECIMAL; }
 __device__ __forceinline__ bool tc_has_pos(int kind) { return tc_is_var(kind) && !tc_leaf(kind); }
 
+// Row bytes of decimal value k: 32 (writeDecimal), or a BigInteger's round8(toByteArray().length).
+__device__ __forceinline__ int64_t tc_dec_bytes(const GNode& nd, const ColumnDev& col, int64_t k) {
+  if (!g_bigint(nd)) return 32;
+  uint32_t w[4];
+  g_load_dec(col.values, k, w);
+  return g_bigint_bytes(w);
+}
+
 // Bytes var value k of (non-item) node c adds to its parent; 0 when null.
 __device__ __forceinline__ int64_t tc_size(const TcTables* T, int c, const GNode& nd, const ColumnDev& col,
                                            int64_t k) {
   if (nd.kind == KIND_BYTES || nd.kind == KIND_DECIMAL) {
     if ((nd.flags & 1) && !gvalid(col.validity, k)) return 0;
-    return nd.kind == KIND_DECIMAL ? 32 : gr8((int64_t)gp(col.offsets)[k + 1] - gp(col.offsets)[k]);
+    return nd.kind == KIND_DECIMAL ? tc_dec_bytes(nd, col, k) : gr8((int64_t)gp(col.offsets)[k + 1] - gp(col.offsets)[k]);
   }
   return gp(T->A[c])[k];
 }
@@ -89,7 +97,7 @@ __device__ __forceinline__ int64_t tc_node_size(const GenLaunch& L, const TcTabl
   if (!root_coll && (nd.flags & 1) && !gvalid(col.validity, j)) return 0;
   switch (nd.kind) {
     case KIND_BYTES: return gr8((int64_t)gp(col.offsets)[j + 1] - gp(col.offsets)[j]);
-    case KIND_DECIMAL: return 32;
+    case KIND_DECIMAL: return tc_dec_bytes(nd, col, j);
     case KIND_STRUCT: {
       int64_t s = gbm(nd.nchild) + 8LL * nd.nchild;
       for (int ch = c + 1; ch < nd.end; ch = L.nodes[ch].end) {
@@ -249,9 +257,15 @@ __device__ __forceinline__ void tc_put(uint8_t* p, uint64_t v, int w) {
   }
 }
 
-// Slot size field of a var value: a string's byte length, else its bytes (decimals 32).
+// Slot size field of a var value: a string's byte length, a BigInteger's toByteArray()
+// length, else its bytes (decimals 32).
 __device__ __forceinline__ uint32_t tc_slot_size(const GNode& nd, const ColumnDev& col, int64_t k, int64_t bytes) {
   if (nd.kind == KIND_BYTES) return (uint32_t)(gp(col.offsets)[k + 1] - gp(col.offsets)[k]);
+  if (g_bigint(nd)) {
+    uint32_t w[4];
+    g_load_dec(col.values, k, w);
+    return (uint32_t)g_bigint_len(w);
+  }
   return (uint32_t)bytes;
 }
 
@@ -283,8 +297,8 @@ __device__ __forceinline__ void tc_copy(uint8_t* dst, const uint8_t* src, int64_
 }
 
 // A leaf value at `at`, S bytes allotted (room for S checked by the caller):
-// writeUnaligned + zeroOutPaddingBytes, or BinaryWriter.writeDecimal
-// (checkPrecisionAndScale: FORY_ERR_UNSUPPORTED). A string whose padded length is not S
+// writeUnaligned + zeroOutPaddingBytes (strings, BigInteger.toByteArray()), or
+// BinaryWriter.writeDecimal (checkPrecisionAndScale: FORY_ERR_UNSUPPORTED). A string whose padded length is not S
 // (sizes from an encoded_size call over other contents) is not written: FORY_ERR_ENCODER.
 __device__ __forceinline__ int32_t tc_leaf_write(uint8_t* out, const GNode& nd, const ColumnDev& col, int64_t k,
                                                  int64_t at, int64_t S) {
@@ -294,10 +308,15 @@ __device__ __forceinline__ int32_t tc_leaf_write(uint8_t* out, const GNode& nd, 
     tc_copy(out + at, col.values + s0, n);
     return 0;
   }
+  uint32_t w[4];
+  g_load_dec(col.values, k, w);
+  if (g_bigint(nd)) {  // BigInteger: write(ordinal, value.toByteArray()) -> writeUnaligned
+    const int len = g_bigint_len(w);
+    if (gr8(len) != S) return FORY_ERR_ENCODER;
+    g_put_bigint(out + at, w, len);
+    return 0;
+  }
   if (S != 32) return FORY_ERR_ENCODER;
-  const uint8_t* x = col.values + 16 * k;
-  const GAS uint32_t* xg = gp(reinterpret_cast<const uint32_t*>(x));  // (an Arrow decimal column)
-  const uint32_t w[4] = {xg[0], xg[1], xg[2], xg[3]};
   if (!g_dec_fits(w, nd.prec)) return FORY_ERR_UNSUPPORTED;
   const uint32_t ext = (w[3] >> 31) ? 0xffffffffu : 0u;
   for (int q = 0; q < 4; ++q) st32(out + at + 4 * q, w[q]);

@@ -9,7 +9,8 @@
 //           lanes of a wave write consecutive elements of each output column. Per field
 //           the lane reads the null bit and slot and writes the value (scalars: the slot's
 //           low bytes; strings: the bytes at the slot's (offset, size); decimals: 32
-//           bytes, the high 16 the sign extension), the count of a string / list / map
+//           bytes, the high 16 the sign extension; BigIntegers: their 1..16 big-endian
+//           bytes sign-extended), the count of a string / list / map
 //           at this decode level, or hands a bean / list / map its position.
 //   items   each list / map node: a workgroup per 256 containers reads their headers
 //           (count, and for maps the key array's bytes), checks the count against the
@@ -106,7 +107,13 @@ __device__ __forceinline__ void td_value(const GenLaunch& L, const TdTables* T, 
   if (nd.kind == KIND_DECIMAL) {  // UnsafeTrait.getDecimal: 32 bytes, the high 16 the sign extension
     if (!col.out_values || (!values && nd.cdepth != level)) return;
     uint32_t w[4] = {0u, 0u, 0u, 0u};
-    if (!isnull) {
+    if (!isnull && g_bigint(nd)) {  // new BigInteger(bytes at the slot's (offset, len))
+      const int64_t rel = (int64_t)(int32_t)(sv >> 32), at = origin + rel, len = (int64_t)(int32_t)(uint32_t)sv;
+      if (rel < 0 || len < 0 || at + len > rend || !g_get_bigint(rows + at, len, w)) {
+        set_status(status, FORY_ERR_CORRUPT);
+        return;
+      }
+    } else if (!isnull) {
       const uint64_t os = sv;
       const int64_t rel = (int64_t)(int32_t)(os >> 32), at = origin + rel;
       if (rel < 0 || (uint32_t)os != 32u || at + 32 > rend || (at & 3)) {

@@ -2028,10 +2028,6 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
   const int64_t total = mis + (B1 - B0);
   V7_STAMP(1);
-  if (L.kn.dbg_skip == 1) {  // debug: the loads alone (timing); keep them live
-    if (tid == 0 && B1 == -7) L.prof[0] = (uint64_t)(e0[0] + R.lo[0] + R.hi[0] + S[0].d[0] + (uint32_t)beg);
-    return;
-  }
   if (!sane || (mis & 3) || total > cap) {
     if (sane && !(mis & 3) && total <= sp.cap) {  // the big-image spill launch takes it
       if (tid == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
@@ -2257,10 +2253,6 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
   }
   __syncthreads();
   V7_STAMP(6);
-  if (L.kn.dbg_skip == 2) {  // debug: everything but the image store (timing); keep the image live
-    if (tid == 0 && B1 == -7) L.prof[0] = ld32(img);
-    return;
-  }
   uint8_t* g = out + B0 - mis;  // 16-byte aligned
   const int tot = (int)total;
   const int nch = (tot + 15) >> 4;
@@ -2281,346 +2273,27 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat7_kernel(VarLaunch L, 
 }
 
 // ---------------------------------------------------------------------------
-// Encode v8: flat plans without nested structs whose fixed columns are 16-byte aligned.
-// Every global access is a 16-byte-per-lane one where the data allows it:
-//  - fixed columns: the tile's segment of each column (64 x w bytes) read as 16-B chunks,
-//    one 1 KiB wave instruction per 16/w fields (chunk -> field by lane / (4w)), held in
-//    registers until the row positions are known, then scattered into the row image's
-//    slots (BinaryRowWriter.write: zero-extended, null -> 0 + setNullAt);
-//  - strings / lists: each owned field's tile span by LDS-DMA, its bounds (offsets[r0],
-//    offsets[r0 + 64]) loaded first so the span is in flight with the rest;
-//  - the image leaves as aligned 16-B stores.
-// Encode v7's per-lane 4- and 8-byte column loads are what held it at ~3 TB/s of reads
-// (its loads alone, FORY_ROWFMT_DBGSKIP=1: 2.08 ms for Mixed's 6.3 GB of columns).
-// Partial tiles and tiles near the end of the offsets arrays take the per-record path.
-// ---------------------------------------------------------------------------
-constexpr int kFix16 = 4;  // fixed-column 1 KiB instructions per wave held in registers
-
-// Fixed-column instruction j of the width-sorted table: group g (width w = 8 >> g), its
-// first field kf and the group's end; false past the last.
-__device__ __forceinline__ bool fix16_instr(const VarLaunch& L, int j, int* kf, int* kend, int* w) {
-  for (int g = 0; g < 4; ++g) {
-    const int a = L.fix_group[g], b = L.fix_group[g + 1];
-    const int ww = 8 >> g, fpi = 16 / ww;  // fields per 1 KiB instruction
-    const int ni = (b - a + fpi - 1) / fpi;
-    if (j < ni) {
-      *kf = a + j * fpi;
-      *kend = b;
-      *w = ww;
-      return true;
-    }
-    j -= ni;
-  }
-  return false;
-}
-
-// Lane's field of instruction (kf, kend, w): k = kf + lane / (4w); its descriptor by a
-// select over the instruction's <= 16/w fields (scalar loads: no per-lane table gather).
-struct Fix16Lane {
-  const uint8_t* values;
-  const uint8_t* validity;
-  int32_t slot, flags;
-  bool ok;
-  int sub;  // 16-B chunk of the field's 64-record segment
-};
-__device__ __forceinline__ Fix16Lane fix16_lane(const FixedFieldDev* __restrict__ fix, int kf, int kend, int w,
-                                                int lane) {
-  const int lg = w == 8 ? 5 : w == 4 ? 4 : w == 2 ? 3 : 2;  // log2(4w): chunks per field
-  const int fi = lane >> lg;
-  Fix16Lane r;
-  r.sub = lane & ((1 << lg) - 1);
-  r.ok = kf + fi < kend;
-  r.values = fix[kf].values;
-  r.validity = fix[kf].validity;
-  r.slot = fix[kf].slot;
-  r.flags = fix[kf].flags;
-  const int fpi = 16 / w;
-#pragma unroll
-  for (int q = 1; q < 16; ++q) {
-    if (q >= fpi || kf + q >= kend) break;
-    const FixedFieldDev& f = fix[kf + q];
-    if (fi == q) {
-      r.values = f.values;
-      r.validity = f.validity;
-      r.slot = f.slot;
-      r.flags = f.flags;
-    }
-  }
-  return r;
-}
-
-// The 16/W values of a lane's chunk (records sub * 16/W + e) into their rows' slots.
-template <int W>
-__device__ __forceinline__ void fix16_scatter(uint8_t* img, const int32_t* rs, int bm, const Fix16Lane& d,
-                                              const u32x4& c, uint64_t vbits) {
-  constexpr int E = 16 / W;
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int rr = d.sub * E + e;
-    uint64_t x;
-    if constexpr (W == 8) {
-      x = ((uint64_t)c[2 * e + 1] << 32) | c[2 * e];
-    } else if constexpr (W == 4) {
-      x = c[e];
-    } else if constexpr (W == 2) {
-      x = (c[e >> 1] >> (16 * (e & 1))) & 0xffffu;
-    } else {
-      x = (c[e >> 2] >> (8 * (e & 3))) & 0xffu;
-    }
-    const bool valid = !d.validity || ((vbits >> rr) & 1);
-    if (!valid) x = 0;
-    if (d.flags & 2) x = x ? 1 : 0;
-    uint8_t* rw = img + rs[rr];
-    st64_lds(rw + bm + 8 * d.slot, x);
-    if (!valid) atomicOr(reinterpret_cast<uint32_t*>(rw) + (d.slot >> 5), 1u << (d.slot & 31));
-  }
-}
-
-template <int HDR, int NW, int OWN>
-__global__ __launch_bounds__(64 * NW) void var_encode_flat8_kernel(VarLaunch L, const Op* __restrict__ prog,
-                                                                   const ColumnDev* __restrict__ cols,
-                                                                   const FixedFieldDev* __restrict__ fix,
-                                                                   const VarFieldDev* __restrict__ vf,
-                                                                   const int64_t* __restrict__ offs,
-                                                                   uint8_t* __restrict__ out, int64_t capacity,
-                                                                   int32_t* status, int cap, int slot, SpillArgs sp) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint8_t* img = lds;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint8_t* stg = lds + cap + wave * slot;                                // this wave's span staging
-  int32_t* sz = reinterpret_cast<int32_t*>(lds + cap + NW * slot);       // [num_var][64] payload bytes, -1 null
-  int32_t* rs = sz + L.num_var * 64;                                     // [64] row starts in the image
-  const int64_t tile = var_tile(blockIdx.x, gridDim.x, L.kn.var_xcd);
-  const int64_t r0 = tile * 64;
-  const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
-  const int64_t i = r0 + lane;
-  if (rows < 64 || r0 + 68 > L.num_rows) {  // the last tiles: per record (offsets read as whole 16-B chunks elsewhere)
-    if (wave == 0 && lane < rows) {
-      const int64_t beg = offs[i], end = offs[i + 1];
-      if (end > capacity || beg < 0 || end < beg) set_status(status, FORY_ERR_CAPACITY);
-      else enc_record(L, prog, cols, i, out + beg, end - beg);
-    }
-    return;
-  }
-  // ---- one round trip. First the span bounds of the owned var fields (used to put the
-  // spans in flight before the rest lands), then their per-record offsets and validity,
-  // the fixed-column chunks and the row bounds
-  int32_t E0[OWN], E1[OWN];
-#pragma unroll
-  for (int k = 0; k < OWN; ++k) {
-    const int v = wave + k * NW;
-    E0[k] = E1[k] = 0;
-    if (v < L.num_var) {
-      E0[k] = vf[v].offsets[r0];
-      E1[k] = vf[v].offsets[r0 + 64];
-    }
-  }
-  int32_t e0[OWN], e1[OWN];
-  uint32_t vvb[OWN];
-#pragma unroll
-  for (int k = 0; k < OWN; ++k) {
-    const int v = wave + k * NW;
-    e0[k] = e1[k] = 0;
-    vvb[k] = 0xffu;
-    if (v < L.num_var) {
-      const VarFieldDev& f = vf[v];
-      e0[k] = f.offsets[i];
-      e1[k] = f.offsets[i + 1];
-      vvb[k] = f.validity ? load_byte(f.validity + (i >> 3)) : 0xffu;
-    }
-  }
-  u32x4 fc[kFix16];
-  uint64_t fv[kFix16];  // the chunk field's validity bits of the tile (nullable fields)
-#pragma unroll
-  for (int q = 0; q < kFix16; ++q) {
-    int kf, kend, w;
-    fc[q] = u32x4{0u, 0u, 0u, 0u};
-    fv[q] = ~0ull;
-    if (!fix16_instr(L, wave + q * NW, &kf, &kend, &w)) continue;
-    const Fix16Lane c = fix16_lane(fix, kf, kend, w, lane);
-    const uint8_t* p = c.values + r0 * w + (c.ok ? c.sub * 16 : 0);
-    fc[q] = __builtin_nontemporal_load(gp(reinterpret_cast<const u32x4*>(p)));
-    if (c.validity) fv[q] = *gp(reinterpret_cast<const uint64_t*>(c.validity + (r0 >> 3)));
-  }
-  const int64_t B0 = offs[r0], B1 = offs[r0 + 64];
-  const int64_t beg = offs[i], end = offs[i + 1];
-  // ---- the spans in flight (their bounds are the first loads: the wait leaves the rest in flight)
-  int so = 0;
-  int sphase[OWN], svofs[OWN], soff[OWN];
-  bool staged[OWN];
-#pragma unroll
-  for (int k = 0; k < OWN; ++k) {
-    const int v = wave + k * NW;
-    staged[k] = false;
-    sphase[k] = svofs[k] = soff[k] = 0;
-    if (v >= L.num_var) continue;
-    const VarFieldDev& f = vf[v];
-    int64_t need = (int64_t)(E1[k] - E0[k]) * f.w + 16 + 4 + 16;  // phase + funnel-copy slack + vofs rounding
-    if (f.item_validity) need += ((E1[k] + 7) >> 3) - ((E0[k] >> 3) & ~3) + 4;
-    need = (need + 15) & ~int64_t(15);
-    if ((f.iflags & 2) == 0 && E1[k] > E0[k] && E1[k] >= E0[k] && so + need <= slot) {
-      flat_stage_span(f, E0[k], E1[k], lane, stg + so, &sphase[k], &svofs[k]);
-      staged[k] = true;
-      soff[k] = so;
-      so += (int)need;
-    }
-  }
-  // ---- row bounds: the tile's rows are one run [B0, B1) of the output
-  const bool inrun = beg >= B0 && end >= beg && end <= B1;
-  const bool capbad = end > capacity || beg < 0 || end < beg;
-  if (__ballot(capbad)) {  // (every wave sees the same bounds: the whole workgroup leaves)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (spans land before the LDS is another workgroup's)
-    if (wave == 0 && capbad) set_status(status, FORY_ERR_CAPACITY);
-    return;
-  }
-  const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
-  const int64_t total = mis + (B1 - B0);
-  const bool sane = __ballot(!inrun) == 0 && ((B0 | B1) & 3) == 0 && B1 >= B0;
-  if (!sane || (mis & 3) || total > cap) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (spans land before the LDS is another workgroup's)
-    if (sane && !(mis & 3) && total <= sp.cap) {      // the big-image spill launch takes it
-      if (tid == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
-      return;
-    }
-    if (wave == 0) enc_record(L, prog, cols, i, out + beg, end - beg);
-    return;
-  }
-  uint8_t* fp = img + mis + (int)(beg - B0);
-  uint8_t* row = fp + HDR;
-  uint8_t* slots = row + L.bitmap_bytes;
-  const int bm = L.bitmap_bytes;
-  // owned var fields: payload sizes (-1 null)
-#pragma unroll
-  for (int k = 0; k < OWN; ++k) {
-    const int v = wave + k * NW;
-    if (v >= L.num_var) continue;
-    const VarFieldDev& f = vf[v];
-    const bool valid = (vvb[k] >> (i & 7)) & 1;
-    const int64_t n = (int64_t)e1[k] - e0[k];
-    sz[v * 64 + lane] = !valid ? -1 : (int32_t)(f.is_list ? 8 + bitmap_bytes(n) + round8(n * f.w) : round8(n));
-  }
-  if (wave == 0) {  // row starts, the frame header, the zeroed bitmap (BinaryRowWriter.reset)
-    rs[lane] = mis + (int)(beg - B0) + HDR;
-    if (HDR == 12) {
-      st32(fp, (uint32_t)(end - beg - 4));
-      st64_lds(fp + 4, (uint64_t)L.schema_hash);
-    } else if (HDR == 8) {
-      st64_lds(fp, (uint64_t)L.schema_hash);
-    }
-    for (int b = 0; b < bm; b += 4) st32(row + b, 0u);
-  }
-  __syncthreads();  // sizes, row starts, zeroed bitmaps
-  // fixed slots from the chunks (null -> 0 + the bit, bool -> 0/1)
-  auto scatter = [&](int kf, int kend, int w, const u32x4& c, uint64_t vbits) {
-    const Fix16Lane d = fix16_lane(fix, kf, kend, w, lane);
-    if (!d.ok) return;
-    switch (w) {  // a compile-time width per case: the chunk's dwords indexed statically
-      case 8: fix16_scatter<8>(img, rs, bm, d, c, vbits); break;
-      case 4: fix16_scatter<4>(img, rs, bm, d, c, vbits); break;
-      case 2: fix16_scatter<2>(img, rs, bm, d, c, vbits); break;
-      default: fix16_scatter<1>(img, rs, bm, d, c, vbits); break;
-    }
-  };
-#pragma unroll
-  for (int q = 0; q < kFix16; ++q) {
-    int kf, kend, w;
-    if (fix16_instr(L, wave + q * NW, &kf, &kend, &w)) scatter(kf, kend, w, fc[q], fv[q]);
-  }
-  for (int j = wave + kFix16 * NW;; j += NW) {  // plans with more fixed fields: a round trip per instruction
-    int kf, kend, w;
-    if (!fix16_instr(L, j, &kf, &kend, &w)) break;
-    const Fix16Lane c = fix16_lane(fix, kf, kend, w, lane);
-    const u32x4 v = __builtin_nontemporal_load(gp(reinterpret_cast<const u32x4*>(c.values + r0 * w + (c.ok ? c.sub * 16 : 0))));
-    const uint64_t vb = c.validity ? *gp(reinterpret_cast<const uint64_t*>(c.validity + (r0 >> 3))) : ~0ull;
-    scatter(kf, kend, w, v, vb);
-  }
-  // var fields: positions (the fixed part + the payloads before, field order), slots, list
-  // headers, null bits, then the payloads from the staged spans
-  int32_t pos[OWN];
-  {
-    int32_t acc = L.fixed_size;
-    int u = 0;
-#pragma unroll
-    for (int k = 0; k < OWN; ++k) {
-      const int v = wave + k * NW;
-      pos[k] = -1;
-      if (v >= L.num_var) continue;
-      for (; u < v; ++u) {
-        const int32_t s = sz[u * 64 + lane];
-        acc += s > 0 ? s : 0;
-      }
-      pos[k] = sz[v * 64 + lane] >= 0 ? acc : -1;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < OWN; ++k) {
-    const int v = wave + k * NW;
-    if (v >= L.num_var) continue;
-    const VarFieldDev& f = vf[v];
-    uint8_t* sl = slots + 8 * f.slot;
-    const int64_t n = (int64_t)e1[k] - e0[k];
-    if (pos[k] < 0) {
-      st64_lds(sl, 0);
-      atomicOr(reinterpret_cast<uint32_t*>(row) + (f.slot >> 5), 1u << (f.slot & 31));
-    } else if (!f.is_list) {
-      st64_lds(sl, ((uint64_t)(uint32_t)pos[k] << 32) | (uint32_t)n);
-    } else {
-      const int32_t ahdr = 8 + bitmap_bytes(n);
-      st64_lds(row + pos[k], (uint64_t)n);
-      for (int b = 8; b < ahdr; b += 4) st32(row + pos[k] + b, 0);
-      st64_lds(sl, ((uint64_t)(uint32_t)pos[k] << 32) | (uint32_t)(ahdr + round8(n * f.w)));
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's spans
-  wave_lds_sync();
-#pragma unroll
-  for (int k = 0; k < OWN; ++k) {
-    const int v = wave + k * NW;
-    if (v >= L.num_var) continue;
-    if (pos[k] >= 0)
-      flat_place(vf[v], staged[k], stg + soff[k], sphase[k], E0[k], svofs[k], pos[k], e0[k],
-                 (int64_t)e1[k] - e0[k], row);
-  }
-  __syncthreads();
-  uint8_t* g = out + B0 - mis;  // 16-byte aligned
-  const int tot = (int)total;
-  const int nch = (tot + 15) >> 4;
-  for (int cc = tid; cc < nch; cc += 64 * NW) {
-    const int lo = cc * 16;
-    if (lo >= mis && lo + 16 <= tot) {
-      *gp(reinterpret_cast<u32x4*>(g + lo)) = *reinterpret_cast<const u32x4*>(img + lo);
-    } else {
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int o = lo + 4 * d;
-        if (o >= mis && o + 4 <= tot) *gp(reinterpret_cast<uint32_t*>(g + o)) = ld32(img + o);
-      }
-    }
-  }
-}
-
-
-// ---------------------------------------------------------------------------
-// Encode v9: encode v7's tile as a persistent, software-pipelined loop (flat plans of
-// fixed fields and strings / binary: no list or nested struct fields, <= kFixBatch * NW
-// fixed fields, <= OWN * NW var fields, a bitmap of <= kV9Bmw words).
+// Encode v9: encode v7's tile, two consecutive tiles per workgroup as straight-line code
+// (flat plans of fixed fields and strings / binary: no list or nested struct fields,
+// <= kFixBatch * NW fixed fields, <= OWN * NW var fields, a bitmap of <= kV9Bmw words).
 //
 // v7 spends a tile's whole life (~16 us at 4 tiles per CU) on a chain of dependent
 // round trips -- row bounds and offsets -> string bytes -> copies -> stores -- so each
-// CU has a tile's loads in flight only part of the time. Here a workgroup walks tiles
-// t, t + G, ... and the next tile's loads fly while this one is assembled:
+// CU has a tile's loads in flight only part of the time. Here workgroup b takes tiles
+// tb = K b .. tb + K - 1 (K = 2) and issues the second tile's loads while the first is
+// assembled (no loop: at a loop back edge LLVM flushes vmcnt):
+//   --  tile tb: offsets, validity, row bounds, fixed values; then its strings' first
+//       32 bytes (once its offsets land); then tile tb + 1's columns -- all in flight
 //   P1  sizes, null bits (partial words per wave) and row starts of tile t -> LDS
-//       (its offsets, validity and row bounds were loaded during tile t - G)
-//   B1  barrier (the previous image has left: its stores were issued before it)
-//   P2  wave 0: header + bitmap; every wave: its fields' positions (prefix of sizes)
-//   P3  fixed values (loaded during tile t - G) and the strings' first 32 bytes
-//       (loaded during P3 of tile t - G) into the image; longer strings: a trip per chunk
-//   --  tile t + G: its strings' first 32 bytes in flight (its offsets have landed)
+//   B1  barrier
+//   P2  the records' sizes against their offsets; wave 0: header + bitmap; every wave:
+//       its fields' positions (prefix of sizes)
+//   P3  fixed values and the strings' first 32 bytes into the image; longer strings: a
+//       round trip per further 32 bytes
+//   --  tile t + 1: its strings' first 32 bytes in flight (its offsets have landed)
 //   B2  barrier; the image leaves as 16-B stores
-//   --  tile t + 2G: offsets, validity, row bounds; tile t + G: fixed values, in flight
-// Every wait is on loads issued a phase or more earlier; the stores are older than
-// anything waited on after them. Bytes are those of var_encode_flat7_kernel.
+// Every wait is on loads issued a phase or more earlier. Bytes are those of
+// var_encode_flat7_kernel.
 // ---------------------------------------------------------------------------
 constexpr int kV9Bmw = 4;  // bitmap words per row (<= 128 fields)
 
@@ -2647,6 +2320,7 @@ __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
   int32_t* sz = reinterpret_cast<int32_t*>(lds + cap);                 // [num_var][64] payload bytes
   uint32_t* pbt = reinterpret_cast<uint32_t*>(sz + L.num_var * 64);     // [NW][64][bmw] partial null bits
   const int bmw = L.bitmap_bytes >> 2;
+  uint32_t* tbad = pbt + NW * 64 * bmw;  // [2] by tile parity: a record's size disagrees with its offsets
   const int64_t ntiles = (L.num_rows + 63) / 64;
   int fk0 = 0, fk1 = 0;
   const bool has_fix = fix_batch(L, wave, &fk0, &fk1);
@@ -2785,6 +2459,7 @@ __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
         if ((NUL & 1) && fk0 + k < fk1 && live && fix[fk0 + k].validity &&
             !((vbyte_get(C0.fvb[k], fix[fk0 + k].validity + (ii >> 3)) >> (ii & 7)) & 1))
           null_bit(fix[fk0 + k].slot);
+      if (tid == 0) tbad[t & 1] = 0u;  // (last read by tile t - 2's store, two barriers ago)
       uint32_t* pw = pbt + (wave * 64 + lane) * bmw;
       pw[0] = (uint32_t)pl;
       if (bmw > 1) pw[1] = (uint32_t)(pl >> 32);
@@ -2795,8 +2470,20 @@ __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
     __syncthreads();  // B1
     V9_STAMP(2);
     if (tiled) {
-      // ---- P2: header and bitmap (wave 0), positions
-      if (wave == 0 && live) {  // Encoders.encode frame header; BinaryRowWriter.reset + setNullAt
+      // ---- P2: the record's size against its offsets (columns changed since encoded_size:
+      // its bytes would overrun its row -- nothing of it is written, the tile is not stored,
+      // FORY_ERR_ENCODER), header and bitmap (wave 0), positions
+      int32_t need = HDR + L.fixed_size;
+      for (int u = 0; u < L.num_var; ++u) {
+        const int32_t su = sz[u * 64 + lane];
+        need += su > 0 ? su : 0;
+      }
+      const bool wr = live && need == C0.end - C0.beg;  // this lane writes its record
+      if (live && !wr) {
+        tbad[t & 1] = 1u;
+        set_status(status, FORY_ERR_ENCODER);
+      }
+      if (wave == 0 && wr) {  // Encoders.encode frame header; BinaryRowWriter.reset + setNullAt
         if (HDR == 12) {
           st32(fp, (uint32_t)(C0.end - C0.beg - 4));
           st64_lds(fp + 4, (uint64_t)L.schema_hash);
@@ -2822,13 +2509,13 @@ __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
             const int32_t s = sz[u * 64 + lane];
             acc += s > 0 ? s : 0;
           }
-          pos[k] = live && sz[v * 64 + lane] >= 0 ? acc : -1;
+          pos[k] = wr && sz[v * 64 + lane] >= 0 ? acc : -1;
         }
       }
       // ---- P3: fixed slots (BinaryRowWriter.write: zero-extended; null -> 0)
       sched_fence();
       ready_vals(FV);
-      if (has_fix && live) {
+      if (has_fix && wr) {
 #pragma unroll
         for (int k = 0; k < kFixBatch; ++k) {
           if (fk0 + k >= fk1) continue;
@@ -2844,7 +2531,7 @@ __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
 #pragma unroll
       for (int k = 0; k < OWN; ++k) {
         const int v = wave + k * NW;
-        if (v >= L.num_var || !live) continue;
+        if (v >= L.num_var || !wr) continue;
         const VarFieldDev& f = vf[v];
         uint8_t* sl = slots + 8 * f.slot;
         const int64_t n = (int64_t)C0.e1[k] - C0.e0[k];
@@ -2881,7 +2568,7 @@ __device__ __forceinline__ void var_encode_flat9_body(FORY_V9_PARAMS) {
     V9_STAMP(4);
     __syncthreads();  // B2: the image is complete
     V9_STAMP(5);
-    if (tiled && L.kn.dbg_skip != 2) {
+    if (tiled && !tbad[t & 1]) {  // (a record whose size disagrees with its offsets: not stored)
       uint8_t* g = out + B0 - mis;  // 16-byte aligned
       const int tot = (int)total;
       const int nch = (tot + 15) >> 4;
@@ -2910,14 +2597,6 @@ template <int HDR, int NW, int OWN, int K, int NUL>
 __global__ __launch_bounds__(64 * NW) void var_encode_flat9_kernel(FORY_V9_PARAMS) {
   var_encode_flat9_body<HDR, NW, OWN, K, NUL>(L, prog, cols, fix, vf, offs, out, capacity, status, cap, sp);
 }
-
-// (A/B, FORY_ROWFMT_VARENC=10) the same held to 128 VGPRs: 4 workgroups per CU, some spilled
-template <int HDR, int NW, int OWN, int K, int NUL>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) void var_encode_flat9_lean_kernel(
-    FORY_V9_PARAMS) {
-  var_encode_flat9_body<HDR, NW, OWN, K, NUL>(L, prog, cols, fix, vf, offs, out, capacity, status, cap, sp);
-}
-
 
 __device__ __forceinline__ int64_t wave_incl_scan64(int64_t x, int lane) {
 #pragma unroll
@@ -3195,7 +2874,6 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
     }
   }
   __syncthreads();
-  if (WRITE && L.kn.dbg_skip == 1) return;  // debug: the staging alone (timing)
   DEC_STAMP(1);
   const int64_t i = r0 + lane;
   const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
@@ -3725,49 +3403,9 @@ void launch_flat_enc7(const VarLaunch& L0, const int64_t* offs, uint8_t* out, in
                      sp.cap, sp);
 }
 
-// Encode v8 LDS: row image, NW span staging slots, the payload-size table, row starts.
-size_t flat8_lds(const VarLaunch& L, int cap, int slot, int nw) {
-  return (size_t)cap + (size_t)nw * slot + (size_t)L.num_var * 64 * sizeof(int32_t) + 64 * sizeof(int32_t);
-}
-
-// Span staging slot of a wave in encode v8: the tile spans of the var fields it owns at
-// 1.25x the batch's mean var bytes per field, + slack; 256-B granular, [1, 32] KiB.
-int flat8_slot(const VarLaunch& L, int64_t capacity, int nw) {
-  if (L.kn.var_stg) return L.kn.var_stg;
-  const int own = (L.num_var + nw - 1) / nw;
-  int64_t var_row = L.num_rows > 0 ? capacity / L.num_rows - L.fixed_size - frame_header_bytes(L.frame) : 0;
-  if (var_row < 0) var_row = 0;
-  const int64_t per = L.num_var > 0 ? 64 * var_row / L.num_var : 0;
-  int64_t b = own * (per * 5 / 4 + 64);
-  b = (b + 255) & ~int64_t(255);
-  return (int)(b < 1024 ? 1024 : (b > 32768 ? 32768 : b));
-}
-
-template <int HDR, int NW, int OWN>
-void launch_flat_enc8(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
-                      int cap, hipStream_t s) {
-  VarLaunch L = L0;
-  L.pl_all = 1;
-  auto* k = &var_encode_flat8_kernel<HDR, NW, OWN>;
-  const int slot = flat8_slot(L, capacity, NW);
-  const size_t lds = flat8_lds(L, cap, slot, NW);
-  raise_lds_cap(k);
-  auto* k2 = &var_encode_flat_kernel<HDR, NW, false, true>;  // tiles beyond the image
-  L.stg_bytes = enc_stg_bytes(k2, L, capacity, cap, NW);
-  const SpillArgs sp = spill_args(L, cap);
-  (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
-  var_diag(L, "encode v8", k, 64 * NW, cap, slot, lds);
-  hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows + 63) / 64)), dim3(64 * NW), lds, s, L, L.prog, L.cols, L.fix,
-                     L.vf, offs, out, capacity, status, cap, slot, sp);
-  raise_lds_cap(k2);
-  hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds_enc(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
-                     flat_lds_enc(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status,
-                     sp.cap, sp);
-}
-
-// Encode v9 LDS: row image, the payload-size table, the partial null-bit words.
+// Encode v9 LDS: row image, the payload-size table, the partial null-bit words, two tile flags.
 size_t flat9_lds(const VarLaunch& L, int cap, int nw) {
-  return (size_t)cap + (size_t)L.num_var * 64 * sizeof(int32_t) + (size_t)nw * 64 * (L.bitmap_bytes >> 2) * 4;
+  return (size_t)cap + (size_t)L.num_var * 64 * sizeof(int32_t) + (size_t)nw * 64 * (L.bitmap_bytes >> 2) * 4 + 8;
 }
 
 // Plans encode v9 takes: fixed fields and strings / binary only, one fixed batch per wave.
@@ -3782,15 +3420,14 @@ void launch_flat_enc9(const VarLaunch& L0, const int64_t* offs, uint8_t* out, in
                       int cap, hipStream_t s) {
   VarLaunch L = L0;
   L.pl_all = 1;
-  // FORY_ROWFMT_VARENC=9: 2 tiles per workgroup, =10: the same held to 4 workgroups per CU
+  // 2 tiles per workgroup; one instantiation per column nullability (NUL bit 0 fixed, bit 1 var)
   using KFn = decltype(&var_encode_flat9_kernel<HDR, NW, 2, 2, 3>);
-  const bool lean = L.kn.var_enc == 10;
   KFn k;
   switch (L.nullable & 3) {
-    case 0: k = lean ? &var_encode_flat9_lean_kernel<HDR, NW, 2, 2, 0> : &var_encode_flat9_kernel<HDR, NW, 2, 2, 0>; break;
-    case 1: k = lean ? &var_encode_flat9_lean_kernel<HDR, NW, 2, 2, 1> : &var_encode_flat9_kernel<HDR, NW, 2, 2, 1>; break;
-    case 2: k = lean ? &var_encode_flat9_lean_kernel<HDR, NW, 2, 2, 2> : &var_encode_flat9_kernel<HDR, NW, 2, 2, 2>; break;
-    default: k = lean ? &var_encode_flat9_lean_kernel<HDR, NW, 2, 2, 3> : &var_encode_flat9_kernel<HDR, NW, 2, 2, 3>;
+    case 0: k = &var_encode_flat9_kernel<HDR, NW, 2, 2, 0>; break;
+    case 1: k = &var_encode_flat9_kernel<HDR, NW, 2, 2, 1>; break;
+    case 2: k = &var_encode_flat9_kernel<HDR, NW, 2, 2, 2>; break;
+    default: k = &var_encode_flat9_kernel<HDR, NW, 2, 2, 3>;
   }
   const int K = 2;
   const size_t lds = flat9_lds(L, cap, NW);
@@ -3824,17 +3461,14 @@ void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int6
   // defaults (measured): plans with nested structs -> the round-3 tile kernel
   // (Nested 0.74 vs v7 0.79 ms); flat plans of fixed fields + strings -> v9 (Mixed 3.2 vs
   // v7 3.6, round 3 4.5 ms); other flat plans (lists) -> v7. FORY_ROWFMT_VARENC=1 / 7 / 9
-  // force round 3 / v7 / v9 where they apply, =8 encode v8.
+  // force round 3 / v7 / v9 where they apply (the parity suite runs every one).
   const int e = L.kn.var_enc;
   const bool v7 = e != 1 && L.num_var <= kOwnVar * NW;
   if (L.num_struct) {
     if (v7 && e == 7) launch_flat_enc7_own<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
     else launch_flat_enc_t<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
-  } else if ((e == 0 || e == 9 || e == 10) && flat9_fits(L, NW)) {
+  } else if ((e == 0 || e == 9) && flat9_fits(L, NW)) {
     launch_flat_enc9<HDR, NW>(L, offs, out, capacity, status, cap, s);
-  } else if (v7 && L.fix16 && L.kn.var_enc == 8 && L.num_rows >= 128) {
-    if (L.num_var <= 2 * NW) launch_flat_enc8<HDR, NW, 2>(L, offs, out, capacity, status, cap, s);
-    else launch_flat_enc8<HDR, NW, kOwnVar>(L, offs, out, capacity, status, cap, s);
   } else {
     if (v7) launch_flat_enc7_own<HDR, NW, false>(L, offs, out, capacity, status, cap, s);
     else launch_flat_enc_t<HDR, NW, false>(L, offs, out, capacity, status, cap, s);

@@ -61,7 +61,7 @@ Binary = _jt("Binary", ArrowType.BINARY, True)
 BigDecimal = type("BigDecimal", (_JavaType,), {"type_id": ArrowType.DECIMAL128, "nullable": True,
                                                "precision": 38, "scale": 18})
 BigInteger = type("BigInteger", (_JavaType,), {"type_id": ArrowType.DECIMAL128, "nullable": True,
-                                               "precision": 38, "scale": 0})
+                                               "precision": 38, "scale": 0, "big_integer": True})
 
 
 def lower_camel_to_lower_underscore(s: str) -> str:
@@ -102,6 +102,8 @@ def _infer_field(name: str, tp, walked: List[type]) -> Field:
         return DataTypes.map_field(name, key, _infer_field("value", vt, walked))
     if isinstance(tp, type) and issubclass(tp, _JavaType):
         if tp.type_id == ArrowType.DECIMAL128:
+            if getattr(tp, "big_integer", False):  # toByteArray() bytes (BaseBinaryEncoderBuilder.java:192-194)
+                return Field(name, DataTypes.big_integer(), tp.nullable)
             return Field(name, DataTypes.decimal(tp.precision, tp.scale), tp.nullable)
         return Field(name, DataType(tp.type_id), tp.nullable)
     if isinstance(tp, type) and getattr(tp, "__annotations__", None):

@@ -67,6 +67,10 @@ class DataType:
     id: int
     precision: int = 0  # DECIMAL128 only (Arrow Decimal(precision, scale)); neither enters the hash
     scale: int = 0
+    # DECIMAL128 only: the bean field is java.math.BigInteger (Decimal(38, 0),
+    # TypeInference.java:203-204), which the codec writes as toByteArray() bytes
+    # (BaseBinaryEncoderBuilder.java:192-194), not with writeDecimal. Not in the hash.
+    big_integer: bool = False
 
     @property
     def width(self) -> int:
@@ -80,7 +84,7 @@ class DataType:
 
     def __repr__(self) -> str:
         if self.id == ArrowType.DECIMAL128:
-            return f"decimal({self.precision}, {self.scale})"
+            return "biginteger" if self.big_integer else f"decimal({self.precision}, {self.scale})"
         return _NAMES.get(self.id, str(self.id))
 
 
@@ -168,6 +172,13 @@ class DataTypes:
         return DataType(ArrowType.DECIMAL128, precision, scale)
 
     @staticmethod
+    def big_integer() -> DataType:
+        """The type of a java.math.BigInteger bean field: DataTypes.bigintDecimal() =
+        decimal(38, 0) (DataTypes.java:300-302, TypeInference.java:203-204), marked as a
+        BigInteger so the row holds value.toByteArray() (BaseBinaryEncoderBuilder.java:192-194)."""
+        return DataType(ArrowType.DECIMAL128, 38, 0, True)
+
+    @staticmethod
     def field(name: str, type_: DataType, nullable: bool = True,
               children: Optional[Sequence[Field]] = None) -> Field:
         return Field(name, type_, nullable, list(children or []))
@@ -235,9 +246,15 @@ def flatten(schema: Schema):
     return arr, len(out)
 
 
+FORY_DECIMAL_BIGINTEGER = 0x100  # include/fory_rowfmt.h
+
+
 def desc_reserved(t: DataType) -> int:
-    """fory_field_desc.reserved: a decimal's precision (0 = 38), else 0."""
-    return (t.precision or 38) if t.id == ArrowType.DECIMAL128 else 0
+    """fory_field_desc.reserved: a decimal's precision (0 = 38), FORY_DECIMAL_BIGINTEGER for
+    a BigInteger field, else 0."""
+    if t.id != ArrowType.DECIMAL128:
+        return 0
+    return FORY_DECIMAL_BIGINTEGER if t.big_integer else (t.precision or 38)
 
 
 def preorder(schema: Schema) -> List[Field]:

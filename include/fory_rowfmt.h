@@ -70,7 +70,8 @@ enum fory_type_id {
   FORY_TYPE_BINARY = 14,
   FORY_TYPE_DATE32 = 16,
   FORY_TYPE_TIMESTAMP = 18,
-  FORY_TYPE_DECIMAL = 23,   /* ArrowType.DECIMAL (= DECIMAL128's id): BigDecimal / BigInteger fields */
+  FORY_TYPE_DECIMAL = 23,   /* ArrowType.DECIMAL (= DECIMAL128's id): BigDecimal / BigInteger fields
+                               (BigInteger: reserved = FORY_DECIMAL_BIGINTEGER) */
   FORY_TYPE_LIST = 25,
   FORY_TYPE_STRUCT = 26,
   FORY_TYPE_MAP = 30
@@ -89,8 +90,22 @@ typedef struct fory_field_desc {
   int32_t type_id;       /* enum fory_type_id */
   int32_t nullable;      /* 1 = boxed/String/bean/List (TypeInference.java:182-247) */
   int32_t num_children;  /* STRUCT: >= 0, LIST: 1, MAP: 2, others: 0 */
-  int32_t reserved;      /* DECIMAL: the precision (0 = 38, DecimalUtils.MAX_PRECISION); else 0 */
+  int32_t reserved;      /* DECIMAL: the precision (0 = 38, DecimalUtils.MAX_PRECISION), or
+                            FORY_DECIMAL_BIGINTEGER; else 0 */
 } fory_field_desc;
+
+/* fory_field_desc.reserved of a DECIMAL node whose bean field is java.math.BigInteger
+ * (TypeInference.java:203-204 types it Decimal(38, 0), like a BigDecimal's type but scale 0).
+ * The codec does not write it with writeDecimal: it writes value.toByteArray()
+ * (BaseBinaryEncoderBuilder.java:192-194) through BinaryWriter.write(int, byte[]) ->
+ * writeUnaligned (BinaryWriter.java:167-194): the minimal big-endian two's complement,
+ * bitLength / 8 + 1 bytes (1..16 for a decimal128 value), zero-padded to 8, behind an
+ * (offset, length) slot; and reads it back as new BigInteger(bytes)
+ * (BaseBinaryEncoderBuilder.java:559-560). No precision check applies. Its column is a
+ * decimal128 column like any DECIMAL's (the value at scale 0); a row whose bytes do not
+ * fit one (0 or more than 16 bytes) decodes as FORY_ERR_CORRUPT. The precision bits
+ * (low 8) must be 0 or 38 with this flag. */
+#define FORY_DECIMAL_BIGINTEGER 0x100
 
 /* Column of one field (index = pre-order index of its fory_field_desc).
  *  fixed-width : values = length * width bytes, little-endian
@@ -104,7 +119,9 @@ typedef struct fory_field_desc {
  *                out of line as 32 bytes sign-extended behind an (offset, 32) slot
  *                (BinaryWriter.writeDecimal, BinaryWriter.java:214-230,
  *                DecimalUtils.DECIMAL_BYTE_LENGTH = 32); |value| > 10^precision - 1
- *                is FORY_ERR_UNSUPPORTED on encode (DecimalUtility.checkPrecisionAndScale)
+ *                is FORY_ERR_UNSUPPORTED on encode (DecimalUtility.checkPrecisionAndScale).
+ *                BigInteger fields (FORY_DECIMAL_BIGINTEGER): the same column; the row holds
+ *                toByteArray()'s bytes instead (see FORY_DECIMAL_BIGINTEGER)
  *  STRUCT      : values/offsets unused; children have the same length
  *  validity    : Arrow validity bitmap, LSB-first, 1 = valid; NULL = all valid.
  *                Only read/written for nullable fields.
@@ -403,6 +420,12 @@ int fory_rowfmt_host_decode_var(fory_host_ctx* ctx, const fory_column* host_out_
 int fory_rowfmt_host_decode_var_into(fory_host_ctx* ctx, const void* host_rows, const int64_t* host_row_offsets,
                                      int64_t num_rows, int32_t frame_mode, const fory_column* host_out_cols,
                                      int64_t* host_counts, int64_t* host_bytes);
+/* Pins [host_ptr, host_ptr + bytes) (hipHostRegister): its copies become direct DMAs.
+ * Registrations pin whole pages, so two live registrations may not share a page
+ * (FORY_ERR_INVALID_ARGUMENT: register page-exclusive buffers). Unregister takes the
+ * start of a registered range (else FORY_ERR_INVALID_ARGUMENT) and checks that the
+ * runtime no longer maps the range (FORY_ERR_DEVICE otherwise). Unregister before the
+ * memory is freed. */
 int fory_rowfmt_host_register(void* host_ptr, int64_t bytes);
 int fory_rowfmt_host_unregister(void* host_ptr);
 

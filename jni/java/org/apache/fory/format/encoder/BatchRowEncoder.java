@@ -72,7 +72,8 @@ public final class BatchRowEncoder<T> implements AutoCloseable {
   public BatchRowEncoder(Class<T> beanClass, int device, long chunkRows) {
     this.schema = TypeInference.inferSchema(beanClass);
     this.beans = new BeanColumns<>(beanClass, schema);
-    this.plan = nPlanCreate(DeviceSchemas.flatten(schema)); // EncoderException / UnsupportedOperation
+    // BigInteger fields flagged (FORY_DECIMAL_BIGINTEGER): the row holds toByteArray()
+    this.plan = nPlanCreate(DeviceSchemas.flatten(schema, beans.bigIntegerColumns())); // EncoderException / UnsupportedOperation
     this.schemaHash = nSchemaHash(plan);
     this.rowSize = nRowSize(plan);
     Preconditions.checkArgument(
@@ -131,7 +132,7 @@ public final class BatchRowEncoder<T> implements AutoCloseable {
     }
     ByteBuffer buf = scratch(offs[n]);
     for (byte[] b : each) buf.put(b);
-    long addr = MemoryBuffer.fromByteBuffer(buf).getUnsafeAddress();
+    long addr = ColumnBatch.baseAddress(buf); // the rows' start (buf's position is past them)
     ColumnBatch out = new ColumnBatch(schema);
     if (rowSize >= 0) {
       for (byte[] b : each) {
@@ -164,7 +165,7 @@ public final class BatchRowEncoder<T> implements AutoCloseable {
       nEncodeWindows(hostCtx, cols, numRows, frame, new long[] {buffer.getUnsafeAddress() + at}, new long[] {need}, bytes);
     } else {
       ByteBuffer tmp = scratch(need);
-      long ta = MemoryBuffer.fromByteBuffer(tmp).getUnsafeAddress();
+      long ta = ColumnBatch.baseAddress(tmp);
       nEncodeWindows(hostCtx, cols, numRows, frame, new long[] {ta}, new long[] {need}, bytes);
       buffer.copyFromUnsafe(at, null, ta, need);
     }
@@ -268,7 +269,7 @@ public final class BatchRowEncoder<T> implements AutoCloseable {
     if (!in.isOffHeap()) { // a heap buffer has no native address: staged through a direct buffer
       int len = in.remaining();
       ByteBuffer tmp = scratch(len);
-      in.copyToUnsafe(in.readerIndex(), null, MemoryBuffer.fromByteBuffer(tmp).getUnsafeAddress(), len);
+      in.copyToUnsafe(in.readerIndex(), null, ColumnBatch.baseAddress(tmp), len);
       tmp.limit(len);
       MemoryBuffer staged = MemoryBuffer.fromByteBuffer(tmp);
       decode(staged, numRows, out);

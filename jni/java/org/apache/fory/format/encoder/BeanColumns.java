@@ -44,8 +44,11 @@ import org.apache.fory.util.Preconditions;
  *       (DecimalUtils.MAX_SCALE); another scale is an UnsupportedOperationException, as
  *       DecimalUtility.checkPrecisionAndScale throws in BinaryWriter.writeDecimal
  *       (BinaryWriter.java:214-225);
- *   <li>{@code BigInteger} as decimal128 at scale 0 (TypeInference.java:203-204); the row
- *       holds {@code toByteArray()} (BaseBinaryEncoderBuilder.java:192-194);
+ *   <li>{@code BigInteger} as decimal128 at scale 0 (TypeInference.java:203-204), its column
+ *       flagged FORY_DECIMAL_BIGINTEGER in the plan ({@link #bigIntegerColumns}), so the device
+ *       writes {@code toByteArray()} into the row (BaseBinaryEncoderBuilder.java:192-194) and
+ *       reads it back as {@code new BigInteger(bytes)} (:559-560); a value beyond 128 bits has
+ *       no decimal128 column value (UnsupportedOperationException);
  *   <li>{@code LocalDate} / {@code java.sql.Date} as days ({@code
  *       DateTimeUtils.localDateToDays / fromJavaDate}), {@code Timestamp} / {@code Instant} as
  *       microseconds ({@code fromJavaTimestamp / instantToMicros}), enums by {@code name()},
@@ -105,6 +108,18 @@ final class BeanColumns<T> {
 
   int numColumns() {
     return numColumns;
+  }
+
+  /** Per pre-order column: a BigInteger field (DeviceSchemas.flatten flags its descriptor). */
+  boolean[] bigIntegerColumns() {
+    boolean[] out = new boolean[numColumns];
+    for (Node f : top) markBigInteger(f, out);
+    return out;
+  }
+
+  private static void markBigInteger(Node f, boolean[] out) {
+    if (f.kind == BIGINT) out[f.column] = true;
+    for (Node c : f.children) markBigInteger(c, out);
   }
 
   // ---------------------------------------------------------------- schema walk
@@ -249,6 +264,8 @@ final class BeanColumns<T> {
       c.validity = Col.room(c.validity, 8);
       c.offsets = Col.room(c.offsets, 8);
       c.values = Col.room(c.values, 16);
+      // (ColumnBatch takes each buffer's byte 0 as the column start: their positions are
+      // past the data here)
       out.set(i, c.values, c.offsets, c.validity, c.length);
     }
   }

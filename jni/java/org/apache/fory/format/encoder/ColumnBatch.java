@@ -129,7 +129,19 @@ public final class ColumnBatch {
   }
 
   private static long address(ByteBuffer b) {
-    return b == null ? 0 : MemoryBuffer.fromByteBuffer(b).getUnsafeAddress(); // MemoryBuffer.java:295
+    return b == null ? 0 : baseAddress(b);
+  }
+
+  /**
+   * The native address of a direct buffer's byte 0, whatever its position: {@code
+   * MemoryBuffer.fromByteBuffer(b).getUnsafeAddress()} adds {@code b.position()}
+   * (MemoryBuffer.java:2639-2640), and buffers that were just written hold their position
+   * at the end of the data.
+   */
+  static long baseAddress(ByteBuffer b) {
+    ByteBuffer at0 = b.duplicate();
+    at0.clear(); // position 0 (a duplicate: b's own position and limit are kept)
+    return MemoryBuffer.fromByteBuffer(at0).getUnsafeAddress(); // MemoryBuffer.java:295
   }
 
   /** The direct buffer of column i's values (null for struct / list / map nodes). */

@@ -11,7 +11,7 @@ import org.apache.fory.format.type.DataTypes;
 
 /**
  * Flattens an inferred row schema into the pre-order {@code fory_field_desc[]} the C-ABI
- * takes: four ints per node, {@code {typeId, nullable, numChildren, 0}}. The schema comes
+ * takes: four ints per node, {@code {typeId, nullable, numChildren, reserved}}. The schema comes
  * from {@code TypeInference.inferSchema(beanClass)} (TypeInference.java:58-80), so the
  * field order (Descriptor order, names sorted) and the schema hash
  * (DataTypes.computeSchemaHash, DataTypes.java:499-544) are the reference's own.
@@ -19,8 +19,23 @@ import org.apache.fory.format.type.DataTypes;
 public final class DeviceSchemas {
   private DeviceSchemas() {}
 
+  /** include/fory_rowfmt.h: reserved word of a decimal node that is a java.math.BigInteger field. */
+  static final int FORY_DECIMAL_BIGINTEGER = 0x100;
+
   /** Pre-order {typeId, nullable, numChildren, 0} of every field node. */
   public static int[] flatten(Schema schema) {
+    return flatten(schema, null);
+  }
+
+  /**
+   * Pre-order {typeId, nullable, numChildren, reserved} of every field node; reserved is
+   * FORY_DECIMAL_BIGINTEGER for the columns {@code bigInteger} marks (decimal(38, 0) nodes of
+   * BigInteger fields, which the codec writes as toByteArray(), BaseBinaryEncoderBuilder.java:192-194,
+   * not with writeDecimal), else 0 (a decimal's precision 0 = 38). The Arrow schema alone
+   * cannot tell a BigInteger from a BigDecimal of scale 0: the bean class does
+   * (BeanColumns.bigIntegerColumns).
+   */
+  public static int[] flatten(Schema schema, boolean[] bigInteger) {
     int nodes = 0;
     for (Field f : schema.getFields()) {
       nodes += count(f);
@@ -29,6 +44,11 @@ public final class DeviceSchemas {
     int at = 0;
     for (Field f : schema.getFields()) {
       at = visit(f, out, at);
+    }
+    if (bigInteger != null) {
+      for (int i = 0; i < nodes && i < bigInteger.length; i++) {
+        if (bigInteger[i]) out[4 * i + 3] = FORY_DECIMAL_BIGINTEGER;
+      }
     }
     return out;
   }

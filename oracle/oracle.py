@@ -70,9 +70,12 @@ def _desc(schema):
     out = []
 
     def visit(f):
-        # a decimal's descriptor carries its precision (0 = 38); the scale is the column's
-        prec = (getattr(f.type, "precision", 0) or 38) if f.type.id == _DECIMAL else 0
-        out.append((f.type.id, 1 if f.nullable else 0, len(f.children), prec))
+        # a decimal's descriptor carries its precision (0 = 38), or FORY_DECIMAL_BIGINTEGER for a
+        # BigInteger field; the scale is the column's
+        res = 0
+        if f.type.id == _DECIMAL:
+            res = _BIGINTEGER if getattr(f.type, "big_integer", False) else (getattr(f.type, "precision", 0) or 38)
+        out.append((f.type.id, 1 if f.nullable else 0, len(f.children), res))
         for c in f.children:
             visit(c)
 
@@ -85,6 +88,7 @@ def _desc(schema):
 
 
 _DECIMAL = 23  # ArrowType.DECIMAL (DECIMAL128's id)
+_BIGINTEGER = 0x100  # FORY_DECIMAL_BIGINTEGER (include/fory_rowfmt.h)
 
 
 def _p(a: Optional[np.ndarray]):

@@ -16,6 +16,7 @@
  *   - map layout           F/row/binary/BinaryMap.java:30-77 (writer:
  *                          F/encoder/BaseBinaryEncoderBuilder.java:370-427)
  *   - per-type dispatch    F/encoder/BaseBinaryEncoderBuilder.java:149-490
+ *                          (BigInteger: :192-194 write, :559-560 read)
  *   - framing              F/encoder/Encoders.java:177-225
  *   - readers              F/row/binary/BinaryRow.java:110-123,
  *                          F/row/binary/UnsafeTrait.java:68-197,
@@ -49,6 +50,7 @@ typedef struct onode {
   int nullable;
   int width;      /* DataTypes.getTypeWidth (DataTypes.java:68-133), -1 = varlen */
   int precision;  /* DECIMAL: from the descriptor's reserved word (0 = 38) */
+  int biginteger; /* DECIMAL with FORY_DECIMAL_BIGINTEGER: a java.math.BigInteger field */
   int nchild;
   int child[64];  /* desc indices of children (struct fields / list item) */
 } onode;
@@ -76,7 +78,8 @@ static int parse(const fory_field_desc* d, int n, int at, otree* t) {
   nd->type_id = d[at].type_id;
   nd->nullable = d[at].nullable;
   nd->width = type_width(d[at].type_id);
-  nd->precision = d[at].type_id == FORY_TYPE_DECIMAL ? (d[at].reserved > 0 ? d[at].reserved : 38) : 0;
+  nd->biginteger = d[at].type_id == FORY_TYPE_DECIMAL && (d[at].reserved & FORY_DECIMAL_BIGINTEGER);
+  nd->precision = d[at].type_id == FORY_TYPE_DECIMAL ? ((d[at].reserved & 0xff) > 0 ? (d[at].reserved & 0xff) : 38) : 0;
   if (nd->precision > 38) return -1;
   nd->nchild = 0;
   int next = at + 1;
@@ -268,6 +271,40 @@ static int w_write_decimal(owriter* w, int64_t ordinal, const uint8_t* v16, int 
   return 0;
 }
 
+/* A java.math.BigInteger field (BaseBinaryEncoderBuilder.java:192-194):
+ * writer.write(ordinal, value.toByteArray()) -> BinaryWriter.write(int, byte[])
+ * (BinaryWriter.java:167-170) -> writeUnaligned. toByteArray() is the minimal big-endian
+ * two's complement: bitLength() / 8 + 1 bytes, bitLength() = the bits of v without its
+ * sign bit (of ~v = -v - 1 when v < 0). The value here is an Arrow decimal128 (16 bytes,
+ * little-endian two's complement, scale 0). */
+static int bigint_to_bytes(const uint8_t* v16, uint8_t out[16]) {
+  __int128 v;
+  memcpy(&v, v16, 16);
+  unsigned __int128 m = v < 0 ? (unsigned __int128)~v : (unsigned __int128)v;
+  int bits = 0;
+  while (m) { bits++; m >>= 1; }
+  int len = bits / 8 + 1;
+  for (int j = 0; j < len; j++) out[j] = v16[len - 1 - j];  /* big-endian: most significant first */
+  return len;
+}
+
+static void w_write_biginteger(owriter* w, int64_t ordinal, const uint8_t* v16) {
+  uint8_t be[16];
+  int len = bigint_to_bytes(v16, be);
+  w_write_unaligned(w, ordinal, be, len);
+}
+
+/* new BigInteger(byte[]) (BaseBinaryEncoderBuilder.java:559-560) of n row bytes into a
+ * decimal128: big-endian two's complement, sign-extended. n == 0 is Java's
+ * NumberFormatException ("Zero length BigInteger"); more than 16 bytes do not fit a
+ * decimal128 (toByteArray never pads, so such a value exceeds 128 bits). Returns 0 or -1. */
+static int bigint_from_bytes(const uint8_t* p, int64_t n, uint8_t out16[16]) {
+  if (n < 1 || n > 16) return -1;
+  memset(out16, (p[0] & 0x80) ? 0xFF : 0x00, 16);
+  for (int64_t j = 0; j < n; j++) out16[j] = p[n - 1 - j];
+  return 0;
+}
+
 /* ---------------------------------------------------------------------- */
 /* column access                                                           */
 /* ---------------------------------------------------------------------- */
@@ -403,6 +440,10 @@ static void write_value(owriter* w, int64_t ordinal, const otree* t, int idx,
       return;
     }
     case FORY_TYPE_DECIMAL:
+      if (nd->biginteger) {  /* BigInteger: toByteArray() bytes, no precision check */
+        w_write_biginteger(w, ordinal, (const uint8_t*)c->values + 16 * i);
+        return;
+      }
       if (w_write_decimal(w, ordinal, (const uint8_t*)c->values + 16 * i, nd->precision)) b->unsupported = 1;
       return;
     case FORY_TYPE_STRUCT:
@@ -577,6 +618,12 @@ static void read_payload(odec* D, const otree* t, int idx, const fory_column* co
     case FORY_TYPE_DECIMAL: { /* UnsafeTrait.getDecimal :139-150: DECIMAL_BYTE_LENGTH = 32 bytes at the slot's
                                  offset, DecimalUtility.getBigDecimalFromArrowBuf; an Arrow decimal128
                                  output holds it when bytes 16..31 are the sign extension of byte 15 */
+      if (nd->biginteger) {  /* getBinary -> new BigInteger(bytes) */
+        uint8_t v16[16];
+        if (bigint_from_bytes(D->p + at, size, v16)) { D->bad = 1; return; }
+        if (!D->sizing) memcpy((uint8_t*)c->values + 16 * i, v16, 16);
+        return;
+      }
       if (size != 32) { D->bad = 1; return; }
       const uint8_t* p = D->p + at;
       const uint8_t ext = (p[15] & 0x80) ? 0xFF : 0x00;

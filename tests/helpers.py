@@ -487,6 +487,15 @@ def random_value(f: Field, rng, depth: int = 0, null_p: float = 0.12):
             return [random_value(f.children[0], rng, depth + 1, null_p) for _ in range(k)]
         return [(random_value(f.children[0], rng, depth + 1, null_p), random_value(f.children[1], rng, depth + 1, null_p))
                 for _ in range(k)]
+    if t == ArrowType.DECIMAL128 and f.type.big_integer:  # any int128: toByteArray() of 1..16 bytes
+        r = rng.random()
+        if r < 0.25:  # the length boundaries of toByteArray() and the int128 extremes
+            edges = (0, -1, 127, 128, -128, -129, 255, 256, 32767, 32768, -32769, 2 ** 63, -(2 ** 63) - 1,
+                     2 ** 127 - 1, -(2 ** 127), 2 ** 119, -(2 ** 119) - 1)
+            return edges[int(rng.integers(0, len(edges)))]
+        bits = int(rng.integers(1, 128))
+        u = int.from_bytes(rng.bytes(16), "little") & ((1 << bits) - 1)
+        return -u - 1 if rng.random() < 0.5 else u
     if t == ArrowType.DECIMAL128:  # the unscaled value: up to `precision` digits, either sign
         p = f.type.precision or 38
         r = rng.random()

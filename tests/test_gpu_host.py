@@ -18,24 +18,6 @@ from helpers import catalog, collection_cases, columns_equal  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def run_isolated(case, *args):
-    """Runs test case `case` of this module in a fresh child process. The cases that
-    register and unregister host pages (hipHostRegister) run there: after such churn the
-    HIP runtime's own pageable-copy path in the same process once faulted at a later,
-    unrelated torch H2D copy of a numpy array (illegal address, test_gpu_parity, round 4;
-    round 2 saw the same at pageable copies of the host path). Our library never takes
-    that path; the suite's other tests do, so the churn stays out of their
-    process."""
-    import os
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    code = (f"import sys; sys.path[:0] = [{os.path.dirname(here)!r}, {here!r}]; "
-            f"import test_gpu_host as T; T.{case}(*{args!r}); print('isolated case ok')")
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0 and "isolated case ok" in r.stdout, (r.stdout[-4000:] + r.stderr[-4000:])
-
-
 def empty_like(schema, n):
     out = []
     for f in preorder(schema):
@@ -71,10 +53,6 @@ def test_host_pipeline_parity(name, n, frame):
 
 
 def test_host_pipeline_registered_buffers_and_errors():
-    run_isolated('case_host_pipeline_registered_buffers_and_errors')
-
-
-def case_host_pipeline_registered_buffers_and_errors():
     schema, make = catalog()["struct104"]
     n = 3000
     cols = make(n, 3)
@@ -101,7 +79,9 @@ def case_host_pipeline_registered_buffers_and_errors():
 def unregister_all(arrays):
     """Unregisters every array, each on its own: one failure must not leave the rest
     registered when numpy frees and re-issues their pages (round-2 cleanup stopped at
-    the first failure)."""
+    the first failure). The library checks that each range no longer reads as
+    registered (fory_rowfmt_host_unregister: FORY_ERR_DEVICE otherwise); here every
+    array's first and last byte are pageable again."""
     errors = []
     for a in arrays:
         try:
@@ -110,6 +90,21 @@ def unregister_all(arrays):
             errors.append(e)
     if errors:
         raise errors[0]
+    for a in arrays:
+        assert copy_path(a) == 0 and copy_path(a[-1:]) == 0
+
+
+@pytest.fixture(autouse=True)
+def _no_registration_left():
+    """Every test leaves no registration behind (a registration that outlives its numpy
+    buffer is how a later pageable copy could be DMA'd through a stale mapping)."""
+    yield
+    assert registered_ranges() == 0
+
+
+def registered_ranges():
+    import ctypes
+    return _internal("fory_rowfmt_internal_host_registered_ranges", ctypes.c_int, [])()
 
 
 def page_buffer(nbytes, pages_before=0):
@@ -148,10 +143,6 @@ def staged_pieces(hp):
 
 
 def test_host_copy_classification_is_by_whole_range():
-    run_isolated('case_host_copy_classification_is_by_whole_range')
-
-
-def case_host_copy_classification_is_by_whole_range():
     """The round-2 host-path fault mechanism, deterministically: a copy was judged
     pinned by its FIRST byte, so a range that begins inside a registration and runs
     past it (or a range whose pages were registered before and have been unregistered
@@ -184,10 +175,6 @@ def case_host_copy_classification_is_by_whole_range():
 
 @pytest.mark.parametrize("name", ["struct104", "mixed40_nulls", "maps"])
 def test_host_copies_straddling_a_registration(name):
-    run_isolated('case_host_copies_straddling_a_registration', name)
-
-
-def case_host_copies_straddling_a_registration(name):
     """Columns and output whose first pages are registered and whose rest is not (and
     pages registered, unregistered and re-used): every copy straddling a registration
     is staged (the context counts its staged pieces), the bytes equal the oracle's,
@@ -245,10 +232,6 @@ def case_host_copies_straddling_a_registration(name):
 
 
 def test_host_registered_buffers_are_never_staged():
-    run_isolated('case_host_registered_buffers_are_never_staged')
-
-
-def case_host_registered_buffers_are_never_staged():
     """Whole-range registered columns and output: every copy is a direct async DMA."""
     schema, make = catalog()["struct104"]
     n = 3000
@@ -397,10 +380,6 @@ def test_host_varlen_nested_collections(name, frame):
 
 @pytest.mark.parametrize("name", ["mixed40_nulls", "nested_nulls", "maps", "list_struct", "holder", "maps_nested"])
 def test_host_varlen_pipeline_registered(name):
-    run_isolated('case_host_varlen_pipeline_registered', name)
-
-
-def case_host_varlen_pipeline_registered(name):
     """Registered (pinned) host columns and output: the chunk pipeline's copies are
     asynchronous (H2D of chunk k+1 || encode of chunk k || D2H of chunk k-1), ordered
     by events only; bytes and offsets == the oracle over many chunks, twice on one
@@ -545,3 +524,27 @@ def test_host_varlen_decode_into_errors_and_empty():
     assert all(c.length == 0 for c in empty)
     assert columns_equal(schema, cols, hp.decode_var_into(expect, eoffs, n, 1)) == []  # usable after an error
     hp.close()
+
+
+def test_host_register_refuses_shared_pages_and_foreign_bases():
+    """fory_rowfmt_host_register pins whole pages: a second registration on a page of a live
+    one is refused; unregister takes only a registered range's start; after it, both ends of
+    the range read as unregistered."""
+    from fury_amd.format import IllegalArgumentException
+    buf, raw = page_buffer(5 * 4096)
+    a, b = buf[:4096 + 100], buf[4096 + 200:3 * 4096]  # b starts on a's second page
+    host_register(a)
+    try:
+        with pytest.raises(IllegalArgumentException):
+            host_register(b)
+        c = buf[3 * 4096:]  # pages of its own: fine
+        host_register(c)
+        assert registered_ranges() == 2
+        with pytest.raises(IllegalArgumentException):
+            host_unregister(a[8:])  # not a registered start
+        host_unregister(c)
+    finally:
+        host_unregister(a)
+    assert copy_path(a) == 0 and copy_path(buf[4096 + 99:4096 + 100]) == 0
+    host_register(b)  # a's pages are free again
+    host_unregister(b)

@@ -99,3 +99,37 @@ def test_v9_is_the_kernel_that_ran(kind, monkeypatch, capfd):
     RowEncoder(schema).encode(to_device(cols), n, 0)
     torch.cuda.synchronize()
     assert "encode v9 tile kernel" in capfd.readouterr().err
+
+
+@pytest.mark.parametrize("delta", [+24, -8, +300])
+def test_v9_offsets_from_other_columns_are_an_encoder_error(delta):
+    """encode with row offsets that encoded_size computed for other contents (a string's
+    length changed since): the record's bytes would overrun its row. v9 writes nothing of
+    it, does not store its tile and reports FORY_ERR_ENCODER; the other tiles are intact
+    and nothing lands outside the rows."""
+    from fury_amd.format import native
+    from fury_amd.format.errors import EncoderException
+    schema = _schema("no_validity")
+    n = 1000
+    rows = _rows(schema, n, 3)
+    rows[500]["s"] = "q" * 40
+    cols_a = build_columns(schema, rows)
+    changed = [dict(r) for r in rows]
+    changed[500]["s"] = "q" * (40 + delta)
+    cols_b = build_columns(schema, changed)
+    expect, offs = oracle.encode(schema, cols_a, n, 0)
+    total = int(offs[n])
+    enc = RowEncoder(schema)
+    dev_b = to_device(cols_b)
+    arr = native.column_array(dev_b)
+    d_offs = torch.from_numpy(offs).cuda()
+    out = torch.full((total + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda")
+    native.encode(enc.plan, arr, n, 0, d_offs, out, status, enc.workspace(n, arr))
+    with pytest.raises(EncoderException):
+        native.read_status(status)
+    got = out.cpu().numpy()
+    assert (got[total:] == 0xAB).all()
+    t0, t1 = int(offs[448]), int(offs[512])  # record 500's tile: not stored
+    assert (got[t0:t1] == 0xAB).all()
+    assert np.array_equal(got[:t0], expect[:t0]) and np.array_equal(got[t1:total], expect[t1:total])

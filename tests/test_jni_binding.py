@@ -124,3 +124,36 @@ def test_bean_columns_conversions():
     batch = read(os.path.join(JAVA, "ColumnBatch.java"))
     assert re.search(r"void set\(int \w+, ByteBuffer \w+, ByteBuffer \w+, ByteBuffer \w+, long \w+\)", batch)
     assert "static final int DECIMAL = 23;" in batch
+
+
+def test_direct_buffer_addresses_start_at_byte_zero():
+    """MemoryBuffer.fromByteBuffer(b).getUnsafeAddress() adds b.position() (reference
+    MemoryBuffer.java:2639-2649): a buffer that was just written (BeanColumns' columns, the
+    decode(byte[][]) staging) would hand the device an address past its data. Every native
+    address of a ByteBuffer goes through ColumnBatch.baseAddress (a position-0 duplicate)."""
+    batch = read(os.path.join(JAVA, "ColumnBatch.java"))
+    m = re.search(r"static long baseAddress\(ByteBuffer \w+\) \{(.*?)\n  \}", batch, re.S)
+    assert m and ".duplicate()" in m.group(1) and ".clear()" in m.group(1)
+    for name in ("BatchRowEncoder.java", "BeanColumns.java", "ColumnBatch.java"):
+        src = read(os.path.join(JAVA, name))
+        body = src.replace(m.group(0), "") if name == "ColumnBatch.java" else src
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)  # (comments may name the pattern)
+        # a ByteBuffer's address only through baseAddress (MemoryBuffers of a fresh allocateDirect
+        # or of a position-0 staging buffer are fine: those are not getUnsafeAddress'd here)
+        assert not re.search(r"fromByteBuffer\(\w+\)\.getUnsafeAddress\(\)", body), name
+    enc = read(os.path.join(JAVA, "BatchRowEncoder.java"))
+    assert "ColumnBatch.baseAddress(buf)" in enc
+
+
+def test_biginteger_columns_are_flagged():
+    """A BigInteger field's descriptor carries FORY_DECIMAL_BIGINTEGER (the row holds
+    toByteArray(), BaseBinaryEncoderBuilder.java:192-194), with the header's value."""
+    hdr = read(os.path.join(REPO, "include", "fory_rowfmt.h"))
+    val = re.search(r"#define FORY_DECIMAL_BIGINTEGER (0x[0-9a-fA-F]+)", hdr).group(1)
+    ds = read(os.path.join(JAVA, "DeviceSchemas.java"))
+    assert f"static final int FORY_DECIMAL_BIGINTEGER = {val};" in ds
+    assert re.search(r"public static int\[\] flatten\(Schema \w+, boolean\[\] \w+\)", ds)
+    enc = read(os.path.join(JAVA, "BatchRowEncoder.java"))
+    assert "DeviceSchemas.flatten(schema, beans.bigIntegerColumns())" in enc
+    bc = read(os.path.join(JAVA, "BeanColumns.java"))
+    assert "boolean[] bigIntegerColumns()" in bc and "f.kind == BIGINT" in bc

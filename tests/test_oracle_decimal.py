@@ -97,3 +97,82 @@ def test_decode_round_trip_and_corrupt_high_bytes():
     with pytest.raises(oracle.OracleError):
         oracle.decode(s, bad, offs, len(rows), 1)
     assert fixed == 32
+
+
+# --- java.math.BigInteger fields ------------------------------------------------------
+# BaseBinaryEncoderBuilder.java:192-194 writes writer.write(ordinal, value.toByteArray()):
+# BinaryWriter.write(int, byte[]) -> writeUnaligned (BinaryWriter.java:167-194), i.e. the
+# minimal big-endian two's complement (bitLength() / 8 + 1 bytes), zero-padded to 8, behind
+# an (offset, length) slot; :559-560 reads it back as new BigInteger(bytes). The vectors
+# below are BigInteger.toByteArray() worked by hand (java.math.BigInteger's documented
+# contract; no JDK here).
+BIGINT_VECTORS = [
+    (0, "00"), (-1, "ff"), (1, "01"), (127, "7f"), (128, "0080"), (-128, "80"), (-129, "ff7f"),
+    (255, "00ff"), (256, "0100"), (-256, "ff00"), (-257, "feff"), (32767, "7fff"), (32768, "008000"),
+    (2 ** 63 - 1, "7fffffffffffffff"), (2 ** 63, "008000000000000000"), (-(2 ** 63), "8000000000000000"),
+    (2 ** 127 - 1, "7f" + "ff" * 15), (-(2 ** 127), "80" + "00" * 15), (-(2 ** 127) + 1, "80" + "00" * 14 + "01"),
+]
+
+
+def big_schema(nullable=True):
+    return Schema([Field("n", DataTypes.big_integer(), nullable)])
+
+
+def test_java_biginteger_vectors_are_self_consistent():
+    # the hand vectors against Python's own minimal two's complement (a second derivation)
+    for v, hx in BIGINT_VECTORS:
+        n = v.bit_length() if v >= 0 else (-v - 1).bit_length()
+        assert len(hx) // 2 == n // 8 + 1
+        assert bytes.fromhex(hx) == v.to_bytes(n // 8 + 1, "big", signed=True)
+
+
+@pytest.mark.parametrize("v,hx", BIGINT_VECTORS)
+def test_biginteger_row_bytes(v, hx):
+    s = big_schema()
+    cols = build_columns(s, [{"n": v}])
+    buf, _ = oracle.encode(s, cols, 1, 0)
+    b = buf.tobytes()
+    want = bytes.fromhex(hx)
+    pad = -len(want) % 8
+    assert b[:8] == bytes(8)  # no null bit
+    assert b[8:16] == (16 << 32 | len(want)).to_bytes(8, "little")  # (offset 16, toByteArray().length)
+    assert b[16:] == want + bytes(pad)  # the bytes, then zeroOutPaddingBytes
+    dec = oracle.decode(s, buf, np.array([0, len(b)], np.int64), 1, 0)
+    assert decimal_value(dec[0].values[0], 0) == v
+
+
+def test_biginteger_null_and_frames():
+    s = big_schema()
+    cols = build_columns(s, [{"n": None}, {"n": -129}])
+    buf, offs = oracle.encode(s, cols, 2, 1)
+    b = buf.tobytes()
+    assert offs.tolist() == [0, 28, 28 + 12 + 24]
+    assert b[12:20] == bytes([1]) + bytes(7) and b[20:28] == bytes(8)  # null: bit set, slot zero
+    assert b[40 + 8:40 + 16] == (16 << 32 | 2).to_bytes(8, "little")
+    assert b[40 + 16:] == bytes.fromhex("ff7f") + bytes(6)
+
+
+def test_biginteger_corrupt_lengths():
+    s = big_schema(False)
+    cols = build_columns(s, [{"n": 5}])
+    buf, offs = oracle.encode(s, cols, 1, 0)
+    for size in (0, 17):  # "Zero length BigInteger"; more bytes than a decimal128 holds
+        bad = np.zeros(16 + 24, np.uint8)
+        bad[:16] = buf[:16]
+        bad[8:12] = np.frombuffer(np.uint32(size).tobytes(), np.uint8)
+        with pytest.raises(oracle.OracleError):
+            oracle.decode(s, bad, np.array([0, len(bad)], np.int64), 1, 0)
+    # a sign-extended (non-minimal) encoding is still a valid BigInteger: ff ff 7f = -129
+    ok = np.zeros(24, np.uint8)
+    ok[8:16] = np.frombuffer((16 << 32 | 3).to_bytes(8, "little"), np.uint8)
+    ok[16:19] = [0xFF, 0xFF, 0x7F]
+    dec = oracle.decode(s, ok, np.array([0, 24], np.int64), 1, 0)
+    assert decimal_value(dec[0].values[0], 0) == -129
+
+
+def test_biginteger_has_no_precision_check():
+    s = big_schema()
+    cols = build_columns(s, [{"n": 10 ** 38}, {"n": -(2 ** 127)}])  # 39 digits: fine for a BigInteger
+    buf, offs = oracle.encode(s, cols, 2, 0)
+    dec = oracle.decode(s, buf, offs, 2, 0)
+    assert [decimal_value(dec[0].values[i], 0) for i in range(2)] == [10 ** 38, -(2 ** 127)]
