@@ -548,3 +548,105 @@ def test_host_register_refuses_shared_pages_and_foreign_bases():
     assert copy_path(a) == 0 and copy_path(buf[4096 + 99:4096 + 100]) == 0
     host_register(b)  # a's pages are free again
     host_unregister(b)
+
+
+def direct_calls(hp):
+    import ctypes
+    f = _internal("fory_rowfmt_internal_host_direct_calls", ctypes.c_int64, [ctypes.c_void_p])
+    return f(hp.handle)
+
+
+def paged_copy(a):
+    """A copy of array a on whole pages of its own (+ the owning buffer)."""
+    pb, raw = page_buffer(max(a.nbytes, 1))
+    pb[:a.nbytes] = a.view(np.uint8).reshape(-1)
+    return pb, pb[:a.nbytes].view(a.dtype).reshape(a.shape)
+
+
+@pytest.mark.parametrize("frame", [0, 1, 3])
+@pytest.mark.parametrize("n", [1, 64, 5003])
+@pytest.mark.parametrize("name", ["struct104", "struct104_boxed", "all_types"])
+def test_host_fixed_zero_copy(name, n, frame):
+    """Fixed-width plans with every column and the output registered: the kernels read the
+    host columns and write the host rows through their device mappings (one launch, no
+    chunk copies) -- the oracle's bytes; decode the same way back; a hash mismatch is
+    still ClassNotCompatibleException."""
+    schema, make = catalog()[name]
+    cols = make(n, n + 19)
+    expect, _ = oracle.encode(schema, cols, n, frame)
+    plan = NativePlan(schema)
+    hp = HostPipeline(plan, chunk_rows=1024)
+    regs = []
+    try:
+        for c in cols:
+            for attr in ("values", "validity"):
+                a = getattr(c, attr)
+                if a is not None:
+                    whole, view = paged_copy(a)
+                    host_register(whole)
+                    regs.append(whole)
+                    setattr(c, attr, view)
+        out_whole, _ = paged_copy(np.zeros(expect.nbytes, np.uint8))
+        host_register(out_whole)
+        regs.append(out_whole)
+        out = out_whole[:expect.nbytes]
+        hp.encode(cols, n, frame, out)
+        assert direct_calls(hp) == 1 and staged_pieces(hp) == 0
+        bad = np.nonzero(out != expect)[0]
+        assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+        dec = empty_like(schema, n)
+        for c in dec:
+            for attr in ("values", "validity"):
+                a = getattr(c, attr)
+                if a is not None:
+                    whole, view = paged_copy(a)
+                    host_register(whole)
+                    regs.append(whole)
+                    setattr(c, attr, view)
+        hp.decode(out, n, frame, dec)
+        assert direct_calls(hp) == 2
+        assert columns_equal(schema, cols, dec) == []
+        if frame in (1, 3):
+            out[(4 if frame == 1 else 0) + (n // 2) * plan.stride(frame)] ^= 1  # a frame's schema hash
+            with pytest.raises(ClassNotCompatibleException):
+                hp.decode(out, n, frame, dec)
+    finally:
+        unregister_all(regs)
+        hp.close()
+
+
+def test_host_fixed_zero_copy_falls_back_per_call():
+    """A window of a nullable plan that starts inside a validity byte, or a column left
+    pageable, takes the chunk pipeline: same bytes either way."""
+    schema, make = catalog()["struct104_boxed"]
+    n = 3001
+    cols = make(n, 7)
+    expect, _ = oracle.encode(schema, cols, n, 1)
+    plan = NativePlan(schema)
+    stride = plan.stride(1)
+    hp = HostPipeline(plan, chunk_rows=1024)
+    regs = []
+    try:
+        for c in cols:
+            for attr in ("values", "validity"):
+                whole, view = paged_copy(getattr(c, attr))
+                host_register(whole)
+                regs.append(whole)
+                setattr(c, attr, view)
+        w1, _ = paged_copy(np.zeros(1003 * stride, np.uint8))  # window 2 starts at row 1003
+        w2, _ = paged_copy(np.zeros((n - 1003) * stride, np.uint8))
+        for w in (w1, w2):
+            host_register(w)
+            regs.append(w)
+        rows, nbytes = hp.encode_windows(cols, n, 1, [w1[:1003 * stride], w2[:(n - 1003) * stride]])
+        assert list(rows) == [1003, n - 1003] and direct_calls(hp) == 0
+        assert np.array_equal(np.concatenate([w1[:nbytes[0]], w2[:nbytes[1]]]), expect)
+        host_unregister(regs.pop(0))  # one column pageable again
+        out_whole, _ = paged_copy(np.zeros(expect.nbytes, np.uint8))
+        host_register(out_whole)
+        regs.append(out_whole)
+        hp.encode(cols, n, 1, out_whole[:expect.nbytes])
+        assert direct_calls(hp) == 0 and np.array_equal(out_whole[:expect.nbytes], expect)
+    finally:
+        unregister_all(regs)
+        hp.close()
