@@ -60,7 +60,8 @@ int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
 int64_t table_bytes(const Plan& p) {
   // fixed-width: the width-ordered field table
-  if (p.fixed_width) return align_up((int64_t)p.top.size() * (int64_t)sizeof(FixedFieldDev));
+  if (p.fixed_width)  // then the per-slot validity pointers (nullable v5 kernels)
+    return align_up((int64_t)p.top.size() * (int64_t)sizeof(FixedFieldDev)) + align_up((int64_t)p.top.size() * 8);
   if (p.generic)  // columns, then the node table
     return align_up((int64_t)p.nodes.size() * (int64_t)sizeof(ColumnDev)) +
            align_up((int64_t)p.gnodes.size() * (int64_t)sizeof(fory_amd::GNode));
@@ -289,10 +290,32 @@ int upload(void* ws, const void* host, int64_t bytes, hipStream_t s) {
   return FORY_OK;
 }
 
+// The field table, then per slot (schema ordinal) the column's validity pointer (input on
+// encode, output on decode; null for not-null fields and absent validity), one upload.
+// *valid8: every such pointer is 8-byte aligned (the nullable v5 kernels' word accesses).
+int upload_fixed_tables(const Plan& p, void* ws, const std::vector<FixedFieldDev>& tab, bool decode, hipStream_t s,
+                        int32_t* valid8) {
+  const int64_t nf = (int64_t)tab.size();
+  const int64_t t0 = align_up(nf * (int64_t)sizeof(FixedFieldDev));
+  std::vector<uint8_t> buf((size_t)(t0 + nf * 8), 0);
+  std::memcpy(buf.data(), tab.data(), (size_t)nf * sizeof(FixedFieldDev));
+  *valid8 = 1;
+  for (const FixedFieldDev& f : tab) {
+    const uint8_t* v = decode ? f.out_validity : f.validity;
+    if (!(f.flags & 1)) v = nullptr;
+    if (v && (reinterpret_cast<uintptr_t>(v) & 7)) *valid8 = 0;
+    std::memcpy(buf.data() + t0 + 8 * f.slot, &v, 8);
+  }
+  (void)p;
+  return upload(ws, buf.data(), (int64_t)buf.size(), s);
+}
+
 fory_amd::FixedLaunch fixed_launch(const Plan& p, const void* table, int64_t n, int frame) {
   fory_amd::FixedLaunch L{};
   L.fields = static_cast<const FixedFieldDev*>(table);
   L.num_fields = (int32_t)p.top.size();
+  L.slot_validity = reinterpret_cast<const uint8_t* const*>(
+      static_cast<const uint8_t*>(table) + align_up((int64_t)p.top.size() * (int64_t)sizeof(FixedFieldDev)));
   L.bitmap_bytes = p.bitmap_bytes;
   L.fixed_size = p.fixed_size;
   L.stride = p.fixed_size + fory_amd::frame_header_bytes(frame);
@@ -1125,7 +1148,7 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
     rc = bind_fixed(p, cols, num_rows, false, &tab);
     if (rc) return rc;
     fory_amd::FixedLaunch L = fixed_launch(p, d_workspace, num_rows, frame_mode);
-    rc = upload(d_workspace, tab.data(), (int64_t)(tab.size() * sizeof(FixedFieldDev)), s);
+    rc = upload_fixed_tables(p, d_workspace, tab, false, s, &L.valid8);
     if (rc) return rc;
     e = fory_amd::launch_encode_fixed(L, static_cast<uint8_t*>(d_out), s);
     return e == hipSuccess ? FORY_OK : hip_fail(e, "encode_fixed");
@@ -1322,9 +1345,9 @@ int fory_rowfmt_decode(const fory_plan* plan, const void* d_rows, const int64_t*
     std::vector<FixedFieldDev> tab;
     rc = bind_fixed(p, out_cols, num_rows, true, &tab);
     if (rc) return rc;
-    rc = upload(d_workspace, tab.data(), (int64_t)(tab.size() * sizeof(FixedFieldDev)), s);
-    if (rc) return rc;
     fory_amd::FixedLaunch L = fixed_launch(p, d_workspace, num_rows, frame_mode);
+    rc = upload_fixed_tables(p, d_workspace, tab, true, s, &L.valid8);
+    if (rc) return rc;
     L.cols_aligned16 = 1;
     for (const FixedFieldDev& f : tab)
       if (reinterpret_cast<uintptr_t>(f.out_values) & 15) L.cols_aligned16 = 0;

@@ -70,6 +70,21 @@ __device__ __forceinline__ void put_slot(uint8_t* row, int hdr_bm, int slot, uin
   }
 }
 
+// The same without the bitmap: the nullable v5 kernels write whole bitmap words
+// (v5_bitmaps); a null record's slot is 0.
+template <int HDR>
+__device__ __forceinline__ void put_slot_nb(uint8_t* row, int hdr_bm, int slot, uint64_t x, bool isnull, int flags) {
+  if (flags & 2) x = x ? 1 : 0;  // MemoryBuffer.putBoolean
+  if (isnull) x = 0;
+  uint8_t* p = row + hdr_bm + 8 * slot;
+  if (HDR == 12) {
+    st32(p, (uint32_t)x);
+    st32(p + 4, (uint32_t)(x >> 32));
+  } else {
+    *reinterpret_cast<uint64_t*>(p) = x;
+  }
+}
+
 // Frame header [i32 8+rowSize][i64 hash] + zeroed null bitmap of this lane's row.
 template <int HDR>
 __device__ __forceinline__ void put_header(uint8_t* row, const FixedLaunch& L) {
@@ -218,51 +233,39 @@ __device__ __forceinline__ void v5_issue(const uint8_t* const (&ptr)[K], const i
   }
 }
 
-// Nullable schemas (NUL): the E validity bits of a lane's chunk (records r0 + rb ..
-// + E - 1; one byte, two for E = 16) are loaded with the chunk. Fields without
-// validity re-read a dummy address, so every lane still issues 2K loads per tile.
-template <int K>
-__device__ __forceinline__ void v5_issue_bits(const uint8_t* const (&vptr)[K], const int (&wk)[K], int64_t r0,
-                                              uint32_t (&b)[K]) {
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const uint8_t* p = vptr[k] + (r0 >> 3);
-    b[k] = wk[k] == 1 ? (uint32_t)load_byte(p) | ((uint32_t)load_byte(p + 1) << 8) : (uint32_t)load_byte(p);
-  }
-}
-
 // sf[k]: slot | flags << 16 | nullable-with-validity << 19 | live << 20 | rb << 21.
-// A null record (BinaryWriter.setNullAt) gets its bit OR-ed into the row bitmap
-// and a zero slot.
+// Nullable schemas (NUL): the tile's null masks per slot are in LDS (mt[slot], bit r:
+// record r of the tile is null, from the Arrow validity words v5_masks loaded); a null
+// record's slot is written 0, its bit set by v5_bitmaps.
 template <int R, int K, int HDR, bool NUL = false>
 __device__ __forceinline__ void v5_write(uint8_t* lds, int stride, int hdr_bm, const int (&wk)[K],
-                                         const uint32_t (&sf)[K], const u32x4 (&d)[K], const uint32_t (&vb)[K]) {
+                                         const uint32_t (&sf)[K], const u32x4 (&d)[K], const uint64_t* mt) {
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int w = wk[k];
     if (!(sf[k] & (1u << 20))) continue;
     const int slot = sf[k] & 0xffff, flags = (sf[k] >> 16) & 0x7, rb = sf[k] >> 21;
-    const uint32_t ok = NUL && (sf[k] & (1u << 19)) ? vb[k] >> (rb & 7) : 0xffffffffu;  // bit e: record rb+e valid
-    auto nul = [&](int e) { return NUL && !((ok >> e) & 1); };
+    uint32_t nm = 0;  // bit e: record rb + e is null
+    if constexpr (NUL) nm = (uint32_t)(mt[slot] >> rb);
+    auto nul = [&](int e) { return NUL && ((nm >> e) & 1); };
     uint8_t* row = lds + rb * stride;
     const u32x4 x = d[k];
     if (w == 8) {
-      put_slot<HDR>(row, hdr_bm, slot, (uint64_t)x.x | ((uint64_t)x.y << 32), nul(0), flags);
-      put_slot<HDR>(row + stride, hdr_bm, slot, (uint64_t)x.z | ((uint64_t)x.w << 32), nul(1), flags);
+      put_slot_nb<HDR>(row, hdr_bm, slot, (uint64_t)x.x | ((uint64_t)x.y << 32), nul(0), flags);
+      put_slot_nb<HDR>(row + stride, hdr_bm, slot, (uint64_t)x.z | ((uint64_t)x.w << 32), nul(1), flags);
     } else if (w == 4) {
-      put_slot<HDR>(row, hdr_bm, slot, x.x, nul(0), flags);
-      put_slot<HDR>(row + stride, hdr_bm, slot, x.y, nul(1), flags);
-      put_slot<HDR>(row + 2 * stride, hdr_bm, slot, x.z, nul(2), flags);
-      put_slot<HDR>(row + 3 * stride, hdr_bm, slot, x.w, nul(3), flags);
-    } else if constexpr (NUL) {  // 2- and 1-byte fields, rolled: unrolled with the null
-      // bits, the NUL form spilled (the dword of record e picked by selects)
+      put_slot_nb<HDR>(row, hdr_bm, slot, x.x, nul(0), flags);
+      put_slot_nb<HDR>(row + stride, hdr_bm, slot, x.y, nul(1), flags);
+      put_slot_nb<HDR>(row + 2 * stride, hdr_bm, slot, x.z, nul(2), flags);
+      put_slot_nb<HDR>(row + 3 * stride, hdr_bm, slot, x.w, nul(3), flags);
+    } else if constexpr (NUL) {  // 2- and 1-byte fields, rolled (the dword of record e picked by selects)
       const int E = 16 / w;
 #pragma unroll 1
       for (int e = 0; e < E; ++e) {
         const int q = e / (E / 4);
         const uint32_t wd = q == 0 ? x.x : q == 1 ? x.y : q == 2 ? x.z : x.w;
         const uint32_t v = (wd >> (8 * w * (e % (E / 4)))) & (w == 2 ? 0xffffu : 0xffu);
-        put_slot<HDR>(row + e * stride, hdr_bm, slot, v, nul(e), flags);
+        put_slot_nb<HDR>(row + e * stride, hdr_bm, slot, v, nul(e), flags);
       }
     } else if (w == 2) {
 #pragma unroll
@@ -276,35 +279,30 @@ __device__ __forceinline__ void v5_write(uint8_t* lds, int stride, int hdr_bm, c
   }
 }
 
-// Nullable schemas: the thread that stores 16-B chunk [lo, lo + 16) of the tile
-// image zeroes the null-bitmap dwords inside it once read (BinaryRowWriter.reset
-// for the next tile; same-thread order, so no extra barrier).
+// Nullable schemas: row r's null bitmap, word j (slots 32j .. 32j + 31), from the tile's
+// masks in LDS (BinaryWriter.setNullAt: bit = 1 for null); wave j builds word j of the
+// 64 rows (lane = row). Masks past the last field are 0, so are the padding bits.
 template <int HDR>
-__device__ __forceinline__ void v5_zero_bitmaps(uint8_t* lds, int lo, int hi, int stride, int bm) {
-  int rr = lo / stride;
-#pragma unroll
-  for (int q = 0; q < 2; ++q, ++rr) {
-    const int b0 = rr * stride + HDR, b1 = b0 + bm;
-    for (int o = lo > b0 ? lo : b0; o < (hi < b1 ? hi : b1); o += 4) st32(lds + o, 0u);
-  }
+__device__ __forceinline__ void v5_bitmaps(uint8_t* lds, int stride, int nbw, const uint64_t* mt, int wave, int lane) {
+  if (wave >= nbw) return;
+  const uint64_t* m = mt + 32 * wave;
+  uint32_t acc = 0;
+#pragma unroll 8
+  for (int b = 0; b < 32; ++b) acc |= (uint32_t)((m[b] >> lane) & 1) << b;
+  st32(lds + lane * stride + HDR + 4 * wave, acc);
 }
 
 // The tile's rows (R * stride contiguous bytes) leave with non-temporal 16-B
 // stores: the once-written row stream does not displace L2 lines
 // (18.43 -> 18.03 ms at 64M Struct104 rows).
-template <int R, int WG, int HDR = 0, bool NUL = false>
+template <int R, int WG>
 __device__ __forceinline__ void v5_store(const FixedLaunch& L, uint8_t* lds, uint8_t* dst, int tid) {
   const int bytes = R * L.stride;
   const int n16 = bytes >> 4;
-  for (int c = tid; c < n16; c += WG) {
+  for (int c = tid; c < n16; c += WG)
     __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(lds + c * 16), gp(reinterpret_cast<u32x4*>(dst + c * 16)));
-    if constexpr (NUL) v5_zero_bitmaps<HDR>(lds, c * 16, c * 16 + 16, L.stride, L.bitmap_bytes);
-  }
   const int tail4 = (bytes & 15) >> 2;
-  if (tid < tail4) {
-    st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
-    if constexpr (NUL) v5_zero_bitmaps<HDR>(lds, n16 * 16 + tid * 4, n16 * 16 + tid * 4 + 4, L.stride, L.bitmap_bytes);
-  }
+  if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
 }
 
 // XCD-grouped tile order: workgroups are dispatched round-robin over the 8 XCDs
@@ -342,7 +340,6 @@ __device__ __forceinline__ void encode_v5_body(const FixedLaunch& L, const Fixed
 
   const uint8_t* dummy = fields[L.group[0]].values;  // any valid column (never null: num_rows > 0)
   const uint8_t* ptr[K];
-  const uint8_t* vptr[K];
   int wk[K];
   uint32_t sf[K];
 #pragma unroll
@@ -353,23 +350,36 @@ __device__ __forceinline__ void encode_v5_body(const FixedLaunch& L, const Fixed
     const int cpf = R * (ok ? w : 8) / 16;
     const int p = p0 + lane / cpf, c = lane % cpf;
     ptr[k] = dummy;
-    vptr[k] = dummy;
     sf[k] = 0;
     if (ok && p < pend) {
       const FixedFieldDev& fd = fields[p];
       const int rb = c * (16 / w);
       ptr[k] = fd.values + c * 16;
-      const bool nv = (fd.flags & 1) && fd.validity;
-      if (nv) vptr[k] = fd.validity + (rb >> 3);
-      sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (nv ? 1u << 19 : 0u) | (1u << 20) | ((uint32_t)rb << 21);
+      sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (1u << 20) | ((uint32_t)rb << 21);
     }
   }
-  // frame header + zeroed bitmaps; the header is constant across tiles, the bitmaps
-  // of nullable schemas are re-zeroed chunk by chunk as the rows leave (v5_store)
+  // Nullable schemas: lane l of wave w loads the tile's Arrow validity word (64 records,
+  // 8 bytes) of slot 64 w + l with the tile's column chunks (one more load per lane and
+  // tile; lanes without a nullable slot re-read the table). A stage ahead of its tile the
+  // words go into an LDS mask table (two, by stage parity): the chunk writes zero null
+  // slots from it and v5_bitmaps builds whole bitmap words -- no atomics, no per-chunk
+  // validity loads, no bitmap re-zeroing (round 4's NUL form: ~90 VGPRs, one workgroup
+  // per CU).
+  const int nmask = (L.num_fields + 63) & ~63;
+  uint64_t* mtab = reinterpret_cast<uint64_t*>(lds + R * stride);  // [2][nmask]
+  const uint8_t* vw = reinterpret_cast<const uint8_t*>(L.slot_validity);
+  bool vw_on = false;
+  if constexpr (NUL) {
+    const int sl = 64 * wave + lane;
+    const uint8_t* v = sl < L.num_fields ? L.slot_validity[sl] : nullptr;
+    vw_on = v != nullptr;
+    if (vw_on) vw = v;
+  }
+  // frame header + zeroed bitmaps; the header is constant across tiles (nullable
+  // schemas: v5_bitmaps rewrites whole bitmap words per tile)
   if (tid < R) put_header<HDR>(lds + tid * stride, L);
-  if constexpr (NUL) __syncthreads();  // null bits are OR-ed into the zeroed bitmaps
   u32x4 dA[K], dB[K];
-  uint32_t bA[K], bB[K];
+  uint64_t mA = 0, mB = 0;
   const int64_t last = tiles - 1;
   // logical tile t -> tile map_tile(t): xcd_run = grid / 8 (each step's grid tiles,
   // one contiguous run per XCD) or 0
@@ -385,34 +395,43 @@ __device__ __forceinline__ void encode_v5_body(const FixedLaunch& L, const Fixed
     if (mine <= 0) return;
     tend = (int64_t)blockIdx.x + mine * gridDim.x;
   }
-  auto issue = [&](int64_t tile, u32x4 (&d)[K], uint32_t (&b)[K]) {
+  auto issue = [&](int64_t tile, u32x4 (&d)[K], uint64_t& m) {
+    if constexpr (NUL) m = *gp(reinterpret_cast<const uint64_t*>(vw_on ? vw + tile * 8 : vw));  // masks first
     v5_issue<R, K, OPT>(ptr, wk, tile * R, d);
-    if constexpr (NUL) v5_issue_bits<K>(vptr, wk, tile * R, b);
   };
-  issue(mt(t), dA, bA);
-  issue(mt(min(t + (int64_t)gridDim.x, tend - 1)), dB, bB);
+  auto put_masks = [&](uint64_t m, int b) {  // (Arrow: 1 = valid; rows: 1 = null)
+    if constexpr (NUL)
+      if (64 * wave < nmask) mtab[b * nmask + 64 * wave + lane] = vw_on ? ~m : 0ull;
+  };
+  issue(mt(t), dA, mA);
+  issue(mt(min(t + (int64_t)gridDim.x, tend - 1)), dB, mB);
+  put_masks(mA, 0);
+  if constexpr (NUL) __syncthreads();
+  const int nbw = L.bitmap_bytes >> 2;
+  // stage of set X (tile t, masks in table bx); the other set's masks go into table by
+  auto stage = [&](u32x4 (&d)[K], uint64_t& m, int bx, uint64_t mo, int by) {
+    v5_write<R, K, HDR, NUL>(lds, stride, hdr_bm, wk, sf, d, mtab + bx * nmask);
+    if constexpr (NUL) v5_bitmaps<HDR>(lds, stride, nbw, mtab + bx * nmask, wave, lane);
+    __syncthreads();
+    put_masks(mo, by);  // (loaded a stage ago; only the other set's chunks are younger)
+    v5_store<R, WG>(L, lds, out + mt(t) * R * stride, tid);
+    issue(mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)), d, m);
+    __syncthreads();
+    t += gridDim.x;
+  };
   for (;;) {
-    v5_write<R, K, HDR, NUL>(lds, stride, hdr_bm, wk, sf, dA, bA);
-    __syncthreads();
-    v5_store<R, WG, HDR, NUL>(L, lds, out + mt(t) * R * stride, tid);
-    issue(mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)), dA, bA);
-    __syncthreads();
-    t += gridDim.x;
+    stage(dA, mA, 0, mB, 1);
     if (t >= tend) break;
-    v5_write<R, K, HDR, NUL>(lds, stride, hdr_bm, wk, sf, dB, bB);
-    __syncthreads();
-    v5_store<R, WG, HDR, NUL>(L, lds, out + mt(t) * R * stride, tid);
-    issue(mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)), dB, bB);
-    __syncthreads();
-    t += gridDim.x;
+    stage(dB, mB, 1, mA, 0);
     if (t >= tend) break;
   }
 }
 
-// NUL (nullable schemas) takes ~90 VGPRs: one 1024-thread workgroup per CU instead
-// of two (forcing 64 spills 27); measured 5.56 vs 4.69 ms for not-null at 16Mi rows.
+// Round 4's NUL form (per-chunk validity loads, atomics into the bitmaps) took ~90
+// VGPRs: one 1024-thread workgroup per CU instead of two; 5.56 vs 4.69 ms for not-null
+// at 16Mi rows. The mask-table form above keeps close to the not-null registers.
 template <int R, int WG, int K, int HDR, int OPT = 0, bool NUL = false>
-__global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
+__global__ __launch_bounds__(WG, NUL ? 2 * WG / 256 : 1) void encode_fixed_v5_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
                                                                  uint8_t* __restrict__ out, int64_t tiles,
                                                                  int64_t xcd_run) {
   encode_v5_body<R, WG, K, HDR, OPT, NUL>(L, fields, out, tiles, xcd_run);
@@ -583,37 +602,27 @@ __device__ __forceinline__ void d5_write(uint8_t* lds, int tid, int n16, int WGT
   }
 }
 
-// Lane k-th column chunk: E records from rb of field slot `sf` (slot | flags << 16 |
-// valid << 20 | rb << 21) gathered from the LDS rows, stored to optr (column + rb * w).
-// Nullable schemas (NUL): the lane's E validity bits (1 = valid, Arrow) are OR-ed
-// across the 32/E lanes that share a 32-bit word of the field's validity (xor
-// shuffles: those lanes are adjacent and the groups aligned), and the group's first
-// lane stores the word's 4 bytes (tiles are 64 records: no byte is shared between
-// tiles).
-template <int R, int K2, int HDR, bool NUL>
-__device__ __forceinline__ void d5_validity(const uint8_t* lds, int stride, const int (&wk)[K2],
-                                            const uint32_t (&sf)[K2], uint8_t* const (&vout)[K2], int64_t r0,
-                                            int lane) {
-#pragma unroll
-  for (int k = 0; k < K2; ++k) {
-    const int w = wk[k];  // wave-uniform
-    const int E = 16 / w;
-    const int rb = sf[k] >> 21;
-    uint32_t m = 0;
-    if (vout[k]) {
-      const int slot = sf[k] & 0xffff;
-      const uint8_t* b = lds + rb * stride + HDR + ((slot >> 5) << 2);
-      const uint32_t bit = 1u << (slot & 31);
-      for (int e = 0; e < E; ++e) m |= (ld32(b + e * stride) & bit) ? 0u : 1u << e;  // BinaryRow.isNullAt
-    }
-    uint32_t word = m << (rb & 31);
-    for (int sh = 1; sh < 32 / E; sh <<= 1) word |= __shfl_xor(word, sh);
-    if (vout[k] && (rb & 31) == 0) {
-      uint8_t* v = vout[k] + ((r0 + rb) >> 3);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) store_byte(v + q, (uint8_t)(word >> (8 * q)));
-    }
+// Nullable schemas (NUL): the Arrow validity of the tile's 64 records, per slot, from the
+// rows' null bitmaps in LDS. Wave w takes slots [64 w, 64 w + 64): lane r reads the two
+// bitmap words of row r that hold them, a ballot per slot gives the slot's 64 null bits
+// across the tile (BinaryRow.isNullAt), and lane s keeps slot 64 w + s's word and stores
+// it, inverted (Arrow: 1 = valid), as 8 bytes at the tile's byte offset of the field's
+// validity (vo: the output validity of slot 64 w + lane, or null). One LDS read and 64
+// ballots per wave and tile instead of a bitmap read per record and chunk.
+template <int HDR>
+__device__ __forceinline__ void d5_validity(const uint8_t* lds, int stride, int nbits, uint8_t* vo, int64_t tile,
+                                            int wave, int lane) {
+  if (64 * wave >= nbits) return;
+  const uint8_t* bm = lds + lane * stride + HDR + 8 * wave;
+  const uint32_t lo = ld32(bm), hi = 64 * wave + 32 < nbits ? ld32(bm + 4) : 0u;
+  uint64_t mine = 0;
+#pragma unroll 8
+  for (int b = 0; b < 64; ++b) {
+    const uint32_t wd = b < 32 ? lo : hi;
+    const uint64_t nb = __ballot((wd >> (b & 31)) & 1);
+    mine = lane == b ? nb : mine;
   }
+  if (vo) *gp(reinterpret_cast<uint64_t*>(vo + tile * 8)) = ~mine;
 }
 
 template <int R, int K2, int HDR>
@@ -684,7 +693,6 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
   int wk[K2];
   uint32_t sf[K2];
   uint8_t* optr[K2];
-  uint8_t* vout[K2];
 #pragma unroll
   for (int k = 0; k < K2; ++k) {
     int w = 0, p0 = 0, pend = 0;
@@ -694,15 +702,20 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
     const int p = p0 + lane / cpf, c = lane % cpf;
     sf[k] = 0;
     optr[k] = nullptr;
-    vout[k] = nullptr;
     if (ok && p < pend) {
       const FixedFieldDev& fd = fields[p];
       const int rb = c * (16 / w);
       sf[k] = (uint32_t)fd.slot | ((uint32_t)fd.flags << 16) | (1u << 20) | ((uint32_t)rb << 21);
       optr[k] = fd.out_values + (int64_t)rb * w;
-      if ((fd.flags & 1) && fd.out_validity) vout[k] = fd.out_validity;
     }
   }
+  // NUL: the output validity of slot 64 * wave + lane (d5_validity)
+  uint8_t* vo = nullptr;
+  if constexpr (NUL) {
+    const int sl = 64 * wave + lane;
+    if (sl < L.num_fields) vo = const_cast<uint8_t*>(L.slot_validity[sl]);
+  }
+  const int nbits = L.bitmap_bytes * 8;
   u32x4 dA[K], dB[K];
   const int64_t last = tiles - 1;
   // OPT & 2: blocked order -- workgroup b walks tiles [b*per, (b+1)*per) in order
@@ -724,7 +737,7 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
     __syncthreads();
     if (HDR && tid < R) check_frame<HDR>(lds + tid * stride, L, status);
     d5_columns<R, K2, HDR>(lds, stride, hdr_bm, wk, sf, optr, mt(t) * R);
-    if constexpr (NUL) d5_validity<R, K2, HDR, NUL>(lds, stride, wk, sf, vout, mt(t) * R, lane);
+    if constexpr (NUL) d5_validity<HDR>(lds, stride, nbits, vo, mt(t), wave, lane);
     d5_issue<R, K>(in, mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, d);
     __syncthreads();
     t += gridDim.x;
@@ -755,7 +768,7 @@ hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   if (full > 0) {
     auto* k = &encode_fixed_v5_kernel<kV5R, kV5WG, kV5K, HDR, 1, NUL>;
     raise_lds_cap(k);
-    const size_t lds = (size_t)kV5R * L.stride;
+    const size_t lds = (size_t)kV5R * L.stride + (NUL ? (size_t)2 * 8 * ((L.num_fields + 63) & ~63) : 0);
     const int64_t grid = persistent_grid(k, lds, full, kV5WG);
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kV5WG), lds, s, L, L.fields, out, full, (int64_t)(full / 8));
   }
@@ -776,7 +789,10 @@ hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   const size_t lds = (size_t)TR * L.stride;
   if constexpr (TR == 64) {
     // v5: schemas whose chunk instructions fit K per wave (nullable ones: the NUL form)
-    if ((v3_insn_count<kV5R>(L.group) + kV5WG / 64 - 1) / (kV5WG / 64) <= kV5K)
+    // nullable: the mask-table form needs 8-byte aligned validity words and a mask wave
+    // per 64 slots, a bitmap word per wave
+    if ((v3_insn_count<kV5R>(L.group) + kV5WG / 64 - 1) / (kV5WG / 64) <= kV5K &&
+        (!L.any_nullable || (L.valid8 && L.num_fields <= 64 * (kV5WG / 64) && L.bitmap_bytes / 4 <= kV5WG / 64)))
       return L.any_nullable ? launch_encode_v5<HDR, true>(L, out, s) : launch_encode_v5<HDR, false>(L, out, s);
   }
   auto* k = &encode_fixed_kernel<TR, HDR>;
@@ -794,11 +810,13 @@ constexpr int kD5R = 64, kD5WG = 1024, kD5K = 4, kD5K2 = 3;
 template <int HDR>
 bool decode_v5_fits(const FixedLaunch& L) {
   return L.cols_aligned16 && kD5R * L.stride <= kD5K * kD5WG * 16 &&
-         (kD5R * L.stride) % 16 == 0 && v3_insn_count<kD5R>(L.group) <= kD5K2 * (kD5WG / 64);
+         (kD5R * L.stride) % 16 == 0 && v3_insn_count<kD5R>(L.group) <= kD5K2 * (kD5WG / 64) &&
+         (!L.any_nullable || (L.valid8 && L.bitmap_bytes * 8 <= 64 * (kD5WG / 64)));
 }
 
 template <int HDR>
 hipError_t launch_decode_v5(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
+  // (decode_v5_fits: nullable schemas need 8-byte aligned validity outputs and <= 64 slots per wave)
   const int64_t full = L.num_rows / kD5R;
   if (full > 0) {
     auto* k = L.any_nullable ? &decode_fixed_v5_kernel<kD5R, kD5WG, kD5K, kD5K2, HDR, 0, true>

@@ -667,13 +667,16 @@ int host_encode_direct(fory_host_ctx* c, const fory_column* h, int64_t n, int32_
   int rc = hip_check(hipMemsetAsync(c->buf[0].status, 0, 4, c->s_k), "hipMemsetAsync");
   std::vector<fory_column> dcols((size_t)N);
   for (size_t w = 0; w < nw && !rc; ++w) {
-    const int64_t f0 = W.first[w], rows = W.first[w + 1] - f0;
-    if (rows <= 0) continue;
-    for (int i = 0; i < N; ++i)
-      dcols[(size_t)i] = fory_column{val[(size_t)i] + f0 * c->width[i], nullptr,
-                                     vld[(size_t)i] ? vld[(size_t)i] + f0 / 8 : nullptr, rows, rows * c->width[i]};
-    rc = fory_rowfmt_encode(c->plan, dcols.data(), rows, frame, nullptr, dst[w], rows * stride, c->buf[0].status,
-                            c->buf[0].ws, c->ws_bytes, c->s_k);
+    const int64_t f0 = W.first[w], f1 = W.first[w + 1];
+    // launches of <= chunk rows (the context's workspace; chunk is a multiple of 64)
+    for (int64_t a = f0; a < f1 && !rc; a += c->chunk) {
+      const int64_t rows = std::min(c->chunk, f1 - a);
+      for (int i = 0; i < N; ++i)
+        dcols[(size_t)i] = fory_column{val[(size_t)i] + a * c->width[i], nullptr,
+                                       vld[(size_t)i] ? vld[(size_t)i] + a / 8 : nullptr, rows, rows * c->width[i]};
+      rc = fory_rowfmt_encode(c->plan, dcols.data(), rows, frame, nullptr, dst[w] + (a - f0) * stride, rows * stride,
+                              c->buf[0].status, c->buf[0].ws, c->ws_bytes, c->s_k);
+    }
   }
   const int rs = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize(kernels)");
   if (rc) return rc;
@@ -689,21 +692,25 @@ int host_decode_direct(fory_host_ctx* c, const uint8_t* rows_h, int64_t n, int32
   const int N = c->info.num_columns;
   uint8_t* rows = mapped_range(rows_h, (size_t)(n * stride));
   if (!rows || (reinterpret_cast<uintptr_t>(rows) & 15)) return -1;
-  std::vector<fory_column> dcols((size_t)N);
+  std::vector<uint8_t*> val((size_t)N), vld((size_t)N, nullptr);
   for (int i = 0; i < N; ++i) {
-    uint8_t* v = mapped_range(h[i].values, (size_t)(n * c->width[i]));
-    if (!v) return -1;
-    uint8_t* vb = nullptr;
+    val[(size_t)i] = mapped_range(h[i].values, (size_t)(n * c->width[i]));
+    if (!val[(size_t)i]) return -1;
     if (c->nullable[i] && h[i].validity) {
-      vb = mapped_range(h[i].validity, (size_t)((n + 7) / 8));
-      if (!vb) return -1;
+      vld[(size_t)i] = mapped_range(h[i].validity, (size_t)((n + 7) / 8));
+      if (!vld[(size_t)i]) return -1;
     }
-    dcols[(size_t)i] = fory_column{v, nullptr, vb, n, n * c->width[i]};
   }
   int rc = hip_check(hipMemsetAsync(c->buf[0].status, 0, 4, c->s_k), "hipMemsetAsync");
-  if (!rc)
-    rc = fory_rowfmt_decode(c->plan, rows, nullptr, n, frame, dcols.data(), c->buf[0].status, c->buf[0].ws, c->ws_bytes,
-                            c->s_k);
+  std::vector<fory_column> dcols((size_t)N);
+  for (int64_t a = 0; a < n && !rc; a += c->chunk) {  // launches of <= chunk rows
+    const int64_t m = std::min(c->chunk, n - a);
+    for (int i = 0; i < N; ++i)
+      dcols[(size_t)i] = fory_column{val[(size_t)i] + a * c->width[i], nullptr,
+                                     vld[(size_t)i] ? vld[(size_t)i] + a / 8 : nullptr, m, m * c->width[i]};
+    rc = fory_rowfmt_decode(c->plan, rows + a * stride, nullptr, m, frame, dcols.data(), c->buf[0].status,
+                            c->buf[0].ws, c->ws_bytes, c->s_k);
+  }
   const int rs = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize(kernels)");
   if (rc) return rc;
   if (rs) return rs;

@@ -31,7 +31,9 @@ struct FixedLaunch {
   int64_t tile0;                // first tile of this launch (tail launches after a persistent kernel)
   int64_t xcd_run;              // XCD-grouped tile order: tiles per XCD run (0 = dispatch order)
   int32_t cols_aligned16;       // decode: every output column 16-byte aligned (decode v5's chunk stores)
-  int32_t pad;
+  int32_t valid8;               // every validity pointer of slot_validity 8-byte aligned
+  const uint8_t* const* slot_validity;  // per slot (schema ordinal): the field's validity (encode:
+                                        // input, decode: output), null when not nullable / absent
 };
 
 hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s);
