@@ -387,6 +387,10 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
       sd.nfields = op.c;
       sd.hdr = (int32_t)(((op.c + 63) / 64) * 8);
       sd.flags = op.d;
+      // word of its bitmap in encode v9n's partial-word table: after the row's and the
+      // structs' before it (pre-order)
+      sd.woff = (int32_t)(p.bitmap_bytes / 4);
+      for (const fory_amd::StructDev& e : st) sd.woff += e.hdr / 4;
       st.push_back(sd);
       stack.push_back((int32_t)st.size());
     } else if (op.code == fory_amd::OP_STRUCT_END) {
@@ -485,11 +489,14 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
   for (const fory_amd::VarFieldDev& v : var) L->nullable |= v.validity ? 2 : 0;
   L->num_list = 0;
   L->list_mask = 0;
+  L->bool_items = 0;
   for (size_t v = 0; v < var.size(); ++v)
     if (var[v].is_list) {
       ++L->num_list;
       if (v < 32) L->list_mask |= 1u << v;
+      if (var[v].iflags & 2) L->bool_items = 1;
     }
+  for (size_t k = 0; k < st.size() && k < (size_t)fory_amd::kMaxTileStructs; ++k) L->st_hdr[k] = st[k].hdr;
   L->cols = static_cast<const ColumnDev*>(ws);
   L->prog = reinterpret_cast<const fory_amd::Op*>(static_cast<uint8_t*>(ws) + col_bytes);
   L->num_ops = (int32_t)p.program.size();

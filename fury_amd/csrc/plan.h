@@ -97,7 +97,7 @@ struct StructDev {
   int32_t hdr;                   // child null-bitmap bytes
   int32_t nfields;               // child field count
   int32_t flags;                 // bit0 nullable
-  int32_t pad;
+  int32_t woff;                  // encode v9n: first word of its bitmap in the partial-word table
 };
 constexpr int kMaxTileStructs = 16;  // struct fields a tile-engine plan may hold
 
