@@ -429,9 +429,11 @@ __device__ __forceinline__ void encode_v5_body(const FixedLaunch& L, const Fixed
 
 // Round 4's NUL form (per-chunk validity loads, atomics into the bitmaps) took ~90
 // VGPRs: one 1024-thread workgroup per CU instead of two; 5.56 vs 4.69 ms for not-null
-// at 16Mi rows. The mask-table form above keeps close to the not-null registers.
+// at 16Mi rows. The mask-table form above takes 76-78: still one workgroup per CU (held
+// to 64 for two it spilled 14-18 and measured 5.42 vs 5.19 ms at 16Mi boxed rows,
+// profiles/r05/nullable/); encode 5.56 -> 5.19 ms raw, 5.37 -> 4.84 ms frames.
 template <int R, int WG, int K, int HDR, int OPT = 0, bool NUL = false>
-__global__ __launch_bounds__(WG, NUL ? 2 * WG / 256 : 1) void encode_fixed_v5_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
+__global__ __launch_bounds__(WG, 1) void encode_fixed_v5_kernel(FixedLaunch L, const FixedFieldDev* __restrict__ fields,
                                                                  uint8_t* __restrict__ out, int64_t tiles,
                                                                  int64_t xcd_run) {
   encode_v5_body<R, WG, K, HDR, OPT, NUL>(L, fields, out, tiles, xcd_run);

@@ -11,8 +11,6 @@
 // capi.cpp (plan_info / workspace_bytes / encode / decode / read_status).
 #include <hip/hip_runtime.h>
 
-#include <unistd.h>
-
 #include <algorithm>
 #include <cstdint>
 #include <map>
@@ -235,14 +233,6 @@ int fail_host(int code, const std::string& msg) { return fory_rowfmt_internal_se
 std::mutex g_reg_mu;
 std::map<uintptr_t, size_t> g_regs;
 
-uintptr_t page_size() {
-  static const uintptr_t p = [] {
-    const long v = sysconf(_SC_PAGESIZE);
-    return (uintptr_t)(v > 0 ? v : 4096);
-  }();
-  return p;
-}
-uintptr_t page_down(uintptr_t a) { return a & ~(page_size() - 1); }
 std::string hex(uintptr_t a) {
   char b[32];
   std::snprintf(b, sizeof b, "0x%llx", (unsigned long long)a);
@@ -540,19 +530,15 @@ void fory_rowfmt_host_ctx_destroy(fory_host_ctx* c) {
 
 int fory_rowfmt_host_register(void* host_ptr, int64_t bytes) {
   if (!host_ptr || bytes <= 0) return fail_host(FORY_ERR_INVALID_ARGUMENT, "null pointer or empty range");
-  const uintptr_t b = reinterpret_cast<uintptr_t>(host_ptr);
-  const uintptr_t p0 = page_down(b), p1 = page_down(b + (uintptr_t)bytes - 1) + page_size();
+  const uintptr_t b = reinterpret_cast<uintptr_t>(host_ptr), e = b + (uintptr_t)bytes;
   std::lock_guard<std::mutex> lock(g_reg_mu);
-  // a registration pins whole pages: two of them on one page would leave that page's
-  // pinning to whichever is unregistered last, and a copy judged by one of them could
-  // reach the other's bytes -- refused (the caller registers page-exclusive buffers)
-  for (const auto& r : g_regs) {
-    const uintptr_t q0 = page_down(r.first), q1 = page_down(r.first + r.second - 1) + page_size();
-    if (p0 < q1 && q0 < p1)
-      return fail_host(FORY_ERR_INVALID_ARGUMENT,
-                       "range shares a page with a registered range at " + hex(r.first) + " (" +
-                           std::to_string(r.second) + " bytes): register page-exclusive buffers");
-  }
+  // the same bytes twice: refused (one of the two unregisters would leave the runtime
+  // mapping bytes the other still counts on; copies are judged by whole ranges,
+  // pinned_range). Ranges that only share a page are fine: each registration pins the page.
+  for (const auto& r : g_regs)
+    if (b < r.first + r.second && r.first < e)
+      return fail_host(FORY_ERR_INVALID_ARGUMENT, "range overlaps a registered range at " + hex(r.first) + " (" +
+                                                      std::to_string(r.second) + " bytes)");
   const int rc = hip_check(hipHostRegister(host_ptr, (size_t)bytes, hipHostRegisterDefault), "hipHostRegister");
   if (!rc) g_regs[b] = (size_t)bytes;
   return rc;

@@ -2628,10 +2628,12 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat9_kernel(FORY_V9_PARAM
 // ---------------------------------------------------------------------------
 constexpr int kV9nW = 8;    // null-bitmap words of the row and all its child rows
 constexpr int kV9nS = 4;    // nested struct fields
-constexpr int kV9nCh = 17;  // dwords of a payload chunk: 64 bytes at any alignment
+// dwords of a payload chunk at any alignment: 64 bytes with two var fields per wave, 128 (a
+// Nested list of 16 int64s in one round trip) with one
 
+template <int CH>
 struct V9nPay {             // one owned var field's first payload chunk
-  uint32_t d[kV9nCh];
+  uint32_t d[CH];
   uint32_t iv[2];           // list item validity: the dwords holding items e0 .. e0 + 63 - (e0 & 31)
 };
 
@@ -2692,8 +2694,9 @@ struct V9nCols {             // one tile's per-lane column registers
       const VarFieldDev* __restrict__ vf, const StructDev* __restrict__ st, const int64_t* __restrict__ offs, \
       uint8_t* __restrict__ out, int64_t capacity, int32_t* status, int cap, SpillArgs sp
 
-template <int HDR, int NW, int OWN, int NS>
+template <int HDR, int NW, int OWN, int NS, int CH>
 __global__ __launch_bounds__(64 * NW) void var_encode_flat9n_kernel(FORY_V9N_PARAMS) {
+  constexpr int kV9nCh = CH;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t* img = lds;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2751,7 +2754,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat9n_kernel(FORY_V9N_PAR
     const int64_t iq = q0 + lane < L.num_rows ? q0 + lane : q0;
     fix_load<false>(fix, fa, fb, iq, F, offs);
   };
-  auto load_pay = [&](const V9nCols<OWN, NS>& C, V9nPay (&P)[OWN]) {
+  auto load_pay = [&](const V9nCols<OWN, NS>& C, V9nPay<kV9nCh> (&P)[OWN]) {
 #pragma unroll
     for (int k = 0; k < OWN; ++k) {
       const VarFieldDev& f = vf[clampv(k)];
@@ -2784,7 +2787,7 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat9n_kernel(FORY_V9N_PAR
   if (tb >= ntiles) return;
   V9nCols<OWN, NS> C[2];
   FixRegs F[2];
-  V9nPay P[OWN];
+  V9nPay<kV9nCh> P[OWN];
   auto ready_vals = [&](FixRegs& R) {
 #pragma unroll
     for (int k = 0; k < kFixBatch; ++k) {
@@ -3017,7 +3020,8 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat9n_kernel(FORY_V9N_PAR
         const int64_t nbytes = n * f.w;
         const int32_t at = here ? pos[k] + (f.is_list ? 8 + bitmap_bytes(n) : 0) : 0;
         const uint8_t* src = f.values + (int64_t)C0.e0[k] * f.w;
-        const int nc = (int)((nbytes + 63) >> 6);
+        constexpr int CB = (kV9nCh - 1) * 4;
+        const int nc = (int)((nbytes + CB - 1) / CB);
         for (int c = 1; __ballot(c < nc); ++c) {
           uint32_t T[kV9nCh];
           pay_load<kV9nCh, false>(src, c < nc ? nbytes : 0, c, T, offs);
@@ -3953,7 +3957,8 @@ void launch_flat_enc9n_k(const VarLaunch& L0, const int64_t* offs, uint8_t* out,
                          int cap, hipStream_t s) {
   VarLaunch L = L0;
   L.pl_all = 1;
-  auto* k = &var_encode_flat9n_kernel<HDR, NW, OWN, NS>;
+  auto* k = OWN == 1 && L.kn.var_enc == 11 ? &var_encode_flat9n_kernel<HDR, NW, OWN, NS, 33>
+                                           : &var_encode_flat9n_kernel<HDR, NW, OWN, NS, 17>;
   const size_t lds = flat9n_lds(L, cap, NW, NS);
   raise_lds_cap(k);
   auto* k2 = &var_encode_flat_kernel<HDR, NW, NS != 0, true>;  // tiles beyond the image
@@ -4001,7 +4006,7 @@ void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int6
   // force round 3 / v7 / v9 where they apply (the parity suite runs every one).
   const int e = L.kn.var_enc;
   const bool v7 = e != 1 && L.num_var <= kOwnVar * NW;
-  if (e == 10 && flat9n_fits(L, NW)) {
+  if ((e == 10 || e == 11) && flat9n_fits(L, NW)) {
     launch_flat_enc9n<HDR, NW>(L, offs, out, capacity, status, cap, s);
   } else if (L.num_struct) {
     if (v7 && e == 7) launch_flat_enc7_own<HDR, NW, true>(L, offs, out, capacity, status, cap, s);

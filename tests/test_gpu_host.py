@@ -526,27 +526,26 @@ def test_host_varlen_decode_into_errors_and_empty():
     hp.close()
 
 
-def test_host_register_refuses_shared_pages_and_foreign_bases():
-    """fory_rowfmt_host_register pins whole pages: a second registration on a page of a live
-    one is refused; unregister takes only a registered range's start; after it, both ends of
-    the range read as unregistered."""
+def test_host_register_refuses_overlaps_and_foreign_bases():
+    """fory_rowfmt_host_register refuses bytes already registered (sharing a page is fine);
+    unregister takes only a registered range's start; after it, both ends of the range read
+    as unregistered while a neighbour on the same page stays registered."""
     from fury_amd.format import IllegalArgumentException
     buf, raw = page_buffer(5 * 4096)
-    a, b = buf[:4096 + 100], buf[4096 + 200:3 * 4096]  # b starts on a's second page
+    a, b = buf[:4096 + 100], buf[4096 + 200:3 * 4096]  # b shares a's second page
     host_register(a)
     try:
         with pytest.raises(IllegalArgumentException):
-            host_register(b)
-        c = buf[3 * 4096:]  # pages of its own: fine
-        host_register(c)
+            host_register(buf[4096:4096 + 150])  # overlaps a's last bytes
+        host_register(b)
         assert registered_ranges() == 2
+        assert copy_path(b) == 1
         with pytest.raises(IllegalArgumentException):
             host_unregister(a[8:])  # not a registered start
-        host_unregister(c)
     finally:
         host_unregister(a)
     assert copy_path(a) == 0 and copy_path(buf[4096 + 99:4096 + 100]) == 0
-    host_register(b)  # a's pages are free again
+    assert copy_path(b) == 1  # the neighbour on the shared page is still registered
     host_unregister(b)
 
 

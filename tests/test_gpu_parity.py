@@ -44,7 +44,7 @@ FIXED = [k for k in catalog() if k not in VARLEN]
 
 
 @pytest.fixture(params=["flat", "flat_stg256", "flat_r3enc", "flat_v7", "flat_v9", "flat_v9_nocap", "flat_v9n",
-                        "flat_v9n_nocap", "flat_v9n_w4", "tile", "global", "spill", "nocap", "tile_nocap", "waves2",
+                        "flat_v9n_nocap", "flat_v9n_w4", "flat_v9n_ch33", "tile", "global", "spill", "nocap", "tile_nocap", "waves2",
                         "waves4"])
 def varlen_engine(request, monkeypatch):
     """Varlen engines: flat cooperative tile kernels (default for flat plans), the
@@ -62,6 +62,7 @@ def varlen_engine(request, monkeypatch):
            "flat_v9n": {"FORY_ROWFMT_VARENC": "10"},
            "flat_v9n_nocap": {"FORY_ROWFMT_VARENC": "10", "FORY_ROWFMT_VARCAP": "2048", "FORY_ROWFMT_SPILLCAP": "2048"},
            "flat_v9n_w4": {"FORY_ROWFMT_VARENC": "10", "FORY_ROWFMT_VARNW": "4"},
+           "flat_v9n_ch33": {"FORY_ROWFMT_VARENC": "11"},
            "tile": {"FORY_ROWFMT_VARFLAT": "0"}, "global": {"FORY_ROWFMT_VARTILE": "0"},
            "spill": {"FORY_ROWFMT_VARCAP": "2048"},
            "nocap": {"FORY_ROWFMT_VARCAP": "2048", "FORY_ROWFMT_SPILLCAP": "2048"},
