@@ -387,10 +387,6 @@ int prepare_var(const Plan& p, const fory_column* cols, int64_t n, int frame, vo
       sd.nfields = op.c;
       sd.hdr = (int32_t)(((op.c + 63) / 64) * 8);
       sd.flags = op.d;
-      // word of its bitmap in encode v9n's partial-word table: after the row's and the
-      // structs' before it (pre-order)
-      sd.woff = (int32_t)(p.bitmap_bytes / 4);
-      for (const fory_amd::StructDev& e : st) sd.woff += e.hdr / 4;
       st.push_back(sd);
       stack.push_back((int32_t)st.size());
     } else if (op.code == fory_amd::OP_STRUCT_END) {
@@ -1000,6 +996,8 @@ void fory_rowfmt_internal_retire_stream(void* stream) {
 
 // Library-internal (host.cpp): shares last_error and the planner's column layout.
 int fory_rowfmt_internal_set_error(int code, const char* msg) { return fail(code, msg); }
+
+int fory_rowfmt_internal_host_path(const fory_plan* plan) { return plan->p.kn.host_path; }
 
 int fory_rowfmt_internal_column_layout(const fory_plan* plan, int32_t* width, int32_t* nullable) {
   const Plan& p = plan->p;

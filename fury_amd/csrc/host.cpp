@@ -106,7 +106,7 @@ class CopyPool {
     for (std::thread& t : threads_) t.join();
   }
   void run_part(int k) {
-    const size_t per = (n_ / parts_ + 63) & ~size_t(63);
+    const size_t per = ((n_ + parts_ - 1) / parts_ + 63) & ~size_t(63);  // parts x per >= n
     const size_t a = std::min(n_, per * (size_t)k), b = std::min(n_, a + per);
     if (b > a) std::memcpy(dst_ + a, src_ + a, b - a);
   }
@@ -152,6 +152,16 @@ struct Staging {
   int64_t pieces = 0;  // statistics: pieces staged over the context's life
 };
 
+// One column slice of a chunk between registered host memory (through its device
+// mapping) and the chunk buffer: bytes [a*width, (a+rows)*width) of the column, or
+// of its validity bitmap (bits = 1: [a/8, a/8 + (rows+7)/8)).
+struct ColSeg {
+  uint8_t* host;
+  uint8_t* dev;
+  int32_t width;
+  int32_t bits;
+};
+
 }  // namespace
 
 struct fory_host_ctx {
@@ -187,6 +197,9 @@ struct fory_host_ctx {
   hipEvent_t ev_sz[2] = {};
   int32_t* vstatus = nullptr;  // one status word per slot (sticky over a call)
   int64_t direct_calls = 0;    // fixed-width calls that took the zero-copy path
+  int64_t gather_calls = 0;    // fixed-width calls whose column slices moved by gather launches
+  int32_t host_path = 0;       // LaunchKnobs.host_path (FORY_ROWFMT_HOSTPATH, A/B)
+  ColSeg* segs[2] = {};        // device: each chunk buffer's gather table (2N entries)
   uint8_t* dbuf = nullptr;   // columns, row offsets, workspace, status
   int64_t dbuf_bytes = 0;
   uint8_t* drows = nullptr;  // rows / frames
@@ -220,6 +233,7 @@ int hip_check(hipError_t e, const char* what) {
 // Library-internal helpers of capi.cpp (not in the public header): last_error
 // is thread-local there; column widths/nullability of a fixed-width plan.
 extern "C" int fory_rowfmt_internal_set_error(int code, const char* msg);
+extern "C" int fory_rowfmt_internal_host_path(const fory_plan* plan);
 extern "C" void fory_rowfmt_internal_retire_stream(void* stream);
 extern "C" int fory_rowfmt_internal_column_layout(const fory_plan* plan, int32_t* width, int32_t* nullable);
 extern "C" int fory_rowfmt_internal_node_layout(const fory_plan* plan, int32_t* kind, int32_t* width,
@@ -463,6 +477,8 @@ int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t c
   for (int i = 0; i < info.num_columns; ++i)
     per += align_up(c->width[i] * chunk_rows) + (c->nullable[i] ? align_up(validity_bytes(chunk_rows)) : 0);
   per += align_up(stride * chunk_rows) + align_up(c->ws_bytes) + kAlign;
+  per += align_up(2 * info.num_columns * (int64_t)sizeof(ColSeg));
+  c->host_path = fory_rowfmt_internal_host_path(plan);
   rc = hip_check(hipMalloc(&c->arena, (size_t)(2 * per)), "hipMalloc(host ctx chunk buffers)");
   if (rc) {
     delete c;
@@ -484,6 +500,8 @@ int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t c
     c->buf[b].ws = p;
     p += align_up(c->ws_bytes);
     c->buf[b].status = reinterpret_cast<int32_t*>(p);
+    p += kAlign;
+    c->segs[b] = reinterpret_cast<ColSeg*>(p);
   }
   rc = hip_check(hipMemset(c->arena, 0, (size_t)(2 * per)), "hipMemset");
   for (hipStream_t* s : {&c->s_in, &c->s_k, &c->s_out})
@@ -620,6 +638,82 @@ int d2h_rows_windows(fory_host_ctx* c, const OutWindows& W, const uint8_t* src, 
   return rc;
 }
 
+constexpr int kSegPiece = 64 * 1024;  // bytes of one segment per workgroup
+constexpr int kSegThreads = 256;
+constexpr int kSegDeep = 4;  // 16-byte loads in flight per lane
+
+// Moves one chunk's column slices between registered host memory and the chunk
+// buffer in ONE launch: blockIdx.y = slice, blockIdx.x = 64 KiB piece of it. Each
+// workgroup streams a contiguous piece (page-sequential host accesses: the host
+// mapping's translations stay hot), 16-byte moves when both ends are 16-byte aligned.
+__global__ __launch_bounds__(kSegThreads) void seg_copy_kernel(const ColSeg* __restrict__ segs, int64_t a,
+                                                               int64_t rows, int32_t to_dev) {
+  const ColSeg sg = segs[blockIdx.y];
+  const int64_t off = sg.bits ? (a >> 3) : a * sg.width;
+  const int64_t bytes = sg.bits ? ((rows + 7) >> 3) : rows * sg.width;
+  const int64_t p0 = (int64_t)blockIdx.x * kSegPiece;
+  if (p0 >= bytes) return;
+  const int64_t p1 = p0 + kSegPiece < bytes ? p0 + kSegPiece : bytes;
+  const uint8_t* s = to_dev ? sg.host + off : sg.dev;
+  uint8_t* d = to_dev ? sg.dev : sg.host + off;
+  const int64_t lane = threadIdx.x;
+  int64_t q = p0;
+  if (((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {
+    constexpr int64_t kRound = 16 * kSegThreads * kSegDeep;
+    for (; q + kRound <= p1; q += kRound) {
+      uint4 r[kSegDeep];
+#pragma unroll
+      for (int u = 0; u < kSegDeep; ++u)
+        r[u] = *reinterpret_cast<const uint4*>(s + q + (u * kSegThreads + lane) * 16);
+#pragma unroll
+      for (int u = 0; u < kSegDeep; ++u) *reinterpret_cast<uint4*>(d + q + (u * kSegThreads + lane) * 16) = r[u];
+    }
+    const int64_t v1 = q + ((p1 - q) & ~(int64_t)15);
+    for (int64_t t = q + lane * 16; t < v1; t += 16 * kSegThreads)
+      *reinterpret_cast<uint4*>(d + t) = *reinterpret_cast<const uint4*>(s + t);
+    q = v1;
+  }
+  for (int64_t t = q + lane; t < p1; t += kSegThreads) d[t] = s[t];
+}
+
+// Gather tables of a fixed-width call: when every column (and the validity of the
+// nullable ones the caller passed) is registered over its whole range, each chunk
+// buffer's table of slices goes to the device once per call and *nseg is set;
+// *nseg = 0: not registered (the per-slice copies run).
+int gather_setup(fory_host_ctx* c, const fory_column* h, int64_t n, int* nseg, int32_t* maxw) {
+  *nseg = 0;
+  *maxw = 1;
+  if (c->host_path != 0) return FORY_OK;
+  const int N = c->info.num_columns;
+  std::vector<ColSeg> t[2];
+  for (int i = 0; i < N; ++i) {
+    uint8_t* v = mapped_range(h[i].values, (size_t)(n * c->width[i]));
+    if (!v) return FORY_OK;
+    for (int b = 0; b < 2; ++b) t[b].push_back(ColSeg{v, c->buf[b].cols[i].values, c->width[i], 0});
+    *maxw = std::max(*maxw, c->width[i]);
+    if (c->nullable[i] && h[i].validity) {
+      uint8_t* m = mapped_range(h[i].validity, (size_t)((n + 7) / 8));
+      if (!m) return FORY_OK;
+      for (int b = 0; b < 2; ++b) t[b].push_back(ColSeg{m, c->buf[b].cols[i].validity, 1, 1});
+    }
+  }
+  for (int b = 0; b < 2; ++b) {
+    const int rc = hip_check(hipMemcpy(c->segs[b], t[b].data(), t[b].size() * sizeof(ColSeg), hipMemcpyHostToDevice),
+                             "hipMemcpy(gather table)");
+    if (rc) return rc;
+  }
+  *nseg = (int)t[0].size();
+  ++c->gather_calls;
+  return FORY_OK;
+}
+
+int launch_seg_copy(fory_host_ctx* c, int b, int nseg, int32_t maxw, int64_t a, int64_t rows, int to_dev,
+                    hipStream_t s) {
+  const int64_t pieces = (rows * maxw + kSegPiece - 1) / kSegPiece;
+  seg_copy_kernel<<<dim3((unsigned)pieces, (unsigned)nseg), kSegThreads, 0, s>>>(c->segs[b], a, rows, to_dev);
+  return hip_check(hipGetLastError(), to_dev ? "gather launch" : "scatter launch");
+}
+
 // Zero copy for fixed-width plans. When every column (values, and the validity of
 // nullable fields) and every output window is registered over its whole range, the
 // encode kernel itself reads the columns and writes the rows through their device
@@ -630,6 +724,7 @@ int d2h_rows_windows(fory_host_ctx* c, const OutWindows& W, const uint8_t* src, 
 // aligned, or a window of a plan with validity starts inside a validity byte.
 int host_encode_direct(fory_host_ctx* c, const fory_column* h, int64_t n, int32_t frame, int64_t stride,
                        const OutWindows& W) {
+  if (c->host_path != 1) return -1;
   const int N = c->info.num_columns;
   std::vector<uint8_t*> val((size_t)N), vld((size_t)N, nullptr);
   bool any_validity = false;
@@ -675,6 +770,7 @@ int host_encode_direct(fory_host_ctx* c, const fory_column* h, int64_t n, int32_
 // ranges -> one decode launch reading the rows and writing the columns in host memory.
 int host_decode_direct(fory_host_ctx* c, const uint8_t* rows_h, int64_t n, int32_t frame, int64_t stride,
                        const fory_column* h) {
+  if (c->host_path != 1) return -1;
   const int N = c->info.num_columns;
   uint8_t* rows = mapped_range(rows_h, (size_t)(n * stride));
   if (!rows || (reinterpret_cast<uintptr_t>(rows) & 15)) return -1;
@@ -722,6 +818,9 @@ int host_encode_fixed(fory_host_ctx* c, const fory_column* host_cols, int64_t n,
   if (rc) return rc;
   const int direct = host_encode_direct(c, host_cols, n, frame, stride, *W);
   if (direct >= 0) return direct;
+  int nseg = 0;
+  int32_t maxw = 1;
+  rc = gather_setup(c, host_cols, n, &nseg, &maxw);
   for (int b = 0; b < 2 && !rc; ++b)
     rc = hip_check(hipMemsetAsync(c->buf[b].status, 0, 4, c->s_k), "hipMemsetAsync");
   const int64_t chunks = (n + c->chunk - 1) / c->chunk;
@@ -733,13 +832,15 @@ int host_encode_fixed(fory_host_ctx* c, const fory_column* host_cols, int64_t n,
     fory_host_ctx::Buf& B = c->buf[b];
     // H2D: column slices (+ validity bytes) into buffer b once chunk k-2's kernel is done with it
     if (k >= 2) rc = hip_check(hipStreamWaitEvent(c->s_in, c->ev_k[b], 0), "hipStreamWaitEvent");
+    if (!rc && nseg) rc = launch_seg_copy(c, b, nseg, maxw, a, rows, 1, c->s_in);
     for (int i = 0; i < c->info.num_columns && !rc; ++i) {
       const fory_column& h = host_cols[i];
+      dcols[i] = fory_column{B.cols[i].values, nullptr, (c->nullable[i] && h.validity) ? B.cols[i].validity : nullptr,
+                             rows, rows * c->width[i]};
+      if (nseg) continue;
       rc = hcopy(c, B.cols[i].values, static_cast<const uint8_t*>(h.values) + a * c->width[i], (size_t)(rows * c->width[i]), hipMemcpyHostToDevice, c->s_in, "H2D");
       if (!rc && c->nullable[i] && h.validity)
         rc = hcopy(c, B.cols[i].validity, h.validity + a / 8, (size_t)((rows + 7) / 8), hipMemcpyHostToDevice, c->s_in, "H2D validity");
-      dcols[i] = fory_column{B.cols[i].values, nullptr, (c->nullable[i] && h.validity) ? B.cols[i].validity : nullptr,
-                             rows, rows * c->width[i]};
     }
     if (!rc) rc = hip_check(hipEventRecord(c->ev_in[b], c->s_in), "hipEventRecord");
     // kernel: after the chunk landed and chunk k-2's rows left buffer b
@@ -800,6 +901,9 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
   if (rc) return rc;
   const int direct = host_decode_direct(c, static_cast<const uint8_t*>(host_rows), n, frame, stride, host_out_cols);
   if (direct >= 0) return direct;
+  int nseg = 0;
+  int32_t maxw = 1;
+  rc = gather_setup(c, host_out_cols, n, &nseg, &maxw);
   for (int b = 0; b < 2 && !rc; ++b)
     rc = hip_check(hipMemsetAsync(c->buf[b].status, 0, 4, c->s_k), "hipMemsetAsync");
   const int64_t chunks = (n + c->chunk - 1) / c->chunk;
@@ -824,7 +928,8 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
                                      c->s_k);
     if (!rc) rc = hip_check(hipEventRecord(c->ev_k[b], c->s_k), "hipEventRecord");
     if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_out, c->ev_k[b], 0), "hipStreamWaitEvent");
-    for (int i = 0; i < c->info.num_columns && !rc; ++i) {
+    if (!rc && nseg) rc = launch_seg_copy(c, b, nseg, maxw, a, rows, 0, c->s_out);
+    for (int i = 0; i < c->info.num_columns && !rc && !nseg; ++i) {
       const fory_column& h = host_out_cols[i];
       rc = hcopy(c, static_cast<uint8_t*>(h.values) + a * c->width[i], B.cols[i].values, (size_t)(rows * c->width[i]), hipMemcpyDeviceToHost, c->s_out, "D2H");
       if (!rc && dcols[i].validity)
@@ -1723,6 +1828,11 @@ extern "C" int fory_rowfmt_internal_host_copy_path(const void* p, int64_t bytes)
 
 extern "C" int64_t fory_rowfmt_internal_host_staged_pieces(const fory_host_ctx* c) { return c ? c->stage.pieces : -1; }
 extern "C" int64_t fory_rowfmt_internal_host_direct_calls(const fory_host_ctx* c) { return c ? c->direct_calls : -1; }
+// The staged copies' host memcpy (CopyPool), for a CPU test of its split.
+extern "C" void fory_rowfmt_internal_pool_copy(void* dst, const void* src, int64_t n) {
+  CopyPool::get().copy(dst, src, (size_t)n);
+}
+extern "C" int64_t fory_rowfmt_internal_host_gather_calls(const fory_host_ctx* c) { return c ? c->gather_calls : -1; }
 
 // Library-internal, for tests: round 2's classification (the first byte's attribute
 // only), kept to show the straddling-range hazard it had next to pinned_range's answer.

@@ -2598,491 +2598,6 @@ __global__ __launch_bounds__(64 * NW) void var_encode_flat9_kernel(FORY_V9_PARAM
   var_encode_flat9_body<HDR, NW, OWN, K, NUL>(L, prog, cols, fix, vf, offs, out, capacity, status, cap, sp);
 }
 
-// ---------------------------------------------------------------------------
-// Encode v9n: encode v9's two-tile straight-line pipeline for plans with nested struct
-// fields and / or list<fixed> fields (BASELINE C3 Nested: Outer{a, b, c: Inner{x, y,
-// z: List<Long>}}), which v9's prefix layout did not cover (they took the round-3 tile
-// kernel: wave 0 walked the program with loads in between, three barriers, one tile per
-// workgroup -- 0.35 of HBM peak, SQ_WAIT_ANY 0.70).
-//   --  tile tb: the owned var fields' offsets and validity, the fixed batch, every
-//       struct's validity, the row bounds (all loads unconditional); then the owned
-//       fields' first 64 payload bytes (and a list's item-validity words); then tile
-//       tb + 1's columns -- all in flight while tile tb is assembled
-//   P1  presence of each struct (its validity and its parent's), payload sizes into
-//       an LDS table (-1 null, -2 absent: under a null struct), null bits as partial
-//       words per wave of the row's and every child row's bitmap (no atomics)
-//   B1
-//   P2  every lane walks the program over the size table (LDS only, no loads): the
-//       positions of its wave's fields and of every child row (BinaryRowWriter(schema,
-//       parent) shares the writerIndex: a struct's child row is reserved where its
-//       field is reached, its var payloads follow, BaseBinaryEncoderBuilder.java:436-490);
-//       the record's size against its offsets; wave 0 writes the frame header and the
-//       row bitmap, the wave owning a struct its child bitmap and its parent slot
-//   P3  fixed slots at their (child) rows, var slots, strings, list headers and items
-//       (BinaryArrayWriter.reset + write, BinaryArrayWriter.java:93-118: [i64 n][null
-//       bitmap][items padded to 8]; null items zero with their bit set); payloads past
-//       64 bytes take a round trip per further 64
-//   --  tile tb + 1's payload chunks in flight; B2; the image leaves as 16-B stores.
-// Var field v is owned by wave NW - 1 - v % NW (the fixed batches go from wave 0 up).
-// Bytes are those of the round-3 tile kernel (var_encode_flat_kernel<NEST>).
-// ---------------------------------------------------------------------------
-constexpr int kV9nW = 8;    // null-bitmap words of the row and all its child rows
-constexpr int kV9nS = 4;    // nested struct fields
-// dwords of a payload chunk at any alignment: 64 bytes with two var fields per wave, 128 (a
-// Nested list of 16 int64s in one round trip) with one
-
-template <int CH>
-struct V9nPay {             // one owned var field's first payload chunk
-  uint32_t d[CH];
-  uint32_t iv[2];           // list item validity: the dwords holding items e0 .. e0 + 63 - (e0 & 31)
-};
-
-// Payload bytes [64 c, 64 c + 64) of n bytes at src through CH aligned dwords (each holds
-// a byte of the payload, so none lies past the column), issued branch-free when ALL (dwords
-// past the payload re-read its last one; an empty payload reads `safe`).
-template <int CH, bool ALL>
-__device__ __forceinline__ void pay_load(const uint8_t* src, int64_t n, int c, uint32_t (&d)[CH], const void* safe) {
-  constexpr int CB = (CH - 1) * 4;
-  const uintptr_t a = reinterpret_cast<uintptr_t>(src) + (uintptr_t)CB * c;
-  const int sb = (int)(a & 3);
-  const uint32_t* p = reinterpret_cast<const uint32_t*>(a - sb);
-  const int64_t left = n - (int64_t)CB * c;
-  const int nd = left <= 0 ? 0 : (int)((sb + (left < CB ? left : CB) + 3) >> 2);
-#pragma unroll
-  for (int q = 0; q < CH; ++q) {
-    if constexpr (ALL) {
-      const uint32_t* at = nd > 0 ? p + (q < nd ? q : nd - 1) : reinterpret_cast<const uint32_t*>(safe);
-      d[q] = *gp(at);
-    } else {
-      d[q] = q < nd ? *gp(p + q) : 0u;
-    }
-  }
-}
-
-// Chunk c of writeUnaligned + zeroOutPaddingBytes (the list items: BinaryArrayWriter's
-// elements + their padding) to the 4-byte aligned LDS image at dst: bytes [64 c, 64 c +
-// 64) of n, zeros past n, the dwords inside round8(n).
-template <int CH>
-__device__ __forceinline__ void pay_store(uint8_t* dst, const uint8_t* src, int64_t n, int c, const uint32_t (&d)[CH]) {
-  constexpr int CB = (CH - 1) * 4;
-  const int sb = (int)((reinterpret_cast<uintptr_t>(src) + (uintptr_t)CB * c) & 3);
-  const int64_t left = n - (int64_t)CB * c;
-  const int64_t outb = round8(n) - (int64_t)CB * c;
-#pragma unroll
-  for (int q = 0; q < CH - 1; ++q) {
-    if (4 * q < outb) {
-      uint32_t w = sb ? funnel(d[q], d[q + 1], sb) : d[q];
-      const int64_t valid = left - 4 * q;
-      if (valid <= 0) w = 0u;
-      else if (valid < 4) w &= (1u << (8 * valid)) - 1u;
-      st32(dst + CB * c + 4 * q, w);
-    }
-  }
-}
-
-template <int OWN, int NS>
-struct V9nCols {             // one tile's per-lane column registers
-  int32_t e0[OWN], e1[OWN];
-  uint32_t vvb[OWN];         // owned var fields: the dword holding the record's validity byte
-  uint32_t fvb[kFixBatch];   // the wave's fixed batch: the same
-  uint32_t svb[NS > 0 ? NS : 1];  // struct fields: the same
-  int64_t beg, end;          // the record's row bounds
-};
-
-#define FORY_V9N_PARAMS                                                                                   \
-  VarLaunch L, const Op* __restrict__ prog, const FixedFieldDev* __restrict__ fix,                       \
-      const VarFieldDev* __restrict__ vf, const StructDev* __restrict__ st, const int64_t* __restrict__ offs, \
-      uint8_t* __restrict__ out, int64_t capacity, int32_t* status, int cap, SpillArgs sp
-
-template <int HDR, int NW, int OWN, int NS, int CH>
-__global__ __launch_bounds__(64 * NW) void var_encode_flat9n_kernel(FORY_V9N_PARAMS) {
-  constexpr int kV9nCh = CH;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint8_t* img = lds;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // bitmap words: the row's [0, bmw0), then each struct's (pre-order; StructDev.woff)
-  int W = L.bitmap_bytes >> 2;
-  if constexpr (NS > 0)
-    if (L.num_struct > 0) W = st[L.num_struct - 1].woff + (st[L.num_struct - 1].hdr >> 2);
-  auto woff = [&](int parent) { return parent ? st[parent - 1].woff : 0; };  // (parent wave-uniform)
-  int32_t* sz = reinterpret_cast<int32_t*>(lds + cap);                 // [num_var][64] payload bytes
-  uint32_t* pbt = reinterpret_cast<uint32_t*>(sz + L.num_var * 64);     // [NW][64][W] partial null bits
-  uint32_t* tbad = pbt + NW * 64 * W;                                   // [2] by tile parity
-  // this wave's child-row starts and sizes per struct ([2][NS + 1][64]; -1: null / absent)
-  int32_t* sbt = reinterpret_cast<int32_t*>(tbad + 2) + wave * 2 * (NS + 1) * 64;
-  int32_t* sst = sbt + (NS + 1) * 64;
-  auto sb_of = [&](int s) { return s ? sbt[s * 64 + lane] : 0; };
-  const int64_t ntiles = (L.num_rows + 63) / 64;
-  int fk0 = 0, fk1 = 0;
-  const bool has_fix = fix_batch(L, wave, &fk0, &fk1);
-  const int fa = has_fix ? fk0 : L.fix_group[4] - 1, fb = has_fix ? fk1 : fa + 1;
-  auto ownv = [&](int k) { return NW - 1 - wave + k * NW; };  // owned var field k (may be >= num_var)
-  auto clampv = [&](int k) { const int v = ownv(k); return v < L.num_var ? v : L.num_var - 1; };
-
-  auto load_cols = [&](int64_t tl, V9nCols<OWN, NS>& C) {
-    tl = tl < ntiles ? tl : ntiles - 1;  // (past the end: the last tile, unused)
-    const int64_t q0 = tl * 64;
-    const int rw = L.num_rows - q0 < 64 ? (int)(L.num_rows - q0) : 64;
-    const bool lq = lane < rw;
-    const int64_t iq = lq ? q0 + lane : q0;
-#pragma unroll
-    for (int k = 0; k < OWN; ++k) {
-      const VarFieldDev& f = vf[clampv(k)];
-      C.e0[k] = *gp(f.offsets + (lq ? iq : q0 + rw));  // dead lanes: the tile's end (empty ranges)
-      C.e1[k] = *gp(f.offsets + (lq ? iq + 1 : q0 + rw));
-      C.vvb[k] = vbyte_issue(f.validity ? f.validity + (iq >> 3) : reinterpret_cast<const uint8_t*>(offs));
-    }
-#pragma unroll
-    for (int k = 0; k < kFixBatch; ++k) {
-      const FixedFieldDev& f = fix[min(fa + k, fb - 1)];
-      C.fvb[k] = vbyte_issue(f.validity ? f.validity + (iq >> 3) : reinterpret_cast<const uint8_t*>(offs));
-    }
-    if constexpr (NS > 0) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const StructDev& sd = st[s < L.num_struct ? s : L.num_struct - 1];
-        C.svb[s] = vbyte_issue(sd.validity ? sd.validity + (iq >> 3) : reinterpret_cast<const uint8_t*>(offs));
-      }
-    }
-    C.beg = offs[iq];
-    C.end = offs[lq ? iq + 1 : q0];
-  };
-  auto load_fixed = [&](int64_t tl, FixRegs& F) {
-    tl = tl < ntiles ? tl : ntiles - 1;
-    const int64_t q0 = tl * 64;
-    const int64_t iq = q0 + lane < L.num_rows ? q0 + lane : q0;
-    fix_load<false>(fix, fa, fb, iq, F, offs);
-  };
-  auto load_pay = [&](const V9nCols<OWN, NS>& C, V9nPay<kV9nCh> (&P)[OWN]) {
-#pragma unroll
-    for (int k = 0; k < OWN; ++k) {
-      const VarFieldDev& f = vf[clampv(k)];
-      const int64_t n = (int64_t)C.e1[k] - C.e0[k];
-      pay_load<kV9nCh, true>(f.values + (int64_t)C.e0[k] * f.w, n * f.w, 0, P[k].d, offs);
-      const uint32_t* iv = reinterpret_cast<const uint32_t*>(offs);  // (unused)
-      if (f.item_validity && n > 0) iv = reinterpret_cast<const uint32_t*>(f.item_validity) + (C.e0[k] >> 5);
-      P[k].iv[0] = *gp(iv);
-      P[k].iv[1] = *gp((C.e0[k] & 31) + n > 32 ? iv + 1 : iv);
-    }
-  };
-  auto ready_cols = [&](V9nCols<OWN, NS>& C) {
-#pragma unroll
-    for (int k = 0; k < OWN; ++k) {
-      ready(C.e0[k]);
-      ready(C.e1[k]);
-      ready(C.vvb[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < kFixBatch; ++k) ready(C.fvb[k]);
-    if constexpr (NS > 0) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) ready(C.svb[s]);
-    }
-    ready(C.beg);
-    ready(C.end);
-  };
-
-  const int64_t tb = (int64_t)blockIdx.x * 2;  // this workgroup's tiles tb, tb + 1
-  if (tb >= ntiles) return;
-  V9nCols<OWN, NS> C[2];
-  FixRegs F[2];
-  V9nPay<kV9nCh> P[OWN];
-  auto ready_vals = [&](FixRegs& R) {
-#pragma unroll
-    for (int k = 0; k < kFixBatch; ++k) {
-      ready(R.lo[k]);
-      ready(R.hi[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < OWN; ++k) {
-#pragma unroll
-      for (int q = 0; q < kV9nCh; ++q) ready(P[k].d[q]);
-      ready(P[k].iv[0]);
-      ready(P[k].iv[1]);
-    }
-  };
-  load_cols(tb, C[0]);
-  load_fixed(tb, F[0]);
-  sched_fence();
-  ready_cols(C[0]);
-  load_pay(C[0], P);
-  sched_fence();
-  load_cols(tb + 1, C[1]);
-  load_fixed(tb + 1, F[1]);
-  sched_fence();
-
-  auto step = [&](int64_t t, V9nCols<OWN, NS>& C0, FixRegs& FV, V9nCols<OWN, NS>& C1, bool more) {
-    sched_fence();
-    ready_cols(C0);
-    const int64_t r0 = t * 64;
-    const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
-    const bool live = lane < rows;
-    const int64_t ii = live ? r0 + lane : r0;
-    // ---- P1: bounds checks (uniform over the workgroup: every wave sees the same rows)
-    const int64_t B0 = __shfl(C0.beg, 0), B1 = __shfl(C0.end, rows - 1);
-    const bool ok = !live || (C0.beg >= B0 && C0.end >= C0.beg && C0.end <= B1);
-    const bool sane = __ballot(!ok) == 0 && ((B0 | B1) & 3) == 0 && B1 >= B0;
-    const bool capbad = live && (C0.end > capacity || C0.beg < 0 || C0.end < C0.beg);
-    const bool skip = __ballot(capbad) != 0;
-    if (skip && wave == 0 && capbad) set_status(status, FORY_ERR_CAPACITY);
-    const int mis = (int)(reinterpret_cast<uintptr_t>(out + B0) & 15);
-    const int64_t total = mis + (B1 - B0);
-    const bool tiled = !skip && sane && !(mis & 3) && total <= cap;
-    uint8_t* fp = img + mis + (int)(C0.beg - B0);
-    uint8_t* row = fp + HDR;
-    // struct presence (bit s: struct s present, bit 0 the row): pre-order, parents first
-    uint32_t pm = 1;
-    if constexpr (NS > 0) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        if (s >= L.num_struct) continue;
-        const StructDev& sd = st[s];
-        const bool valid = !sd.validity || ((vbyte_get(C0.svb[s], sd.validity + (ii >> 3)) >> (ii & 7)) & 1);
-        if (valid && ((pm >> sd.parent) & 1)) pm |= 1u << (s + 1);
-      }
-    }
-    if (tiled) {
-      uint32_t pw[kV9nW];
-#pragma unroll
-      for (int q = 0; q < kV9nW; ++q) pw[q] = 0u;
-      auto null_bit = [&](int parent, int slot) {  // (parent wave-uniform)
-        const int wi = woff(parent) + (slot >> 5);
-#pragma unroll
-        for (int q = 0; q < kV9nW; ++q) pw[q] |= q == wi ? 1u << (slot & 31) : 0u;
-      };
-#pragma unroll
-      for (int k = 0; k < OWN; ++k) {
-        const int v = ownv(k);
-        if (v >= L.num_var) continue;
-        const VarFieldDev& f = vf[v];
-        const bool present = live && ((pm >> f.parent) & 1);
-        const bool valid = !f.validity || ((vbyte_get(C0.vvb[k], f.validity + (ii >> 3)) >> (ii & 7)) & 1);
-        const int64_t n = (int64_t)C0.e1[k] - C0.e0[k];
-        const int32_t bytes = (int32_t)(f.is_list ? 8 + bitmap_bytes(n) + round8(n * f.w) : round8(n));
-        sz[v * 64 + lane] = !present ? -2 : !valid ? -1 : bytes;
-        if (present && !valid) null_bit(f.parent, f.slot);
-      }
-#pragma unroll
-      for (int k = 0; k < kFixBatch; ++k) {
-        if (fk0 + k >= fk1) continue;
-        const FixedFieldDev& f = fix[fk0 + k];
-        if (f.validity && live && ((pm >> f.parent) & 1) &&
-            !((vbyte_get(C0.fvb[k], f.validity + (ii >> 3)) >> (ii & 7)) & 1))
-          null_bit(f.parent, f.slot);
-      }
-      if constexpr (NS > 0) {
-        if (wave == 0) {  // null structs (their parent present): BinaryWriter.setNullAt in the parent
-#pragma unroll
-          for (int s = 0; s < NS; ++s)
-            if (s < L.num_struct && live && ((pm >> st[s].parent) & 1) && !((pm >> (s + 1)) & 1))
-              null_bit(st[s].parent, st[s].slot);
-        }
-      }
-      uint32_t* pwl = pbt + (wave * 64 + lane) * W;
-#pragma unroll
-      for (int q = 0; q < kV9nW; ++q)
-        if (q < W) pwl[q] = pw[q];
-      if (tid == 0) tbad[t & 1] = 0u;  // (last read by tile t - 2's store, two barriers ago)
-    }
-    __syncthreads();  // B1
-    if (tiled) {
-      // ---- P2: the program walk over the size table: positions of the wave's fields,
-      // child-row starts (-1: null / absent) and sizes
-      int32_t acc = L.fixed_size;
-      int32_t pos[OWN];
-#pragma unroll
-      for (int k = 0; k < OWN; ++k) pos[k] = -2;
-      int vi = 0, si = 0, cur = 0;
-      for (int pc = 0; pc < L.num_ops; ++pc) {
-        const Op op = prog[pc];
-        if (op.code == OP_BYTES || op.code == OP_LIST) {
-          const int32_t s = sz[vi * 64 + lane];
-#pragma unroll
-          for (int k = 0; k < OWN; ++k)
-            if (vi == ownv(k)) pos[k] = s >= 0 ? acc : s;
-          acc += s > 0 ? s : 0;
-          ++vi;
-        } else if (NS > 0 && op.code == OP_STRUCT_BEGIN) {
-          ++si;
-          cur = si;
-          const StructDev& sd = st[si - 1];
-          const bool present = live && ((pm >> si) & 1);
-          sbt[si * 64 + lane] = present ? acc : -1;
-          if (present) acc += sd.hdr + 8 * sd.nfields;
-        } else if (NS > 0 && op.code == OP_STRUCT_END) {
-          const int32_t b = sbt[cur * 64 + lane];
-          sst[cur * 64 + lane] = b >= 0 ? acc - b : -1;
-          cur = st[cur - 1].parent;
-        }
-      }
-      const bool wr = live && acc + HDR == C0.end - C0.beg;  // this lane writes its record
-      if (live && !wr) {  // columns changed since encoded_size: nothing of the record, the tile not stored
-        tbad[t & 1] = 1u;
-        set_status(status, FORY_ERR_ENCODER);
-      }
-      if (wave == 0 && wr) {  // Encoders.encode frame header; BinaryRowWriter.reset + setNullAt
-        if (HDR == 12) {
-          st32(fp, (uint32_t)(C0.end - C0.beg - 4));
-          st64_lds(fp + 4, (uint64_t)L.schema_hash);
-        } else if (HDR == 8) {
-          st64_lds(fp, (uint64_t)L.schema_hash);
-        }
-        for (int q = 0; q < (L.bitmap_bytes >> 2); ++q) {
-          uint32_t w = 0;
-          for (int v2 = 0; v2 < NW; ++v2) w |= pbt[(v2 * 64 + lane) * W + q];
-          st32(row + 4 * q, w);
-        }
-      }
-      if constexpr (NS > 0) {  // child rows of the structs this wave owns: bitmap + parent slot
-#pragma unroll
-        for (int s = 1; s <= NS; ++s) {
-          if (s > L.num_struct || (s - 1) % NW != wave || !wr) continue;
-          const StructDev& sd = st[s - 1];
-          const int32_t pb = sb_of(sd.parent);
-          if (pb < 0) continue;  // absent
-          const int32_t ph = sd.parent ? st[sd.parent - 1].hdr : L.bitmap_bytes;
-          uint8_t* sl = row + pb + ph + 8 * sd.slot;
-          const int32_t b = sbt[s * 64 + lane];
-          if (b < 0) {  // null: slot 0 (its bit is wave 0's partial word)
-            st64_lds(sl, 0);
-            continue;
-          }
-          st64_lds(sl, ((uint64_t)(uint32_t)(b - pb) << 32) | (uint32_t)sst[s * 64 + lane]);
-          for (int q = 0; q < (sd.hdr >> 2); ++q) {
-            uint32_t w = 0;
-            for (int v2 = 0; v2 < NW; ++v2) w |= pbt[(v2 * 64 + lane) * W + sd.woff + q];
-            st32(row + b + 4 * q, w);
-          }
-        }
-      }
-      // ---- P3: fixed slots at their rows (BinaryRowWriter.write: zero-extended; null -> 0)
-      sched_fence();
-      ready_vals(FV);
-      if (has_fix && wr) {
-#pragma unroll
-        for (int k = 0; k < kFixBatch; ++k) {
-          if (fk0 + k >= fk1) continue;
-          const FixedFieldDev& f = fix[fk0 + k];
-          const int32_t base = sb_of(f.parent);
-          if (base < 0) continue;  // under a null struct
-          const int32_t hdr = f.parent ? st[f.parent - 1].hdr : L.bitmap_bytes;
-          const bool valid = !f.validity || ((vbyte_get(C0.fvb[k], f.validity + (ii >> 3)) >> (ii & 7)) & 1);
-          uint64_t x = valid ? elem_value(f.values, f.width, ii, FV.lo[k], FV.hi[k]) : 0;
-          if (f.flags & 2) x = x ? 1 : 0;
-          st64_lds(row + base + hdr + 8 * f.slot, x);
-        }
-      }
-      // var slots, strings / list headers and items: the first chunk from registers
-#pragma unroll
-      for (int k = 0; k < OWN; ++k) {
-        const int v = ownv(k);
-        if (v >= L.num_var || !wr) continue;
-        const VarFieldDev& f = vf[v];
-        const int32_t base = sb_of(f.parent);
-        if (base < 0) continue;  // under a null struct
-        const int32_t hdr = f.parent ? st[f.parent - 1].hdr : L.bitmap_bytes;
-        uint8_t* sl = row + base + hdr + 8 * f.slot;
-        const int32_t p = pos[k];
-        if (p < 0) {
-          st64_lds(sl, 0);
-          continue;
-        }
-        const int64_t n = (int64_t)C0.e1[k] - C0.e0[k];
-        const uint8_t* src = f.values + (int64_t)C0.e0[k] * f.w;
-        if (!f.is_list) {  // writeUnaligned: (offset << 32 | size), padded payload
-          st64_lds(sl, ((uint64_t)(uint32_t)(p - base) << 32) | (uint32_t)n);
-          pay_store<kV9nCh>(row + p, src, n, 0, P[k].d);
-        } else {  // BinaryArrayWriter.reset(n): [i64 n][null bitmap][n x w, padded to 8]
-          const int32_t ahdr = 8 + bitmap_bytes(n);
-          st64_lds(row + p, (uint64_t)n);
-          st64_lds(sl, ((uint64_t)(uint32_t)(p - base) << 32) | (uint32_t)(ahdr + round8(n * f.w)));
-          if (n > 0 && n <= 32) {  // the item null bits from the loaded words (setNullAt)
-            const uint64_t iw = ((uint64_t)P[k].iv[1] << 32) | P[k].iv[0];
-            const uint32_t nb = f.item_validity ? ~(uint32_t)(iw >> (C0.e0[k] & 31)) & (uint32_t)((1ull << n) - 1)
-                                                : 0u;
-            st32(row + p + 8, nb);
-            st32(row + p + 12, 0u);
-          } else {
-            for (int q = 8; q < ahdr; q += 4) st32(row + p + q, 0u);
-          }
-          pay_store<kV9nCh>(row + p + ahdr, src, n * f.w, 0, P[k].d);
-        }
-      }
-      // payloads past 64 bytes: their further chunks (a round trip each); then null list items
-#pragma unroll
-      for (int k = 0; k < OWN; ++k) {
-        const int v = ownv(k);
-        if (v >= L.num_var) continue;
-        const VarFieldDev& f = vf[v];
-        const bool here = wr && sb_of(f.parent) >= 0 && pos[k] >= 0;
-        const int64_t n = here ? (int64_t)C0.e1[k] - C0.e0[k] : 0;
-        const int64_t nbytes = n * f.w;
-        const int32_t at = here ? pos[k] + (f.is_list ? 8 + bitmap_bytes(n) : 0) : 0;
-        const uint8_t* src = f.values + (int64_t)C0.e0[k] * f.w;
-        constexpr int CB = (kV9nCh - 1) * 4;
-        const int nc = (int)((nbytes + CB - 1) / CB);
-        for (int c = 1; __ballot(c < nc); ++c) {
-          uint32_t T[kV9nCh];
-          pay_load<kV9nCh, false>(src, c < nc ? nbytes : 0, c, T, offs);
-          if (c < nc) pay_store<kV9nCh>(row + at, src, nbytes, c, T);
-        }
-        if (f.is_list && f.item_validity && n > 0) {
-          const int32_t p = pos[k];
-          if (n > 32) {  // item null bits beyond the loaded words: from the column (rare)
-            for (int64_t j0 = 0; j0 < n; j0 += 32) {
-              uint32_t nbw = 0;
-              for (int64_t j = j0; j < n && j < j0 + 32; ++j) {
-                const int64_t q = C0.e0[k] + j;
-                if (!((*gp(f.item_validity + (q >> 3)) >> (q & 7)) & 1)) nbw |= 1u << (j - j0);
-              }
-              st32(row + p + 8 + 4 * (j0 >> 5), nbw);
-            }
-          }
-          // null items read as 0 (BinaryArrayWriter.setNullAt leaves the element zero)
-          uint8_t* items = row + at;
-          for (int64_t j0 = 0; j0 < n; j0 += 32) {
-            uint32_t nbw = ld32(row + p + 8 + 4 * (j0 >> 5));
-            while (nbw) {
-              const int64_t j = j0 + __builtin_ctz(nbw);
-              nbw &= nbw - 1;
-              for (int b = 0; b < f.w; ++b) items[j * f.w + b] = 0;
-            }
-          }
-        }
-      }
-    } else if (!skip && tid == 0) {  // unaligned or big tile: the spill launch
-      sp.list[atomicAdd(sp.count, 1)] = (int32_t)t;
-    }
-    sched_fence();
-    if (more) {  // the next tile: its payloads' first chunks in flight
-      ready_cols(C1);
-      load_pay(C1, P);
-    }
-    sched_fence();
-    __syncthreads();  // B2: the image is complete
-    if (tiled && !tbad[t & 1]) {
-      uint8_t* g = out + B0 - mis;  // 16-byte aligned
-      const int tot = (int)total;
-      const int nch = (tot + 15) >> 4;
-      for (int cc = tid; cc < nch; cc += 64 * NW) {
-        const int lo = cc * 16;
-        if (lo >= mis && lo + 16 <= tot) {
-          *gp(reinterpret_cast<u32x4*>(g + lo)) = *reinterpret_cast<const u32x4*>(img + lo);
-        } else {
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const int o = lo + 4 * d;
-            if (o >= mis && o + 4 <= tot) *gp(reinterpret_cast<uint32_t*>(g + o)) = ld32(img + o);
-          }
-        }
-      }
-    }
-  };
-  step(tb, C[0], F[0], C[1], tb + 1 < ntiles);
-  if (tb + 1 < ntiles) step(tb + 1, C[1], F[1], C[1], false);
-}
-
 __device__ __forceinline__ int64_t wave_incl_scan64(int64_t x, int lane) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -3931,63 +3446,6 @@ void launch_flat_enc9(const VarLaunch& L0, const int64_t* offs, uint8_t* out, in
                      sp.cap, sp);
 }
 
-// Encode v9n LDS: row image, payload-size table, partial null words of every bitmap, two tile flags.
-int v9n_words(const VarLaunch& L) {
-  int w = L.bitmap_bytes >> 2;
-  for (int s = 0; s < L.num_struct; ++s) w += L.st_hdr[s] >> 2;
-  return w;
-}
-size_t flat9n_lds(const VarLaunch& L, int cap, int nw, int ns) {
-  return (size_t)cap + (size_t)L.num_var * 64 * sizeof(int32_t) + (size_t)nw * 64 * v9n_words(L) * 4 + 8 +
-         (size_t)nw * 2 * (ns + 1) * 64 * sizeof(int32_t);
-}
-
-// Plans encode v9n takes: fixed fields, strings / binary and lists of non-bool fixed-width
-// items at any struct level; <= kV9nS structs, <= kV9nW bitmap words, one fixed batch
-// per wave, <= 2 var fields per wave.
-bool flat9n_fits(const VarLaunch& L, int nw) {
-  if (L.num_struct > kV9nS || L.num_var < 1 || L.num_var > 2 * nw || L.fix_group[4] < 1 ||
-      L.fix_group[4] > kFixBatch * nw || v9n_words(L) > kV9nW)
-    return false;
-  return !L.bool_items;
-}
-
-template <int HDR, int NW, int OWN, int NS>
-void launch_flat_enc9n_k(const VarLaunch& L0, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
-                         int cap, hipStream_t s) {
-  VarLaunch L = L0;
-  L.pl_all = 1;
-  auto* k = OWN == 1 && L.kn.var_enc == 11 ? &var_encode_flat9n_kernel<HDR, NW, OWN, NS, 33>
-                                           : &var_encode_flat9n_kernel<HDR, NW, OWN, NS, 17>;
-  const size_t lds = flat9n_lds(L, cap, NW, NS);
-  raise_lds_cap(k);
-  auto* k2 = &var_encode_flat_kernel<HDR, NW, NS != 0, true>;  // tiles beyond the image
-  L.stg_bytes = enc_stg_bytes(k2, L, capacity, cap, NW);
-  const SpillArgs sp = spill_args(L, cap);
-  (void)hipMemsetAsync(L.spill_count, 0, sizeof(int32_t), s);
-  var_diag(L, "encode v9n", k, 64 * NW, cap, 0, lds);
-  const unsigned grid = (unsigned)(((L.num_rows + 63) / 64 + 1) / 2);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(64 * NW), lds, s, L, L.prog, L.fix, L.vf, L.st, offs, out, capacity, status,
-                     cap, sp);
-  raise_lds_cap(k2);
-  hipLaunchKernelGGL(k2, dim3(spill_grid(k2, L, flat_lds_enc(L, sp.cap, NW), 64 * NW)), dim3(64 * NW),
-                     flat_lds_enc(L, sp.cap, NW), s, L, L.prog, L.cols, L.fix, L.vf, L.st, offs, out, capacity, status,
-                     sp.cap, sp);
-}
-
-template <int HDR, int NW>
-void launch_flat_enc9n(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
-                       int cap, hipStream_t s) {
-  const bool one = L.num_var <= NW;  // one var field per wave
-  if (L.num_struct) {
-    if (one) launch_flat_enc9n_k<HDR, NW, 1, kV9nS>(L, offs, out, capacity, status, cap, s);
-    else launch_flat_enc9n_k<HDR, NW, 2, kV9nS>(L, offs, out, capacity, status, cap, s);
-  } else {
-    if (one) launch_flat_enc9n_k<HDR, NW, 1, 0>(L, offs, out, capacity, status, cap, s);
-    else launch_flat_enc9n_k<HDR, NW, 2, 0>(L, offs, out, capacity, status, cap, s);
-  }
-}
-
 template <int HDR, int NW, bool NEST>
 void launch_flat_enc7_own(const VarLaunch& L, const int64_t* offs, uint8_t* out, int64_t capacity, int32_t* status,
                           int cap, hipStream_t s) {
@@ -4006,9 +3464,7 @@ void launch_flat_enc(const VarLaunch& L, const int64_t* offs, uint8_t* out, int6
   // force round 3 / v7 / v9 where they apply (the parity suite runs every one).
   const int e = L.kn.var_enc;
   const bool v7 = e != 1 && L.num_var <= kOwnVar * NW;
-  if ((e == 10 || e == 11) && flat9n_fits(L, NW)) {
-    launch_flat_enc9n<HDR, NW>(L, offs, out, capacity, status, cap, s);
-  } else if (L.num_struct) {
+  if (L.num_struct) {
     if (v7 && e == 7) launch_flat_enc7_own<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
     else launch_flat_enc_t<HDR, NW, true>(L, offs, out, capacity, status, cap, s);
   } else if ((e == 0 || e == 9) && flat9_fits(L, NW)) {

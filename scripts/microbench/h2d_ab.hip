@@ -3,7 +3,9 @@
 //   A: one hipMemcpyAsync per column (today's host_encode)
 //   B: one copy of the same bytes (upper bound of batching)
 //   C: a gather kernel reading the mapped host columns over PCIe (zero-copy)
-// Usage: h2d_ab [rows]  (prints GB/s of the H2D leg and of the concurrent D2H)
+// Usage: h2d_ab [rows] [reg]  (prints GB/s of the H2D leg and of the concurrent D2H;
+// reg: host buffers are malloc'd and hipHostRegister'd, as a caller's heap arrays are,
+// instead of hipHostMalloc'd)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -36,13 +38,23 @@ int main(int argc, char** argv) {
   const int64_t rows = argc > 1 ? atoll(argv[1]) : (1 << 20);
   const int ncol = 104;
   const size_t col_bytes = rows * 8, total = col_bytes * ncol;
+  const bool reg = argc > 2 && !strcmp(argv[2], "reg");
+  auto host_alloc = [&](void** p, size_t n) {
+    if (!reg) {
+      CK(hipHostMalloc(p, n, hipHostMallocDefault));
+      return;
+    }
+    *p = aligned_alloc(4096, (n + 4095) / 4096 * 4096);
+    memset(*p, 0, n);
+    CK(hipHostRegister(*p, n, hipHostRegisterMapped));
+  };
   std::vector<void*> h(ncol);
   for (int i = 0; i < ncol; ++i) {
-    CK(hipHostMalloc(&h[i], col_bytes, hipHostMallocDefault));
+    host_alloc(&h[i], col_bytes);
     memset(h[i], i, col_bytes);
   }
   void* hrows = nullptr;
-  CK(hipHostMalloc(&hrows, total + 16 * rows, hipHostMallocDefault));
+  host_alloc(&hrows, total + 16 * rows);
   void *dcols = nullptr, *drows = nullptr;
   CK(hipMalloc(&dcols, total));
   CK(hipMalloc(&drows, total + 16 * rows));
@@ -89,8 +101,9 @@ int main(int argc, char** argv) {
         if (t_in < best_in) best_in = t_in;
         if (duplex && t_out < best_out) best_out = t_out;
       }
-      printf("{\"mode\": \"%s\", \"duplex\": %d, \"h2d_ms\": %.3f, \"h2d_GBps\": %.1f, \"d2h_GBps\": %.1f}\n",
-             mode == 0 ? "per_column" : mode == 1 ? "one_copy" : "gather_kernel", duplex, best_in,
+      printf("{\"host\": \"%s\", \"mode\": \"%s\", \"duplex\": %d, \"h2d_ms\": %.3f, \"h2d_GBps\": %.1f, \"d2h_GBps\": %.1f}\n",
+             reg ? "registered" : "hipHostMalloc", mode == 0 ? "per_column" : mode == 1 ? "one_copy" : "gather_kernel",
+             duplex, best_in,
              total / best_in / 1e6, duplex ? out_bytes / best_out / 1e6 : 0.0);
     }
   }

@@ -286,6 +286,31 @@ def test_host_varlen_parity(name, n, frame, chunk):
     hp.close()
 
 
+@pytest.mark.parametrize("name,n,chunk", [("mixed40_nulls", 40009, 1 << 20), ("struct104", 20011, 8192),
+                                          ("nested_nulls", 60013, 16384)])
+def test_host_pageable_pieces_over_a_mib(name, n, chunk):
+    """Pageable caller memory with staged pieces of 1..4 MiB whose sizes the host copy
+    threads do not divide evenly: every byte crosses (round 5 lost the last n mod parts
+    bytes of such pieces -- tests/test_host_copy_pool.py)."""
+    schema, make = catalog()[name]
+    cols = make(n, 11)
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    hp = HostPipeline(NativePlan(schema), chunk_rows=chunk)
+    if name == "struct104":
+        out = np.zeros(expect.nbytes, np.uint8)
+        hp.encode(cols, n, 1, out)
+        dec = empty_like(schema, n)
+        hp.decode(expect, n, 1, dec)
+    else:
+        out, offs = hp.encode_var(cols, n, 1, np.zeros(expect.nbytes, np.uint8))
+        assert np.array_equal(offs, eoffs)
+        dec = hp.decode_var(expect, eoffs, n, 1)
+    bad = np.nonzero(out != expect)[0]
+    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+    assert columns_equal(schema, cols, dec) == []
+    hp.close()
+
+
 def test_host_varlen_collection_frames():
     for schema, cols in collection_cases(900, 21):
         n = cols[0].length
@@ -555,6 +580,17 @@ def direct_calls(hp):
     return f(hp.handle)
 
 
+def gather_calls(hp):
+    import ctypes
+    f = _internal("fory_rowfmt_internal_host_gather_calls", ctypes.c_int64, [ctypes.c_void_p])
+    return f(hp.handle)
+
+
+# registered fixed-width calls: one gather / scatter launch per chunk (default), or the
+# kernels on the host mappings themselves (FORY_ROWFMT_HOSTPATH=1, A/B)
+ZERO_COPY_PATHS = {"gather": ("0", gather_calls), "direct": ("1", direct_calls)}
+
+
 def paged_copy(a):
     """A copy of array a on whole pages of its own (+ the owning buffer)."""
     pb, raw = page_buffer(max(a.nbytes, 1))
@@ -562,14 +598,18 @@ def paged_copy(a):
     return pb, pb[:a.nbytes].view(a.dtype).reshape(a.shape)
 
 
+@pytest.mark.parametrize("path", sorted(ZERO_COPY_PATHS))
 @pytest.mark.parametrize("frame", [0, 1, 3])
 @pytest.mark.parametrize("n", [1, 64, 5003])
 @pytest.mark.parametrize("name", ["struct104", "struct104_boxed", "all_types"])
-def test_host_fixed_zero_copy(name, n, frame):
-    """Fixed-width plans with every column and the output registered: the kernels read the
-    host columns and write the host rows through their device mappings (one launch, no
-    chunk copies) -- the oracle's bytes; decode the same way back; a hash mismatch is
-    still ClassNotCompatibleException."""
+def test_host_fixed_zero_copy(name, n, frame, path, monkeypatch):
+    """Fixed-width plans with every column and the output registered: one gather launch per
+    chunk reads the column slices through their device mappings (decode: one scatter
+    launch writes them), or the kernels themselves read the host columns and write the
+    host rows (one launch per window, no chunk copies) -- the oracle's bytes; decode the
+    same way back; a hash mismatch is still ClassNotCompatibleException."""
+    knob, calls = ZERO_COPY_PATHS[path]
+    monkeypatch.setenv("FORY_ROWFMT_HOSTPATH", knob)
     schema, make = catalog()[name]
     cols = make(n, n + 19)
     expect, _ = oracle.encode(schema, cols, n, frame)
@@ -590,7 +630,7 @@ def test_host_fixed_zero_copy(name, n, frame):
         regs.append(out_whole)
         out = out_whole[:expect.nbytes]
         hp.encode(cols, n, frame, out)
-        assert direct_calls(hp) == 1 and staged_pieces(hp) == 0
+        assert calls(hp) == 1 and staged_pieces(hp) == 0
         bad = np.nonzero(out != expect)[0]
         assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
         dec = empty_like(schema, n)
@@ -603,7 +643,7 @@ def test_host_fixed_zero_copy(name, n, frame):
                     regs.append(whole)
                     setattr(c, attr, view)
         hp.decode(out, n, frame, dec)
-        assert direct_calls(hp) == 2
+        assert calls(hp) == 2 and staged_pieces(hp) == 0
         assert columns_equal(schema, cols, dec) == []
         if frame in (1, 3):
             out[(4 if frame == 1 else 0) + (n // 2) * plan.stride(frame)] ^= 1  # a frame's schema hash
@@ -614,9 +654,13 @@ def test_host_fixed_zero_copy(name, n, frame):
         hp.close()
 
 
-def test_host_fixed_zero_copy_falls_back_per_call():
-    """A window of a nullable plan that starts inside a validity byte, or a column left
-    pageable, takes the chunk pipeline: same bytes either way."""
+@pytest.mark.parametrize("path", sorted(ZERO_COPY_PATHS))
+def test_host_fixed_zero_copy_falls_back_per_call(path, monkeypatch):
+    """A column left pageable takes the per-slice copies, and (kernels on the mappings) a
+    window of a nullable plan that starts inside a validity byte takes the chunk pipeline:
+    same bytes either way."""
+    knob, calls = ZERO_COPY_PATHS[path]
+    monkeypatch.setenv("FORY_ROWFMT_HOSTPATH", knob)
     schema, make = catalog()["struct104_boxed"]
     n = 3001
     cols = make(n, 7)
@@ -638,14 +682,15 @@ def test_host_fixed_zero_copy_falls_back_per_call():
             host_register(w)
             regs.append(w)
         rows, nbytes = hp.encode_windows(cols, n, 1, [w1[:1003 * stride], w2[:(n - 1003) * stride]])
-        assert list(rows) == [1003, n - 1003] and direct_calls(hp) == 0
+        assert list(rows) == [1003, n - 1003] and calls(hp) == (1 if path == "gather" else 0)
         assert np.array_equal(np.concatenate([w1[:nbytes[0]], w2[:nbytes[1]]]), expect)
         host_unregister(regs.pop(0))  # one column pageable again
         out_whole, _ = paged_copy(np.zeros(expect.nbytes, np.uint8))
         host_register(out_whole)
         regs.append(out_whole)
         hp.encode(cols, n, 1, out_whole[:expect.nbytes])
-        assert direct_calls(hp) == 0 and np.array_equal(out_whole[:expect.nbytes], expect)
+        assert calls(hp) == (1 if path == "gather" else 0)
+        assert np.array_equal(out_whole[:expect.nbytes], expect)
     finally:
         unregister_all(regs)
         hp.close()

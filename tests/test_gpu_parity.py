@@ -43,9 +43,8 @@ VARLEN = [k for k, (sch, _) in catalog().items()
 FIXED = [k for k in catalog() if k not in VARLEN]
 
 
-@pytest.fixture(params=["flat", "flat_stg256", "flat_r3enc", "flat_v7", "flat_v9", "flat_v9_nocap", "flat_v9n",
-                        "flat_v9n_nocap", "flat_v9n_w4", "flat_v9n_ch33", "tile", "global", "spill", "nocap", "tile_nocap", "waves2",
-                        "waves4"])
+@pytest.fixture(params=["flat", "flat_stg256", "flat_r3enc", "flat_v7", "flat_v9", "flat_v9_nocap", "tile", "global",
+                        "spill", "nocap", "tile_nocap", "waves2", "waves4"])
 def varlen_engine(request, monkeypatch):
     """Varlen engines: flat cooperative tile kernels (default for flat plans), the
     generic one-wave tile interpreter (FORY_ROWFMT_VARFLAT=0), the per-record global
@@ -54,15 +53,10 @@ def varlen_engine(request, monkeypatch):
     inside the tile kernels (flat and generic); flat with a 256-byte staging buffer
     (most spans take the per-lane copy); cooperative tiles of 2 / 4 waves forced; flat
     plans encoded by the round-3 tile kernel (FORY_ROWFMT_VARENC=1), encode v7 (=7) and encode
-    v9 (=9; with 2 KiB images: its spill and per-record paths), encode v9n for struct / list plans (=10;
-    2 KiB images; 4 waves per tile)."""
+    v9 (=9; with 2 KiB images: its spill and per-record paths)."""
     env = {"flat": {}, "flat_stg256": {"FORY_ROWFMT_VARSTG": "256"}, "flat_r3enc": {"FORY_ROWFMT_VARENC": "1"},
            "flat_v7": {"FORY_ROWFMT_VARENC": "7"}, "flat_v9": {"FORY_ROWFMT_VARENC": "9"},
            "flat_v9_nocap": {"FORY_ROWFMT_VARENC": "9", "FORY_ROWFMT_VARCAP": "2048", "FORY_ROWFMT_SPILLCAP": "2048"},
-           "flat_v9n": {"FORY_ROWFMT_VARENC": "10"},
-           "flat_v9n_nocap": {"FORY_ROWFMT_VARENC": "10", "FORY_ROWFMT_VARCAP": "2048", "FORY_ROWFMT_SPILLCAP": "2048"},
-           "flat_v9n_w4": {"FORY_ROWFMT_VARENC": "10", "FORY_ROWFMT_VARNW": "4"},
-           "flat_v9n_ch33": {"FORY_ROWFMT_VARENC": "11"},
            "tile": {"FORY_ROWFMT_VARFLAT": "0"}, "global": {"FORY_ROWFMT_VARTILE": "0"},
            "spill": {"FORY_ROWFMT_VARCAP": "2048"},
            "nocap": {"FORY_ROWFMT_VARCAP": "2048", "FORY_ROWFMT_SPILLCAP": "2048"},
