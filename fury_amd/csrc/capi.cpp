@@ -997,8 +997,6 @@ void fory_rowfmt_internal_retire_stream(void* stream) {
 // Library-internal (host.cpp): shares last_error and the planner's column layout.
 int fory_rowfmt_internal_set_error(int code, const char* msg) { return fail(code, msg); }
 
-int fory_rowfmt_internal_host_path(const fory_plan* plan) { return plan->p.kn.host_path; }
-
 int fory_rowfmt_internal_column_layout(const fory_plan* plan, int32_t* width, int32_t* nullable) {
   const Plan& p = plan->p;
   for (size_t i = 0; i < p.nodes.size(); ++i) {
@@ -1183,8 +1181,12 @@ int fory_rowfmt_encode(const fory_plan* plan, const fory_column* cols, int64_t n
       for (size_t v = 0; v < plan->tc.var.size() && e == hipSuccess; ++v) {
         const int node = plan->tc.var[v].node;
         if (!tc_needs_pos(p, plan->tc.var[v])) continue;  // written by their parents
+        const int key = node + 1;  // a list's items / a map's keys, then its values (pre-order)
+        const bool cont = p.gnodes[node].kind == fory_amd::KIND_LIST || p.gnodes[node].kind == fory_amd::KIND_MAP;
+        const int kk = cont ? p.gnodes[key].kind : 0;
+        const int vk = p.gnodes[node].kind == fory_amd::KIND_MAP ? p.gnodes[p.gnodes[key].end].kind : 0;
         e = fory_amd::launch_tc_write_node(G, dT, node, T.m[node], out, out_capacity, d_status, s, p.nodes[node].kind,
-                                           (int)p.nodes[node].children.size());
+                                           (int)p.nodes[node].children.size(), kk, vk);
       }
       return e == hipSuccess ? FORY_OK : hip_fail(e, "tc_write");
     }

@@ -92,9 +92,10 @@ class CopyPool {
 
  private:
   static constexpr size_t kMinSplit = size_t(1) << 20;
+  static constexpr unsigned kMaxThreads = 15;  // a GPU's share of a host's cores (16 per MI355X)
   CopyPool() {
     const unsigned hw = std::thread::hardware_concurrency();
-    nthreads_ = (int)std::min<unsigned>(7, hw > 1 ? hw - 1 : 0);
+    nthreads_ = (int)std::min<unsigned>(kMaxThreads, hw > 1 ? hw - 1 : 0);
     for (int i = 0; i < nthreads_; ++i) threads_.emplace_back([this] { loop(); });
   }
   ~CopyPool() {
@@ -142,7 +143,7 @@ class CopyPool {
 };
 
 struct Staging {
-  static constexpr size_t kBlock = size_t(4) << 20;
+  static constexpr size_t kBlock = size_t(16) << 20;  // a staged piece: one pool-split memcpy + one DMA
   static constexpr int kBlocks = 8;
   uint8_t* mem = nullptr;  // kBlocks x kBlock, hipHostMalloc'd on first use
   hipEvent_t ev[kBlocks] = {};
@@ -150,16 +151,6 @@ struct Staging {
   struct Owed { uint8_t* dst = nullptr; size_t len = 0; } owed[kBlocks];  // D2H host copies pending
   int next = 0;
   int64_t pieces = 0;  // statistics: pieces staged over the context's life
-};
-
-// One column slice of a chunk between registered host memory (through its device
-// mapping) and the chunk buffer: bytes [a*width, (a+rows)*width) of the column, or
-// of its validity bitmap (bits = 1: [a/8, a/8 + (rows+7)/8)).
-struct ColSeg {
-  uint8_t* host;
-  uint8_t* dev;
-  int32_t width;
-  int32_t bits;
 };
 
 }  // namespace
@@ -196,10 +187,6 @@ struct fory_host_ctx {
   } vs[2];
   hipEvent_t ev_sz[2] = {};
   int32_t* vstatus = nullptr;  // one status word per slot (sticky over a call)
-  int64_t direct_calls = 0;    // fixed-width calls that took the zero-copy path
-  int64_t gather_calls = 0;    // fixed-width calls whose column slices moved by gather launches
-  int32_t host_path = 0;       // LaunchKnobs.host_path (FORY_ROWFMT_HOSTPATH, A/B)
-  ColSeg* segs[2] = {};        // device: each chunk buffer's gather table (2N entries)
   uint8_t* dbuf = nullptr;   // columns, row offsets, workspace, status
   int64_t dbuf_bytes = 0;
   uint8_t* drows = nullptr;  // rows / frames
@@ -233,7 +220,6 @@ int hip_check(hipError_t e, const char* what) {
 // Library-internal helpers of capi.cpp (not in the public header): last_error
 // is thread-local there; column widths/nullability of a fixed-width plan.
 extern "C" int fory_rowfmt_internal_set_error(int code, const char* msg);
-extern "C" int fory_rowfmt_internal_host_path(const fory_plan* plan);
 extern "C" void fory_rowfmt_internal_retire_stream(void* stream);
 extern "C" int fory_rowfmt_internal_column_layout(const fory_plan* plan, int32_t* width, int32_t* nullable);
 extern "C" int fory_rowfmt_internal_node_layout(const fory_plan* plan, int32_t* kind, int32_t* width,
@@ -243,9 +229,16 @@ namespace {
 
 int fail_host(int code, const std::string& msg) { return fory_rowfmt_internal_set_error(code, msg.c_str()); }
 
-// Ranges registered through fory_rowfmt_host_register (base -> bytes).
+// Ranges registered through fory_rowfmt_host_register: base -> (bytes, the device
+// address of base). Copies inside one of them find their mapping here, without the
+// four runtime pointer queries of mapped_range (each tens of microseconds: a chunk's
+// 104 column copies were issued ~110 us apart, the DMA idle in between).
+struct Reg {
+  size_t bytes;
+  uint8_t* dev;
+};
 std::mutex g_reg_mu;
-std::map<uintptr_t, size_t> g_regs;
+std::map<uintptr_t, Reg> g_regs;
 
 std::string hex(uintptr_t a) {
   char b[32];
@@ -279,6 +272,15 @@ bool pinned_range(const void* p, size_t bytes) { return mapped_range(p, bytes) !
 // conditions above), else nullptr.
 uint8_t* mapped_range(const void* p, size_t bytes) {
   if (!p || bytes == 0) return nullptr;
+  {  // inside a range this library registered: its mapping is known
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> lock(g_reg_mu);
+    auto it = g_regs.upper_bound(a);
+    if (it != g_regs.begin()) {
+      --it;
+      if (a >= it->first && a + bytes <= it->first + it->second.bytes) return it->second.dev + (a - it->first);
+    }
+  }
   const uint8_t* first = static_cast<const uint8_t*>(p);
   const uint8_t* last = first + (bytes - 1);
   hipPointerAttribute_t a{}, b{};
@@ -477,8 +479,6 @@ int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t c
   for (int i = 0; i < info.num_columns; ++i)
     per += align_up(c->width[i] * chunk_rows) + (c->nullable[i] ? align_up(validity_bytes(chunk_rows)) : 0);
   per += align_up(stride * chunk_rows) + align_up(c->ws_bytes) + kAlign;
-  per += align_up(2 * info.num_columns * (int64_t)sizeof(ColSeg));
-  c->host_path = fory_rowfmt_internal_host_path(plan);
   rc = hip_check(hipMalloc(&c->arena, (size_t)(2 * per)), "hipMalloc(host ctx chunk buffers)");
   if (rc) {
     delete c;
@@ -500,8 +500,6 @@ int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t c
     c->buf[b].ws = p;
     p += align_up(c->ws_bytes);
     c->buf[b].status = reinterpret_cast<int32_t*>(p);
-    p += kAlign;
-    c->segs[b] = reinterpret_cast<ColSeg*>(p);
   }
   rc = hip_check(hipMemset(c->arena, 0, (size_t)(2 * per)), "hipMemset");
   for (hipStream_t* s : {&c->s_in, &c->s_k, &c->s_out})
@@ -554,12 +552,23 @@ int fory_rowfmt_host_register(void* host_ptr, int64_t bytes) {
   // mapping bytes the other still counts on; copies are judged by whole ranges,
   // pinned_range). Ranges that only share a page are fine: each registration pins the page.
   for (const auto& r : g_regs)
-    if (b < r.first + r.second && r.first < e)
+    if (b < r.first + r.second.bytes && r.first < e)
       return fail_host(FORY_ERR_INVALID_ARGUMENT, "range overlaps a registered range at " + hex(r.first) + " (" +
-                                                      std::to_string(r.second) + " bytes)");
-  const int rc = hip_check(hipHostRegister(host_ptr, (size_t)bytes, hipHostRegisterDefault), "hipHostRegister");
-  if (!rc) g_regs[b] = (size_t)bytes;
-  return rc;
+                                                      std::to_string(r.second.bytes) + " bytes)");
+  int rc = hip_check(hipHostRegister(host_ptr, (size_t)bytes, hipHostRegisterDefault), "hipHostRegister");
+  if (rc) return rc;
+  // its device mapping, checked at both ends like mapped_range does for other memory
+  hipPointerAttribute_t a{}, z{};
+  const uint8_t* last = static_cast<const uint8_t*>(host_ptr) + (bytes - 1);
+  if (hipPointerGetAttributes(&a, host_ptr) != hipSuccess || hipPointerGetAttributes(&z, last) != hipSuccess ||
+      !a.devicePointer || !z.devicePointer ||
+      static_cast<const uint8_t*>(z.devicePointer) - static_cast<const uint8_t*>(a.devicePointer) != bytes - 1) {
+    (void)hipGetLastError();
+    (void)hipHostUnregister(host_ptr);
+    return fail_host(FORY_ERR_DEVICE, "registered range has no contiguous device mapping");
+  }
+  g_regs[b] = Reg{(size_t)bytes, static_cast<uint8_t*>(a.devicePointer)};
+  return FORY_OK;
 }
 
 int fory_rowfmt_host_unregister(void* host_ptr) {
@@ -569,7 +578,7 @@ int fory_rowfmt_host_unregister(void* host_ptr) {
   auto it = g_regs.find(b);
   if (it == g_regs.end())
     return fail_host(FORY_ERR_INVALID_ARGUMENT, "not the start of a range fory_rowfmt_host_register registered");
-  const size_t bytes = it->second;
+  const size_t bytes = it->second.bytes;
   int rc = hip_check(hipHostUnregister(host_ptr), "hipHostUnregister");
   if (rc) return rc;  // (still registered: kept in the table)
   g_regs.erase(it);
@@ -638,168 +647,6 @@ int d2h_rows_windows(fory_host_ctx* c, const OutWindows& W, const uint8_t* src, 
   return rc;
 }
 
-constexpr int kSegPiece = 64 * 1024;  // bytes of one segment per workgroup
-constexpr int kSegThreads = 256;
-constexpr int kSegDeep = 4;  // 16-byte loads in flight per lane
-
-// Moves one chunk's column slices between registered host memory and the chunk
-// buffer in ONE launch: blockIdx.y = slice, blockIdx.x = 64 KiB piece of it. Each
-// workgroup streams a contiguous piece (page-sequential host accesses: the host
-// mapping's translations stay hot), 16-byte moves when both ends are 16-byte aligned.
-__global__ __launch_bounds__(kSegThreads) void seg_copy_kernel(const ColSeg* __restrict__ segs, int64_t a,
-                                                               int64_t rows, int32_t to_dev) {
-  const ColSeg sg = segs[blockIdx.y];
-  const int64_t off = sg.bits ? (a >> 3) : a * sg.width;
-  const int64_t bytes = sg.bits ? ((rows + 7) >> 3) : rows * sg.width;
-  const int64_t p0 = (int64_t)blockIdx.x * kSegPiece;
-  if (p0 >= bytes) return;
-  const int64_t p1 = p0 + kSegPiece < bytes ? p0 + kSegPiece : bytes;
-  const uint8_t* s = to_dev ? sg.host + off : sg.dev;
-  uint8_t* d = to_dev ? sg.dev : sg.host + off;
-  const int64_t lane = threadIdx.x;
-  int64_t q = p0;
-  if (((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {
-    constexpr int64_t kRound = 16 * kSegThreads * kSegDeep;
-    for (; q + kRound <= p1; q += kRound) {
-      uint4 r[kSegDeep];
-#pragma unroll
-      for (int u = 0; u < kSegDeep; ++u)
-        r[u] = *reinterpret_cast<const uint4*>(s + q + (u * kSegThreads + lane) * 16);
-#pragma unroll
-      for (int u = 0; u < kSegDeep; ++u) *reinterpret_cast<uint4*>(d + q + (u * kSegThreads + lane) * 16) = r[u];
-    }
-    const int64_t v1 = q + ((p1 - q) & ~(int64_t)15);
-    for (int64_t t = q + lane * 16; t < v1; t += 16 * kSegThreads)
-      *reinterpret_cast<uint4*>(d + t) = *reinterpret_cast<const uint4*>(s + t);
-    q = v1;
-  }
-  for (int64_t t = q + lane; t < p1; t += kSegThreads) d[t] = s[t];
-}
-
-// Gather tables of a fixed-width call: when every column (and the validity of the
-// nullable ones the caller passed) is registered over its whole range, each chunk
-// buffer's table of slices goes to the device once per call and *nseg is set;
-// *nseg = 0: not registered (the per-slice copies run).
-int gather_setup(fory_host_ctx* c, const fory_column* h, int64_t n, int* nseg, int32_t* maxw) {
-  *nseg = 0;
-  *maxw = 1;
-  if (c->host_path != 0) return FORY_OK;
-  const int N = c->info.num_columns;
-  std::vector<ColSeg> t[2];
-  for (int i = 0; i < N; ++i) {
-    uint8_t* v = mapped_range(h[i].values, (size_t)(n * c->width[i]));
-    if (!v) return FORY_OK;
-    for (int b = 0; b < 2; ++b) t[b].push_back(ColSeg{v, c->buf[b].cols[i].values, c->width[i], 0});
-    *maxw = std::max(*maxw, c->width[i]);
-    if (c->nullable[i] && h[i].validity) {
-      uint8_t* m = mapped_range(h[i].validity, (size_t)((n + 7) / 8));
-      if (!m) return FORY_OK;
-      for (int b = 0; b < 2; ++b) t[b].push_back(ColSeg{m, c->buf[b].cols[i].validity, 1, 1});
-    }
-  }
-  for (int b = 0; b < 2; ++b) {
-    const int rc = hip_check(hipMemcpy(c->segs[b], t[b].data(), t[b].size() * sizeof(ColSeg), hipMemcpyHostToDevice),
-                             "hipMemcpy(gather table)");
-    if (rc) return rc;
-  }
-  *nseg = (int)t[0].size();
-  ++c->gather_calls;
-  return FORY_OK;
-}
-
-int launch_seg_copy(fory_host_ctx* c, int b, int nseg, int32_t maxw, int64_t a, int64_t rows, int to_dev,
-                    hipStream_t s) {
-  const int64_t pieces = (rows * maxw + kSegPiece - 1) / kSegPiece;
-  seg_copy_kernel<<<dim3((unsigned)pieces, (unsigned)nseg), kSegThreads, 0, s>>>(c->segs[b], a, rows, to_dev);
-  return hip_check(hipGetLastError(), to_dev ? "gather launch" : "scatter launch");
-}
-
-// Zero copy for fixed-width plans. When every column (values, and the validity of
-// nullable fields) and every output window is registered over its whole range, the
-// encode kernel itself reads the columns and writes the rows through their device
-// mappings -- PCIe in both directions at once, one launch per window, no chunk copies.
-// Round 4 measured the chunk pipeline at 26 GiB/s: its 104 column copies per chunk ran
-// as 104 runtime blit-kernel launches each. Returns -1 (not taken: the chunk pipeline
-// runs) when a range is not registered, a window's device address is not 16-byte
-// aligned, or a window of a plan with validity starts inside a validity byte.
-int host_encode_direct(fory_host_ctx* c, const fory_column* h, int64_t n, int32_t frame, int64_t stride,
-                       const OutWindows& W) {
-  if (c->host_path != 1) return -1;
-  const int N = c->info.num_columns;
-  std::vector<uint8_t*> val((size_t)N), vld((size_t)N, nullptr);
-  bool any_validity = false;
-  for (int i = 0; i < N; ++i) {
-    val[(size_t)i] = mapped_range(h[i].values, (size_t)(n * c->width[i]));
-    if (!val[(size_t)i]) return -1;
-    if (c->nullable[i] && h[i].validity) {
-      vld[(size_t)i] = mapped_range(h[i].validity, (size_t)((n + 7) / 8));
-      if (!vld[(size_t)i]) return -1;
-      any_validity = true;
-    }
-  }
-  const size_t nw = W.cap.size();
-  std::vector<uint8_t*> dst(nw, nullptr);
-  for (size_t w = 0; w < nw; ++w) {
-    const int64_t f0 = W.first[w], rows = W.first[w + 1] - f0;
-    if (rows <= 0) continue;
-    dst[w] = mapped_range(W.ptr[w], (size_t)(rows * stride));
-    if (!dst[w] || (reinterpret_cast<uintptr_t>(dst[w]) & 15) || (any_validity && (f0 & 7))) return -1;
-  }
-  int rc = hip_check(hipMemsetAsync(c->buf[0].status, 0, 4, c->s_k), "hipMemsetAsync");
-  std::vector<fory_column> dcols((size_t)N);
-  for (size_t w = 0; w < nw && !rc; ++w) {
-    const int64_t f0 = W.first[w], f1 = W.first[w + 1];
-    // launches of <= chunk rows (the context's workspace; chunk is a multiple of 64)
-    for (int64_t a = f0; a < f1 && !rc; a += c->chunk) {
-      const int64_t rows = std::min(c->chunk, f1 - a);
-      for (int i = 0; i < N; ++i)
-        dcols[(size_t)i] = fory_column{val[(size_t)i] + a * c->width[i], nullptr,
-                                       vld[(size_t)i] ? vld[(size_t)i] + a / 8 : nullptr, rows, rows * c->width[i]};
-      rc = fory_rowfmt_encode(c->plan, dcols.data(), rows, frame, nullptr, dst[w] + (a - f0) * stride, rows * stride,
-                              c->buf[0].status, c->buf[0].ws, c->ws_bytes, c->s_k);
-    }
-  }
-  const int rs = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize(kernels)");
-  if (rc) return rc;
-  if (rs) return rs;
-  ++c->direct_calls;
-  return fory_rowfmt_read_status(c->buf[0].status, c->s_k);
-}
-
-// The decode's zero copy: rows and every output column registered over their whole
-// ranges -> one decode launch reading the rows and writing the columns in host memory.
-int host_decode_direct(fory_host_ctx* c, const uint8_t* rows_h, int64_t n, int32_t frame, int64_t stride,
-                       const fory_column* h) {
-  if (c->host_path != 1) return -1;
-  const int N = c->info.num_columns;
-  uint8_t* rows = mapped_range(rows_h, (size_t)(n * stride));
-  if (!rows || (reinterpret_cast<uintptr_t>(rows) & 15)) return -1;
-  std::vector<uint8_t*> val((size_t)N), vld((size_t)N, nullptr);
-  for (int i = 0; i < N; ++i) {
-    val[(size_t)i] = mapped_range(h[i].values, (size_t)(n * c->width[i]));
-    if (!val[(size_t)i]) return -1;
-    if (c->nullable[i] && h[i].validity) {
-      vld[(size_t)i] = mapped_range(h[i].validity, (size_t)((n + 7) / 8));
-      if (!vld[(size_t)i]) return -1;
-    }
-  }
-  int rc = hip_check(hipMemsetAsync(c->buf[0].status, 0, 4, c->s_k), "hipMemsetAsync");
-  std::vector<fory_column> dcols((size_t)N);
-  for (int64_t a = 0; a < n && !rc; a += c->chunk) {  // launches of <= chunk rows
-    const int64_t m = std::min(c->chunk, n - a);
-    for (int i = 0; i < N; ++i)
-      dcols[(size_t)i] = fory_column{val[(size_t)i] + a * c->width[i], nullptr,
-                                     vld[(size_t)i] ? vld[(size_t)i] + a / 8 : nullptr, m, m * c->width[i]};
-    rc = fory_rowfmt_decode(c->plan, rows + a * stride, nullptr, m, frame, dcols.data(), c->buf[0].status,
-                            c->buf[0].ws, c->ws_bytes, c->s_k);
-  }
-  const int rs = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize(kernels)");
-  if (rc) return rc;
-  if (rs) return rs;
-  ++c->direct_calls;
-  return fory_rowfmt_read_status(c->buf[0].status, c->s_k);
-}
-
 int host_encode_fixed(fory_host_ctx* c, const fory_column* host_cols, int64_t n, int32_t frame, OutWindows* W) {
   if (c->varlen) return fail_host(FORY_ERR_INVALID_ARGUMENT, "varlen plan: use fory_rowfmt_host_encode_var");
   if (frame != FORY_FRAME_RAW && frame != FORY_FRAME_STREAM && frame != FORY_FRAME_HASHED)
@@ -816,11 +663,6 @@ int host_encode_fixed(fory_host_ctx* c, const fory_column* host_cols, int64_t n,
       return fail_host(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(i) + " missing or shorter than num_rows");
   rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
-  const int direct = host_encode_direct(c, host_cols, n, frame, stride, *W);
-  if (direct >= 0) return direct;
-  int nseg = 0;
-  int32_t maxw = 1;
-  rc = gather_setup(c, host_cols, n, &nseg, &maxw);
   for (int b = 0; b < 2 && !rc; ++b)
     rc = hip_check(hipMemsetAsync(c->buf[b].status, 0, 4, c->s_k), "hipMemsetAsync");
   const int64_t chunks = (n + c->chunk - 1) / c->chunk;
@@ -832,12 +674,10 @@ int host_encode_fixed(fory_host_ctx* c, const fory_column* host_cols, int64_t n,
     fory_host_ctx::Buf& B = c->buf[b];
     // H2D: column slices (+ validity bytes) into buffer b once chunk k-2's kernel is done with it
     if (k >= 2) rc = hip_check(hipStreamWaitEvent(c->s_in, c->ev_k[b], 0), "hipStreamWaitEvent");
-    if (!rc && nseg) rc = launch_seg_copy(c, b, nseg, maxw, a, rows, 1, c->s_in);
     for (int i = 0; i < c->info.num_columns && !rc; ++i) {
       const fory_column& h = host_cols[i];
       dcols[i] = fory_column{B.cols[i].values, nullptr, (c->nullable[i] && h.validity) ? B.cols[i].validity : nullptr,
                              rows, rows * c->width[i]};
-      if (nseg) continue;
       rc = hcopy(c, B.cols[i].values, static_cast<const uint8_t*>(h.values) + a * c->width[i], (size_t)(rows * c->width[i]), hipMemcpyHostToDevice, c->s_in, "H2D");
       if (!rc && c->nullable[i] && h.validity)
         rc = hcopy(c, B.cols[i].validity, h.validity + a / 8, (size_t)((rows + 7) / 8), hipMemcpyHostToDevice, c->s_in, "H2D validity");
@@ -899,11 +739,6 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
   }
   int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
-  const int direct = host_decode_direct(c, static_cast<const uint8_t*>(host_rows), n, frame, stride, host_out_cols);
-  if (direct >= 0) return direct;
-  int nseg = 0;
-  int32_t maxw = 1;
-  rc = gather_setup(c, host_out_cols, n, &nseg, &maxw);
   for (int b = 0; b < 2 && !rc; ++b)
     rc = hip_check(hipMemsetAsync(c->buf[b].status, 0, 4, c->s_k), "hipMemsetAsync");
   const int64_t chunks = (n + c->chunk - 1) / c->chunk;
@@ -928,8 +763,7 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
                                      c->s_k);
     if (!rc) rc = hip_check(hipEventRecord(c->ev_k[b], c->s_k), "hipEventRecord");
     if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_out, c->ev_k[b], 0), "hipStreamWaitEvent");
-    if (!rc && nseg) rc = launch_seg_copy(c, b, nseg, maxw, a, rows, 0, c->s_out);
-    for (int i = 0; i < c->info.num_columns && !rc && !nseg; ++i) {
+    for (int i = 0; i < c->info.num_columns && !rc; ++i) {
       const fory_column& h = host_out_cols[i];
       rc = hcopy(c, static_cast<uint8_t*>(h.values) + a * c->width[i], B.cols[i].values, (size_t)(rows * c->width[i]), hipMemcpyDeviceToHost, c->s_out, "D2H");
       if (!rc && dcols[i].validity)
@@ -1827,12 +1661,10 @@ extern "C" int fory_rowfmt_internal_host_copy_path(const void* p, int64_t bytes)
 }
 
 extern "C" int64_t fory_rowfmt_internal_host_staged_pieces(const fory_host_ctx* c) { return c ? c->stage.pieces : -1; }
-extern "C" int64_t fory_rowfmt_internal_host_direct_calls(const fory_host_ctx* c) { return c ? c->direct_calls : -1; }
 // The staged copies' host memcpy (CopyPool), for a CPU test of its split.
 extern "C" void fory_rowfmt_internal_pool_copy(void* dst, const void* src, int64_t n) {
   CopyPool::get().copy(dst, src, (size_t)n);
 }
-extern "C" int64_t fory_rowfmt_internal_host_gather_calls(const fory_host_ctx* c) { return c ? c->gather_calls : -1; }
 
 // Library-internal, for tests: round 2's classification (the first byte's attribute
 // only), kept to show the straddling-range hazard it had next to pinned_range's answer.

@@ -192,8 +192,11 @@ hipError_t launch_tc_size_scan(const GenLaunch& L, const TcTables* T, int node, 
 // instances (node, m = its instance count), parents before children.
 hipError_t launch_tc_write_rows(const GenLaunch& L, const TcTables* T, int nroot, const int64_t* offs, uint8_t* out,
                                 int64_t capacity, int32_t* status, hipStream_t s);
+// kind / nchild: the node's; key_kind / val_kind: a list's item kind (a map's key and
+// value kinds), for the container kernel's instantiation
 hipError_t launch_tc_write_node(const GenLaunch& L, const TcTables* T, int node, int64_t m, uint8_t* out,
-                                int64_t capacity, int32_t* status, hipStream_t s, int kind, int nchild);
+                                int64_t capacity, int32_t* status, hipStream_t s, int kind, int nchild, int key_kind,
+                                int val_kind);
 
 // Columnar decode (treedec.hip): per-node passes over instances, field-major for rows and
 // beans, item-parallel for lists / maps. Positions of the bean / list / map instances:

@@ -117,7 +117,6 @@ LaunchKnobs knobs_from_env() {
   k.var_xcd = num("FORY_ROWFMT_VARXCD", 0);
   k.dec_regs = num("FORY_ROWFMT_DECREGS", 0);
   k.tree_col = num("FORY_ROWFMT_TREECOL", 1);
-  k.host_path = num("FORY_ROWFMT_HOSTPATH", 0);
   return k;
 }
 

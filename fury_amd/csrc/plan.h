@@ -166,9 +166,6 @@ struct LaunchKnobs {
   int32_t var_xcd;   // FORY_ROWFMT_VARXCD=C: varlen tile kernels take tiles in XCD runs of C (-1: one run per XCD), 0 = dispatch order
   int32_t dec_regs;  // FORY_ROWFMT_DECREGS=1: varlen decode stages its tile rows through registers, not LDS-DMA (A/B)
   int32_t tree_col;  // FORY_ROWFMT_TREECOL: 0 = tree-engine encode per lane only; else the columnar engine when the workspace allows
-  int32_t host_path; // FORY_ROWFMT_HOSTPATH (A/B, registered host memory, fixed-width plans): 0 = one
-                     // column-gather launch per chunk, 1 = the kernels read / write host memory directly,
-                     // 2 = one runtime copy per column slice
 };
 LaunchKnobs knobs_from_env();
 

@@ -643,7 +643,7 @@ __device__ __forceinline__ void tc_bitmap(uint8_t* dst, const uint8_t* validity,
     uint32_t bits = 0;
     if (rem > 0 && validity) {  // the 32 bits from bit b: one or two aligned dwords (Arrow pads to 8 bytes)
       const int64_t b = o0 + 32LL * w;
-      const uint32_t* v = reinterpret_cast<const uint32_t*>(validity) + (b >> 5);
+      const GAS uint32_t* v = gp(reinterpret_cast<const uint32_t*>(validity)) + (b >> 5);
       const int sh = (int)(b & 31);
       const int take = rem < 32 ? (int)rem : 32;
       uint64_t win = v[0];
@@ -740,45 +740,149 @@ __device__ __forceinline__ int32_t tc_element(const GenLaunch& L, const TcTables
   return 0;
 }
 
-// Lists / maps: a workgroup per kTcWG containers. Headers lane per container, then the
-// elements item-parallel over the workgroup's items.
-template <bool MAP>  // per container kind: a list's instantiation carries no value-array path
+// Item classes of a container node's items / keys / values (the plan's, from the host):
+// scalars, strings, beans / lists / maps (positioned: their own pass writes them), and
+// decimals (the generic element path).
+constexpr int kTcScalar = 0, kTcStr = 1, kTcPos = 2, kTcOther = 3;
+constexpr int kTcU = 4;  // items per lane whose inputs are in flight together
+
+// One element's inputs, loaded before any is used. The loads are unconditional (an
+// absent validity reads a dummy byte), so the compiler's counted waits stay exact and
+// kTcU items' loads overlap.
+struct TcIn {
+  uint32_t vb;     // the validity byte holding the item's bit
+  uint64_t v;      // scalar: the value
+  int64_t a0, a1;  // string / positioned: the items' scanned sizes A[e], A[e + 1]
+  int32_t s0, s1;  // string: its Arrow offsets
+};
+
+template <int CLS>
+__device__ __forceinline__ void tc_in_load(const GNode& it, const ColumnDev& col, const int64_t* A, int64_t e,
+                                           const uint8_t* dummy, TcIn& in) {
+  in.vb = *gp((it.flags & 1) && col.validity ? col.validity + (e >> 3) : dummy);
+  if (CLS == kTcScalar) {
+    in.v = load_elem(col.values, elem_size(it), e);
+  } else if (CLS == kTcStr || CLS == kTcPos) {
+    in.a0 = gp(A)[e];
+    in.a1 = gp(A)[e + 1];
+    if (CLS == kTcStr) {
+      in.s0 = gp(col.offsets)[e];
+      in.s1 = gp(col.offsets)[e + 1];
+    }
+  }
+}
+
+// Element e (item q = e - o0 of n) of the array at Pa from its loaded inputs: the
+// same bytes as tc_element. ab: A[x][o0] of the container (string / positioned items).
+template <int CLS>
+__device__ __forceinline__ int32_t tc_el_store(const GenLaunch& L, const TcTables* T, uint8_t* out, int64_t cap,
+                                               int x, const GNode& it, const ColumnDev& col, int64_t o0, int64_t n,
+                                               int64_t Pa, int64_t ab, int64_t e, const TcIn& in) {
+  if (CLS == kTcOther) return tc_element(L, T, out, cap, x, o0, n, Pa, e);
+  const int es = elem_size(it);
+  const int64_t hb = 8 + gbm(n);
+  uint8_t* el = out + Pa + hb + (e - o0) * es;
+  const bool isnull = (it.flags & 1) && col.validity && !((in.vb >> (e & 7)) & 1);
+  if (isnull) {  // null: zero element (the header set the bit)
+    tc_put(el, 0, es);
+    if (CLS == kTcPos) gp(T->P[x])[e] = -1;
+    return 0;
+  }
+  if (CLS == kTcScalar) {
+    tc_put(el, it.kind == KIND_BOOL ? (in.v ? 1 : 0) : in.v, es);
+    return 0;
+  }
+  const int64_t S = in.a1 - in.a0;
+  const int64_t at = Pa + hb + gr8(n * 8) + (in.a0 - ab);
+  if (S < 0 || at + S > cap) {
+    tc_put(el, 0, 8);
+    if (CLS == kTcPos) gp(T->P[x])[e] = -1;
+    return FORY_ERR_ENCODER;
+  }
+  if (CLS == kTcPos) {
+    tc_put(el, ((uint64_t)(at - Pa) << 32) | (uint32_t)S, 8);
+    gp(T->P[x])[e] = at;
+    return 0;
+  }
+  const int64_t len = (int64_t)in.s1 - in.s0;  // writeUnaligned + zeroOutPaddingBytes
+  tc_put(el, ((uint64_t)(at - Pa) << 32) | (uint32_t)len, 8);
+  if (len < 0 || gr8(len) != S) return FORY_ERR_ENCODER;
+  tc_copy(out + at, col.values + in.s0, len);
+  return 0;
+}
+
+// Lists / maps: a workgroup per kTcWG containers. (1) lane per container: its position and
+// item range; (2) the first kTcU items of every lane issue their inputs' loads together with
+// the container headers' (array sizes, validity windows), and the headers are written; (3)
+// the elements item-parallel, kTcU per lane per round, each finding its container by a
+// binary search over the workgroup's item starts in LDS. KC / VC: the item (key) / value
+// classes, so each instantiation carries only its items' paths.
+template <bool MAP, int KC, int VC>
 __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const TcTables* __restrict__ T, int c,
                                                               int64_t m, uint8_t* __restrict__ out, int64_t cap,
                                                               int32_t* status) {
-  __shared__ int64_t sP[kTcWG];   // container position (-1: absent / null / does not fit)
+  __shared__ int64_t sP[kTcWG];      // container position (-1: absent / null / does not fit)
   __shared__ int32_t sO[kTcWG + 1];  // first item of each container (+ the end)
-  __shared__ int32_t sK[kTcWG];   // maps: key array bytes
+  __shared__ int32_t sK[kTcWG];      // maps: key array bytes
+  __shared__ int64_t sAk[kTcWG], sAv[kTcWG];  // A[key][o0], A[val][o0]: the items' sizes before the container's
   const int tid = threadIdx.x;
   const int64_t j0 = (int64_t)blockIdx.x * kTcWG;
   const int cnt = m - j0 < kTcWG ? (int)(m - j0) : kTcWG;
   constexpr bool map = MAP;
   const int key = c + 1, val = map ? L.nodes[key].end : key;  // (val: maps only)
+  const GNode kit = L.nodes[key], vit = L.nodes[val];
+  const ColumnDev kcol = L.cols[key], vcol = L.cols[val];
+  const int64_t* Ak = T->A[key];
+  const int64_t* Av = T->A[val];
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(T);
+  constexpr bool kvar = KC != kTcScalar, vvar = MAP && VC != kTcScalar;
   const int64_t mx = T->m[key];
   int32_t err = 0;
+  int64_t P = -1, o0 = 0, o1 = 0;
   if (tid < cnt) {
     const int64_t j = j0 + tid;
-    int64_t o0, o1;
-    int64_t P = gp(T->P[c])[j];
+    P = gp(T->P[c])[j];
     // offsets past the items' column length (a short fory_column.length): an error, not a
     // silently shorter array (present containers only: absent ones read no items)
     if (!tc_items(L, T, c, j, &o0, &o1) && P >= 0) err = FORY_ERR_INVALID_ARGUMENT;
+    sO[tid] = (int32_t)o0;
+    if (tid == cnt - 1) sO[cnt] = (int32_t)o1;
+  }
+  __syncthreads();
+  const int64_t e0 = sO[0], e1 = sO[cnt];
+  TcIn ki[kTcU], vi[kTcU];
+  auto load_round = [&](int64_t r0) {
+#pragma unroll
+    for (int u = 0; u < kTcU; ++u) {
+      const int64_t e = r0 + tid + u * kTcWG;
+      const int64_t ee = e < e1 ? e : e0;  // (past the end: a readable item, unused)
+      tc_in_load<KC>(kit, kcol, Ak, ee, dummy, ki[u]);
+      if (map) tc_in_load<VC>(vit, vcol, Av, ee, dummy, vi[u]);
+    }
+  };
+  if (e1 > e0) load_round(e0);
+  if (tid < cnt) {
     const int64_t n = o1 - o0;
-    int64_t kb = 0;
-    // the items' validity windows, loaded with the array sizes (the bitmaps need them next)
-    const TcVwin vk = tc_vwin((L.nodes[key].flags & 1) ? L.cols[key].validity : nullptr, o0, o1);
-    const TcVwin vv = map ? tc_vwin((L.nodes[val].flags & 1) ? L.cols[val].validity : nullptr, o0, o1) : TcVwin{};
-    if (P >= 0) {
-      const int64_t need = map ? 8 + tc_array_bytes(L, T, key, o0, o1) + tc_array_bytes(L, T, val, o0, o1)
-                               : tc_array_bytes(L, T, key, o0, o1);
-      if (P + need > cap) {
-        err = FORY_ERR_ENCODER;
-        P = -1;
-      }
+    // the header's inputs: the items' validity windows and scanned sizes
+    const TcVwin vk = tc_vwin((kit.flags & 1) ? kcol.validity : nullptr, o0, o1);
+    const TcVwin vv = map ? tc_vwin((vit.flags & 1) ? vcol.validity : nullptr, o0, o1) : TcVwin{};
+    int64_t ak0 = 0, ak1 = 0, av0 = 0, av1 = 0;
+    if (kvar) {
+      ak0 = gp(Ak)[o0];
+      ak1 = gp(Ak)[o1];
+    }
+    if (vvar) {
+      av0 = gp(Av)[o0];
+      av1 = gp(Av)[o1];
+    }
+    const int64_t kb = 8 + gbm(n) + gr8(n * elem_size(kit)) + (ak1 - ak0);  // tc_array_bytes
+    const int64_t vb = map ? 8 + gbm(n) + gr8(n * elem_size(vit)) + (av1 - av0) : 0;
+    if (P >= 0 && P + (map ? 8 + kb + vb : kb) > cap) {
+      err = FORY_ERR_ENCODER;
+      P = -1;
     }
     if (P >= 0) {
       if (map) {  // [i64 key array bytes][key array][value array]
-        kb = tc_array_bytes(L, T, key, o0, o1);
         tc_put(out + P, (uint64_t)kb, 8);
         tc_array_head(L, out, key, o0, n, P + 8, vk);
         tc_array_head(L, out, val, o0, n, P + 8 + kb, vv);
@@ -787,47 +891,49 @@ __global__ __launch_bounds__(kTcWG) void tc_write_cont_kernel(GenLaunch L, const
       }
     }
     sP[tid] = P;
-    sO[tid] = (int32_t)o0;
     sK[tid] = (int32_t)kb;
-    if (tid == cnt - 1) sO[cnt] = (int32_t)o1;
+    sAk[tid] = ak0;
+    sAv[tid] = av0;
   }
   __syncthreads();
-  const int64_t e0 = sO[0], e1 = sO[cnt];
-  const bool kvar = tc_has_pos(L.nodes[key].kind), vvar = map && tc_has_pos(L.nodes[val].kind);
-  for (int64_t e = e0 + tid; e < e1; e += kTcWG) {
-    int a = 0, b = cnt - 1;  // the last container whose items start at or before e
-    while (a < b) {
-      const int mid = (a + b + 1) >> 1;
-      if (sO[mid] <= e) a = mid;
-      else b = mid - 1;
+  for (int64_t r0 = e0; r0 < e1; r0 += kTcU * kTcWG) {
+    if (r0 != e0) load_round(r0);
+#pragma unroll
+    for (int u = 0; u < kTcU; ++u) {
+      const int64_t e = r0 + tid + u * kTcWG;
+      if (e >= e1) break;
+      int a = 0, b = cnt - 1;  // the last container whose items start at or before e
+      while (a < b) {
+        const int mid = (a + b + 1) >> 1;
+        if (sO[mid] <= e) a = mid;
+        else b = mid - 1;
+      }
+      const int64_t Pa = sP[a];
+      const int64_t ao = sO[a], n = sO[a + 1] - ao;
+      if (Pa < 0 || e >= ao + n) {  // absent container (or items between non-adjacent ranges)
+        if (KC == kTcPos) gp(T->P[key])[e] = -1;
+        if (map && VC == kTcPos) gp(T->P[val])[e] = -1;
+        continue;
+      }
+      int32_t r = tc_el_store<KC>(L, T, out, cap, key, kit, kcol, ao, n, map ? Pa + 8 : Pa, sAk[a], e, ki[u]);
+      if (map) {
+        const int32_t r2 = tc_el_store<VC>(L, T, out, cap, val, vit, vcol, ao, n, Pa + 8 + sK[a], sAv[a], e, vi[u]);
+        if (!r) r = r2;
+      }
+      if (r) err = r;
     }
-    const int64_t P = sP[a];
-    const int64_t o0 = sO[a], n = sO[a + 1] - o0;
-    if (P < 0 || e >= o0 + n) {  // absent container (or items between non-adjacent ranges)
-      if (kvar) gp(T->P[key])[e] = -1;
-      if (vvar) gp(T->P[val])[e] = -1;
-      continue;
-    }
-    int32_t r;
-    if (map) {
-      r = tc_element(L, T, out, cap, key, o0, n, P + 8, e);
-      const int32_t r2 = tc_element(L, T, out, cap, val, o0, n, P + 8 + sK[a], e);
-      if (!r) r = r2;
-    } else {
-      r = tc_element(L, T, out, cap, key, o0, n, P, e);
-    }
-    if (r) err = r;
   }
   // items no container of the call references: no position
-  if (blockIdx.x == 0 && (kvar || vvar))
+  constexpr bool kpos = KC == kTcPos, vpos = MAP && VC == kTcPos;
+  if (blockIdx.x == 0 && (kpos || vpos))
     for (int64_t e = tid; e < e0; e += kTcWG) {
-      if (kvar) gp(T->P[key])[e] = -1;
-      if (vvar) gp(T->P[val])[e] = -1;
+      if (kpos) gp(T->P[key])[e] = -1;
+      if (vpos) gp(T->P[val])[e] = -1;
     }
-  if (j0 + cnt == m && (kvar || vvar))
+  if (j0 + cnt == m && (kpos || vpos))
     for (int64_t e = e1 + tid; e < mx; e += kTcWG) {
-      if (kvar) gp(T->P[key])[e] = -1;
-      if (vvar) gp(T->P[val])[e] = -1;
+      if (kpos) gp(T->P[key])[e] = -1;
+      if (vpos) gp(T->P[val])[e] = -1;
     }
   if (err) set_status(status, err);
 }
@@ -892,11 +998,49 @@ hipError_t launch_tc_write_rows(const GenLaunch& L, const TcTables* T, int nroot
   return hipGetLastError();
 }
 
+// tc_write_cont_kernel's instantiation for item (key) class kc and value class vc.
+template <bool MAP, int KC>
+auto* tc_cont_kernel_v(int vc) {
+  switch (vc) {
+    case kTcScalar: return &tc_write_cont_kernel<MAP, KC, kTcScalar>;
+    case kTcStr: return &tc_write_cont_kernel<MAP, KC, kTcStr>;
+    case kTcPos: return &tc_write_cont_kernel<MAP, KC, kTcPos>;
+    default: return &tc_write_cont_kernel<MAP, KC, kTcOther>;
+  }
+}
+
+auto* tc_cont_kernel_map(int kc, int vc) {
+  switch (kc) {
+    case kTcScalar: return tc_cont_kernel_v<true, kTcScalar>(vc);
+    case kTcStr: return tc_cont_kernel_v<true, kTcStr>(vc);
+    case kTcPos: return tc_cont_kernel_v<true, kTcPos>(vc);
+    default: return tc_cont_kernel_v<true, kTcOther>(vc);
+  }
+}
+
+auto* tc_cont_kernel_list(int kc) {  // (the value class is unused: one instantiation per item class)
+  switch (kc) {
+    case kTcScalar: return &tc_write_cont_kernel<false, kTcScalar, kTcScalar>;
+    case kTcStr: return &tc_write_cont_kernel<false, kTcStr, kTcScalar>;
+    case kTcPos: return &tc_write_cont_kernel<false, kTcPos, kTcScalar>;
+    default: return &tc_write_cont_kernel<false, kTcOther, kTcScalar>;
+  }
+}
+
+int tc_item_class(int kind) {
+  return kind == KIND_FIXED || kind == KIND_BOOL ? kTcScalar
+         : kind == KIND_BYTES                    ? kTcStr
+         : kind == KIND_DECIMAL                  ? kTcOther
+                                                 : kTcPos;
+}
+
 hipError_t launch_tc_write_node(const GenLaunch& L, const TcTables* T, int node, int64_t m, uint8_t* out,
-                                int64_t capacity, int32_t* status, hipStream_t s, int kind, int nchild) {
+                                int64_t capacity, int32_t* status, hipStream_t s, int kind, int nchild, int key_kind,
+                                int val_kind) {
   if (m <= 0) return hipSuccess;
   if (kind == KIND_LIST || kind == KIND_MAP) {
-    hipLaunchKernelGGL(kind == KIND_MAP ? tc_write_cont_kernel<true> : tc_write_cont_kernel<false>,
+    const int kc = tc_item_class(key_kind), vc = tc_item_class(val_kind);
+    hipLaunchKernelGGL(kind == KIND_MAP ? tc_cont_kernel_map(kc, vc) : tc_cont_kernel_list(kc),
                        dim3((unsigned)((m + kTcWG - 1) / kTcWG)), dim3(kTcWG), 0, s, L, T, node, m, out, capacity,
                        status);
   } else {

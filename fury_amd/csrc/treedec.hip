@@ -31,6 +31,7 @@ namespace {
 
 constexpr int kTdWG = 256;
 constexpr int kTdBatch = 4;
+constexpr int kTdU = 2;  // item groups per lane whose loads are in flight together (td_items_kernel)
 constexpr int kTdStageMax = 264;  // bitmap + slots of up to 32 fields staged per lane  // fields whose slot words an instance loads together
 
 __device__ __forceinline__ bool td_leaf(int kind) { return kind == KIND_BYTES || kind == KIND_DECIMAL; }
@@ -374,54 +375,90 @@ __global__ __launch_bounds__(kTdWG) void td_items_kernel(GenLaunch L, const TdTa
   }
   __syncthreads();
   const int64_t e0 = sO[0], e1 = sO[cnt];
-  const int ends = map ? 2 : 1;
-  // waves walk 64-aligned groups of items (uniform trip count: validity by ballot)
-  for (int64_t eb = e0 & ~int64_t(63); eb < e1; eb += kTdWG) {
-    const int64_t e = eb + tid;
-    const bool inr_all = e >= e0 && e < e1;
-    int a = 0;
-    if (inr_all) {
-      int b = cnt - 1;  // the last container whose items start at or before e
-      while (a < b) {
-        const int mid = (a + b + 1) >> 1;
-        if (sO[mid] <= e) a = mid;
-        else b = mid - 1;
+  constexpr int ends = map ? 2 : 1;
+  // waves walk 64-aligned groups of items (uniform trip count: validity by ballot), kTdU
+  // groups per round: every item's null byte and element of the round are loaded (both
+  // unconditionally, an absent item's from the rows' first bytes) before any is used
+  struct ItemIn {
+    int64_t arr;
+    bool inr, present;
+    uint32_t nb;  // the null byte holding the item's bit
+    uint64_t sv;  // its element (a null item's is read and dropped)
+  };
+  for (int64_t r0 = e0 & ~int64_t(63); r0 < e1; r0 += kTdU * kTdWG) {
+    int A[kTdU];
+    int64_t Q[kTdU];
+    ItemIn I[kTdU][ends];
+#pragma unroll
+    for (int u = 0; u < kTdU; ++u) {
+      const int64_t e = r0 + u * kTdWG + tid;
+      const bool inr_all = e >= e0 && e < e1;
+      int a = 0;
+      if (inr_all) {
+        int b = cnt - 1;  // the last container whose items start at or before e
+        while (a < b) {
+          const int mid = (a + b + 1) >> 1;
+          if (sO[mid] <= e) a = mid;
+          else b = mid - 1;
+        }
+      }
+      const int64_t n = sO[a + 1] - sO[a], q = e - sO[a];
+      A[u] = a, Q[u] = q;
+#pragma unroll
+      for (int w = 0; w < ends; ++w) {
+        const int x = w ? val : key;
+        const GNode it = L.nodes[x];
+        ItemIn& in = I[u][w];
+        in.inr = inr_all && e < T->m[x];
+        in.arr = in.inr ? (w ? sV[a] : sK[a]) : -1;
+        in.present = in.arr >= 0 && q < n;
+        const int64_t nat = in.present ? in.arr + 8 + (q >> 3) : 0;
+        const int64_t eat = in.present ? in.arr + 8 + gbm(n) + q * elem_size(it) : 0;
+        in.nb = rows[nat];
+        in.sv = gget(rows + eat, elem_size(it));
       }
     }
-    const int64_t n = sO[a + 1] - sO[a], q = e - sO[a];
-    for (int w = 0; w < ends; ++w) {
-      const int x = w ? val : key;
-      const GNode it = L.nodes[x];
-      const ColumnDev ic = L.cols[x];
-      // an item past its output column's length (a short fory_column.length): nothing is
-      // written for it (its arrays end there) and the call reports FORY_ERR_CAPACITY
-      const bool inr = inr_all && e < T->m[x];
-      if (inr_all && !inr && (level < 0 || it.cdepth == level || !is_scalar(it.kind)))
-        set_status(status, FORY_ERR_CAPACITY);
-      const int64_t arr = inr ? (w ? sV[a] : sK[a]) : -1;
-      const bool present = arr >= 0 && q < n;
-      const bool isnull = !present || ((rows[arr + 8 + (q >> 3)] >> (q & 7)) & 1);
-      if ((level < 0 || it.cdepth == level) && (it.flags & 1) && ic.out_validity)
-        td_valid_words(ic.out_validity, e, inr, !isnull);
-      const int es = elem_size(it);
-      const uint64_t sv = isnull ? 0 : gget(rows + arr + 8 + gbm(n) + q * es, es);
-      if (FLAT && (it.flags & kGNodeFlatBean)) {  // a bean of leaf fields: read here, no pass of its own
-        int64_t P = -1;
-        if (!isnull) {  // BinaryArray.getStruct: the child row at the element's offset
-          const int64_t rel = (int32_t)(sv >> 32);
-          if (rel < 0 || arr + rel + gbm(it.nchild) + 8LL * it.nchild > sE[a]) set_status(status, FORY_ERR_CORRUPT);
-          else P = arr + rel;
+#pragma unroll
+    for (int u = 0; u < kTdU; ++u) {
+      const int64_t e = r0 + u * kTdWG + tid;
+      const bool inr_all = e >= e0 && e < e1;
+      const int a = A[u];
+      const int64_t q = Q[u];
+#pragma unroll
+      for (int w = 0; w < ends; ++w) {
+        const int x = w ? val : key;
+        const GNode it = L.nodes[x];
+        const ColumnDev ic = L.cols[x];
+        const ItemIn& in = I[u][w];
+        // an item past its output column's length (a short fory_column.length): nothing is
+        // written for it (its arrays end there) and the call reports FORY_ERR_CAPACITY
+        const bool inr = in.inr;
+        if (inr_all && !inr && (level < 0 || it.cdepth == level || !is_scalar(it.kind)))
+          set_status(status, FORY_ERR_CAPACITY);
+        const int64_t arr = in.arr;
+        const bool present = in.present;
+        const bool isnull = !present || ((in.nb >> (q & 7)) & 1);
+        if ((level < 0 || it.cdepth == level) && (it.flags & 1) && ic.out_validity)
+          td_valid_words(ic.out_validity, e, inr, !isnull);
+        const uint64_t sv = isnull ? 0 : in.sv;
+        if (FLAT && (it.flags & kGNodeFlatBean)) {  // a bean of leaf fields: read here, no pass of its own
+          int64_t P = -1;
+          if (!isnull) {  // BinaryArray.getStruct: the child row at the element's offset
+            const int64_t rel = (int32_t)(sv >> 32);
+            if (rel < 0 || arr + rel + gbm(it.nchild) + 8LL * it.nchild > sE[a]) set_status(status, FORY_ERR_CORRUPT);
+            else P = arr + rel;
+          }
+          td_instance(L, T, it.nchild, T->kid0[x], gbm(it.nchild), e, inr, P, P < 0 ? 0 : sE[a], rows, status);
+          continue;
         }
-        td_instance(L, T, it.nchild, T->kid0[x], gbm(it.nchild), e, inr, P, P < 0 ? 0 : sE[a], rows, status);
-        continue;
+        if (!inr) continue;
+        if (is_scalar(it.kind)) {
+          if ((level < 0 || it.cdepth == level) && ic.out_values) td_scalar(it, ic, e, sv, isnull);
+          continue;
+        }
+        if (!present && td_leaf(it.kind)) continue;
+        td_value(L, T, x, it, ic, e, rows, sv, present ? arr : 0, sE[a], isnull, level, status);
       }
-      if (!inr) continue;
-      if (is_scalar(it.kind)) {
-        if ((level < 0 || it.cdepth == level) && ic.out_values) td_scalar(it, ic, e, sv, isnull);
-        continue;
-      }
-      if (!present && td_leaf(it.kind)) continue;
-      td_value(L, T, x, it, ic, e, rows, sv, present ? arr : 0, sE[a], isnull, level, status);
     }
   }
 }

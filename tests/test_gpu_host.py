@@ -574,23 +574,6 @@ def test_host_register_refuses_overlaps_and_foreign_bases():
     host_unregister(b)
 
 
-def direct_calls(hp):
-    import ctypes
-    f = _internal("fory_rowfmt_internal_host_direct_calls", ctypes.c_int64, [ctypes.c_void_p])
-    return f(hp.handle)
-
-
-def gather_calls(hp):
-    import ctypes
-    f = _internal("fory_rowfmt_internal_host_gather_calls", ctypes.c_int64, [ctypes.c_void_p])
-    return f(hp.handle)
-
-
-# registered fixed-width calls: one gather / scatter launch per chunk (default), or the
-# kernels on the host mappings themselves (FORY_ROWFMT_HOSTPATH=1, A/B)
-ZERO_COPY_PATHS = {"gather": ("0", gather_calls), "direct": ("1", direct_calls)}
-
-
 def paged_copy(a):
     """A copy of array a on whole pages of its own (+ the owning buffer)."""
     pb, raw = page_buffer(max(a.nbytes, 1))
@@ -598,18 +581,14 @@ def paged_copy(a):
     return pb, pb[:a.nbytes].view(a.dtype).reshape(a.shape)
 
 
-@pytest.mark.parametrize("path", sorted(ZERO_COPY_PATHS))
 @pytest.mark.parametrize("frame", [0, 1, 3])
 @pytest.mark.parametrize("n", [1, 64, 5003])
 @pytest.mark.parametrize("name", ["struct104", "struct104_boxed", "all_types"])
-def test_host_fixed_zero_copy(name, n, frame, path, monkeypatch):
-    """Fixed-width plans with every column and the output registered: one gather launch per
-    chunk reads the column slices through their device mappings (decode: one scatter
-    launch writes them), or the kernels themselves read the host columns and write the
-    host rows (one launch per window, no chunk copies) -- the oracle's bytes; decode the
-    same way back; a hash mismatch is still ClassNotCompatibleException."""
-    knob, calls = ZERO_COPY_PATHS[path]
-    monkeypatch.setenv("FORY_ROWFMT_HOSTPATH", knob)
+def test_host_fixed_registered(name, n, frame):
+    """Fixed-width plans with every column (values and validity) and the output registered
+    on pages of their own: every column slice and row piece is one DMA (nothing staged),
+    the oracle's bytes; decode the same way back; a hash mismatch is still
+    ClassNotCompatibleException."""
     schema, make = catalog()[name]
     cols = make(n, n + 19)
     expect, _ = oracle.encode(schema, cols, n, frame)
@@ -630,7 +609,7 @@ def test_host_fixed_zero_copy(name, n, frame, path, monkeypatch):
         regs.append(out_whole)
         out = out_whole[:expect.nbytes]
         hp.encode(cols, n, frame, out)
-        assert calls(hp) == 1 and staged_pieces(hp) == 0
+        assert staged_pieces(hp) == 0
         bad = np.nonzero(out != expect)[0]
         assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
         dec = empty_like(schema, n)
@@ -643,7 +622,7 @@ def test_host_fixed_zero_copy(name, n, frame, path, monkeypatch):
                     regs.append(whole)
                     setattr(c, attr, view)
         hp.decode(out, n, frame, dec)
-        assert calls(hp) == 2 and staged_pieces(hp) == 0
+        assert staged_pieces(hp) == 0
         assert columns_equal(schema, cols, dec) == []
         if frame in (1, 3):
             out[(4 if frame == 1 else 0) + (n // 2) * plan.stride(frame)] ^= 1  # a frame's schema hash
@@ -654,13 +633,9 @@ def test_host_fixed_zero_copy(name, n, frame, path, monkeypatch):
         hp.close()
 
 
-@pytest.mark.parametrize("path", sorted(ZERO_COPY_PATHS))
-def test_host_fixed_zero_copy_falls_back_per_call(path, monkeypatch):
-    """A column left pageable takes the per-slice copies, and (kernels on the mappings) a
-    window of a nullable plan that starts inside a validity byte takes the chunk pipeline:
-    same bytes either way."""
-    knob, calls = ZERO_COPY_PATHS[path]
-    monkeypatch.setenv("FORY_ROWFMT_HOSTPATH", knob)
+def test_host_fixed_registered_windows_and_a_pageable_column():
+    """Registered output windows that split a validity byte, then one column left pageable
+    (its slices staged, the others one DMA each): the same bytes either way."""
     schema, make = catalog()["struct104_boxed"]
     n = 3001
     cols = make(n, 7)
@@ -682,14 +657,14 @@ def test_host_fixed_zero_copy_falls_back_per_call(path, monkeypatch):
             host_register(w)
             regs.append(w)
         rows, nbytes = hp.encode_windows(cols, n, 1, [w1[:1003 * stride], w2[:(n - 1003) * stride]])
-        assert list(rows) == [1003, n - 1003] and calls(hp) == (1 if path == "gather" else 0)
+        assert list(rows) == [1003, n - 1003] and staged_pieces(hp) == 0
         assert np.array_equal(np.concatenate([w1[:nbytes[0]], w2[:nbytes[1]]]), expect)
         host_unregister(regs.pop(0))  # one column pageable again
         out_whole, _ = paged_copy(np.zeros(expect.nbytes, np.uint8))
         host_register(out_whole)
         regs.append(out_whole)
         hp.encode(cols, n, 1, out_whole[:expect.nbytes])
-        assert calls(hp) == (1 if path == "gather" else 0)
+        assert staged_pieces(hp) > 0
         assert np.array_equal(out_whole[:expect.nbytes], expect)
     finally:
         unregister_all(regs)

@@ -21,7 +21,7 @@ ALLOWED = {
     "FORY_ROWFMT_VARTILE", "FORY_ROWFMT_VARFLAT", "FORY_ROWFMT_VARCAP", "FORY_ROWFMT_VARFIT",
     "FORY_ROWFMT_VARSTG", "FORY_ROWFMT_SPILLCAP", "FORY_ROWFMT_VARNW", "FORY_ROWFMT_SIZES_PROGRAM",
     "FORY_ROWFMT_IDXFRAMES", "FORY_ROWFMT_VARPROF", "FORY_ROWFMT_VARDIAG", "FORY_ROWFMT_VARENC",
-    "FORY_ROWFMT_VARXCD", "FORY_ROWFMT_DECREGS", "FORY_ROWFMT_TREECOL", "FORY_ROWFMT_HOSTPATH",
+    "FORY_ROWFMT_VARXCD", "FORY_ROWFMT_DECREGS", "FORY_ROWFMT_TREECOL",
 }
 
 
