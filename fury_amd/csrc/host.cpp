@@ -16,6 +16,9 @@
 #include <map>
 #include <cstdio>
 #include <cstring>
+#if defined(__x86_64__)
+#include <emmintrin.h>
+#endif
 #include <string>
 #include <condition_variable>
 #include <mutex>
@@ -51,6 +54,33 @@ struct Slice {  // one column's device chunk buffers
 // Host memcpy of the staged copies, split over a small process-wide pool of threads: a
 // pageable buffer's bytes cross host memory twice (caller <-> pinned block), and one thread
 // copying them held the staged path at ~29 GB/s of PCIe (round 4).
+// memcpy with non-temporal 16-byte stores: a staged piece is written once and read by
+// the DMA engine (or by nobody on the host again), so the stores skip the caches'
+// read-for-ownership; fenced before returning (the DMA that follows must see them).
+void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+#if defined(__x86_64__) && defined(__SSE2__)
+  if (n >= 4096) {
+    const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
+    std::memcpy(dst, src, head);
+    size_t i = head;
+    for (; i + 64 <= n; i += 64) {
+      const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+      const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+      const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+      const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    }
+    std::memcpy(dst + i, src + i, n - i);
+    _mm_sfence();
+    return;
+  }
+#endif
+  std::memcpy(dst, src, n);
+}
+
 class CopyPool {
  public:
   static CopyPool& get() {
@@ -109,7 +139,7 @@ class CopyPool {
   void run_part(int k) {
     const size_t per = ((n_ + parts_ - 1) / parts_ + 63) & ~size_t(63);  // parts x per >= n
     const size_t a = std::min(n_, per * (size_t)k), b = std::min(n_, a + per);
-    if (b > a) std::memcpy(dst_ + a, src_ + a, b - a);
+    if (b > a) stream_copy(dst_ + a, src_ + a, b - a);
   }
   void loop() {
     uint64_t seen = 0;
@@ -142,9 +172,15 @@ class CopyPool {
   uint64_t gen_ = 0;
 };
 
+#ifndef FORY_STAGE_BLOCK_MB  // (build-time A/B of the staging geometry)
+#define FORY_STAGE_BLOCK_MB 16
+#endif
+#ifndef FORY_STAGE_BLOCKS
+#define FORY_STAGE_BLOCKS 8
+#endif
 struct Staging {
-  static constexpr size_t kBlock = size_t(16) << 20;  // a staged piece: one pool-split memcpy + one DMA
-  static constexpr int kBlocks = 8;
+  static constexpr size_t kBlock = size_t(FORY_STAGE_BLOCK_MB) << 20;  // a staged piece: one pool-split memcpy + one DMA
+  static constexpr int kBlocks = FORY_STAGE_BLOCKS;
   uint8_t* mem = nullptr;  // kBlocks x kBlock, hipHostMalloc'd on first use
   hipEvent_t ev[kBlocks] = {};
   bool inflight[kBlocks] = {};  // ev recorded, completion not yet observed
@@ -272,6 +308,7 @@ bool pinned_range(const void* p, size_t bytes) { return mapped_range(p, bytes) !
 // conditions above), else nullptr.
 uint8_t* mapped_range(const void* p, size_t bytes) {
   if (!p || bytes == 0) return nullptr;
+#ifndef FORY_AB_MAPPING_QUERIES  // (build-time A/B: -D it to resolve every copy by runtime queries, as round 4)
   {  // inside a range this library registered: its mapping is known
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     std::lock_guard<std::mutex> lock(g_reg_mu);
@@ -281,6 +318,7 @@ uint8_t* mapped_range(const void* p, size_t bytes) {
       if (a >= it->first && a + bytes <= it->first + it->second.bytes) return it->second.dev + (a - it->first);
     }
   }
+#endif
   const uint8_t* first = static_cast<const uint8_t*>(p);
   const uint8_t* last = first + (bytes - 1);
   hipPointerAttribute_t a{}, b{};

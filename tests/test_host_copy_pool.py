@@ -20,11 +20,13 @@ def pool_copy():
 
 @pytest.mark.parametrize("n", [0, 1, 63, 1 << 20, (1 << 20) + 5, 8 * 64 * 2048 + 5, (1 << 20) * 3 + 7,
                                (4 << 20) - 3, 4 << 20, 8 * 64 * 8192 + 7, 4194303])
-def test_pool_copy_moves_every_byte(n):
+@pytest.mark.parametrize("dst_off,src_off", [(0, 0), (3, 0), (0, 5), (7, 9)])
+def test_pool_copy_moves_every_byte(n, dst_off, src_off):
+    """(non-temporal 16-byte stores from any source alignment into any destination alignment)"""
     f = pool_copy()
     rng = np.random.default_rng(n)
     src = rng.integers(0, 256, n + 64, dtype=np.uint8)
     dst = np.zeros(n + 64, np.uint8)
-    f(dst.ctypes.data, src.ctypes.data, n)
-    assert np.array_equal(dst[:n], src[:n])
-    assert not dst[n:].any()  # nothing past the piece
+    f(dst.ctypes.data + dst_off, src.ctypes.data + src_off, n)
+    assert np.array_equal(dst[dst_off:dst_off + n], src[src_off:src_off + n])
+    assert not dst[:dst_off].any() and not dst[dst_off + n:].any()  # nothing outside the piece
