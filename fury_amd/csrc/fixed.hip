@@ -237,9 +237,15 @@ __device__ __forceinline__ void v5_issue(const uint8_t* const (&ptr)[K], const i
 // Nullable schemas (NUL): the tile's null masks per slot are in LDS (mt[slot], bit r:
 // record r of the tile is null, from the Arrow validity words v5_masks loaded); a null
 // record's slot is written 0, its bit set by v5_bitmaps.
+// The records of a 4- or 8-byte chunk go into the image starting at record
+// (c >> rot) mod E (c: the lane's chunk in the field, E records per chunk), so the
+// lanes of one LDS store instruction spread over the banks: at Struct104's raw stride
+// (848 B = 212 dwords) the in-order writes of a 4-byte field put a 16-lane store group on
+// 4 banks (v5_rotation picks rot per plan from the store grouping).
 template <int R, int K, int HDR, bool NUL = false>
 __device__ __forceinline__ void v5_write(uint8_t* lds, int stride, int hdr_bm, const int (&wk)[K],
-                                         const uint32_t (&sf)[K], const u32x4 (&d)[K], const uint64_t* mt) {
+                                         const uint32_t (&sf)[K], const u32x4 (&d)[K], const uint64_t* mt,
+                                         int rot4, int rot8) {
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int w = wk[k];
@@ -251,13 +257,23 @@ __device__ __forceinline__ void v5_write(uint8_t* lds, int stride, int hdr_bm, c
     uint8_t* row = lds + rb * stride;
     const u32x4 x = d[k];
     if (w == 8) {
-      put_slot_nb<HDR>(row, hdr_bm, slot, (uint64_t)x.x | ((uint64_t)x.y << 32), nul(0), flags);
-      put_slot_nb<HDR>(row + stride, hdr_bm, slot, (uint64_t)x.z | ((uint64_t)x.w << 32), nul(1), flags);
+      const bool s = ((rb >> 1) >> rot8) & 1;  // the chunk's records in order 1, 0
+      const uint32_t a0 = s ? x.z : x.x, a1 = s ? x.w : x.y, b0 = s ? x.x : x.z, b1 = s ? x.y : x.w;
+      uint8_t* ra = row + (s ? stride : 0);
+      put_slot_nb<HDR>(ra, hdr_bm, slot, (uint64_t)a0 | ((uint64_t)a1 << 32), nul(s), flags);
+      put_slot_nb<HDR>(row + (s ? 0 : stride), hdr_bm, slot, (uint64_t)b0 | ((uint64_t)b1 << 32), nul(!s), flags);
     } else if (w == 4) {
-      put_slot_nb<HDR>(row, hdr_bm, slot, x.x, nul(0), flags);
-      put_slot_nb<HDR>(row + stride, hdr_bm, slot, x.y, nul(1), flags);
-      put_slot_nb<HDR>(row + 2 * stride, hdr_bm, slot, x.z, nul(2), flags);
-      put_slot_nb<HDR>(row + 3 * stride, hdr_bm, slot, x.w, nul(3), flags);
+      const int s = ((rb >> 2) >> rot4) & 3;  // the chunk's records from record s, wrapping
+      // the dwords rotated by s in place (by 2, then by 1): y[e] = x[(e + s) & 3]
+      const bool h = s & 2, o = s & 1;
+      const uint32_t p0 = h ? x.z : x.x, p1 = h ? x.w : x.y, p2 = h ? x.x : x.z, p3 = h ? x.y : x.w;
+      const uint32_t y0 = o ? p1 : p0, y1 = o ? p2 : p1, y2 = o ? p3 : p2, y3 = o ? p0 : p3;
+      uint8_t* r0 = row + s * stride;
+      const int wrap = 4 * stride;
+      put_slot_nb<HDR>(r0, hdr_bm, slot, y0, nul(s), flags);
+      put_slot_nb<HDR>(r0 + stride - (s >= 3 ? wrap : 0), hdr_bm, slot, y1, nul((s + 1) & 3), flags);
+      put_slot_nb<HDR>(r0 + 2 * stride - (s >= 2 ? wrap : 0), hdr_bm, slot, y2, nul((s + 2) & 3), flags);
+      put_slot_nb<HDR>(r0 + 3 * stride - (s >= 1 ? wrap : 0), hdr_bm, slot, y3, nul((s + 3) & 3), flags);
     } else if constexpr (NUL) {  // 2- and 1-byte fields, rolled (the dword of record e picked by selects)
       const int E = 16 / w;
 #pragma unroll 1
@@ -303,6 +319,41 @@ __device__ __forceinline__ void v5_store(const FixedLaunch& L, uint8_t* lds, uin
     __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(lds + c * 16), gp(reinterpret_cast<u32x4*>(dst + c * 16)));
   const int tail4 = (bytes & 15) >> 2;
   if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
+}
+
+// LDS store cycles of one v5_write field chunk step over a wave (64 lanes: fields of
+// 4 w chunks each, consecutive slots) for a record rotation shift `rot` -- ds_write_b64
+// (4 groups of 16 lanes, 2 dwords each) or, in stream frames (4-byte aligned slots), two
+// ds_write_b32 (2 groups of 32), banks (address / 4) mod 32 (MI355X_MICROARCH.md, LDS).
+// read: the decode's d5_columns instead -- per record a ds_read_b32 of its null-bitmap
+// word and one per value dword (2 groups of 32 lanes, banks (address / 4) mod 32).
+int v5_store_cycles(int stride, int hdr, int hdr_bm, int w, int rot, bool read = false) {
+  const int lpf = 4 * w, E = 16 / w;
+  int total = 0;
+  for (int e = 0; e < E; ++e) {
+    int64_t addr[64];
+    for (int l = 0; l < 64; ++l) {
+      const int f = l / lpf, c = l % lpf;
+      const int q = (e + (rot >= 31 ? 0 : (c >> rot))) % E;
+      addr[l] = (int64_t)(c * E + q) * stride + hdr_bm + 8 * f;
+    }
+    const bool b32 = read || hdr == 12;
+    const int groups = b32 ? 2 : 4, gl = 64 / groups;
+    const int reads = read ? 1 + w / 4 : (hdr == 12 ? 2 : 1);  // instructions per step
+    for (int d = 0; d < reads; ++d)
+      for (int g = 0; g < groups; ++g) {
+        int load[32] = {0};
+        for (int l = g * gl; l < (g + 1) * gl; ++l) {
+          // (read: instruction 0 is the bitmap word, at the row start + hdr)
+          const int64_t a = read && d == 0 ? addr[l] - hdr_bm - 8 * (l / lpf) + hdr : addr[l] + 4 * (read ? d - 1 : d);
+          for (int dw = 0; dw < (b32 ? 1 : 2); ++dw) ++load[(a / 4 + dw) % 32];
+        }
+        int mx = 0;
+        for (int b = 0; b < 32; ++b) mx = load[b] > mx ? load[b] : mx;
+        total += mx;
+      }
+  }
+  return total;
 }
 
 // XCD-grouped tile order: workgroups are dispatched round-robin over the 8 XCDs
@@ -410,7 +461,7 @@ __device__ __forceinline__ void encode_v5_body(const FixedLaunch& L, const Fixed
   const int nbw = L.bitmap_bytes >> 2;
   // stage of set X (tile t, masks in table bx); the other set's masks go into table by
   auto stage = [&](u32x4 (&d)[K], uint64_t& m, int bx, uint64_t mo, int by) {
-    v5_write<R, K, HDR, NUL>(lds, stride, hdr_bm, wk, sf, d, mtab + bx * nmask);
+    v5_write<R, K, HDR, NUL>(lds, stride, hdr_bm, wk, sf, d, mtab + bx * nmask, L.rot4, L.rot8);
     if constexpr (NUL) v5_bitmaps<HDR>(lds, stride, nbw, mtab + bx * nmask, wave, lane);
     __syncthreads();
     put_masks(mo, by);  // (loaded a stage ago; only the other set's chunks are younger)
@@ -629,7 +680,8 @@ __device__ __forceinline__ void d5_validity(const uint8_t* lds, int stride, int 
 
 template <int R, int K2, int HDR>
 __device__ __forceinline__ void d5_columns(const uint8_t* lds, int stride, int hdr_bm, const int (&wk)[K2],
-                                           const uint32_t (&sf)[K2], uint8_t* const (&optr)[K2], int64_t r0) {
+                                           const uint32_t (&sf)[K2], uint8_t* const (&optr)[K2], int64_t r0,
+                                           int rot4, int rot8) {
 #pragma unroll
   for (int k = 0; k < K2; ++k) {
     if (!(sf[k] & (1u << 20))) continue;
@@ -645,11 +697,19 @@ __device__ __forceinline__ void d5_columns(const uint8_t* lds, int stride, int h
       return w == 8 ? ((uint64_t)ld32(p) | ((uint64_t)ld32(p + 4) << 32)) : (uint64_t)ld32(p);
     };
     u32x4 x;
-    if (w == 8) {
-      const uint64_t a = val(0), b = val(1);
-      x = u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
-    } else if (w == 4) {
-      x = u32x4{(uint32_t)val(0), (uint32_t)val(1), (uint32_t)val(2), (uint32_t)val(3)};
+    if (w == 8) {  // the chunk's records read in order 1, 0 on lanes with s (LDS bank spread, v5_rotation)
+      const bool s = ((rb >> 1) >> rot8) & 1;
+      const uint64_t a = val(s ? 1 : 0), b = val(s ? 0 : 1);
+      const uint64_t v0 = s ? b : a, v1 = s ? a : b;
+      x = u32x4{(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32)};
+    } else if (w == 4) {  // records read from record s, wrapping; y[e] = record (e + s) & 3
+      const int s = ((rb >> 2) >> rot4) & 3;
+      const uint32_t y0 = (uint32_t)val(s), y1 = (uint32_t)val((s + 1) & 3), y2 = (uint32_t)val((s + 2) & 3),
+                     y3 = (uint32_t)val((s + 3) & 3);
+      // x[j] = y[(j - s) & 3]: rotate back by s (by 2, then by 1)
+      const bool h = s & 2, o = s & 1;
+      const uint32_t p0 = h ? y2 : y0, p1 = h ? y3 : y1, p2 = h ? y0 : y2, p3 = h ? y1 : y3;
+      x = u32x4{o ? p3 : p0, o ? p0 : p1, o ? p1 : p2, o ? p2 : p3};
     } else {
       // 2- and 1-byte fields: one dword (2 or 4 records) per iteration of a rolled
       // loop, placed by selects; unrolled, the 16 records' LDS reads were all hoisted
@@ -738,7 +798,7 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
     d5_write<K>(lds, tid, n16, WG, d);
     __syncthreads();
     if (HDR && tid < R) check_frame<HDR>(lds + tid * stride, L, status);
-    d5_columns<R, K2, HDR>(lds, stride, hdr_bm, wk, sf, optr, mt(t) * R);
+    d5_columns<R, K2, HDR>(lds, stride, hdr_bm, wk, sf, optr, mt(t) * R, L.drot4, L.drot8);
     if constexpr (NUL) d5_validity<HDR>(lds, stride, nbits, vo, mt(t), wave, lane);
     d5_issue<R, K>(in, mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, d);
     __syncthreads();
@@ -889,6 +949,17 @@ hipError_t decode_hdr(const FixedLaunch& L, const uint8_t* in, int32_t* status, 
 }
 
 }  // namespace
+
+// v5_write's rotation shift for w-byte fields at this row layout: the fewest modelled
+// LDS store cycles (v5_store_cycles), in order (31) on ties.
+int v5_rotation(int stride, int hdr, int hdr_bm, int w, bool read) {
+  int best = 31, cyc = v5_store_cycles(stride, hdr, hdr_bm, w, 31, read);
+  for (int r = 0; r <= 4; ++r) {
+    const int c = v5_store_cycles(stride, hdr, hdr_bm, w, r, read);
+    if (c < cyc) best = r, cyc = c;
+  }
+  return best;
+}
 
 hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
   if (L.num_rows <= 0) return hipSuccess;

@@ -32,11 +32,15 @@ struct FixedLaunch {
   int64_t xcd_run;              // XCD-grouped tile order: tiles per XCD run (0 = dispatch order)
   int32_t cols_aligned16;       // decode: every output column 16-byte aligned (decode v5's chunk stores)
   int32_t valid8;               // every validity pointer of slot_validity 8-byte aligned
+  int32_t rot4, rot8;           // encode v5: lane c of a 4- / 8-byte field writes its records starting at
+                                // (c >> rot) mod records-per-chunk (LDS bank spread; 31 = in order)
+  int32_t drot4, drot8;         // decode v5: the same for the records a lane reads
   const uint8_t* const* slot_validity;  // per slot (schema ordinal): the field's validity (encode:
                                         // input, decode: output), null when not nullable / absent
 };
 
 hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s);
+int v5_rotation(int stride, int hdr, int hdr_bm, int w, bool read);
 hipError_t launch_decode_fixed(const FixedLaunch& L, const uint8_t* rows, int32_t* status,
                                hipStream_t s);
 hipError_t launch_fill_offsets(int64_t* offs, int64_t n, int64_t stride, hipStream_t s);

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-5 closing run, part A, on the final build: the full GPU suite and smoke().
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r05close
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; tail -2 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+rc=$?; tail -1 $O/smoke.log; exit $rc
