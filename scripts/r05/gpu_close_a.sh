@@ -2,7 +2,7 @@
 # Round-5 closing run, part A, on the final build: the full GPU suite and smoke().
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
-O=gpurun_out/r05close
+O=gpurun_out/${1:-r05close}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
