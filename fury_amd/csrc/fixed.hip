@@ -823,23 +823,27 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
 // boxes (profiles/r02/ab_order_box*.jsonl): runs of grid/8 17.98 / 17.53 ms,
 // XCD-blocked 16.45 / 16.35, + nt column loads 16.38 / 16.12.
 constexpr int kV5R = 64, kV5WG = 1024, kV5K = 3;
+#ifndef FORY_V5R_NOTNULL  // (build-time A/B: records per tile of the not-null encode)
+#define FORY_V5R_NOTNULL 64
+#endif
 
 template <int HDR, bool NUL>
 hipError_t launch_encode_v5(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
-  const int64_t full = L.num_rows / kV5R;
+  constexpr int R = NUL ? kV5R : FORY_V5R_NOTNULL, K = R == 128 ? 5 : kV5K;
+  const int64_t full = L.num_rows / R;
   if (full > 0) {
-    auto* k = &encode_fixed_v5_kernel<kV5R, kV5WG, kV5K, HDR, 1, NUL>;
+    auto* k = &encode_fixed_v5_kernel<R, kV5WG, K, HDR, 1, NUL>;
     raise_lds_cap(k);
-    const size_t lds = (size_t)kV5R * L.stride + (NUL ? (size_t)2 * 8 * ((L.num_fields + 63) & ~63) : 0);
+    const size_t lds = (size_t)R * L.stride + (NUL ? (size_t)2 * 8 * ((L.num_fields + 63) & ~63) : 0);
     const int64_t grid = persistent_grid(k, lds, full, kV5WG);
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kV5WG), lds, s, L, L.fields, out, full, (int64_t)(full / 8));
   }
-  if (L.num_rows > full * kV5R) {  // tail (< R records): one-tile kernel
+  if (L.num_rows > full * R) {  // tail (< R records): one-tile kernel
     FixedLaunch T = L;
-    T.tile0 = full * kV5R / 64;
+    T.tile0 = full * R / 64;
     auto* k = &encode_fixed_kernel<64, HDR>;
     raise_lds_cap(k);
-    const int64_t tail_tiles = (L.num_rows - full * kV5R + 63) / 64;
+    const int64_t tail_tiles = (L.num_rows - full * R + 63) / 64;
     hipLaunchKernelGGL(k, dim3((unsigned)tail_tiles), dim3(kWG), (size_t)64 * L.stride, s, T, L.fields, out);
   }
   return hipGetLastError();
@@ -853,7 +857,9 @@ hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
     // v5: schemas whose chunk instructions fit K per wave (nullable ones: the NUL form)
     // nullable: the mask-table form needs 8-byte aligned validity words and a mask wave
     // per 64 slots, a bitmap word per wave
-    if ((v3_insn_count<kV5R>(L.group) + kV5WG / 64 - 1) / (kV5WG / 64) <= kV5K &&
+    constexpr int RN = FORY_V5R_NOTNULL, KN = RN == 128 ? 5 : kV5K;  // the not-null form's tile
+    if ((L.any_nullable ? (v3_insn_count<kV5R>(L.group) + kV5WG / 64 - 1) / (kV5WG / 64) <= kV5K
+                        : (v3_insn_count<RN>(L.group) + kV5WG / 64 - 1) / (kV5WG / 64) <= KN) &&
         (!L.any_nullable || (L.valid8 && L.num_fields <= 64 * (kV5WG / 64) && L.bitmap_bytes / 4 <= kV5WG / 64)))
       return L.any_nullable ? launch_encode_v5<HDR, true>(L, out, s) : launch_encode_v5<HDR, false>(L, out, s);
   }
@@ -959,6 +965,15 @@ int v5_rotation(int stride, int hdr, int hdr_bm, int w, bool read) {
     if (c < cyc) best = r, cyc = c;
   }
   return best;
+}
+
+// Library-internal, for a CPU test (not in the public header): the rotation v5_rotation
+// picks and the modelled store / read cycles of a rotation.
+extern "C" int fory_rowfmt_internal_v5_rotation(int stride, int hdr, int hdr_bm, int w, int read) {
+  return v5_rotation(stride, hdr, hdr_bm, w, read != 0);
+}
+extern "C" int fory_rowfmt_internal_v5_cycles(int stride, int hdr, int hdr_bm, int w, int rot, int read) {
+  return v5_store_cycles(stride, hdr, hdr_bm, w, rot, read != 0);
 }
 
 hipError_t launch_encode_fixed(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
