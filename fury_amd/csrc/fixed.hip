@@ -875,8 +875,16 @@ hipError_t launch_encode_tr(const FixedLaunch& L, uint8_t* out, hipStream_t s) {
 // profiles/r02/ab_dec5.jsonl): 17.51 -> 15.31 ms; WG 512 15.65, WG 256 18.00.
 constexpr int kD5R = 64, kD5WG = 1024, kD5K = 4, kD5K2 = 3;
 
+#ifndef FORY_D5R_NOTNULL  // (build-time A/B: records per tile of the not-null decode)
+#define FORY_D5R_NOTNULL 64
+#endif
+constexpr int kD5RN = FORY_D5R_NOTNULL, kD5KN = kD5RN == 128 ? 7 : kD5K, kD5K2N = kD5RN == 128 ? 5 : kD5K2;
+
 template <int HDR>
 bool decode_v5_fits(const FixedLaunch& L) {
+  if (!L.any_nullable)
+    return L.cols_aligned16 && kD5RN * L.stride <= kD5KN * kD5WG * 16 && (kD5RN * L.stride) % 16 == 0 &&
+           v3_insn_count<kD5RN>(L.group) <= kD5K2N * (kD5WG / 64);
   return L.cols_aligned16 && kD5R * L.stride <= kD5K * kD5WG * 16 &&
          (kD5R * L.stride) % 16 == 0 && v3_insn_count<kD5R>(L.group) <= kD5K2 * (kD5WG / 64) &&
          (!L.any_nullable || (L.valid8 && L.bitmap_bytes * 8 <= 64 * (kD5WG / 64)));
@@ -885,21 +893,23 @@ bool decode_v5_fits(const FixedLaunch& L) {
 template <int HDR>
 hipError_t launch_decode_v5(const FixedLaunch& L, const uint8_t* in, int32_t* status, hipStream_t s) {
   // (decode_v5_fits: nullable schemas need 8-byte aligned validity outputs and <= 64 slots per wave)
-  const int64_t full = L.num_rows / kD5R;
+  const int R = L.any_nullable ? kD5R : kD5RN;
+  const int64_t full = L.num_rows / R;
   if (full > 0) {
     auto* k = L.any_nullable ? &decode_fixed_v5_kernel<kD5R, kD5WG, kD5K, kD5K2, HDR, 0, true>
-                             : &decode_fixed_v5_kernel<kD5R, kD5WG, kD5K, kD5K2, HDR, 0, false>;
+                             : &decode_fixed_v5_kernel<kD5RN, kD5WG, kD5KN, kD5K2N, HDR, 0, false>;
     raise_lds_cap(k);
-    const size_t lds = (size_t)kD5R * L.stride;
+    const size_t lds = (size_t)R * L.stride;
     const int64_t grid = persistent_grid(k, lds, full, kD5WG);
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kD5WG), lds, s, L, L.fields, in, full, status);
   }
-  if (L.num_rows > full * kD5R) {  // tail (< 64 records): the one-tile kernel
+  if (L.num_rows > full * R) {  // tail (< R records): the one-tile kernel, 64 records per tile
     FixedLaunch T = L;
-    T.tile0 = full;
+    T.tile0 = full * R / 64;
     auto* k = &decode_fixed_kernel<64, HDR, 12>;
     raise_lds_cap(k);
-    hipLaunchKernelGGL(k, dim3(1), dim3(kWG), (size_t)64 * L.stride, s, T, L.fields, in, status);
+    hipLaunchKernelGGL(k, dim3((unsigned)((L.num_rows - full * R + 63) / 64)), dim3(kWG), (size_t)64 * L.stride, s, T,
+                       L.fields, in, status);
   }
   return hipGetLastError();
 }
