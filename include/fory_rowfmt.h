@@ -420,8 +420,9 @@ int fory_rowfmt_host_decode_var(fory_host_ctx* ctx, const fory_column* host_out_
 int fory_rowfmt_host_decode_var_into(fory_host_ctx* ctx, const void* host_rows, const int64_t* host_row_offsets,
                                      int64_t num_rows, int32_t frame_mode, const fory_column* host_out_cols,
                                      int64_t* host_counts, int64_t* host_bytes);
-/* Pins [host_ptr, host_ptr + bytes) (hipHostRegister): its copies become direct DMAs, and
- * fixed-width host calls whose every buffer is registered run zero-copy. Two live
+/* Pins [host_ptr, host_ptr + bytes) (hipHostRegister): copies inside it become direct
+ * DMAs (their device mapping comes from the library's registration table, no runtime
+ * query per copy); other memory goes through the context's pinned staging. Two live
  * registrations may not overlap (FORY_ERR_INVALID_ARGUMENT; sharing a page is fine).
  * Unregister takes the start of a registered range (else FORY_ERR_INVALID_ARGUMENT) and
  * checks that the runtime no longer maps the range (FORY_ERR_DEVICE otherwise).
