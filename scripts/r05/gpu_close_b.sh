@@ -5,7 +5,7 @@
 # then the default bench line (which reads that file).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
-O=gpurun_out/r05close
+O=gpurun_out/${1:-r05close}
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 cp profiles/pmc_latest.json $O/pmc_latest.json
