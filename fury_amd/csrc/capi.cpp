@@ -270,7 +270,7 @@ int upload(void* ws, const void* host, int64_t bytes, hipStream_t s) {
     sl->buf = nullptr;
     sl->cap = 0;
     const size_t want = std::max<size_t>((size_t)bytes, 64 * 1024);
-    e = hipHostMalloc(&sl->buf, want, hipHostMallocPortable);
+    e = hipHostMalloc(&sl->buf, want, hipHostMallocPortable | hipHostMallocCoherent);
     if (e == hipSuccess) sl->cap = want;
   }
   bool queued = false;
@@ -1525,7 +1525,7 @@ int fory_rowfmt_read_status(const int32_t* d_status, void* stream) {
     }
   }
   hipError_t e = hipSuccess;
-  if (!word.p) e = hipHostMalloc(reinterpret_cast<void**>(&word.p), 64, hipHostMallocPortable);
+  if (!word.p) e = hipHostMalloc(reinterpret_cast<void**>(&word.p), 64, hipHostMallocPortable | hipHostMallocCoherent);
   if (e != hipSuccess) {
     word.p = nullptr;
     return hip_fail(e, "read_status (pinned word)");

@@ -351,8 +351,11 @@ uint8_t* mapped_range(const void* p, size_t bytes) {
 
 int stage_alloc(Staging& st) {
   if (st.mem) return FORY_OK;
+  // coherent (fine-grained) host memory: the blocks are rewritten by the host between
+  // DMAs and re-allocated across contexts, so no device-side cached line of an earlier
+  // use may serve a later copy
   int rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&st.mem), Staging::kBlock * Staging::kBlocks,
-                                   hipHostMallocPortable),
+                                   hipHostMallocPortable | hipHostMallocCoherent),
                      "hipHostMalloc(staging)");
   for (int j = 0; j < Staging::kBlocks && !rc; ++j)
     if (!st.ev[j]) rc = hip_check(hipEventCreateWithFlags(&st.ev[j], hipEventDisableTiming), "hipEventCreate");
@@ -435,7 +438,7 @@ int ensure_hpin(fory_host_ctx* c, int64_t bytes) {
   c->hpin = nullptr;
   c->hpin_bytes = 0;
   const int64_t sz = align_up(bytes + bytes / 2);
-  int rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)sz, hipHostMallocDefault),
+  int rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)sz, hipHostMallocCoherent),
                      "hipHostMalloc(ctx scratch)");
   if (!rc) c->hpin_bytes = sz;
   return rc;
@@ -1062,7 +1065,7 @@ int host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, i
       if (S.used) r = hip_check(hipEventSynchronize(c->ev_sz[b]), "hipEventSynchronize");
       if (S.pin) (void)hipHostFree(S.pin);
       S.pin = nullptr, S.pin_words = 0;
-      if (!r) r = hip_check(hipHostMalloc(reinterpret_cast<void**>(&S.pin), (size_t)(c->chunk + 1) * 8, hipHostMallocDefault),
+      if (!r) r = hip_check(hipHostMalloc(reinterpret_cast<void**>(&S.pin), (size_t)(c->chunk + 1) * 8, hipHostMallocCoherent),
                             "hipHostMalloc(row offsets)");
       if (!r) S.pin_words = c->chunk + 1;
     }
@@ -1487,7 +1490,7 @@ int host_decode_var_into(fory_host_ctx* c, const uint8_t* host_rows, const int64
     if (!r && S.pin_words < rows + 1) {
       if (S.pin) (void)hipHostFree(S.pin);
       S.pin = nullptr, S.pin_words = 0;
-      r = hip_check(hipHostMalloc(reinterpret_cast<void**>(&S.pin), (size_t)(c->chunk + 1) * 8, hipHostMallocDefault),
+      r = hip_check(hipHostMalloc(reinterpret_cast<void**>(&S.pin), (size_t)(c->chunk + 1) * 8, hipHostMallocCoherent),
                     "hipHostMalloc(row offsets)");
       if (!r) S.pin_words = c->chunk + 1;
     }

@@ -306,7 +306,18 @@ def test_host_pageable_pieces_over_a_mib(name, n, chunk):
         assert np.array_equal(offs, eoffs)
         dec = hp.decode_var(expect, eoffs, n, 1)
     bad = np.nonzero(out != expect)[0]
-    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+    if len(bad):  # (a diagnosis for the report: which frames, and what they hold instead)
+        offs_e = eoffs if eoffs is not None else np.arange(n + 1, dtype=np.int64) * (expect.nbytes // n)
+        frames = np.unique(np.searchsorted(offs_e, bad, side="right") - 1)
+        f0 = int(frames[0])
+        got = out[offs_e[f0]:offs_e[f0 + 1]]
+        same = [int(r) for r in range(n) if offs_e[r + 1] - offs_e[r] == len(got)
+                and np.array_equal(expect[offs_e[r]:offs_e[r + 1]], got)][:4]
+        detail = (f"frames {frames[:6].tolist()}..{frames[-3:].tolist()} ({len(frames)}), chunks "
+                  f"{sorted(set((frames // chunk).tolist()))[:8]}, zero bytes among them {int((out[bad] == 0).sum())}, "
+                  f"got {out[bad[:8]].tolist()} want {expect[bad[:8]].tolist()}, frame {f0} as written equals "
+                  f"expected frames {same}, staged pieces {staged_pieces(hp)}")
+        assert False, f"{len(bad)} bytes differ, first at {bad[:8]}: {detail}"
     assert columns_equal(schema, cols, dec) == []
     hp.close()
 
