@@ -83,6 +83,7 @@ struct VarLaunch {
   int32_t nullable;             // bit 0: some fixed column has validity, bit 1: some var column (encode v9)
   int32_t bool_items;           // some list field has bool items (0/1 normalised per item)
   int32_t st_hdr[kMaxTileStructs];  // host copy of each struct's child bitmap bytes (launch sizing)
+  int32_t fr_bytes;             // decode totals pass: stage only each record's first fr_bytes (0 = whole rows)
 };
 
 // sizes -> d_row_offsets[0..n-1] (row/frame byte sizes), then exclusive scan.

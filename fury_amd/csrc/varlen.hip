@@ -2773,6 +2773,10 @@ __device__ __forceinline__ void dec_item_validity(const VarFieldDev& f, int64_t 
   wave_lds_sync();
 }
 
+#ifndef FORY_DEC_FR
+#define FORY_DEC_FR 1
+#endif
+
 template <int HDR, bool WRITE, int NW, bool SPILL>
 __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, const Op* __restrict__ prog, const ColumnDev* __restrict__ cols,
                                                                   const FixedFieldDev* __restrict__ fix, const VarFieldDev* __restrict__ vf,
@@ -2803,7 +2807,11 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   const int mis = (int)(reinterpret_cast<uintptr_t>(in + B0) & 15);
   const int64_t total = mis + (B1 - B0);
   const int64_t tiles = (L.num_rows + 63) / 64;
-  if (!sane || (mis & 3) || total > cap) {  // per-lane path on global rows (one wave)
+  // totals pass of string-only flat plans (fr_bytes: frame header + bitmap + slots): only
+  // each record's fixed part is staged, when every record of the tile has one
+  const int frb = !WRITE && !SPILL ? L.fr_bytes : 0;
+  const bool fr = frb && __ballot(live && end - beg < frb) == 0;
+  if (!sane || (mis & 3) || (!fr && total > cap)) {  // per-lane path on global rows (one wave)
     if (!SPILL && sane && !(mis & 3) && total <= sp.cap) {  // spill: the big-image launch takes it
       if (threadIdx.x == 0) sp.list[atomicAdd(sp.count, 1)] = (int32_t)tile;
       return;
@@ -2842,7 +2850,23 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
      // edge chunks' bytes outside the tile (same 16-B blocks) are never read
     const uint8_t* g = in + B0 - mis;
     const int nch = (int)((total + 15) >> 4);
-    if (L.kn.dec_regs) {  // A/B: non-temporal 16-B loads into registers, kDecRegs per thread in flight, then LDS
+    if (fr) {  // record r's window [beg & ~15, end of its fixed part) at r * frc 16-B chunks
+      const int frc = (frb + 15) / 16 + 1;
+      const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
+      const int fch = rows * frc;
+      for (int c0 = 0; c0 < fch; c0 += 64 * NW) {
+        const int cc = c0 + tid;
+        const int rr = cc < fch ? cc / frc : 0;
+        const int64_t b = __shfl(beg, rr);
+        const int64_t ws = b & ~(int64_t)15, we = (b + frb + 15) & ~(int64_t)15;
+        const int64_t at = ws + (int64_t)(cc - rr * frc) * 16;
+        if (cc < fch && at < we)
+          __builtin_amdgcn_global_load_lds((const GAS void*)(in + at),
+                                           (__attribute__((address_space(3))) void*)(img + (c0 + wave * 64) * 16), 16,
+                                           0, 2);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (L.kn.dec_regs) {  // A/B: non-temporal 16-B loads into registers, kDecRegs per thread in flight, then LDS
       if (WRITE && lane < L.num_var) obase = *gp(vf[lane].out_offsets + r0);
       constexpr int kDecRegs = 8;
       const u32x4* g16 = reinterpret_cast<const u32x4*>(g);
@@ -2877,7 +2901,7 @@ __global__ __launch_bounds__(64 * NW) void var_decode_flat_kernel(VarLaunch L, c
   DEC_STAMP(1);
   const int64_t i = r0 + lane;
   const int rows = L.num_rows - r0 < 64 ? (int)(L.num_rows - r0) : 64;
-  const uint8_t* fp = img + mis + (int)(beg - B0);
+  const uint8_t* fp = fr ? img + lane * ((frb + 15) / 16 + 1) * 16 + (int)(beg & 15) : img + mis + (int)(beg - B0);
   const uint8_t* row = fp + HDR;
   int64_t row_len = end - beg;
   bool bad = !live;
@@ -3481,6 +3505,17 @@ void launch_flat_dec(const VarLaunch& L0, const uint8_t* rows, const int64_t* of
   auto* k = &var_decode_flat_kernel<HDR, WRITE, NW, false>;
   raise_lds_cap(k);
   VarLaunch L = L0;
+  L.fr_bytes = 0;
+  if (!WRITE && FORY_DEC_FR && !L.num_struct && !L.num_list && !L.level2) {
+    // totals pass of a string-only flat plan: a tile image of each record's fixed part (tiles
+    // with a shorter record keep the whole-row image, or spill)
+    const int frb = HDR + L.fixed_size;
+    const int img = ((frb + 15) / 16 + 1) * 16 * 64;
+    if (img < cap) {
+      L.fr_bytes = frb;
+      cap = img;
+    }
+  }
   if (WRITE) L.stg_bytes = dec_stg_bytes(k, L0, cap, NW);
   if (WRITE && L.mean_row > 0) cap = grow_cap(L, k, 64 * NW, cap, [&](int c) { return flat_lds_dec(L, c, NW); });
   const SpillArgs sp = spill_args(L, cap);
