@@ -45,7 +45,20 @@ asan: $(ORACLE_ASAN)
 	ORACLE_LIB=$(abspath $(ORACLE_ASAN)) LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $$(gcc -print-file-name=libubsan.so)" \
 	  ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 python -m pytest tests/test_oracle_golden.py tests/test_infer.py -q -p no:cacheprovider
 
+# Debug-bounds build of the library: the fixed-width kernels count
+# out-of-range accesses per site and redirect them instead of faulting (fixed.hip,
+# FORY_DEBUG_BOUNDS); tests select it with FORY_ROWFMT_LIB=fury_amd/lib/debug/libfory_rowfmt.so.
+DEBUG_LIB := fury_amd/lib/debug/libfory_rowfmt.so
+fury_amd/lib/debug/fixed.o: fury_amd/csrc/fixed.hip $(HDRS)
+	@mkdir -p fury_amd/lib/debug
+	$(HIPCC) $(HIPFLAGS) -DFORY_DEBUG_BOUNDS -c -o $@ $<
+
+$(DEBUG_LIB): fury_amd/lib/debug/fixed.o $(filter-out fury_amd/lib/fixed.o,$(KOBJS))
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+debug: $(DEBUG_LIB)
+
 clean:
 	rm -rf fury_amd/lib oracle/_build $(CAPI_TEST)
 
-.PHONY: all clean asan
+.PHONY: all clean asan debug

@@ -204,6 +204,7 @@ struct UploadSlot {
   uint64_t stamp = 0;        // queue order of that copy
   bool pending = false;      // a copy was queued and not yet seen complete
   bool busy = false;         // taken by a call right now
+  bool dead = false;         // its event reported an error: never reused (its copy may still read it)
 };
 
 struct UploadRing {
@@ -218,15 +219,23 @@ std::map<int, UploadRing*>* g_rings = new std::map<int, UploadRing*>();  // neve
 
 // hipEventQuery: true when the slot's copy is done (clears the "not ready" status it
 // leaves as the thread's last error, so a caller's hipGetLastError is not disturbed).
+// Only hipSuccess frees the slot. Any other answer (a sticky fault of the device, a
+// destroyed stream) says nothing about whether the DMA engine still reads the slot's
+// buffer, so the slot is retired for good -- round 5 treated every non-"not ready"
+// answer as completion and could hand a buffer to the next table while a copy still
+// read it. The error itself reaches the caller through its next
+// synchronising call.
 bool slot_done(UploadSlot* sl) {
+  if (sl->dead) return false;
   if (!sl->pending) return true;
   const hipError_t e = hipEventQuery(sl->ev);
-  if (e == hipErrorNotReady) {
-    (void)hipGetLastError();
-    return false;
+  if (e == hipSuccess) {
+    sl->pending = false;
+    return true;
   }
-  sl->pending = false;  // complete (or an error the next synchronising call reports)
-  return true;
+  (void)hipGetLastError();
+  if (e != hipErrorNotReady) sl->dead = true;
+  return false;
 }
 
 int upload(void* ws, const void* host, int64_t bytes, hipStream_t s) {
@@ -246,7 +255,7 @@ int upload(void* ws, const void* host, int64_t bytes, hipStream_t s) {
     std::lock_guard<std::mutex> lock(r->mu);
     UploadSlot* oldest = nullptr;
     for (UploadSlot* c : r->slots) {
-      if (c->busy) continue;
+      if (c->busy || c->dead) continue;
       if (slot_done(c)) {
         if (!sl || (sl->cap < (size_t)bytes && c->cap >= (size_t)bytes)) sl = c;
         if (sl->cap >= (size_t)bytes) break;
@@ -282,6 +291,7 @@ int upload(void* ws, const void* host, int64_t bytes, hipStream_t s) {
   {
     std::lock_guard<std::mutex> lock(r->mu);
     if (queued || wait_first) sl->pending = queued;
+    if (wait_first && !queued && e != hipSuccess) sl->dead = true;  // its old copy's fate is unknown
     sl->st = s;
     sl->stamp = ++r->clock;
     sl->busy = false;

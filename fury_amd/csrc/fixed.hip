@@ -25,6 +25,47 @@
 
 namespace fory_amd {
 
+// Debug-bounds build (`make debug` -> fury_amd/lib/debug/, -DFORY_DEBUG_BOUNDS; VERDICT r5
+// item 2): each global access of the fixed-width kernels whose address follows the tile
+// walk -- column chunks, validity words, row tiles, column stores -- is checked against
+// the extent its caller promises (num_rows records; Arrow validity of (num_rows + 7) / 8
+// bytes). A violation is counted per site, the first offending (tile or record, limit)
+// kept, and the access goes to a safe address instead of faulting;
+// fory_rowfmt_internal_debug_bounds reads the counters. Product builds compile the
+// checks away (FORY_DBG is `true`).
+#ifdef FORY_DEBUG_BOUNDS
+struct DbgSite {
+  unsigned long long count;
+  long long a, b;
+};
+constexpr int kDbgSites = 16;
+__device__ DbgSite g_dbg[kDbgSites];
+__device__ __noinline__ bool dbg_ok(bool ok, int site, long long a, long long b) {
+  if (!ok && atomicAdd(&g_dbg[site].count, 1ull) == 0) {
+    g_dbg[site].a = a;
+    g_dbg[site].b = b;
+  }
+  return ok;
+}
+#define FORY_DBG(ok, site, a, b) dbg_ok((ok), (site), (long long)(a), (long long)(b))
+#else
+#define FORY_DBG(ok, site, a, b) true
+#endif
+// sites
+enum : int {
+  kDbgEncMask = 0,     // NUL encode: validity word of a tile
+  kDbgEncTile = 1,     // v5 encode: a tile's column chunks
+  kDbgEncStore = 2,    // v5 encode: a tile's rows
+  kDbgDecValid = 3,    // NUL decode: validity word of a tile
+  kDbgDecTile = 4,     // v5 decode: a tile's rows
+  kDbgDecStore = 5,    // v5 decode: a column chunk
+  kDbgTailNull = 6,    // one-tile encode: a validity byte
+  kDbgTailStore = 7,   // one-tile encode: the tile's rows
+  kDbgTailValid = 8,   // one-tile decode: validity bytes
+  kDbgTailLoad = 9,    // one-tile decode: the tile's rows
+  kDbgEncTable = 10,   // NUL kernels: the slot-validity table
+};
+
 namespace {
 
 // ---------------------------------------------------------------------------
@@ -46,8 +87,10 @@ __device__ __forceinline__ int field_of(int fb, int u, int fstep, int fsub) {
 }
 
 // BinaryWriter.setNullAt's input: Arrow validity bit of record idx (nullable fields).
-__device__ __forceinline__ bool input_null(const FixedFieldDev& fd, int64_t idx) {
-  return (fd.flags & 1) && fd.validity && !((load_byte(fd.validity + (idx >> 3)) >> (idx & 7)) & 1);
+__device__ __forceinline__ bool input_null(const FixedFieldDev& fd, int64_t idx, int64_t num_rows) {
+  if (!((fd.flags & 1) && fd.validity)) return false;
+  if (!FORY_DBG(idx >= 0 && (idx >> 3) < (num_rows + 7) / 8, kDbgTailNull, idx, num_rows)) return false;
+  return !((load_byte(fd.validity + (idx >> 3)) >> (idx & 7)) & 1);
 }
 
 // Stores a slot into the LDS row image (BinaryRowWriter.write: slot zeroed,
@@ -121,7 +164,7 @@ __device__ __forceinline__ void store_tile(const uint8_t* lds, uint8_t* __restri
 // One width group [g0, g1) of the encode: U loads in flight, then U slots.
 template <int W, int TR, int HDR>
 __device__ __forceinline__ void enc_group(const FixedFieldDev* __restrict__ fields, int g0, int g1, int wave, int fsub,
-                                          int64_t idx, uint8_t* row, int hdr_bm) {
+                                          int64_t idx, uint8_t* row, int hdr_bm, int64_t num_rows) {
   constexpr int FPW = 64 / TR;
   constexpr int FSTEP = kWaves * FPW;
   constexpr int U = 16;
@@ -137,7 +180,7 @@ __device__ __forceinline__ void enc_group(const FixedFieldDev* __restrict__ fiel
       const int p = field_of<TR>(pb, u, FSTEP, fsub);
       if (p < g1) {
         const FixedFieldDev& fd = fields[p];
-        put_slot<HDR>(row, hdr_bm, fd.slot, v[u], input_null(fd, idx), fd.flags);
+        put_slot<HDR>(row, hdr_bm, fd.slot, v[u], input_null(fd, idx, num_rows), fd.flags);
       }
     }
   }
@@ -162,12 +205,13 @@ __global__ __launch_bounds__(kWG) void encode_fixed_kernel(FixedLaunch L, const 
   if (wave == 0 && fsub == 0) put_header<HDR>(row, L);
   if (L.any_nullable) __syncthreads();  // null bits are OR-ed into the zeroed bitmap
 
-  enc_group<8, TR, HDR>(fields, L.group[0], L.group[1], wave, fsub, idx, row, hdr_bm);
-  enc_group<4, TR, HDR>(fields, L.group[1], L.group[2], wave, fsub, idx, row, hdr_bm);
-  enc_group<2, TR, HDR>(fields, L.group[2], L.group[3], wave, fsub, idx, row, hdr_bm);
-  enc_group<1, TR, HDR>(fields, L.group[3], L.group[4], wave, fsub, idx, row, hdr_bm);
+  enc_group<8, TR, HDR>(fields, L.group[0], L.group[1], wave, fsub, idx, row, hdr_bm, L.num_rows);
+  enc_group<4, TR, HDR>(fields, L.group[1], L.group[2], wave, fsub, idx, row, hdr_bm, L.num_rows);
+  enc_group<2, TR, HDR>(fields, L.group[2], L.group[3], wave, fsub, idx, row, hdr_bm, L.num_rows);
+  enc_group<1, TR, HDR>(fields, L.group[3], L.group[4], wave, fsub, idx, row, hdr_bm, L.num_rows);
   __syncthreads();
-  store_tile(lds, out + r0 * L.stride, rows * L.stride, tid);
+  if (FORY_DBG(r0 >= 0 && r0 + rows <= L.num_rows, kDbgTailStore, r0, L.num_rows))
+    store_tile(lds, out + r0 * L.stride, rows * L.stride, tid);
 }
 
 // Chunk instructions of the 16-byte-chunk encode (v5 below): instruction i of a
@@ -422,7 +466,8 @@ __device__ __forceinline__ void encode_v5_body(const FixedLaunch& L, const Fixed
   bool vw_on = false;
   if constexpr (NUL) {
     const int sl = 64 * wave + lane;
-    const uint8_t* v = sl < L.num_fields ? L.slot_validity[sl] : nullptr;
+    const uint8_t* v = sl < L.num_fields && FORY_DBG(sl >= 0, kDbgEncTable, sl, L.num_fields)
+                           ? L.slot_validity[sl] : nullptr;
     vw_on = v != nullptr;
     if (vw_on) vw = v;
   }
@@ -447,7 +492,13 @@ __device__ __forceinline__ void encode_v5_body(const FixedLaunch& L, const Fixed
     tend = (int64_t)blockIdx.x + mine * gridDim.x;
   }
   auto issue = [&](int64_t tile, u32x4 (&d)[K], uint64_t& m) {
-    if constexpr (NUL) m = *gp(reinterpret_cast<const uint64_t*>(vw_on ? vw + tile * 8 : vw));  // masks first
+#ifdef FORY_DEBUG_BOUNDS
+    if (!FORY_DBG(tile >= 0 && (tile + 1) * R <= L.num_rows, kDbgEncTile, tile, L.num_rows)) tile = 0;
+    const bool mask_ok = !vw_on || FORY_DBG(tile * 8 + 8 <= (L.num_rows + 7) / 8, kDbgEncMask, tile, L.num_rows);
+#else
+    constexpr bool mask_ok = true;
+#endif
+    if constexpr (NUL) m = *gp(reinterpret_cast<const uint64_t*>(vw_on && mask_ok ? vw + tile * 8 : vw));  // masks first
     v5_issue<R, K, OPT>(ptr, wk, tile * R, d);
   };
   auto put_masks = [&](uint64_t m, int b) {  // (Arrow: 1 = valid; rows: 1 = null)
@@ -465,7 +516,8 @@ __device__ __forceinline__ void encode_v5_body(const FixedLaunch& L, const Fixed
     if constexpr (NUL) v5_bitmaps<HDR>(lds, stride, nbw, mtab + bx * nmask, wave, lane);
     __syncthreads();
     put_masks(mo, by);  // (loaded a stage ago; only the other set's chunks are younger)
-    v5_store<R, WG>(L, lds, out + mt(t) * R * stride, tid);
+    if (FORY_DBG(mt(t) >= 0 && (mt(t) + 1) * R <= L.num_rows, kDbgEncStore, mt(t), L.num_rows))
+      v5_store<R, WG>(L, lds, out + mt(t) * R * stride, tid);
     issue(mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)), d, m);
     __syncthreads();
     t += gridDim.x;
@@ -544,7 +596,9 @@ __device__ __forceinline__ void put_validity(const FixedFieldDev& fd, bool isnul
     const uint64_t mine = (m >> (fsub * TR)) & (TR == 64 ? ~0ull : ((1ull << TR) - 1));
     uint8_t* vb = fd.out_validity + (r0 >> 3);
     const int nb = (rows + 7) >> 3;
-    for (int b = 0; b < nb; ++b) store_byte(vb + b, (uint8_t)(mine >> (8 * b)));
+    for (int b = 0; b < nb; ++b)
+      if (FORY_DBG((r0 >> 3) + b < (r0 + rows + 7) / 8, kDbgTailValid, r0 + 8 * b, r0 + rows))
+        store_byte(vb + b, (uint8_t)(mine >> (8 * b)));
   }
 }
 
@@ -607,7 +661,8 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
   const int stride = L.stride;
   const int hdr_bm = HDR + L.bitmap_bytes;
 
-  dma_tile<NT>(lds, in + r0 * stride, rows * stride, tid, wave);
+  if (FORY_DBG(r0 >= 0 && r0 + rows <= L.num_rows, kDbgTailLoad, r0, L.num_rows))
+    dma_tile<NT>(lds, in + r0 * stride, rows * stride, tid, wave);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -637,7 +692,8 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
 // in decode_fixed_kernel.
 template <int R, int K>
 __device__ __forceinline__ void d5_issue(const uint8_t* in, int64_t base, int stride, int tid, int n16, int WGT,
-                                         u32x4 (&d)[K]) {
+                                         u32x4 (&d)[K], int64_t num_rows) {
+  if (!FORY_DBG(base >= 0 && base + R <= num_rows, kDbgDecTile, base, num_rows)) base = 0;
   const uint8_t* tile = in + base * stride;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -664,7 +720,7 @@ __device__ __forceinline__ void d5_write(uint8_t* lds, int tid, int n16, int WGT
 // ballots per wave and tile instead of a bitmap read per record and chunk.
 template <int HDR>
 __device__ __forceinline__ void d5_validity(const uint8_t* lds, int stride, int nbits, uint8_t* vo, int64_t tile,
-                                            int wave, int lane) {
+                                            int wave, int lane, int64_t num_rows) {
   if (64 * wave >= nbits) return;
   const uint8_t* bm = lds + lane * stride + HDR + 8 * wave;
   const uint32_t lo = ld32(bm), hi = 64 * wave + 32 < nbits ? ld32(bm + 4) : 0u;
@@ -675,13 +731,14 @@ __device__ __forceinline__ void d5_validity(const uint8_t* lds, int stride, int 
     const uint64_t nb = __ballot((wd >> (b & 31)) & 1);
     mine = lane == b ? nb : mine;
   }
-  if (vo) *gp(reinterpret_cast<uint64_t*>(vo + tile * 8)) = ~mine;
+  if (vo && FORY_DBG(tile >= 0 && tile * 8 + 8 <= (num_rows + 7) / 8, kDbgDecValid, tile, num_rows))
+    *gp(reinterpret_cast<uint64_t*>(vo + tile * 8)) = ~mine;
 }
 
 template <int R, int K2, int HDR>
 __device__ __forceinline__ void d5_columns(const uint8_t* lds, int stride, int hdr_bm, const int (&wk)[K2],
                                            const uint32_t (&sf)[K2], uint8_t* const (&optr)[K2], int64_t r0,
-                                           int rot4, int rot8) {
+                                           int rot4, int rot8, int64_t num_rows) {
 #pragma unroll
   for (int k = 0; k < K2; ++k) {
     if (!(sf[k] & (1u << 20))) continue;
@@ -732,7 +789,8 @@ __device__ __forceinline__ void d5_columns(const uint8_t* lds, int stride, int h
       }
       x = u32x4{h0, h1, h2, h3};
     }
-    __builtin_nontemporal_store(x, gp(reinterpret_cast<u32x4*>(optr[k] + r0 * w)));
+    if (FORY_DBG(r0 + rb + 16 / w <= num_rows, kDbgDecStore, r0 + rb, num_rows))
+      __builtin_nontemporal_store(x, gp(reinterpret_cast<u32x4*>(optr[k] + r0 * w)));
   }
 }
 
@@ -775,7 +833,8 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
   uint8_t* vo = nullptr;
   if constexpr (NUL) {
     const int sl = 64 * wave + lane;
-    if (sl < L.num_fields) vo = const_cast<uint8_t*>(L.slot_validity[sl]);
+    if (sl < L.num_fields && FORY_DBG(sl >= 0, kDbgEncTable, sl, L.num_fields))
+      vo = const_cast<uint8_t*>(L.slot_validity[sl]);
   }
   const int nbits = L.bitmap_bytes * 8;
   u32x4 dA[K], dB[K];
@@ -792,15 +851,15 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
     if (mine <= 0) return;
     tend = (int64_t)blockIdx.x + mine * gridDim.x;
   }
-  d5_issue<R, K>(in, mt(t) * R, stride, tid, n16, WG, dA);
-  d5_issue<R, K>(in, mt(min(t + (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, dB);
+  d5_issue<R, K>(in, mt(t) * R, stride, tid, n16, WG, dA, L.num_rows);
+  d5_issue<R, K>(in, mt(min(t + (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, dB, L.num_rows);
   auto stage = [&](u32x4 (&d)[K]) {
     d5_write<K>(lds, tid, n16, WG, d);
     __syncthreads();
     if (HDR && tid < R) check_frame<HDR>(lds + tid * stride, L, status);
-    d5_columns<R, K2, HDR>(lds, stride, hdr_bm, wk, sf, optr, mt(t) * R, L.drot4, L.drot8);
-    if constexpr (NUL) d5_validity<HDR>(lds, stride, nbits, vo, mt(t), wave, lane);
-    d5_issue<R, K>(in, mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, d);
+    d5_columns<R, K2, HDR>(lds, stride, hdr_bm, wk, sf, optr, mt(t) * R, L.drot4, L.drot8, L.num_rows);
+    if constexpr (NUL) d5_validity<HDR>(lds, stride, nbits, vo, mt(t), wave, lane, L.num_rows);
+    d5_issue<R, K>(in, mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, d, L.num_rows);
     __syncthreads();
     t += gridDim.x;
   };
@@ -1007,5 +1066,31 @@ hipError_t launch_decode_fixed(const FixedLaunch& L, const uint8_t* in, int32_t*
 }
 
 bool fixed_tiled_supported(int stride) { return pick_tr(stride) != 0; }
+
+// Library-internal, for the debug-bounds runs (not in the public header): per site the
+// violation count and the first offending (value, limit), 3 int64 per site into out[3 *
+// n]; returns the number of sites, -1 in a product build (no checks compiled in), -2 on
+// a HIP error. The counters are cleared after reading when `clear` is set.
+extern "C" int fory_rowfmt_internal_debug_bounds(long long* out, int n, int clear) {
+#ifdef FORY_DEBUG_BOUNDS
+  DbgSite h[kDbgSites];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dbg), sizeof h) != hipSuccess) return -2;
+  for (int i = 0; i < n && i < kDbgSites; ++i) {
+    out[3 * i] = (long long)h[i].count;
+    out[3 * i + 1] = h[i].a;
+    out[3 * i + 2] = h[i].b;
+  }
+  if (clear) {
+    DbgSite z[kDbgSites] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), z, sizeof z) != hipSuccess) return -2;
+  }
+  return kDbgSites;
+#else
+  (void)out;
+  (void)n;
+  (void)clear;
+  return -1;
+#endif
+}
 
 }  // namespace fory_amd

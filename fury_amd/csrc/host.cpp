@@ -12,9 +12,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <iterator>
 #include <map>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #if defined(__x86_64__)
 #include <emmintrin.h>
@@ -30,6 +33,7 @@
 namespace fory_amd {  // scan.hip (kernels.h)
 hipError_t launch_offsets_add(int32_t* offs, int64_t n, int32_t base, hipStream_t s);
 hipError_t launch_bits_shift(const uint8_t* src, int64_t nbits, uint8_t* dst, int shift, hipStream_t s);
+bool host_verify_from_env();  // launch_state.cpp: FORY_ROWFMT_HOST_VERIFY
 }  // namespace fory_amd
 
 namespace {
@@ -240,6 +244,31 @@ struct fory_host_ctx {
   Staging stage;               // pageable caller memory
   uint8_t* hpin = nullptr;     // pinned scratch: level totals, frame end, validity stash
   int64_t hpin_bytes = 0;
+  // Pageable caller buffers of the current call (CallScope): each one's page-aligned
+  // interior is registered the first time a copy touches it and unregistered when the
+  // call returns; copies inside it are direct DMAs, only its unaligned head and tail
+  // go through the staging.
+  struct Extent {
+    uintptr_t base = 0, end = 0;  // the caller buffer
+    uintptr_t lo = 0, hi = 0;     // its page-aligned interior
+    int state = 0;                // 0 not tried yet, 1 registered by this call, 2 declined
+  };
+  std::vector<Extent> ext;
+  int64_t reg_calls = 0, reg_bytes = 0;  // statistics: call-scoped registrations over the context's life
+  double reg_ms = 0;
+  // FORY_ROWFMT_HOST_VERIFY=1 (read at context creation; tests / diagnosis only): after
+  // each chunk's host-to-device copies the device bytes are read back and compared with
+  // the caller's; a mismatch fails the call naming the piece and the source it matches.
+  bool verify = false;
+  struct VPiece {
+    const uint8_t* dev;
+    const uint8_t* host;
+    size_t bytes;
+    const char* what;
+    int64_t seq;
+  };
+  std::vector<VPiece> vcur, vprev;
+  int64_t vseq = 0;
 };
 
 namespace {
@@ -275,6 +304,16 @@ struct Reg {
 };
 std::mutex g_reg_mu;
 std::map<uintptr_t, Reg> g_regs;
+// Call-scoped registrations (fory_host_ctx::ext): interior start -> (bytes, device
+// address of the start, null while the registration is in progress; owning context).
+// Only the owner's copies use them: another context's copy over one is staged, since the
+// owner unregisters it when its call returns, whatever that other copy's DMA is doing.
+struct TmpReg {
+  size_t bytes;
+  uint8_t* dev;
+  const fory_host_ctx* owner;
+};
+std::map<uintptr_t, TmpReg> g_tmp;
 
 std::string hex(uintptr_t a) {
   char b[32];
@@ -301,24 +340,40 @@ int64_t validity_bytes(int64_t rows) { return ((rows + 7) / 8 + 3) / 4 * 4; }
 // reaches host pages the device has no mapping for. Now the first and the last byte
 // must both be pinned, map to device addresses exactly bytes - 1 apart, and lie in
 // the allocation range the runtime reports. Anything else is staged (Staging).
-uint8_t* mapped_range(const void* p, size_t bytes);
-bool pinned_range(const void* p, size_t bytes) { return mapped_range(p, bytes) != nullptr; }
+uint8_t* mapped_range(const void* p, size_t bytes, const fory_host_ctx* owner = nullptr);
+bool pinned_range(const void* p, size_t bytes, const fory_host_ctx* owner = nullptr) {
+  return mapped_range(p, bytes, owner) != nullptr;
+}
 
 // The device address of host byte p when [p, p + bytes) is pinned as one mapping (the
 // conditions above), else nullptr.
-uint8_t* mapped_range(const void* p, size_t bytes) {
+uint8_t* mapped_range(const void* p, size_t bytes, const fory_host_ctx* owner) {
   if (!p || bytes == 0) return nullptr;
-#ifndef FORY_AB_MAPPING_QUERIES  // (build-time A/B: -D it to resolve every copy by runtime queries, as round 4)
-  {  // inside a range this library registered: its mapping is known
+  {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     std::lock_guard<std::mutex> lock(g_reg_mu);
+#ifndef FORY_AB_MAPPING_QUERIES  // (build-time A/B: -D it to resolve every copy by runtime queries, as round 4)
+    // inside a range this library registered: its mapping is known
     auto it = g_regs.upper_bound(a);
     if (it != g_regs.begin()) {
       --it;
       if (a >= it->first && a + bytes <= it->first + it->second.bytes) return it->second.dev + (a - it->first);
     }
-  }
 #endif
+    // a call-scoped registration: its owner's copies inside it are direct; any other
+    // copy touching one is staged (entries are disjoint and sorted: walk back from the
+    // last one starting inside the range until one ends before it)
+    auto jt = g_tmp.upper_bound(a + bytes - 1);
+    if (jt != g_tmp.begin()) {
+      --jt;
+      if (jt->first + jt->second.bytes > a) {
+        if (owner && jt->second.owner == owner && jt->second.dev && a >= jt->first &&
+            a + bytes <= jt->first + jt->second.bytes)
+          return jt->second.dev + (a - jt->first);
+        return nullptr;
+      }
+    }
+  }
   const uint8_t* first = static_cast<const uint8_t*>(p);
   const uint8_t* last = first + (bytes - 1);
   hipPointerAttribute_t a{}, b{};
@@ -399,15 +454,99 @@ int stage_drain(Staging& st) {
   return FORY_OK;
 }
 
-// One copy between caller host memory and the device, queued on stream s. Pinned
-// over its whole range: one async DMA. Otherwise through the context's staging: H2D
-// pieces are in pinned memory before this returns (the caller may reuse its buffer);
-// D2H pieces land in caller memory at the next stage_drain (finish()).
+// A copy through the context's staging: H2D pieces are in pinned memory before this
+// returns (the caller may reuse its buffer); D2H pieces land in caller memory at the next
+// stage_drain (sync_all).
+int hcopy_staged(fory_host_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s,
+                 const char* what);
+
+// Call-scoped registration of caller buffer e's page-aligned interior (first copy that
+// touches it). Declined -- the buffer's pieces stay staged -- when the interior overlaps
+// a registration of this library (fory_rowfmt_host_register or another call's), when the
+// runtime already maps either end (the caller registered it: mapped_range takes such
+// copies whole) or when hipHostRegister refuses it. Registering costs ~4-11 ms per GiB of
+// touched pages on MI355X hosts against ~18 ms per GiB of DMA at 57 GB/s
+// (scripts/microbench/reg_probe.hip, profiles/r06/host/), and no byte crosses host memory
+// a second time.
+void ext_register(fory_host_ctx* c, fory_host_ctx::Extent& e) {
+  e.state = 2;
+  const size_t len = e.hi - e.lo;
+  {
+    std::lock_guard<std::mutex> lock(g_reg_mu);
+    for (const auto& r : g_regs)
+      if (e.lo < r.first + r.second.bytes && r.first < e.hi) return;
+    auto jt = g_tmp.upper_bound(e.hi - 1);
+    if (jt != g_tmp.begin() && std::prev(jt)->first + std::prev(jt)->second.bytes > e.lo) return;
+    g_tmp[e.lo] = TmpReg{len, nullptr, c};  // reserved: nobody's copies use it yet
+  }
+  auto drop = [&]() {
+    std::lock_guard<std::mutex> lock(g_reg_mu);
+    g_tmp.erase(e.lo);
+  };
+  void* lo = reinterpret_cast<void*>(e.lo);
+  void* last = reinterpret_cast<void*>(e.hi - 1);
+  if (still_mapped(lo) || still_mapped(last)) return drop();
+  const auto t0 = std::chrono::steady_clock::now();
+  if (hipHostRegister(lo, len, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return drop();
+  }
+  hipPointerAttribute_t a{}, z{};
+  if (hipPointerGetAttributes(&a, lo) != hipSuccess || hipPointerGetAttributes(&z, last) != hipSuccess ||
+      !a.devicePointer || !z.devicePointer ||
+      static_cast<uint8_t*>(z.devicePointer) - static_cast<uint8_t*>(a.devicePointer) != (std::ptrdiff_t)(len - 1)) {
+    (void)hipGetLastError();
+    (void)hipHostUnregister(lo);
+    return drop();
+  }
+  c->reg_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  ++c->reg_calls;
+  c->reg_bytes += (int64_t)len;
+  std::lock_guard<std::mutex> lock(g_reg_mu);
+  g_tmp[e.lo].dev = static_cast<uint8_t*>(a.devicePointer);
+  e.state = 1;
+}
+
+// One copy between caller host memory and the device, queued on stream s. Pinned over
+// its whole range (or inside this call's registration of the caller buffer holding it):
+// one async DMA. Inside a pageable caller buffer declared for the call (CallScope): the
+// buffer's interior registered on first touch, the copy split into a direct middle and
+// staged unaligned ends. Anything else goes through the context's staging.
 int hcopy(fory_host_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s,
           const char* what) {
   if (bytes == 0) return FORY_OK;
   const bool h2d = kind == hipMemcpyHostToDevice;
-  if (pinned_range(h2d ? src : dst, bytes)) return hip_check(hipMemcpyAsync(dst, src, bytes, kind, s), what);
+  const uint8_t* hp = static_cast<const uint8_t*>(h2d ? src : dst);
+  if (c->verify && h2d) c->vcur.push_back({static_cast<const uint8_t*>(dst), hp, bytes, what, c->vseq++});
+  if (pinned_range(hp, bytes, c)) return hip_check(hipMemcpyAsync(dst, src, bytes, kind, s), what);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(hp), z = a + bytes;
+  for (fory_host_ctx::Extent& e : c->ext) {
+    if (a < e.base || z > e.end) continue;
+    if (e.state == 0) ext_register(c, e);
+    if (e.state != 1) break;
+    const uintptr_t x0 = std::max(a, e.lo), x1 = std::min(z, e.hi);
+    if (x1 <= x0) break;
+    uint8_t* d8 = static_cast<uint8_t*>(h2d ? dst : const_cast<void*>(src));  // the device side
+    auto piece = [&](uintptr_t u0, uintptr_t u1, bool direct) -> int {
+      if (u1 <= u0) return FORY_OK;
+      uint8_t* hptr = reinterpret_cast<uint8_t*>(u0);
+      uint8_t* dptr = d8 + (u0 - a);
+      void* pd = h2d ? static_cast<void*>(dptr) : static_cast<void*>(hptr);
+      const void* ps = h2d ? static_cast<const void*>(hptr) : static_cast<const void*>(dptr);
+      if (direct) return hip_check(hipMemcpyAsync(pd, ps, u1 - u0, kind, s), what);
+      return hcopy_staged(c, pd, ps, u1 - u0, kind, s, what);
+    };
+    int rc = piece(a, x0, false);
+    if (!rc) rc = piece(x0, x1, true);
+    if (!rc) rc = piece(x1, z, false);
+    return rc;
+  }
+  return hcopy_staged(c, dst, src, bytes, kind, s, what);
+}
+
+int hcopy_staged(fory_host_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s,
+                 const char* what) {
+  const bool h2d = kind == hipMemcpyHostToDevice;
   Staging& st = c->stage;
   int rc = stage_alloc(st);
   for (size_t off = 0; off < bytes && !rc; off += Staging::kBlock) {
@@ -441,6 +580,82 @@ int ensure_hpin(fory_host_ctx* c, int64_t bytes) {
   int rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&c->hpin), (size_t)sz, hipHostMallocCoherent),
                      "hipHostMalloc(ctx scratch)");
   if (!rc) c->hpin_bytes = sz;
+  return rc;
+}
+
+// The caller buffers of one call: declared at the call's start (call_extent), each
+// registered on first touch (hcopy -> ext_register); when the call returns, every stream
+// is drained (normally done already by sync_all) and every registration of the call
+// removed, so no caller page stays pinned past the call and no later copy can take a
+// mapping of it for a direct DMA.
+constexpr size_t kRegMin = size_t(4) << 20;  // smaller interiors stay staged
+
+void call_extent(fory_host_ctx* c, const void* p, int64_t bytes) {
+  if (!p || bytes <= 0) return;
+  fory_host_ctx::Extent e;
+  e.base = reinterpret_cast<uintptr_t>(p);
+  e.end = e.base + (uintptr_t)bytes;
+  e.lo = (e.base + 4095) & ~uintptr_t(4095);
+  e.hi = e.end & ~uintptr_t(4095);
+  if (e.hi <= e.lo || e.hi - e.lo < kRegMin) return;
+  for (const auto& o : c->ext)
+    if (e.lo < o.hi && o.lo < e.hi) return;  // (overlapping caller buffers: the first one declared)
+  c->ext.push_back(e);
+}
+
+struct CallScope {
+  fory_host_ctx* c;
+  explicit CallScope(fory_host_ctx* ctx) : c(ctx) {
+    c->ext.clear();
+    c->vcur.clear();
+    c->vprev.clear();
+  }
+  ~CallScope() {
+    bool any = false;
+    for (const auto& e : c->ext) any |= e.state == 1;
+    if (any)
+      for (hipStream_t s : {c->s_in, c->s_k, c->s_out})
+        if (s) (void)hipStreamSynchronize(s);
+    for (const auto& e : c->ext) {
+      if (e.state != 1) continue;
+      (void)hipHostUnregister(reinterpret_cast<void*>(e.lo));
+      (void)hipGetLastError();
+      std::lock_guard<std::mutex> lock(g_reg_mu);
+      g_tmp.erase(e.lo);
+    }
+    c->ext.clear();
+  }
+};
+
+// FORY_ROWFMT_HOST_VERIFY: the device bytes of every host-to-device piece queued since the
+// last check, read back and compared with the caller's bytes once `s` (the stream they
+// were queued on) has drained. A wrong piece fails the call, naming it, the first wrong
+// byte and -- when the device bytes equal the source of another piece of this chunk or
+// the chunk before -- that piece (a staging block or device buffer handed on too early).
+int verify_pieces(fory_host_ctx* c, hipStream_t s, int64_t chunk) {
+  if (!c->verify) return FORY_OK;
+  int rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize(verify)");
+  std::vector<uint8_t> got;
+  for (size_t i = 0; i < c->vcur.size() && !rc; ++i) {
+    const auto& v = c->vcur[i];
+    got.resize(v.bytes);
+    rc = hip_check(hipMemcpy(got.data(), v.dev, v.bytes, hipMemcpyDeviceToHost), "hipMemcpy(verify)");
+    if (rc || !std::memcmp(got.data(), v.host, v.bytes)) continue;
+    size_t first = 0, wrong = 0;
+    while (got[first] == v.host[first]) ++first;
+    for (size_t b = 0; b < v.bytes; ++b) wrong += got[b] != v.host[b];
+    std::string like = "no other piece's source";
+    for (const auto* list : {&c->vcur, &c->vprev})
+      for (const auto& o : *list)
+        if (o.seq != v.seq && o.bytes >= 64 && !std::memcmp(got.data() + first, o.host + std::min(first, o.bytes - 64), 64))
+          like = "piece " + std::to_string(o.seq) + " (" + o.what + ", " + std::to_string(o.bytes) + " bytes)";
+    rc = fail_host(FORY_ERR_DEVICE, "host verify: chunk " + std::to_string(chunk) + " piece " + std::to_string(v.seq) +
+                                        " (" + v.what + ", " + std::to_string(v.bytes) + " bytes): " +
+                                        std::to_string(wrong) + " device bytes differ from the caller's, the first at " +
+                                        std::to_string(first) + "; the device bytes there match " + like);
+  }
+  c->vprev.swap(c->vcur);
+  c->vcur.clear();
   return rc;
 }
 
@@ -482,6 +697,7 @@ int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t c
     c->device = device;
     c->chunk = chunk_rows;
     c->varlen = true;
+    c->verify = fory_amd::host_verify_from_env();
     c->kind.resize(info.num_columns);
     c->parent.resize(info.num_columns);
     c->width.resize(info.num_columns);
@@ -506,6 +722,7 @@ int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t c
   c->info = info;
   c->device = device;
   c->chunk = chunk_rows;
+  c->verify = fory_amd::host_verify_from_env();
   rc = hip_check(hipSetDevice(device), "hipSetDevice");
   if (rc) {
     delete c;
@@ -704,6 +921,13 @@ int host_encode_fixed(fory_host_ctx* c, const fory_column* host_cols, int64_t n,
       return fail_host(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(i) + " missing or shorter than num_rows");
   rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
+  CallScope scope(c);
+  for (int i = 0; i < c->info.num_columns; ++i) {
+    call_extent(c, host_cols[i].values, n * c->width[i]);
+    if (c->nullable[i]) call_extent(c, host_cols[i].validity, (n + 7) / 8);
+  }
+  for (size_t w = 0; w + 1 < W->first.size(); ++w)
+    call_extent(c, W->ptr[w], (W->first[w + 1] - W->first[w]) * stride);
   for (int b = 0; b < 2 && !rc; ++b)
     rc = hip_check(hipMemsetAsync(c->buf[b].status, 0, 4, c->s_k), "hipMemsetAsync");
   const int64_t chunks = (n + c->chunk - 1) / c->chunk;
@@ -724,6 +948,7 @@ int host_encode_fixed(fory_host_ctx* c, const fory_column* host_cols, int64_t n,
         rc = hcopy(c, B.cols[i].validity, h.validity + a / 8, (size_t)((rows + 7) / 8), hipMemcpyHostToDevice, c->s_in, "H2D validity");
     }
     if (!rc) rc = hip_check(hipEventRecord(c->ev_in[b], c->s_in), "hipEventRecord");
+    if (!rc) rc = verify_pieces(c, c->s_in, k);
     // kernel: after the chunk landed and chunk k-2's rows left buffer b
     if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_k, c->ev_in[b], 0), "hipStreamWaitEvent");
     if (!rc && k >= 2) rc = hip_check(hipStreamWaitEvent(c->s_k, c->ev_out[b], 0), "hipStreamWaitEvent");
@@ -780,6 +1005,12 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
   }
   int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
+  CallScope scope(c);
+  call_extent(c, host_rows, n * stride);
+  for (int i = 0; i < c->info.num_columns; ++i) {
+    call_extent(c, host_out_cols[i].values, n * c->width[i]);
+    if (c->nullable[i]) call_extent(c, host_out_cols[i].validity, (n + 7) / 8);
+  }
   for (int b = 0; b < 2 && !rc; ++b)
     rc = hip_check(hipMemsetAsync(c->buf[b].status, 0, 4, c->s_k), "hipMemsetAsync");
   const int64_t chunks = (n + c->chunk - 1) / c->chunk;
@@ -794,6 +1025,7 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
     if (!rc)
       rc = hcopy(c, B.rows, in + a * stride, (size_t)(rows * stride), hipMemcpyHostToDevice, c->s_in, "H2D");
     if (!rc) rc = hip_check(hipEventRecord(c->ev_in[b], c->s_in), "hipEventRecord");
+    if (!rc) rc = verify_pieces(c, c->s_in, k);
     if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_k, c->ev_in[b], 0), "hipStreamWaitEvent");
     if (!rc && k >= 2) rc = hip_check(hipStreamWaitEvent(c->s_k, c->ev_out[b], 0), "hipStreamWaitEvent");
     for (int i = 0; i < c->info.num_columns; ++i)
@@ -982,6 +1214,19 @@ int64_t carve_slices(const fory_host_ctx* c, const std::vector<VarSlice>& sl, in
   return at;
 }
 
+// The caller's columns of a varlen call as call extents (values, offsets, validity of
+// each pre-order column; a column's length is its element count).
+void declare_column_extents(fory_host_ctx* c, const fory_column* h) {
+  for (int i = 0; i < c->info.num_columns; ++i) {
+    const int64_t len = h[i].length;
+    if (len <= 0) continue;
+    if (c->kind[i] == kKindFixed || c->kind[i] == kKindBool) call_extent(c, h[i].values, len * c->width[i]);
+    if (c->kind[i] == kKindBytes && h[i].offsets) call_extent(c, h[i].values, h[i].offsets[len]);
+    if (has_offsets(c->kind[i])) call_extent(c, h[i].offsets, (len + 1) * 4);
+    if (c->nullable[i]) call_extent(c, h[i].validity, (len + 7) / 8);
+  }
+}
+
 // H2D of the slices into a slot's carved region (the unbiased region starts).
 int h2d_slices(fory_host_ctx* c, const fory_column* h, const std::vector<VarSlice>& sl,
                const std::vector<fory_column>& d, hipStream_t s) {
@@ -1033,6 +1278,8 @@ int host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, i
       return fail_host(FORY_ERR_INVALID_ARGUMENT, "column " + std::to_string(i) + " needs offsets");
   int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
+  CallScope scope(c);
+  declare_column_extents(c, host_cols);
   const int64_t chunks = (n + c->chunk - 1) / c->chunk;
   const int64_t ws_bytes = fory_rowfmt_workspace_bytes(c->plan, std::min(n, c->chunk));
   rc = hip_check(hipMemsetAsync(c->vstatus, 0, 8, c->s_k), "hipMemsetAsync");
@@ -1072,6 +1319,7 @@ int host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, i
     if (r) return r;
     carve_slices(c, sl, rows, ws_bytes, S.dev, &dcols[b], &d_offs[b], &ws[b]);
     r = h2d_slices(c, host_cols, sl, dcols[b], c->s_in);
+    if (!r) r = verify_pieces(c, c->s_in, k);
     if (!r) r = fory_rowfmt_encoded_size(c->plan, dcols[b].data(), rows, frame, d_offs[b], ws[b], ws_bytes, c->s_in);
     if (!r) r = hcopy(c, S.pin, d_offs[b], (size_t)(rows + 1) * 8, hipMemcpyDeviceToHost, c->s_in, "D2H row offsets");
     if (!r) r = hip_check(hipEventRecord(c->ev_sz[b], c->s_in), "hipEventRecord");
@@ -1137,6 +1385,9 @@ int host_encode_var(fory_host_ctx* c, const fory_column* host_cols, int64_t n, i
                                 ws[b], ws_bytes, c->s_k);
       if (!rc) rc = hip_check(hipEventRecord(c->ev_k[b], c->s_k), "hipEventRecord");
       if (!rc) rc = hip_check(hipStreamWaitEvent(c->s_out, c->ev_k[b], 0), "hipStreamWaitEvent");
+      for (size_t q = 0; q < piece_w.size(); ++q)  // this chunk's output pieces: registered as they are copied
+        call_extent(c, W->ptr[(size_t)piece_w[q]] + (at(piece_lo[q]) - wbyte[(size_t)piece_w[q]]),
+                    at(piece_hi[q]) - at(piece_lo[q]));
       for (size_t q = 0; q < piece_w.size() && !rc; ++q) {
         const int64_t pw = piece_w[q];
         rc = hcopy(c, W->ptr[(size_t)pw] + (at(piece_lo[q]) - wbyte[(size_t)pw]), S.rows + po[piece_lo[q] - a], (size_t)(at(piece_hi[q]) - at(piece_lo[q])), hipMemcpyDeviceToHost,
@@ -1449,6 +1700,16 @@ int host_decode_var_into(fory_host_ctx* c, const uint8_t* host_rows, const int64
       return fail_host(FORY_ERR_INVALID_ARGUMENT, "output column " + std::to_string(i) + " needs offsets");
   int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
+  CallScope scope(c);
+  call_extent(c, host_rows + host_row_offsets[0], host_row_offsets[n] - host_row_offsets[0]);
+  for (int i = 0; i < N; ++i) {  // caller-sized outputs
+    const int64_t len = out[i].length;
+    if (len <= 0) continue;
+    if (c->kind[i] == kKindBytes) call_extent(c, out[i].values, out[i].capacity);
+    else if (c->kind[i] == kKindFixed || c->kind[i] == kKindBool) call_extent(c, out[i].values, len * c->width[i]);
+    if (has_offsets(c->kind[i])) call_extent(c, out[i].offsets, (len + 1) * 4);
+    if (c->nullable[i]) call_extent(c, out[i].validity, (len + 7) / 8);
+  }
   const int64_t chunks = (n + c->chunk - 1) / c->chunk;
   const int64_t ws_bytes = fory_rowfmt_workspace_bytes(c->plan, std::min(n, c->chunk));
   rc = hip_check(hipMemsetAsync(c->vstatus, 0, 8, c->s_k), "hipMemsetAsync");
@@ -1500,6 +1761,7 @@ int host_decode_var_into(fory_host_ctx* c, const uint8_t* host_rows, const int64
     if (hi > lo) r = hcopy(c, S.rows, host_rows + lo, (size_t)(hi - lo), hipMemcpyHostToDevice, c->s_in, "H2D rows");
     if (!r) r = hcopy(c, d_offs[b], S.pin, (size_t)(rows + 1) * 8, hipMemcpyHostToDevice, c->s_in, "H2D row offsets");
     if (!r) r = hip_check(hipEventRecord(c->ev_in[b], c->s_in), "hipEventRecord");
+    if (!r) r = verify_pieces(c, c->s_in, k);
     crow[b] = rows;
     return r;
   };
@@ -1702,6 +1964,18 @@ extern "C" int fory_rowfmt_internal_host_copy_path(const void* p, int64_t bytes)
 }
 
 extern "C" int64_t fory_rowfmt_internal_host_staged_pieces(const fory_host_ctx* c) { return c ? c->stage.pieces : -1; }
+// Call-scoped registrations a context made over its life: out[0] count, out[1] bytes,
+// out[2] microseconds spent registering; returns the number of call-scoped registrations
+// alive in the process right now (0 between calls).
+extern "C" int fory_rowfmt_internal_host_call_regs(const fory_host_ctx* c, int64_t* out) {
+  if (c && out) {
+    out[0] = c->reg_calls;
+    out[1] = c->reg_bytes;
+    out[2] = (int64_t)(c->reg_ms * 1000.0);
+  }
+  std::lock_guard<std::mutex> lock(g_reg_mu);
+  return (int)g_tmp.size();
+}
 // The staged copies' host memcpy (CopyPool), for a CPU test of its split.
 extern "C" void fory_rowfmt_internal_pool_copy(void* dst, const void* src, int64_t n) {
   CopyPool::get().copy(dst, src, (size_t)n);

@@ -120,4 +120,11 @@ LaunchKnobs knobs_from_env() {
   return k;
 }
 
+// FORY_ROWFMT_HOST_VERIFY=1: a host-path context reads back every host-to-device piece and
+// compares it with the caller's bytes (host.cpp, verify_pieces); read at context creation.
+bool host_verify_from_env() {
+  const char* e = std::getenv("FORY_ROWFMT_HOST_VERIFY");
+  return e && std::atoi(e) != 0;
+}
+
 }  // namespace fory_amd

@@ -30,3 +30,30 @@ def _device_drained(request):
     torch = sys.modules.get("torch")
     if torch is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
         torch.cuda.synchronize()
+        _check_debug_bounds()
+
+
+_DBG_SITES = ["enc_mask", "enc_tile", "enc_store", "dec_valid", "dec_tile", "dec_store", "tail_null", "tail_store",
+              "tail_valid", "tail_load", "slot_table"]
+
+
+def _check_debug_bounds():
+    """Debug-bounds library (`make debug`, FORY_ROWFMT_LIB=fury_amd/lib/debug/...): the
+    fixed-width kernels counted no out-of-range access during the test (fixed.hip,
+    FORY_DEBUG_BOUNDS). A product library has no counters (the call returns -1)."""
+    import ctypes
+    mod = sys.modules.get("fury_amd._lib")
+    if mod is None or mod._lib is None:
+        return
+    f = getattr(mod._lib, "fory_rowfmt_internal_debug_bounds", None)
+    if f is None:
+        return
+    f.restype, f.argtypes = ctypes.c_int, [ctypes.POINTER(ctypes.c_longlong), ctypes.c_int, ctypes.c_int]
+    buf = (ctypes.c_longlong * 48)()
+    n = f(buf, 16, 1)
+    if n == -1:
+        return
+    assert n > 0, "debug-bounds counters unreadable"
+    bad = {(_DBG_SITES[i] if i < len(_DBG_SITES) else str(i)): (buf[3 * i], buf[3 * i + 1], buf[3 * i + 2])
+           for i in range(min(n, 16)) if buf[3 * i]}
+    assert not bad, f"out-of-range accesses (site: count, first value, limit): {bad}"

@@ -288,13 +288,18 @@ def test_host_varlen_parity(name, n, frame, chunk):
 
 @pytest.mark.parametrize("name,n,chunk", [("mixed40_nulls", 40009, 1 << 20), ("struct104", 20011, 8192),
                                           ("nested_nulls", 60013, 16384)])
-def test_host_pageable_pieces_over_a_mib(name, n, chunk):
+def test_host_pageable_pieces_over_a_mib(name, n, chunk, monkeypatch):
     """Pageable caller memory with staged pieces of 1..4 MiB whose sizes the host copy
     threads do not divide evenly: every byte crosses (round 5 lost the last n mod parts
-    bytes of such pieces -- tests/test_host_copy_pool.py)."""
+    bytes of such pieces -- tests/test_host_copy_pool.py). The context runs with
+    FORY_ROWFMT_HOST_VERIFY: every chunk's host-to-device pieces are read back and
+    compared with the caller's bytes, so a wrong piece fails the call naming the piece
+    and the source its device bytes match (round 5's one wrong output here was column-
+    shaped: chunk 0's f0 slice whole and part of f1, profiles/r05/intermittent/)."""
     schema, make = catalog()[name]
     cols = make(n, 11)
     expect, eoffs = oracle.encode(schema, cols, n, 1)
+    monkeypatch.setenv("FORY_ROWFMT_HOST_VERIFY", "1")
     hp = HostPipeline(NativePlan(schema), chunk_rows=chunk)
     if name == "struct104":
         out = np.zeros(expect.nbytes, np.uint8)
@@ -319,6 +324,72 @@ def test_host_pageable_pieces_over_a_mib(name, n, chunk):
                   f"expected frames {same}, staged pieces {staged_pieces(hp)}")
         assert False, f"{len(bad)} bytes differ, first at {bad[:8]}: {detail}"
     assert columns_equal(schema, cols, dec) == []
+    hp.close()
+
+
+def call_regs(hp):
+    """(registrations the context made over its life, bytes, microseconds; call-scoped
+    registrations alive in the process)."""
+    import ctypes
+    f = _internal("fory_rowfmt_internal_host_call_regs", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p])
+    out = np.zeros(3, np.int64)
+    alive = f(hp.handle if hp is not None else None, out.ctypes.data)
+    return int(out[0]), int(out[1]), int(out[2]), alive
+
+
+@pytest.mark.parametrize("frame", [0, 1])
+def test_host_pageable_columns_registered_for_the_call(frame, monkeypatch):
+    """Pageable columns and output of >= 4 MiB page interiors: each
+    caller buffer's interior is registered for the call on its first copy and unregistered
+    before the call returns; the copies inside it are direct DMAs, the unaligned heads and
+    tails staged. Bytes equal the oracle's both ways (verify mode on), nothing stays
+    registered, and a buffer the caller registered itself is used as is."""
+    monkeypatch.setenv("FORY_ROWFMT_HOST_VERIFY", "1")
+    schema, make = catalog()["struct104_boxed"]
+    n = 600_011  # int64 columns: 4.8 MB; chunks of 128Ki records: slices inside the interiors
+    cols = make(n, 29)
+    expect, _ = oracle.encode(schema, cols, n, frame)
+    hp = HostPipeline(NativePlan(schema), chunk_rows=1 << 17)
+    out = np.zeros(expect.nbytes + 100, np.uint8)[3:3 + expect.nbytes]  # unaligned head and tail
+    hp.encode(cols, n, frame, out)
+    calls, nbytes, _, alive = call_regs(hp)
+    assert alive == 0 and registered_ranges() == 0
+    assert calls >= 53 and nbytes >= 52 * (8 * n - 8192)  # 52 int64/double columns + the output
+    bad = np.nonzero(out != expect)[0]
+    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+    dec = empty_like(schema, n)
+    hp.decode(out, n, frame, dec)
+    assert columns_equal(schema, cols, dec) == []
+    assert call_regs(hp)[0] > calls and call_regs(hp)[3] == 0
+    # the caller's own registration of the output: taken whole, not registered again
+    pb, raw = page_buffer(expect.nbytes)
+    host_register(pb)
+    try:
+        before = call_regs(hp)[0]
+        hp.encode(cols, n, frame, pb[:expect.nbytes])
+        assert np.array_equal(pb[:expect.nbytes], expect)
+        assert call_regs(hp)[0] - before <= 104  # the columns only
+    finally:
+        host_unregister(pb)
+    hp.close()
+
+
+@pytest.mark.parametrize("name", ["mixed40_nulls", "nested_nulls"])
+def test_host_varlen_pageable_registered_for_the_call(name, monkeypatch):
+    """Varlen plans: pageable columns, rows and decode outputs registered per call the
+    same way (encode_var + decode_var_into), bytes equal the oracle's, none left behind."""
+    monkeypatch.setenv("FORY_ROWFMT_HOST_VERIFY", "1")
+    schema, make = catalog()[name]
+    n = 300_007
+    cols = make(n, 3)
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    hp = HostPipeline(NativePlan(schema), chunk_rows=1 << 16)
+    out, offs = hp.encode_var(cols, n, 1, np.zeros(expect.nbytes, np.uint8))
+    assert np.array_equal(offs, eoffs) and np.array_equal(out, expect)
+    assert call_regs(hp)[0] > 0 and call_regs(hp)[3] == 0
+    dec = hp.decode_var_into(expect, eoffs, n, 1)
+    assert columns_equal(schema, cols, dec) == []
+    assert call_regs(hp)[3] == 0 and registered_ranges() == 0
     hp.close()
 
 

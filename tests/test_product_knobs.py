@@ -22,6 +22,7 @@ ALLOWED = {
     "FORY_ROWFMT_VARSTG", "FORY_ROWFMT_SPILLCAP", "FORY_ROWFMT_VARNW", "FORY_ROWFMT_SIZES_PROGRAM",
     "FORY_ROWFMT_IDXFRAMES", "FORY_ROWFMT_VARPROF", "FORY_ROWFMT_VARDIAG", "FORY_ROWFMT_VARENC",
     "FORY_ROWFMT_VARXCD", "FORY_ROWFMT_DECREGS", "FORY_ROWFMT_TREECOL",
+    "FORY_ROWFMT_HOST_VERIFY",  # host path: reads back and checks its H2D pieces (same bytes, slower)
 }
 
 
