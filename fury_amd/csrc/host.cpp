@@ -23,7 +23,9 @@
 #include <emmintrin.h>
 #endif
 #include <string>
+#include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -191,6 +193,27 @@ struct Staging {
   struct Owed { uint8_t* dst = nullptr; size_t len = 0; } owed[kBlocks];  // D2H host copies pending
   int next = 0;
   int64_t pieces = 0;  // statistics: pieces staged over the context's life
+  // Small pieces (<= kSmall: the unaligned ends of registered caller buffers) are packed
+  // into small buffers instead of taking a block each: per stream two buffers, filled in
+  // turn; a buffer is reused only after the event of its last DMA completed. (A block per
+  // 4 KiB end piece made the 104 column heads of a decode chunk wait, 8 pieces apart, for
+  // the D2H stream: the host thread followed the DMA engine.)
+  static constexpr size_t kSmall = size_t(64) << 10;
+  static constexpr size_t kSmallBuf = size_t(2) << 20;
+  static constexpr int kSmallStreams = 3;
+  struct SmallOwed {
+    uint8_t* dst;
+    size_t at, len;
+  };
+  struct Small {
+    hipStream_t s = nullptr;
+    int cur = 0;
+    size_t used[2] = {};
+    hipEvent_t ev[2] = {};
+    bool inflight[2] = {};
+    std::vector<SmallOwed> owed[2];
+  } small[kSmallStreams];
+  uint8_t* smem = nullptr;  // kSmallStreams x 2 x kSmallBuf
 };
 
 }  // namespace
@@ -245,15 +268,23 @@ struct fory_host_ctx {
   uint8_t* hpin = nullptr;     // pinned scratch: level totals, frame end, validity stash
   int64_t hpin_bytes = 0;
   // Pageable caller buffers of the current call (CallScope): each one's page-aligned
-  // interior is registered the first time a copy touches it and unregistered when the
-  // call returns; copies inside it are direct DMAs, only its unaligned head and tail
-  // go through the staging.
+  // interior, in pieces of <= 256 MiB, is registered by a helper thread in the order the
+  // call declared them (ahead of the copies that need them) and unregistered when the
+  // call returns; copies inside a registered piece are direct DMAs, the buffers'
+  // unaligned heads and tails go through the staging.
   struct Extent {
-    uintptr_t base = 0, end = 0;  // the caller buffer
+    uintptr_t base = 0, end = 0;  // the part of the caller buffer this piece covers
     uintptr_t lo = 0, hi = 0;     // its page-aligned interior
-    int state = 0;                // 0 not tried yet, 1 registered by this call, 2 declined
+    std::atomic<int> state{0};    // 0 not registered yet, 1 registered by this call, 2 declined
+    bool taken = false;           // the helper has taken it (under reg_mu)
   };
-  std::vector<Extent> ext;
+  std::deque<Extent> ext;         // (stable references: the helper works on entries while more are added)
+  std::mutex reg_mu;
+  std::condition_variable reg_cv;
+  std::thread reg_thread;
+  size_t reg_next = 0;            // entries before it are taken
+  Extent* reg_want = nullptr;     // a piece a copy is waiting for: the helper takes it next
+  bool reg_stop = false;
   int64_t reg_calls = 0, reg_bytes = 0;  // statistics: call-scoped registrations over the context's life
   double reg_ms = 0;
   // FORY_ROWFMT_HOST_VERIFY=1 (read at context creation; tests / diagnosis only): after
@@ -425,6 +456,75 @@ void stage_abandon(Staging& st) {
     st.inflight[j] = false;
     st.owed[j] = Staging::Owed{};
   }
+  for (auto& sm : st.small)
+    for (int b = 0; b < 2; ++b) sm.inflight[b] = false, sm.owed[b].clear(), sm.used[b] = 0;
+}
+
+uint8_t* small_buf(Staging& st, int k, int b) { return st.smem + ((size_t)k * 2 + b) * Staging::kSmallBuf; }
+
+// Small buffer b of stream slot k free again: its last DMA done, its owed D2H copies made.
+int small_retire(Staging& st, int k, int b) {
+  Staging::Small& sm = st.small[k];
+  if (sm.inflight[b]) {
+    int rc = hip_check(hipEventSynchronize(sm.ev[b]), "hipEventSynchronize(small staging)");
+    if (rc) {
+      stage_abandon(st);
+      return rc;
+    }
+    sm.inflight[b] = false;
+  }
+  for (const auto& o : sm.owed[b]) std::memcpy(o.dst, small_buf(st, k, b) + o.at, o.len);
+  sm.owed[b].clear();
+  sm.used[b] = 0;
+  return FORY_OK;
+}
+
+// A small piece on stream s through the stream's small buffers.
+int stage_small(Staging& st, void* dst, const void* src, size_t len, hipMemcpyKind kind, hipStream_t s,
+                const char* what) {
+  int rc = FORY_OK;
+  if (!st.smem) {
+    rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&st.smem), Staging::kSmallBuf * 2 * Staging::kSmallStreams,
+                                 hipHostMallocPortable | hipHostMallocCoherent),
+                   "hipHostMalloc(small staging)");
+    if (rc) return rc;
+  }
+  int k = 0;
+  while (k < Staging::kSmallStreams && st.small[k].s && st.small[k].s != s) ++k;
+  if (k == Staging::kSmallStreams) {  // (more streams than slots: slot 0 is drained and taken over)
+    k = 0;
+    for (int b = 0; b < 2 && !rc; ++b) rc = small_retire(st, 0, b);
+    if (rc) return rc;
+    st.small[0].s = nullptr;
+  }
+  Staging::Small& sm = st.small[k];
+  if (!sm.s) {
+    sm.s = s;
+    for (int b = 0; b < 2 && !rc; ++b)
+      if (!sm.ev[b]) rc = hip_check(hipEventCreateWithFlags(&sm.ev[b], hipEventDisableTiming), "hipEventCreate");
+    if (rc) return rc;
+  }
+  const size_t need = (len + 15) & ~size_t(15);
+  if (sm.used[sm.cur] + need > Staging::kSmallBuf) {  // the other buffer, once its last DMA is done
+    sm.cur ^= 1;
+    rc = small_retire(st, k, sm.cur);
+    if (rc) return rc;
+  }
+  const int b = sm.cur;
+  const size_t at = sm.used[b];
+  uint8_t* p = small_buf(st, k, b) + at;
+  if (kind == hipMemcpyHostToDevice) {
+    std::memcpy(p, src, len);
+    rc = hip_check(hipMemcpyAsync(dst, p, len, kind, s), what);
+  } else {
+    rc = hip_check(hipMemcpyAsync(p, src, len, kind, s), what);
+    if (!rc) sm.owed[b].push_back(Staging::SmallOwed{static_cast<uint8_t*>(dst), at, len});
+  }
+  if (!rc) rc = hip_check(hipEventRecord(sm.ev[b], s), "hipEventRecord(small staging)");
+  if (!rc) sm.inflight[b] = true;
+  sm.used[b] += need;
+  ++st.pieces;
+  return rc;
 }
 
 // Block j free for a new piece: its last DMA done, an owed D2H host copy made.
@@ -446,6 +546,15 @@ int stage_retire(Staging& st, int j) {
 
 // Every staged piece complete, every owed D2H copy in caller memory (oldest first).
 int stage_drain(Staging& st) {
+  if (st.smem)
+    for (int k = 0; k < Staging::kSmallStreams; ++k) {
+      for (int i = 0; i < 2; ++i) {
+        const int rc = small_retire(st, k, st.small[k].cur ^ 1 ^ i);  // the older buffer first
+        if (rc) return rc;
+      }
+      st.small[k].s = nullptr;  // (streams are the context's; a slot is re-bound per call)
+      st.small[k].cur = 0;
+    }
   if (!st.mem) return FORY_OK;
   for (int i = 0; i < Staging::kBlocks; ++i) {
     const int rc = stage_retire(st, (st.next + i) % Staging::kBlocks);
@@ -468,20 +577,29 @@ int hcopy_staged(fory_host_ctx* c, void* dst, const void* src, size_t bytes, hip
 // touched pages on MI355X hosts against ~18 ms per GiB of DMA at 57 GB/s
 // (scripts/microbench/reg_probe.hip, profiles/r06/host/), and no byte crosses host memory
 // a second time.
+// Runs on the context's registration helper; the outcome is published in e.state.
+int ext_register_state(fory_host_ctx* c, fory_host_ctx::Extent& e);
 void ext_register(fory_host_ctx* c, fory_host_ctx::Extent& e) {
-  e.state = 2;
+  const int st = ext_register_state(c, e);
+  std::lock_guard<std::mutex> lock(c->reg_mu);
+  e.state.store(st);
+  c->reg_cv.notify_all();
+}
+
+int ext_register_state(fory_host_ctx* c, fory_host_ctx::Extent& e) {
   const size_t len = e.hi - e.lo;
   {
     std::lock_guard<std::mutex> lock(g_reg_mu);
     for (const auto& r : g_regs)
-      if (e.lo < r.first + r.second.bytes && r.first < e.hi) return;
+      if (e.lo < r.first + r.second.bytes && r.first < e.hi) return 2;
     auto jt = g_tmp.upper_bound(e.hi - 1);
-    if (jt != g_tmp.begin() && std::prev(jt)->first + std::prev(jt)->second.bytes > e.lo) return;
+    if (jt != g_tmp.begin() && std::prev(jt)->first + std::prev(jt)->second.bytes > e.lo) return 2;
     g_tmp[e.lo] = TmpReg{len, nullptr, c};  // reserved: nobody's copies use it yet
   }
   auto drop = [&]() {
     std::lock_guard<std::mutex> lock(g_reg_mu);
     g_tmp.erase(e.lo);
+    return 2;
   };
   void* lo = reinterpret_cast<void*>(e.lo);
   void* last = reinterpret_cast<void*>(e.hi - 1);
@@ -499,12 +617,28 @@ void ext_register(fory_host_ctx* c, fory_host_ctx::Extent& e) {
     (void)hipHostUnregister(lo);
     return drop();
   }
-  c->reg_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  ++c->reg_calls;
-  c->reg_bytes += (int64_t)len;
+  {
+    std::lock_guard<std::mutex> lock(c->reg_mu);
+    c->reg_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ++c->reg_calls;
+    c->reg_bytes += (int64_t)len;
+  }
   std::lock_guard<std::mutex> lock(g_reg_mu);
   g_tmp[e.lo].dev = static_cast<uint8_t*>(a.devicePointer);
-  e.state = 1;
+  return 1;
+}
+
+// The registration state of piece e once the helper has decided it.
+int ext_wait(fory_host_ctx* c, fory_host_ctx::Extent& e) {
+  int st = e.state.load();
+  if (st) return st;
+  std::unique_lock<std::mutex> lock(c->reg_mu);
+  if (!e.taken) {  // out of order: the helper takes this one next
+    c->reg_want = &e;
+    c->reg_cv.notify_all();
+  }
+  c->reg_cv.wait(lock, [&] { return e.state.load() != 0; });
+  return e.state.load();
 }
 
 // One copy between caller host memory and the device, queued on stream s. Pinned over
@@ -520,34 +654,40 @@ int hcopy(fory_host_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyK
   if (c->verify && h2d) c->vcur.push_back({static_cast<const uint8_t*>(dst), hp, bytes, what, c->vseq++});
   if (pinned_range(hp, bytes, c)) return hip_check(hipMemcpyAsync(dst, src, bytes, kind, s), what);
   const uintptr_t a = reinterpret_cast<uintptr_t>(hp), z = a + bytes;
+  uint8_t* d8 = static_cast<uint8_t*>(h2d ? dst : const_cast<void*>(src));  // the device side
+  auto piece = [&](uintptr_t u0, uintptr_t u1, bool direct) -> int {
+    if (u1 <= u0) return FORY_OK;
+    uint8_t* hptr = reinterpret_cast<uint8_t*>(u0);
+    uint8_t* dptr = d8 + (u0 - a);
+    void* pd = h2d ? static_cast<void*>(dptr) : static_cast<void*>(hptr);
+    const void* ps = h2d ? static_cast<const void*>(hptr) : static_cast<const void*>(dptr);
+    if (direct) return hip_check(hipMemcpyAsync(pd, ps, u1 - u0, kind, s), what);
+    return hcopy_staged(c, pd, ps, u1 - u0, kind, s, what);
+  };
+  // the registered pieces of declared caller buffers over [a, z), in address order (a
+  // buffer's pieces were declared in order and abut): one direct DMA per piece (a DMA
+  // may not run past a registration), the gaps -- unaligned ends, declined pieces -- staged
+  uintptr_t cur = a;
+  int rc = FORY_OK;
   for (fory_host_ctx::Extent& e : c->ext) {
-    if (a < e.base || z > e.end) continue;
-    if (e.state == 0) ext_register(c, e);
-    if (e.state != 1) break;
-    const uintptr_t x0 = std::max(a, e.lo), x1 = std::min(z, e.hi);
-    if (x1 <= x0) break;
-    uint8_t* d8 = static_cast<uint8_t*>(h2d ? dst : const_cast<void*>(src));  // the device side
-    auto piece = [&](uintptr_t u0, uintptr_t u1, bool direct) -> int {
-      if (u1 <= u0) return FORY_OK;
-      uint8_t* hptr = reinterpret_cast<uint8_t*>(u0);
-      uint8_t* dptr = d8 + (u0 - a);
-      void* pd = h2d ? static_cast<void*>(dptr) : static_cast<void*>(hptr);
-      const void* ps = h2d ? static_cast<const void*>(hptr) : static_cast<const void*>(dptr);
-      if (direct) return hip_check(hipMemcpyAsync(pd, ps, u1 - u0, kind, s), what);
-      return hcopy_staged(c, pd, ps, u1 - u0, kind, s, what);
-    };
-    int rc = piece(a, x0, false);
+    if (rc || cur >= z) break;
+    if (e.base >= z || e.end <= cur || e.lo >= z || e.hi <= cur) continue;
+    if (ext_wait(c, e) != 1) continue;
+    const uintptr_t x0 = std::max(cur, e.lo), x1 = std::min(z, e.hi);
+    if (x1 <= x0) continue;
+    rc = piece(cur, x0, false);
     if (!rc) rc = piece(x0, x1, true);
-    if (!rc) rc = piece(x1, z, false);
-    return rc;
+    cur = x1;
   }
-  return hcopy_staged(c, dst, src, bytes, kind, s, what);
+  if (!rc) rc = piece(cur, z, false);
+  return rc;
 }
 
 int hcopy_staged(fory_host_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s,
                  const char* what) {
   const bool h2d = kind == hipMemcpyHostToDevice;
   Staging& st = c->stage;
+  if (bytes <= Staging::kSmall) return stage_small(st, dst, src, bytes, kind, s, what);
   int rc = stage_alloc(st);
   for (size_t off = 0; off < bytes && !rc; off += Staging::kBlock) {
     const size_t len = std::min(bytes - off, Staging::kBlock);
@@ -590,34 +730,80 @@ int ensure_hpin(fory_host_ctx* c, int64_t bytes) {
 // mapping of it for a direct DMA.
 constexpr size_t kRegMin = size_t(4) << 20;  // smaller interiors stay staged
 
+constexpr uintptr_t kRegPiece = uintptr_t(256) << 20;  // registration granularity of big buffers
+
+// The helper: registers the declared pieces in order until the call ends.
+void reg_worker(fory_host_ctx* c) {
+  for (;;) {
+    fory_host_ctx::Extent* e = nullptr;
+    {
+      std::unique_lock<std::mutex> lock(c->reg_mu);
+      for (;;) {
+        while (c->reg_next < c->ext.size() && c->ext[c->reg_next].taken) ++c->reg_next;
+        if (c->reg_want && !c->reg_want->taken) e = c->reg_want;  // a copy waits for it
+        else if (c->reg_next < c->ext.size()) e = &c->ext[c->reg_next];
+        c->reg_want = nullptr;
+        if (e || c->reg_stop) break;
+        c->reg_cv.wait(lock);
+      }
+      if (!e) return;  // stopped with nothing left
+      e->taken = true;
+    }
+    ext_register(c, *e);
+  }
+}
+
 void call_extent(fory_host_ctx* c, const void* p, int64_t bytes) {
   if (!p || bytes <= 0) return;
-  fory_host_ctx::Extent e;
-  e.base = reinterpret_cast<uintptr_t>(p);
-  e.end = e.base + (uintptr_t)bytes;
-  e.lo = (e.base + 4095) & ~uintptr_t(4095);
-  e.hi = e.end & ~uintptr_t(4095);
-  if (e.hi <= e.lo || e.hi - e.lo < kRegMin) return;
+  const uintptr_t base = reinterpret_cast<uintptr_t>(p), end = base + (uintptr_t)bytes;
+  const uintptr_t lo = (base + 4095) & ~uintptr_t(4095), hi = end & ~uintptr_t(4095);
+  if (hi <= lo || hi - lo < kRegMin) return;
   for (const auto& o : c->ext)
-    if (e.lo < o.hi && o.lo < e.hi) return;  // (overlapping caller buffers: the first one declared)
-  c->ext.push_back(e);
+    if (lo < o.hi && o.lo < hi) return;  // (overlapping caller buffers: the first one declared)
+  {
+    std::lock_guard<std::mutex> lock(c->reg_mu);
+    for (uintptr_t x = lo; x < hi; x += kRegPiece) {
+      fory_host_ctx::Extent& e = c->ext.emplace_back();
+      e.lo = x;
+      e.hi = std::min(hi, x + kRegPiece);
+      e.base = x == lo ? base : x;
+      e.end = e.hi == hi ? end : e.hi;
+    }
+  }
+  if (!c->reg_thread.joinable()) c->reg_thread = std::thread(reg_worker, c);
+  c->reg_cv.notify_all();
 }
 
 struct CallScope {
   fory_host_ctx* c;
   explicit CallScope(fory_host_ctx* ctx) : c(ctx) {
     c->ext.clear();
+    c->reg_next = 0;
+    c->reg_want = nullptr;
+    c->reg_stop = false;
     c->vcur.clear();
     c->vprev.clear();
   }
   ~CallScope() {
+    if (c->reg_thread.joinable()) {
+      {
+        std::lock_guard<std::mutex> lock(c->reg_mu);
+        c->reg_stop = true;
+        // pieces the helper has not taken: never registered
+        for (auto& e : c->ext)
+          if (!e.taken) e.taken = true, e.state.store(2);
+        c->reg_want = nullptr;
+      }
+      c->reg_cv.notify_all();
+      c->reg_thread.join();
+    }
     bool any = false;
-    for (const auto& e : c->ext) any |= e.state == 1;
+    for (const auto& e : c->ext) any |= e.state.load() == 1;
     if (any)
       for (hipStream_t s : {c->s_in, c->s_k, c->s_out})
         if (s) (void)hipStreamSynchronize(s);
     for (const auto& e : c->ext) {
-      if (e.state != 1) continue;
+      if (e.state.load() != 1) continue;
       (void)hipHostUnregister(reinterpret_cast<void*>(e.lo));
       (void)hipGetLastError();
       std::lock_guard<std::mutex> lock(g_reg_mu);
@@ -798,6 +984,10 @@ void fory_rowfmt_host_ctx_destroy(fory_host_ctx* c) {
   for (hipEvent_t e : c->stage.ev)
     if (e) (void)hipEventDestroy(e);
   if (c->stage.mem) (void)hipHostFree(c->stage.mem);
+  for (auto& sm : c->stage.small)
+    for (hipEvent_t e : sm.ev)
+      if (e) (void)hipEventDestroy(e);
+  if (c->stage.smem) (void)hipHostFree(c->stage.smem);
   if (c->hpin) (void)hipHostFree(c->hpin);
   delete c;
 }
@@ -1006,11 +1196,15 @@ int fory_rowfmt_host_decode(fory_host_ctx* c, const void* host_rows, int64_t row
   int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
   CallScope scope(c);
-  call_extent(c, host_rows, n * stride);
+  // in the order the copies first need them: the first chunk's rows, the output columns
+  // (its D2H), then the other chunks' rows
+  const int64_t first = std::min(n, c->chunk) * stride;
+  call_extent(c, host_rows, first);
   for (int i = 0; i < c->info.num_columns; ++i) {
     call_extent(c, host_out_cols[i].values, n * c->width[i]);
     if (c->nullable[i]) call_extent(c, host_out_cols[i].validity, (n + 7) / 8);
   }
+  call_extent(c, static_cast<const uint8_t*>(host_rows) + first, n * stride - first);
   for (int b = 0; b < 2 && !rc; ++b)
     rc = hip_check(hipMemsetAsync(c->buf[b].status, 0, 4, c->s_k), "hipMemsetAsync");
   const int64_t chunks = (n + c->chunk - 1) / c->chunk;
@@ -1481,6 +1675,8 @@ int decode_var_stage(fory_host_ctx* c, const void* host_rows, const int64_t* hos
   }
   int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
+  CallScope scope(c);
+  call_extent(c, static_cast<const uint8_t*>(host_rows) + r0, r1 - r0);
   // device run: [rows (16-byte aligned start)][row offsets n+1][index status][index workspace]
   const int64_t rows_sz = align_up((r1 - r0) + 16), offs_sz = align_up((n + 1) * 8);
   const int64_t iws = host_row_offsets ? 0 : fory_rowfmt_index_workspace_bytes(c->plan, n, r1 - r0);
@@ -1628,6 +1824,13 @@ int fory_rowfmt_host_decode_var(fory_host_ctx* c, const fory_column* host_out_co
   }
   int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
+  CallScope scope(c);
+  for (int i = 0; i < N; ++i) {
+    const fory_column& h = host_out_cols[i];
+    call_extent(c, h.values, c->dec_bytes[i]);
+    if (has_offsets(c->kind[i])) call_extent(c, h.offsets, (c->dec_count[i] + 1) * 4);
+    if (c->nullable[i]) call_extent(c, h.validity, (c->dec_count[i] + 7) / 8);
+  }
   std::vector<char> wv(N, 0);
   for (int i = 0; i < N; ++i) wv[i] = c->nullable[i] && host_out_cols[i].validity;
   const int64_t ws_bytes = fory_rowfmt_workspace_bytes(c->plan, n);
