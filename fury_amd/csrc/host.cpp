@@ -99,8 +99,12 @@ class CopyPool {
       std::memcpy(dst, src, n);
       return;
     }
-    std::unique_lock<std::mutex> lock(mu_);  // one job at a time (callers: one per context call)
-    idle_.wait(lock, [&] { return !busy_; });
+    std::unique_lock<std::mutex> lock(mu_);  // one job at a time
+    if (busy_) {  // another context's job has the pool: copy on this thread rather than queue
+      lock.unlock();
+      stream_copy(static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), n);
+      return;
+    }
     busy_ = true;
     dst_ = static_cast<uint8_t*>(dst);
     src_ = static_cast<const uint8_t*>(src);
@@ -122,8 +126,6 @@ class CopyPool {
     }
     done_.wait(lock, [&] { return left_ == 0 && active_ == 0; });
     busy_ = false;
-    lock.unlock();
-    idle_.notify_one();
   }
 
  private:
@@ -167,7 +169,7 @@ class CopyPool {
     }
   }
   std::mutex mu_;
-  std::condition_variable work_, done_, idle_;
+  std::condition_variable work_, done_;
   std::vector<std::thread> threads_;
   int nthreads_ = 0;
   bool busy_ = false, stop_ = false;
