@@ -355,12 +355,14 @@ __device__ __forceinline__ void v5_bitmaps(uint8_t* lds, int stride, int nbw, co
 // The tile's rows (R * stride contiguous bytes) leave with non-temporal 16-B
 // stores: the once-written row stream does not displace L2 lines
 // (18.43 -> 18.03 ms at 64M Struct104 rows).
-template <int R, int WG>
+// (OPT & 4, an A/B form only -- scripts/microbench/enc_ab.hip: plain stores instead)
+template <int R, int WG, int OPT = 0>
 __device__ __forceinline__ void v5_store(const FixedLaunch& L, uint8_t* lds, uint8_t* dst, int tid) {
   const int bytes = R * L.stride;
   const int n16 = bytes >> 4;
   for (int c = tid; c < n16; c += WG)
-    __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(lds + c * 16), gp(reinterpret_cast<u32x4*>(dst + c * 16)));
+    if constexpr (OPT & 4) *gp(reinterpret_cast<u32x4*>(dst + c * 16)) = *reinterpret_cast<const u32x4*>(lds + c * 16);
+    else __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(lds + c * 16), gp(reinterpret_cast<u32x4*>(dst + c * 16)));
   const int tail4 = (bytes & 15) >> 2;
   if (tid < tail4) st32(dst + n16 * 16 + tid * 4, ld32(lds + n16 * 16 + tid * 4));
 }
@@ -517,7 +519,7 @@ __device__ __forceinline__ void encode_v5_body(const FixedLaunch& L, const Fixed
     __syncthreads();
     put_masks(mo, by);  // (loaded a stage ago; only the other set's chunks are younger)
     if (FORY_DBG(mt(t) >= 0 && (mt(t) + 1) * R <= L.num_rows, kDbgEncStore, mt(t), L.num_rows))
-      v5_store<R, WG>(L, lds, out + mt(t) * R * stride, tid);
+      v5_store<R, WG, OPT>(L, lds, out + mt(t) * R * stride, tid);
     issue(mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)), d, m);
     __syncthreads();
     t += gridDim.x;
@@ -690,7 +692,8 @@ __global__ __launch_bounds__(kWG) void decode_fixed_kernel(FixedLaunch L, const 
 // chunks fit K2 instructions per wave; nullable ones also write the Arrow validity
 // (NUL form, d5_validity). Null bits are always read: a set bit decodes to 0, as
 // in decode_fixed_kernel.
-template <int R, int K>
+// (OPT & 8, an A/B form only -- scripts/microbench/enc_ab.hip: plain row loads)
+template <int R, int K, int OPT = 0>
 __device__ __forceinline__ void d5_issue(const uint8_t* in, int64_t base, int stride, int tid, int n16, int WGT,
                                          u32x4 (&d)[K], int64_t num_rows) {
   if (!FORY_DBG(base >= 0 && base + R <= num_rows, kDbgDecTile, base, num_rows)) base = 0;
@@ -698,7 +701,9 @@ __device__ __forceinline__ void d5_issue(const uint8_t* in, int64_t base, int st
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int c = tid + k * WGT;
-    d[k] = __builtin_nontemporal_load(gp(reinterpret_cast<const u32x4*>(tile + (int64_t)(c < n16 ? c : 0) * 16)));
+    const u32x4* a = reinterpret_cast<const u32x4*>(tile + (int64_t)(c < n16 ? c : 0) * 16);
+    if constexpr (OPT & 8) d[k] = *gp(a);
+    else d[k] = __builtin_nontemporal_load(gp(a));
   }
 }
 
@@ -735,7 +740,8 @@ __device__ __forceinline__ void d5_validity(const uint8_t* lds, int stride, int 
     *gp(reinterpret_cast<uint64_t*>(vo + tile * 8)) = ~mine;
 }
 
-template <int R, int K2, int HDR>
+// (OPT & 4, an A/B form only: plain column stores)
+template <int R, int K2, int HDR, int OPT = 0>
 __device__ __forceinline__ void d5_columns(const uint8_t* lds, int stride, int hdr_bm, const int (&wk)[K2],
                                            const uint32_t (&sf)[K2], uint8_t* const (&optr)[K2], int64_t r0,
                                            int rot4, int rot8, int64_t num_rows) {
@@ -789,8 +795,10 @@ __device__ __forceinline__ void d5_columns(const uint8_t* lds, int stride, int h
       }
       x = u32x4{h0, h1, h2, h3};
     }
-    if (FORY_DBG(r0 + rb + 16 / w <= num_rows, kDbgDecStore, r0 + rb, num_rows))
-      __builtin_nontemporal_store(x, gp(reinterpret_cast<u32x4*>(optr[k] + r0 * w)));
+    if (FORY_DBG(r0 + rb + 16 / w <= num_rows, kDbgDecStore, r0 + rb, num_rows)) {
+      if constexpr (OPT & 4) *gp(reinterpret_cast<u32x4*>(optr[k] + r0 * w)) = x;
+      else __builtin_nontemporal_store(x, gp(reinterpret_cast<u32x4*>(optr[k] + r0 * w)));
+    }
   }
 }
 
@@ -851,15 +859,15 @@ __global__ __launch_bounds__(WG, 1) void decode_fixed_v5_kernel(FixedLaunch L,
     if (mine <= 0) return;
     tend = (int64_t)blockIdx.x + mine * gridDim.x;
   }
-  d5_issue<R, K>(in, mt(t) * R, stride, tid, n16, WG, dA, L.num_rows);
-  d5_issue<R, K>(in, mt(min(t + (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, dB, L.num_rows);
+  d5_issue<R, K, OPT>(in, mt(t) * R, stride, tid, n16, WG, dA, L.num_rows);
+  d5_issue<R, K, OPT>(in, mt(min(t + (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, dB, L.num_rows);
   auto stage = [&](u32x4 (&d)[K]) {
     d5_write<K>(lds, tid, n16, WG, d);
     __syncthreads();
     if (HDR && tid < R) check_frame<HDR>(lds + tid * stride, L, status);
-    d5_columns<R, K2, HDR>(lds, stride, hdr_bm, wk, sf, optr, mt(t) * R, L.drot4, L.drot8, L.num_rows);
+    d5_columns<R, K2, HDR, OPT>(lds, stride, hdr_bm, wk, sf, optr, mt(t) * R, L.drot4, L.drot8, L.num_rows);
     if constexpr (NUL) d5_validity<HDR>(lds, stride, nbits, vo, mt(t), wave, lane, L.num_rows);
-    d5_issue<R, K>(in, mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, d, L.num_rows);
+    d5_issue<R, K, OPT>(in, mt(min(t + 2 * (int64_t)gridDim.x, tend - 1)) * R, stride, tid, n16, WG, d, L.num_rows);
     __syncthreads();
     t += gridDim.x;
   };

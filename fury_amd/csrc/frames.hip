@@ -231,6 +231,78 @@ __global__ __launch_bounds__(kWG) void frame_write_kernel(FrameIndexLaunch L, co
   }
 }
 
+// The same offsets with the stores coalesced (round 6): a workgroup per kWG chunks stages
+// their first frame indices, counts and saved positions in LDS, then its threads write
+// consecutive offs[f] -- each finds its chunk by a binary search over the staged frame
+// bases -- where frame_write_kernel had each lane store its own chunk's ~16 offsets at a
+// 128-byte stride from the next lane's (64 partial lines per store instruction). Chunks
+// whose positions were not all saved (a fix-up re-walk, > kSaved frames) are walked by
+// their own thread as before.
+__global__ __launch_bounds__(kWG) void frame_write_co_kernel(FrameIndexLaunch L, const uint8_t* __restrict__ rows,
+                                                             const int64_t* __restrict__ start,
+                                                             const int64_t* __restrict__ exit_,
+                                                             const int64_t* __restrict__ base,
+                                                             const uint16_t* __restrict__ pos,
+                                                             const int32_t* __restrict__ saved,
+                                                             int64_t* __restrict__ offs, int32_t* status) {
+  __shared__ int64_t fb[kWG + 1];        // first frame index of each chunk (+ the end)
+  __shared__ uint8_t ok[kWG];            // its frames' positions are all saved
+  __shared__ uint16_t sp[kSaved][kWG];   // the saved positions, position-major
+  const int t = threadIdx.x;
+  const int64_t k0 = (int64_t)blockIdx.x * kWG;
+  const int nk = L.chunks - k0 < kWG ? (int)(L.chunks - k0) : kWG;
+  const int64_t k = k0 + t;
+  if (k == 0 && base[L.chunks] < L.num_rows) set_status(status, FORY_ERR_CORRUPT);  // fewer than N frames
+  int64_t f = 0, cnt = 0, p = -1;
+  bool sv = false;
+  if (t < nk) {
+    f = base[k];
+    cnt = base[k + 1] - f;
+    p = start[k];
+    sv = p >= 0 && saved[k] == cnt;
+#pragma unroll 8
+    for (int j = 0; j < kSaved; ++j) sp[j][t] = pos[j * L.chunks + k];
+    fb[t] = f;
+    ok[t] = sv ? 1 : 0;
+    if (t == nk - 1) fb[nk] = base[k + 1];
+  }
+  __syncthreads();
+  if (t < nk && p >= 0 && f < L.num_rows) {
+    const int64_t cbase = k * L.chunk, end = min(cbase + L.chunk, L.rows_bytes);
+    if (sv) {
+      // the chain broke inside this chunk before frame N: Encoders.decode would read past it
+      if (exit_[k] == kBroken && f + cnt < L.num_rows) set_status(status, FORY_ERR_CORRUPT);
+    } else {
+      int64_t g = f;
+      while (p < end && g < L.num_rows) {
+        const uint32_t size = frame_size(rows, p);
+        if (!sane_size(size, p, L)) {  // Encoders.decode would read past the frame: corrupt stream
+          set_status(status, FORY_ERR_CORRUPT);
+          break;
+        }
+        offs[g] = p;
+        p += 4 + (int64_t)size;
+        if (g == L.num_rows - 1) offs[L.num_rows] = p;
+        ++g;
+      }
+    }
+  }
+  // the saved chunks' frames: consecutive threads, consecutive offsets
+  const int64_t F0 = fb[0], F1 = min(fb[nk], L.num_rows);
+  for (int64_t g = F0 + t; g < F1; g += kWG) {
+    int a = 0, b = nk - 1;  // the last chunk whose first frame is at or before g
+    while (a < b) {
+      const int mid = (a + b + 1) >> 1;
+      if (fb[mid] <= g) a = mid;
+      else b = mid - 1;
+    }
+    if (!ok[a]) continue;
+    const int64_t q = (k0 + a) * L.chunk + sp[g - fb[a]][a];
+    offs[g] = q;
+    if (g == L.num_rows - 1) offs[L.num_rows] = q + 4 + (int64_t)frame_size(rows, q);
+  }
+}
+
 }  // namespace
 
 void frame_index_plan(int64_t num_rows, int64_t rows_bytes, int32_t idx_frames, int64_t* chunk, int64_t* chunks) {
@@ -278,7 +350,7 @@ hipError_t launch_frame_index(const FrameIndexLaunch& L0, const uint8_t* rows, i
                      moved);
   hipError_t e = launch_scan_i64(count, K, partials, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(frame_write_kernel, dim3(blocks), dim3(kWG), 0, s, L, rows, start, exit_, count, pos, saved,
+  hipLaunchKernelGGL(frame_write_co_kernel, dim3(blocks), dim3(kWG), 0, s, L, rows, start, exit_, count, pos, saved,
                      offs, status);
   return hipGetLastError();
 }
