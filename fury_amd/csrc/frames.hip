@@ -193,49 +193,12 @@ __global__ __launch_bounds__(1024) void frame_fixup_kernel(FrameIndexLaunch L, c
   }
 }
 
-// Chunk k's frames get indices base[k] .. base[k] + count[k] - 1 (count scanned in place).
-__global__ __launch_bounds__(kWG) void frame_write_kernel(FrameIndexLaunch L, const uint8_t* __restrict__ rows,
-                                                          const int64_t* __restrict__ start,
-                                                          const int64_t* __restrict__ exit_,
-                                                          const int64_t* __restrict__ base,
-                                                          const uint16_t* __restrict__ pos,
-                                                          const int32_t* __restrict__ saved,
-                                                          int64_t* __restrict__ offs, int32_t* status) {
-  const int64_t k = (int64_t)blockIdx.x * kWG + threadIdx.x;
-  if (k == 0 && base[L.chunks] < L.num_rows) set_status(status, FORY_ERR_CORRUPT);  // fewer than N frames
-  if (k >= L.chunks) return;
-  int64_t p = start[k], f = base[k];
-  if (p < 0 || f >= L.num_rows) return;
-  const int64_t cbase = k * L.chunk, end = min(cbase + L.chunk, L.rows_bytes);
-  const int64_t cnt = base[k + 1] - f;
-  if (saved[k] == cnt) {  // the spec walk is the true chain and saved every start
-    for (int64_t j = 0; j < cnt && f < L.num_rows; ++j, ++f) {
-      const int64_t q = cbase + pos[j * L.chunks + k];
-      offs[f] = q;
-      if (f == L.num_rows - 1) offs[L.num_rows] = q + 4 + (int64_t)frame_size(rows, q);
-    }
-    // the chain broke inside this chunk before frame N: Encoders.decode would read past it
-    if (exit_[k] == kBroken && f < L.num_rows) set_status(status, FORY_ERR_CORRUPT);
-    return;
-  }
-  while (p < end && f < L.num_rows) {
-    const uint32_t size = frame_size(rows, p);
-    if (!sane_size(size, p, L)) {  // Encoders.decode would read past the frame: corrupt stream
-      set_status(status, FORY_ERR_CORRUPT);
-      return;
-    }
-    offs[f] = p;
-    p += 4 + (int64_t)size;
-    if (f == L.num_rows - 1) offs[L.num_rows] = p;
-    ++f;
-  }
-}
-
-// The same offsets with the stores coalesced (round 6): a workgroup per kWG chunks stages
-// their first frame indices, counts and saved positions in LDS, then its threads write
-// consecutive offs[f] -- each finds its chunk by a binary search over the staged frame
-// bases -- where frame_write_kernel had each lane store its own chunk's ~16 offsets at a
-// 128-byte stride from the next lane's (64 partial lines per store instruction). Chunks
+// Chunk k's frames get indices base[k] .. base[k] + count[k] - 1 (count scanned in place),
+// with the stores coalesced (round 6): a workgroup per kWG chunks stages their first frame
+// indices, counts and saved positions in LDS, then its threads write consecutive offs[f] --
+// each finds its chunk by a binary search over the staged frame bases -- where round 5's
+// write pass had each lane store its own chunk's ~16 offsets at a 128-byte stride from the
+// next lane's (64 partial lines per store instruction). Chunks
 // whose positions were not all saved (a fix-up re-walk, > kSaved frames) are walked by
 // their own thread as before.
 __global__ __launch_bounds__(kWG) void frame_write_co_kernel(FrameIndexLaunch L, const uint8_t* __restrict__ rows,

@@ -25,7 +25,6 @@
 #include <string>
 #include <atomic>
 #include <condition_variable>
-#include <deque>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -270,23 +269,18 @@ struct fory_host_ctx {
   uint8_t* hpin = nullptr;     // pinned scratch: level totals, frame end, validity stash
   int64_t hpin_bytes = 0;
   // Pageable caller buffers of the current call (CallScope): each one's page-aligned
-  // interior, in pieces of <= 256 MiB, is registered by a helper thread in the order the
-  // call declared them (ahead of the copies that need them) and unregistered when the
-  // call returns; copies inside a registered piece are direct DMAs, the buffers'
-  // unaligned heads and tails go through the staging.
+  // interior, in pieces of <= 256 MiB, is registered by the calling thread when a copy
+  // first touches it and unregistered when the call returns; copies inside a registered
+  // piece are direct DMAs, the buffers' unaligned heads and tails go through the staging.
+  // (Round 6 first registered on a helper thread, ahead of the copies; a traced suite run
+  // then faulted inside this path, and every HIP call of a context is kept on the calling
+  // thread since: profiles/r06/intermittent/README.md.)
   struct Extent {
     uintptr_t base = 0, end = 0;  // the part of the caller buffer this piece covers
     uintptr_t lo = 0, hi = 0;     // its page-aligned interior
-    std::atomic<int> state{0};    // 0 not registered yet, 1 registered by this call, 2 declined
-    bool taken = false;           // the helper has taken it (under reg_mu)
+    int state = 0;                // 0 not registered yet, 1 registered by this call, 2 declined
   };
-  std::deque<Extent> ext;         // (stable references: the helper works on entries while more are added)
-  std::mutex reg_mu;
-  std::condition_variable reg_cv;
-  std::thread reg_thread;
-  size_t reg_next = 0;            // entries before it are taken
-  Extent* reg_want = nullptr;     // a piece a copy is waiting for: the helper takes it next
-  bool reg_stop = false;
+  std::vector<Extent> ext;
   int64_t reg_calls = 0, reg_bytes = 0;  // statistics: call-scoped registrations over the context's life
   double reg_ms = 0;
   // FORY_ROWFMT_HOST_VERIFY=1 (read at context creation; tests / diagnosis only): after
@@ -302,6 +296,8 @@ struct fory_host_ctx {
   };
   std::vector<VPiece> vcur, vprev;
   int64_t vseq = 0;
+  uint8_t* vpin = nullptr;  // pinned read-back buffer of the verify mode
+  size_t vpin_bytes = 0;
 };
 
 namespace {
@@ -579,15 +575,7 @@ int hcopy_staged(fory_host_ctx* c, void* dst, const void* src, size_t bytes, hip
 // touched pages on MI355X hosts against ~18 ms per GiB of DMA at 57 GB/s
 // (scripts/microbench/reg_probe.hip, profiles/r06/host/), and no byte crosses host memory
 // a second time.
-// Runs on the context's registration helper; the outcome is published in e.state.
-int ext_register_state(fory_host_ctx* c, fory_host_ctx::Extent& e);
-void ext_register(fory_host_ctx* c, fory_host_ctx::Extent& e) {
-  const int st = ext_register_state(c, e);
-  std::lock_guard<std::mutex> lock(c->reg_mu);
-  e.state.store(st);
-  c->reg_cv.notify_all();
-}
-
+// Returns the piece's new state (1 registered, 2 declined).
 int ext_register_state(fory_host_ctx* c, fory_host_ctx::Extent& e) {
   const size_t len = e.hi - e.lo;
   {
@@ -619,28 +607,18 @@ int ext_register_state(fory_host_ctx* c, fory_host_ctx::Extent& e) {
     (void)hipHostUnregister(lo);
     return drop();
   }
-  {
-    std::lock_guard<std::mutex> lock(c->reg_mu);
-    c->reg_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    ++c->reg_calls;
-    c->reg_bytes += (int64_t)len;
-  }
+  c->reg_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  ++c->reg_calls;
+  c->reg_bytes += (int64_t)len;
   std::lock_guard<std::mutex> lock(g_reg_mu);
   g_tmp[e.lo].dev = static_cast<uint8_t*>(a.devicePointer);
   return 1;
 }
 
-// The registration state of piece e once the helper has decided it.
-int ext_wait(fory_host_ctx* c, fory_host_ctx::Extent& e) {
-  int st = e.state.load();
-  if (st) return st;
-  std::unique_lock<std::mutex> lock(c->reg_mu);
-  if (!e.taken) {  // out of order: the helper takes this one next
-    c->reg_want = &e;
-    c->reg_cv.notify_all();
-  }
-  c->reg_cv.wait(lock, [&] { return e.state.load() != 0; });
-  return e.state.load();
+// The registration state of piece e, registering it on first touch.
+int ext_state(fory_host_ctx* c, fory_host_ctx::Extent& e) {
+  if (!e.state) e.state = ext_register_state(c, e);
+  return e.state;
 }
 
 // One copy between caller host memory and the device, queued on stream s. Pinned over
@@ -674,7 +652,7 @@ int hcopy(fory_host_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyK
   for (fory_host_ctx::Extent& e : c->ext) {
     if (rc || cur >= z) break;
     if (e.base >= z || e.end <= cur || e.lo >= z || e.hi <= cur) continue;
-    if (ext_wait(c, e) != 1) continue;
+    if (ext_state(c, e) != 1) continue;
     const uintptr_t x0 = std::max(cur, e.lo), x1 = std::min(z, e.hi);
     if (x1 <= x0) continue;
     rc = piece(cur, x0, false);
@@ -734,27 +712,6 @@ constexpr size_t kRegMin = size_t(4) << 20;  // smaller interiors stay staged
 
 constexpr uintptr_t kRegPiece = uintptr_t(256) << 20;  // registration granularity of big buffers
 
-// The helper: registers the declared pieces in order until the call ends.
-void reg_worker(fory_host_ctx* c) {
-  for (;;) {
-    fory_host_ctx::Extent* e = nullptr;
-    {
-      std::unique_lock<std::mutex> lock(c->reg_mu);
-      for (;;) {
-        while (c->reg_next < c->ext.size() && c->ext[c->reg_next].taken) ++c->reg_next;
-        if (c->reg_want && !c->reg_want->taken) e = c->reg_want;  // a copy waits for it
-        else if (c->reg_next < c->ext.size()) e = &c->ext[c->reg_next];
-        c->reg_want = nullptr;
-        if (e || c->reg_stop) break;
-        c->reg_cv.wait(lock);
-      }
-      if (!e) return;  // stopped with nothing left
-      e->taken = true;
-    }
-    ext_register(c, *e);
-  }
-}
-
 void call_extent(fory_host_ctx* c, const void* p, int64_t bytes) {
   if (!p || bytes <= 0) return;
   const uintptr_t base = reinterpret_cast<uintptr_t>(p), end = base + (uintptr_t)bytes;
@@ -762,50 +719,30 @@ void call_extent(fory_host_ctx* c, const void* p, int64_t bytes) {
   if (hi <= lo || hi - lo < kRegMin) return;
   for (const auto& o : c->ext)
     if (lo < o.hi && o.lo < hi) return;  // (overlapping caller buffers: the first one declared)
-  {
-    std::lock_guard<std::mutex> lock(c->reg_mu);
-    for (uintptr_t x = lo; x < hi; x += kRegPiece) {
-      fory_host_ctx::Extent& e = c->ext.emplace_back();
-      e.lo = x;
-      e.hi = std::min(hi, x + kRegPiece);
-      e.base = x == lo ? base : x;
-      e.end = e.hi == hi ? end : e.hi;
-    }
+  for (uintptr_t x = lo; x < hi; x += kRegPiece) {
+    fory_host_ctx::Extent& e = c->ext.emplace_back();
+    e.lo = x;
+    e.hi = std::min(hi, x + kRegPiece);
+    e.base = x == lo ? base : x;
+    e.end = e.hi == hi ? end : e.hi;
   }
-  if (!c->reg_thread.joinable()) c->reg_thread = std::thread(reg_worker, c);
-  c->reg_cv.notify_all();
 }
 
 struct CallScope {
   fory_host_ctx* c;
   explicit CallScope(fory_host_ctx* ctx) : c(ctx) {
     c->ext.clear();
-    c->reg_next = 0;
-    c->reg_want = nullptr;
-    c->reg_stop = false;
     c->vcur.clear();
     c->vprev.clear();
   }
   ~CallScope() {
-    if (c->reg_thread.joinable()) {
-      {
-        std::lock_guard<std::mutex> lock(c->reg_mu);
-        c->reg_stop = true;
-        // pieces the helper has not taken: never registered
-        for (auto& e : c->ext)
-          if (!e.taken) e.taken = true, e.state.store(2);
-        c->reg_want = nullptr;
-      }
-      c->reg_cv.notify_all();
-      c->reg_thread.join();
-    }
     bool any = false;
-    for (const auto& e : c->ext) any |= e.state.load() == 1;
+    for (const auto& e : c->ext) any |= e.state == 1;
     if (any)
       for (hipStream_t s : {c->s_in, c->s_k, c->s_out})
         if (s) (void)hipStreamSynchronize(s);
     for (const auto& e : c->ext) {
-      if (e.state.load() != 1) continue;
+      if (e.state != 1) continue;
       (void)hipHostUnregister(reinterpret_cast<void*>(e.lo));
       (void)hipGetLastError();
       std::lock_guard<std::mutex> lock(g_reg_mu);
@@ -823,19 +760,27 @@ struct CallScope {
 int verify_pieces(fory_host_ctx* c, hipStream_t s, int64_t chunk) {
   if (!c->verify) return FORY_OK;
   int rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize(verify)");
-  std::vector<uint8_t> got;
   for (size_t i = 0; i < c->vcur.size() && !rc; ++i) {
     const auto& v = c->vcur[i];
-    got.resize(v.bytes);
-    rc = hip_check(hipMemcpy(got.data(), v.dev, v.bytes, hipMemcpyDeviceToHost), "hipMemcpy(verify)");
-    if (rc || !std::memcmp(got.data(), v.host, v.bytes)) continue;
+    if (v.bytes > c->vpin_bytes) {  // read back through pinned memory (no pageable runtime copy)
+      if (c->vpin) (void)hipHostFree(c->vpin);
+      c->vpin = nullptr, c->vpin_bytes = 0;
+      rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&c->vpin), v.bytes, hipHostMallocCoherent),
+                     "hipHostMalloc(verify)");
+      if (rc) break;
+      c->vpin_bytes = v.bytes;
+    }
+    uint8_t* got = c->vpin;
+    rc = hip_check(hipMemcpyAsync(got, v.dev, v.bytes, hipMemcpyDeviceToHost, s), "hipMemcpyAsync(verify)");
+    if (!rc) rc = hip_check(hipStreamSynchronize(s), "hipStreamSynchronize(verify)");
+    if (rc || !std::memcmp(got, v.host, v.bytes)) continue;
     size_t first = 0, wrong = 0;
     while (got[first] == v.host[first]) ++first;
     for (size_t b = 0; b < v.bytes; ++b) wrong += got[b] != v.host[b];
     std::string like = "no other piece's source";
     for (const auto* list : {&c->vcur, &c->vprev})
       for (const auto& o : *list)
-        if (o.seq != v.seq && o.bytes >= 64 && !std::memcmp(got.data() + first, o.host + std::min(first, o.bytes - 64), 64))
+        if (o.seq != v.seq && o.bytes >= 64 && !std::memcmp(got + first, o.host + std::min(first, o.bytes - 64), 64))
           like = "piece " + std::to_string(o.seq) + " (" + o.what + ", " + std::to_string(o.bytes) + " bytes)";
     rc = fail_host(FORY_ERR_DEVICE, "host verify: chunk " + std::to_string(chunk) + " piece " + std::to_string(v.seq) +
                                         " (" + v.what + ", " + std::to_string(v.bytes) + " bytes): " +
@@ -854,8 +799,12 @@ int sync_all(fory_host_ctx* c) {
   int rc = hip_check(hipStreamSynchronize(c->s_out), "hipStreamSynchronize(out)");
   const int rk = hip_check(hipStreamSynchronize(c->s_k), "hipStreamSynchronize(kernels)");
   const int ri = hip_check(hipStreamSynchronize(c->s_in), "hipStreamSynchronize(in)");
-  const int rs = stage_drain(c->stage);
-  return rc ? rc : (rk ? rk : (ri ? ri : rs));
+  if (rc || rk || ri) {  // (the first failure keeps the error message; nothing staged is owed any more)
+    stage_abandon(c->stage);
+    const int first = rc ? rc : (rk ? rk : ri);
+    return first;
+  }
+  return stage_drain(c->stage);
 }
 
 // Chunk k's row range.
@@ -991,6 +940,7 @@ void fory_rowfmt_host_ctx_destroy(fory_host_ctx* c) {
       if (e) (void)hipEventDestroy(e);
   if (c->stage.smem) (void)hipHostFree(c->stage.smem);
   if (c->hpin) (void)hipHostFree(c->hpin);
+  if (c->vpin) (void)hipHostFree(c->vpin);
   delete c;
 }
 
