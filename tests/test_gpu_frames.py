@@ -182,11 +182,12 @@ def test_mixed_stream_decode_large():
     assert torch.equal(offs, rows.offsets)
 
 
-@pytest.mark.parametrize("per", ["1", "2", "4"])
+@pytest.mark.parametrize("per", ["1", "2", "4", "64"])
 def test_stream_decode_small_chunks_many_fixups(per, monkeypatch):
     """Chunks of 1-4 frames' bytes (FORY_ROWFMT_IDXFRAMES): many chunks hold no frame
     start or a misleading one, so most of the chain goes through the fix-up, which
-    visits only dirty chunks and the chunks whose entry it moved."""
+    visits only dirty chunks and the chunks whose entry it moved. 64: chunks of more
+    frames than the spec walk saves, walked again by the write pass (with their sizes)."""
     monkeypatch.setenv("FORY_ROWFMT_IDXFRAMES", per)
     schema, make = catalog()["mixed40_nulls"]
     check_stream("mixed40_nulls", schema, make(6000, 17), 6000)
@@ -195,3 +196,37 @@ def test_stream_decode_small_chunks_many_fixups(per, monkeypatch):
     h = enc.plan.schema_hash
     cols = _adversarial_columns(800, h if h < 2**63 else h - 2**64, enc.plan.fixed_size, 5, 41)
     check_stream("adversarial", schema, cols, 800)
+
+
+def test_stream_sizes_corrupt_slot():
+    """A string slot whose size runs past its row (frame 200): CorruptRowException from
+    the decode's sizing pass; the same damage in a frame past the N decoded is never read."""
+    schema, make = catalog()["mixed40"]
+    n = 500
+    cols = make(n, 4)
+    expect, eoffs = oracle.encode(schema, cols, n, 1)
+    enc = encoder_for("mixed40", schema)
+    first_string = next(i for i, f in enumerate(schema.fields) if f.type.id == ArrowType.STRING)
+    slot = 12 + ((len(schema.fields) + 63) // 64) * 8 + 8 * first_string  # size word of its slot
+    for frame, rows, raises in ((200, n, True), (450, 400, False)):
+        bad = expect.copy()
+        at = int(eoffs[frame]) + slot
+        bad[at:at + 4] = np.frombuffer(struct.pack("<i", 0x7fff0000), np.uint8)
+        if raises:
+            with pytest.raises(CorruptRowException):
+                enc.decode(device_bytes(bad), rows, 1)
+        else:
+            dec = to_host(enc.decode(device_bytes(bad), rows, 1))
+            assert columns_equal(schema, [_head(c, rows) for c in cols], dec) == []
+
+
+def _head(c, rows):
+    """The first `rows` records of a host column."""
+    from fury_amd.format.columns import pack_validity, unpack_validity
+    if c.offsets is not None:
+        o = c.offsets[:rows + 1]
+        v = c.values[:int(o[-1])] if c.values is not None else None
+    else:
+        o, v = None, c.values[:rows]
+    val = pack_validity(unpack_validity(c.validity, c.length)[:rows]) if c.validity is not None else None
+    return HostColumn(v, o, val, rows)
