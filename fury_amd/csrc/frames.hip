@@ -36,7 +36,7 @@ constexpr int64_t kNone = -1;    // chunk holds no candidate frame start
 constexpr int64_t kBroken = -2;  // the chain hit a size out of range
 // Frame starts the spec walk saves per chunk (uint16 offsets from the chunk base,
 // chunk <= 64 KiB), stored position-major (pos[j * chunks + k]) so the write pass
-// reads them coalesced; chunks target ~16 frames.
+// reads them coalesced; chunks target ~20 frames.
 constexpr int kSaved = 32;
 
 // Frame header at p (4-byte aligned offset into the stream): size field and hash.
@@ -269,10 +269,12 @@ __global__ __launch_bounds__(kWG) void frame_write_co_kernel(FrameIndexLaunch L,
 }  // namespace
 
 void frame_index_plan(int64_t num_rows, int64_t rows_bytes, int32_t idx_frames, int64_t* chunk, int64_t* chunks) {
-  // ~16 frames per chunk at the batch's mean frame size, in [1, 64] KiB
-  // (the plan's FORY_ROWFMT_IDXFRAMES knob overrides the 16, for A/B)
+  // ~20 frames per chunk at the batch's mean frame size, in [1, 64] KiB (the plan's
+  // FORY_ROWFMT_IDXFRAMES knob overrides the 20, for A/B). Round 6, three alternating
+  // rounds on one box (profiles/r06/idxframes/): index 0.78 -> 0.70-0.73 ms (Mixed 16Mi),
+  // 0.336 -> 0.317 ms (Nested 8Mi) against 16; 24 was between them.
   const int64_t n = num_rows > 0 ? num_rows : 1;
-  const int64_t per = idx_frames > 0 ? idx_frames : 16;
+  const int64_t per = idx_frames > 0 ? idx_frames : 20;
   int64_t c = (per * (rows_bytes / n) + 255) / 256 * 256;
   c = c < 1024 ? 1024 : (c > 65536 ? 65536 : c);
   *chunk = c;

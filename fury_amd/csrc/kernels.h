@@ -234,7 +234,7 @@ struct FrameIndexLaunch {
   int64_t num_rows;
   int64_t schema_hash;
   int32_t fixed_size;
-  int32_t idx_frames;  // frames per chunk (0 = 16; LaunchKnobs::idx_frames)
+  int32_t idx_frames;  // frames per chunk (0 = 20; LaunchKnobs::idx_frames)
   int64_t chunk;   // bytes per chunk (frame_index_plan)
   int64_t chunks;
 };
