@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 6: the whole GPU suite (untraced, one process) and smoke on the final library, with
+# this box's encode probe first. Usage: gpu_final.sh TAG (output under gpurun_out/TAG).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/${1:-r06final}
+mkdir -p $O
+bash scripts/r06/gpu_box.sh || exit $?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+sha256sum fury_amd/lib/libfory_rowfmt.so | cut -c1-16 > $O/lib_sha16.txt
