@@ -9,8 +9,17 @@ KOBJS := fury_amd/lib/fixed.o fury_amd/lib/scan.o fury_amd/lib/varlen.o fury_amd
 HDRS := fury_amd/csrc/kernels.h fury_amd/csrc/kcommon.h fury_amd/csrc/gen_device.h fury_amd/csrc/plan.h include/fory_rowfmt.h
 
 CAPI_TEST := tests/c/capi_roundtrip
+MOCK_TEST := tests/c/host_copy_mock
 
-all: $(LIB) $(ORACLE) $(CAPI_TEST)
+all: $(LIB) $(ORACLE) $(CAPI_TEST) $(MOCK_TEST)
+
+# The host path's copy machinery (host.cpp) on the CPU against a mock HIP runtime whose DMAs
+# run late (tests/test_host_copy_mock.py): small staging blocks and registration pieces so a
+# few MiB exercise reuse; host code only, under ASan + UBSan.
+$(MOCK_TEST): tests/c/host_copy_mock.cpp fury_amd/csrc/host.cpp include/fory_rowfmt.h $(HDRS)
+	g++ -O1 -g -std=c++17 -Wall -Wno-unused-function -D__HIP_PLATFORM_AMD__ -DFORY_STAGE_BLOCK_MB=1 -DFORY_STAGE_BLOCKS=4 \
+	  -DFORY_REG_MIN_KB=64 -DFORY_REG_PIECE_KB=1024 -fsanitize=address,undefined -fno-omit-frame-pointer \
+	  -I/opt/rocm/include -Ifury_amd/csrc fury_amd/csrc/host.cpp tests/c/host_copy_mock.cpp -o $@ -lpthread
 
 # C driver of the C-ABI (GPU test tests/test_gpu_capi_c.py): plain C + HIP runtime C API
 $(CAPI_TEST): tests/c/capi_roundtrip.c include/fory_rowfmt.h $(LIB) $(ORACLE)

@@ -708,9 +708,15 @@ int ensure_hpin(fory_host_ctx* c, int64_t bytes) {
 // is drained (normally done already by sync_all) and every registration of the call
 // removed, so no caller page stays pinned past the call and no later copy can take a
 // mapping of it for a direct DMA.
-constexpr size_t kRegMin = size_t(4) << 20;  // smaller interiors stay staged
+#ifndef FORY_REG_MIN_KB  // (the CPU mock test, tests/c/host_copy_mock.cpp, shrinks both)
+#define FORY_REG_MIN_KB 4096
+#endif
+#ifndef FORY_REG_PIECE_KB
+#define FORY_REG_PIECE_KB (256 * 1024)
+#endif
+constexpr size_t kRegMin = size_t(FORY_REG_MIN_KB) << 10;  // smaller interiors stay staged
 
-constexpr uintptr_t kRegPiece = uintptr_t(256) << 20;  // registration granularity of big buffers
+constexpr uintptr_t kRegPiece = uintptr_t(FORY_REG_PIECE_KB) << 10;  // registration granularity of big buffers
 
 void call_extent(fory_host_ctx* c, const void* p, int64_t bytes) {
   if (!p || bytes <= 0) return;
@@ -736,11 +742,12 @@ struct CallScope {
     c->vprev.clear();
   }
   ~CallScope() {
-    bool any = false;
-    for (const auto& e : c->ext) any |= e.state == 1;
-    if (any)
-      for (hipStream_t s : {c->s_in, c->s_k, c->s_out})
-        if (s) (void)hipStreamSynchronize(s);
+    // whatever path the call returns by (an error return skips sync_all): every queued copy
+    // done and every owed D2H host copy made while the caller's buffers are still this
+    // call's, then the call's registrations removed. After a normal return both are no-ops.
+    for (hipStream_t s : {c->s_in, c->s_k, c->s_out})
+      if (s) (void)hipStreamSynchronize(s);
+    if (stage_drain(c->stage)) stage_abandon(c->stage);
     for (const auto& e : c->ext) {
       if (e.state != 1) continue;
       (void)hipHostUnregister(reinterpret_cast<void*>(e.lo));
@@ -2131,6 +2138,38 @@ extern "C" int fory_rowfmt_internal_host_call_regs(const fory_host_ctx* c, int64
   std::lock_guard<std::mutex> lock(g_reg_mu);
   return (int)g_tmp.size();
 }
+// Library-internal, for tests of the copy machinery alone: one call's worth of copies
+// through hcopy, then the end-of-call drain. The caller buffers decl[0..ndecl) are declared
+// for the call, as the host entry points declare theirs, so they are registered for it.
+// Staged pieces go through the ring and small pieces through the small buffers.
+// kinds[i]: 1 = H2D, 2 = D2H; streams[i]: 0 = in, 1 = kernels, 2 = out. On the GPU it is one
+// more parity check. On the CPU, tests/c/host_copy_mock.cpp links host.cpp against a
+// mock HIP runtime whose DMAs run late, so a staging block rewritten, or a registration
+// dropped, before its DMA ran shows up as wrong bytes or a logged violation.
+// flags & 1: return right after queuing the copies, as an error return does (CallScope then
+// drains them).
+extern "C" int fory_rowfmt_internal_host_copies(fory_host_ctx* c, int32_t n, void* const* dst,
+                                                const void* const* src, const int64_t* bytes,
+                                                const int32_t* kinds, const int32_t* streams, int32_t ndecl,
+                                                const void* const* decl, const int64_t* decl_bytes, int32_t flags) {
+  if (!c || n < 0 || (n > 0 && (!dst || !src || !bytes || !kinds || !streams)) || ndecl < 0 ||
+      (ndecl > 0 && (!decl || !decl_bytes)))
+    return fail_host(FORY_ERR_INVALID_ARGUMENT, "host_copies: bad arguments");
+  int rc = hip_check(hipSetDevice(c->device), "hipSetDevice");
+  if (rc) return rc;
+  CallScope scope(c);
+  for (int32_t i = 0; i < ndecl; ++i) call_extent(c, decl[i], decl_bytes[i]);
+  for (int32_t i = 0; i < n && !rc; ++i) {
+    if (kinds[i] != 1 && kinds[i] != 2) return fail_host(FORY_ERR_INVALID_ARGUMENT, "host_copies: kind");
+    hipStream_t s = streams[i] == 0 ? c->s_in : (streams[i] == 1 ? c->s_k : c->s_out);
+    rc = hcopy(c, dst[i], src[i], (size_t)bytes[i], kinds[i] == 1 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, s,
+               "host_copies");
+  }
+  if (flags & 1) return rc;
+  const int rs = sync_all(c);
+  return rc ? rc : rs;
+}
+
 // The staged copies' host memcpy (CopyPool), for a CPU test of its split.
 extern "C" void fory_rowfmt_internal_pool_copy(void* dst, const void* src, int64_t n) {
   CopyPool::get().copy(dst, src, (size_t)n);
