@@ -193,6 +193,25 @@ __device__ __forceinline__ void td_scalar(const GNode& nd, const ColumnDev& col,
 // in order: nf fields kids[k0..], bm bitmap bytes. Lanes of a wave hold consecutive
 // instances from a 64-aligned one (inb: the lane's instance is in this call's range);
 // every lane runs it (validity by ballot).
+// The instance's bitmap / slot bytes at p (4-byte aligned), 4 or 8 of them: LDS loads from
+// the wave's staged image (IMG), global loads from the rows otherwise. (One generic pointer
+// for both compiled to flat loads, which wait on both counters.)
+template <bool IMG>
+__device__ __forceinline__ uint64_t td_hget(const uint8_t* p, int w) {
+  uint32_t lo, hi = 0;
+  if constexpr (IMG) {
+    const __attribute__((address_space(3))) uint32_t* q = (const __attribute__((address_space(3))) uint32_t*)p;
+    lo = q[0];
+    if (w == 8) hi = q[1];
+  } else {
+    const GAS uint32_t* q = (const GAS uint32_t*)p;
+    lo = q[0];
+    if (w == 8) hi = q[1];
+  }
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+template <bool IMG = false>
 __device__ __forceinline__ void td_instance(const GenLaunch& L, const TdTables* T, int nf, int k0, int bm, int64_t k,
                                             bool inb, int64_t base, int64_t rend, const uint8_t* rows,
                                             int32_t* status, const uint8_t* img = nullptr) {
@@ -206,9 +225,9 @@ __device__ __forceinline__ void td_instance(const GenLaunch& L, const TdTables* 
   // before any is used, so an instance costs one memory latency per batch, not per field
   for (int q0 = 0; q0 < nf; q0 += kTdBatch) {
     uint64_t sv[kTdBatch];
-    if ((q0 & 63) == 0) nulls = rd ? gget(hb + (q0 >> 3), bm - (q0 >> 3) >= 8 ? 8 : 4) : ~0ull;
+    if ((q0 & 63) == 0) nulls = rd ? td_hget<IMG>(hb + (q0 >> 3), bm - (q0 >> 3) >= 8 ? 8 : 4) : ~0ull;
 #pragma unroll
-    for (int u = 0; u < kTdBatch; ++u) sv[u] = rd && q0 + u < nf ? gget(hb + bm + 8 * (q0 + u), 8) : 0;
+    for (int u = 0; u < kTdBatch; ++u) sv[u] = rd && q0 + u < nf ? td_hget<IMG>(hb + bm + 8 * (q0 + u), 8) : 0;
 #pragma unroll 1
     for (int u = 0; u < kTdBatch; ++u) {  // rolled: one copy of the field body
       const int q = q0 + u;
@@ -292,7 +311,7 @@ __global__ __launch_bounds__(kTdWG) void td_fields_kernel(GenLaunch L, const TdT
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    td_instance(L, T, nf, k0, bm, k, inb, base, rend, rows, status, wimg + (size_t)lane * FS);
+    td_instance<true>(L, T, nf, k0, bm, k, inb, base, rend, rows, status, wimg + (size_t)lane * FS);
     return;
   }
   td_instance(L, T, nf, k0, bm, k, inb, base, rend, rows, status);

@@ -168,53 +168,88 @@ __global__ __launch_bounds__(kWG) void var_sizes_kernel(VarLaunch L, const Op* _
 // is loaded before any is used (unrolled batches), so a row costs one memory latency
 // per batch rather than one per op.
 constexpr int kSizeBatch = 8;
+// Rows per thread of the sizing kernel: the rows of a workgroup's 256 x kSizeRows block,
+// kWG apart, so every load stays coalesced; all their loads are issued before any is used.
+// One row per thread left each wave bound by two serial round trips (the field table,
+// then the columns): round 6, Mixed encode sizing 0.47 -> 0.27 ms.
+constexpr int kSizeRows = 4;
 
 __global__ __launch_bounds__(kWG) void var_sizes_flat_kernel(VarLaunch L, const VarFieldDev* __restrict__ vf,
                                                              const StructDev* __restrict__ st, int64_t* sizes) {
-  const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
-  if (i >= L.num_rows) return;
-  int64_t size = L.fixed_size + frame_header_bytes(L.frame);
-  uint32_t present = 1;  // bit id: struct id present (id 0 = the row)
+  const int64_t i0 = (int64_t)blockIdx.x * (kWG * kSizeRows) + threadIdx.x;
+  int64_t size[kSizeRows];
+  uint32_t present[kSizeRows];  // bit id: struct id present (id 0 = the row)
+#pragma unroll
+  for (int r = 0; r < kSizeRows; ++r) {
+    size[r] = L.fixed_size + frame_header_bytes(L.frame);
+    present[r] = 1;
+  }
   if (L.num_struct) {
-    bool valid[kMaxTileStructs];
+    uint32_t valid[kSizeRows];  // bit s: struct s's validity bit (a mask, not a bool array: no scratch)
+#pragma unroll
+    for (int r = 0; r < kSizeRows; ++r) valid[r] = 0;
 #pragma unroll
     for (int s = 0; s < kMaxTileStructs; ++s) {
-      valid[s] = true;
-      if (s < L.num_struct && (st[s].flags & 1) && st[s].validity) valid[s] = (st[s].validity[i >> 3] >> (i & 7)) & 1;
+      const bool nullable = s < L.num_struct && (st[s].flags & 1) && st[s].validity;
+#pragma unroll
+      for (int r = 0; r < kSizeRows; ++r) {
+        const int64_t i = i0 + r * kWG;
+        uint32_t v = 1;
+        if (nullable && i < L.num_rows) v = (gp(st[s].validity)[i >> 3] >> (i & 7)) & 1;
+        valid[r] |= v << s;
+      }
     }
 #pragma unroll
     for (int s = 0; s < kMaxTileStructs; ++s) {
       if (s >= L.num_struct) break;
-      if (valid[s] && ((present >> st[s].parent) & 1)) {
-        present |= 1u << (s + 1);
-        size += st[s].hdr + 8LL * st[s].nfields;
-      }
+#pragma unroll
+      for (int r = 0; r < kSizeRows; ++r)
+        if (((valid[r] >> s) & 1) && ((present[r] >> st[s].parent) & 1)) {
+          present[r] |= 1u << (s + 1);
+          size[r] += st[s].hdr + 8LL * st[s].nfields;
+        }
     }
   }
   for (int v0 = 0; v0 < L.num_var; v0 += kSizeBatch) {
-    int32_t a[kSizeBatch], b[kSizeBatch];
-    bool on[kSizeBatch];
+    int32_t a[kSizeRows][kSizeBatch], b[kSizeRows][kSizeBatch];
+    uint32_t vb[kSizeRows][kSizeBatch];
 #pragma unroll
     for (int k = 0; k < kSizeBatch; ++k) {
       const int v = v0 + k;
-      a[k] = b[k] = 0;
-      on[k] = false;
+#pragma unroll
+      for (int r = 0; r < kSizeRows; ++r) a[r][k] = b[r][k] = 0, vb[r][k] = 0xffu;
       if (v < L.num_var) {
         const VarFieldDev& f = vf[v];
-        on[k] = ((present >> f.parent) & 1) && (!(f.flags & 1) || !f.validity || ((f.validity[i >> 3] >> (i & 7)) & 1));
-        a[k] = f.offsets[i];
-        b[k] = f.offsets[i + 1];
+        const bool nullable = (f.flags & 1) && f.validity;
+#pragma unroll
+        for (int r = 0; r < kSizeRows; ++r) {
+          const int64_t i = i0 + r * kWG;
+          if (i >= L.num_rows) continue;
+          if (nullable) vb[r][k] = gp(f.validity)[i >> 3];
+          a[r][k] = gp(f.offsets)[i];
+          b[r][k] = gp(f.offsets)[i + 1];
+        }
       }
     }
 #pragma unroll
     for (int k = 0; k < kSizeBatch; ++k) {
       const int v = v0 + k;
-      if (v >= L.num_var || !on[k]) continue;
-      const int64_t n = (int64_t)b[k] - a[k];
-      size += vf[v].is_list ? 8 + bitmap_bytes(n) + round8(n * vf[v].w) : round8(n);
+      if (v >= L.num_var) break;
+      const VarFieldDev& f = vf[v];
+#pragma unroll
+      for (int r = 0; r < kSizeRows; ++r) {
+        const int64_t i = i0 + r * kWG;
+        if (!((present[r] >> f.parent) & 1) || !((vb[r][k] >> (i & 7)) & 1)) continue;
+        const int64_t n = (int64_t)b[r][k] - a[r][k];
+        size[r] += f.is_list ? 8 + bitmap_bytes(n) + round8(n * f.w) : round8(n);
+      }
     }
   }
-  sizes[i] = size;
+#pragma unroll
+  for (int r = 0; r < kSizeRows; ++r) {
+    const int64_t i = i0 + r * kWG;
+    if (i < L.num_rows) *gp(sizes + i) = size[r];
+  }
 }
 
 constexpr int kFixBatch = 8;  // consecutive OP_FIXED ops whose loads are issued together
@@ -3131,7 +3166,8 @@ hipError_t launch_var_sizes(const VarLaunch& L, int64_t* d_row_offsets, hipStrea
   if (L.num_rows <= 0) return hipSuccess;
   const int64_t blocks = (L.num_rows + kWG - 1) / kWG;
   if (L.flat && !L.kn.sizes_program)  // (A/B knob of the plan)
-    hipLaunchKernelGGL(var_sizes_flat_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.vf, L.st, d_row_offsets);
+    hipLaunchKernelGGL(var_sizes_flat_kernel, dim3((unsigned)((L.num_rows + kWG * kSizeRows - 1) / (kWG * kSizeRows))),
+                       dim3(kWG), 0, s, L, L.vf, L.st, d_row_offsets);
   else
     hipLaunchKernelGGL(var_sizes_kernel, dim3((unsigned)blocks), dim3(kWG), 0, s, L, L.prog, L.cols, d_row_offsets);
   return hipGetLastError();
