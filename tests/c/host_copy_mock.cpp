@@ -401,6 +401,9 @@ int run_call(fory_host_ctx* c, const std::vector<Piece>& ps, const std::vector<s
 // from a byte to several staging blocks, on random streams; per call, every host piece is
 // distinct memory. After the call: every H2D's device bytes equal the source, every D2H's
 // host bytes equal the device source.
+// flags & 2 (test side, not passed on): the caller registers its first buffer itself
+// (fory_rowfmt_host_register) before the call and unregisters it after; the call's own
+// registration must decline it and its copies go direct through the caller's mapping.
 void scenario_mixed(fory_host_ctx* c, const char* name, int calls, int pieces, size_t max_piece, uint64_t seed,
                     bool declare, int32_t flags) {
   std::mt19937_64 r(seed);
@@ -420,6 +423,9 @@ void scenario_mixed(fory_host_ctx* c, const char* name, int calls, int pieces, s
       big[i].resize((size_t)pieces * max_piece / nbuf + 4096 + (size_t)(r() % 4096));
       bigdev[i] = dev_alloc(big[i].size());
       if (declare) decl.push_back({big[i].data(), (int64_t)big[i].size()});
+      if ((flags & 2) && i == 0)
+        expect(fory_rowfmt_host_register(big[0].data(), (int64_t)big[0].size()) == FORY_OK, name,
+               "host_register: " + g_err);
     }
     std::vector<int> which;
     for (int i = 0; i < pieces; ++i) {
@@ -444,7 +450,7 @@ void scenario_mixed(fory_host_ctx* c, const char* name, int calls, int pieces, s
       const uint8_t* from = static_cast<const uint8_t*>(ps[i].src);
       want[i].assign(from, from + ps[i].n);
     }
-    const int rc = run_call(c, ps, decl, flags);
+    const int rc = run_call(c, ps, decl, flags & 1);
     expect(rc == FORY_OK, name, "call failed: " + g_err);
     for (size_t i = 0; i < ps.size(); ++i) {
       const uint8_t* got = static_cast<const uint8_t*>(ps[i].dst);
@@ -460,6 +466,8 @@ void scenario_mixed(fory_host_ctx* c, const char* name, int calls, int pieces, s
     int64_t regs[3];
     const int alive = fory_rowfmt_internal_host_call_regs(c, regs);
     expect(alive == 0, name, "call-scoped registrations alive after the call: " + std::to_string(alive));
+    if (flags & 2)
+      expect(fory_rowfmt_host_unregister(big[0].data()) == FORY_OK, name, "host_unregister: " + g_err);
     for (uint8_t* d : bigdev) (void)hipFree(d);
   }
 }
@@ -490,6 +498,7 @@ int main(int argc, char** argv) {
       {"declared buffers, DMAs progress randomly", 4, 5, 60, 2u << 20, true, 0},
       {"declared buffers, small pieces", 2, 3, 6000, 8192, true, 0},
       {"declared buffers, the call returns before its drain", 0, 5, 60, 2u << 20, true, 1},
+      {"declared buffers, one registered by the caller", 2, 4, 60, 2u << 20, true, 2},
   };
   for (const auto& k : cases) {
     g_progress = k.progress;

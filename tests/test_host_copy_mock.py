@@ -62,7 +62,7 @@ def test_host_copies_against_late_dmas(seed):
     bad = [l for l in lines if "failed" in l]
     assert rc == 0 and summary.get("summary") and summary["failures"] == 0 and summary["violations"] == 0, bad[:5]
     # every scenario ran, and the paths it is meant to reach were reached
-    assert sum(1 for l in lines if l.get("ok") is True) == 8
+    assert sum(1 for l in lines if l.get("ok") is True) == 9
     assert summary["staged_pieces"] > 10000 and summary["call_registrations"] > 100
 
 
