@@ -12,22 +12,6 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
 
 
-# The host-path files run last in a session. They register and unregister host memory (the
-# registration API, and call-scoped registration of large pageable buffers). Every
-# unexplained illegal address of rounds 2-6 came in a process after such churn, in whatever
-# device test ran next (profiles/r06/intermittent/README.md). Last, a recurrence can be
-# charged only to the host path itself, not to an unrelated kernel's parity case. The
-# files' own order is kept.
-_HOST_PATH_LAST = ("test_gpu_host.py", "test_gpu_host_copies.py", "test_gpu_windows.py")
-
-
-def pytest_collection_modifyitems(session, config, items):
-    def rank(item):
-        name = os.path.basename(str(item.fspath))
-        return _HOST_PATH_LAST.index(name) + 1 if name in _HOST_PATH_LAST else 0
-    items[:] = sorted(items, key=rank)  # (stable: every other test keeps its place)
-
-
 @pytest.fixture(scope="session")
 def golden():
     import json
