@@ -903,9 +903,16 @@ int fory_rowfmt_host_ctx_create(const fory_plan* plan, int32_t device, int64_t c
     p += align_up(c->ws_bytes);
     c->buf[b].status = reinterpret_cast<int32_t*>(p);
   }
-  rc = hip_check(hipMemset(c->arena, 0, (size_t)(2 * per)), "hipMemset");
   for (hipStream_t* s : {&c->s_in, &c->s_k, &c->s_out})
     if (!rc) rc = hip_check(hipStreamCreateWithFlags(s, hipStreamNonBlocking), "hipStreamCreate");
+  // The arena is zeroed on the context's own stream and waited for here. Until round 6 this
+  // was a hipMemset on the null stream, which non-blocking streams do not wait for, and it
+  // may still run when hipMemset returns. A first call's H2D copies on s_in could then land
+  // before the fill and be zeroed by it: chunk 0's kernels read zero columns. That is the
+  // "first chunk of a fresh context wrong" failure of rounds 5 and 6
+  // (profiles/r06/intermittent/README.md §6).
+  if (!rc) rc = hip_check(hipMemsetAsync(c->arena, 0, (size_t)(2 * per), c->s_in), "hipMemsetAsync(arena)");
+  if (!rc) rc = hip_check(hipStreamSynchronize(c->s_in), "hipStreamSynchronize(arena)");
   for (int b = 0; b < 2 && !rc; ++b)
     for (hipEvent_t* e : {&c->ev_in[b], &c->ev_k[b], &c->ev_out[b]})
       if (!rc) rc = hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");

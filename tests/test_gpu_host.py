@@ -52,6 +52,30 @@ def test_host_pipeline_parity(name, n, frame):
     hp.close()
 
 
+@pytest.mark.parametrize("frame", [0, 1])
+def test_host_fresh_context_while_the_null_stream_is_busy(frame):
+    """A context created and used at once while the device's null stream is still busy
+    (torch's current stream, here a spin kernel). Until round 6 the context zeroed its
+    arena with a null-stream hipMemset, which its non-blocking streams do not wait for:
+    the first call's H2D copies could land first and be zeroed, so chunk 0 encoded zero
+    columns (the first-chunk failures of rounds 5 and 6, profiles/r06/intermittent/README.md
+    §6). Now the arena is zeroed on the context's own stream and waited for."""
+    schema, make = catalog()["struct104"]
+    n = 5000
+    cols = make(n, 11)
+    expect, _ = oracle.encode(schema, cols, n, frame)
+    plan = NativePlan(schema)
+    for _ in range(3):
+        torch.cuda._sleep(50_000_000)  # ~20 ms of spinning on the current stream
+        hp = HostPipeline(plan, chunk_rows=1024)
+        out = np.zeros(expect.nbytes, np.uint8)
+        hp.encode(cols, n, frame, out)
+        bad = np.nonzero(out != expect)[0]
+        assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}, rows {np.unique(bad // (expect.nbytes // n))[:4]}"
+        hp.close()
+    torch.cuda.synchronize()
+
+
 def test_host_pipeline_registered_buffers_and_errors():
     schema, make = catalog()["struct104"]
     n = 3000
