@@ -7,7 +7,7 @@
 #    bytes, no fault;
 # 3. the same test and the whole host file against the fixed library.
 set -o pipefail
-O=gpurun_out/${1:-r06q}
+O=gpurun_out/r06q
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 120 scripts/microbench/bin/memset_race 5 100000000 > $O/memset_race.jsonl 2>&1 || { cat $O/memset_race.jsonl; exit 1; }

@@ -12,7 +12,11 @@
 //   3. an H2D of 0xAB bytes into buf goes on a non-blocking stream, which is synchronised;
 //   4. after a device sync, buf is counted for zero bytes.
 // Then the fixed protocol: hipMemsetAsync on the non-blocking stream and a stream sync before
-// the copy. Usage: memset_race <trials> <spin cycles>
+// the copy. Two more protocols keep the old hipMemset but make a call between it and the copy
+// that the library's first encode makes on a fresh context (a pinned staging allocation,
+// hipHostMalloc; a device allocation, hipMalloc): if such a call waits for the null stream,
+// the race cannot hit through that path. The last protocol is the old library's exact
+// order: hipMemset, then three non-blocking streams created, and the copy on the first. Usage: memset_race <trials> <spin cycles>
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -52,27 +56,41 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> got(n);
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  for (int fixed = 0; fixed < 2; ++fixed) {
+  const char* names[5] = {"hipMemset (null stream)", "memsetAsync on the stream + sync",
+                          "hipMemset, then hipHostMalloc", "hipMemset, then hipMalloc",
+                          "hipMemset, then 3 new non-blocking streams (old library order)"};
+  for (int fixed = 0; fixed < 5; ++fixed) {
     for (int t = 0; t < trials; ++t) {
       CK(hipMemset(flag, 0, sizeof(int)));
       CK(hipDeviceSynchronize());
       hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, 0, spin, flag);  // the null stream
       const auto t0 = std::chrono::steady_clock::now();
-      if (!fixed) {
+      void* extra = nullptr;
+      if (fixed != 1) {
         CK(hipMemset(buf, 0, n));  // the round-5/6 arena zeroing
       } else {
         CK(hipMemsetAsync(buf, 0, n, s));  // the fix: on the context's stream, waited for
         CK(hipStreamSynchronize(s));
       }
+      if (fixed == 2) CK(hipHostMalloc(&extra, size_t(16) << 20, hipHostMallocPortable | hipHostMallocCoherent));
+      if (fixed == 3) CK(hipMalloc(&extra, size_t(16) << 20));
+      hipStream_t fresh[3] = {};
+      if (fixed == 4)
+        for (hipStream_t& f : fresh) CK(hipStreamCreateWithFlags(&f, hipStreamNonBlocking));
+      hipStream_t cs = fixed == 4 ? fresh[0] : s;
       const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-      CK(hipMemcpyAsync(buf, src, n, hipMemcpyHostToDevice, s));  // nothing on the null stream before it
-      CK(hipStreamSynchronize(s));
+      CK(hipMemcpyAsync(buf, src, n, hipMemcpyHostToDevice, cs));  // nothing on the null stream before it
+      CK(hipStreamSynchronize(cs));
       CK(hipDeviceSynchronize());
       CK(hipMemcpy(got.data(), buf, n, hipMemcpyDeviceToHost));
+      if (fixed == 2) CK(hipHostFree(extra));
+      if (fixed == 3) CK(hipFree(extra));
+      if (fixed == 4)
+        for (hipStream_t f : fresh) CK(hipStreamDestroy(f));
       size_t zeros = 0;
       for (size_t i = 0; i < n; ++i) zeros += got[i] == 0;
       printf("{\"protocol\": \"%s\", \"trial\": %d, \"memset_returned_ms\": %.3f, \"zero_bytes_after_copy\": %zu}\n",
-             fixed ? "memsetAsync on the stream + sync" : "hipMemset (null stream)", t, ms, zeros);
+             names[fixed], t, ms, zeros);
       fflush(stdout);
     }
   }

@@ -55,7 +55,7 @@ def test_host_pipeline_parity(name, n, frame):
 @pytest.mark.parametrize("frame", [0, 1])
 def test_host_fresh_context_while_the_null_stream_is_busy(frame):
     """A context created and used at once while the device's null stream is still busy
-    (torch's current stream, here a spin kernel). Until round 6 the context zeroed its
+    (here a spin kernel launched on it). Until round 6 the context zeroed its
     arena with a null-stream hipMemset, which its non-blocking streams do not wait for:
     the first call's H2D copies could land first and be zeroed, so chunk 0 encoded zero
     columns (the first-chunk failures of rounds 5 and 6, profiles/r06/intermittent/README.md
@@ -65,8 +65,12 @@ def test_host_fresh_context_while_the_null_stream_is_busy(frame):
     cols = make(n, 11)
     expect, _ = oracle.encode(schema, cols, n, frame)
     plan = NativePlan(schema)
+    null = torch.cuda.ExternalStream(0)  # the device's null stream itself
     for _ in range(3):
-        torch.cuda._sleep(50_000_000)  # ~20 ms of spinning on the current stream
+        with torch.cuda.stream(null):
+            # ~1 s of spinning on the null stream: it must outlast the first call's pinned
+            # staging allocation (128 MiB, tens of ms), or the fill lands before the copies
+            torch.cuda._sleep(2_000_000_000)
         hp = HostPipeline(plan, chunk_rows=1024)
         out = np.zeros(expect.nbytes, np.uint8)
         hp.encode(cols, n, frame, out)
