@@ -2,7 +2,8 @@
 # Round 6, call Q: the null-stream arena memset race (host.cpp context creation).
 # 1. scripts/microbench/memset_race.hip: hipMemset (null stream) behind a busy null stream,
 #    then an H2D on a non-blocking stream: are the copied bytes zeroed by the late fill?
-# 2. tests/test_gpu_host.py::test_host_fresh_context_while_the_null_stream_is_busy against the
+# 2. tests/test_gpu_host.py::test_host_fresh_context_while_the_null_stream_is_busy (a ~1 s spin
+#    on torch's default stream, the null stream) against the
 #    library with the old hipMemset (fury_amd/lib/ab_oldmemset), expected to fail on wrong
 #    bytes, no fault;
 # 3. the same test and the whole host file against the fixed library.

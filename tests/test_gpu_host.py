@@ -65,12 +65,13 @@ def test_host_fresh_context_while_the_null_stream_is_busy(frame):
     cols = make(n, 11)
     expect, _ = oracle.encode(schema, cols, n, frame)
     plan = NativePlan(schema)
-    null = torch.cuda.ExternalStream(0)  # the device's null stream itself
+    assert torch.cuda.current_stream().cuda_stream == 0  # torch's default stream is the null stream
     for _ in range(3):
-        with torch.cuda.stream(null):
-            # ~1 s of spinning on the null stream: it must outlast the first call's pinned
-            # staging allocation (128 MiB, tens of ms), or the fill lands before the copies
-            torch.cuda._sleep(2_000_000_000)
+        # ~1 s of spinning on the null stream: it must outlast the context's creation and the
+        # first call's pinned staging allocations (a 20 ms spin did not, q1 in
+        # profiles/r06/memset_race/). Not through torch.cuda.ExternalStream(0): a spin launched
+        # under it leaves hipStreamQuery(null stream) ready (close6/null_stream_probe.json)
+        torch.cuda._sleep(2_000_000_000)
         hp = HostPipeline(plan, chunk_rows=1024)
         out = np.zeros(expect.nbytes, np.uint8)
         hp.encode(cols, n, frame, out)
