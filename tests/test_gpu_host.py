@@ -59,7 +59,9 @@ def test_host_fresh_context_while_the_null_stream_is_busy(frame):
     arena with a null-stream hipMemset, which its non-blocking streams do not wait for:
     the first call's H2D copies could land first and be zeroed, so chunk 0 encoded zero
     columns (the first-chunk failures of rounds 5 and 6, profiles/r06/intermittent/README.md
-    §6). Now the arena is zeroed on the context's own stream and waited for."""
+    §6). Now the arena is zeroed on the context's own stream and waited for. (A guard, not a
+    reproduction: the old build passed this test too, profiles/r06/memset_race/q1-q4; the
+    race itself is shown by scripts/microbench/memset_race.hip.)"""
     schema, make = catalog()["struct104"]
     n = 5000
     cols = make(n, 11)
