@@ -210,7 +210,11 @@ int64_t fory_rowfmt_encode_workspace_bytes(const fory_plan* plan, const fory_col
  * lists and maps element by element) with the positions of every bean / list / map
  * instance of the levels allocated so far in out_cols (their fory_column.length) as
  * temporaries. Ask again after allocating a deeper level: the need grows with it. A smaller
- * workspace keeps the per-record decoder; the columns are identical. */
+ * workspace keeps the per-record decoder; the columns are identical. The positions are
+ * state between calls: a decode_sizes of the next level and the final decode read the
+ * positions the previous decode_sizes of the same plan, rows and columns left in the
+ * workspace, so the workspace must not be written in between. Any other call with that
+ * workspace discards them, and the next call starts at level 0. */
 int64_t fory_rowfmt_decode_workspace_bytes(const fory_plan* plan, const fory_column* out_cols,
                                            int64_t num_rows);
 
